@@ -1,0 +1,116 @@
+"""ctypes binding of the product library fbthrift_amd/lib/libtgpu.so.
+
+The library is the C-ABI declared in include/thrift_gpu.h. There is no
+fallback: if the library is missing, importing a GPU entry point raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libtgpu.so")
+
+PROTOCOL_BINARY = 0
+PROTOCOL_COMPACT = 2
+
+# TType (thrift/lib/cpp/protocol/TType.h:31-51)
+T_STOP, T_VOID, T_BOOL, T_BYTE, T_DOUBLE = 0, 1, 2, 3, 4
+T_I16, T_I32, T_U64, T_I64, T_STRING = 6, 8, 9, 10, 11
+T_STRUCT, T_MAP, T_SET, T_LIST = 12, 13, 14, 15
+T_UTF8, T_UTF16, T_STREAM, T_FLOAT = 16, 17, 18, 19
+
+CODES = {
+    0: "OK", 1: "UNDERFLOW", 2: "INVALID_VARINT", 3: "BOOL_VALUE",
+    4: "INVALID_SKIP_TYPE", 5: "TRUNCATED", 6: "NEGATIVE_SIZE", 7: "SIZE_LIMIT",
+    8: "DEPTH_LIMIT", 9: "BAD_TYPE", 10: "INVALID_BOOL_WRITE",
+    11: "WRITE_SIZE_LIMIT", 20: "INDEX_MISMATCH", 21: "OUTPUT_OVERFLOW",
+    22: "UNSUPPORTED", 23: "INVALID_ARGUMENT", 24: "HIP",
+}
+CODE = {v: k for k, v in CODES.items()}
+
+
+class FieldDesc(ctypes.Structure):
+    _fields_ = [("id", ctypes.c_int16), ("ttype", ctypes.c_uint8),
+                ("elem_ttype", ctypes.c_uint8), ("qualifier", ctypes.c_uint8),
+                ("reserved0", ctypes.c_uint8 * 3), ("member_offset", ctypes.c_uint32),
+                ("isset_offset", ctypes.c_uint32), ("struct_index", ctypes.c_int32),
+                ("reserved1", ctypes.c_uint32)]
+
+
+class StructDesc(ctypes.Structure):
+    _fields_ = [("first_field", ctypes.c_uint32), ("num_fields", ctypes.c_uint32),
+                ("size", ctypes.c_uint32), ("align", ctypes.c_uint32)]
+
+
+class Limits(ctypes.Structure):
+    _fields_ = [("string_limit", ctypes.c_int32), ("container_limit", ctypes.c_int32),
+                ("max_depth", ctypes.c_int32), ("height", ctypes.c_int32)]
+
+
+class Status(ctypes.Structure):
+    _fields_ = [("code", ctypes.c_int32), ("exc_class", ctypes.c_int32),
+                ("tproto_type", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("record", ctypes.c_uint64), ("byte_offset", ctypes.c_uint64)]
+
+    def as_tuple(self):
+        return (self.code, self.exc_class, self.tproto_type, self.record, self.byte_offset)
+
+
+assert ctypes.sizeof(FieldDesc) == 24 and ctypes.sizeof(StructDesc) == 16
+assert ctypes.sizeof(Status) == 32
+
+# Every symbol declared in include/thrift_gpu.h (checked by tests/test_abi.py).
+EXPORTS = [
+    "tgpu_abi_version", "tgpu_code_name", "tgpu_code_classify", "tgpu_layout_compute",
+    "tgpu_schema_create", "tgpu_schema_destroy", "tgpu_schema_record_size",
+    "tgpu_schema_fixed_wire_size", "tgpu_context_create", "tgpu_context_destroy",
+    "tgpu_context_reserve", "tgpu_context_wait", "tgpu_encode_batch", "tgpu_encoded_size",
+    "tgpu_decode_batch",
+]
+
+_lib = None
+
+
+def lib():
+    """Loads libtgpu.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            "fbthrift_amd native library missing: %s (run __graft_entry__.build())" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    P, U32, U64, I32 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    L.tgpu_abi_version.restype = I32
+    L.tgpu_code_name.restype = ctypes.c_char_p
+    L.tgpu_code_name.argtypes = [I32]
+    L.tgpu_code_classify.argtypes = [I32, ctypes.POINTER(ctypes.c_int32),
+                                     ctypes.POINTER(ctypes.c_int32)]
+    L.tgpu_layout_compute.restype = I32
+    L.tgpu_layout_compute.argtypes = [P, U32, P, U32]
+    L.tgpu_schema_create.restype = I32
+    L.tgpu_schema_create.argtypes = [P, U32, P, U32, ctypes.POINTER(P)]
+    L.tgpu_schema_destroy.argtypes = [P]
+    L.tgpu_schema_record_size.restype = U32
+    L.tgpu_schema_record_size.argtypes = [P]
+    L.tgpu_schema_fixed_wire_size.restype = U64
+    L.tgpu_schema_fixed_wire_size.argtypes = [P, I32]
+    L.tgpu_context_create.restype = I32
+    L.tgpu_context_create.argtypes = [ctypes.POINTER(P)]
+    L.tgpu_context_destroy.argtypes = [P]
+    L.tgpu_context_reserve.restype = I32
+    L.tgpu_context_reserve.argtypes = [P, U64]
+    L.tgpu_context_wait.restype = I32
+    L.tgpu_context_wait.argtypes = [P, P, ctypes.POINTER(Status), ctypes.POINTER(U64),
+                                    ctypes.POINTER(U64)]
+    L.tgpu_encode_batch.restype = I32
+    L.tgpu_encode_batch.argtypes = [P, P, I32, P, U64, P, P, P, U64, P, P,
+                                    ctypes.POINTER(Status), ctypes.POINTER(U64)]
+    L.tgpu_encoded_size.restype = I32
+    L.tgpu_encoded_size.argtypes = [P, P, I32, P, U64, P, P, ctypes.POINTER(Status),
+                                    ctypes.POINTER(U64)]
+    L.tgpu_decode_batch.restype = I32
+    L.tgpu_decode_batch.argtypes = [P, P, I32, P, U64, P, U64, P, P, U64,
+                                    ctypes.POINTER(Limits), P, ctypes.POINTER(Status),
+                                    ctypes.POINTER(U64), ctypes.POINTER(U64)]
+    _lib = L
+    return L

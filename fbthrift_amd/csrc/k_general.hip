@@ -1,0 +1,343 @@
+// k_general.hip — table-driven gfx950 kernels for arbitrary schemas:
+//   general_decode   one lane per record, full readNoXfer semantics
+//   walk_offsets     record boundary discovery by skip-parsing (one lane;
+//                    fallback for unindexed irregular streams)
+//   encode_size /    three-pass variable-length encode: per-record wire size,
+//   scan_blocks /    exclusive scan of block sums, block-local scan + emit
+//   encode_write
+//   *_finish         single-lane epilogues: re-run the first failing record to
+//                    recover its exact error code and byte offset (the
+//                    exception the reference would have thrown) and publish
+//                    the batch result.
+// All state lives in the caller's stream order; nothing is read back to the
+// host inside a call, so calls can be captured into a hipGraph.
+#include "tgpu_device.h"
+
+namespace tgpu {
+namespace {
+
+using namespace dev;
+
+constexpr unsigned long long kNone = ~0ull;
+
+__global__ void result_init_kernel(DevResult* res, uint64_t n) {
+  res->first_fail = kNone;
+  res->first_irregular = kNone;
+  res->code = 0;
+  res->pad = 0;
+  res->fail_offset = 0;
+  res->total_bytes = 0;
+  res->n_records = n;
+}
+
+__device__ __forceinline__ Reader make_reader(const DecodeArgs& a, uint64_t start) {
+  Reader r;
+  r.p = a.in;
+  r.pos = start;
+  r.end = a.in_len;
+  r.height = (int64_t)(a.height ? a.height : a.max_depth) + 1;
+  r.string_limit = a.string_limit;
+  r.container_limit = a.container_limit;
+  r.max_depth = a.max_depth;
+  r.err = 0;
+  r.err_off = 0;
+  r.has_bool = false;
+  r.bool_val = false;
+  return r;
+}
+
+// Parses record i (record buffer zeroed first). Returns the reader.
+template <int P>
+__device__ Reader decode_one(const DecodeArgs& a, uint64_t i) {
+  uint8_t* rec = a.recs + i * a.rec_size;
+  if ((a.rec_size & 7) == 0) {
+    for (uint32_t b = 0; b < a.rec_size; b += 8) *(uint64_t*)(rec + b) = 0;
+  } else {
+    for (uint32_t b = 0; b < a.rec_size; ++b) rec[b] = 0;
+  }
+  const uint64_t start = a.offs[i];
+  Reader r = make_reader(a, start);
+  if (start > a.in_len || (a.check_index && a.offs[i + 1] < start)) {
+    r.fail(TGPU_ERR_INDEX_MISMATCH, start);
+    return r;
+  }
+  read_record<P>(r, a.sc, rec, a.arena, a.arena_cap);
+  if (r.ok() && a.check_index && r.pos != a.offs[i + 1]) r.fail(TGPU_ERR_INDEX_MISMATCH, r.pos);
+  return r;
+}
+
+// Indexed streams: one lane per record, records independent.
+template <int P>
+__global__ __launch_bounds__(256) void general_decode_kernel(DecodeArgs a) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+    const Reader r = decode_one<P>(a, i);
+    if (!r.ok()) atomicMin(&a.res->first_fail, (unsigned long long)i);
+  }
+}
+
+// Unindexed streams the fixed-layout path cannot take: one lane reads the
+// records back to back exactly like repeated deserialize<T>(Cursor&)
+// (Serializer.h:97-100) and records each start offset. Serial by nature;
+// used from the first non-canonical record of a fixed-layout batch and for
+// unindexed variable-length streams.
+template <int P>
+__global__ void serial_decode_kernel(DecodeArgs a, int from_irregular, uint64_t fixed_len) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint64_t first = from_irregular ? a.res->first_irregular : 0;
+  if (first >= a.n) return;
+  uint64_t* offs = const_cast<uint64_t*>(a.offs);
+  uint64_t pos = first * fixed_len;
+  for (uint64_t i = first; i < a.n; ++i) {
+    offs[i] = pos;
+    const Reader r = decode_one<P>(a, i);
+    if (!r.ok()) {
+      atomicMin(&a.res->first_fail, (unsigned long long)i);
+      return;
+    }
+    pos = r.pos;
+  }
+  offs[a.n] = pos;
+}
+
+template <int P>
+__global__ void decode_finish_kernel(DecodeArgs a, uint64_t fixed_len) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  DevResult* res = a.res;
+  const uint64_t f = res->first_fail;
+  const uint64_t irr = res->first_irregular;
+  // start offset of record i (fixed path: i * L below the first irregular one)
+  auto start_of = [&](uint64_t i) -> uint64_t {
+    if (fixed_len && i <= irr && irr != kNone) return i * fixed_len;
+    if (fixed_len && irr == kNone) return i * fixed_len;
+    return a.offs[i];
+  };
+  const uint64_t base = start_of(0);
+  if (f < a.n) {
+    const Reader r = decode_one<P>(a, f);
+    res->code = r.ok() ? TGPU_ERR_INDEX_MISMATCH : r.err;
+    res->fail_offset = r.ok() ? r.pos : r.err_off;
+    res->n_records = f;
+    res->total_bytes = start_of(f) - base;
+  } else {
+    res->code = 0;
+    res->n_records = a.n;
+    res->total_bytes = (fixed_len && irr == kNone) ? a.n * fixed_len : a.offs[a.n] - base;
+  }
+}
+
+// ------------------------------------------------------------------ encode --
+template <int P>
+__device__ __forceinline__ Writer size_one(const EncodeArgs& a, uint64_t i) {
+  Writer w{nullptr, 0, 0, 0, 0};
+  write_record<P>(w, a.sc, a.recs + i * a.rec_size, a.sbase, a.lbase);
+  return w;
+}
+
+__device__ __forceinline__ unsigned long long block_sum(unsigned long long v) {
+  __shared__ unsigned long long part[4];
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) part[wid] = v;
+  __syncthreads();
+  unsigned long long t = 0;
+  if (threadIdx.x == 0) t = part[0] + part[1] + part[2] + part[3];
+  return t;
+}
+
+// Block-wide exclusive scan (256 threads).
+__device__ __forceinline__ unsigned long long block_exscan(unsigned long long v) {
+  __shared__ unsigned long long part[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  unsigned long long x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) part[wid] = x;
+  __syncthreads();
+  unsigned long long pre = 0;
+  for (int w = 0; w < wid; ++w) pre += part[w];
+  return pre + x - v;
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void encode_size_kernel(EncodeArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  unsigned long long sz = 0;
+  if (i < a.n) {
+    const Writer w = size_one<P>(a, i);
+    if (!w.ok()) atomicMin(&a.res->first_fail, (unsigned long long)i);
+    sz = w.pos;
+    a.offs[i] = sz;
+  }
+  const unsigned long long t = block_sum(sz);
+  if (threadIdx.x == 0) a.block_sums[blockIdx.x] = t;
+}
+
+// Exclusive scan of nb block sums by one 1024-thread block; total -> res.
+__global__ __launch_bounds__(1024) void scan_blocks_kernel(unsigned long long* sums, uint64_t nb,
+                                                           DevResult* res, uint64_t* offs,
+                                                           uint64_t n) {
+  __shared__ unsigned long long part[1024];
+  const uint64_t per = (nb + 1023) / 1024;
+  const uint64_t b = threadIdx.x * per, e = min(nb, b + per);
+  unsigned long long s = 0;
+  for (uint64_t k = b; k < e; ++k) s += sums[k];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const unsigned long long y = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0;
+    __syncthreads();
+    part[threadIdx.x] += y;
+    __syncthreads();
+  }
+  unsigned long long run = part[threadIdx.x] - s;
+  for (uint64_t k = b; k < e; ++k) {
+    const unsigned long long v = sums[k];
+    sums[k] = run;
+    run += v;
+  }
+  if (threadIdx.x == 1023) {
+    res->total_bytes = part[1023];
+    offs[n] = part[1023];
+  }
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void encode_write_kernel(EncodeArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const unsigned long long sz = i < a.n ? a.offs[i] : 0;
+  const unsigned long long start = a.block_sums[blockIdx.x] + block_exscan(sz);
+  if (i >= a.n) return;
+  a.offs[i] = start;
+  if (start + sz > a.cap) {
+    atomicMin(&a.res->first_fail, (unsigned long long)i);
+    return;
+  }
+  Writer w{a.out, start, a.cap, 0, 0};
+  write_record<P>(w, a.sc, a.recs + i * a.rec_size, a.sbase, a.lbase);
+}
+
+// sizes -> exclusive offsets (block-local scan + scanned block sums)
+__global__ __launch_bounds__(256) void size_offsets_kernel(EncodeArgs a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const unsigned long long sz = i < a.n ? a.offs[i] : 0;
+  const unsigned long long start = a.block_sums[blockIdx.x] + block_exscan(sz);
+  if (i < a.n) a.offs[i] = start;
+}
+
+template <int P>
+__global__ void encode_finish_kernel(EncodeArgs a, uint64_t fixed_len) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  DevResult* res = a.res;
+  const uint64_t f = res->first_fail;
+  if (f < a.n) {
+    const Writer w = size_one<P>(a, f);
+    const uint64_t start = fixed_len ? f * fixed_len : a.offs[f];
+    res->code = w.ok() ? TGPU_ERR_OUTPUT_OVERFLOW : w.err;
+    res->fail_offset = start + (w.ok() ? 0 : w.err_off);
+    res->n_records = f;
+    res->total_bytes = start;
+  } else {
+    res->code = 0;
+    res->n_records = a.n;
+    res->total_bytes = fixed_len ? a.n * fixed_len : a.offs[a.n];
+  }
+}
+
+uint32_t grid_for(uint64_t n) {
+  const uint64_t b = (n + 255) / 256;
+  return (uint32_t)(b < 4096 ? (b ? b : 1) : 4096);
+}
+
+}  // namespace
+
+hipError_t launch_result_init(DevResult* res, uint64_t n, hipStream_t stream) {
+  hipLaunchKernelGGL(result_init_kernel, dim3(1), dim3(1), 0, stream, res, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_general_decode(const DecodeArgs& a, int protocol, hipStream_t stream) {
+  const uint32_t g = grid_for(a.n);
+  if (protocol == TGPU_PROTOCOL_BINARY)
+    hipLaunchKernelGGL(general_decode_kernel<TGPU_PROTOCOL_BINARY>, dim3(g), dim3(256), 0, stream,
+                       a);
+  else
+    hipLaunchKernelGGL(general_decode_kernel<TGPU_PROTOCOL_COMPACT>, dim3(g), dim3(256), 0, stream,
+                       a);
+  return hipGetLastError();
+}
+
+hipError_t launch_serial_decode(const DecodeArgs& a, int protocol, bool from_irregular,
+                                uint64_t fixed_len, hipStream_t stream) {
+  if (protocol == TGPU_PROTOCOL_BINARY)
+    hipLaunchKernelGGL(serial_decode_kernel<TGPU_PROTOCOL_BINARY>, dim3(1), dim3(64), 0, stream, a,
+                       (int)from_irregular, fixed_len);
+  else
+    hipLaunchKernelGGL(serial_decode_kernel<TGPU_PROTOCOL_COMPACT>, dim3(1), dim3(64), 0, stream, a,
+                       (int)from_irregular, fixed_len);
+  return hipGetLastError();
+}
+
+hipError_t launch_decode_finish(const DecodeArgs& a, int protocol, uint64_t fixed_len,
+                                hipStream_t stream) {
+  if (protocol == TGPU_PROTOCOL_BINARY)
+    hipLaunchKernelGGL(decode_finish_kernel<TGPU_PROTOCOL_BINARY>, dim3(1), dim3(64), 0, stream, a,
+                       fixed_len);
+  else
+    hipLaunchKernelGGL(decode_finish_kernel<TGPU_PROTOCOL_COMPACT>, dim3(1), dim3(64), 0, stream, a,
+                       fixed_len);
+  return hipGetLastError();
+}
+
+hipError_t launch_general_encode(const EncodeArgs& a, int protocol, uint64_t n_blocks,
+                                 hipStream_t stream) {
+  if (a.n == 0) return hipSuccess;
+  const dim3 grid((uint32_t)n_blocks);
+  if (protocol == TGPU_PROTOCOL_BINARY) {
+    hipLaunchKernelGGL(encode_size_kernel<TGPU_PROTOCOL_BINARY>, grid, dim3(256), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(encode_size_kernel<TGPU_PROTOCOL_COMPACT>, grid, dim3(256), 0, stream, a);
+  }
+  hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(1024), 0, stream, a.block_sums, n_blocks,
+                     a.res, a.offs, a.n);
+  if (protocol == TGPU_PROTOCOL_BINARY) {
+    hipLaunchKernelGGL(encode_write_kernel<TGPU_PROTOCOL_BINARY>, grid, dim3(256), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(encode_write_kernel<TGPU_PROTOCOL_COMPACT>, grid, dim3(256), 0, stream, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_general_size(const EncodeArgs& a, int protocol, uint64_t n_blocks,
+                               hipStream_t stream) {
+  if (a.n == 0) return hipSuccess;
+  const dim3 grid((uint32_t)n_blocks);
+  if (protocol == TGPU_PROTOCOL_BINARY) {
+    hipLaunchKernelGGL(encode_size_kernel<TGPU_PROTOCOL_BINARY>, grid, dim3(256), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(encode_size_kernel<TGPU_PROTOCOL_COMPACT>, grid, dim3(256), 0, stream, a);
+  }
+  hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(1024), 0, stream, a.block_sums, n_blocks,
+                     a.res, a.offs, a.n);
+  if (protocol == TGPU_PROTOCOL_BINARY) {
+    hipLaunchKernelGGL(size_offsets_kernel, grid, dim3(256), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(size_offsets_kernel, grid, dim3(256), 0, stream, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_encode_finish(const EncodeArgs& a, int protocol, uint64_t fixed_len,
+                                hipStream_t stream) {
+  if (protocol == TGPU_PROTOCOL_BINARY)
+    hipLaunchKernelGGL(encode_finish_kernel<TGPU_PROTOCOL_BINARY>, dim3(1), dim3(64), 0, stream, a,
+                       fixed_len);
+  else
+    hipLaunchKernelGGL(encode_finish_kernel<TGPU_PROTOCOL_COMPACT>, dim3(1), dim3(64), 0, stream, a,
+                       fixed_len);
+  return hipGetLastError();
+}
+
+}  // namespace tgpu

@@ -1,0 +1,534 @@
+// tgpu_api.cpp — host side of the C-ABI (include/thrift_gpu.h): schema
+// validation/upload, the canonical Binary template, context workspaces and
+// the stream-ordered launch sequences of encode/decode.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "tgpu_internal.h"
+
+using namespace tgpu;
+
+struct tgpu_schema {
+  std::vector<tgpu_struct_desc> structs;
+  std::vector<tgpu_field_desc> fields;
+  tgpu_struct_desc* d_structs = nullptr;
+  tgpu_field_desc* d_fields = nullptr;
+  int device = 0;
+  bool has_lists = false;
+  bool fixed_binary = false;
+  FixedTemplate tmpl{};
+  FixedTemplate* d_tmpl = nullptr;
+};
+
+struct tgpu_context {
+  int device = 0;
+  DevResult* d_res = nullptr;
+  DevResult* h_res = nullptr;  // pinned
+  uint64_t* d_offs = nullptr;
+  unsigned long long* d_block_sums = nullptr;
+  uint64_t reserved = 0;  // records
+  int last_op = 0;        // 1 decode, 2 encode
+};
+
+namespace {
+
+bool is_scalar(uint32_t t) {
+  switch (t) {
+    case TGPU_T_BOOL: case TGPU_T_BYTE: case TGPU_T_I16: case TGPU_T_I32:
+    case TGPU_T_I64: case TGPU_T_DOUBLE: case TGPU_T_FLOAT:
+      return true;
+    default:
+      return false;
+  }
+}
+uint32_t scalar_size(uint32_t t) {
+  switch (t) {
+    case TGPU_T_BOOL: case TGPU_T_BYTE: return 1;
+    case TGPU_T_I16: return 2;
+    case TGPU_T_I32: case TGPU_T_FLOAT: return 4;
+    default: return 8;
+  }
+}
+uint32_t align_up(uint32_t x, uint32_t a) { return (x + a - 1) / a * a; }
+
+// Layout of struct si (memoized in `done`): declaration-order members at
+// natural alignment, then one isset byte per field (Isset.h:243-296).
+int layout_struct(tgpu_struct_desc* s, uint32_t ns, tgpu_field_desc* f, uint32_t nf,
+                  uint32_t si, std::vector<int>& state) {
+  if (si >= ns) return TGPU_ERR_INVALID_ARGUMENT;
+  if (state[si] == 2) return TGPU_OK;
+  if (state[si] == 1) return TGPU_ERR_UNSUPPORTED;  // recursive struct
+  state[si] = 1;
+  tgpu_struct_desc& sd = s[si];
+  if ((uint64_t)sd.first_field + sd.num_fields > nf) return TGPU_ERR_INVALID_ARGUMENT;
+  uint32_t off = 0, align = 1;
+  for (uint32_t k = 0; k < sd.num_fields; ++k) {
+    tgpu_field_desc& fd = f[sd.first_field + k];
+    uint32_t sz, al;
+    if (is_scalar(fd.ttype)) {
+      sz = al = scalar_size(fd.ttype);
+    } else if (fd.ttype == TGPU_T_STRING || fd.ttype == TGPU_T_LIST || fd.ttype == TGPU_T_SET) {
+      sz = 16;
+      al = 8;
+    } else if (fd.ttype == TGPU_T_STRUCT) {
+      if (fd.struct_index < 0) return TGPU_ERR_INVALID_ARGUMENT;
+      const int rc = layout_struct(s, ns, f, nf, (uint32_t)fd.struct_index, state);
+      if (rc) return rc;
+      sz = s[fd.struct_index].size;
+      al = s[fd.struct_index].align;
+    } else {
+      return TGPU_ERR_UNSUPPORTED;
+    }
+    off = align_up(off, al);
+    fd.member_offset = off;
+    off += sz;
+    align = std::max(align, al);
+  }
+  for (uint32_t k = 0; k < sd.num_fields; ++k) f[sd.first_field + k].isset_offset = off + k;
+  off += sd.num_fields;
+  sd.align = align;
+  sd.size = align_up(std::max(off, 1u), align);
+  state[si] = 2;
+  return TGPU_OK;
+}
+
+int validate(const tgpu_struct_desc* s, uint32_t ns, const tgpu_field_desc* f, uint32_t nf,
+             uint32_t si, int depth, bool& has_lists) {
+  if (si >= ns || depth > kMaxSchemaDepth) return TGPU_ERR_UNSUPPORTED;
+  const tgpu_struct_desc& sd = s[si];
+  if ((uint64_t)sd.first_field + sd.num_fields > nf || sd.size == 0 || sd.align == 0 ||
+      sd.size % sd.align)
+    return TGPU_ERR_INVALID_ARGUMENT;
+  for (uint32_t k = 0; k < sd.num_fields; ++k) {
+    const tgpu_field_desc& fd = f[sd.first_field + k];
+    for (uint32_t j = 0; j < k; ++j)
+      if (f[sd.first_field + j].id == fd.id) return TGPU_ERR_INVALID_ARGUMENT;
+    if (fd.qualifier > TGPU_OPTIONAL) return TGPU_ERR_UNSUPPORTED;
+    if (fd.isset_offset >= sd.size) return TGPU_ERR_INVALID_ARGUMENT;
+    uint32_t sz;
+    if (is_scalar(fd.ttype)) {
+      sz = scalar_size(fd.ttype);
+    } else if (fd.ttype == TGPU_T_STRING) {
+      sz = 16;
+    } else if (fd.ttype == TGPU_T_LIST || fd.ttype == TGPU_T_SET) {
+      if (!is_scalar(fd.elem_ttype)) return TGPU_ERR_UNSUPPORTED;
+      has_lists = true;
+      sz = 16;
+    } else if (fd.ttype == TGPU_T_STRUCT) {
+      if (fd.struct_index < 0 || (uint32_t)fd.struct_index >= ns) return TGPU_ERR_INVALID_ARGUMENT;
+      const int rc = validate(s, ns, f, nf, (uint32_t)fd.struct_index, depth + 1, has_lists);
+      if (rc) return rc;
+      sz = s[fd.struct_index].size;
+    } else {
+      return TGPU_ERR_UNSUPPORTED;
+    }
+    if ((uint64_t)fd.member_offset + sz > sd.size) return TGPU_ERR_INVALID_ARGUMENT;
+    if (fd.member_offset % (sz >= 8 ? 8 : sz)) return TGPU_ERR_INVALID_ARGUMENT;
+  }
+  return TGPU_OK;
+}
+
+// Canonical Binary wire template (BinaryProtocol-inl.h:53-67 headers/STOP,
+// :120-161 values) for schemas with only unqualified fixed-width fields.
+bool build_template(const tgpu_schema& sc, uint32_t si, uint32_t base, FixedTemplate& t,
+                    uint32_t& wire) {
+  const tgpu_struct_desc& sd = sc.structs[si];
+  for (uint32_t k = 0; k < sd.num_fields; ++k) {
+    const tgpu_field_desc& fd = sc.fields[sd.first_field + k];
+    if (fd.qualifier != TGPU_UNQUALIFIED) return false;
+    if (t.n_items >= (uint32_t)kMaxTemplateItems || t.n_isset >= 64) return false;
+    TemplateItem it{};
+    it.wire_off = (uint16_t)wire;
+    it.hdr_len = 3;
+    it.hdr = (uint32_t)fd.ttype | ((uint32_t)((uint16_t)fd.id >> 8) << 8) |
+             ((uint32_t)((uint16_t)fd.id & 0xff) << 16);
+    if (is_scalar(fd.ttype)) {
+      it.width = (uint8_t)scalar_size(fd.ttype);
+      it.member_off = (uint16_t)(base + fd.member_offset);
+      it.is_bool = fd.ttype == TGPU_T_BOOL;
+      t.items[t.n_items++] = it;
+      wire += 3 + it.width;
+    } else if (fd.ttype == TGPU_T_STRUCT) {
+      t.items[t.n_items++] = it;
+      wire += 3;
+      if (!build_template(sc, (uint32_t)fd.struct_index, base + fd.member_offset, t, wire))
+        return false;
+    } else {
+      return false;
+    }
+    t.isset_off[t.n_isset++] = (uint16_t)(base + fd.isset_offset);
+  }
+  if (t.n_items >= (uint32_t)kMaxTemplateItems) return false;
+  TemplateItem stop{};
+  stop.wire_off = (uint16_t)wire;
+  stop.hdr_len = 1;
+  stop.hdr = 0;
+  t.items[t.n_items++] = stop;
+  wire += 1;
+  return true;
+}
+
+void classify(int code, int32_t* exc, int32_t* tp) {
+  int32_t e = TGPU_EXC_RUNTIME, t = 0;
+  switch (code) {
+    case TGPU_OK: e = TGPU_EXC_NONE; break;
+    case TGPU_ERR_UNDERFLOW: case TGPU_ERR_INVALID_VARINT: e = TGPU_EXC_OUT_OF_RANGE; break;
+    case TGPU_ERR_BOOL_VALUE: case TGPU_ERR_INVALID_SKIP_TYPE: case TGPU_ERR_TRUNCATED:
+      e = TGPU_EXC_PROTOCOL; t = 1; break;
+    case TGPU_ERR_NEGATIVE_SIZE: e = TGPU_EXC_PROTOCOL; t = 2; break;
+    case TGPU_ERR_SIZE_LIMIT: case TGPU_ERR_WRITE_SIZE_LIMIT: e = TGPU_EXC_PROTOCOL; t = 3; break;
+    case TGPU_ERR_DEPTH_LIMIT: e = TGPU_EXC_PROTOCOL; t = 8; break;
+    case TGPU_ERR_BAD_TYPE: e = TGPU_EXC_PROTOCOL; t = 0; break;
+    case TGPU_ERR_INVALID_BOOL_WRITE: e = TGPU_EXC_ABORT; break;
+    default: break;
+  }
+  if (exc) *exc = e;
+  if (tp) *tp = t;
+}
+
+void fill_status(tgpu_status* st, int code, uint64_t rec, uint64_t off) {
+  if (!st) return;
+  std::memset(st, 0, sizeof(*st));
+  st->code = code;
+  classify(code, &st->exc_class, &st->tproto_type);
+  st->record = rec;
+  st->byte_offset = off;
+}
+
+int ensure_workspace(tgpu_context* ctx, uint64_t n) {
+  if (n <= ctx->reserved && ctx->d_offs) return TGPU_OK;
+  const uint64_t want = std::max<uint64_t>(n, 1024);
+  if (ctx->d_offs) (void)hipFree(ctx->d_offs);
+  if (ctx->d_block_sums) (void)hipFree(ctx->d_block_sums);
+  ctx->d_offs = nullptr;
+  ctx->d_block_sums = nullptr;
+  ctx->reserved = 0;
+  if (hipMalloc(&ctx->d_offs, (want + 1) * sizeof(uint64_t)) != hipSuccess) return TGPU_ERR_HIP;
+  if (hipMalloc(&ctx->d_block_sums, ((want + 255) / 256 + 1) * sizeof(unsigned long long)) !=
+      hipSuccess)
+    return TGPU_ERR_HIP;
+  ctx->reserved = want;
+  return TGPU_OK;
+}
+
+DevSchema dev_schema(const tgpu_schema* s) {
+  return DevSchema{s->d_structs, s->d_fields, (uint32_t)s->structs.size(),
+                   (uint32_t)s->fields.size()};
+}
+
+}  // namespace
+
+extern "C" {
+
+int tgpu_abi_version(void) { return TGPU_ABI_VERSION; }
+
+const char* tgpu_code_name(int code) {
+  switch (code) {
+    case TGPU_OK: return "OK";
+    case TGPU_ERR_UNDERFLOW: return "UNDERFLOW";
+    case TGPU_ERR_INVALID_VARINT: return "INVALID_VARINT";
+    case TGPU_ERR_BOOL_VALUE: return "BOOL_VALUE";
+    case TGPU_ERR_INVALID_SKIP_TYPE: return "INVALID_SKIP_TYPE";
+    case TGPU_ERR_TRUNCATED: return "TRUNCATED";
+    case TGPU_ERR_NEGATIVE_SIZE: return "NEGATIVE_SIZE";
+    case TGPU_ERR_SIZE_LIMIT: return "SIZE_LIMIT";
+    case TGPU_ERR_DEPTH_LIMIT: return "DEPTH_LIMIT";
+    case TGPU_ERR_BAD_TYPE: return "BAD_TYPE";
+    case TGPU_ERR_INVALID_BOOL_WRITE: return "INVALID_BOOL_WRITE";
+    case TGPU_ERR_WRITE_SIZE_LIMIT: return "WRITE_SIZE_LIMIT";
+    case TGPU_ERR_INDEX_MISMATCH: return "INDEX_MISMATCH";
+    case TGPU_ERR_OUTPUT_OVERFLOW: return "OUTPUT_OVERFLOW";
+    case TGPU_ERR_UNSUPPORTED: return "UNSUPPORTED";
+    case TGPU_ERR_INVALID_ARGUMENT: return "INVALID_ARGUMENT";
+    case TGPU_ERR_HIP: return "HIP";
+    default: return "UNKNOWN";
+  }
+}
+
+void tgpu_code_classify(int code, int32_t* exc_class, int32_t* tproto_type) {
+  classify(code, exc_class, tproto_type);
+}
+
+int tgpu_layout_compute(tgpu_struct_desc* structs, uint32_t n_structs, tgpu_field_desc* fields,
+                        uint32_t n_fields) {
+  if (!structs || n_structs == 0 || (!fields && n_fields)) return TGPU_ERR_INVALID_ARGUMENT;
+  std::vector<int> state(n_structs, 0);
+  for (uint32_t si = 0; si < n_structs; ++si) {
+    const int rc = layout_struct(structs, n_structs, fields, n_fields, si, state);
+    if (rc) return rc;
+  }
+  return TGPU_OK;
+}
+
+int tgpu_schema_create(const tgpu_struct_desc* structs, uint32_t n_structs,
+                       const tgpu_field_desc* fields, uint32_t n_fields, tgpu_schema** out) {
+  if (!out || !structs || n_structs == 0 || (!fields && n_fields)) return TGPU_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  bool has_lists = false;
+  int rc = validate(structs, n_structs, fields, n_fields, 0, 0, has_lists);
+  if (rc) return rc;
+  auto* s = new (std::nothrow) tgpu_schema();
+  if (!s) return TGPU_ERR_HIP;
+  s->structs.assign(structs, structs + n_structs);
+  s->fields.assign(fields, fields + n_fields);
+  s->has_lists = has_lists;
+  (void)hipGetDevice(&s->device);
+  if (hipMalloc(&s->d_structs, sizeof(tgpu_struct_desc) * n_structs) != hipSuccess ||
+      hipMalloc(&s->d_fields, sizeof(tgpu_field_desc) * std::max(n_fields, 1u)) != hipSuccess) {
+    tgpu_schema_destroy(s);
+    return TGPU_ERR_HIP;
+  }
+  if (hipMemcpy(s->d_structs, structs, sizeof(tgpu_struct_desc) * n_structs,
+                hipMemcpyHostToDevice) != hipSuccess ||
+      (n_fields && hipMemcpy(s->d_fields, fields, sizeof(tgpu_field_desc) * n_fields,
+                             hipMemcpyHostToDevice) != hipSuccess)) {
+    tgpu_schema_destroy(s);
+    return TGPU_ERR_HIP;
+  }
+  FixedTemplate t{};
+  uint32_t wire = 0;
+  if (build_template(*s, 0, 0, t, wire) && wire <= kMaxFixedWire &&
+      s->structs[0].size <= kMaxFixedRecord) {
+    t.wire_len = wire;
+    t.record_size = s->structs[0].size;
+    s->tmpl = t;
+    if (hipMalloc(&s->d_tmpl, sizeof(FixedTemplate)) != hipSuccess ||
+        hipMemcpy(s->d_tmpl, &t, sizeof(FixedTemplate), hipMemcpyHostToDevice) != hipSuccess) {
+      tgpu_schema_destroy(s);
+      return TGPU_ERR_HIP;
+    }
+    s->fixed_binary = true;
+  }
+  *out = s;
+  return TGPU_OK;
+}
+
+void tgpu_schema_destroy(tgpu_schema* s) {
+  if (!s) return;
+  if (s->d_structs) (void)hipFree(s->d_structs);
+  if (s->d_fields) (void)hipFree(s->d_fields);
+  if (s->d_tmpl) (void)hipFree(s->d_tmpl);
+  delete s;
+}
+
+uint32_t tgpu_schema_record_size(const tgpu_schema* s) { return s ? s->structs[0].size : 0; }
+
+uint64_t tgpu_schema_fixed_wire_size(const tgpu_schema* s, int protocol) {
+  return (s && protocol == TGPU_PROTOCOL_BINARY && s->fixed_binary) ? s->tmpl.wire_len : 0;
+}
+
+int tgpu_context_create(tgpu_context** out) {
+  if (!out) return TGPU_ERR_INVALID_ARGUMENT;
+  auto* c = new (std::nothrow) tgpu_context();
+  if (!c) return TGPU_ERR_HIP;
+  (void)hipGetDevice(&c->device);
+  if (hipMalloc(&c->d_res, sizeof(DevResult)) != hipSuccess ||
+      hipHostMalloc(&c->h_res, sizeof(DevResult), hipHostMallocDefault) != hipSuccess) {
+    tgpu_context_destroy(c);
+    return TGPU_ERR_HIP;
+  }
+  *out = c;
+  return TGPU_OK;
+}
+
+void tgpu_context_destroy(tgpu_context* c) {
+  if (!c) return;
+  if (c->d_res) (void)hipFree(c->d_res);
+  if (c->h_res) (void)hipHostFree(c->h_res);
+  if (c->d_offs) (void)hipFree(c->d_offs);
+  if (c->d_block_sums) (void)hipFree(c->d_block_sums);
+  delete c;
+}
+
+int tgpu_context_reserve(tgpu_context* ctx, uint64_t n) {
+  if (!ctx) return TGPU_ERR_INVALID_ARGUMENT;
+  return ensure_workspace(ctx, n);
+}
+
+int tgpu_context_wait(tgpu_context* ctx, void* stream, tgpu_status* st, uint64_t* n_done,
+                      uint64_t* bytes) {
+  if (!ctx) return TGPU_ERR_INVALID_ARGUMENT;
+  const hipStream_t s = (hipStream_t)stream;
+  if (hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s) !=
+          hipSuccess ||
+      hipStreamSynchronize(s) != hipSuccess) {
+    fill_status(st, TGPU_ERR_HIP, 0, 0);
+    return TGPU_ERR_HIP;
+  }
+  const DevResult& r = *ctx->h_res;
+  const int code = r.code;
+  fill_status(st, code, code ? r.first_fail : r.n_records, code ? r.fail_offset : 0);
+  if (n_done) *n_done = r.n_records;
+  if (bytes) *bytes = r.total_bytes;
+  return code;
+}
+
+int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                      const void* records, uint64_t n, const void* string_base,
+                      const void* list_base, void* out, uint64_t out_capacity,
+                      uint64_t* out_offsets, void* stream, tgpu_status* st, uint64_t* out_size) {
+  if (!ctx || !schema || (protocol != TGPU_PROTOCOL_BINARY && protocol != TGPU_PROTOCOL_COMPACT) ||
+      (n && (!records || !out))) {
+    fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+    return TGPU_ERR_INVALID_ARGUMENT;
+  }
+  const hipStream_t s = (hipStream_t)stream;
+  const uint32_t rs = schema->structs[0].size;
+  if (((uintptr_t)records) % schema->structs[0].align) {
+    fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+    return TGPU_ERR_INVALID_ARGUMENT;
+  }
+  hipError_t e = launch_result_init(ctx->d_res, n, s);
+  EncodeArgs a{};
+  a.sc = dev_schema(schema);
+  a.recs = (const uint8_t*)records;
+  a.n = n;
+  a.sbase = (const uint8_t*)string_base;
+  a.lbase = (const uint8_t*)list_base;
+  a.out = (uint8_t*)out;
+  a.cap = out_capacity;
+  a.rec_size = rs;
+  a.res = ctx->d_res;
+  uint64_t fixed = 0;
+  if (protocol == TGPU_PROTOCOL_BINARY && schema->fixed_binary &&
+      n * schema->tmpl.wire_len <= out_capacity) {
+    fixed = schema->tmpl.wire_len;
+    if (e == hipSuccess)
+      e = launch_fixed_binary_encode(&schema->tmpl, schema->d_tmpl, a.recs, n, a.out, out_offsets, ctx->d_res, s);
+  } else {
+    const uint64_t nb = (n + 255) / 256;
+    int rc = ensure_workspace(ctx, n);
+    if (rc) {
+      fill_status(st, rc, 0, 0);
+      return rc;
+    }
+    a.offs = out_offsets ? out_offsets : ctx->d_offs;
+    a.block_sums = ctx->d_block_sums;
+    if (e == hipSuccess && n) e = launch_general_encode(a, protocol, nb, s);
+  }
+  if (e == hipSuccess && n) e = launch_encode_finish(a, protocol, fixed, s);
+  ctx->last_op = 2;
+  if (e != hipSuccess) {
+    fill_status(st, TGPU_ERR_HIP, 0, 0);
+    return TGPU_ERR_HIP;
+  }
+  if (st || out_size) {
+    tgpu_status tmp;
+    uint64_t bytes = 0;
+    const int rc = tgpu_context_wait(ctx, stream, st ? st : &tmp, nullptr, &bytes);
+    if (out_size) *out_size = bytes;
+    return rc;
+  }
+  return TGPU_OK;
+}
+
+int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                      const void* records, uint64_t n, uint64_t* out_offsets, void* stream,
+                      tgpu_status* st, uint64_t* total) {
+  if (!ctx || !schema || !out_offsets ||
+      (protocol != TGPU_PROTOCOL_BINARY && protocol != TGPU_PROTOCOL_COMPACT) ||
+      (n && !records) || ((uintptr_t)records) % schema->structs[0].align) {
+    fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+    return TGPU_ERR_INVALID_ARGUMENT;
+  }
+  const hipStream_t s = (hipStream_t)stream;
+  int rc = ensure_workspace(ctx, n);
+  if (rc) {
+    fill_status(st, rc, 0, 0);
+    return rc;
+  }
+  EncodeArgs a{};
+  a.sc = dev_schema(schema);
+  a.recs = (const uint8_t*)records;
+  a.n = n;
+  a.offs = out_offsets;
+  a.block_sums = ctx->d_block_sums;
+  a.rec_size = schema->structs[0].size;
+  a.res = ctx->d_res;
+  a.cap = ~0ull;
+  hipError_t e = launch_result_init(ctx->d_res, n, s);
+  if (e == hipSuccess && n) e = launch_general_size(a, protocol, (n + 255) / 256, s);
+  if (e == hipSuccess && n) e = launch_encode_finish(a, protocol, 0, s);
+  if (e == hipSuccess && !n) e = hipMemsetAsync(out_offsets, 0, sizeof(uint64_t), s);
+  if (e != hipSuccess) {
+    fill_status(st, TGPU_ERR_HIP, 0, 0);
+    return TGPU_ERR_HIP;
+  }
+  if (st || total) {
+    tgpu_status tmp;
+    return tgpu_context_wait(ctx, stream, st ? st : &tmp, nullptr, total);
+  }
+  return TGPU_OK;
+}
+
+int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol, const void* in,
+                      uint64_t in_len, const uint64_t* offsets, uint64_t n, void* records,
+                      void* list_arena, uint64_t list_arena_capacity, const tgpu_limits* limits,
+                      void* stream, tgpu_status* st, uint64_t* n_decoded, uint64_t* consumed) {
+  if (!ctx || !schema || (protocol != TGPU_PROTOCOL_BINARY && protocol != TGPU_PROTOCOL_COMPACT) ||
+      (n && (!records || (!in && in_len)))) {
+    fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+    return TGPU_ERR_INVALID_ARGUMENT;
+  }
+  if (((uintptr_t)records) % schema->structs[0].align) {
+    fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+    return TGPU_ERR_INVALID_ARGUMENT;
+  }
+  const hipStream_t s = (hipStream_t)stream;
+  int rc = ensure_workspace(ctx, n);
+  if (rc) {
+    fill_status(st, rc, 0, 0);
+    return rc;
+  }
+  DecodeArgs a{};
+  a.sc = dev_schema(schema);
+  a.in = (const uint8_t*)in;
+  a.in_len = in_len;
+  a.n = n;
+  a.recs = (uint8_t*)records;
+  a.arena = (uint8_t*)list_arena;
+  a.arena_cap = list_arena_capacity;
+  a.string_limit = limits ? limits->string_limit : 0;
+  a.container_limit = limits ? limits->container_limit : 0;
+  a.max_depth = limits ? limits->max_depth : 12000;
+  a.height = limits ? limits->height : 0;
+  a.rec_size = schema->structs[0].size;
+  a.res = ctx->d_res;
+  hipError_t e = launch_result_init(ctx->d_res, n, s);
+  uint64_t fixed = 0;
+  if (n && protocol == TGPU_PROTOCOL_BINARY && schema->fixed_binary && !offsets &&
+      in_len >= n * (uint64_t)schema->tmpl.wire_len) {
+    fixed = schema->tmpl.wire_len;
+    if (e == hipSuccess)
+      e = launch_fixed_binary_decode(&schema->tmpl, schema->d_tmpl, a.in, n, a.recs, ctx->d_res, s);
+    a.offs = ctx->d_offs;
+    a.check_index = 0;
+    if (e == hipSuccess) e = launch_serial_decode(a, protocol, true, fixed, s);
+  } else if (n) {
+    if (offsets) {
+      a.offs = offsets;
+      a.check_index = 1;
+      if (e == hipSuccess) e = launch_general_decode(a, protocol, s);
+    } else {
+      a.offs = ctx->d_offs;
+      a.check_index = 0;
+      if (e == hipSuccess) e = launch_serial_decode(a, protocol, false, 0, s);
+    }
+  }
+  if (e == hipSuccess && n) e = launch_decode_finish(a, protocol, fixed, s);
+  ctx->last_op = 1;
+  if (e != hipSuccess) {
+    fill_status(st, TGPU_ERR_HIP, 0, 0);
+    return TGPU_ERR_HIP;
+  }
+  if (st || n_decoded || consumed) {
+    tgpu_status tmp;
+    return tgpu_context_wait(ctx, stream, st ? st : &tmp, n_decoded, consumed);
+  }
+  return TGPU_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,698 @@
+// tgpu_device.h — per-lane Binary/Compact reader and writer used by the
+// general (table-driven) gfx950 kernels. One lane parses or emits one record.
+//
+// Semantics follow the reference exactly (file:line in the fbthrift tree):
+//   field headers   BinaryProtocol-inl.h:586-632; CompactProtocol-inl.h:811-910
+//   scalar reads    BinaryProtocol-inl.h:489-533; CompactProtocol-inl.h:692-740
+//   varints         VarintUtils-inl.h:94-134 (max ceil(bits/7) bytes, junk high
+//                   bits dropped, overlong zeros accepted), :648-663 zigzag
+//   strings         Protocol.h:435-449 readStringBody (truncation checked first)
+//   lists           protocol_methods.h:389-467 (reset, type-mismatch skip_n,
+//                   canReadNElements, element reads)
+//   skip            BinaryProtocol.cpp:140-225; Protocol.h:187-344 (Compact)
+//   depth           Protocol.h:59-78 descend/ascend (height = max_depth + 1)
+//   struct driver   deserialize_struct.whisker:19-160 (any order, unknown and
+//                   type-mismatched fields skipped, isset set after the read)
+//   writers         BinaryProtocol-inl.h:41-222; CompactProtocol-inl.h:91-383;
+//                   serialize_struct.whisker:40-67
+// Device code cannot throw: the first error is latched in the reader/writer
+// (code + byte offset) and every later operation becomes a no-op.
+#pragma once
+
+#include "tgpu_internal.h"
+
+namespace tgpu {
+namespace dev {
+
+__device__ __forceinline__ bool is_scalar(uint32_t t) {
+  return t == TGPU_T_BOOL || t == TGPU_T_BYTE || t == TGPU_T_I16 || t == TGPU_T_I32 ||
+         t == TGPU_T_I64 || t == TGPU_T_DOUBLE || t == TGPU_T_FLOAT;
+}
+__device__ __forceinline__ uint32_t scalar_size(uint32_t t) {
+  return (t == TGPU_T_BOOL || t == TGPU_T_BYTE) ? 1
+         : t == TGPU_T_I16                      ? 2
+         : (t == TGPU_T_I32 || t == TGPU_T_FLOAT) ? 4
+                                                  : 8;
+}
+// CompactProtocol-inl.h:48-86
+__device__ __forceinline__ uint32_t ctype_to_ttype(uint32_t ct) {
+  // packed nibble table for ct 0..13
+  constexpr uint8_t tbl[14] = {TGPU_T_STOP, TGPU_T_BOOL, TGPU_T_BOOL, TGPU_T_BYTE,
+                               TGPU_T_I16,  TGPU_T_I32,  TGPU_T_I64,  TGPU_T_DOUBLE,
+                               TGPU_T_STRING, TGPU_T_LIST, TGPU_T_SET, TGPU_T_MAP,
+                               TGPU_T_STRUCT, TGPU_T_FLOAT};
+  return tbl[ct];
+}
+__device__ __forceinline__ uint32_t ttype_to_ctype(uint32_t t) {
+  switch (t) {
+    case TGPU_T_BOOL: return 1;
+    case TGPU_T_BYTE: return 3;
+    case TGPU_T_I16: return 4;
+    case TGPU_T_I32: return 5;
+    case TGPU_T_I64: return 6;
+    case TGPU_T_DOUBLE: return 7;
+    case TGPU_T_STRING: return 8;
+    case TGPU_T_LIST: return 9;
+    case TGPU_T_SET: return 10;
+    case TGPU_T_MAP: return 11;
+    case TGPU_T_STRUCT: return 12;
+    case TGPU_T_FLOAT: return 13;
+    default: return 0;
+  }
+}
+__device__ __forceinline__ int32_t zz_to_i32(uint32_t n) {
+  return (n & 1) ? (int32_t)~(n >> 1) : (int32_t)(n >> 1);
+}
+__device__ __forceinline__ int64_t zz_to_i64(uint64_t n) {
+  return (n & 1) ? (int64_t)~(n >> 1) : (int64_t)(n >> 1);
+}
+__device__ __forceinline__ uint32_t i32_to_zz(int32_t n) {
+  return ((uint32_t)n << 1) ^ (uint32_t)(n >> 31);
+}
+__device__ __forceinline__ uint64_t i64_to_zz(int64_t n) {
+  return ((uint64_t)n << 1) ^ (uint64_t)(n >> 63);
+}
+
+// ------------------------------------------------------------------ reader --
+struct Reader {
+  const uint8_t* p;
+  uint64_t pos, end;
+  int64_t height;
+  int32_t string_limit, container_limit, max_depth;
+  int32_t err;
+  uint64_t err_off;
+  bool has_bool, bool_val;  // Compact boolValue_ latch
+
+  __device__ __forceinline__ bool ok() const { return err == 0; }
+  __device__ __forceinline__ void fail(int32_t code, uint64_t off) {
+    if (!err) {
+      err = code;
+      err_off = off;
+    }
+  }
+  __device__ __forceinline__ uint32_t read8() {
+    if (pos >= end) {
+      fail(TGPU_ERR_UNDERFLOW, pos);
+      return 0;
+    }
+    return p[pos++];
+  }
+  __device__ __forceinline__ uint64_t readBE(uint32_t nbytes) {
+    if (end - pos < nbytes) {
+      fail(TGPU_ERR_UNDERFLOW, pos);
+      pos = end;
+      return 0;
+    }
+    uint64_t v = 0;
+    for (uint32_t i = 0; i < nbytes; ++i) v = (v << 8) | p[pos + i];
+    pos += nbytes;
+    return v;
+  }
+  __device__ __forceinline__ void skip_bytes(uint64_t n) {
+    if (end - pos < n) {
+      fail(TGPU_ERR_UNDERFLOW, pos);
+      pos = end;
+      return;
+    }
+    pos += n;
+  }
+  // LEB128 with kMax = ceil(bits/7) bytes; value truncated to `bits`.
+  __device__ __forceinline__ uint64_t varint(uint32_t bits) {
+    const uint32_t kmax = (bits + 6) / 7;
+    const uint64_t start = pos;
+    uint64_t r = 0;
+    for (uint32_t i = 0; i < kmax; ++i) {
+      if (pos >= end) {
+        fail(TGPU_ERR_UNDERFLOW, pos);
+        return 0;
+      }
+      const uint64_t b = p[pos++];
+      r |= (b & 0x7f) << (7 * i);
+      if (!(b & 0x80)) return bits < 64 ? (r & ((1ull << bits) - 1)) : r;
+    }
+    fail(TGPU_ERR_INVALID_VARINT, start);
+    return 0;
+  }
+  __device__ __forceinline__ void descend(uint64_t off) {
+    if (!--height) fail(TGPU_ERR_DEPTH_LIMIT, off);
+  }
+  __device__ __forceinline__ void ascend() { ++height; }
+};
+
+template <int P>
+struct Proto;
+
+// ---------------------------------------------------------------- Binary ----
+template <>
+struct Proto<TGPU_PROTOCOL_BINARY> {
+  static constexpr uint64_t kArenaScale = 1;
+  // returns false on STOP (or error)
+  static __device__ __forceinline__ bool field_header(Reader& r, int32_t /*prev*/,
+                                                      uint32_t& type, int32_t& id) {
+    type = r.read8();
+    if (!r.ok() || type == TGPU_T_STOP) return false;
+    id = (int16_t)r.readBE(2);
+    return r.ok();
+  }
+  static __device__ __forceinline__ uint32_t read_bool(Reader& r) {
+    const uint64_t off = r.pos;
+    const uint32_t b = r.read8();
+    if (b >= 2) r.fail(TGPU_ERR_BOOL_VALUE, off);
+    return b ? 1 : 0;
+  }
+  static __device__ __forceinline__ void check_container(Reader& r, int32_t size, uint64_t off) {
+    if (size < 0) r.fail(TGPU_ERR_NEGATIVE_SIZE, off);
+    else if (r.container_limit && size > r.container_limit) r.fail(TGPU_ERR_SIZE_LIMIT, off);
+  }
+  static __device__ __forceinline__ void list_begin(Reader& r, uint32_t& elem, int32_t& size) {
+    r.descend(r.pos);
+    if (!r.ok()) return;
+    elem = r.read8();
+    const uint64_t soff = r.pos;
+    size = (int32_t)(uint32_t)r.readBE(4);
+    if (r.ok()) check_container(r, size, soff);
+  }
+  static __device__ __forceinline__ void map_begin(Reader& r, uint32_t& k, uint32_t& v, int32_t& size) {
+    r.descend(r.pos);
+    if (!r.ok()) return;
+    k = r.read8();
+    v = r.read8();
+    const uint64_t soff = r.pos;
+    size = (int32_t)(uint32_t)r.readBE(4);
+    if (r.ok()) check_container(r, size, soff);
+  }
+  static __device__ __forceinline__ void read_string(Reader& r, uint64_t& view, uint32_t& len) {
+    const uint64_t off = r.pos;
+    const int32_t size = (int32_t)(uint32_t)r.readBE(4);
+    if (!r.ok()) return;
+    if (size < 0) return r.fail(TGPU_ERR_NEGATIVE_SIZE, off);
+    if (r.string_limit > 0 && size > r.string_limit) return r.fail(TGPU_ERR_SIZE_LIMIT, off);
+    if (r.end - r.pos < (uint64_t)size) return r.fail(TGPU_ERR_TRUNCATED, r.pos);
+    view = r.pos;
+    len = (uint32_t)size;
+    r.pos += (uint64_t)size;
+  }
+  static __device__ __forceinline__ uint32_t fixed_in_container(uint32_t t) {
+    return (t == TGPU_T_BOOL || t == TGPU_T_BYTE) ? 1
+           : t == TGPU_T_I16                      ? 2
+           : (t == TGPU_T_I32 || t == TGPU_T_FLOAT) ? 4
+           : (t == TGPU_T_I64 || t == TGPU_T_DOUBLE) ? 8
+                                                     : 0;
+  }
+  // Skip of a leaf value; returns false if `t` is a container/struct that
+  // needs a frame (handled by the caller's explicit stack).
+  static __device__ __forceinline__ bool skip_leaf(Reader& r, uint32_t t) {
+    switch (t) {
+      case TGPU_T_BYTE: case TGPU_T_BOOL: r.skip_bytes(1); return true;
+      case TGPU_T_I16: r.skip_bytes(2); return true;
+      case TGPU_T_FLOAT: case TGPU_T_I32: r.skip_bytes(4); return true;
+      case TGPU_T_DOUBLE: case TGPU_T_U64: case TGPU_T_I64: r.skip_bytes(8); return true;
+      case TGPU_T_UTF8: case TGPU_T_UTF16: case TGPU_T_STRING: {
+        const uint64_t before = r.pos;
+        const int32_t size = (int32_t)(uint32_t)r.readBE(4);
+        if (!r.ok()) return true;
+        // canAdvance from the cursor copy taken before the length
+        const uint64_t want = (uint64_t)(int64_t)size;
+        if (r.end - before < want) {
+          r.fail(TGPU_ERR_TRUNCATED, r.pos);
+          return true;
+        }
+        r.skip_bytes((uint64_t)(uint32_t)size);
+        return true;
+      }
+      default: return false;
+    }
+  }
+  static __device__ __forceinline__ void read_scalar(Reader& r, uint32_t t, uint8_t* dst) {
+    switch (t) {
+      case TGPU_T_BOOL: *dst = (uint8_t)read_bool(r); break;
+      case TGPU_T_BYTE: *dst = (uint8_t)r.read8(); break;
+      case TGPU_T_I16: { const uint16_t v = (uint16_t)r.readBE(2); if (r.ok()) *(uint16_t*)dst = v; break; }
+      case TGPU_T_I32:
+      case TGPU_T_FLOAT: { const uint32_t v = (uint32_t)r.readBE(4); if (r.ok()) *(uint32_t*)dst = v; break; }
+      default: { const uint64_t v = r.readBE(8); if (r.ok()) *(uint64_t*)dst = v; break; }
+    }
+  }
+};
+
+// --------------------------------------------------------------- Compact ----
+template <>
+struct Proto<TGPU_PROTOCOL_COMPACT> {
+  static constexpr uint64_t kArenaScale = 8;
+  static __device__ __forceinline__ uint32_t get_type(Reader& r, uint32_t ct, uint64_t off) {
+    if (ct >= 14) {
+      r.fail(TGPU_ERR_BAD_TYPE, off);
+      return TGPU_T_STOP;
+    }
+    return ctype_to_ttype(ct);
+  }
+  static __device__ __forceinline__ bool field_header(Reader& r, int32_t prev, uint32_t& type,
+                                                      int32_t& id) {
+    const uint64_t off = r.pos;
+    const uint32_t b = r.read8();
+    if (!r.ok() || (b & 0x0f) == 0) return false;  // STOP
+    const int32_t mod = (int32_t)(b >> 4);
+    if (mod) id = (int16_t)(prev + mod);
+    else id = (int16_t)zz_to_i32((uint32_t)r.varint(32));
+    if (!r.ok()) return false;
+    const uint32_t ct = b & 0x0f;
+    type = get_type(r, ct, off);
+    if (ct == 1 || ct == 2) {
+      r.has_bool = true;
+      r.bool_val = ct == 1;
+    }
+    return r.ok();
+  }
+  static __device__ __forceinline__ uint32_t read_bool(Reader& r) {
+    if (r.has_bool) {
+      r.has_bool = false;
+      return r.bool_val ? 1 : 0;
+    }
+    return r.read8() == 1 ? 1 : 0;
+  }
+  static __device__ __forceinline__ void list_begin(Reader& r, uint32_t& elem, int32_t& size) {
+    const uint64_t off = r.pos;
+    r.descend(off);
+    if (!r.ok()) return;
+    const uint32_t b = r.read8();
+    if (!r.ok()) return;
+    int32_t lsize = (int32_t)((b >> 4) & 0x0f);
+    if (lsize == 15) lsize = (int32_t)(uint32_t)r.varint(32);
+    if (!r.ok()) return;
+    if (lsize < 0) return r.fail(TGPU_ERR_NEGATIVE_SIZE, off);
+    if (r.container_limit && lsize > r.container_limit) return r.fail(TGPU_ERR_SIZE_LIMIT, off);
+    elem = get_type(r, b & 0x0f, off);
+    size = lsize;
+  }
+  static __device__ __forceinline__ void map_begin(Reader& r, uint32_t& k, uint32_t& v, int32_t& size) {
+    const uint64_t off = r.pos;
+    r.descend(off);
+    if (!r.ok()) return;
+    uint32_t kv = 0;
+    const int32_t msize = (int32_t)(uint32_t)r.varint(32);
+    if (!r.ok()) return;
+    if (msize != 0) kv = r.read8();
+    if (!r.ok()) return;
+    if (msize < 0) return r.fail(TGPU_ERR_NEGATIVE_SIZE, off);
+    if (r.container_limit && msize > r.container_limit) return r.fail(TGPU_ERR_SIZE_LIMIT, off);
+    k = get_type(r, kv >> 4, off);
+    v = get_type(r, kv & 0xf, off);
+    size = msize;
+  }
+  static __device__ __forceinline__ void read_string(Reader& r, uint64_t& view, uint32_t& len) {
+    const uint64_t off = r.pos;
+    const int32_t size = (int32_t)(uint32_t)r.varint(32);
+    if (!r.ok()) return;
+    if (size < 0) return r.fail(TGPU_ERR_NEGATIVE_SIZE, off);
+    if (r.string_limit > 0 && size > r.string_limit) return r.fail(TGPU_ERR_SIZE_LIMIT, off);
+    if (size == 0) {
+      view = 0;
+      len = 0;
+      return;
+    }
+    if (r.end - r.pos < (uint64_t)size) return r.fail(TGPU_ERR_TRUNCATED, r.pos);
+    view = r.pos;
+    len = (uint32_t)size;
+    r.pos += (uint64_t)size;
+  }
+  static __device__ __forceinline__ uint32_t fixed_in_container(uint32_t t) {
+    return (t == TGPU_T_BOOL || t == TGPU_T_BYTE) ? 1
+           : t == TGPU_T_FLOAT                    ? 4
+           : t == TGPU_T_DOUBLE                   ? 8
+                                                  : 0;
+  }
+  static __device__ __forceinline__ bool skip_leaf(Reader& r, uint32_t t) {
+    switch (t) {
+      case TGPU_T_BOOL: read_bool(r); return true;
+      case TGPU_T_BYTE: r.read8(); return true;
+      case TGPU_T_I16: case TGPU_T_I32: r.varint(32); return true;
+      case TGPU_T_U64: case TGPU_T_I64: r.varint(64); return true;
+      case TGPU_T_DOUBLE: r.readBE(8); return true;
+      case TGPU_T_FLOAT: r.readBE(4); return true;
+      case TGPU_T_UTF8: case TGPU_T_UTF16: case TGPU_T_STRING: {
+        uint64_t v;
+        uint32_t l;
+        read_string(r, v, l);
+        return true;
+      }
+      default: return false;
+    }
+  }
+  static __device__ __forceinline__ void read_scalar(Reader& r, uint32_t t, uint8_t* dst) {
+    switch (t) {
+      case TGPU_T_BOOL: *dst = (uint8_t)read_bool(r); break;
+      case TGPU_T_BYTE: *dst = (uint8_t)r.read8(); break;
+      case TGPU_T_I16: { const int16_t v = (int16_t)zz_to_i32((uint32_t)r.varint(32)); if (r.ok()) *(int16_t*)dst = v; break; }
+      case TGPU_T_I32: { const int32_t v = zz_to_i32((uint32_t)r.varint(32)); if (r.ok()) *(int32_t*)dst = v; break; }
+      case TGPU_T_I64: { const int64_t v = zz_to_i64(r.varint(64)); if (r.ok()) *(int64_t*)dst = v; break; }
+      case TGPU_T_FLOAT: { const uint32_t v = (uint32_t)r.readBE(4); if (r.ok()) *(uint32_t*)dst = v; break; }
+      default: { const uint64_t v = r.readBE(8); if (r.ok()) *(uint64_t*)dst = v; break; }
+    }
+  }
+};
+
+// -------------------------------------------------------------------- skip --
+// Iterative skip with an explicit frame stack (no recursion on the GPU).
+// Frame kinds: struct (Binary: no delta; Compact: last field id), list/set
+// (remaining elements), map (remaining pairs, key/value phase).
+struct SkipFrame {
+  uint8_t kind;  // 1 struct, 2 list, 3 map
+  uint8_t t0, t1, phase;
+  int32_t last_or_remaining;
+  int32_t depth;  // depth of the values inside this frame
+};
+
+template <int P>
+__device__ void skip(Reader& r, uint32_t type, int32_t depth) {
+  using Pr = Proto<P>;
+  SkipFrame st[kMaxSkipDepth];
+  int sp = 0;
+  uint32_t cur = type;
+  int32_t cdepth = depth;
+  bool have = true;  // a value of type `cur` at `cdepth` is to be skipped
+  while (r.ok()) {
+    if (have) {
+      have = false;
+      if (cdepth >= r.max_depth) return r.fail(TGPU_ERR_DEPTH_LIMIT, r.pos);
+      if (!Pr::skip_leaf(r, cur)) {
+        if (cur == TGPU_T_STRUCT) {
+          r.descend(r.pos);  // readStructBegin
+          if (!r.ok()) return;
+          if (sp == kMaxSkipDepth) return r.fail(TGPU_ERR_UNSUPPORTED, r.pos);
+          st[sp++] = SkipFrame{1, 0, 0, 0, 0, cdepth + 1};
+        } else if (cur == TGPU_T_LIST || cur == TGPU_T_SET || cur == TGPU_T_MAP) {
+          uint32_t a = 0, b = 0;
+          int32_t n = 0;
+          const bool is_map = cur == TGPU_T_MAP;
+          if (is_map) Pr::map_begin(r, a, b, n);
+          else Pr::list_begin(r, a, n);
+          if (!r.ok()) return;
+          // skip_n(n, types, depth + 1) (Protocol.h:317-344)
+          if (cdepth + 1 >= r.max_depth) return r.fail(TGPU_ERR_DEPTH_LIMIT, r.pos);
+          const uint32_t fa = Pr::fixed_in_container(a);
+          const uint32_t fb = is_map ? Pr::fixed_in_container(b) : 1;
+          if (fa && fb) {
+            const uint64_t sum = fa + (is_map ? fb : 0);
+            r.skip_bytes(sum * (uint64_t)(uint32_t)n);
+            r.ascend();
+          } else {
+            if (sp == kMaxSkipDepth) return r.fail(TGPU_ERR_UNSUPPORTED, r.pos);
+            st[sp++] = SkipFrame{(uint8_t)(is_map ? 3 : 2), (uint8_t)a, (uint8_t)b, 0, n,
+                                 cdepth + 2};
+          }
+        } else {
+          return r.fail(TGPU_ERR_INVALID_SKIP_TYPE, r.pos);
+        }
+      }
+      continue;
+    }
+    if (sp == 0) return;
+    SkipFrame& f = st[sp - 1];
+    if (f.kind == 1) {
+      uint32_t ft;
+      int32_t fid = 0;
+      if (P == TGPU_PROTOCOL_BINARY) {
+        // BinaryProtocolReader::skip: readByte, STOP?, skipBytes(2)
+        ft = r.read8();
+        if (!r.ok()) return;
+        if (ft == TGPU_T_STOP) {
+          r.ascend();
+          --sp;
+          continue;
+        }
+        r.skip_bytes(2);
+        if (!r.ok()) return;
+      } else {
+        if (!Pr::field_header(r, f.last_or_remaining, ft, fid)) {
+          if (!r.ok()) return;
+          r.ascend();
+          --sp;
+          continue;
+        }
+        f.last_or_remaining = fid;
+      }
+      cur = ft;
+      cdepth = f.depth;
+      have = true;
+    } else {
+      if (f.last_or_remaining == 0 && f.phase == 0) {
+        r.ascend();
+        --sp;
+        continue;
+      }
+      if (f.kind == 2) {
+        --f.last_or_remaining;
+        cur = f.t0;
+      } else {
+        if (f.phase == 0) {
+          --f.last_or_remaining;
+          cur = f.t0;
+          f.phase = 1;
+        } else {
+          cur = f.t1;
+          f.phase = 0;
+        }
+      }
+      cdepth = f.depth;
+      have = true;
+    }
+  }
+}
+
+// ------------------------------------------------------------ struct read ---
+struct ReadFrame {
+  uint32_t si;
+  uint32_t obj;  // byte offset of the struct inside the record
+  int32_t prev;  // Compact delta base
+  uint32_t fidx; // field being read into (for isset after a nested struct)
+};
+
+template <int P>
+__device__ void read_list(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8_t* arena,
+                          uint64_t arena_cap) {
+  using Pr = Proto<P>;
+  tgpu_span sp{0, 0, 0};
+  *(tgpu_span*)m = sp;
+  uint32_t reported = 0;
+  int32_t n = 0;
+  Pr::list_begin(r, reported, n);
+  if (!r.ok()) return;
+  if (reported != f.elem_ttype) {
+    // skip_n(protocol, n, {reported}) with depth 0
+    if (0 >= r.max_depth) return r.fail(TGPU_ERR_DEPTH_LIMIT, r.pos);
+    const uint32_t fs = Pr::fixed_in_container(reported);
+    if (fs) {
+      r.skip_bytes((uint64_t)fs * (uint32_t)n);
+    } else {
+      for (int32_t i = 0; i < n && r.ok(); ++i) skip<P>(r, reported, 1);
+    }
+  } else {
+    if (r.end - r.pos < (uint64_t)(uint32_t)n) return r.fail(TGPU_ERR_TRUNCATED, r.pos);
+    const uint32_t es = scalar_size(f.elem_ttype);
+    const uint64_t aoff = Pr::kArenaScale * r.pos;
+    if (n > 0) {
+      if (!arena || aoff + (uint64_t)n * es > arena_cap) return r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
+      sp.offset = aoff;
+      sp.length = (uint32_t)n;
+      for (int32_t i = 0; i < n && r.ok(); ++i)
+        Pr::read_scalar(r, f.elem_ttype, arena + aoff + (uint64_t)i * es);
+      *(tgpu_span*)m = sp;
+    }
+  }
+  if (r.ok()) r.ascend();
+}
+
+template <int P>
+__device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, uint8_t* arena,
+                            uint64_t arena_cap) {
+  using Pr = Proto<P>;
+  ReadFrame st[kMaxSchemaDepth];
+  int sp = 0;
+  st[sp++] = ReadFrame{0, 0, 0, 0};
+  while (sp > 0 && r.ok()) {
+    ReadFrame& fr = st[sp - 1];
+    uint32_t wt = 0;
+    int32_t id = 0;
+    if (!Pr::field_header(r, fr.prev, wt, id)) {
+      if (!r.ok()) return;
+      // STOP: struct done; mark the parent's field set
+      --sp;
+      if (sp > 0) {
+        const ReadFrame& parent = st[sp - 1];
+        const tgpu_field_desc& pf = sc.f[parent.fidx];
+        rec[parent.obj + pf.isset_offset] = 1;
+      }
+      continue;
+    }
+    fr.prev = id;
+    const tgpu_struct_desc sd = sc.s[fr.si];
+    int32_t hit = -1;
+    for (uint32_t k = 0; k < sd.num_fields; ++k) {
+      if (sc.f[sd.first_field + k].id == id) {
+        hit = (int32_t)(sd.first_field + k);
+        break;
+      }
+    }
+    if (hit < 0 || sc.f[hit].ttype != wt) {
+      skip<P>(r, wt, 0);
+      continue;
+    }
+    const tgpu_field_desc f = sc.f[hit];
+    uint8_t* m = rec + fr.obj + f.member_offset;
+    if (is_scalar(f.ttype)) {
+      Pr::read_scalar(r, f.ttype, m);
+    } else if (f.ttype == TGPU_T_STRING) {
+      uint64_t v = 0;
+      uint32_t l = 0;
+      Pr::read_string(r, v, l);
+      if (r.ok()) *(tgpu_span*)m = tgpu_span{l ? v : 0, l, 0};
+    } else if (f.ttype == TGPU_T_STRUCT) {
+      if (sp == kMaxSchemaDepth) return r.fail(TGPU_ERR_UNSUPPORTED, r.pos);
+      fr.fidx = (uint32_t)hit;
+      st[sp++] = ReadFrame{(uint32_t)f.struct_index, fr.obj + f.member_offset, 0, 0};
+      continue;  // isset set when the nested STOP is reached
+    } else {
+      read_list<P>(r, f, m, arena, arena_cap);
+    }
+    if (r.ok()) rec[fr.obj + f.isset_offset] = 1;
+  }
+}
+
+// ------------------------------------------------------------------ writer --
+struct Writer {
+  uint8_t* out;  // nullptr: size only
+  uint64_t pos, cap;
+  int32_t err;
+  uint64_t err_off;
+  __device__ __forceinline__ bool ok() const { return err == 0; }
+  __device__ __forceinline__ void fail(int32_t code, uint64_t off) {
+    if (!err) {
+      err = code;
+      err_off = off;
+    }
+  }
+  __device__ __forceinline__ void put(uint32_t b) {
+    if (out) out[pos] = (uint8_t)b;
+    ++pos;
+  }
+  __device__ __forceinline__ void put_be(uint64_t v, uint32_t n) {
+    for (int i = (int)n - 1; i >= 0; --i) put((uint32_t)(v >> (8 * i)));
+  }
+  __device__ __forceinline__ void varint(uint64_t v) {
+    while (v & ~0x7full) {
+      put((uint32_t)((v & 0x7f) | 0x80));
+      v >>= 7;
+    }
+    put((uint32_t)v);
+  }
+  __device__ __forceinline__ void bytes(const uint8_t* src, uint32_t n) {
+    if (out) for (uint32_t i = 0; i < n; ++i) out[pos + i] = src[i];
+    pos += n;
+  }
+};
+
+__device__ __forceinline__ uint32_t load_bool(Writer& w, const uint8_t* p) {
+  const uint32_t b = *p;
+  if (b > 1) w.fail(TGPU_ERR_INVALID_BOOL_WRITE, w.pos);  // validate_bool
+  return b;
+}
+
+template <int P>
+__device__ __forceinline__ void write_scalar(Writer& w, uint32_t t, const uint8_t* p) {
+  if (P == TGPU_PROTOCOL_BINARY) {
+    switch (t) {
+      case TGPU_T_BOOL: w.put(load_bool(w, p)); break;
+      case TGPU_T_BYTE: w.put(*p); break;
+      case TGPU_T_I16: w.put_be(*(const uint16_t*)p, 2); break;
+      case TGPU_T_I32: case TGPU_T_FLOAT: w.put_be(*(const uint32_t*)p, 4); break;
+      default: w.put_be(*(const uint64_t*)p, 8); break;
+    }
+  } else {
+    switch (t) {
+      case TGPU_T_BOOL: w.put(load_bool(w, p) ? 1 : 2); break;
+      case TGPU_T_BYTE: w.put(*p); break;
+      case TGPU_T_I16: w.varint(i32_to_zz(*(const int16_t*)p)); break;
+      case TGPU_T_I32: w.varint(i32_to_zz(*(const int32_t*)p)); break;
+      case TGPU_T_I64: w.varint(i64_to_zz(*(const int64_t*)p)); break;
+      case TGPU_T_FLOAT: w.put_be(*(const uint32_t*)p, 4); break;
+      default: w.put_be(*(const uint64_t*)p, 8); break;
+    }
+  }
+}
+
+struct WriteFrame {
+  uint32_t si;
+  uint32_t obj;
+  uint32_t k;     // next field index within the struct
+  int32_t last;   // Compact lastFieldId_
+};
+
+template <int P>
+__device__ void write_record(Writer& w, const DevSchema& sc, const uint8_t* rec,
+                             const uint8_t* sbase, const uint8_t* lbase) {
+  WriteFrame st[kMaxSchemaDepth];
+  int sp = 0;
+  st[sp++] = WriteFrame{0, 0, 0, 0};
+  while (sp > 0 && w.ok()) {
+    WriteFrame& fr = st[sp - 1];
+    const tgpu_struct_desc sd = sc.s[fr.si];
+    if (fr.k == sd.num_fields) {
+      w.put(0);  // writeFieldStop (T_STOP / CT_STOP are both 0)
+      --sp;
+      continue;
+    }
+    const tgpu_field_desc f = sc.f[sd.first_field + fr.k++];
+    const uint8_t* obj = rec + fr.obj;
+    if (f.qualifier == TGPU_OPTIONAL && !obj[f.isset_offset]) continue;
+    const uint8_t* m = obj + f.member_offset;
+    if (P == TGPU_PROTOCOL_BINARY) {
+      w.put(f.ttype);
+      w.put_be((uint16_t)f.id, 2);
+    } else {
+      uint32_t ct = ttype_to_ctype(f.ttype);
+      if (f.ttype == TGPU_T_BOOL) ct = load_bool(w, m) ? 1 : 2;
+      const int32_t id = f.id;
+      if (id > fr.last && id - fr.last <= 15) {
+        w.put((uint32_t)(((id - fr.last) << 4) | ct));
+      } else {
+        w.put(ct);
+        w.varint(i32_to_zz(id));
+      }
+      fr.last = id;
+      if (f.ttype == TGPU_T_BOOL) continue;
+    }
+    if (is_scalar(f.ttype)) {
+      write_scalar<P>(w, f.ttype, m);
+    } else if (f.ttype == TGPU_T_STRING) {
+      const tgpu_span sp_ = *(const tgpu_span*)m;
+      if (sp_.length > 0x7fffffffu) return w.fail(TGPU_ERR_WRITE_SIZE_LIMIT, w.pos);
+      if (P == TGPU_PROTOCOL_BINARY) w.put_be(sp_.length, 4);
+      else w.varint(sp_.length);
+      w.bytes(sbase + sp_.offset, sp_.length);
+    } else if (f.ttype == TGPU_T_STRUCT) {
+      if (sp == kMaxSchemaDepth) return w.fail(TGPU_ERR_UNSUPPORTED, w.pos);
+      st[sp++] = WriteFrame{(uint32_t)f.struct_index, fr.obj + f.member_offset, 0, 0};
+    } else {  // list / set of scalars
+      const tgpu_span sp_ = *(const tgpu_span*)m;
+      if (sp_.length > 0x7fffffffu) return w.fail(TGPU_ERR_WRITE_SIZE_LIMIT, w.pos);
+      if (P == TGPU_PROTOCOL_BINARY) {
+        w.put(f.elem_ttype);
+        w.put_be(sp_.length, 4);
+      } else {
+        const uint32_t ct = ttype_to_ctype(f.elem_ttype);
+        if (sp_.length <= 14) {
+          w.put((sp_.length << 4) | ct);
+        } else {
+          w.put(0xf0 | ct);
+          w.varint(sp_.length);
+        }
+      }
+      const uint32_t es = scalar_size(f.elem_ttype);
+      const uint8_t* e = lbase + sp_.offset;
+      for (uint32_t i = 0; i < sp_.length && w.ok(); ++i) write_scalar<P>(w, f.elem_ttype, e + (uint64_t)i * es);
+    }
+  }
+}
+
+}  // namespace dev
+}  // namespace tgpu

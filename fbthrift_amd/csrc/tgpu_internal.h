@@ -1,0 +1,119 @@
+// tgpu_internal.h — definitions shared by the C-ABI host code and the gfx950
+// kernels of the bulk Thrift record codec. Not part of the public ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/thrift_gpu.h"
+
+namespace tgpu {
+
+// Records per workgroup tile in the fixed-layout Binary kernels. 256 records x
+// any wire length L is a multiple of 16 bytes, so every tile starts on the
+// same 16-byte phase as the stream base.
+constexpr int kTileRecords = 256;
+constexpr int kBlock = 256;
+// Upper bound on the canonical wire length handled by the fixed-layout
+// kernels (LDS: 256 x (L + S) bytes must fit beside a second block).
+constexpr uint32_t kMaxFixedWire = 192;
+constexpr uint32_t kMaxFixedRecord = 160;
+constexpr int kMaxTemplateItems = 96;
+// Nesting supported by the general device reader/writer.
+constexpr int kMaxSchemaDepth = 8;
+constexpr int kMaxSkipDepth = 32;
+
+// One step of the canonical Binary wire template of a fixed-layout schema
+// (every field unqualified, fixed width; nested structs flattened). The item
+// covers `hdr_len` constant bytes (field header / STOP / nested header)
+// followed by `width` value bytes (big-endian on the wire).
+struct TemplateItem {
+  uint16_t wire_off;  // offset of the first byte of the item in the record
+  uint8_t hdr_len;    // 0..4 constant bytes
+  uint8_t width;      // 0,1,2,4,8 value bytes
+  uint32_t hdr;       // constant bytes, little-endian packed (byte 0 first)
+  uint16_t member_off;
+  uint8_t is_bool;    // value must be 0/1 (Binary readBool / validate_bool)
+  uint8_t pad;
+};
+
+struct FixedTemplate {
+  uint32_t wire_len;     // L
+  uint32_t record_size;  // S
+  uint32_t n_items;
+  uint32_t n_isset;      // isset bytes set to 1 (all of them; unqualified)
+  uint16_t isset_off[64];
+  TemplateItem items[kMaxTemplateItems];
+};
+
+// Device-side result slot of a context (one per in-flight call).
+struct DevResult {
+  unsigned long long first_fail;       // first failing record (UINT64_MAX: none)
+  unsigned long long first_irregular;  // fixed path: first non-canonical record
+  int32_t code;                        // diagnosed code of first_fail
+  int32_t pad;
+  unsigned long long fail_offset;      // diagnosed byte offset
+  unsigned long long total_bytes;      // encode: output size; decode: consumed
+  unsigned long long n_records;
+};
+
+struct DevSchema {
+  const tgpu_struct_desc* s;
+  const tgpu_field_desc* f;
+  uint32_t ns, nf;
+};
+
+struct DecodeArgs {
+  DevSchema sc;
+  const uint8_t* in;
+  uint64_t in_len;
+  const uint64_t* offs;  // n+1 record starts (given or computed)
+  uint64_t n;
+  uint8_t* recs;
+  uint8_t* arena;
+  uint64_t arena_cap;
+  int32_t string_limit, container_limit, max_depth, height;
+  uint32_t rec_size;
+  int check_index;  // offsets were supplied by the caller: verify lengths
+  DevResult* res;
+};
+
+struct EncodeArgs {
+  DevSchema sc;
+  const uint8_t* recs;
+  uint64_t n;
+  const uint8_t* sbase;
+  const uint8_t* lbase;
+  uint8_t* out;
+  uint64_t cap;
+  uint64_t* offs;  // n+1: sizes, then offsets
+  unsigned long long* block_sums;
+  uint32_t rec_size;
+  DevResult* res;
+};
+
+// Launchers (defined in the .hip files; all asynchronous on `stream`).
+// `t` is the host copy (launch geometry), `d_t` the device copy the kernels read.
+hipError_t launch_fixed_binary_decode(const FixedTemplate* t, const FixedTemplate* d_t,
+                                      const uint8_t* in, uint64_t n, uint8_t* out,
+                                      DevResult* res, hipStream_t stream);
+hipError_t launch_fixed_binary_encode(const FixedTemplate* t, const FixedTemplate* d_t,
+                                      const uint8_t* recs, uint64_t n, uint8_t* out,
+                                      uint64_t* offsets, DevResult* res,
+                                      hipStream_t stream);
+hipError_t launch_general_decode(const DecodeArgs& a, int protocol,
+                                 hipStream_t stream);
+hipError_t launch_serial_decode(const DecodeArgs& a, int protocol,
+                                bool from_irregular, uint64_t fixed_len,
+                                hipStream_t stream);
+hipError_t launch_decode_finish(const DecodeArgs& a, int protocol,
+                                uint64_t fixed_len, hipStream_t stream);
+hipError_t launch_general_encode(const EncodeArgs& a, int protocol,
+                                 uint64_t n_blocks, hipStream_t stream);
+hipError_t launch_general_size(const EncodeArgs& a, int protocol,
+                               uint64_t n_blocks, hipStream_t stream);
+hipError_t launch_encode_finish(const EncodeArgs& a, int protocol,
+                                uint64_t fixed_len, hipStream_t stream);
+hipError_t launch_result_init(DevResult* res, uint64_t n, hipStream_t stream);
+
+}  // namespace tgpu

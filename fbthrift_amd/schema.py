@@ -1,0 +1,165 @@
+"""Schema descriptors: the runtime-table form of a Thrift struct.
+
+Mirrors the reference's table-based serializer metadata (StructInfo /
+FieldInfo / TypeInfo, thrift/lib/cpp2/protocol/TableBasedSerializer.h:90-118,
+205-302) and the layout of codegen'd structs (members in IDL declaration
+order, thrift/compiler/generate/t_whisker_generator.cc:231-236, then one isset
+byte per field, thrift/lib/cpp2/detail/Isset.h:243-296). Strings and lists use
+16-byte spans (tgpu_span) in the device layout.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import (T_BOOL, T_BYTE, T_DOUBLE, T_FLOAT, T_I16, T_I32, T_I64, T_LIST,
+                   T_SET, T_STRING, T_STRUCT)
+
+SCALAR = {T_BOOL: 1, T_BYTE: 1, T_I16: 2, T_I32: 4, T_FLOAT: 4, T_I64: 8, T_DOUBLE: 8}
+NP_SCALAR = {T_BOOL: np.uint8, T_BYTE: np.int8, T_I16: np.int16, T_I32: np.int32,
+             T_I64: np.int64, T_DOUBLE: np.float64, T_FLOAT: np.float32}
+SPAN = np.dtype([("offset", "<u8"), ("length", "<u4"), ("reserved", "<u4")])
+
+OPTIONAL = 1
+
+
+class Field:
+    def __init__(self, id, ttype, elem_ttype=0, optional=False, struct=None, name=None):
+        self.id, self.ttype, self.elem_ttype = int(id), int(ttype), int(elem_ttype)
+        self.optional, self.struct = bool(optional), struct
+        self.name = name or "f%d" % self.id
+
+
+class Struct:
+    def __init__(self, name, fields):
+        self.name, self.fields = name, list(fields)
+
+
+class Schema:
+    """A record type (struct 0) plus the structs it nests, with the layout
+    computed by the same rule as tgpu_layout_compute()."""
+
+    def __init__(self, root):
+        self.root = root
+        self.structs = []
+        index = {}
+
+        def visit(s):
+            if id(s) in index:
+                return index[id(s)]
+            index[id(s)] = len(self.structs)
+            self.structs.append(s)
+            for f in s.fields:
+                if f.ttype == T_STRUCT:
+                    visit(f.struct)
+            return index[id(s)]
+
+        visit(root)
+        self._index = index
+        self._layout()
+
+    # -- layout -------------------------------------------------------------
+    def _layout(self):
+        self.size, self.align, self.member, self.isset = {}, {}, {}, {}
+        done = set()
+
+        def lay(si):
+            if si in done:
+                return
+            s = self.structs[si]
+            off, al_max = 0, 1
+            for k, f in enumerate(s.fields):
+                if f.ttype in SCALAR:
+                    sz = al = SCALAR[f.ttype]
+                elif f.ttype in (T_STRING, T_LIST, T_SET):
+                    sz, al = 16, 8
+                elif f.ttype == T_STRUCT:
+                    sub = self._index[id(f.struct)]
+                    lay(sub)
+                    sz, al = self.size[sub], self.align[sub]
+                else:
+                    raise ValueError("unsupported field type %d" % f.ttype)
+                off = (off + al - 1) // al * al
+                self.member[(si, k)] = off
+                off += sz
+                al_max = max(al_max, al)
+            for k in range(len(s.fields)):
+                self.isset[(si, k)] = off + k
+            off += len(s.fields)
+            self.align[si] = al_max
+            self.size[si] = (max(off, 1) + al_max - 1) // al_max * al_max
+            done.add(si)
+
+        for si in range(len(self.structs)):
+            lay(si)
+        self.record_size = self.size[0]
+
+    # -- C descriptors --------------------------------------------------------
+    def descriptors(self):
+        structs = (_lib.StructDesc * len(self.structs))()
+        nf = sum(len(s.fields) for s in self.structs)
+        fields = (_lib.FieldDesc * max(nf, 1))()
+        j = 0
+        for si, s in enumerate(self.structs):
+            structs[si].first_field = j
+            structs[si].num_fields = len(s.fields)
+            structs[si].size = self.size[si]
+            structs[si].align = self.align[si]
+            for k, f in enumerate(s.fields):
+                fd = fields[j]
+                fd.id, fd.ttype, fd.elem_ttype = f.id, f.ttype, f.elem_ttype
+                fd.qualifier = OPTIONAL if f.optional else 0
+                fd.member_offset = self.member[(si, k)]
+                fd.isset_offset = self.isset[(si, k)]
+                fd.struct_index = self._index[id(f.struct)] if f.ttype == T_STRUCT else -1
+                j += 1
+        return structs, len(self.structs), fields, nf
+
+    # -- numpy view of the record layout -------------------------------------
+    def dtype(self, si=0):
+        s = self.structs[si]
+        names, formats, offsets = [], [], []
+        for k, f in enumerate(s.fields):
+            names.append(f.name)
+            if f.ttype in SCALAR:
+                formats.append(NP_SCALAR[f.ttype])
+            elif f.ttype in (T_STRING, T_LIST, T_SET):
+                formats.append(SPAN)
+            else:
+                formats.append(self.dtype(self._index[id(f.struct)]))
+            offsets.append(self.member[(si, k)])
+        if s.fields:
+            names.append("__isset")
+            formats.append((np.uint8, (len(s.fields),)))
+            offsets.append(self.isset[(si, 0)])
+        return np.dtype({"names": names, "formats": formats, "offsets": offsets,
+                         "itemsize": self.size[si]})
+
+    def struct_index(self, s):
+        return self._index[id(s)]
+
+    @classmethod
+    def from_table(cls, table):
+        """Builds a Schema from the tests/golden manifest form: a list of
+        structs, each a list of [id, ttype, elem_ttype, qualifier, struct_index]."""
+        structs = [Struct("S%d" % i, []) for i in range(len(table))]
+        for si, rows in enumerate(table):
+            for fid, tt, et, q, sub in rows:
+                structs[si].fields.append(
+                    Field(fid, tt, et, optional=q == OPTIONAL,
+                          struct=structs[sub] if tt == T_STRUCT else None))
+        return cls(structs[0])
+
+
+def layout_compute_c(schema):
+    """Runs tgpu_layout_compute on the schema's descriptors (host-only) and
+    returns (structs, fields) as lists of tuples for comparison."""
+    structs, ns, fields, nf = schema.descriptors()
+    for i in range(nf):
+        fields[i].member_offset = 0
+        fields[i].isset_offset = 0
+    rc = _lib.lib().tgpu_layout_compute(ctypes.addressof(structs), ns, ctypes.addressof(fields), nf)
+    if rc:
+        raise RuntimeError("tgpu_layout_compute failed: %s" % _lib.CODES.get(rc, rc))
+    return ([(s.first_field, s.num_fields, s.size, s.align) for s in structs],
+            [(f.member_offset, f.isset_offset) for f in fields[:nf]])

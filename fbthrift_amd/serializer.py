@@ -1,0 +1,258 @@
+"""Python host mirror of fbthrift's Serializer<Reader, Writer> for whole
+batches (thrift/lib/cpp2/protocol/Serializer.h:34-224), over the C-ABI.
+
+    BinarySerializer.serialize(schema, records)   -> (wire, offsets)
+    CompactSerializer.deserialize(schema, wire, n) -> (records, arena, consumed)
+
+Device memory comes from torch (plumbing only); every byte of protocol work is
+done by the gfx950 kernels in libtgpu.so. Errors are raised as the exception
+the reference would throw: TProtocolException(type) or OutOfRange (the
+std::out_of_range of folly cursors / invalid varints); a bool byte > 1 on write
+raises AbortError where the reference calls LOG(FATAL) (Protocol.h:126-163).
+"""
+import ctypes
+
+from . import _lib
+from ._lib import PROTOCOL_BINARY, PROTOCOL_COMPACT
+
+
+class TProtocolException(Exception):
+    """apache::thrift::protocol::TProtocolException (TProtocolException.h:41-51)."""
+
+    UNKNOWN, INVALID_DATA, NEGATIVE_SIZE, SIZE_LIMIT = 0, 1, 2, 3
+    BAD_VERSION, NOT_IMPLEMENTED, MISSING_REQUIRED_FIELD = 4, 5, 6
+    CHECKSUM_MISMATCH, DEPTH_LIMIT = 7, 8
+
+    def __init__(self, type_, message, status=None):
+        super().__init__(message)
+        self.type = type_
+        self.status = status
+
+
+class OutOfRange(IndexError):
+    """std::out_of_range (folly cursor underflow, "invalid varint read")."""
+
+    def __init__(self, message, status=None):
+        super().__init__(message)
+        self.status = status
+
+
+class AbortError(RuntimeError):
+    """Where the reference terminates the process (validate_bool)."""
+
+    def __init__(self, message, status=None):
+        super().__init__(message)
+        self.status = status
+
+
+class TgpuError(RuntimeError):
+    def __init__(self, message, status=None):
+        super().__init__(message)
+        self.status = status
+
+
+def raise_for_status(st):
+    if st.code == 0:
+        return
+    name = _lib.CODES.get(st.code, str(st.code))
+    msg = "%s at record %d, byte %d" % (name, st.record, st.byte_offset)
+    if st.exc_class == 1:
+        raise OutOfRange(msg, st)
+    if st.exc_class == 2:
+        raise TProtocolException(st.tproto_type, msg, st)
+    if st.exc_class == 3:
+        raise AbortError(msg, st)
+    raise TgpuError(msg, st)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(stream):
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class GpuSchema:
+    """A Schema uploaded to the current device (tgpu_schema_create)."""
+
+    def __init__(self, schema):
+        self.schema = schema
+        structs, ns, fields, nf = schema.descriptors()
+        self._keep = (structs, fields)
+        h = ctypes.c_void_p()
+        rc = _lib.lib().tgpu_schema_create(ctypes.addressof(structs), ns,
+                                           ctypes.addressof(fields), nf, ctypes.byref(h))
+        if rc:
+            raise TgpuError("tgpu_schema_create: %s" % _lib.CODES.get(rc, rc))
+        self.handle = h
+        self.record_size = _lib.lib().tgpu_schema_record_size(h)
+        self.has_lists = any(f.ttype in (_lib.T_LIST, _lib.T_SET)
+                             for s in schema.structs for f in s.fields)
+
+    def fixed_wire_size(self, protocol):
+        return _lib.lib().tgpu_schema_fixed_wire_size(self.handle, protocol)
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and _lib._lib is not None:
+            _lib.lib().tgpu_schema_destroy(h)
+            self.handle = None
+
+
+class Context:
+    """Workspace + result slot (tgpu_context). One in-flight call at a time."""
+
+    def __init__(self, reserve=0):
+        h = ctypes.c_void_p()
+        rc = _lib.lib().tgpu_context_create(ctypes.byref(h))
+        if rc:
+            raise TgpuError("tgpu_context_create: %s" % _lib.CODES.get(rc, rc))
+        self.handle = h
+        if reserve:
+            self.reserve(reserve)
+
+    def reserve(self, n):
+        rc = _lib.lib().tgpu_context_reserve(self.handle, n)
+        if rc:
+            raise TgpuError("tgpu_context_reserve: %s" % _lib.CODES.get(rc, rc))
+
+    def wait(self, stream=None):
+        st = _lib.Status()
+        n, b = ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.lib().tgpu_context_wait(self.handle, _stream(stream), ctypes.byref(st),
+                                     ctypes.byref(n), ctypes.byref(b))
+        return st, n.value, b.value
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and _lib._lib is not None:
+            _lib.lib().tgpu_context_destroy(h)
+            self.handle = None
+
+
+class BatchSerializer:
+    """Serializer<Reader, Writer> for batches of records of one schema."""
+
+    def __init__(self, protocol):
+        self.protocol = protocol
+        self._ctx = None
+
+    def context(self):
+        if self._ctx is None:
+            self._ctx = Context()
+        return self._ctx
+
+    # -- size -----------------------------------------------------------------
+    def encoded_size(self, gschema, records, n=None, offsets=None, stream=None):
+        import torch
+
+        n = records.numel() // gschema.record_size if n is None else n
+        if offsets is None:
+            offsets = torch.empty(n + 1, dtype=torch.int64, device=records.device)
+        st, total = _lib.Status(), ctypes.c_uint64()
+        _lib.lib().tgpu_encoded_size(self.context().handle, gschema.handle, self.protocol,
+                                     _ptr(records), n, _ptr(offsets), _stream(stream),
+                                     ctypes.byref(st), ctypes.byref(total))
+        raise_for_status(st)
+        return offsets, total.value
+
+    # -- encode ---------------------------------------------------------------
+    def serialize(self, gschema, records, n=None, string_base=None, list_base=None,
+                  out=None, offsets=True, stream=None, sync=True):
+        """Encodes n records (a uint8 device tensor in the schema layout).
+        Returns (wire[:size], offsets or None) when sync, else the raw buffers."""
+        import torch
+
+        n = records.numel() // gschema.record_size if n is None else n
+        dev = records.device
+        off_t = None
+        if offsets is True:
+            off_t = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        elif offsets is not None and offsets is not False:
+            off_t = offsets
+        if out is None:
+            L = gschema.fixed_wire_size(self.protocol)
+            if L:
+                cap = n * L
+            else:
+                size_offs = off_t if off_t is not None else torch.empty(
+                    n + 1, dtype=torch.int64, device=dev)
+                _, cap = self.encoded_size(gschema, records, n, size_offs, stream)
+            out = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
+        st, size = _lib.Status(), ctypes.c_uint64()
+        rc = _lib.lib().tgpu_encode_batch(
+            self.context().handle, gschema.handle, self.protocol, _ptr(records), n,
+            _ptr(string_base), _ptr(list_base), _ptr(out), out.numel(), _ptr(off_t),
+            _stream(stream), ctypes.byref(st) if sync else None,
+            ctypes.byref(size) if sync else None)
+        if not sync:
+            if rc:
+                raise TgpuError("tgpu_encode_batch: %s" % _lib.CODES.get(rc, rc))
+            return out, off_t
+        raise_for_status(st)
+        return out[: size.value], off_t
+
+    # -- decode ---------------------------------------------------------------
+    def arena_bytes(self, gschema, in_len):
+        if not gschema.has_lists:
+            return 0
+        return in_len * (8 if self.protocol == PROTOCOL_COMPACT else 1)
+
+    def deserialize(self, gschema, wire, n, offsets=None, limits=None, records=None,
+                    arena=None, stream=None, sync=True):
+        """Decodes n records from the stream `wire` (uint8 device tensor).
+        Returns (records, arena, consumed_bytes)."""
+        import torch
+
+        dev = wire.device
+        if records is None:
+            records = torch.empty(max(n * gschema.record_size, 1), dtype=torch.uint8, device=dev)
+        cap = self.arena_bytes(gschema, wire.numel())
+        if arena is None and cap:
+            arena = torch.empty(cap, dtype=torch.uint8, device=dev)
+        lim = None
+        if limits is not None:
+            lim = _lib.Limits(*limits) if not isinstance(limits, _lib.Limits) else limits
+        st = _lib.Status()
+        n_dec, consumed = ctypes.c_uint64(), ctypes.c_uint64()
+        rc = _lib.lib().tgpu_decode_batch(
+            self.context().handle, gschema.handle, self.protocol, _ptr(wire), wire.numel(),
+            _ptr(offsets), n, _ptr(records), _ptr(arena), arena.numel() if arena is not None else 0,
+            ctypes.byref(lim) if lim is not None else None, _stream(stream),
+            ctypes.byref(st) if sync else None, ctypes.byref(n_dec) if sync else None,
+            ctypes.byref(consumed) if sync else None)
+        if not sync:
+            if rc:
+                raise TgpuError("tgpu_decode_batch: %s" % _lib.CODES.get(rc, rc))
+            return records, arena, None
+        raise_for_status(st)
+        return records, arena, consumed.value
+
+    def deserialize_status(self, gschema, wire, n, offsets=None, limits=None, stream=None):
+        """Like deserialize but returns (records, arena, status, n_decoded,
+        consumed) instead of raising — used by the parity tests."""
+        import torch
+
+        dev = wire.device
+        records = torch.zeros(max(n * gschema.record_size, 1), dtype=torch.uint8, device=dev)
+        cap = self.arena_bytes(gschema, wire.numel())
+        arena = torch.zeros(max(cap, 1), dtype=torch.uint8, device=dev)
+        lim = None
+        if limits is not None:
+            lim = _lib.Limits(*limits)
+        st = _lib.Status()
+        n_dec, consumed = ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.lib().tgpu_decode_batch(
+            self.context().handle, gschema.handle, self.protocol, _ptr(wire), wire.numel(),
+            _ptr(offsets), n, _ptr(records), _ptr(arena), cap,
+            ctypes.byref(lim) if lim is not None else None, _stream(stream), ctypes.byref(st),
+            ctypes.byref(n_dec), ctypes.byref(consumed))
+        return records, arena, st, n_dec.value, consumed.value
+
+
+BinarySerializer = BatchSerializer(PROTOCOL_BINARY)
+CompactSerializer = BatchSerializer(PROTOCOL_COMPACT)

@@ -1,0 +1,280 @@
+/*
+ * thrift_gpu.h — C-ABI boundary of the MI355X bulk Thrift record codec.
+ *
+ * This is the drop-in boundary for fbthrift's bulk serialization path: whole
+ * batches of same-schema records cross it into gfx950 HIP kernels. Every entry
+ * point is plain C (pointers + sizes, no C++/torch types), so it can be bound
+ * from C++ (include/thrift_gpu/GpuBatchSerializer.h), ctypes, cgo or JNI.
+ *
+ * What each entry point replaces in the reference (fbthrift, paths relative to
+ * the fbthrift source tree):
+ *
+ *  tgpu_schema_create
+ *      the codegen'd per-type metadata that drives T::readNoXfer / T::write
+ *      (thrift/compiler/generate/templates/cpp2/module_types_custom_protocol_h/
+ *       deserialize_struct.whisker:19-160, serialize_struct.whisker:40-67) and
+ *      its runtime-table twin StructInfo/FieldInfo/TypeInfo
+ *      (thrift/lib/cpp2/protocol/TableBasedSerializer.h:90-118,205-302).
+ *  tgpu_encode_batch
+ *      N x Serializer<R,W>::serialize(obj, &queue) appending to one IOBufQueue
+ *      (thrift/lib/cpp2/protocol/Serializer.h:136-148) i.e. N x T::write<P>.
+ *  tgpu_decode_batch
+ *      N x Serializer<R,W>::deserialize<T>(Cursor&) over a concatenated record
+ *      stream (Serializer.h:97-100, :192-204), i.e. N x T::readNoXfer<P>.
+ *  tgpu_status
+ *      the exceptions the reference throws: TProtocolException{type}
+ *      (thrift/lib/cpp/protocol/TProtocolException.h:41-51) and
+ *      std::out_of_range (folly cursor underflow; invalid varint,
+ *      thrift/lib/cpp/util/VarintUtils.cpp:125-127). A C-ABI cannot throw, so
+ *      the first failing record, its byte offset and exception class are
+ *      latched (the transcode C-ABI precedent:
+ *      thrift/lib/cpp2/transcode/TranscodeErrc.h:32-44).
+ *  tgpu_limits
+ *      gflags thrift_cpp2_protocol_reader_string_limit / _container_limit
+ *      (thrift/lib/cpp2/protocol/BinaryProtocol.cpp:23-30) and
+ *      thrift_protocol_max_depth (thrift/lib/cpp2/protocol/Protocol.cpp:21-24).
+ *
+ * Memory: every data pointer passed to encode/decode is a DEVICE pointer
+ * (hipMalloc'd HBM) unless stated otherwise; `stream` is a hipStream_t passed
+ * as void* (NULL = the default stream). Calls are asynchronous with respect to
+ * the host unless a host `tgpu_status*` is passed, in which case the call waits
+ * for the stream and fills it (the synchronous, exception-equivalent form).
+ *
+ * Record layout (the "codegen'd struct layout", device form): members in IDL
+ * declaration order at natural alignment, then one isset byte per field
+ * (thrift/lib/cpp2/detail/Isset.h:243-296), size rounded up to the alignment.
+ * Device-unfriendly members use 16-byte spans instead of std::string /
+ * std::vector: see tgpu_span. tgpu_layout_compute() fills offsets by that rule.
+ */
+#ifndef THRIFT_GPU_H_
+#define THRIFT_GPU_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TGPU_ABI_VERSION 1
+
+/* Protocol ids: thrift/lib/cpp/protocol/TProtocolTypes.h:24-27. */
+enum tgpu_protocol {
+  TGPU_PROTOCOL_BINARY = 0,
+  TGPU_PROTOCOL_COMPACT = 2,
+};
+
+/* Wire types: thrift/lib/cpp/protocol/TType.h:31-51 (same numeric values). */
+enum tgpu_ttype {
+  TGPU_T_STOP = 0,
+  TGPU_T_VOID = 1,
+  TGPU_T_BOOL = 2,
+  TGPU_T_BYTE = 3,
+  TGPU_T_DOUBLE = 4,
+  TGPU_T_I16 = 6,
+  TGPU_T_I32 = 8,
+  TGPU_T_U64 = 9,
+  TGPU_T_I64 = 10,
+  TGPU_T_STRING = 11,
+  TGPU_T_STRUCT = 12,
+  TGPU_T_MAP = 13,
+  TGPU_T_SET = 14,
+  TGPU_T_LIST = 15,
+  TGPU_T_UTF8 = 16,
+  TGPU_T_UTF16 = 17,
+  TGPU_T_STREAM = 18,
+  TGPU_T_FLOAT = 19,
+};
+
+/* Field qualifiers (module_types_custom_protocol.whisker:79-94). */
+enum tgpu_qualifier {
+  TGPU_UNQUALIFIED = 0, /* always written, isset set on read */
+  TGPU_OPTIONAL = 1,    /* written only when isset != 0 */
+};
+
+/*
+ * One field of a struct, in IDL declaration order (= serialization order,
+ * thrift/compiler/generate/t_whisker_generator.cc:231-236).
+ *   ttype        T_BOOL..T_FLOAT scalar, T_STRING (binary/string), T_STRUCT,
+ *                T_LIST or T_SET of a scalar element type.
+ *   elem_ttype   element type for T_LIST/T_SET (scalar), else 0.
+ *   struct_index nested struct (index into the schema's struct table) for
+ *                T_STRUCT, else -1.
+ */
+typedef struct tgpu_field_desc {
+  int16_t id;
+  uint8_t ttype;
+  uint8_t elem_ttype;
+  uint8_t qualifier;
+  uint8_t reserved0[3];
+  uint32_t member_offset;
+  uint32_t isset_offset;
+  int32_t struct_index;
+  uint32_t reserved1;
+} tgpu_field_desc; /* 24 bytes */
+
+/* A struct = a contiguous run of fields. Struct 0 is the record (root) type. */
+typedef struct tgpu_struct_desc {
+  uint32_t first_field;
+  uint32_t num_fields;
+  uint32_t size;  /* sizeof(record), multiple of align */
+  uint32_t align;
+} tgpu_struct_desc;
+
+/*
+ * Device form of a string/binary or list/set member (16 bytes, align 8).
+ * Decode: a string's `offset` is relative to the decoded input stream `in`
+ *         (zero-copy view, ExternalBufferSharing::SHARE_EXTERNAL_BUFFER,
+ *         thrift/lib/cpp2/protocol/Protocol.h:96-99); a list's `offset` is
+ *         relative to `list_arena` where its elements were written in native
+ *         little-endian layout. Empty strings/lists decode to {0, 0}.
+ * Encode: a string's `offset` is relative to `string_base`, a list's to
+ *         `list_base`; `length` is bytes (string) or elements (list).
+ */
+typedef struct tgpu_span {
+  uint64_t offset;
+  uint32_t length;
+  uint32_t reserved;
+} tgpu_span;
+
+/* Reader limits. 0 = unlimited for string/container (reference defaults).
+ * max_depth is FLAGS_thrift_protocol_max_depth (skip recursion limit,
+ * Protocol.h:202-205); height is ProtocolBase::setHeight (container/struct
+ * nesting counter, Protocol.h:59-78), 0 = max_depth as in the reference. */
+typedef struct tgpu_limits {
+  int32_t string_limit;
+  int32_t container_limit;
+  int32_t max_depth; /* default 12000 */
+  int32_t height;    /* default 0 (= max_depth) */
+} tgpu_limits;
+
+/* Result codes. */
+enum tgpu_code {
+  TGPU_OK = 0,
+  /* std::out_of_range */
+  TGPU_ERR_UNDERFLOW = 1,        /* cursor ran out of bytes (folly readBE) */
+  TGPU_ERR_INVALID_VARINT = 2,   /* "invalid varint read" */
+  /* TProtocolException */
+  TGPU_ERR_BOOL_VALUE = 3,       /* INVALID_DATA: Binary bool byte >= 2 */
+  TGPU_ERR_INVALID_SKIP_TYPE = 4,/* INVALID_DATA */
+  TGPU_ERR_TRUNCATED = 5,        /* INVALID_DATA: throwTruncatedData */
+  TGPU_ERR_NEGATIVE_SIZE = 6,    /* NEGATIVE_SIZE */
+  TGPU_ERR_SIZE_LIMIT = 7,       /* SIZE_LIMIT */
+  TGPU_ERR_DEPTH_LIMIT = 8,      /* DEPTH_LIMIT */
+  TGPU_ERR_BAD_TYPE = 9,         /* UNKNOWN: Compact "don't know what type" */
+  /* writer-side: the reference aborts the process (validate_bool,
+     thrift/lib/cpp2/protocol/Protocol.h:126-163) or throws SIZE_LIMIT */
+  TGPU_ERR_INVALID_BOOL_WRITE = 10,
+  TGPU_ERR_WRITE_SIZE_LIMIT = 11,
+  /* boundary / runtime errors (no reference counterpart) */
+  TGPU_ERR_INDEX_MISMATCH = 20,  /* record length disagrees with offsets[] */
+  TGPU_ERR_OUTPUT_OVERFLOW = 21, /* encode output / list arena too small */
+  TGPU_ERR_UNSUPPORTED = 22,     /* schema feature not supported on device */
+  TGPU_ERR_INVALID_ARGUMENT = 23,
+  TGPU_ERR_HIP = 24,
+};
+
+enum tgpu_exc_class {
+  TGPU_EXC_NONE = 0,
+  TGPU_EXC_OUT_OF_RANGE = 1,  /* std::out_of_range */
+  TGPU_EXC_PROTOCOL = 2,      /* apache::thrift::protocol::TProtocolException */
+  TGPU_EXC_ABORT = 3,         /* reference would LOG(FATAL) */
+  TGPU_EXC_RUNTIME = 4,       /* tgpu usage / HIP error */
+};
+
+typedef struct tgpu_status {
+  int32_t code;         /* enum tgpu_code */
+  int32_t exc_class;    /* enum tgpu_exc_class */
+  int32_t tproto_type;  /* TProtocolExceptionType when exc_class == PROTOCOL */
+  int32_t reserved;
+  uint64_t record;      /* index of the first failing record */
+  uint64_t byte_offset; /* stream offset of the read/write that failed */
+} tgpu_status;
+
+typedef struct tgpu_schema tgpu_schema;   /* opaque; lives on one device */
+typedef struct tgpu_context tgpu_context; /* opaque; workspace + result slot */
+
+/* ---- library ---------------------------------------------------------- */
+int tgpu_abi_version(void);
+const char* tgpu_code_name(int code);
+/* Maps a code to (exc_class, tproto_type). */
+void tgpu_code_classify(int code, int32_t* exc_class, int32_t* tproto_type);
+
+/* ---- schema ----------------------------------------------------------- */
+/* Fills member_offset / isset_offset of every field and size/align of every
+ * struct by the declaration-order layout rule. Host-only, no device work. */
+int tgpu_layout_compute(tgpu_struct_desc* structs, uint32_t n_structs,
+                        tgpu_field_desc* fields, uint32_t n_fields);
+/* Validates and uploads a schema to the current HIP device. */
+int tgpu_schema_create(const tgpu_struct_desc* structs, uint32_t n_structs,
+                       const tgpu_field_desc* fields, uint32_t n_fields,
+                       tgpu_schema** out);
+void tgpu_schema_destroy(tgpu_schema* schema);
+/* sizeof(record) of the root struct. */
+uint32_t tgpu_schema_record_size(const tgpu_schema* schema);
+/* Canonical wire length of every record if it is fixed for `protocol`
+ * (Binary with only fixed-width fields), else 0. */
+uint64_t tgpu_schema_fixed_wire_size(const tgpu_schema* schema, int protocol);
+
+/* ---- context ---------------------------------------------------------- */
+int tgpu_context_create(tgpu_context** out);
+void tgpu_context_destroy(tgpu_context* ctx);
+/* Pre-sizes the workspace for batches of up to n_records (so later calls do
+ * no allocation and can be captured into a hipGraph). */
+int tgpu_context_reserve(tgpu_context* ctx, uint64_t n_records);
+/* Waits for `stream` and reports the last call's result on this context. */
+int tgpu_context_wait(tgpu_context* ctx, void* stream, tgpu_status* st,
+                      uint64_t* n_done, uint64_t* bytes);
+
+/* ---- batch encode ----------------------------------------------------- */
+/*
+ * Serializes records[0..n) (stride = tgpu_schema_record_size) back to back
+ * into `out` (capacity out_capacity bytes). out_offsets (device, n+1 entries,
+ * may be NULL) receives each record's start offset and the total size.
+ * string_base / list_base are the bases the records' spans point into.
+ * If st != NULL the call waits and fills st and *out_size.
+ */
+int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema,
+                      int protocol, const void* records, uint64_t n_records,
+                      const void* string_base, const void* list_base,
+                      void* out, uint64_t out_capacity, uint64_t* out_offsets,
+                      void* stream, tgpu_status* st, uint64_t* out_size);
+
+/*
+ * Exact wire size of each record (out_offsets, device, n+1 entries, required)
+ * and of the whole batch, without writing it: the bulk form of
+ * T::serializedSize<P> (serialize_struct.whisker:17-26; the reference returns
+ * an upper bound with varints counted at their maximum width, this is exact).
+ * Validates like encode (bool bytes, string/list sizes).
+ */
+int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                      const void* records, uint64_t n_records,
+                      uint64_t* out_offsets, void* stream, tgpu_status* st,
+                      uint64_t* total);
+
+/* ---- batch decode ----------------------------------------------------- */
+/*
+ * Deserializes n_records records from the concatenated stream in[0..in_len).
+ * offsets (device, n_records+1 entries) may be given as a record index; NULL
+ * means records are read back to back from offset 0 like repeated
+ * deserialize<T>(Cursor&). Records are default-initialized (zero, isset 0)
+ * before reading. List elements are written to list_arena (capacity
+ * list_arena_capacity bytes; required size: in_len for Binary,
+ * 8 * in_len for Compact, 0 when the schema has no lists).
+ * limits may be NULL (reference defaults).
+ * If st != NULL the call waits and fills st, *n_decoded (records fully
+ * decoded before the first failure) and *consumed (bytes consumed by them).
+ */
+int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema,
+                      int protocol, const void* in, uint64_t in_len,
+                      const uint64_t* offsets, uint64_t n_records,
+                      void* records, void* list_arena,
+                      uint64_t list_arena_capacity, const tgpu_limits* limits,
+                      void* stream, tgpu_status* st, uint64_t* n_decoded,
+                      uint64_t* consumed);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* THRIFT_GPU_H_ */

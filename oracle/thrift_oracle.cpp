@@ -1,0 +1,1112 @@
+/*
+ * thrift_oracle.cpp — TEST INFRASTRUCTURE ONLY. See thrift_oracle.h.
+ *
+ * CPU restatement of the reference's bulk-record semantics. Each reader/writer
+ * method cites the fbthrift source it follows (paths relative to the fbthrift
+ * tree; the reference checkout is not needed to build or run this file).
+ */
+#include "thrift_oracle.h"
+
+#include <algorithm>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+namespace {
+
+// ---------------------------------------------------------------- errors ----
+struct OErr {
+  int code;
+  uint64_t off;
+};
+
+[[noreturn]] inline void fail(int code, uint64_t off) { throw OErr{code, off}; }
+
+void classify(int code, int32_t* exc, int32_t* tp) {
+  // TProtocolException.h:41-51 types; std::out_of_range for cursor/varint.
+  int32_t e = TGPU_EXC_RUNTIME, t = 0;
+  switch (code) {
+    case TGPU_OK: e = TGPU_EXC_NONE; break;
+    case TGPU_ERR_UNDERFLOW:
+    case TGPU_ERR_INVALID_VARINT: e = TGPU_EXC_OUT_OF_RANGE; break;
+    case TGPU_ERR_BOOL_VALUE:
+    case TGPU_ERR_INVALID_SKIP_TYPE:
+    case TGPU_ERR_TRUNCATED: e = TGPU_EXC_PROTOCOL; t = 1; break;  // INVALID_DATA
+    case TGPU_ERR_NEGATIVE_SIZE: e = TGPU_EXC_PROTOCOL; t = 2; break;
+    case TGPU_ERR_SIZE_LIMIT:
+    case TGPU_ERR_WRITE_SIZE_LIMIT: e = TGPU_EXC_PROTOCOL; t = 3; break;
+    case TGPU_ERR_DEPTH_LIMIT: e = TGPU_EXC_PROTOCOL; t = 8; break;
+    case TGPU_ERR_BAD_TYPE: e = TGPU_EXC_PROTOCOL; t = 0; break;  // UNKNOWN
+    case TGPU_ERR_INVALID_BOOL_WRITE: e = TGPU_EXC_ABORT; break;
+    default: break;
+  }
+  if (exc) *exc = e;
+  if (tp) *tp = t;
+}
+
+void set_status(tgpu_status* st, int code, uint64_t rec, uint64_t off) {
+  if (!st) return;
+  std::memset(st, 0, sizeof(*st));
+  st->code = code;
+  classify(code, &st->exc_class, &st->tproto_type);
+  st->record = rec;
+  st->byte_offset = off;
+}
+
+// ---------------------------------------------------------------- cursor ----
+// folly::io::Cursor over one contiguous buffer: every read is bounds checked
+// and underflow raises std::out_of_range (BinaryProtocol-inl.h:503-533 use
+// in_.read / in_.readBE).
+struct Cursor {
+  const uint8_t* p;
+  uint64_t pos, end;
+  uint64_t avail() const { return end - pos; }
+  bool canAdvance(uint64_t n) const { return avail() >= n; }
+  uint8_t read8() {
+    if (pos >= end) fail(TGPU_ERR_UNDERFLOW, pos);
+    return p[pos++];
+  }
+  template <class T>
+  T readBE() {
+    if (avail() < sizeof(T)) fail(TGPU_ERR_UNDERFLOW, pos);
+    uint64_t v = 0;
+    for (size_t i = 0; i < sizeof(T); ++i) v = (v << 8) | p[pos + i];
+    pos += sizeof(T);
+    return (T)v;
+  }
+  void skip(uint64_t n) {
+    if (avail() < n) fail(TGPU_ERR_UNDERFLOW, pos);
+    pos += n;
+  }
+};
+
+// -------------------------------------------------------------- varints ----
+// VarintUtils-inl.h:85-87 kVarintMaxBytes = ceil(bits/7); :94-107 readVarintSlow
+// and :109-134 the unrolled x86 decoder: stop at the first byte without 0x80,
+// more continuation bytes than max -> std::out_of_range("invalid varint read")
+// (VarintUtils.cpp:125-127); bits beyond the type width are dropped; overlong
+// zeros are accepted. Underflow in the middle of a varint -> out_of_range too.
+template <int BITS>
+uint64_t readVarint(Cursor& c) {
+  constexpr int kMax = (BITS + 6) / 7;
+  const uint64_t start = c.pos;
+  uint64_t result = 0;
+  for (int i = 0; i < kMax; ++i) {
+    if (c.pos >= c.end) fail(TGPU_ERR_UNDERFLOW, c.pos);
+    const uint64_t b = c.p[c.pos++];
+    result |= (b & 0x7f) << (7 * i);
+    if (!(b & 0x80)) {
+      if constexpr (BITS < 64) result &= (1ull << BITS) - 1;  // cast to T
+      return result;
+    }
+  }
+  fail(TGPU_ERR_INVALID_VARINT, start);
+}
+
+// VarintUtils-inl.h:72-83 zigzag.
+inline int32_t zigzagToI32(uint32_t n) { return (n & 1) ? (int32_t)~(n >> 1) : (int32_t)(n >> 1); }
+inline int64_t zigzagToI64(uint64_t n) { return (n & 1) ? (int64_t)~(n >> 1) : (int64_t)(n >> 1); }
+inline uint32_t i32ToZigzag(int32_t n) { return ((uint32_t)n << 1) ^ (uint32_t)(n >> 31); }
+inline uint64_t i64ToZigzag(int64_t n) { return ((uint64_t)n << 1) ^ (uint64_t)(n >> 63); }
+
+// ------------------------------------------------------------- schema view --
+struct Schema {
+  const tgpu_struct_desc* s;
+  uint32_t ns;
+  const tgpu_field_desc* f;
+  uint32_t nf;
+};
+
+bool is_scalar(uint8_t t) {
+  switch (t) {
+    case TGPU_T_BOOL: case TGPU_T_BYTE: case TGPU_T_I16: case TGPU_T_I32:
+    case TGPU_T_I64: case TGPU_T_DOUBLE: case TGPU_T_FLOAT:
+      return true;
+    default:
+      return false;
+  }
+}
+uint32_t scalar_size(uint8_t t) {
+  switch (t) {
+    case TGPU_T_BOOL: case TGPU_T_BYTE: return 1;
+    case TGPU_T_I16: return 2;
+    case TGPU_T_I32: case TGPU_T_FLOAT: return 4;
+    default: return 8;
+  }
+}
+
+// ================================================================ readers ===
+struct Limits {
+  int32_t string_limit = 0, container_limit = 0, max_depth = 12000, height = 0;
+  int64_t initial_height() const { return (int64_t)(height ? height : max_depth) + 1; }
+};
+
+// ProtocolBase::descend/ascend (Protocol.h:59-78, height = max_depth + 1).
+struct Height {
+  int64_t h;
+  void descend(uint64_t off) {
+    if (!--h) fail(TGPU_ERR_DEPTH_LIMIT, off);
+  }
+  void ascend() { ++h; }
+};
+
+// ---- Binary (BinaryProtocol-inl.h:384-661, BinaryProtocol.cpp:140-225) ----
+struct BinaryReader {
+  Cursor c;
+  Limits lim;
+  Height height;
+
+  void checkStringSize(int32_t size, uint64_t off) {  // -inl.h:535-543
+    if (size < 0) fail(TGPU_ERR_NEGATIVE_SIZE, off);
+    if (lim.string_limit > 0 && size > lim.string_limit) fail(TGPU_ERR_SIZE_LIMIT, off);
+  }
+  void checkContainerSize(int32_t size, uint64_t off) {  // -inl.h:545-551
+    if (size < 0) fail(TGPU_ERR_NEGATIVE_SIZE, off);
+    if (lim.container_limit && size > lim.container_limit) fail(TGPU_ERR_SIZE_LIMIT, off);
+  }
+  // readFieldBeginWithState (-inl.h:623-632): type byte, STOP has no id.
+  // advanceToNextField's 3-byte fast path (:586-621) yields the same result.
+  bool readFieldHeader(int16_t /*prev*/, uint8_t& type, int16_t& id) {
+    type = c.read8();
+    if (type == TGPU_T_STOP) return false;
+    id = c.readBE<int16_t>();
+    return true;
+  }
+  bool readBool() {  // -inl.h:489-495
+    const uint64_t off = c.pos;
+    const uint8_t b = c.read8();
+    if (b >= 2) fail(TGPU_ERR_BOOL_VALUE, off);
+    return b != 0;
+  }
+  void readListBegin(uint8_t& elem, int32_t& size) {  // -inl.h:457-467
+    const uint64_t off = c.pos;
+    height.descend(off);
+    elem = c.read8();
+    const uint64_t soff = c.pos;
+    size = c.readBE<int32_t>();
+    checkContainerSize(size, soff);
+  }
+  void readMapBegin(uint8_t& k, uint8_t& v, int32_t& size) {  // -inl.h:439-451
+    height.descend(c.pos);
+    k = c.read8();
+    v = c.read8();
+    const uint64_t soff = c.pos;
+    size = c.readBE<int32_t>();
+    checkContainerSize(size, soff);
+  }
+  // readString -> readStringBody -> checkStringSize + detail::readStringBody
+  // (Protocol.h:435-449: canAdvance before allocation -> throwTruncatedData).
+  void readString(uint64_t& view, uint32_t& len) {
+    const uint64_t off = c.pos;
+    const int32_t size = c.readBE<int32_t>();
+    checkStringSize(size, off);
+    if (!c.canAdvance((uint64_t)size)) fail(TGPU_ERR_TRUNCATED, c.pos);
+    view = c.pos;
+    len = (uint32_t)size;
+    c.pos += (uint64_t)size;
+  }
+  static uint32_t fixedSizeInContainer(uint8_t t) {  // -inl.h:634-661
+    switch (t) {
+      case TGPU_T_BOOL: case TGPU_T_BYTE: return 1;
+      case TGPU_T_I16: return 2;
+      case TGPU_T_I32: case TGPU_T_FLOAT: return 4;
+      case TGPU_T_I64: case TGPU_T_DOUBLE: return 8;
+      default: return 0;
+    }
+  }
+  // Protocol.h:297-344 skip_n.
+  void skip_n(uint32_t n, const uint8_t* types, int nt, int depth) {
+    if (depth >= lim.max_depth) fail(TGPU_ERR_DEPTH_LIMIT, c.pos);
+    uint64_t sum = 0;
+    bool allFixed = true;
+    for (int i = 0; i < nt; ++i) {
+      const uint32_t s = fixedSizeInContainer(types[i]);
+      sum += s;
+      allFixed = allFixed && s;
+    }
+    if (allFixed) {
+      c.skip(sum * n);
+      return;
+    }
+    for (uint32_t i = 0; i < n; ++i)
+      for (int j = 0; j < nt; ++j) skip(types[j], depth + 1);
+  }
+  // BinaryProtocolReader::skip (BinaryProtocol.cpp:140-225).
+  void skip(uint8_t type, int depth) {
+    if (depth >= lim.max_depth) fail(TGPU_ERR_DEPTH_LIMIT, c.pos);
+    uint64_t bytes = 0;
+    switch (type) {
+      case TGPU_T_BYTE: case TGPU_T_BOOL: bytes = 1; break;
+      case TGPU_T_I16: bytes = 2; break;
+      case TGPU_T_FLOAT: case TGPU_T_I32: bytes = 4; break;
+      case TGPU_T_DOUBLE: case TGPU_T_U64: case TGPU_T_I64: bytes = 8; break;
+      case TGPU_T_UTF8: case TGPU_T_UTF16: case TGPU_T_STRING: {
+        // canAdvance(size) is checked from the cursor copy taken BEFORE the
+        // length was read, with size cast through int32 -> size_t.
+        const uint64_t before = c.pos;
+        const int32_t size = c.readBE<int32_t>();
+        const uint64_t want = (uint64_t)(int64_t)size;  // negative -> huge
+        if (c.end - before < want) fail(TGPU_ERR_TRUNCATED, c.pos);
+        bytes = (uint64_t)(uint32_t)size;
+        break;
+      }
+      case TGPU_T_STRUCT: {
+        height.descend(c.pos);  // readStructBegin
+        while (true) {
+          const uint8_t ft = c.read8();
+          if (ft == TGPU_T_STOP) {
+            height.ascend();
+            return;
+          }
+          c.skip(2);
+          skip(ft, depth + 1);
+        }
+      }
+      case TGPU_T_MAP: {
+        uint8_t kv[2];
+        int32_t size;
+        readMapBegin(kv[0], kv[1], size);
+        skip_n((uint32_t)size, kv, 2, depth + 1);
+        height.ascend();
+        return;
+      }
+      case TGPU_T_SET:
+      case TGPU_T_LIST: {
+        uint8_t e;
+        int32_t size;
+        readListBegin(e, size);
+        skip_n((uint32_t)size, &e, 1, depth + 1);
+        height.ascend();
+        return;
+      }
+      default:
+        fail(TGPU_ERR_INVALID_SKIP_TYPE, c.pos);
+    }
+    c.skip(bytes);
+  }
+  // Scalar value reads (-inl.h:503-533).
+  void readScalar(uint8_t t, uint8_t* dst) {
+    switch (t) {
+      case TGPU_T_BOOL: *dst = readBool() ? 1 : 0; break;
+      case TGPU_T_BYTE: *dst = c.read8(); break;
+      case TGPU_T_I16: { int16_t v = c.readBE<int16_t>(); std::memcpy(dst, &v, 2); break; }
+      case TGPU_T_I32:
+      case TGPU_T_FLOAT: { int32_t v = c.readBE<int32_t>(); std::memcpy(dst, &v, 4); break; }
+      default: { int64_t v = c.readBE<int64_t>(); std::memcpy(dst, &v, 8); break; }
+    }
+  }
+  uint8_t listElemWire(uint8_t elem) const { return elem; }
+  static constexpr uint64_t kArenaScale = 1;
+};
+
+// ---- Compact (CompactProtocol-inl.h:531-938, CompactProtocol.cpp:48-54) ----
+// CTypeToTType (-inl.h:70-85); index >= 14 -> throwBadType.
+const uint8_t kCTypeToTType[14] = {
+    TGPU_T_STOP, TGPU_T_BOOL, TGPU_T_BOOL, TGPU_T_BYTE, TGPU_T_I16,
+    TGPU_T_I32, TGPU_T_I64, TGPU_T_DOUBLE, TGPU_T_STRING, TGPU_T_LIST,
+    TGPU_T_SET, TGPU_T_MAP, TGPU_T_STRUCT, TGPU_T_FLOAT};
+// TTypeToCType (-inl.h:48-69).
+uint8_t ttypeToCType(uint8_t t) {
+  switch (t) {
+    case TGPU_T_STOP: return 0;
+    case TGPU_T_BOOL: return 1;
+    case TGPU_T_BYTE: return 3;
+    case TGPU_T_DOUBLE: return 7;
+    case TGPU_T_I16: return 4;
+    case TGPU_T_I32: return 5;
+    case TGPU_T_I64: return 6;
+    case TGPU_T_STRING: return 8;
+    case TGPU_T_STRUCT: return 12;
+    case TGPU_T_MAP: return 11;
+    case TGPU_T_SET: return 10;
+    case TGPU_T_LIST: return 9;
+    case TGPU_T_FLOAT: return 13;
+    default: return 0;
+  }
+}
+
+struct CompactReader {
+  Cursor c;
+  Limits lim;
+  Height height;
+  bool hasBool = false, boolVal = false;  // boolValue_ latch
+
+  uint8_t getType(uint8_t ct, uint64_t off) {  // -inl.h:783-791
+    if (ct >= 14) fail(TGPU_ERR_BAD_TYPE, off);
+    return kCTypeToTType[ct];
+  }
+  void checkStringSize(int32_t size, uint64_t off) {  // -inl.h:742-749
+    if (size < 0) fail(TGPU_ERR_NEGATIVE_SIZE, off);
+    if (lim.string_limit > 0 && size > lim.string_limit) fail(TGPU_ERR_SIZE_LIMIT, off);
+  }
+  // readFieldBeginWithStateImpl (-inl.h:884-910). Any byte with a zero low
+  // nibble ends the struct after consuming 1 byte (0x00 directly; 0xN0 via
+  // getType(0) == T_STOP).
+  bool readFieldHeader(int16_t prev, uint8_t& type, int16_t& id) {
+    const uint64_t off = c.pos;
+    const uint8_t b = c.read8();
+    if ((b & 0x0f) == 0) return false;
+    const int16_t modifier = (int16_t)(b >> 4);
+    if (modifier != 0) {
+      id = (int16_t)(prev + modifier);
+    } else {
+      id = (int16_t)zigzagToI32((uint32_t)readVarint<32>(c));  // readI16 via i32
+    }
+    const uint8_t ct = b & 0x0f;
+    type = getType(ct, off);
+    if (ct == 1 || ct == 2) {
+      hasBool = true;
+      boolVal = (ct == 1);
+    }
+    return true;
+  }
+  bool readBool() {  // -inl.h:692-701
+    if (hasBool) {
+      hasBool = false;
+      return boolVal;
+    }
+    return c.read8() == 1;
+  }
+  void readListBegin(uint8_t& elem, int32_t& size) {  // -inl.h:615-640
+    const uint64_t off = c.pos;
+    height.descend(off);
+    const uint8_t b = c.read8();
+    int32_t lsize = (b >> 4) & 0x0f;
+    if (lsize == 15) lsize = (int32_t)(uint32_t)readVarint<32>(c);
+    if (lsize < 0) fail(TGPU_ERR_NEGATIVE_SIZE, off);
+    if (lim.container_limit && lsize > lim.container_limit) fail(TGPU_ERR_SIZE_LIMIT, off);
+    elem = getType(b & 0x0f, off);
+    size = lsize;
+  }
+  void readMapBegin(uint8_t& k, uint8_t& v, int32_t& size) {  // -inl.h:578-610
+    const uint64_t off = c.pos;
+    height.descend(off);
+    uint8_t kv = 0;
+    const int32_t msize = (int32_t)(uint32_t)readVarint<32>(c);
+    if (msize != 0) kv = c.read8();
+    if (msize < 0) fail(TGPU_ERR_NEGATIVE_SIZE, off);
+    if (lim.container_limit && msize > lim.container_limit) fail(TGPU_ERR_SIZE_LIMIT, off);
+    k = getType(kv >> 4, off);
+    v = getType(kv & 0xf, off);
+    size = msize;
+  }
+  void readString(uint64_t& view, uint32_t& len) {  // -inl.h:751-781
+    const uint64_t off = c.pos;
+    const int32_t size = (int32_t)(uint32_t)readVarint<32>(c);
+    checkStringSize(size, off);
+    if (size == 0) {
+      view = 0;
+      len = 0;
+      return;
+    }
+    if (!c.canAdvance((uint64_t)size)) fail(TGPU_ERR_TRUNCATED, c.pos);
+    view = c.pos;
+    len = (uint32_t)size;
+    c.pos += (uint64_t)size;
+  }
+  static uint32_t fixedSizeInContainer(uint8_t t) {  // -inl.h:912-938
+    switch (t) {
+      case TGPU_T_BOOL: case TGPU_T_BYTE: return 1;
+      case TGPU_T_FLOAT: return 4;
+      case TGPU_T_DOUBLE: return 8;
+      default: return 0;
+    }
+  }
+  void skip_n(uint32_t n, const uint8_t* types, int nt, int depth) {  // Protocol.h:317-344
+    if (depth >= lim.max_depth) fail(TGPU_ERR_DEPTH_LIMIT, c.pos);
+    uint64_t sum = 0;
+    bool allFixed = true;
+    for (int i = 0; i < nt; ++i) {
+      const uint32_t s = fixedSizeInContainer(types[i]);
+      sum += s;
+      allFixed = allFixed && s;
+    }
+    if (allFixed) {
+      c.skip(sum * n);
+      return;
+    }
+    for (uint32_t i = 0; i < n; ++i)
+      for (int j = 0; j < nt; ++j) skip(types[j], depth + 1);
+  }
+  // apache::thrift::skip (Protocol.h:187-283) instantiated for Compact.
+  void skip(uint8_t type, int depth) {
+    if (depth >= lim.max_depth) fail(TGPU_ERR_DEPTH_LIMIT, c.pos);
+    switch (type) {
+      case TGPU_T_BOOL: readBool(); return;
+      case TGPU_T_BYTE: c.read8(); return;
+      case TGPU_T_I16:
+      case TGPU_T_I32: readVarint<32>(c); return;
+      case TGPU_T_U64:
+      case TGPU_T_I64: readVarint<64>(c); return;
+      case TGPU_T_DOUBLE: c.readBE<int64_t>(); return;
+      case TGPU_T_FLOAT: c.readBE<int32_t>(); return;
+      case TGPU_T_UTF8: case TGPU_T_UTF16: case TGPU_T_STRING: {
+        uint64_t v;
+        uint32_t l;
+        readString(v, l);
+        return;
+      }
+      case TGPU_T_STRUCT: {
+        height.descend(c.pos);  // readStructBegin: push lastFieldId_, = 0
+        int16_t last = 0;
+        while (true) {
+          uint8_t ft;
+          int16_t fid;
+          if (!readFieldHeader(last, ft, fid)) break;
+          last = fid;
+          skip(ft, depth + 1);
+        }
+        height.ascend();
+        return;
+      }
+      case TGPU_T_MAP: {
+        uint8_t kv[2];
+        int32_t size;
+        readMapBegin(kv[0], kv[1], size);
+        skip_n((uint32_t)size, kv, 2, depth + 1);
+        height.ascend();
+        return;
+      }
+      case TGPU_T_SET:
+      case TGPU_T_LIST: {
+        uint8_t e;
+        int32_t size;
+        readListBegin(e, size);
+        skip_n((uint32_t)size, &e, 1, depth + 1);
+        height.ascend();
+        return;
+      }
+      default:
+        fail(TGPU_ERR_INVALID_SKIP_TYPE, c.pos);
+    }
+  }
+  void readScalar(uint8_t t, uint8_t* dst) {  // -inl.h:703-740
+    switch (t) {
+      case TGPU_T_BOOL: *dst = readBool() ? 1 : 0; break;
+      case TGPU_T_BYTE: *dst = c.read8(); break;
+      case TGPU_T_I16: { int16_t v = (int16_t)zigzagToI32((uint32_t)readVarint<32>(c)); std::memcpy(dst, &v, 2); break; }
+      case TGPU_T_I32: { int32_t v = zigzagToI32((uint32_t)readVarint<32>(c)); std::memcpy(dst, &v, 4); break; }
+      case TGPU_T_I64: { int64_t v = zigzagToI64(readVarint<64>(c)); std::memcpy(dst, &v, 8); break; }
+      case TGPU_T_FLOAT: { int32_t v = c.readBE<int32_t>(); std::memcpy(dst, &v, 4); break; }
+      default: { int64_t v = c.readBE<int64_t>(); std::memcpy(dst, &v, 8); break; }  // double
+    }
+  }
+  static constexpr uint64_t kArenaScale = 8;
+};
+
+// ---- generated readNoXfer restated, table-driven (TableBasedSerializerImpl.h
+// :695-767 has the same contract; deserialize_struct.whisker:19-160) --------
+struct DecodeCtx {
+  const Schema* sc;
+  uint8_t* arena;
+  uint64_t arena_cap;
+};
+
+template <class R>
+void readList(R& r, const tgpu_field_desc& f, uint8_t* member, DecodeCtx& dc) {
+  // protocol_methods<list>::read (protocol_methods.h:389-467). The member is
+  // reset to empty first (deserialize_field.whisker:44-47).
+  tgpu_span span{0, 0, 0};
+  std::memcpy(member, &span, sizeof(span));
+  uint8_t reported;
+  int32_t n;
+  r.readListBegin(reported, n);
+  if (reported != f.elem_ttype) {
+    r.skip_n((uint32_t)n, &reported, 1, 0);
+  } else {
+    if (!r.c.canAdvance((uint64_t)(uint32_t)n)) fail(TGPU_ERR_TRUNCATED, r.c.pos);  // canReadNElements
+    const uint32_t es = scalar_size(f.elem_ttype);
+    const uint64_t aoff = R::kArenaScale * r.c.pos;
+    if (n > 0 && (aoff + (uint64_t)n * es > dc.arena_cap || !dc.arena))
+      fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
+    if (n > 0) {
+      span.offset = aoff;
+      span.length = (uint32_t)n;
+    }
+    for (int32_t i = 0; i < n; ++i) {
+      r.readScalar(f.elem_ttype, dc.arena + aoff + (uint64_t)i * es);
+      // the list object holds the elements read so far
+    }
+    std::memcpy(member, &span, sizeof(span));
+  }
+  r.height.ascend();  // readListEnd
+}
+
+template <class R>
+void readStruct(R& r, uint32_t si, uint8_t* obj, DecodeCtx& dc) {
+  const tgpu_struct_desc& sd = dc.sc->s[si];
+  int16_t prev = 0;
+  while (true) {
+    uint8_t wt;
+    int16_t id;
+    if (!r.readFieldHeader(prev, wt, id)) break;
+    prev = id;
+    const tgpu_field_desc* f = nullptr;
+    for (uint32_t k = 0; k < sd.num_fields; ++k) {
+      const tgpu_field_desc& c = dc.sc->f[sd.first_field + k];
+      if (c.id == id) {
+        f = &c;
+        break;
+      }
+    }
+    // isCompatibleWithType: fieldType == expected (BinaryProtocol.h:353-356,
+    // CompactProtocol.h:433-437); else skip (deserialize_struct.whisker:140-157).
+    if (!f || f->ttype != wt) {
+      r.skip(wt, 0);
+      continue;
+    }
+    uint8_t* m = obj + f->member_offset;
+    if (is_scalar(f->ttype)) {
+      r.readScalar(f->ttype, m);
+    } else if (f->ttype == TGPU_T_STRING) {
+      tgpu_span sp{0, 0, 0};
+      r.readString(sp.offset, sp.length);
+      if (sp.length == 0) sp.offset = 0;
+      std::memcpy(m, &sp, sizeof(sp));
+    } else if (f->ttype == TGPU_T_STRUCT) {
+      readStruct(r, (uint32_t)f->struct_index, m, dc);  // merges into member
+    } else if (f->ttype == TGPU_T_LIST || f->ttype == TGPU_T_SET) {
+      readList(r, *f, m, dc);
+    }
+    obj[f->isset_offset] = 1;  // __isset.set(idx, true)
+  }
+}
+
+void init_record(const Schema& sc, uint8_t* rec) {
+  std::memset(rec, 0, sc.s[0].size);  // default-constructed T (zero defaults)
+}
+
+template <class R>
+int decode_impl(const Schema& sc, const uint8_t* in, uint64_t in_len,
+                const uint64_t* offsets, uint64_t n, uint8_t* recs,
+                uint8_t* arena, uint64_t arena_cap, const Limits& lim,
+                tgpu_status* st, uint64_t* n_dec, uint64_t* consumed) {
+  DecodeCtx dc{&sc, arena, arena_cap};
+  uint64_t pos = offsets ? offsets[0] : 0;
+  const uint32_t rs = sc.s[0].size;
+  for (uint64_t i = 0; i < n; ++i) {
+    uint8_t* rec = recs + i * rs;
+    init_record(sc, rec);
+    const uint64_t start = offsets ? offsets[i] : pos;
+    R r;
+    r.c = Cursor{in, start, in_len};
+    r.lim = lim;
+    r.height.h = lim.initial_height();
+    try {
+      readStruct(r, 0, rec, dc);
+    } catch (const OErr& e) {
+      set_status(st, e.code, i, e.off);
+      if (n_dec) *n_dec = i;
+      if (consumed) *consumed = start - (offsets ? offsets[0] : 0);
+      return e.code;
+    }
+    if (offsets && r.c.pos != offsets[i + 1]) {
+      set_status(st, TGPU_ERR_INDEX_MISMATCH, i, r.c.pos);
+      if (n_dec) *n_dec = i;
+      if (consumed) *consumed = start - offsets[0];
+      return TGPU_ERR_INDEX_MISMATCH;
+    }
+    pos = r.c.pos;
+  }
+  set_status(st, TGPU_OK, n, 0);
+  if (n_dec) *n_dec = n;
+  if (consumed) *consumed = pos - (offsets ? offsets[0] : 0);
+  return TGPU_OK;
+}
+
+// ================================================================ writers ===
+struct Sink {
+  uint8_t* out;  // may be null (size only)
+  uint64_t pos, cap;
+  void put(uint8_t b) {
+    if (out) {
+      if (pos >= cap) fail(TGPU_ERR_OUTPUT_OVERFLOW, pos);
+      out[pos] = b;
+    }
+    ++pos;
+  }
+  void putBE(uint64_t v, int nbytes) {
+    for (int i = nbytes - 1; i >= 0; --i) put((uint8_t)(v >> (8 * i)));
+  }
+  void putBytes(const uint8_t* p, uint64_t n) {
+    if (out) {
+      if (pos + n > cap) fail(TGPU_ERR_OUTPUT_OVERFLOW, pos);
+      std::memcpy(out + pos, p, n);
+    }
+    pos += n;
+  }
+  // writeVarintSlow / writeVarintUnrolled (VarintUtils-inl.h:413-447); the
+  // BMI2 branch-free encoder (:545-595) produces the same bytes.
+  void varint(uint64_t v) {
+    while (v & ~0x7full) {
+      put((uint8_t)((v & 0x7f) | 0x80));
+      v >>= 7;
+    }
+    put((uint8_t)v);
+  }
+};
+
+struct EncodeCtx {
+  const Schema* sc;
+  const uint8_t* sbase;
+  const uint8_t* lbase;
+};
+
+uint8_t load_bool_checked(const uint8_t* p, uint64_t off) {
+  // validate_bool (Protocol.h:126-163): LOG(FATAL) on a byte not in {0,1}.
+  if (*p > 1) fail(TGPU_ERR_INVALID_BOOL_WRITE, off);
+  return *p;
+}
+
+template <class T>
+T ld(const uint8_t* p) {
+  T v;
+  std::memcpy(&v, p, sizeof(T));
+  return v;
+}
+
+// BinaryProtocolWriter (BinaryProtocol-inl.h:41-222) + generated write
+// (serialize_struct.whisker:40-67; gen/module_types_tcc.h:106-121).
+struct BinaryWriter {
+  Sink s;
+  void scalar(uint8_t t, const uint8_t* p) {
+    switch (t) {
+      case TGPU_T_BOOL: s.put(load_bool_checked(p, s.pos)); break;
+      case TGPU_T_BYTE: s.put(*p); break;
+      case TGPU_T_I16: s.putBE((uint16_t)ld<int16_t>(p), 2); break;
+      case TGPU_T_I32: case TGPU_T_FLOAT: s.putBE(ld<uint32_t>(p), 4); break;
+      default: s.putBE(ld<uint64_t>(p), 8); break;
+    }
+  }
+  void structure(const EncodeCtx& ec, uint32_t si, const uint8_t* obj) {
+    const tgpu_struct_desc& sd = ec.sc->s[si];
+    for (uint32_t k = 0; k < sd.num_fields; ++k) {
+      const tgpu_field_desc& f = ec.sc->f[sd.first_field + k];
+      if (f.qualifier == TGPU_OPTIONAL && !obj[f.isset_offset]) continue;
+      const uint8_t* m = obj + f.member_offset;
+      s.put(f.ttype);  // writeFieldBegin: byte type + BE i16 id
+      s.putBE((uint16_t)f.id, 2);
+      if (is_scalar(f.ttype)) {
+        scalar(f.ttype, m);
+      } else if (f.ttype == TGPU_T_STRING) {
+        const tgpu_span sp = ld<tgpu_span>(m);
+        if (sp.length > 0x7fffffffu) fail(TGPU_ERR_WRITE_SIZE_LIMIT, s.pos);  // checkBinarySize
+        s.putBE(sp.length, 4);
+        s.putBytes(ec.sbase + sp.offset, sp.length);
+      } else if (f.ttype == TGPU_T_STRUCT) {
+        structure(ec, (uint32_t)f.struct_index, m);
+      } else {  // list/set: writeListBegin + writeArithmeticVector (BinaryProtocol.cpp:95-117)
+        const tgpu_span sp = ld<tgpu_span>(m);
+        if (sp.length > 0x7fffffffu) fail(TGPU_ERR_WRITE_SIZE_LIMIT, s.pos);
+        s.put(f.elem_ttype);
+        s.putBE(sp.length, 4);
+        const uint32_t es = scalar_size(f.elem_ttype);
+        for (uint32_t i = 0; i < sp.length; ++i)
+          scalar(f.elem_ttype, ec.lbase + sp.offset + (uint64_t)i * es);
+      }
+    }
+    s.put(TGPU_T_STOP);  // writeFieldStop
+  }
+};
+
+// CompactProtocolWriter (CompactProtocol-inl.h:91-383).
+struct CompactWriter {
+  Sink s;
+  void fieldHeader(uint8_t ctype, int16_t id, int16_t& last) {  // :133-160
+    if (id > last && id - last <= 15) {
+      s.put((uint8_t)(((id - last) << 4) | ctype));
+    } else {
+      s.put(ctype);
+      s.varint(i32ToZigzag(id));  // writeI16 -> i32ToZigzag -> writeVarint
+    }
+    last = id;
+  }
+  void scalar(uint8_t t, const uint8_t* p) {
+    switch (t) {
+      case TGPU_T_BOOL: s.put(load_bool_checked(p, s.pos) ? 1 : 2); break;  // :252-273 (container form)
+      case TGPU_T_BYTE: s.put(*p); break;
+      case TGPU_T_I16: s.varint(i32ToZigzag(ld<int16_t>(p))); break;
+      case TGPU_T_I32: s.varint(i32ToZigzag(ld<int32_t>(p))); break;
+      case TGPU_T_I64: s.varint(i64ToZigzag(ld<int64_t>(p))); break;
+      case TGPU_T_FLOAT: s.putBE(ld<uint32_t>(p), 4); break;
+      default: s.putBE(ld<uint64_t>(p), 8); break;  // double, BE (v2)
+    }
+  }
+  void structure(const EncodeCtx& ec, uint32_t si, const uint8_t* obj) {
+    const tgpu_struct_desc& sd = ec.sc->s[si];
+    int16_t last = 0;  // writeStructBegin pushes lastFieldId_ and resets it
+    for (uint32_t k = 0; k < sd.num_fields; ++k) {
+      const tgpu_field_desc& f = ec.sc->f[sd.first_field + k];
+      if (f.qualifier == TGPU_OPTIONAL && !obj[f.isset_offset]) continue;
+      const uint8_t* m = obj + f.member_offset;
+      if (f.ttype == TGPU_T_BOOL) {  // bool value rides in the header
+        const uint8_t b = load_bool_checked(m, s.pos);
+        fieldHeader(b ? 1 : 2, f.id, last);
+        continue;
+      }
+      fieldHeader(ttypeToCType(f.ttype), f.id, last);
+      if (is_scalar(f.ttype)) {
+        scalar(f.ttype, m);
+      } else if (f.ttype == TGPU_T_STRING) {
+        const tgpu_span sp = ld<tgpu_span>(m);
+        if (sp.length > 0x7fffffffu) fail(TGPU_ERR_WRITE_SIZE_LIMIT, s.pos);
+        s.varint(sp.length);  // writeVarint(out_, (int32_t)size)
+        s.putBytes(ec.sbase + sp.offset, sp.length);
+      } else if (f.ttype == TGPU_T_STRUCT) {
+        structure(ec, (uint32_t)f.struct_index, m);
+      } else {  // writeCollectionBegin (:209-224)
+        const tgpu_span sp = ld<tgpu_span>(m);
+        if (sp.length > 0x7fffffffu) fail(TGPU_ERR_WRITE_SIZE_LIMIT, s.pos);
+        const uint8_t ct = ttypeToCType(f.elem_ttype);
+        if (sp.length <= 14) {
+          s.put((uint8_t)((sp.length << 4) | ct));
+        } else {
+          s.put((uint8_t)(0xf0 | ct));
+          s.varint(sp.length);
+        }
+        const uint32_t es = scalar_size(f.elem_ttype);
+        for (uint32_t i = 0; i < sp.length; ++i)
+          scalar(f.elem_ttype, ec.lbase + sp.offset + (uint64_t)i * es);
+      }
+    }
+    s.put(0);  // writeFieldStop
+  }
+};
+
+template <class W>
+int encode_impl(const Schema& sc, const uint8_t* recs, uint64_t n,
+                const uint8_t* sbase, const uint8_t* lbase, uint8_t* out,
+                uint64_t cap, uint64_t* offs, tgpu_status* st,
+                uint64_t* out_size) {
+  EncodeCtx ec{&sc, sbase, lbase};
+  W w;
+  w.s = Sink{out, 0, cap};
+  const uint32_t rs = sc.s[0].size;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (offs) offs[i] = w.s.pos;
+    const uint64_t start = w.s.pos;
+    try {
+      w.structure(ec, 0, recs + i * rs);
+    } catch (const OErr& e) {
+      set_status(st, e.code, i, e.off);
+      if (out_size) *out_size = start;
+      return e.code;
+    }
+  }
+  if (offs) offs[n] = w.s.pos;
+  set_status(st, TGPU_OK, n, 0);
+  if (out_size) *out_size = w.s.pos;
+  return TGPU_OK;
+}
+
+Limits to_limits(const tgpu_limits* l) {
+  Limits r;
+  if (l) {
+    r.string_limit = l->string_limit;
+    r.container_limit = l->container_limit;
+    r.max_depth = l->max_depth;
+    r.height = l->height;
+  }
+  return r;
+}
+
+template <class F>
+void parallel_for(uint64_t n, int threads, F&& fn) {
+  if (threads <= 1 || n < 1024) {
+    fn(0, n);
+    return;
+  }
+  std::vector<std::thread> ts;
+  const uint64_t chunk = (n + threads - 1) / threads;
+  for (int t = 0; t < threads; ++t) {
+    const uint64_t b = std::min(n, chunk * t), e = std::min(n, chunk * (t + 1));
+    if (b < e) ts.emplace_back([&fn, b, e] { fn(b, e); });
+  }
+  for (auto& t : ts) t.join();
+}
+
+inline uint64_t load_be64(const uint8_t* p) {
+  uint64_t v;
+  std::memcpy(&v, p, 8);
+  return __builtin_bswap64(v);
+}
+
+}  // namespace
+
+// ================================================================ C entry ===
+extern "C" {
+
+int oracle_encode_batch(const tgpu_struct_desc* structs, uint32_t n_structs,
+                        const tgpu_field_desc* fields, uint32_t n_fields,
+                        int protocol, const void* records, uint64_t n_records,
+                        const void* string_base, const void* list_base,
+                        void* out, uint64_t out_capacity, uint64_t* out_offsets,
+                        tgpu_status* st, uint64_t* out_size) {
+  Schema sc{structs, n_structs, fields, n_fields};
+  auto rec = (const uint8_t*)records;
+  auto sb = (const uint8_t*)string_base;
+  auto lb = (const uint8_t*)list_base;
+  if (protocol == TGPU_PROTOCOL_BINARY)
+    return encode_impl<BinaryWriter>(sc, rec, n_records, sb, lb, (uint8_t*)out,
+                                     out_capacity, out_offsets, st, out_size);
+  if (protocol == TGPU_PROTOCOL_COMPACT)
+    return encode_impl<CompactWriter>(sc, rec, n_records, sb, lb, (uint8_t*)out,
+                                      out_capacity, out_offsets, st, out_size);
+  set_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+  return TGPU_ERR_INVALID_ARGUMENT;
+}
+
+int oracle_decode_batch(const tgpu_struct_desc* structs, uint32_t n_structs,
+                        const tgpu_field_desc* fields, uint32_t n_fields,
+                        int protocol, const void* in, uint64_t in_len,
+                        const uint64_t* offsets, uint64_t n_records,
+                        void* records, void* list_arena,
+                        uint64_t list_arena_capacity, const tgpu_limits* limits,
+                        tgpu_status* st, uint64_t* n_decoded,
+                        uint64_t* consumed) {
+  Schema sc{structs, n_structs, fields, n_fields};
+  const Limits lim = to_limits(limits);
+  auto p = (const uint8_t*)in;
+  if (protocol == TGPU_PROTOCOL_BINARY)
+    return decode_impl<BinaryReader>(sc, p, in_len, offsets, n_records,
+                                     (uint8_t*)records, (uint8_t*)list_arena,
+                                     list_arena_capacity, lim, st, n_decoded,
+                                     consumed);
+  if (protocol == TGPU_PROTOCOL_COMPACT)
+    return decode_impl<CompactReader>(sc, p, in_len, offsets, n_records,
+                                      (uint8_t*)records, (uint8_t*)list_arena,
+                                      list_arena_capacity, lim, st, n_decoded,
+                                      consumed);
+  set_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+  return TGPU_ERR_INVALID_ARGUMENT;
+}
+
+int64_t oracle_record_length(int protocol, const void* in, uint64_t in_len,
+                             uint64_t pos, int32_t max_depth, int32_t height) {
+  Limits lim;
+  lim.max_depth = max_depth;
+  lim.height = height;
+  try {
+    if (protocol == TGPU_PROTOCOL_BINARY) {
+      BinaryReader r;
+      r.c = Cursor{(const uint8_t*)in, pos, in_len};
+      r.lim = lim;
+      r.height.h = lim.initial_height();
+      r.skip(TGPU_T_STRUCT, 0);
+      return (int64_t)(r.c.pos - pos);
+    }
+    CompactReader r;
+    r.c = Cursor{(const uint8_t*)in, pos, in_len};
+    r.lim = lim;
+    r.height.h = lim.initial_height();
+    r.skip(TGPU_T_STRUCT, 0);
+    return (int64_t)(r.c.pos - pos);
+  } catch (const OErr& e) {
+    return -(int64_t)e.code;
+  }
+}
+
+int64_t oracle_skip_value(int protocol, const void* in, uint64_t in_len, uint64_t pos,
+                          int ttype, int32_t max_depth, int32_t height) {
+  Limits lim;
+  lim.max_depth = max_depth;
+  lim.height = height;
+  try {
+    if (protocol == TGPU_PROTOCOL_BINARY) {
+      BinaryReader r;
+      r.c = Cursor{(const uint8_t*)in, pos, in_len};
+      r.lim = lim;
+      r.height.h = lim.initial_height();
+      r.skip((uint8_t)ttype, 0);
+      return (int64_t)(r.c.pos - pos);
+    }
+    CompactReader r;
+    r.c = Cursor{(const uint8_t*)in, pos, in_len};
+    r.lim = lim;
+    r.height.h = lim.initial_height();
+    r.skip((uint8_t)ttype, 0);
+    return (int64_t)(r.c.pos - pos);
+  } catch (const OErr& e) {
+    return -(int64_t)e.code;
+  }
+}
+
+int oracle_read_varint(const void* in, uint64_t len, int bits, uint64_t* value,
+                       uint64_t* consumed) {
+  Cursor c{(const uint8_t*)in, 0, len};
+  try {
+    uint64_t v = 0;
+    if (bits == 64) v = readVarint<64>(c);
+    else if (bits == 32) v = readVarint<32>(c);
+    else if (bits == 16) v = (uint16_t)readVarint<32>(c);  // i16 reads via i32
+    else return TGPU_ERR_INVALID_ARGUMENT;
+    *value = v;
+    *consumed = c.pos;
+    return TGPU_OK;
+  } catch (const OErr& e) {
+    *consumed = c.pos;
+    return e.code;
+  }
+}
+
+int oracle_write_varint(uint64_t value, void* out) {
+  Sink s{(uint8_t*)out, 0, 16};
+  s.varint(value);
+  return (int)s.pos;
+}
+
+// ---- codegen-equivalent flat {1..8: i64}, Binary ---------------------------
+// Generated readNoXfer (deserialize_struct.whisker:19-160) with
+// BinaryProtocolReader::advanceToNextField's fast path (BinaryProtocol-inl.h
+// :586-621): >= 3 bytes, type byte == T_I64, BE id == expected -> readBE<i64>.
+// Baseline timing runs on canonical streams only: a miss (the generated
+// _loop / switch / skip path) is reported as TGPU_ERR_UNSUPPORTED and the
+// caller uses oracle_decode_batch for irregular streams.
+int oracle_flat8_binary_decode(const void* in, uint64_t n, void* records,
+                               int n_threads) {
+  const uint8_t* p = (const uint8_t*)in;
+  uint8_t* out = (uint8_t*)records;
+  int rc = TGPU_OK;
+  parallel_for(n, n_threads, [&](uint64_t b, uint64_t e) {
+    for (uint64_t i = b; i < e; ++i) {
+      const uint8_t* r = p + i * 89;
+      uint8_t* o = out + i * 72;
+      bool ok = true;
+      for (int k = 0; k < 8 && ok; ++k) {
+        const uint8_t* f = r + 11 * k;
+        ok = f[0] == TGPU_T_I64 && f[1] == 0 && f[2] == (uint8_t)(k + 1);
+        if (ok) {
+          const uint64_t v = load_be64(f + 3);
+          std::memcpy(o + 8 * k, &v, 8);
+          o[64 + k] = 1;
+        }
+      }
+      if (!ok || r[88] != TGPU_T_STOP) rc = TGPU_ERR_UNSUPPORTED;  // irregular
+    }
+  });
+  return rc;
+}
+
+int oracle_flat8_binary_encode(const void* records, uint64_t n, void* out,
+                               int n_threads) {
+  const uint8_t* rp = (const uint8_t*)records;
+  uint8_t* o = (uint8_t*)out;
+  parallel_for(n, n_threads, [&](uint64_t b, uint64_t e) {
+    for (uint64_t i = b; i < e; ++i) {
+      const uint8_t* r = rp + i * 72;
+      uint8_t* w = o + i * 89;
+      for (int k = 0; k < 8; ++k) {
+        w[11 * k] = TGPU_T_I64;
+        w[11 * k + 1] = 0;
+        w[11 * k + 2] = (uint8_t)(k + 1);
+        uint64_t v;
+        std::memcpy(&v, r + 8 * k, 8);
+        v = __builtin_bswap64(v);
+        std::memcpy(w + 11 * k + 3, &v, 8);
+      }
+      w[88] = TGPU_T_STOP;
+    }
+  });
+  return TGPU_OK;
+}
+
+// ---- codegen-equivalent {1..4: i32, 5..6: string}, Compact -----------------
+// Device layout: i32 @0,4,8,12; span @16,32; isset[6] @48; size 56.
+int oracle_mixed_compact_decode(const void* in, const uint64_t* offsets,
+                                uint64_t n, void* records, int n_threads) {
+  const uint8_t* p = (const uint8_t*)in;
+  uint8_t* out = (uint8_t*)records;
+  int rc = TGPU_OK;
+  parallel_for(n, n_threads, [&](uint64_t b, uint64_t e) {
+    for (uint64_t i = b; i < e; ++i) {
+      uint8_t* o = out + i * 56;
+      std::memset(o, 0, 56);
+      CompactReader r;
+      r.c = Cursor{p, offsets[i], offsets[n]};
+      r.height.h = 12001;
+      try {
+        // advanceToNextField(prev, next, T_I32): 1-byte header (Δ=1 | CT_I32)
+        for (int k = 0; k < 4; ++k) {
+          if (r.c.avail() && r.c.p[r.c.pos] == 0x15) {
+            r.c.pos++;
+            const int32_t v = zigzagToI32((uint32_t)readVarint<32>(r.c));
+            std::memcpy(o + 4 * k, &v, 4);
+            o[48 + k] = 1;
+          } else {
+            throw OErr{TGPU_ERR_UNSUPPORTED, r.c.pos};
+          }
+        }
+        for (int k = 0; k < 2; ++k) {
+          if (r.c.avail() && r.c.p[r.c.pos] == 0x18) {
+            r.c.pos++;
+            tgpu_span sp{0, 0, 0};
+            r.readString(sp.offset, sp.length);
+            std::memcpy(o + 16 + 16 * k, &sp, 16);
+            o[52 + k] = 1;
+          } else {
+            throw OErr{TGPU_ERR_UNSUPPORTED, r.c.pos};
+          }
+        }
+        if (!(r.c.avail() && r.c.p[r.c.pos] == 0)) throw OErr{TGPU_ERR_UNSUPPORTED, r.c.pos};
+      } catch (const OErr& err) {
+        rc = err.code;
+      }
+    }
+  });
+  return rc;
+}
+
+int oracle_mixed_compact_encode(const void* records, uint64_t n,
+                                const void* string_base, void* out,
+                                const uint64_t* offsets, int n_threads) {
+  const uint8_t* rp = (const uint8_t*)records;
+  const uint8_t* sb = (const uint8_t*)string_base;
+  uint8_t* o = (uint8_t*)out;
+  parallel_for(n, n_threads, [&](uint64_t b, uint64_t e) {
+    for (uint64_t i = b; i < e; ++i) {
+      const uint8_t* r = rp + i * 56;
+      Sink s{o, offsets[i], offsets[n]};
+      for (int k = 0; k < 4; ++k) {
+        s.put(0x15);
+        s.varint(i32ToZigzag(ld<int32_t>(r + 4 * k)));
+      }
+      for (int k = 0; k < 2; ++k) {
+        const tgpu_span sp = ld<tgpu_span>(r + 16 + 16 * k);
+        s.put(0x18);
+        s.varint(sp.length);
+        s.putBytes(sb + sp.offset, sp.length);
+      }
+      s.put(0);
+    }
+  });
+  return TGPU_OK;
+}
+
+// ---- generators ------------------------------------------------------------
+// Counter-based splitmix64 (Steele/Lea/Flood; the survey's PRNG, seed 0x1729 =
+// VarintUtilsTestUtil.h:59): z = seed + (index+1)*golden, then the finalizer.
+uint64_t oracle_splitmix64_at(uint64_t seed, uint64_t index) {
+  uint64_t z = seed + (index + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// Config 1/2: value(i, k) = splitmix64_at(seed, 8*i + k); records with
+// i % 997 < 5 carry edge values {0, -1, 1, INT64_MIN, INT64_MAX} rotated.
+void oracle_gen_flat8(uint64_t seed, uint64_t first, uint64_t n, void* records) {
+  static const int64_t edges[5] = {0, -1, 1, INT64_MIN, INT64_MAX};
+  uint8_t* o = (uint8_t*)records;
+  for (uint64_t j = 0; j < n; ++j) {
+    const uint64_t i = first + j;
+    uint8_t* r = o + j * 72;
+    for (int k = 0; k < 8; ++k) {
+      int64_t v = (int64_t)oracle_splitmix64_at(seed, 8 * i + k);
+      if (i % 997 < 5) v = edges[(i % 997 + k) % 5];
+      std::memcpy(r + 8 * k, &v, 8);
+      r[64 + k] = 1;
+    }
+  }
+}
+
+}  // extern "C"

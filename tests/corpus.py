@@ -1,0 +1,157 @@
+"""Semantic pins restated from the reference's C++ tests, as decode cases.
+
+Each entry: (name, protocol, schema table, stream bytes, n_records, limits,
+expected code or None). `expected` comes from the cited reference test; the
+oracle must produce it, and the GPU must produce the oracle's full status.
+"""
+import struct
+
+from wire import B, C, W, varint, zz32, zz64
+
+I64, I32, I16, BOOL, BYTE, STR, LIST, SET, STRUCT, MAP, DBL = 10, 8, 6, 2, 3, 11, 15, 14, 12, 13, 4
+
+# codes (include/thrift_gpu.h)
+OK, UNDERFLOW, VARINT, BOOLV, SKIPT, TRUNC, NEG, LIMIT, DEPTH, BADT = 0, 1, 2, 3, 4, 5, 6, 7, 8, 9
+
+TRUNC_SCHEMA = [[[1, LIST, I64, 1, -1], [2, SET, I32, 1, -1], [4, STR, 0, 1, -1]]]
+BOOL_SCHEMA = [[[1, BOOL, 0, 0, -1], [2, I32, 0, 0, -1]]]
+FLAT = [[[k, I64, 0, 0, -1] for k in range(1, 9)]]
+EMPTY = [[]]
+
+
+def truncated_list(proto):
+    # ProtocolTruncatedDataTest.cpp:98-108: 30 x (1 << i) as list<i64>
+    w = W(proto).field(LIST, 1).list_begin(I64, 30)
+    for i in range(30):
+        w.i64(1 << i)
+    return w.stop().bytes()
+
+
+def truncated_set(proto):
+    w = W(proto).field(SET, 2).list_begin(I32, 30)
+    for i in range(30):
+        w.i32((1 << i) - (1 << 32 if (1 << i) >= (1 << 31) else 0))
+    return w.stop().bytes()
+
+
+def truncated_string(proto):
+    return W(proto).field(STR, 4).string(b"foobarbazstring").stop().bytes()
+
+
+def cases():
+    out = []
+    # --- ProtocolTruncatedDataTest.cpp:28-120 (Compact list/set, both strings)
+    for p, name, full, keep in [
+        (C, "trunc_list", truncated_list(C), 3 + 30),
+        (C, "trunc_set", truncated_set(C), 3 + 30),
+        (C, "trunc_str_compact", truncated_string(C), 2 + 15),
+        (B, "trunc_str_binary", truncated_string(B), 7 + 15),
+    ]:
+        out.append((name + "_full", p, TRUNC_SCHEMA, full, 1, None, OK))
+        # trimmed to just pass the size check: std::out_of_range
+        out.append((name + "_pass_check", p, TRUNC_SCHEMA, full[:keep], 1, None, UNDERFLOW))
+        # one byte less: TProtocolException (throwTruncatedData)
+        out.append((name + "_fail_check", p, TRUNC_SCHEMA, full[:keep - 1], 1, None, TRUNC))
+    # --- BinaryProtocolTest.cpp:30-41 readBool: byte >= 2 throws INVALID_DATA
+    for v, code in ((0, OK), (1, OK), (2, BOOLV), (0x42, BOOLV)):
+        wb = W(B).field(BOOL, 1).byte(v).field(I32, 2).i32(5).stop().bytes()
+        out.append(("binary_bool_%d" % v, B, BOOL_SCHEMA, wb, 1, None, code))
+    # Compact container bools accept any byte (== 1 -> true), field bools ride
+    # in the header (CompactProtocol-inl.h:692-701)
+    for v in (0, 1, 2, 0x42):
+        wc = W(C).field(LIST, 1).list_begin(BOOL, 2).byte(v).byte(1).stop().bytes()
+        out.append(("compact_bool_list_%d" % v, C, [[[1, LIST, BOOL, 0, -1]]], wc, 1, None, OK))
+    # --- VarintUtilsTest.cpp:238-280: overflow, junk high bits, big zeros
+    for p_name, bits, ttype, kmax in (("i32", 32, I32, 5), ("i64", 64, I64, 10)):
+        sch = [[[1, ttype, 0, 0, -1]]]
+        hdr = bytes([0x10 | (5 if bits == 32 else 6)])
+        out.append(("varint_overflow_" + p_name, C, sch, hdr + b"\x80" * kmax + b"\x00", 1, None,
+                    VARINT))
+        out.append(("varint_junk_" + p_name, C, sch, hdr + b"\x80" * (kmax - 1) + b"\x7f\x00", 1,
+                    None, OK))
+        for i in range(1, kmax):
+            z = b"\x80" * i + b"\x00"
+            out.append(("varint_bigzero_%s_%d" % (p_name, i), C, sch, hdr + z + b"\x00", 1, None,
+                        OK))
+        out.append(("varint_cut_" + p_name, C, sch, hdr + b"\x80\x80", 1, None, UNDERFLOW))
+    # --- sizes: negative / limits (BinaryProtocol-inl.h:535-551,
+    # CompactProtocol-inl.h:615-640,742-749)
+    sstr = [[[1, STR, 0, 0, -1]]]
+    out.append(("binary_neg_string", B, sstr, b"\x0b\x00\x01\xff\xff\xff\xff\x00", 1, None, NEG))
+    out.append(("compact_neg_string", C, sstr, b"\x18" + varint(0x80000000) + b"\x00", 1, None, NEG))
+    out.append(("binary_string_limit", B, sstr, W(B).field(STR, 1).string(b"abcdef").stop().bytes(),
+                1, (4, 0, 12000, 0), LIMIT))
+    out.append(("compact_string_limit", C, sstr,
+                W(C).field(STR, 1).string(b"abcdef").stop().bytes(), 1, (4, 0, 12000, 0), LIMIT))
+    slist = [[[1, LIST, I32, 0, -1]]]
+    out.append(("binary_neg_list", B, slist, b"\x0f\x00\x01\x08\xff\xff\xff\xfe\x00", 1, None, NEG))
+    out.append(("compact_neg_list", C, slist, b"\x19\xf5" + varint(0xFFFFFFFF) + b"\x00", 1, None,
+                NEG))
+    lst = W(C).field(LIST, 1).list_begin(I32, 5)
+    for i in range(5):
+        lst.i32(i)
+    out.append(("compact_container_limit", C, slist, lst.stop().bytes(), 1, (0, 3, 12000, 0),
+                LIMIT))
+    # element-type mismatch: list skipped, left empty, no error
+    # (protocol_methods.h:405-406)
+    mm = W(B).field(LIST, 1).list_begin(I64, 2).i64(1).i64(2).stop().bytes()
+    out.append(("binary_list_type_mismatch", B, slist, mm, 1, None, OK))
+    mmc = W(C).field(LIST, 1).list_begin(STR, 2).string(b"x").string(b"yz").stop().bytes()
+    out.append(("compact_list_type_mismatch", C, slist, mmc, 1, None, OK))
+    # --- Compact "don't know what type" (CompactProtocol-inl.h:783-791)
+    out.append(("compact_bad_type_field", C, EMPTY, b"\x1e\x00", 1, None, BADT))
+    out.append(("compact_bad_list_elem", C, EMPTY, b"\x19\x1e\x00", 1, None, BADT))
+    # --- ProtocolSkipTest.cpp: invalid skip types (VOID/STREAM/unknown) in
+    # Binary unknown fields, valid ones skipped
+    for t, code in ((1, SKIPT), (18, SKIPT), (0x55, SKIPT), (16, OK), (17, OK), (9, OK)):
+        body = b"\x00\x00\x00\x02ab" if t in (16, 17) else (b"\x00" * 8 if t == 9 else b"")
+        out.append(("binary_skip_type_%d" % t, B, EMPTY, bytes([t, 0, 7]) + body + b"\x00", 1,
+                    None, code))
+    # Binary skip of a string whose length passes the pre-length canAdvance
+    # check but not the real one: out_of_range (BinaryProtocol.cpp:163-172)
+    out.append(("binary_skip_string_edge", B, EMPTY, b"\x0b\x00\x07\x00\x00\x00\x05abcd", 1, None,
+                UNDERFLOW))
+    out.append(("binary_skip_string_neg", B, EMPTY, b"\x0b\x00\x07\xff\xff\xff\xff\x00", 1, None,
+                TRUNC))
+    # --- field ids: long form, negative, out of order, duplicates
+    w = W(C)
+    w.field(I64, 8).i64(-8).field(I64, 1).i64(1).field(I64, 100).i64(9)  # unknown 100
+    w.field(I64, 1).i64(11)  # duplicate: later wins
+    out.append(("compact_reorder_dup", C, FLAT, w.stop().bytes(), 1, None, OK))
+    w = W(B)
+    for k in (3, 1, 2):
+        w.field(I64, k).i64(k * 1000)
+    w.field(I32, 4).i32(7)  # type mismatch with schema (i64): skipped
+    out.append(("binary_reorder_mismatch", B, FLAT, w.stop().bytes(), 1, None, OK))
+    # --- truncation inside headers / values
+    full = W(B).field(I64, 1).i64(5).stop().bytes()
+    for cut in range(len(full)):
+        out.append(("binary_cut_%d" % cut, B, FLAT, full[:cut], 1, None, UNDERFLOW))
+    fullc = W(C).field(I64, 1).i64(-300).stop().bytes()
+    for cut in range(len(fullc)):
+        out.append(("compact_cut_%d" % cut, C, FLAT, fullc[:cut], 1, None, UNDERFLOW))
+    # --- Compact STOP forms: any byte with zero low nibble ends the struct
+    for b0 in (0x00, 0x10, 0xF0):
+        out.append(("compact_stop_%02x" % b0, C, FLAT, bytes([b0]), 1, None, OK))
+    # --- skip depth (ProtocolTest.cpp:275-300, kTestingProtocolMaxDepth = 4)
+    for p in (B, C):
+        for t in (STRUCT, LIST, SET, MAP):
+            ok_stream = nested_record(p, 4, 3, t)
+            out.append(("depth_ok_%d_%d" % (p, t), p, EMPTY, ok_stream, 1, (0, 0, 12000, 4), None))
+            deep = nested_record(p, 5, 5, t)
+            out.append(("depth_deep_%d_%d" % (p, t), p, EMPTY, deep, 1, (0, 0, 12000, 4), None))
+    # --- multi-record streams with a failure in the middle: first failing
+    # record index and consumed bytes
+    good = W(B).field(I64, 1).i64(1).stop().bytes()
+    bad = W(B).field(BOOL, 2).byte(9).stop().bytes()
+    two = [[[1, I64, 0, 0, -1], [2, BOOL, 0, 0, -1]]]
+    out.append(("binary_mid_failure", B, two, good * 5 + bad + good * 3, 9, None, BOOLV))
+    goodc = W(C).field(I64, 1).i64(1).stop().bytes()
+    badc = W(C).field(I64, 1).raw(b"\xff" * 10).stop().bytes()
+    out.append(("compact_mid_failure", C, two, goodc * 7 + badc + goodc, 9, None, VARINT))
+    return out
+
+
+def nested_record(proto, height, levels, ttype):
+    import wire
+    return wire.nested(proto, height, levels, ttype)
