@@ -106,7 +106,7 @@ def lib():
     L.tgpu_encode_batch.argtypes = [P, P, I32, P, U64, P, P, P, U64, P, P,
                                     ctypes.POINTER(Status), ctypes.POINTER(U64)]
     L.tgpu_encoded_size.restype = I32
-    L.tgpu_encoded_size.argtypes = [P, P, I32, P, U64, P, P, ctypes.POINTER(Status),
+    L.tgpu_encoded_size.argtypes = [P, P, I32, P, U64, P, P, P, ctypes.POINTER(Status),
                                     ctypes.POINTER(U64)]
     L.tgpu_decode_batch.restype = I32
     L.tgpu_decode_batch.argtypes = [P, P, I32, P, U64, P, U64, P, P, U64,

@@ -18,6 +18,7 @@ struct tgpu_schema {
   tgpu_field_desc* d_fields = nullptr;
   int device = 0;
   bool has_lists = false;
+  bool has_strings = false;
   bool fixed_binary = false;
   FixedTemplate tmpl{};
   FixedTemplate* d_tmpl = nullptr;
@@ -275,6 +276,7 @@ int tgpu_schema_create(const tgpu_struct_desc* structs, uint32_t n_structs,
   s->structs.assign(structs, structs + n_structs);
   s->fields.assign(fields, fields + n_fields);
   s->has_lists = has_lists;
+  for (uint32_t k = 0; k < n_fields; ++k) s->has_strings |= fields[k].ttype == TGPU_T_STRING;
   (void)hipGetDevice(&s->device);
   if (hipMalloc(&s->d_structs, sizeof(tgpu_struct_desc) * n_structs) != hipSuccess ||
       hipMalloc(&s->d_fields, sizeof(tgpu_field_desc) * std::max(n_fields, 1u)) != hipSuccess) {
@@ -352,10 +354,12 @@ int tgpu_context_wait(tgpu_context* ctx, void* stream, tgpu_status* st, uint64_t
                       uint64_t* bytes) {
   if (!ctx) return TGPU_ERR_INVALID_ARGUMENT;
   const hipStream_t s = (hipStream_t)stream;
-  if (hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s) !=
-          hipSuccess ||
-      hipStreamSynchronize(s) != hipSuccess) {
+  hipError_t e = hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(DevResult),
+                                hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
     fill_status(st, TGPU_ERR_HIP, 0, 0);
+    if (st) st->reserved = (int32_t)e;
     return TGPU_ERR_HIP;
   }
   const DevResult& r = *ctx->h_res;
@@ -377,10 +381,12 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   }
   const hipStream_t s = (hipStream_t)stream;
   const uint32_t rs = schema->structs[0].size;
-  if (((uintptr_t)records) % schema->structs[0].align) {
+  if (((uintptr_t)records) % schema->structs[0].align ||
+      (n && schema->has_lists && !list_base) || (n && schema->has_strings && !string_base)) {
     fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
     return TGPU_ERR_INVALID_ARGUMENT;
   }
+  (void)hipGetLastError();  // drop a stale error left by another library
   hipError_t e = launch_result_init(ctx->d_res, n, s);
   EncodeArgs a{};
   a.sc = dev_schema(schema);
@@ -413,6 +419,7 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   ctx->last_op = 2;
   if (e != hipSuccess) {
     fill_status(st, TGPU_ERR_HIP, 0, 0);
+    if (st) st->reserved = (int32_t)e;
     return TGPU_ERR_HIP;
   }
   if (st || out_size) {
@@ -426,8 +433,8 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
 }
 
 int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
-                      const void* records, uint64_t n, uint64_t* out_offsets, void* stream,
-                      tgpu_status* st, uint64_t* total) {
+                      const void* records, uint64_t n, const void* list_base,
+                      uint64_t* out_offsets, void* stream, tgpu_status* st, uint64_t* total) {
   if (!ctx || !schema || !out_offsets ||
       (protocol != TGPU_PROTOCOL_BINARY && protocol != TGPU_PROTOCOL_COMPACT) ||
       (n && !records) || ((uintptr_t)records) % schema->structs[0].align) {
@@ -449,12 +456,19 @@ int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   a.rec_size = schema->structs[0].size;
   a.res = ctx->d_res;
   a.cap = ~0ull;
+  a.lbase = (const uint8_t*)list_base;
+  if (schema->has_lists && n && !list_base) {
+    fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+    return TGPU_ERR_INVALID_ARGUMENT;
+  }
+  (void)hipGetLastError();  // drop a stale error left by another library
   hipError_t e = launch_result_init(ctx->d_res, n, s);
   if (e == hipSuccess && n) e = launch_general_size(a, protocol, (n + 255) / 256, s);
   if (e == hipSuccess && n) e = launch_encode_finish(a, protocol, 0, s);
   if (e == hipSuccess && !n) e = hipMemsetAsync(out_offsets, 0, sizeof(uint64_t), s);
   if (e != hipSuccess) {
     fill_status(st, TGPU_ERR_HIP, 0, 0);
+    if (st) st->reserved = (int32_t)e;
     return TGPU_ERR_HIP;
   }
   if (st || total) {
@@ -497,6 +511,7 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   a.height = limits ? limits->height : 0;
   a.rec_size = schema->structs[0].size;
   a.res = ctx->d_res;
+  (void)hipGetLastError();  // drop a stale error left by another library
   hipError_t e = launch_result_init(ctx->d_res, n, s);
   uint64_t fixed = 0;
   if (n && protocol == TGPU_PROTOCOL_BINARY && schema->fixed_binary && !offsets &&
@@ -522,6 +537,7 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   ctx->last_op = 1;
   if (e != hipSuccess) {
     fill_status(st, TGPU_ERR_HIP, 0, 0);
+    if (st) st->reserved = (int32_t)e;
     return TGPU_ERR_HIP;
   }
   if (st || n_decoded || consumed) {

@@ -225,8 +225,8 @@ struct Proto<TGPU_PROTOCOL_BINARY> {
   }
   static __device__ __forceinline__ void read_scalar(Reader& r, uint32_t t, uint8_t* dst) {
     switch (t) {
-      case TGPU_T_BOOL: *dst = (uint8_t)read_bool(r); break;
-      case TGPU_T_BYTE: *dst = (uint8_t)r.read8(); break;
+      case TGPU_T_BOOL: { const uint32_t v = read_bool(r); if (r.ok()) *dst = (uint8_t)v; break; }
+      case TGPU_T_BYTE: { const uint32_t v = r.read8(); if (r.ok()) *dst = (uint8_t)v; break; }
       case TGPU_T_I16: { const uint16_t v = (uint16_t)r.readBE(2); if (r.ok()) *(uint16_t*)dst = v; break; }
       case TGPU_T_I32:
       case TGPU_T_FLOAT: { const uint32_t v = (uint32_t)r.readBE(4); if (r.ok()) *(uint32_t*)dst = v; break; }
@@ -340,8 +340,8 @@ struct Proto<TGPU_PROTOCOL_COMPACT> {
   }
   static __device__ __forceinline__ void read_scalar(Reader& r, uint32_t t, uint8_t* dst) {
     switch (t) {
-      case TGPU_T_BOOL: *dst = (uint8_t)read_bool(r); break;
-      case TGPU_T_BYTE: *dst = (uint8_t)r.read8(); break;
+      case TGPU_T_BOOL: { const uint32_t v = read_bool(r); if (r.ok()) *dst = (uint8_t)v; break; }
+      case TGPU_T_BYTE: { const uint32_t v = r.read8(); if (r.ok()) *dst = (uint8_t)v; break; }
       case TGPU_T_I16: { const int16_t v = (int16_t)zz_to_i32((uint32_t)r.varint(32)); if (r.ok()) *(int16_t*)dst = v; break; }
       case TGPU_T_I32: { const int32_t v = zz_to_i32((uint32_t)r.varint(32)); if (r.ok()) *(int32_t*)dst = v; break; }
       case TGPU_T_I64: { const int64_t v = zz_to_i64(r.varint(64)); if (r.ok()) *(int64_t*)dst = v; break; }
@@ -491,12 +491,29 @@ __device__ void read_list(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8
     const uint32_t es = scalar_size(f.elem_ttype);
     const uint64_t aoff = Pr::kArenaScale * r.pos;
     if (n > 0) {
-      if (!arena || aoff + (uint64_t)n * es > arena_cap) return r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
+      if (!arena) return r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
+      // the list is resized to n before the element reads
       sp.offset = aoff;
       sp.length = (uint32_t)n;
-      for (int32_t i = 0; i < n && r.ok(); ++i)
-        Pr::read_scalar(r, f.elem_ttype, arena + aoff + (uint64_t)i * es);
       *(tgpu_span*)m = sp;
+      int32_t i = 0;
+      for (; i < n; ++i) {
+        const uint64_t at = aoff + (uint64_t)i * es;
+        if (at + es > arena_cap) {
+          r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
+          break;
+        }
+        Pr::read_scalar(r, f.elem_ttype, arena + at);
+        if (!r.ok()) break;
+      }
+      if (!r.ok()) {
+        // leftover elements are value-initialized (protocol_methods.h:441-451)
+        for (; i < n; ++i) {
+          const uint64_t at = aoff + (uint64_t)i * es;
+          if (at + es > arena_cap) break;
+          for (uint32_t b = 0; b < es; ++b) arena[at + b] = 0;
+        }
+      }
     }
   }
   if (r.ok()) r.ascend();
@@ -572,6 +589,7 @@ struct Writer {
     }
   }
   __device__ __forceinline__ void put(uint32_t b) {
+    if (err) return;  // never write past the byte that failed validation
     if (out) out[pos] = (uint8_t)b;
     ++pos;
   }

@@ -147,7 +147,7 @@ class BatchSerializer:
         return self._ctx
 
     # -- size -----------------------------------------------------------------
-    def encoded_size(self, gschema, records, n=None, offsets=None, stream=None):
+    def encoded_size(self, gschema, records, n=None, offsets=None, stream=None, list_base=None):
         import torch
 
         n = records.numel() // gschema.record_size if n is None else n
@@ -155,7 +155,8 @@ class BatchSerializer:
             offsets = torch.empty(n + 1, dtype=torch.int64, device=records.device)
         st, total = _lib.Status(), ctypes.c_uint64()
         _lib.lib().tgpu_encoded_size(self.context().handle, gschema.handle, self.protocol,
-                                     _ptr(records), n, _ptr(offsets), _stream(stream),
+                                     _ptr(records), n, _ptr(list_base), _ptr(offsets),
+                                     _stream(stream),
                                      ctypes.byref(st), ctypes.byref(total))
         raise_for_status(st)
         return offsets, total.value
@@ -181,7 +182,7 @@ class BatchSerializer:
             else:
                 size_offs = off_t if off_t is not None else torch.empty(
                     n + 1, dtype=torch.int64, device=dev)
-                _, cap = self.encoded_size(gschema, records, n, size_offs, stream)
+                _, cap = self.encoded_size(gschema, records, n, size_offs, stream, list_base)
             out = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev)
         st, size = _lib.Status(), ctypes.c_uint64()
         rc = _lib.lib().tgpu_encode_batch(

@@ -245,12 +245,14 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema,
  * and of the whole batch, without writing it: the bulk form of
  * T::serializedSize<P> (serialize_struct.whisker:17-26; the reference returns
  * an upper bound with varints counted at their maximum width, this is exact).
- * Validates like encode (bool bytes, string/list sizes).
+ * Validates like encode (bool bytes, string/list sizes). list_base is
+ * required when the schema has lists (Compact element widths depend on the
+ * element values); string payloads are not read.
  */
 int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
                       const void* records, uint64_t n_records,
-                      uint64_t* out_offsets, void* stream, tgpu_status* st,
-                      uint64_t* total);
+                      const void* list_base, uint64_t* out_offsets,
+                      void* stream, tgpu_status* st, uint64_t* total);
 
 /* ---- batch decode ----------------------------------------------------- */
 /*

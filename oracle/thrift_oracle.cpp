@@ -517,17 +517,29 @@ void readList(R& r, const tgpu_field_desc& f, uint8_t* member, DecodeCtx& dc) {
     if (!r.c.canAdvance((uint64_t)(uint32_t)n)) fail(TGPU_ERR_TRUNCATED, r.c.pos);  // canReadNElements
     const uint32_t es = scalar_size(f.elem_ttype);
     const uint64_t aoff = R::kArenaScale * r.c.pos;
-    if (n > 0 && (aoff + (uint64_t)n * es > dc.arena_cap || !dc.arena))
-      fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
     if (n > 0) {
+      if (!dc.arena) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
+      // resizeWithoutInitialization(out, n) happens before the element reads
       span.offset = aoff;
       span.length = (uint32_t)n;
+      std::memcpy(member, &span, sizeof(span));
     }
-    for (int32_t i = 0; i < n; ++i) {
-      r.readScalar(f.elem_ttype, dc.arena + aoff + (uint64_t)i * es);
-      // the list object holds the elements read so far
+    int32_t i = 0;
+    try {
+      for (; i < n; ++i) {
+        const uint64_t at = aoff + (uint64_t)i * es;
+        if (at + es > dc.arena_cap) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
+        r.readScalar(f.elem_ttype, dc.arena + at);
+      }
+    } catch (const OErr&) {
+      // protocol_methods.h:441-451: leftover elements are value-initialized
+      for (; i < n; ++i) {
+        const uint64_t at = aoff + (uint64_t)i * es;
+        if (at + es > dc.arena_cap) break;
+        std::memset(dc.arena + at, 0, es);
+      }
+      throw;
     }
-    std::memcpy(member, &span, sizeof(span));
   }
   r.height.ascend();  // readListEnd
 }

@@ -1,0 +1,210 @@
+"""GPU parity: every call goes through the C-ABI (libtgpu.so) on cuda:0 and is
+compared with the oracle (CPU restatement pinned to the reference's golden
+vectors) byte for byte — records, list arenas, wire bytes, offsets and the
+full error status (code, exception class, record, byte offset)."""
+import numpy as np
+import pytest
+
+import corpus
+import datagen
+import helpers
+from fbthrift_amd.schema import Schema
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a, dev):
+    import torch
+
+    a = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+    if a.size == 0:
+        a = np.zeros(1, np.uint8)
+    return torch.from_numpy(a.copy()).to(dev)
+
+
+def _np(t):
+    return t.cpu().numpy()
+
+
+def _ser(protocol):
+    from fbthrift_amd.serializer import BinarySerializer, CompactSerializer
+
+    return BinarySerializer if protocol == 0 else CompactSerializer
+
+
+def _gschema(schema):
+    from fbthrift_amd.serializer import GpuSchema
+
+    return GpuSchema(schema)
+
+
+def gpu_decode(schema, protocol, stream, n, offsets=None, limits=None, dev=None):
+    import torch
+
+    gs = _gschema(schema)
+    w = torch.from_numpy(np.frombuffer(bytes(stream), np.uint8).copy()).to(dev) if len(stream) \
+        else torch.zeros(0, dtype=torch.uint8, device=dev)
+    offs = None
+    if offsets is not None:
+        offs = torch.from_numpy(np.asarray(offsets, dtype=np.int64).copy()).to(dev)
+    rec, arena, st, nd, cons = _ser(protocol).deserialize_status(gs, w, n, offs, limits)
+    return st, _np(rec), _np(arena), nd, cons
+
+
+@pytest.mark.parametrize("name", helpers.case_names())
+@pytest.mark.parametrize("indexed", [False, True])
+def test_decode_golden(gpu, name, indexed):
+    c = helpers.Case(name)
+    offs = c.offsets if indexed else None
+    st, rec, arena, nd, cons = gpu_decode(c.schema, c.protocol, c.wire, c.n, offs, dev=gpu)
+    assert st.code == 0, st.as_tuple()
+    assert nd == c.n and cons == len(c.wire)
+    ost, orec, oarena, _, _ = oracle.decode(c.schema, c.protocol, c.wire, c.n, offsets=offs)
+    assert np.array_equal(rec[: c.n * c.schema.record_size], orec[: c.n * c.schema.record_size])
+    k = min(arena.size, oarena.size)
+    assert np.array_equal(arena[:k], oarena[:k])
+    helpers.assert_values_equal(helpers.unpack(c.schema, rec, c.n, c.wire, arena), c.values)
+
+
+@pytest.mark.parametrize("name", helpers.case_names())
+def test_encode_golden(gpu, name):
+    c = helpers.Case(name)
+    rec, sarena, larena = helpers.pack(c.schema, c.values, c.n)
+    gs = _gschema(c.schema)
+    out, offs = _ser(c.protocol).serialize(gs, _t(rec, gpu), c.n, _t(sarena, gpu),
+                                           _t(larena, gpu))
+    assert bytes(_np(out)) == c.wire
+    assert np.array_equal(_np(offs).astype(np.uint64), c.offsets)
+    sz_offs, total = _ser(c.protocol).encoded_size(gs, _t(rec, gpu), c.n,
+                                                   list_base=_t(larena, gpu))
+    assert total == len(c.wire)
+    assert np.array_equal(_np(sz_offs).astype(np.uint64), c.offsets)
+
+
+@pytest.mark.parametrize("case", corpus.cases(), ids=lambda c: c[0])
+def test_corpus_status_parity(gpu, case):
+    name, proto, table, stream, n, limits, expected = case
+    schema = Schema.from_table(table)
+    st, rec, arena, nd, cons = gpu_decode(schema, proto, stream, n, None, limits, dev=gpu)
+    ost, orec, oarena, ond, ocons = oracle.decode(schema, proto, stream, n, limits=limits)
+    assert st.as_tuple() == ost.as_tuple(), name
+    assert (nd, cons) == (ond, ocons)
+    k = (nd + (1 if st.code else 0)) * schema.record_size  # failing record is partial in both
+    assert np.array_equal(rec[:k], orec[:k])
+
+
+def _flat8(n, first=0):
+    buf = np.zeros(n * 72, np.uint8)
+    oracle.lib().oracle_gen_flat8(datagen.SEED, first, n, buf.ctypes.data)
+    return buf
+
+
+def test_flat8_fixed_path_roundtrip(gpu):
+    """Config 1/2 shape at 1M records: fixed-layout kernels vs the
+    codegen-equivalent oracle, both directions."""
+    n = 1 << 20
+    schema = Schema.from_table(datagen.SCHEMAS["flat8"])
+    gs = _gschema(schema)
+    assert gs.fixed_wire_size(0) == 89
+    recs = _flat8(n)
+    want = np.zeros(n * 89, np.uint8)
+    oracle.lib().oracle_flat8_binary_encode(recs.ctypes.data, n, want.ctypes.data, 8)
+    from fbthrift_amd.serializer import BinarySerializer as BS
+
+    wire, offs = BS.serialize(gs, _t(recs, gpu), n)
+    assert np.array_equal(_np(wire), want)
+    assert np.array_equal(_np(offs), np.arange(n + 1, dtype=np.int64) * 89)
+    out, _, consumed = BS.deserialize(gs, wire, n)
+    assert consumed == n * 89
+    assert np.array_equal(_np(out), recs)
+
+
+@pytest.mark.parametrize("where", [0, 1, 255, 256, 4097, 9999])
+def test_flat8_irregular_fallback(gpu, where):
+    """A non-canonical record (reordered fields + an unknown field) at index
+    `where` sends the rest of the stream through the serial decoder; results
+    equal the oracle's sequential read."""
+    import wire as wb
+
+    n = 10000
+    schema = Schema.from_table(datagen.SCHEMAS["flat8"])
+    recs = _flat8(n)
+    canon = np.zeros(n * 89, np.uint8)
+    oracle.lib().oracle_flat8_binary_encode(recs.ctypes.data, n, canon.ctypes.data, 1)
+    w = wb.W(0)
+    for k in (2, 1, 3, 4, 5, 6, 7, 8):
+        w.field(10, k).i64(k * 111)
+    w.field(11, 99).string(b"unknown-field")
+    irregular = w.stop().bytes()
+    stream = canon[: where * 89].tobytes() + irregular + canon[(where + 1) * 89:].tobytes()
+    st, rec, arena, nd, cons = gpu_decode(schema, 0, stream, n, dev=gpu)
+    ost, orec, _, ond, ocons = oracle.decode(schema, 0, stream, n)
+    assert st.as_tuple() == ost.as_tuple() and st.code == 0
+    assert (nd, cons) == (ond, ocons)
+    assert np.array_equal(rec, orec)
+
+
+def test_flat8_invalid_bool_stream_and_write(gpu):
+    """A bool field with byte 2 in a fixed-layout schema: decode reports
+    TProtocolException(INVALID_DATA) at that record; encoding a record whose
+    bool byte is 2 reports the abort-class error."""
+    table = [[[1, 10, 0, 0, -1], [2, 2, 0, 0, -1], [3, 8, 0, 0, -1]]]
+    schema = Schema.from_table(table)
+    n = 3000
+    rng = np.random.default_rng(7)
+    rec = np.zeros(n, dtype=schema.dtype())
+    rec["f1"] = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64)
+    rec["f2"] = rng.integers(0, 2, n)
+    rec["f3"] = rng.integers(-2**31, 2**31 - 1, n, dtype=np.int32)
+    rec["__isset"] = 1
+    st, wire_, _ = oracle.encode(schema, 0, rec.view(np.uint8), n)
+    w = bytearray(wire_)
+    L = len(wire_) // n
+    w[1234 * L + 11 + 3] = 2  # bool byte of record 1234
+    gst, grec, _, gnd, gcons = gpu_decode(schema, 0, bytes(w), n, dev=gpu)
+    ost, orec, _, ond, ocons = oracle.decode(schema, 0, bytes(w), n)
+    assert gst.as_tuple() == ost.as_tuple() and gst.code == 3 and gst.record == 1234
+    assert (gnd, gcons) == (ond, ocons)
+    rec["f2"][777] = 2
+    gs = _gschema(schema)
+    from fbthrift_amd.serializer import AbortError, BinarySerializer as BS, CompactSerializer as CS
+
+    for ser in (BS, CS):
+        with pytest.raises(AbortError) as ei:
+            ser.serialize(gs, _t(rec.view(np.uint8), gpu), n)
+        assert ei.value.status.record == 777
+
+
+def _records(sname, n):
+    table = datagen.SCHEMAS[sname]
+    gen = {"mixed": datagen.gen_mixed, "nested": datagen.gen_nested}[sname]
+    vals = datagen.flatten_values(table, [gen(i) for i in range(n)])
+    schema = Schema.from_table(table)
+    return schema, helpers.pack(schema, vals, n)
+
+
+@pytest.mark.parametrize("sname,proto", [("mixed", 2), ("mixed", 0), ("nested", 0), ("nested", 2)])
+def test_config_shapes_roundtrip(gpu, sname, proto):
+    """Config 3 / 4 shapes (100k records): GPU encode == oracle encode; GPU
+    decode (indexed and unindexed) == oracle decode; decode∘encode = id."""
+    n = 100_000 if proto == (2 if sname == "mixed" else 0) else 20_000
+    schema, (rec, sarena, larena) = _records(sname, n)
+    gs = _gschema(schema)
+    st, want, woffs = oracle.encode(schema, proto, rec, n, sarena, larena)
+    assert st.code == 0
+    ser = _ser(proto)
+    wire, offs = ser.serialize(gs, _t(rec, gpu), n, _t(sarena, gpu), _t(larena, gpu))
+    assert bytes(_np(wire)) == want
+    assert np.array_equal(_np(offs).astype(np.uint64), woffs)
+    for indexed in (True, False):
+        if not indexed and n > 20_000:
+            continue  # the unindexed variable-length path is serial (one lane)
+        gst, grec, garena, gnd, gcons = gpu_decode(schema, proto, want, n,
+                                                   woffs if indexed else None, dev=gpu)
+        ost, orec, oarena, _, _ = oracle.decode(schema, proto, want, n,
+                                                offsets=woffs if indexed else None)
+        assert gst.code == 0 and gcons == len(want)
+        assert np.array_equal(grec, orec)
+        k = min(garena.size, oarena.size)
+        assert np.array_equal(garena[:k], oarena[:k])
