@@ -186,13 +186,16 @@ def main():
                    "records_per_gpu": n, "wire_bytes_per_gpu": wire_bytes,
                    "record_bytes": 72, "wire_bytes_per_record": L,
                    "parallelism": "dp%d (independent record shards, no collective)" % world},
-        "roofline": {"bound": "hbm", "kernel": "fixed_binary_decode_kernel",
+        "roofline": {"bound": "hbm", "kernel": "plan_binary_decode_kernel",
                      "achieved": round(dec_alg / dec_avg / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(dec_alg / dec_avg / 1e9 / HBM_PEAK_GBS, 4),
-                     "traffic": None,
+                     "traffic": pmc_traffic("plan_binary_decode_kernel", n),
                      "algorithmic_bytes_per_launch": dec_alg,
                      "avg_launch_ms": round(dec_avg * 1e3, 4),
-                     "encode": {"kernel": "fixed_binary_encode_kernel",
+                     "timing": "HIP events on the launch stream around the decode call "
+                               "(main kernel + 4 tiny bookkeeping kernels)",
+                     "copy_ceiling_GBps": copy_ceiling(dev),
+                     "encode": {"kernel": "plan_binary_encode_kernel",
                                 "achieved": round(enc_alg / enc_avg / 1e9, 1),
                                 "frac": round(enc_alg / enc_avg / 1e9 / HBM_PEAK_GBS, 4),
                                 "avg_launch_ms": round(enc_avg * 1e3, 4)}},
@@ -205,6 +208,40 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def copy_ceiling(dev, nbytes=4 << 30):
+    """Measured HBM copy ceiling on this GPU (torch device-to-device copy of
+    4 GiB: read + write bytes / time), reported beside the 8 TB/s spec."""
+    import torch
+
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / 5 / 1e3
+    del a, b
+    return round(2 * nbytes / t / 1e9, 1)
+
+
+def pmc_traffic(kernel, n):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    summary (profiles/pmc_latest.json, written by tools/pmc_summary.py from
+    separate --pmc passes, gfx950 FETCH_SIZE x2 correction applied), scaled to
+    this launch's record count; None when no summary exists."""
+    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)[kernel]
+        return int(d["hbm_bytes_per_record"] * n)
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def host_start(gs, recs, wire, back, n, L, dev):

@@ -1,0 +1,256 @@
+// k_plan_binary.hip — word-gather kernels for fixed-layout Binary records
+// (BASELINE config 1/2 {1..8: i64}: L = 89 wire bytes, S = 72 record bytes).
+//
+// Same semantics as k_fixed_binary.hip (canonical template match, first
+// non-canonical record latched for the serial fallback), organised so that
+// the HBM side of each kernel is a plain coalesced stream:
+//   decode: wire tile HBM -> LDS (16-byte loads); each lane then produces
+//           whole 8-byte words of the output records (word j of record r =
+//           const isset/padding bits | the values whose members live in that
+//           word, read from LDS with aligned dword reads + v_alignbyte +
+//           byte swap) and stores them coalesced, 512 bytes per wave store.
+//           No output tile, no LDS zero-fill, one barrier.
+//   encode: each lane loads whole 8-byte record words coalesced into
+//           registers, ORs the header + big-endian value bytes of the items
+//           they own into the LDS wire tile (ds_or_b32; items of one record
+//           are disjoint, the 2 dwords shared with a neighbour record are
+//           merged by the OR), then the tile goes LDS -> HBM with 16-byte
+//           stores.
+// LDS per workgroup is one wire tile (~23 KB) + the 1.5 KB plan, so 6
+// workgroups (24 waves) fit a CU; the HBM streams of the co-resident
+// workgroups overlap each other's LDS phases.
+#include "tgpu_internal.h"
+
+namespace tgpu {
+namespace {
+
+constexpr uint32_t kT = 256;  // records per tile; 256 * L is a multiple of 16
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+__device__ __forceinline__ uint32_t wire_region_bytes(uint32_t L) {
+  return ((kT * L + 16 + 16 + 15) >> 4) << 4;  // + phase + over-read/-write slack
+}
+
+__device__ __forceinline__ void copy_plan(FixedPlan* dst, const FixedPlan* src) {
+  constexpr uint32_t n16 = (uint32_t)(sizeof(FixedPlan) / 16);
+  static_assert(sizeof(FixedPlan) % 16 == 0, "plan must be a multiple of 16 bytes");
+  for (uint32_t i = threadIdx.x; i < n16; i += kBlock) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+}
+
+__global__ __launch_bounds__(kBlock) void plan_binary_decode_kernel(
+    const FixedPlan* __restrict__ pp, const uint8_t* __restrict__ in, uint64_t n,
+    unsigned long long* __restrict__ out, DevResult* __restrict__ res) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t L = pp->wire_len, Q = pp->n_words;
+  const uint64_t tile0 = (uint64_t)blockIdx.x * kT;
+  const uint32_t nrec = (uint32_t)min((uint64_t)kT, n - tile0);
+  FixedPlan* P = (FixedPlan*)(smem + wire_region_bytes(L));
+
+  // stage the wire tile (16-byte phase of the stream preserved)
+  const uint8_t* g = in + tile0 * L;
+  const uint32_t sh = (uint32_t)((uintptr_t)g & 15);
+  {
+    const uint4* src = (const uint4*)(g - sh);
+    const uint32_t nvec = (nrec * L + sh + 15) >> 4;
+    for (uint32_t i = threadIdx.x; i < nvec; i += kBlock) ((uint4*)smem)[i] = src[i];
+  }
+  copy_plan(P, pp);
+  __syncthreads();
+
+  const uint32_t* w32 = (const uint32_t*)smem;
+  const uint32_t total = nrec * Q;
+  uint32_t r = threadIdx.x / Q, j = threadIdx.x - r * Q;
+  const uint32_t sr = kBlock / Q, sj = kBlock - sr * Q;
+  unsigned long long* o = out + tile0 * Q;
+  for (uint32_t q = threadIdx.x; q < total; q += kBlock) {
+    const PlanWord w = P->words[j];
+    unsigned long long v = w.const_bits;
+    bool ok = true;
+    const uint32_t base = sh + r * L;
+    for (uint32_t k = 0; k < w.n_items; ++k) {
+      const PlanItem it = P->items[w.first_item + k];
+      const uint32_t a = base + it.wire_off;
+      const uint32_t d = a >> 2, s = a & 3;
+      const uint32_t W0 = w32[d], W1 = w32[d + 1], W2 = w32[d + 2], W3 = w32[d + 3];
+      const uint32_t G0 = __builtin_amdgcn_alignbyte(W1, W0, s);
+      const uint32_t G1 = __builtin_amdgcn_alignbyte(W2, W1, s);
+      const uint32_t G2 = __builtin_amdgcn_alignbyte(W3, W2, s);
+      const uint32_t h = it.hdr_len;
+      if (h) {
+        const uint32_t mask = h >= 4 ? 0xffffffffu : ((1u << (8 * h)) - 1);
+        ok &= ((G0 ^ it.hdr) & mask) == 0;
+      }
+      if (it.width) {
+        const uint32_t X0 = __builtin_amdgcn_alignbyte(G1, G0, h);
+        const uint32_t X1 = __builtin_amdgcn_alignbyte(G2, G1, h);
+        unsigned long long val;
+        switch (it.width) {
+          case 8: val = ((unsigned long long)bswap32(X0) << 32) | bswap32(X1); break;
+          case 4: val = bswap32(X0); break;
+          case 2: val = bswap32(X0) >> 16; break;
+          default:
+            val = X0 & 0xff;
+            if (it.is_bool) ok &= val <= 1;  // readBool: byte >= 2 throws
+            break;
+        }
+        v |= val << (8 * it.dst);
+      }
+    }
+    o[q] = v;
+    if (!ok) atomicMin(&res->first_irregular, (unsigned long long)(tile0 + r));
+    r += sr;
+    j += sj;
+    if (j >= Q) {
+      j -= Q;
+      ++r;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void plan_binary_encode_kernel(
+    const FixedPlan* __restrict__ pp, const unsigned long long* __restrict__ recs, uint64_t n,
+    uint32_t value_words, uint8_t* __restrict__ out, uint64_t* __restrict__ offsets,
+    DevResult* __restrict__ res) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t L = pp->wire_len, Q = pp->n_words;
+  const uint64_t tile0 = (uint64_t)blockIdx.x * kT;
+  const uint32_t nrec = (uint32_t)min((uint64_t)kT, n - tile0);
+  const uint32_t wreg = wire_region_bytes(L);
+  FixedPlan* P = (FixedPlan*)(smem + wreg);
+  const uint32_t total = nrec * Q;
+
+  // 1. record words -> registers (coalesced 8-byte loads, issued first)
+  unsigned long long vals[kMaxPlanWords];
+  {
+    uint32_t j = threadIdx.x % Q;
+    const uint32_t sj = kBlock % Q;
+#pragma unroll
+    for (int m = 0; m < kMaxPlanWords; ++m) {
+      const uint32_t q = threadIdx.x + kBlock * m;
+      vals[m] = 0;
+      if ((uint32_t)m < Q && q < total && ((value_words >> j) & 1)) vals[m] = recs[tile0 * Q + q];
+      j += sj;
+      if (j >= Q) j -= Q;
+    }
+  }
+  // 2. zero the wire tile, plan -> LDS
+  uint8_t* gout = out + tile0 * L;
+  const uint32_t osh = (uint32_t)((uintptr_t)gout & 15);
+  {
+    const uint4 z = {0u, 0u, 0u, 0u};
+    for (uint32_t i = threadIdx.x; i < (wreg >> 4); i += kBlock) ((uint4*)smem)[i] = z;
+  }
+  copy_plan(P, pp);
+  __syncthreads();
+
+  // 3. OR each owned item's wire bytes into the tile
+  uint32_t* w32 = (uint32_t*)smem;
+  bool bad_bool = false;
+  uint32_t bad_rec = 0;
+  {
+    uint32_t r = threadIdx.x / Q, j = threadIdx.x - r * Q;
+    const uint32_t sr = kBlock / Q, sj = kBlock - sr * Q;
+#pragma unroll
+    for (int m = 0; m < kMaxPlanWords; ++m) {
+      const uint32_t q = threadIdx.x + kBlock * m;
+      if ((uint32_t)m < Q && q < total) {
+        const PlanWord w = P->words[j];
+        const unsigned long long v = vals[m];
+        const uint32_t base = osh + r * L;
+        for (uint32_t k = 0; k < w.n_items; ++k) {
+          const PlanItem it = P->items[w.first_item + k];
+          const uint32_t h = it.hdr_len;
+          const unsigned long long raw = v >> (8 * it.dst);
+          unsigned long long vbe;  // big-endian value bytes, first byte lowest
+          switch (it.width) {
+            case 8:
+              vbe = ((unsigned long long)bswap32((uint32_t)raw) << 32) |
+                    bswap32((uint32_t)(raw >> 32));
+              break;
+            case 4: vbe = bswap32((uint32_t)raw); break;
+            case 2: vbe = bswap32((uint32_t)(raw & 0xffff)) >> 16; break;
+            case 1:
+              vbe = raw & 0xff;
+              if (it.is_bool && vbe > 1) {  // validate_bool
+                bad_bool = true;
+                bad_rec = r;
+              }
+              break;
+            default: vbe = 0; break;
+          }
+          const unsigned long long Flo = (unsigned long long)it.hdr | (vbe << (8 * h));
+          const unsigned long long Fhi = h ? (vbe >> (64 - 8 * h)) : 0;
+          const uint32_t a = base + it.wire_off;
+          const uint32_t d = a >> 2, s = a & 3;
+          const unsigned long long Hlo = Flo << (8 * s);
+          const unsigned long long Hhi = (Fhi << (8 * s)) | (s ? (Flo >> (64 - 8 * s)) : 0);
+          const uint32_t nb = s + h + it.width;
+          atomicOr(&w32[d], (uint32_t)Hlo);
+          if (nb > 4) atomicOr(&w32[d + 1], (uint32_t)(Hlo >> 32));
+          if (nb > 8) atomicOr(&w32[d + 2], (uint32_t)Hhi);
+          if (nb > 12) atomicOr(&w32[d + 3], (uint32_t)(Hhi >> 32));
+        }
+      }
+      r += sr;
+      j += sj;
+      if (j >= Q) {
+        j -= Q;
+        ++r;
+      }
+    }
+  }
+  if (bad_bool) atomicMin(&res->first_fail, (unsigned long long)(tile0 + bad_rec));
+  if (offsets) {
+    for (uint32_t i = threadIdx.x; i < nrec; i += kBlock) offsets[tile0 + i] = (tile0 + i) * L;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) offsets[n] = n * L;
+  }
+  __syncthreads();
+
+  // 4. wire tile -> HBM (full 16-byte chunks; byte stores at the tile edges)
+  {
+    uint8_t* base = gout - osh;
+    const uint32_t end = osh + nrec * L;
+    const uint32_t nvec = (end + 15) >> 4;
+    for (uint32_t i = threadIdx.x; i < nvec; i += kBlock) {
+      const uint32_t lo = i << 4, hi = lo + 16;
+      if (lo >= osh && hi <= end) {
+        ((uint4*)base)[i] = ((const uint4*)smem)[i];
+      } else {
+        for (uint32_t b = (lo < osh ? osh : lo); b < (hi < end ? hi : end); ++b) base[b] = smem[b];
+      }
+    }
+  }
+}
+
+inline uint32_t host_lds_bytes(const FixedPlan& p) {
+  return (((kT * p.wire_len + 16 + 16 + 15) >> 4) << 4) + (uint32_t)sizeof(FixedPlan);
+}
+
+}  // namespace
+
+hipError_t launch_plan_binary_decode(const FixedPlan* p, const FixedPlan* d_p, const uint8_t* in,
+                                     uint64_t n, uint8_t* out, DevResult* res,
+                                     hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const uint64_t blocks = (n + kT - 1) / kT;
+  hipLaunchKernelGGL(plan_binary_decode_kernel, dim3((uint32_t)blocks), dim3(kBlock),
+                     host_lds_bytes(*p), stream, d_p, in, n, (unsigned long long*)out, res);
+  return hipGetLastError();
+}
+
+hipError_t launch_plan_binary_encode(const FixedPlan* p, const FixedPlan* d_p,
+                                     const uint8_t* recs, uint64_t n, uint8_t* out,
+                                     uint64_t* offsets, DevResult* res, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  uint32_t value_words = 0;
+  for (uint32_t j = 0; j < p->n_words; ++j)
+    if (p->words[j].has_value) value_words |= 1u << j;
+  const uint64_t blocks = (n + kT - 1) / kT;
+  hipLaunchKernelGGL(plan_binary_encode_kernel, dim3((uint32_t)blocks), dim3(kBlock),
+                     host_lds_bytes(*p), stream, d_p, (const unsigned long long*)recs, n,
+                     value_words, out, offsets, res);
+  return hipGetLastError();
+}
+
+}  // namespace tgpu

@@ -22,6 +22,9 @@ struct tgpu_schema {
   bool fixed_binary = false;
   FixedTemplate tmpl{};
   FixedTemplate* d_tmpl = nullptr;
+  bool has_plan = false;  // word-gather form of tmpl (S % 8 == 0)
+  FixedPlan plan{};
+  FixedPlan* d_plan = nullptr;
 };
 
 struct tgpu_context {
@@ -172,6 +175,45 @@ bool build_template(const tgpu_schema& sc, uint32_t si, uint32_t base, FixedTemp
   return true;
 }
 
+// Regroups the template by 8-byte word of the record layout (FixedPlan).
+bool build_plan(const FixedTemplate& t, FixedPlan& p) {
+  if (t.record_size % 8 || t.record_size / 8 > (uint32_t)kMaxPlanWords || t.record_size == 0)
+    return false;
+  p = FixedPlan{};
+  p.wire_len = t.wire_len;
+  p.n_words = t.record_size / 8;
+  std::vector<std::vector<PlanItem>> bucket(p.n_words);
+  for (uint32_t i = 0; i < t.n_items; ++i) {
+    const TemplateItem& ti = t.items[i];
+    PlanItem pi{};
+    pi.wire_off = ti.wire_off;
+    pi.hdr_len = ti.hdr_len;
+    pi.width = ti.width;
+    pi.hdr = ti.hdr;
+    pi.is_bool = ti.is_bool;
+    uint32_t j = p.n_words - 1;
+    if (ti.width) {
+      j = ti.member_off / 8;
+      pi.dst = (uint8_t)(ti.member_off % 8);
+      if (pi.dst + ti.width > 8) return false;
+    }
+    bucket[j].push_back(pi);
+  }
+  for (uint32_t k = 0; k < t.n_isset; ++k)
+    p.words[t.isset_off[k] / 8].const_bits |= 1ull << (8 * (t.isset_off[k] % 8));
+  uint32_t at = 0;
+  for (uint32_t j = 0; j < p.n_words; ++j) {
+    p.words[j].first_item = (uint16_t)at;
+    p.words[j].n_items = (uint8_t)bucket[j].size();
+    for (const PlanItem& pi : bucket[j]) {
+      p.words[j].has_value |= pi.width ? 1 : 0;
+      p.items[at++] = pi;
+    }
+  }
+  p.n_items = at;
+  return true;
+}
+
 void classify(int code, int32_t* exc, int32_t* tp) {
   int32_t e = TGPU_EXC_RUNTIME, t = 0;
   switch (code) {
@@ -303,6 +345,14 @@ int tgpu_schema_create(const tgpu_struct_desc* structs, uint32_t n_structs,
       return TGPU_ERR_HIP;
     }
     s->fixed_binary = true;
+    if (build_plan(t, s->plan)) {
+      if (hipMalloc(&s->d_plan, sizeof(FixedPlan)) != hipSuccess ||
+          hipMemcpy(s->d_plan, &s->plan, sizeof(FixedPlan), hipMemcpyHostToDevice) != hipSuccess) {
+        tgpu_schema_destroy(s);
+        return TGPU_ERR_HIP;
+      }
+      s->has_plan = true;
+    }
   }
   *out = s;
   return TGPU_OK;
@@ -313,6 +363,7 @@ void tgpu_schema_destroy(tgpu_schema* s) {
   if (s->d_structs) (void)hipFree(s->d_structs);
   if (s->d_fields) (void)hipFree(s->d_fields);
   if (s->d_tmpl) (void)hipFree(s->d_tmpl);
+  if (s->d_plan) (void)hipFree(s->d_plan);
   delete s;
 }
 
@@ -402,8 +453,12 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   if (protocol == TGPU_PROTOCOL_BINARY && schema->fixed_binary &&
       n * schema->tmpl.wire_len <= out_capacity) {
     fixed = schema->tmpl.wire_len;
-    if (e == hipSuccess)
-      e = launch_fixed_binary_encode(&schema->tmpl, schema->d_tmpl, a.recs, n, a.out, out_offsets, ctx->d_res, s);
+    if (e == hipSuccess && schema->has_plan && ((uintptr_t)records & 7) == 0)
+      e = launch_plan_binary_encode(&schema->plan, schema->d_plan, a.recs, n, a.out, out_offsets,
+                                    ctx->d_res, s);
+    else if (e == hipSuccess)
+      e = launch_fixed_binary_encode(&schema->tmpl, schema->d_tmpl, a.recs, n, a.out,
+                                     out_offsets, ctx->d_res, s);
   } else {
     const uint64_t nb = (n + 255) / 256;
     int rc = ensure_workspace(ctx, n);
@@ -517,8 +572,11 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   if (n && protocol == TGPU_PROTOCOL_BINARY && schema->fixed_binary && !offsets &&
       in_len >= n * (uint64_t)schema->tmpl.wire_len) {
     fixed = schema->tmpl.wire_len;
-    if (e == hipSuccess)
-      e = launch_fixed_binary_decode(&schema->tmpl, schema->d_tmpl, a.in, n, a.recs, ctx->d_res, s);
+    if (e == hipSuccess && schema->has_plan && ((uintptr_t)records & 7) == 0)
+      e = launch_plan_binary_decode(&schema->plan, schema->d_plan, a.in, n, a.recs, ctx->d_res, s);
+    else if (e == hipSuccess)
+      e = launch_fixed_binary_decode(&schema->tmpl, schema->d_tmpl, a.in, n, a.recs, ctx->d_res,
+                                     s);
     a.offs = ctx->d_offs;
     a.check_index = 0;
     if (e == hipSuccess) e = launch_serial_decode(a, protocol, true, fixed, s);

@@ -46,6 +46,37 @@ struct FixedTemplate {
   TemplateItem items[kMaxTemplateItems];
 };
 
+// The same template regrouped by output 8-byte word of the record layout
+// (records with S % 8 == 0): word j = const_bits (isset bytes, zero padding)
+// OR the values of items[first .. first+n) placed at byte `dst`. Items with
+// width 0 (STOP, nested struct headers) ride on the last word; each item is
+// owned by exactly one word, so every header byte is checked exactly once.
+constexpr int kMaxPlanWords = 20;  // S <= 160
+struct PlanItem {
+  uint16_t wire_off;
+  uint8_t hdr_len;
+  uint8_t width;
+  uint32_t hdr;
+  uint8_t dst;  // byte offset of the value inside its 8-byte word
+  uint8_t is_bool;
+  uint8_t pad[2];
+};
+struct PlanWord {
+  unsigned long long const_bits;
+  uint16_t first_item;
+  uint8_t n_items;
+  uint8_t has_value;  // at least one item with width > 0 (encode must load it)
+  uint8_t pad[4];
+};
+struct FixedPlan {
+  uint32_t wire_len;   // L
+  uint32_t n_words;    // Q = S / 8
+  uint32_t n_items;
+  uint32_t pad;
+  PlanWord words[kMaxPlanWords];
+  PlanItem items[kMaxTemplateItems];
+};
+
 // Device-side result slot of a context (one per in-flight call).
 struct DevResult {
   unsigned long long first_fail;       // first failing record (UINT64_MAX: none)
@@ -101,6 +132,14 @@ hipError_t launch_fixed_binary_encode(const FixedTemplate* t, const FixedTemplat
                                       const uint8_t* recs, uint64_t n, uint8_t* out,
                                       uint64_t* offsets, DevResult* res,
                                       hipStream_t stream);
+// Word-gather variants (S % 8 == 0, record buffer 8-byte aligned).
+hipError_t launch_plan_binary_decode(const FixedPlan* p, const FixedPlan* d_p,
+                                     const uint8_t* in, uint64_t n, uint8_t* out,
+                                     DevResult* res, hipStream_t stream);
+hipError_t launch_plan_binary_encode(const FixedPlan* p, const FixedPlan* d_p,
+                                     const uint8_t* recs, uint64_t n, uint8_t* out,
+                                     uint64_t* offsets, DevResult* res,
+                                     hipStream_t stream);
 hipError_t launch_general_decode(const DecodeArgs& a, int protocol,
                                  hipStream_t stream);
 hipError_t launch_serial_decode(const DecodeArgs& a, int protocol,
