@@ -19,33 +19,74 @@
 // LDS per workgroup is one wire tile (~23 KB) + the 1.5 KB plan, so 6
 // workgroups (24 waves) fit a CU; the HBM streams of the co-resident
 // workgroups overlap each other's LDS phases.
+#include <cstdio>
+#include <cstdlib>
+
 #include "tgpu_internal.h"
 
 namespace tgpu {
 namespace {
 
-constexpr uint32_t kT = 256;  // records per tile; 256 * L is a multiple of 16
-
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
-__device__ __forceinline__ uint32_t wire_region_bytes(uint32_t L) {
-  return ((kT * L + 16 + 16 + 15) >> 4) << 4;  // + phase + over-read/-write slack
+// LDS bytes of a T-record wire tile: + 16-byte phase + over-read/-write slack,
+// rounded to whole rounds of T x 16-byte staging chunks (LDS-DMA writes a
+// full round).
+__host__ __device__ __forceinline__ uint32_t wire_region(uint32_t T, uint32_t L) {
+  return (T * L + 32 + 16 * T - 1) / (16 * T) * (16 * T);
 }
 
-__device__ __forceinline__ void copy_plan(FixedPlan* dst, const FixedPlan* src) {
-  constexpr uint32_t n16 = (uint32_t)(sizeof(FixedPlan) / 16);
-  static_assert(sizeof(FixedPlan) % 16 == 0, "plan must be a multiple of 16 bytes");
-  for (uint32_t i = threadIdx.x; i < n16; i += kBlock) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+
+// Output word j of the record whose wire bytes start at LDS byte `base`.
+__device__ __forceinline__ unsigned long long decode_word(const FixedPlan* P,
+                                                          const uint32_t* w32, uint32_t base,
+                                                          uint32_t j, bool& ok) {
+  const PlanWord w = P->words[j];
+  unsigned long long v = w.const_bits;
+  for (uint32_t k = 0; k < w.n_items; ++k) {
+    const PlanItem it = P->items[w.first_item + k];
+    const uint32_t a = base + it.wire_off;
+    const uint32_t d = a >> 2, s = a & 3;
+    const uint32_t W0 = w32[d], W1 = w32[d + 1], W2 = w32[d + 2], W3 = w32[d + 3];
+    const uint32_t G0 = __builtin_amdgcn_alignbyte(W1, W0, s);
+    const uint32_t G1 = __builtin_amdgcn_alignbyte(W2, W1, s);
+    const uint32_t G2 = __builtin_amdgcn_alignbyte(W3, W2, s);
+    const uint32_t h = it.hdr_len;
+    if (h) {
+      const uint32_t mask = h >= 4 ? 0xffffffffu : ((1u << (8 * h)) - 1);
+      ok &= ((G0 ^ it.hdr) & mask) == 0;
+    }
+    if (it.width) {
+      const uint32_t X0 = __builtin_amdgcn_alignbyte(G1, G0, h);
+      const uint32_t X1 = __builtin_amdgcn_alignbyte(G2, G1, h);
+      unsigned long long val;
+      switch (it.width) {
+        case 8: val = ((unsigned long long)bswap32(X0) << 32) | bswap32(X1); break;
+        case 4: val = bswap32(X0); break;
+        case 2: val = bswap32(X0) >> 16; break;
+        default:
+          val = X0 & 0xff;
+          if (it.is_bool) ok &= val <= 1;  // readBool: byte >= 2 throws
+          break;
+      }
+      v |= val << (8 * it.dst);
+    }
+  }
+  return v;
 }
 
-__global__ __launch_bounds__(kBlock) void plan_binary_decode_kernel(
+// T records (= threads) per tile. kGlds: stage through LDS-DMA
+// (global_load_lds_dwordx4) instead of registers. kPair: 16-byte stores of
+// two consecutive words. kNT: non-temporal stores (output is never re-read).
+template <uint32_t T, bool kGlds, bool kPair, bool kNT>
+__global__ __launch_bounds__(T) void plan_binary_decode_kernel(
     const FixedPlan* __restrict__ pp, const uint8_t* __restrict__ in, uint64_t n,
     unsigned long long* __restrict__ out, DevResult* __restrict__ res) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t L = pp->wire_len, Q = pp->n_words;
-  const uint64_t tile0 = (uint64_t)blockIdx.x * kT;
-  const uint32_t nrec = (uint32_t)min((uint64_t)kT, n - tile0);
-  FixedPlan* P = (FixedPlan*)(smem + wire_region_bytes(L));
+  const uint64_t tile0 = (uint64_t)blockIdx.x * T;
+  const uint32_t nrec = (uint32_t)min((uint64_t)T, n - tile0);
+  FixedPlan* P = (FixedPlan*)(smem + wire_region(T, L));
 
   // stage the wire tile (16-byte phase of the stream preserved)
   const uint8_t* g = in + tile0 * L;
@@ -53,70 +94,83 @@ __global__ __launch_bounds__(kBlock) void plan_binary_decode_kernel(
   {
     const uint4* src = (const uint4*)(g - sh);
     const uint32_t nvec = (nrec * L + sh + 15) >> 4;
-    for (uint32_t i = threadIdx.x; i < nvec; i += kBlock) ((uint4*)smem)[i] = src[i];
+    if (kGlds) {
+      const uint32_t wave = threadIdx.x >> 6;
+      for (uint32_t k = 0; k * T < nvec; ++k) {
+        const uint32_t i = k * T + threadIdx.x;
+        const uint4* s = src + (i < nvec ? i : nvec - 1);  // clamp: never past the stream
+        __builtin_amdgcn_global_load_lds(
+            (const void*)s,
+            (__attribute__((address_space(3))) void*)(smem + (size_t)(k * T + wave * 64) * 16), 16,
+            0, 0);
+      }
+    } else {
+      for (uint32_t i = threadIdx.x; i < nvec; i += T) ((uint4*)smem)[i] = src[i];
+    }
   }
-  copy_plan(P, pp);
+  for (uint32_t i = threadIdx.x; i < (uint32_t)(sizeof(FixedPlan) / 16); i += T)
+    ((uint4*)P)[i] = ((const uint4*)pp)[i];
   __syncthreads();
 
   const uint32_t* w32 = (const uint32_t*)smem;
   const uint32_t total = nrec * Q;
-  uint32_t r = threadIdx.x / Q, j = threadIdx.x - r * Q;
-  const uint32_t sr = kBlock / Q, sj = kBlock - sr * Q;
   unsigned long long* o = out + tile0 * Q;
-  for (uint32_t q = threadIdx.x; q < total; q += kBlock) {
-    const PlanWord w = P->words[j];
-    unsigned long long v = w.const_bits;
-    bool ok = true;
-    const uint32_t base = sh + r * L;
-    for (uint32_t k = 0; k < w.n_items; ++k) {
-      const PlanItem it = P->items[w.first_item + k];
-      const uint32_t a = base + it.wire_off;
-      const uint32_t d = a >> 2, s = a & 3;
-      const uint32_t W0 = w32[d], W1 = w32[d + 1], W2 = w32[d + 2], W3 = w32[d + 3];
-      const uint32_t G0 = __builtin_amdgcn_alignbyte(W1, W0, s);
-      const uint32_t G1 = __builtin_amdgcn_alignbyte(W2, W1, s);
-      const uint32_t G2 = __builtin_amdgcn_alignbyte(W3, W2, s);
-      const uint32_t h = it.hdr_len;
-      if (h) {
-        const uint32_t mask = h >= 4 ? 0xffffffffu : ((1u << (8 * h)) - 1);
-        ok &= ((G0 ^ it.hdr) & mask) == 0;
-      }
-      if (it.width) {
-        const uint32_t X0 = __builtin_amdgcn_alignbyte(G1, G0, h);
-        const uint32_t X1 = __builtin_amdgcn_alignbyte(G2, G1, h);
-        unsigned long long val;
-        switch (it.width) {
-          case 8: val = ((unsigned long long)bswap32(X0) << 32) | bswap32(X1); break;
-          case 4: val = bswap32(X0); break;
-          case 2: val = bswap32(X0) >> 16; break;
-          default:
-            val = X0 & 0xff;
-            if (it.is_bool) ok &= val <= 1;  // readBool: byte >= 2 throws
-            break;
-        }
-        v |= val << (8 * it.dst);
+  if (!kPair) {
+    uint32_t r = threadIdx.x / Q, j = threadIdx.x - r * Q;
+    const uint32_t sr = T / Q, sj = T - sr * Q;
+    for (uint32_t q = threadIdx.x; q < total; q += T) {
+      bool ok = true;
+      const unsigned long long v = decode_word(P, w32, sh + r * L, j, ok);
+      if (kNT) __builtin_nontemporal_store(v, o + q);
+      else o[q] = v;
+      if (!ok) atomicMin(&res->first_irregular, (unsigned long long)(tile0 + r));
+      r += sr;
+      j += sj;
+      if (j >= Q) {
+        j -= Q;
+        ++r;
       }
     }
-    o[q] = v;
-    if (!ok) atomicMin(&res->first_irregular, (unsigned long long)(tile0 + r));
-    r += sr;
-    j += sj;
-    if (j >= Q) {
-      j -= Q;
-      ++r;
+  } else {
+    const uint32_t q0 = 2 * threadIdx.x;
+    uint32_t r = q0 / Q, j = q0 - r * Q;
+    const uint32_t sr = (2 * T) / Q, sj = 2 * T - sr * Q;
+    for (uint32_t q = q0; q < total; q += 2 * T) {
+      bool ok0 = true, ok1 = true;
+      const unsigned long long v0 = decode_word(P, w32, sh + r * L, j, ok0);
+      const uint32_t r1 = j + 1 == Q ? r + 1 : r, j1 = j + 1 == Q ? 0 : j + 1;
+      if (q + 1 < total) {
+        const unsigned long long v1 = decode_word(P, w32, sh + r1 * L, j1, ok1);
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        u64x2 pr = {v0, v1};
+        if (kNT) __builtin_nontemporal_store(pr, (u64x2*)(o + q));
+        else *(u64x2*)(o + q) = pr;
+      } else {
+        o[q] = v0;
+      }
+      if (!ok0) atomicMin(&res->first_irregular, (unsigned long long)(tile0 + r));
+      if (!ok1) atomicMin(&res->first_irregular, (unsigned long long)(tile0 + r1));
+      r += sr;
+      j += sj;
+      if (j >= Q) {
+        j -= Q;
+        ++r;
+      }
     }
   }
 }
 
-__global__ __launch_bounds__(kBlock) void plan_binary_encode_kernel(
+
+template <uint32_t T, bool kNT>
+__global__ __launch_bounds__(T) void plan_binary_encode_kernel(
     const FixedPlan* __restrict__ pp, const unsigned long long* __restrict__ recs, uint64_t n,
     uint32_t value_words, uint8_t* __restrict__ out, uint64_t* __restrict__ offsets,
     DevResult* __restrict__ res) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t L = pp->wire_len, Q = pp->n_words;
-  const uint64_t tile0 = (uint64_t)blockIdx.x * kT;
-  const uint32_t nrec = (uint32_t)min((uint64_t)kT, n - tile0);
-  const uint32_t wreg = wire_region_bytes(L);
+  const uint64_t tile0 = (uint64_t)blockIdx.x * T;
+  const uint32_t nrec = (uint32_t)min((uint64_t)T, n - tile0);
+  const uint32_t wreg = wire_region(T, L);
   FixedPlan* P = (FixedPlan*)(smem + wreg);
   const uint32_t total = nrec * Q;
 
@@ -124,12 +178,13 @@ __global__ __launch_bounds__(kBlock) void plan_binary_encode_kernel(
   unsigned long long vals[kMaxPlanWords];
   {
     uint32_t j = threadIdx.x % Q;
-    const uint32_t sj = kBlock % Q;
+    const uint32_t sj = T % Q;
 #pragma unroll
     for (int m = 0; m < kMaxPlanWords; ++m) {
-      const uint32_t q = threadIdx.x + kBlock * m;
+      const uint32_t q = threadIdx.x + T * m;
       vals[m] = 0;
-      if ((uint32_t)m < Q && q < total && ((value_words >> j) & 1)) vals[m] = recs[tile0 * Q + q];
+      if ((uint32_t)m < Q && q < total && ((value_words >> j) & 1))
+        vals[m] = kNT ? __builtin_nontemporal_load(recs + tile0 * Q + q) : recs[tile0 * Q + q];
       j += sj;
       if (j >= Q) j -= Q;
     }
@@ -139,9 +194,10 @@ __global__ __launch_bounds__(kBlock) void plan_binary_encode_kernel(
   const uint32_t osh = (uint32_t)((uintptr_t)gout & 15);
   {
     const uint4 z = {0u, 0u, 0u, 0u};
-    for (uint32_t i = threadIdx.x; i < (wreg >> 4); i += kBlock) ((uint4*)smem)[i] = z;
+    for (uint32_t i = threadIdx.x; i < (wreg >> 4); i += T) ((uint4*)smem)[i] = z;
   }
-  copy_plan(P, pp);
+  for (uint32_t i = threadIdx.x; i < (uint32_t)(sizeof(FixedPlan) / 16); i += T)
+    ((uint4*)P)[i] = ((const uint4*)pp)[i];
   __syncthreads();
 
   // 3. OR each owned item's wire bytes into the tile
@@ -150,10 +206,10 @@ __global__ __launch_bounds__(kBlock) void plan_binary_encode_kernel(
   uint32_t bad_rec = 0;
   {
     uint32_t r = threadIdx.x / Q, j = threadIdx.x - r * Q;
-    const uint32_t sr = kBlock / Q, sj = kBlock - sr * Q;
+    const uint32_t sr = T / Q, sj = T - sr * Q;
 #pragma unroll
     for (int m = 0; m < kMaxPlanWords; ++m) {
-      const uint32_t q = threadIdx.x + kBlock * m;
+      const uint32_t q = threadIdx.x + T * m;
       if ((uint32_t)m < Q && q < total) {
         const PlanWord w = P->words[j];
         const unsigned long long v = vals[m];
@@ -202,7 +258,7 @@ __global__ __launch_bounds__(kBlock) void plan_binary_encode_kernel(
   }
   if (bad_bool) atomicMin(&res->first_fail, (unsigned long long)(tile0 + bad_rec));
   if (offsets) {
-    for (uint32_t i = threadIdx.x; i < nrec; i += kBlock) offsets[tile0 + i] = (tile0 + i) * L;
+    for (uint32_t i = threadIdx.x; i < nrec; i += T) offsets[tile0 + i] = (tile0 + i) * L;
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) offsets[n] = n * L;
   }
   __syncthreads();
@@ -212,10 +268,12 @@ __global__ __launch_bounds__(kBlock) void plan_binary_encode_kernel(
     uint8_t* base = gout - osh;
     const uint32_t end = osh + nrec * L;
     const uint32_t nvec = (end + 15) >> 4;
-    for (uint32_t i = threadIdx.x; i < nvec; i += kBlock) {
+    for (uint32_t i = threadIdx.x; i < nvec; i += T) {
       const uint32_t lo = i << 4, hi = lo + 16;
       if (lo >= osh && hi <= end) {
-        ((uint4*)base)[i] = ((const uint4*)smem)[i];
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        if (kNT) __builtin_nontemporal_store(((const u32x4*)smem)[i], (u32x4*)base + i);
+        else ((uint4*)base)[i] = ((const uint4*)smem)[i];
       } else {
         for (uint32_t b = (lo < osh ? osh : lo); b < (hi < end ? hi : end); ++b) base[b] = smem[b];
       }
@@ -223,8 +281,46 @@ __global__ __launch_bounds__(kBlock) void plan_binary_encode_kernel(
   }
 }
 
-inline uint32_t host_lds_bytes(const FixedPlan& p) {
-  return (((kT * p.wire_len + 16 + 16 + 15) >> 4) << 4) + (uint32_t)sizeof(FixedPlan);
+// ---- variant selection -----------------------------------------------------
+// Defaults are the tuned configuration ("fixed-layout kernels");
+// TGPU_PLAN_DECODE="T,glds,pair,nt" / TGPU_PLAN_ENCODE="T,nt" override them for
+// tuning runs (tools/kbench.py).
+struct DecVariant { uint32_t T; int glds, pair, nt; };
+struct EncVariant { uint32_t T; int nt; };
+
+DecVariant dec_variant() {
+  DecVariant v{256, 0, 0, 0};
+  if (const char* s = getenv("TGPU_PLAN_DECODE")) {
+    unsigned t = 256;
+    int g = 0, p = 0, nt = 0;
+    if (sscanf(s, "%u,%d,%d,%d", &t, &g, &p, &nt) == 4) v = DecVariant{t, g, p, nt};
+  }
+  return v;
+}
+EncVariant enc_variant() {
+  EncVariant v{256, 0};
+  if (const char* s = getenv("TGPU_PLAN_ENCODE")) {
+    unsigned t = 256;
+    int nt = 0;
+    if (sscanf(s, "%u,%d", &t, &nt) == 2) v = EncVariant{t, nt};
+  }
+  return v;
+}
+
+template <uint32_t T>
+hipError_t launch_dec_T(const DecVariant& v, uint32_t lds, uint64_t blocks, hipStream_t stream,
+                        const FixedPlan* d_p, const uint8_t* in, uint64_t n,
+                        unsigned long long* out, DevResult* res) {
+#define TGPU_DEC(G, P_, N)                                                                   \
+  if (v.glds == G && v.pair == P_ && v.nt == N) {                                            \
+    hipLaunchKernelGGL((plan_binary_decode_kernel<T, G, P_, N>), dim3((uint32_t)blocks),     \
+                       dim3(T), lds, stream, d_p, in, n, out, res);                          \
+    return hipGetLastError();                                                                \
+  }
+  TGPU_DEC(0, 0, 0) TGPU_DEC(1, 0, 0) TGPU_DEC(0, 1, 0) TGPU_DEC(1, 1, 0)
+  TGPU_DEC(0, 0, 1) TGPU_DEC(1, 0, 1) TGPU_DEC(0, 1, 1) TGPU_DEC(1, 1, 1)
+#undef TGPU_DEC
+  return hipErrorInvalidValue;
 }
 
 }  // namespace
@@ -233,24 +329,40 @@ hipError_t launch_plan_binary_decode(const FixedPlan* p, const FixedPlan* d_p, c
                                      uint64_t n, uint8_t* out, DevResult* res,
                                      hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  const uint64_t blocks = (n + kT - 1) / kT;
-  hipLaunchKernelGGL(plan_binary_decode_kernel, dim3((uint32_t)blocks), dim3(kBlock),
-                     host_lds_bytes(*p), stream, d_p, in, n, (unsigned long long*)out, res);
-  return hipGetLastError();
+  const DecVariant v = dec_variant();
+  DecVariant use = v;
+  if (((uintptr_t)out & 15) != 0) use.pair = 0;  // 16-byte stores need 16-byte records base
+  const uint64_t blocks = (n + use.T - 1) / use.T;
+  const uint32_t lds = wire_region(use.T, p->wire_len) + (uint32_t)sizeof(FixedPlan);
+  auto* o = (unsigned long long*)out;
+  switch (use.T) {
+    case 128: return launch_dec_T<128>(use, lds, blocks, stream, d_p, in, n, o, res);
+    case 512: return launch_dec_T<512>(use, lds, blocks, stream, d_p, in, n, o, res);
+    default: return launch_dec_T<256>(use, lds, blocks, stream, d_p, in, n, o, res);
+  }
 }
 
 hipError_t launch_plan_binary_encode(const FixedPlan* p, const FixedPlan* d_p,
                                      const uint8_t* recs, uint64_t n, uint8_t* out,
                                      uint64_t* offsets, DevResult* res, hipStream_t stream) {
   if (n == 0) return hipSuccess;
+  const EncVariant v = enc_variant();
   uint32_t value_words = 0;
   for (uint32_t j = 0; j < p->n_words; ++j)
     if (p->words[j].has_value) value_words |= 1u << j;
-  const uint64_t blocks = (n + kT - 1) / kT;
-  hipLaunchKernelGGL(plan_binary_encode_kernel, dim3((uint32_t)blocks), dim3(kBlock),
-                     host_lds_bytes(*p), stream, d_p, (const unsigned long long*)recs, n,
-                     value_words, out, offsets, res);
-  return hipGetLastError();
+  const uint64_t blocks = (n + v.T - 1) / v.T;
+  const uint32_t lds = wire_region(v.T, p->wire_len) + (uint32_t)sizeof(FixedPlan);
+  const auto* r = (const unsigned long long*)recs;
+#define TGPU_ENC(TT, N)                                                                        \
+  if (v.T == TT && v.nt == N) {                                                                \
+    hipLaunchKernelGGL((plan_binary_encode_kernel<TT, N>), dim3((uint32_t)blocks), dim3(TT), lds, \
+                       stream, d_p, r, n, value_words, out, offsets, res);                     \
+    return hipGetLastError();                                                                  \
+  }
+  TGPU_ENC(128, 0) TGPU_ENC(128, 1) TGPU_ENC(256, 0) TGPU_ENC(256, 1) TGPU_ENC(512, 0)
+  TGPU_ENC(512, 1)
+#undef TGPU_ENC
+  return hipErrorInvalidValue;
 }
 
 }  // namespace tgpu

@@ -156,3 +156,5 @@ hipError_t launch_encode_finish(const EncodeArgs& a, int protocol,
 hipError_t launch_result_init(DevResult* res, uint64_t n, hipStream_t stream);
 
 }  // namespace tgpu
+
+static_assert(sizeof(tgpu::FixedPlan) % 16 == 0, "FixedPlan is copied to LDS in 16-byte chunks");
