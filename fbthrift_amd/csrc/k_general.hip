@@ -28,6 +28,7 @@ __global__ void result_init_kernel(DevResult* res, uint64_t n) {
   res->fail_offset = 0;
   res->total_bytes = 0;
   res->n_records = n;
+  res->n_irregular = 0;
 }
 
 __device__ __forceinline__ Reader make_reader(const DecodeArgs& a, uint64_t start) {

@@ -289,7 +289,9 @@ struct DecVariant { uint32_t T; int glds, pair, nt; };
 struct EncVariant { uint32_t T; int nt; };
 
 DecVariant dec_variant() {
-  DecVariant v{256, 0, 0, 0};
+  // tuned on MI355X (profiles/r01_kbench_sweep.log): 512-record tiles, LDS-DMA
+  // staging, 8-byte non-temporal stores
+  DecVariant v{512, 1, 0, 1};
   if (const char* s = getenv("TGPU_PLAN_DECODE")) {
     unsigned t = 256;
     int g = 0, p = 0, nt = 0;
@@ -298,7 +300,7 @@ DecVariant dec_variant() {
   return v;
 }
 EncVariant enc_variant() {
-  EncVariant v{256, 0};
+  EncVariant v{512, 1};  // tuned: 512-record tiles, non-temporal loads/stores
   if (const char* s = getenv("TGPU_PLAN_ENCODE")) {
     unsigned t = 256;
     int nt = 0;

@@ -25,6 +25,9 @@ struct tgpu_schema {
   bool has_plan = false;  // word-gather form of tmpl (S % 8 == 0)
   FixedPlan plan{};
   FixedPlan* d_plan = nullptr;
+  bool has_prog[3] = {false, false, false};  // compiled programs by protocol id
+  VProgram prog[3]{};
+  VProgram* d_prog[3] = {nullptr, nullptr, nullptr};
 };
 
 struct tgpu_context {
@@ -173,6 +176,137 @@ bool build_template(const tgpu_schema& sc, uint32_t si, uint32_t base, FixedTemp
   t.items[t.n_items++] = stop;
   wire += 1;
   return true;
+}
+
+uint32_t compact_ctype(uint32_t t) {  // CompactProtocol-inl.h:48-69 TTypeToCType
+  switch (t) {
+    case TGPU_T_BOOL: return 1;
+    case TGPU_T_BYTE: return 3;
+    case TGPU_T_I16: return 4;
+    case TGPU_T_I32: return 5;
+    case TGPU_T_I64: return 6;
+    case TGPU_T_DOUBLE: return 7;
+    case TGPU_T_STRING: return 8;
+    case TGPU_T_LIST: return 9;
+    case TGPU_T_SET: return 10;
+    case TGPU_T_MAP: return 11;
+    case TGPU_T_STRUCT: return 12;
+    case TGPU_T_FLOAT: return 13;
+    default: return 0;
+  }
+}
+
+bool push_op(VProgram& P, const VOp& op) {
+  if (P.n_ops >= (uint32_t)kMaxProgramOps) return false;
+  P.ops[P.n_ops++] = op;
+  return true;
+}
+
+VOp make_op(uint8_t kind) {
+  VOp op{};
+  op.kind = kind;
+  op.isset = 0xffff;
+  return op;
+}
+
+// Compiles struct si (members at `base`) into the canonical-form program: the
+// header bytes the generated writer emits (BinaryProtocol-inl.h:53-59,
+// CompactProtocol-inl.h:133-160 incl. long-form ids, bools in the header) and
+// each value's encoding.
+bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, VProgram& P) {
+  const tgpu_struct_desc& sd = sc.structs[si];
+  int32_t prev = 0;
+  for (uint32_t k = 0; k < sd.num_fields; ++k) {
+    const tgpu_field_desc& f = sc.fields[sd.first_field + k];
+    if (f.qualifier != TGPU_UNQUALIFIED) return false;
+    const uint32_t member = base + f.member_offset, isset = base + f.isset_offset;
+    if (member > 0xfffe || isset > 0xfffe) return false;
+    VOp hdr = make_op(VOP_CONST);
+    if (proto == TGPU_PROTOCOL_BINARY) {
+      hdr.hdr_len = 3;
+      hdr.hdr = f.ttype | ((uint32_t)((uint16_t)f.id >> 8) << 8) |
+                ((uint32_t)((uint16_t)f.id & 0xff) << 16);
+    } else {
+      const int32_t id = f.id;
+      const uint32_t ct = f.ttype == TGPU_T_BOOL ? 0 : compact_ctype(f.ttype);
+      if (id > prev && id - prev <= 15) {
+        hdr.hdr_len = 1;
+        hdr.hdr = ((uint32_t)(id - prev) << 4) | ct;
+      } else {
+        uint32_t zz = ((uint32_t)id << 1) ^ (uint32_t)(id >> 31);
+        uint32_t bytes = ct, n = 1;
+        do {
+          const uint32_t b = (zz & 0x7f) | (zz > 0x7f ? 0x80 : 0);
+          bytes |= b << (8 * n++);
+          zz >>= 7;
+        } while (zz);
+        if (n > 4) return false;
+        hdr.hdr_len = (uint8_t)n;
+        hdr.hdr = bytes;
+      }
+      prev = id;
+      if (f.ttype == TGPU_T_BOOL) {
+        hdr.kind = VOP_CBOOL;
+        hdr.member = (uint16_t)member;
+        hdr.isset = (uint16_t)isset;
+        if (!push_op(P, hdr)) return false;
+        continue;
+      }
+    }
+    if (!push_op(P, hdr)) return false;
+    VOp v = make_op(VOP_FIXED);
+    v.member = (uint16_t)member;
+    v.isset = (uint16_t)isset;
+    if (is_scalar(f.ttype)) {
+      const uint32_t w = scalar_size(f.ttype);
+      if (proto == TGPU_PROTOCOL_COMPACT &&
+          (f.ttype == TGPU_T_I16 || f.ttype == TGPU_T_I32 || f.ttype == TGPU_T_I64)) {
+        v.kind = VOP_VARINT;
+        v.bits = f.ttype == TGPU_T_I64 ? 64 : 32;
+      }
+      v.width = (uint8_t)w;
+      v.is_bool = f.ttype == TGPU_T_BOOL;
+      if (!push_op(P, v)) return false;
+    } else if (f.ttype == TGPU_T_STRING) {
+      v.kind = VOP_STRING;
+      if (!push_op(P, v)) return false;
+    } else if (f.ttype == TGPU_T_LIST || f.ttype == TGPU_T_SET) {
+      v.kind = VOP_LIST;
+      const uint32_t e = f.elem_ttype;
+      v.width = (uint8_t)scalar_size(e);
+      v.elem_ttype = (uint8_t)e;
+      v.elem_ct = (uint8_t)compact_ctype(e);
+      v.elem_kind = VEL_FIXED;
+      if (e == TGPU_T_BOOL) v.elem_kind = VEL_BOOL;
+      if (proto == TGPU_PROTOCOL_COMPACT &&
+          (e == TGPU_T_I16 || e == TGPU_T_I32 || e == TGPU_T_I64)) {
+        v.elem_kind = VEL_VARINT;
+        v.bits = e == TGPU_T_I64 ? 64 : 32;
+      }
+      P.has_list = 1;
+      if (!push_op(P, v)) return false;
+    } else if (f.ttype == TGPU_T_STRUCT) {
+      if (!emit_program(sc, (uint32_t)f.struct_index, member, proto, P)) return false;
+      VOp stop = make_op(VOP_CONST);
+      stop.hdr_len = 1;
+      VOp is = make_op(VOP_ISSET);
+      is.isset = (uint16_t)isset;
+      if (!push_op(P, stop) || !push_op(P, is)) return false;
+    } else {
+      return false;
+    }
+  }
+  return true;
+}
+
+bool build_program(const tgpu_schema& sc, int proto, VProgram& P) {
+  P = VProgram{};
+  P.protocol = (uint32_t)proto;
+  P.rec_size = sc.structs[0].size;
+  if (!emit_program(sc, 0, 0, proto, P)) return false;
+  VOp stop = make_op(VOP_CONST);
+  stop.hdr_len = 1;
+  return push_op(P, stop);
 }
 
 // Regroups the template by 8-byte word of the record layout (FixedPlan).
@@ -332,6 +466,16 @@ int tgpu_schema_create(const tgpu_struct_desc* structs, uint32_t n_structs,
     tgpu_schema_destroy(s);
     return TGPU_ERR_HIP;
   }
+  for (int proto : {TGPU_PROTOCOL_BINARY, TGPU_PROTOCOL_COMPACT}) {
+    if (!build_program(*s, proto, s->prog[proto])) continue;
+    if (hipMalloc(&s->d_prog[proto], sizeof(VProgram)) != hipSuccess ||
+        hipMemcpy(s->d_prog[proto], &s->prog[proto], sizeof(VProgram), hipMemcpyHostToDevice) !=
+            hipSuccess) {
+      tgpu_schema_destroy(s);
+      return TGPU_ERR_HIP;
+    }
+    s->has_prog[proto] = true;
+  }
   FixedTemplate t{};
   uint32_t wire = 0;
   if (build_template(*s, 0, 0, t, wire) && wire <= kMaxFixedWire &&
@@ -364,6 +508,8 @@ void tgpu_schema_destroy(tgpu_schema* s) {
   if (s->d_fields) (void)hipFree(s->d_fields);
   if (s->d_tmpl) (void)hipFree(s->d_tmpl);
   if (s->d_plan) (void)hipFree(s->d_plan);
+  for (VProgram* p : s->d_prog)
+    if (p) (void)hipFree(p);
   delete s;
 }
 
@@ -584,7 +730,18 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
     if (offsets) {
       a.offs = offsets;
       a.check_index = 1;
-      if (e == hipSuccess) e = launch_general_decode(a, protocol, s);
+      // compiled-program fast path; a list depth of 1 must be allowed by the
+      // limits (the program never skips, so max_depth is not reached)
+      const int32_t height = a.height ? a.height : a.max_depth;
+      if (schema->has_prog[protocol] && height >= 2 && a.max_depth >= 2) {
+        if (e == hipSuccess)
+          e = launch_program_decode(a, schema->d_prog[protocol], a.rec_size, ctx->d_offs,
+                                    &ctx->d_res->n_irregular, s);
+        if (e == hipSuccess)
+          e = launch_general_decode_list(a, protocol, ctx->d_offs, &ctx->d_res->n_irregular, s);
+      } else if (e == hipSuccess) {
+        e = launch_general_decode(a, protocol, s);
+      }
     } else {
       a.offs = ctx->d_offs;
       a.check_index = 0;

@@ -77,6 +77,49 @@ struct FixedPlan {
   PlanItem items[kMaxTemplateItems];
 };
 
+// ---- compiled record programs (variable-length canonical fast path) -------
+// A schema whose fields are all unqualified compiles to a straight-line
+// program describing the canonical wire form of one record: the header bytes
+// the generated readNoXfer expects at each step (advanceToNextField's fast
+// path, BinaryProtocol-inl.h:586-621 / CompactProtocol-inl.h:811-872) and the
+// value encoding that follows. Nested structs are flattened; members are at
+// absolute offsets of the root record.
+enum VOpKind : uint8_t {
+  VOP_CONST = 1,   // hdr_len constant bytes (field header, STOP, nested header)
+  VOP_FIXED = 2,   // width big-endian bytes -> member (Binary ints, doubles, floats, bytes)
+  VOP_VARINT = 3,  // zigzag varint (bits 32/64) -> member of `width` bytes (Compact ints)
+  VOP_STRING = 4,  // length (Binary BE i32 / Compact varint) + bytes -> tgpu_span view
+  VOP_LIST = 5,    // list header + scalar elements -> arena, tgpu_span
+  VOP_CBOOL = 6,   // Compact bool field: value carried in the header byte
+  VOP_ISSET = 7,   // set an isset byte (after a nested struct's STOP)
+};
+enum VElemKind : uint8_t {
+  VEL_FIXED = 1,   // big-endian fixed width (Binary ints, doubles/floats, bytes)
+  VEL_VARINT = 2,  // zigzag varint (Compact i16/i32/i64)
+  VEL_BOOL = 3,    // Binary: byte must be 0/1; Compact: value = (byte == 1)
+};
+struct VOp {
+  uint8_t kind;
+  uint8_t hdr_len;   // CONST / CBOOL header length
+  uint8_t width;     // FIXED / VARINT store width; LIST element store width
+  uint8_t bits;      // VARINT / list varint element: 32 or 64
+  uint32_t hdr;      // CONST / CBOOL bytes (CBOOL: low nibble of byte 0 is the value)
+  uint16_t member;   // absolute member offset
+  uint16_t isset;    // absolute isset offset to set after the op (0xffff: none)
+  uint8_t elem_kind;  // LIST
+  uint8_t elem_ttype; // LIST: TType of the elements (wire element type)
+  uint8_t elem_ct;    // LIST: Compact element ctype
+  uint8_t is_bool;    // FIXED: Binary bool (byte must be 0/1)
+};
+constexpr int kMaxProgramOps = 128;
+struct VProgram {
+  uint32_t n_ops;
+  uint32_t rec_size;
+  uint32_t protocol;
+  uint32_t has_list;
+  VOp ops[kMaxProgramOps];
+};
+
 // Device-side result slot of a context (one per in-flight call).
 struct DevResult {
   unsigned long long first_fail;       // first failing record (UINT64_MAX: none)
@@ -86,6 +129,7 @@ struct DevResult {
   unsigned long long fail_offset;      // diagnosed byte offset
   unsigned long long total_bytes;      // encode: output size; decode: consumed
   unsigned long long n_records;
+  unsigned long long n_irregular;      // program path: records sent to the general decoder
 };
 
 struct DevSchema {
@@ -142,6 +186,16 @@ hipError_t launch_plan_binary_encode(const FixedPlan* p, const FixedPlan* d_p,
                                      hipStream_t stream);
 hipError_t launch_general_decode(const DecodeArgs& a, int protocol,
                                  hipStream_t stream);
+// Compiled-program fast path over an indexed stream (a.offs): canonical records
+// are decoded from an LDS-staged tile; the others are appended to `irregular`
+// (count in *n_irregular) and decoded by launch_general_decode_list.
+hipError_t launch_program_decode(const DecodeArgs& a, const VProgram* d_prog,
+                                 uint32_t rec_size, uint64_t* irregular,
+                                 unsigned long long* n_irregular, hipStream_t stream);
+hipError_t launch_general_decode_list(const DecodeArgs& a, int protocol,
+                                      const uint64_t* list,
+                                      const unsigned long long* n_list,
+                                      hipStream_t stream);
 hipError_t launch_serial_decode(const DecodeArgs& a, int protocol,
                                 bool from_irregular, uint64_t fixed_len,
                                 hipStream_t stream);

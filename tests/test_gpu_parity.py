@@ -208,3 +208,53 @@ def test_config_shapes_roundtrip(gpu, sname, proto):
         assert np.array_equal(grec, orec)
         k = min(garena.size, oarena.size)
         assert np.array_equal(garena[:k], oarena[:k])
+
+
+@pytest.mark.parametrize("case", [c for c in corpus.cases() if c[4] == 1], ids=lambda c: c[0])
+def test_corpus_status_parity_indexed(gpu, case):
+    """The same pins through an index (compiled-program fast path, then the
+    general decoder for the records it does not take)."""
+    name, proto, table, stream, n, limits, expected = case
+    schema = Schema.from_table(table)
+    offs = np.array([0, len(stream)], dtype=np.uint64)
+    st, rec, arena, nd, cons = gpu_decode(schema, proto, stream, 1, offs, limits, dev=gpu)
+    ost, orec, oarena, ond, ocons = oracle.decode(schema, proto, stream, 1, offsets=offs,
+                                                  limits=limits)
+    assert st.as_tuple() == ost.as_tuple(), name
+    assert (nd, cons) == (ond, ocons)
+    k = (nd + (1 if st.code else 0)) * schema.record_size
+    assert np.array_equal(rec[:k], orec[:k])
+
+
+@pytest.mark.parametrize("name,every", [("mixed_compact", 7), ("mixed_binary", 3),
+                                        ("nested_binary", 5), ("nested_compact", 11),
+                                        ("scalars_compact", 4), ("scalars_binary", 9)])
+def test_program_path_with_irregular_records(gpu, name, every):
+    """Indexed stream where every `every`-th record is re-encoded in a
+    non-canonical but valid form (fields reversed + an unknown field): the
+    program path must hand exactly those records to the general decoder."""
+    import wire as wb
+
+    c = helpers.Case(name)
+    parts = []
+    for i in range(c.n):
+        rec_bytes = c.wire[c.offsets[i]:c.offsets[i + 1]]
+        if i % every == 0:
+            # prepend an unknown field that the reader skips: Binary i32 field
+            # 777; Compact list<byte> with long-form id 0 (so the record's own
+            # first delta header still lands on its first field id)
+            if c.protocol == 0:
+                head = wb.W(0).field(8, 777).i32(-5).bytes()
+            else:
+                head = bytes([0x09, 0x00, 0x23, 0x01, 0x02])
+            rec_bytes = head + rec_bytes
+        parts.append(rec_bytes)
+    stream = b"".join(parts)
+    offs = np.concatenate([[0], np.cumsum([len(p) for p in parts])]).astype(np.uint64)
+    st, rec, arena, nd, cons = gpu_decode(c.schema, c.protocol, stream, c.n, offs, dev=gpu)
+    ost, orec, oarena, _, ocons = oracle.decode(c.schema, c.protocol, stream, c.n, offsets=offs)
+    assert st.as_tuple() == ost.as_tuple()
+    assert st.code == 0 and cons == ocons == len(stream)
+    assert np.array_equal(rec, orec)
+    k = min(arena.size, oarena.size)
+    assert np.array_equal(arena[:k], oarena[:k])
