@@ -30,4 +30,16 @@ if [[ $STEPS == all || $STEPS == *prof* ]]; then
   (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$OLDPWD/bench.py" --steps 5 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-}) > "$OUT/prof.log" 2>&1 || { echo "rocprof failed $?"; tail -20 "$OUT/prof.log"; exit 5; }
   find "$OUT/prof" -name "*stats*" | head
 fi
+if [[ $STEPS == *pmc* ]]; then
+  run pmc
+  export TMPDIR=/tmp
+  P=$OUT/pmc; rm -rf "$P"; mkdir -p "$P"
+  for c in FETCH_SIZE WRITE_SIZE; do
+    d=$(echo ${c%_SIZE} | tr A-Z a-z)
+    (cd /tmp && timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$P/${d}_calib" -o run -- python3 "$OLDPWD/tools/pmc_calib.py") > "$P/${d}_calib.log" 2>&1 || { echo "pmc calib $c failed $?"; tail -20 "$P/${d}_calib.log"; exit 6; }
+    (cd /tmp && timeout -k 10 600 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$P/${d}_bench" -o run -- python3 "$OLDPWD/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-copy-ceiling ${PROF_ARGS:-}) > "$P/${d}_bench.log" 2>&1 || { echo "pmc bench $c failed $?"; tail -20 "$P/${d}_bench.log"; exit 6; }
+  done
+  python3 tools/pmc_summary.py "$P" ${PMC_RECORDS:-67108864} "$OUT/pmc_latest.json" > "$P/summary.log" 2>&1 || { echo "pmc summary failed"; tail -20 "$P/summary.log"; }
+  tail -30 "$P/summary.log"
+fi
 echo done

@@ -1,0 +1,86 @@
+#!/usr/bin/env python3
+"""Turns two rocprofv3 --pmc passes (FETCH_SIZE and WRITE_SIZE, each its own
+run, --kernel-trace only) into profiles/pmc_latest.json: HBM bytes per launch
+and per record for each kernel of interest.
+
+Units and gfx950 corrections follow MI355X_MICROARCH.md (HBM / rocprofv3):
+FETCH_SIZE and WRITE_SIZE are in KiB; FETCH_SIZE reports half the bytes of a
+16-byte-per-lane streaming read, WRITE_SIZE is exact for 16-byte stores, and
+other widths are uncalibrated. We therefore calibrate every access width we
+use on the copy kernels of tools/copy_ceiling.hip (1 GiB read + 1 GiB written,
+launched by tools/pmc_calib.py in the same passes) and scale each kernel's
+counters by the factor of the access width it issues:
+
+  plan_binary_decode_kernel : reads 16 B/lane (LDS-DMA), writes 8 B/lane
+  plan_binary_encode_kernel : reads 8 B/lane, writes 16 B/lane
+
+usage: pmc_summary.py PMC_ROOT RECORDS_PER_LAUNCH [OUT.json]
+  PMC_ROOT holds fetch_calib/, write_calib/ (pmc_calib.py) and fetch_bench/,
+  write_bench/ (bench.py) rocprofv3 output directories.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+CALIB_BYTES = 1 << 30
+WIDTHS = {"plan_binary_decode_kernel": (16, 8), "plan_binary_encode_kernel": (8, 16)}
+ALGO = {"plan_binary_decode_kernel": 89 + 72, "plan_binary_encode_kernel": 64 + 89}
+
+
+def load(d, counter):
+    """kernel short name -> list of per-dispatch counter values (KiB)."""
+    out = {}
+    files = glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True)
+    if not files:
+        raise SystemExit("no counter_collection csv under %s" % d)
+    for f in files:
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row.get("Counter_Name") != counter:
+                    continue
+                name = row["Kernel_Name"].replace("(anonymous namespace)::", "")
+                name = name.replace("void ", "").split("(")[0].split("<")[0].split("::")[-1]
+                out.setdefault(name, []).append(float(row["Counter_Value"]))
+    return out
+
+
+def main():
+    root, n = sys.argv[1], int(sys.argv[2])
+    out_path = sys.argv[3] if len(sys.argv) > 3 else os.path.join(
+        os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_latest.json")
+    fetch = load(os.path.join(root, "fetch_bench"), "FETCH_SIZE")
+    write = load(os.path.join(root, "write_bench"), "WRITE_SIZE")
+    cfetch = load(os.path.join(root, "fetch_calib"), "FETCH_SIZE")
+    cwrite = load(os.path.join(root, "write_calib"), "WRITE_SIZE")
+
+    def avg(v):
+        return sum(v) / len(v)
+
+    calib = {}
+    for w, k in ((16, "copy_kernel"), (8, "copy8_kernel")):
+        calib[w] = {"fetch": CALIB_BYTES / (avg(cfetch[k]) * 1024),
+                    "write": CALIB_BYTES / (avg(cwrite[k]) * 1024)}
+    res = {"calibration": {"bytes": CALIB_BYTES,
+                           "factor_by_width": {str(w): {a: round(b, 4) for a, b in c.items()}
+                                               for w, c in calib.items()}},
+           "records_per_launch": n}
+    for k, (rw, ww) in WIDTHS.items():
+        if k not in fetch or k not in write:
+            continue
+        fb = avg(fetch[k]) * 1024 * calib[rw]["fetch"]
+        wb = avg(write[k]) * 1024 * calib[ww]["write"]
+        res[k] = {"fetch_bytes": int(fb), "write_bytes": int(wb),
+                  "raw_fetch_kib": avg(fetch[k]), "raw_write_kib": avg(write[k]),
+                  "dispatches": [len(fetch[k]), len(write[k])],
+                  "hbm_bytes_per_record": round((fb + wb) / n, 3),
+                  "algorithmic_bytes_per_record": ALGO[k],
+                  "traffic_over_algorithmic": round((fb + wb) / n / ALGO[k], 4)}
+    with open(out_path, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
