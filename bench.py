@@ -92,12 +92,179 @@ def cpu_baseline(seconds=12.0):
             "sample": "%d x encode+decode of 4Mi config-2 records (%.1f s wall)" % (reps, el)}
 
 
+class Workload:
+    """One BASELINE config: resident inputs, one encode+decode step, checks."""
+
+    def timed_step(self, ev):
+        ev[0].record(self.stream)
+        self.encode()
+        ev[1].record(self.stream)
+        self.decode()
+        ev[2].record(self.stream)
+
+
+class Flat8(Workload):
+    """Config 2: Binary, flat {1..8: i64} (72-byte records, 89-byte wire)."""
+    name = "config 2: Binary protocol, flat {1..8: i64} records, encode+decode"
+    default_records = 1 << 26
+    dec_kernel, enc_kernel = "plan_binary_decode_kernel", "plan_binary_encode_kernel"
+
+    def __init__(self, n, rank, dev):
+        import torch
+
+        from fbthrift_amd.schema import Schema
+        from fbthrift_amd.serializer import BinarySerializer, GpuSchema
+        import datagen
+
+        self.S = BinarySerializer
+        self.gs = GpuSchema(Schema.from_table(datagen.SCHEMAS["flat8"]))
+        self.L = self.gs.fixed_wire_size(0)
+        assert self.L == 89 and self.gs.record_size == 72
+        self.n = n
+        self.S.context().reserve(n)
+        self.recs = gen_flat8_device(n, rank * n, dev)  # shard `rank` of the record space
+        self.wire = torch.empty(n * self.L, dtype=torch.uint8, device=dev)
+        self.back = torch.empty(n * 72, dtype=torch.uint8, device=dev)
+        self.stream = torch.cuda.current_stream()
+        self.wire_bytes = n * self.L
+        self.record_bytes = 72
+
+    def encode(self):
+        self.S.serialize(self.gs, self.recs, self.n, out=self.wire, offsets=None, sync=False)
+
+    def decode(self):
+        self.S.deserialize(self.gs, self.wire, self.n, records=self.back, sync=False)
+
+    def verify(self):
+        import torch
+
+        st, nd, consumed = self.S.context().wait()
+        if st.code or consumed != self.wire_bytes:
+            raise RuntimeError("decode failed: %s" % (st.as_tuple(),))
+        if not torch.equal(self.back, self.recs):
+            raise RuntimeError("round trip mismatch")
+
+    def algorithmic(self):
+        # SURVEY §8d: decode reads 89 wire + writes 64 values + 8 isset;
+        # encode reads 64 values + writes 89 wire.
+        return self.n * (89 + 72), self.n * (64 + 89)
+
+
+class VarLen(Workload):
+    """Configs 3 / 4: variable-length records. The encode writes the record
+    index (n+1 offsets) the decode then uses; the round trip is checked by
+    comparing the fixed members and re-encoding the decoded batch, which must
+    reproduce the wire stream byte for byte."""
+
+    def __init__(self, n, rank, dev):
+        import ctypes
+
+        import torch
+
+        from fbthrift_amd.schema import Schema
+        from fbthrift_amd.serializer import BinarySerializer, CompactSerializer, GpuSchema
+        import datagen
+
+        self.S = CompactSerializer if self.protocol == 2 else BinarySerializer
+        schema = Schema.from_table(datagen.SCHEMAS[self.schema])
+        self.gs = GpuSchema(schema)
+        self.n = n
+        self.record_bytes = rs = schema.record_size
+        self.S.context().reserve(n)
+        self.stream = torch.cuda.current_stream()
+        lib = ctypes.CDLL(os.path.join(ROOT, "tools", "build", "libtgpu_datagen.so"))
+        self.recs = torch.empty(n * rs, dtype=torch.uint8, device=dev)
+        self.side = torch.empty(n * 64, dtype=torch.uint8, device=dev)  # string / list slots
+        gen = lib.tgpu_gen_mixed if self.schema == "mixed" else lib.tgpu_gen_nested
+        if gen(ctypes.c_uint64(datagen.SEED), ctypes.c_uint64(rank * n), ctypes.c_uint64(n),
+               ctypes.c_void_p(self.recs.data_ptr()), ctypes.c_void_p(self.side.data_ptr()),
+               ctypes.c_void_p(self.stream.cuda_stream)):
+            raise RuntimeError("device record generator failed")
+        self.sbase = self.side if self.schema == "mixed" else None
+        self.lbase = self.side if self.schema == "nested" else None
+        self.offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        _, total = self.S.encoded_size(self.gs, self.recs, n, self.offs, list_base=self.lbase)
+        self.wire_bytes = total
+        self.wire = torch.empty(total, dtype=torch.uint8, device=dev)
+        self.back = torch.empty(n * rs, dtype=torch.uint8, device=dev)
+        cap = self.S.arena_bytes(self.gs, total)
+        self.arena = torch.empty(max(cap, 1), dtype=torch.uint8, device=dev) if cap else None
+        # payload bytes behind the spans: string bytes (config 3) or list
+        # elements, 4 bytes each (config 4)
+        v = self.recs.view(n, rs)
+        lens = [v[:, o:o + 16].contiguous().view(torch.int64)[:, 1] & 0xFFFFFFFF
+                for o in self.span_offsets]
+        self.side_bytes = int(sum(int(x.sum().item()) for x in lens)) * self.elem_width
+
+    def encode(self):
+        self.S.serialize(self.gs, self.recs, self.n, string_base=self.sbase,
+                         list_base=self.lbase, out=self.wire, offsets=self.offs, sync=False)
+
+    def decode(self):
+        self.S.deserialize(self.gs, self.wire, self.n, offsets=self.offs, records=self.back,
+                           arena=self.arena, sync=False)
+
+    def verify(self):
+        import torch
+
+        st, nd, consumed = self.S.context().wait()
+        if st.code or consumed != self.wire_bytes or nd != self.n:
+            raise RuntimeError("decode failed: %s" % (st.as_tuple(),))
+        rs = self.record_bytes
+        a, b = self.recs.view(self.n, rs), self.back.view(self.n, rs)
+        for lo, hi in self.fixed_ranges:
+            if not torch.equal(a[:, lo:hi], b[:, lo:hi]):
+                raise RuntimeError("round trip mismatch in bytes %d..%d" % (lo, hi))
+        # decoded strings are views into the wire; decoded list elements live
+        # in the arena: re-encoding from those must give the same stream
+        again = torch.empty_like(self.wire)
+        offs2 = torch.empty_like(self.offs)
+        self.S.serialize(self.gs, self.back, self.n,
+                         string_base=self.wire if self.schema == "mixed" else None,
+                         list_base=self.arena if self.schema == "nested" else None,
+                         out=again, offsets=offs2, sync=True)
+        if not torch.equal(again, self.wire) or not torch.equal(offs2, self.offs):
+            raise RuntimeError("re-encode of the decoded batch differs from the wire stream")
+        del again, offs2
+
+    def algorithmic(self):
+        # decode: read the wire + write the records (+ list elements to the
+        # arena; strings are views into the wire); encode: read the records
+        # and the string/list payloads + write the wire. The record index
+        # (8 B/record) is bookkeeping, not counted.
+        arena = self.side_bytes if self.schema == "nested" else 0
+        return (self.wire_bytes + self.n * self.record_bytes + arena,
+                self.n * self.record_bytes + self.side_bytes + self.wire_bytes)
+
+
+class Mixed(VarLen):
+    name = "config 3: Compact protocol, {4 x i32, 2 x string[0..32]} records, indexed encode+decode"
+    schema, protocol = "mixed", 2
+    default_records = 1 << 26
+    dec_kernel, enc_kernel = "program_decode_kernel", "encode_write_kernel"
+    fixed_ranges = [(0, 16), (48, 54)]
+    span_offsets, elem_width = (16, 32), 1
+
+
+class Nested(VarLen):
+    name = "config 4: Binary protocol, {i64, list<i32>[0..16], inner{3 x double}}, indexed encode+decode"
+    schema, protocol = "nested", 0
+    default_records = 1 << 25
+    dec_kernel, enc_kernel = "program_decode_kernel", "encode_write_kernel"
+    fixed_ranges = [(0, 8), (24, 51), (56, 59)]
+    span_offsets, elem_width = (8,), 4
+
+
+WORKLOADS = {2: Flat8, 3: Mixed, 4: Nested}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--records", type=int, default=1 << 26)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(WORKLOADS))
+    ap.add_argument("--records", type=int, default=0, help="records per GPU (default: config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-copy-ceiling", action="store_true")
     ap.add_argument("--host-start", action="store_true",
@@ -115,41 +282,15 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from fbthrift_amd.schema import Schema
-    from fbthrift_amd.serializer import BinarySerializer as BS, GpuSchema, TgpuError
-    import datagen
-
-    n = args.records
-    schema = Schema.from_table(datagen.SCHEMAS["flat8"])
-    gs = GpuSchema(schema)
-    L = gs.fixed_wire_size(0)
-    assert L == 89 and schema.record_size == 72
-    ctx = BS.context()
-    ctx.reserve(n)
-
-    recs = gen_flat8_device(n, rank * n, dev)  # shard `rank` of the record space
-    wire = torch.empty(n * L, dtype=torch.uint8, device=dev)
-    back = torch.empty(n * 72, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream()
-
-    def step(ev=None):
-        if ev:
-            ev[0].record(stream)
-        BS.serialize(gs, recs, n, out=wire, offsets=None, sync=False)
-        if ev:
-            ev[1].record(stream)
-        BS.deserialize(gs, wire, n, records=back, sync=False)
-        if ev:
-            ev[2].record(stream)
+    W = WORKLOADS[args.config]
+    n = args.records or W.default_records
+    wl = W(n, rank, dev)
 
     for _ in range(args.warmup):
-        step()
+        wl.encode()
+        wl.decode()
     torch.cuda.synchronize()
-    st, nd, consumed = ctx.wait()
-    if st.code or consumed != n * L:
-        raise TgpuError("warmup decode failed: %s" % (st.as_tuple(),))
-    if not torch.equal(back, recs):
-        raise RuntimeError("round trip mismatch")
+    wl.verify()
 
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     if world > 1:
@@ -157,53 +298,54 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(evs[k])
+        wl.timed_step(evs[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    st, nd, consumed = ctx.wait()
-    assert st.code == 0 and consumed == n * L
-    enc_ms = sorted(e[0].elapsed_time(e[1]) for e in evs)
-    dec_ms = sorted(e[1].elapsed_time(e[2]) for e in evs)
+    st, nd, consumed = wl.S.context().wait()
+    if st.code or consumed != wl.wire_bytes:
+        raise RuntimeError("timed decode failed: %s" % (st.as_tuple(),))
+    enc_ms = [e[0].elapsed_time(e[1]) for e in evs]
+    dec_ms = [e[1].elapsed_time(e[2]) for e in evs]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    wire_bytes = n * L
-    value = 2.0 * wire_bytes * args.steps * world / elapsed / 2**30
+    value = 2.0 * wl.wire_bytes * args.steps * world / elapsed / 2**30
     dec_avg = sum(dec_ms) / len(dec_ms) / 1e3
     enc_avg = sum(enc_ms) / len(enc_ms) / 1e3
-    dec_alg = n * (89 + 72)  # read 89 wire + write 64 values + 8 isset
-    enc_alg = n * (64 + 89)  # read 64 values + write 89 wire
+    dec_alg, enc_alg = wl.algorithmic()
     line = {
         "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic: splitmix64(seed 0x1729) int64 values + edge values, generated on device",
-        "config": {"workload": "config 2: Binary protocol, flat {1..8: i64} records, encode+decode",
-                   "records_per_gpu": n, "wire_bytes_per_gpu": wire_bytes,
-                   "record_bytes": 72, "wire_bytes_per_record": L,
+        "data": "synthetic: splitmix64(seed 0x1729) records per tests/golden/datagen.py, "
+                "generated on device",
+        "config": {"workload": wl.name, "records_per_gpu": n, "wire_bytes_per_gpu": wl.wire_bytes,
+                   "record_bytes": wl.record_bytes,
+                   "wire_bytes_per_record": round(wl.wire_bytes / n, 3),
                    "parallelism": "dp%d (independent record shards, no collective)" % world},
-        "roofline": {"bound": "hbm", "kernel": "plan_binary_decode_kernel",
+        "roofline": {"bound": "hbm", "kernel": wl.dec_kernel,
                      "achieved": round(dec_alg / dec_avg / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(dec_alg / dec_avg / 1e9 / HBM_PEAK_GBS, 4),
-                     "traffic": pmc_traffic("plan_binary_decode_kernel", n),
+                     "traffic": pmc_traffic(wl.dec_kernel, n, args.config),
                      "algorithmic_bytes_per_launch": dec_alg,
                      "avg_launch_ms": round(dec_avg * 1e3, 4),
-                     "timing": "HIP events on the launch stream around the decode call "
-                               "(main kernel + 4 tiny bookkeeping kernels)",
+                     "timing": "HIP events on the launch stream around the whole decode call "
+                               "(main kernel + small bookkeeping kernels)",
                      "copy_ceiling": None if args.no_copy_ceiling else copy_ceiling(dev),
-                     "encode": {"kernel": "plan_binary_encode_kernel",
+                     "encode": {"kernel": wl.enc_kernel,
                                 "achieved": round(enc_alg / enc_avg / 1e9, 1),
                                 "frac": round(enc_alg / enc_avg / 1e9 / HBM_PEAK_GBS, 4),
+                                "algorithmic_bytes_per_launch": enc_alg,
                                 "avg_launch_ms": round(enc_avg * 1e3, 4)}},
     }
     if args.host_start and rank == 0:
-        line["host_start"] = host_start(gs, recs, wire, back, n, L, dev)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["host_start"] = host_start(wl, dev)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == 2:
         line["cpu_baseline"] = cpu_baseline()
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -251,7 +393,7 @@ def copy_ceiling(dev, nbytes=4 << 30):
     return {"GBps": round(2 * nbytes / t / 1e9, 1), "how": how}
 
 
-def pmc_traffic(kernel, n):
+def pmc_traffic(kernel, n, config=2):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
     summary (profiles/pmc_latest.json, written by tools/pmc_summary.py from
     separate --pmc passes, gfx950 FETCH_SIZE x2 correction applied), scaled to
@@ -259,33 +401,32 @@ def pmc_traffic(kernel, n):
     path = os.path.join(ROOT, "profiles", "pmc_latest.json")
     try:
         with open(path) as f:
-            d = json.load(f)[kernel]
+            d = json.load(f)
+        if d.get("config", 2) != config:
+            return None
+        d = d[kernel]
         return int(d["hbm_bytes_per_record"] * n)
     except (OSError, KeyError, ValueError):
         return None
 
 
-def host_start(gs, recs, wire, back, n, L, dev):
+def host_start(wl, dev):
     """Host-memory start/end rates (pinned buffers, PCIe-inclusive): decode =
     H2D(wire) + kernels + D2H(records); encode = H2D(records) + kernels +
-    D2H(wire). Reported for DESIGN.md, never as `value`."""
+    D2H(wire). Serialized on one stream (no overlap). Reported for DESIGN.md,
+    never as `value`."""
     import torch
 
-    from fbthrift_amd.serializer import BinarySerializer as BS
-
-    h_wire = torch.empty(n * L, dtype=torch.uint8, pin_memory=True)
-    h_recs = torch.empty(n * 72, dtype=torch.uint8, pin_memory=True)
-    h_wire.copy_(wire)
-    h_recs.copy_(recs)
+    h_wire = torch.empty(wl.wire.numel(), dtype=torch.uint8, pin_memory=True)
+    h_recs = torch.empty(wl.recs.numel(), dtype=torch.uint8, pin_memory=True)
+    h_wire.copy_(wl.wire)
+    h_recs.copy_(wl.recs)
     torch.cuda.synchronize()
     res = {}
-    for name, fn in (("decode", lambda: (wire.copy_(h_wire, non_blocking=True),
-                                        BS.deserialize(gs, wire, n, records=back, sync=False),
-                                        h_recs.copy_(back, non_blocking=True))),
-                     ("encode", lambda: (recs.copy_(h_recs, non_blocking=True),
-                                        BS.serialize(gs, recs, n, out=wire, offsets=None,
-                                                     sync=False),
-                                        h_wire.copy_(wire, non_blocking=True)))):
+    for name, fn in (("decode", lambda: (wl.wire.copy_(h_wire, non_blocking=True), wl.decode(),
+                                        h_recs.copy_(wl.back, non_blocking=True))),
+                     ("encode", lambda: (wl.recs.copy_(h_recs, non_blocking=True), wl.encode(),
+                                        h_wire.copy_(wl.wire, non_blocking=True)))):
         fn()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -293,7 +434,7 @@ def host_start(gs, recs, wire, back, n, L, dev):
             fn()
         torch.cuda.synchronize()
         el = (time.perf_counter() - t0) / 3
-        res[name + "_gibps"] = round(n * L / el / 2**30, 3)
+        res[name + "_gibps"] = round(wl.wire_bytes / el / 2**30, 3)
     return res
 
 

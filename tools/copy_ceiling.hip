@@ -48,9 +48,9 @@ __global__ __launch_bounds__(256) void copy8_kernel(const unsigned long long* __
 }
 
 extern "C" int copy_calibrate(const void* src, void* dst, uint64_t bytes) {
-  (void)hipLaunchKernelGGL(copy_kernel, dim3(2048), dim3(256), 0, 0, (const u32x4*)src,
+  hipLaunchKernelGGL(copy_kernel, dim3(2048), dim3(256), 0, 0, (const u32x4*)src,
                            (u32x4*)dst, bytes / 16);
-  (void)hipLaunchKernelGGL(copy8_kernel, dim3(2048), dim3(256), 0, 0,
+  hipLaunchKernelGGL(copy8_kernel, dim3(2048), dim3(256), 0, 0,
                            (const unsigned long long*)src, (unsigned long long*)dst, bytes / 8);
   return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }
@@ -61,14 +61,14 @@ static void launch_variant(int variant, const void* src, void* dst, uint64_t byt
   u32x4* d = (u32x4*)dst;
   const uint32_t full1 = (uint32_t)((n16 + 255) / 256), full4 = (uint32_t)((n16 + 1023) / 1024);
   switch (variant) {
-    case 0: (void)hipLaunchKernelGGL((copy_t<u32x4, true, 4>), dim3(2048), dim3(256), 0, 0, s, d, n16); break;
-    case 1: (void)hipLaunchKernelGGL((copy_t<u32x4, false, 4>), dim3(2048), dim3(256), 0, 0, s, d, n16); break;
-    case 2: (void)hipLaunchKernelGGL((copy_t<u32x4, true, 1>), dim3(full1), dim3(256), 0, 0, s, d, n16); break;
-    case 3: (void)hipLaunchKernelGGL((copy_t<u32x4, false, 1>), dim3(full1), dim3(256), 0, 0, s, d, n16); break;
-    case 4: (void)hipLaunchKernelGGL((copy_t<u32x4, true, 4>), dim3(full4), dim3(256), 0, 0, s, d, n16); break;
-    case 5: (void)hipLaunchKernelGGL((copy_t<u32x4, false, 4>), dim3(full4), dim3(256), 0, 0, s, d, n16); break;
-    case 6: (void)hipLaunchKernelGGL((copy_t<u32x4, false, 8>), dim3(4096), dim3(256), 0, 0, s, d, n16); break;
-    default: (void)hipLaunchKernelGGL((copy_t<u32x4, false, 2>), dim3(8192), dim3(256), 0, 0, s, d, n16); break;
+    case 0: hipLaunchKernelGGL((copy_t<u32x4, true, 4>), dim3(2048), dim3(256), 0, 0, s, d, n16); break;
+    case 1: hipLaunchKernelGGL((copy_t<u32x4, false, 4>), dim3(2048), dim3(256), 0, 0, s, d, n16); break;
+    case 2: hipLaunchKernelGGL((copy_t<u32x4, true, 1>), dim3(full1), dim3(256), 0, 0, s, d, n16); break;
+    case 3: hipLaunchKernelGGL((copy_t<u32x4, false, 1>), dim3(full1), dim3(256), 0, 0, s, d, n16); break;
+    case 4: hipLaunchKernelGGL((copy_t<u32x4, true, 4>), dim3(full4), dim3(256), 0, 0, s, d, n16); break;
+    case 5: hipLaunchKernelGGL((copy_t<u32x4, false, 4>), dim3(full4), dim3(256), 0, 0, s, d, n16); break;
+    case 6: hipLaunchKernelGGL((copy_t<u32x4, false, 8>), dim3(4096), dim3(256), 0, 0, s, d, n16); break;
+    default: hipLaunchKernelGGL((copy_t<u32x4, false, 2>), dim3(8192), dim3(256), 0, 0, s, d, n16); break;
   }
 }
 
