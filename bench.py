@@ -241,7 +241,7 @@ class Mixed(VarLen):
     name = "config 3: Compact protocol, {4 x i32, 2 x string[0..32]} records, indexed encode+decode"
     schema, protocol = "mixed", 2
     default_records = 1 << 26
-    dec_kernel, enc_kernel = "program_decode_kernel", "encode_write_kernel"
+    dec_kernel, enc_kernel = "program_decode_kernel", "program_write_kernel"
     fixed_ranges = [(0, 16), (48, 54)]
     span_offsets, elem_width = (16, 32), 1
 
@@ -250,7 +250,7 @@ class Nested(VarLen):
     name = "config 4: Binary protocol, {i64, list<i32>[0..16], inner{3 x double}}, indexed encode+decode"
     schema, protocol = "nested", 0
     default_records = 1 << 25
-    dec_kernel, enc_kernel = "program_decode_kernel", "encode_write_kernel"
+    dec_kernel, enc_kernel = "program_decode_kernel", "program_write_kernel"
     fixed_ranges = [(0, 8), (24, 51), (56, 59)]
     span_offsets, elem_width = (8,), 4
 
@@ -419,12 +419,13 @@ def host_start(wl, dev):
 
     h_wire = torch.empty(wl.wire.numel(), dtype=torch.uint8, pin_memory=True)
     h_recs = torch.empty(wl.recs.numel(), dtype=torch.uint8, pin_memory=True)
+    h_back = torch.empty(wl.back.numel(), dtype=torch.uint8, pin_memory=True)
     h_wire.copy_(wl.wire)
     h_recs.copy_(wl.recs)
     torch.cuda.synchronize()
     res = {}
     for name, fn in (("decode", lambda: (wl.wire.copy_(h_wire, non_blocking=True), wl.decode(),
-                                        h_recs.copy_(wl.back, non_blocking=True))),
+                                        h_back.copy_(wl.back, non_blocking=True))),
                      ("encode", lambda: (wl.recs.copy_(h_recs, non_blocking=True), wl.encode(),
                                         h_wire.copy_(wl.wire, non_blocking=True)))):
         fn()

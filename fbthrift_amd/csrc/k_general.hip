@@ -176,35 +176,6 @@ __global__ __launch_bounds__(256) void encode_size_kernel(EncodeArgs a) {
   if (threadIdx.x == 0) a.block_sums[blockIdx.x] = t;
 }
 
-// Exclusive scan of nb block sums by one 1024-thread block; total -> res.
-__global__ __launch_bounds__(1024) void scan_blocks_kernel(unsigned long long* sums, uint64_t nb,
-                                                           DevResult* res, uint64_t* offs,
-                                                           uint64_t n) {
-  __shared__ unsigned long long part[1024];
-  const uint64_t per = (nb + 1023) / 1024;
-  const uint64_t b = threadIdx.x * per, e = min(nb, b + per);
-  unsigned long long s = 0;
-  for (uint64_t k = b; k < e; ++k) s += sums[k];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const unsigned long long y = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0;
-    __syncthreads();
-    part[threadIdx.x] += y;
-    __syncthreads();
-  }
-  unsigned long long run = part[threadIdx.x] - s;
-  for (uint64_t k = b; k < e; ++k) {
-    const unsigned long long v = sums[k];
-    sums[k] = run;
-    run += v;
-  }
-  if (threadIdx.x == 1023) {
-    res->total_bytes = part[1023];
-    offs[n] = part[1023];
-  }
-}
-
 template <int P>
 __global__ __launch_bounds__(256) void encode_write_kernel(EncodeArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
@@ -301,8 +272,9 @@ hipError_t launch_general_encode(const EncodeArgs& a, int protocol, uint64_t n_b
   } else {
     hipLaunchKernelGGL(encode_size_kernel<TGPU_PROTOCOL_COMPACT>, grid, dim3(256), 0, stream, a);
   }
-  hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(1024), 0, stream, a.block_sums, n_blocks,
-                     a.res, a.offs, a.n);
+  const hipError_t e = launch_scan_tiles(a.block_sums, n_blocks, a.scan_part, a.res, a.offs, a.n,
+                                         stream);
+  if (e != hipSuccess) return e;
   if (protocol == TGPU_PROTOCOL_BINARY) {
     hipLaunchKernelGGL(encode_write_kernel<TGPU_PROTOCOL_BINARY>, grid, dim3(256), 0, stream, a);
   } else {
@@ -320,13 +292,15 @@ hipError_t launch_general_size(const EncodeArgs& a, int protocol, uint64_t n_blo
   } else {
     hipLaunchKernelGGL(encode_size_kernel<TGPU_PROTOCOL_COMPACT>, grid, dim3(256), 0, stream, a);
   }
-  hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(1024), 0, stream, a.block_sums, n_blocks,
-                     a.res, a.offs, a.n);
-  if (protocol == TGPU_PROTOCOL_BINARY) {
-    hipLaunchKernelGGL(size_offsets_kernel, grid, dim3(256), 0, stream, a);
-  } else {
-    hipLaunchKernelGGL(size_offsets_kernel, grid, dim3(256), 0, stream, a);
-  }
+  const hipError_t e = launch_scan_tiles(a.block_sums, n_blocks, a.scan_part, a.res, a.offs, a.n,
+                                         stream);
+  if (e != hipSuccess) return e;
+  return launch_size_offsets(a, n_blocks, stream);
+}
+
+hipError_t launch_size_offsets(const EncodeArgs& a, uint64_t n_blocks, hipStream_t stream) {
+  if (a.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(size_offsets_kernel, dim3((uint32_t)n_blocks), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 

@@ -36,6 +36,7 @@ struct tgpu_context {
   DevResult* h_res = nullptr;  // pinned
   uint64_t* d_offs = nullptr;
   unsigned long long* d_block_sums = nullptr;
+  unsigned long long* d_scan_part = nullptr;  // partial sums of the tile scan
   uint64_t reserved = 0;  // records
   int last_op = 0;        // 1 decode, 2 encode
 };
@@ -380,11 +381,16 @@ int ensure_workspace(tgpu_context* ctx, uint64_t n) {
   const uint64_t want = std::max<uint64_t>(n, 1024);
   if (ctx->d_offs) (void)hipFree(ctx->d_offs);
   if (ctx->d_block_sums) (void)hipFree(ctx->d_block_sums);
+  if (ctx->d_scan_part) (void)hipFree(ctx->d_scan_part);
   ctx->d_offs = nullptr;
   ctx->d_block_sums = nullptr;
+  ctx->d_scan_part = nullptr;
   ctx->reserved = 0;
+  const uint64_t tiles = (want + 255) / 256;
   if (hipMalloc(&ctx->d_offs, (want + 1) * sizeof(uint64_t)) != hipSuccess) return TGPU_ERR_HIP;
-  if (hipMalloc(&ctx->d_block_sums, ((want + 255) / 256 + 1) * sizeof(unsigned long long)) !=
+  if (hipMalloc(&ctx->d_block_sums, (tiles + 1) * sizeof(unsigned long long)) != hipSuccess)
+    return TGPU_ERR_HIP;
+  if (hipMalloc(&ctx->d_scan_part, (scan_tiles_parts(tiles) + 1) * sizeof(unsigned long long)) !=
       hipSuccess)
     return TGPU_ERR_HIP;
   ctx->reserved = want;
@@ -539,6 +545,7 @@ void tgpu_context_destroy(tgpu_context* c) {
   if (c->h_res) (void)hipHostFree(c->h_res);
   if (c->d_offs) (void)hipFree(c->d_offs);
   if (c->d_block_sums) (void)hipFree(c->d_block_sums);
+  if (c->d_scan_part) (void)hipFree(c->d_scan_part);
   delete c;
 }
 
@@ -614,7 +621,13 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
     }
     a.offs = out_offsets ? out_offsets : ctx->d_offs;
     a.block_sums = ctx->d_block_sums;
-    if (e == hipSuccess && n) e = launch_general_encode(a, protocol, nb, s);
+    a.scan_part = ctx->d_scan_part;
+    if (e == hipSuccess && n) {
+      if (schema->has_prog[protocol] && program_encode_fits(rs))
+        e = launch_program_encode(a, schema->d_prog[protocol], ctx->d_scan_part, false, s);
+      else
+        e = launch_general_encode(a, protocol, nb, s);
+    }
   }
   if (e == hipSuccess && n) e = launch_encode_finish(a, protocol, fixed, s);
   ctx->last_op = 2;
@@ -654,6 +667,7 @@ int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   a.n = n;
   a.offs = out_offsets;
   a.block_sums = ctx->d_block_sums;
+  a.scan_part = ctx->d_scan_part;
   a.rec_size = schema->structs[0].size;
   a.res = ctx->d_res;
   a.cap = ~0ull;
@@ -664,7 +678,14 @@ int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   }
   (void)hipGetLastError();  // drop a stale error left by another library
   hipError_t e = launch_result_init(ctx->d_res, n, s);
-  if (e == hipSuccess && n) e = launch_general_size(a, protocol, (n + 255) / 256, s);
+  if (e == hipSuccess && n) {
+    if (schema->has_prog[protocol] && program_encode_fits(a.rec_size)) {
+      e = launch_program_encode(a, schema->d_prog[protocol], ctx->d_scan_part, true, s);
+      if (e == hipSuccess) e = launch_size_offsets(a, (n + 255) / 256, s);
+    } else {
+      e = launch_general_size(a, protocol, (n + 255) / 256, s);
+    }
+  }
   if (e == hipSuccess && n) e = launch_encode_finish(a, protocol, 0, s);
   if (e == hipSuccess && !n) e = hipMemsetAsync(out_offsets, 0, sizeof(uint64_t), s);
   if (e != hipSuccess) {

@@ -163,6 +163,7 @@ struct EncodeArgs {
   uint64_t cap;
   uint64_t* offs;  // n+1: sizes, then offsets
   unsigned long long* block_sums;
+  unsigned long long* scan_part;  // scan_tiles_parts(tiles) partial sums
   uint32_t rec_size;
   DevResult* res;
 };
@@ -208,6 +209,18 @@ hipError_t launch_general_size(const EncodeArgs& a, int protocol,
 hipError_t launch_encode_finish(const EncodeArgs& a, int protocol,
                                 uint64_t fixed_len, hipStream_t stream);
 hipError_t launch_result_init(DevResult* res, uint64_t n, hipStream_t stream);
+// Exclusive scan of nb per-tile byte counts in place; total -> res->total_bytes
+// and offs[n]. `part` holds scan_tiles_parts(nb) entries.
+hipError_t launch_scan_tiles(unsigned long long* sums, uint64_t nb, unsigned long long* part,
+                             DevResult* res, uint64_t* offs, uint64_t n, hipStream_t stream);
+uint64_t scan_tiles_parts(uint64_t nb);
+// Compiled-program encode (all-unqualified schemas): size pass, tile scan and,
+// unless size_only, the write pass. a.offs receives sizes then start offsets
+// (size_only: sizes, tile sums scanned; launch_size_offsets finishes them).
+bool program_encode_fits(uint32_t rec_size);
+hipError_t launch_program_encode(const EncodeArgs& a, const VProgram* d_prog,
+                                 unsigned long long* part, bool size_only, hipStream_t stream);
+hipError_t launch_size_offsets(const EncodeArgs& a, uint64_t n_blocks, hipStream_t stream);
 
 }  // namespace tgpu
 

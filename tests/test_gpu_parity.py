@@ -258,3 +258,66 @@ def test_program_path_with_irregular_records(gpu, name, every):
     assert np.array_equal(rec, orec)
     k = min(arena.size, oarena.size)
     assert np.array_equal(arena[:k], oarena[:k])
+
+
+def _long_string_records(n, seed, max_len):
+    """mixed-schema records with strings up to max_len bytes (tiles overflow
+    the encoder's LDS output tile, exercising its direct-to-HBM records)."""
+    schema = Schema.from_table(datagen.SCHEMAS["mixed"])
+    rng = np.random.default_rng(seed)
+    rec = np.zeros(n, dtype=schema.dtype())
+    for k in range(4):
+        rec["f%d" % (k + 1)] = rng.integers(-2**31, 2**31 - 1, n, dtype=np.int32)
+    lens = rng.integers(0, max_len + 1, (n, 2))
+    total = int(lens.sum())
+    sarena = rng.integers(0, 256, max(total, 1), dtype=np.uint8)
+    off = 0
+    for i in range(n):
+        for k in range(2):
+            rec["f%d" % (k + 5)][i]["offset"] = off
+            rec["f%d" % (k + 5)][i]["length"] = lens[i, k]
+            off += int(lens[i, k])
+    rec["__isset"] = 1
+    return schema, rec.view(np.uint8), sarena
+
+
+@pytest.mark.parametrize("proto", [0, 2])
+@pytest.mark.parametrize("max_len", [40, 3000])
+def test_program_encode_matches_oracle(gpu, proto, max_len):
+    """Compiled-program encode (records in the LDS output tile and, for long
+    strings, records written straight to HBM) == oracle bytes and offsets;
+    tgpu_encoded_size agrees."""
+    n = 5000
+    schema, rec, sarena = _long_string_records(n, 11 + max_len, max_len)
+    st, want, woffs = oracle.encode(schema, proto, rec, n, sarena, None)
+    assert st.code == 0
+    gs = _gschema(schema)
+    ser = _ser(proto)
+    wire, offs = ser.serialize(gs, _t(rec, gpu), n, _t(sarena, gpu))
+    assert bytes(_np(wire)) == want
+    assert np.array_equal(_np(offs).astype(np.uint64), woffs)
+    soffs, total = ser.encoded_size(gs, _t(rec, gpu), n)
+    assert total == len(want)
+    assert np.array_equal(_np(soffs).astype(np.uint64), woffs)
+
+
+@pytest.mark.parametrize("proto", [0, 2])
+def test_program_encode_output_overflow(gpu, proto):
+    """Output capacity ends inside record k: status OUTPUT_OVERFLOW at record
+    k (offset = its start), records before it written exactly."""
+    import torch
+
+    from fbthrift_amd.serializer import TgpuError
+
+    n = 3000
+    schema, rec, sarena = _long_string_records(n, 5, 60)
+    st, want, woffs = oracle.encode(schema, proto, rec, n, sarena, None)
+    k = 2345
+    cap = int(woffs[k]) + 3
+    gs = _gschema(schema)
+    out = torch.zeros(cap, dtype=torch.uint8, device=gpu)
+    with pytest.raises(TgpuError) as ei:
+        _ser(proto).serialize(gs, _t(rec, gpu), n, _t(sarena, gpu), out=out)
+    s = ei.value.status
+    assert (s.code, s.record, s.byte_offset) == (21, k, int(woffs[k]))
+    assert bytes(_np(out)[: int(woffs[k])]) == want[: int(woffs[k])]
