@@ -64,7 +64,7 @@ EXPORTS = [
     "tgpu_schema_create", "tgpu_schema_destroy", "tgpu_schema_record_size",
     "tgpu_schema_fixed_wire_size", "tgpu_context_create", "tgpu_context_destroy",
     "tgpu_context_reserve", "tgpu_context_wait", "tgpu_encode_batch", "tgpu_encoded_size",
-    "tgpu_decode_batch",
+    "tgpu_decode_batch", "tgpu_index_stream",
 ]
 
 _lib = None
@@ -112,5 +112,10 @@ def lib():
     L.tgpu_decode_batch.argtypes = [P, P, I32, P, U64, P, U64, P, P, U64,
                                     ctypes.POINTER(Limits), P, ctypes.POINTER(Status),
                                     ctypes.POINTER(U64), ctypes.POINTER(U64)]
+    L.tgpu_index_stream.restype = I32
+    L.tgpu_index_stream.argtypes = [P, P, I32, P, U64, U64, U64, I32, P, U64,
+                                    ctypes.POINTER(Limits), P, ctypes.POINTER(Status),
+                                    ctypes.POINTER(U64), ctypes.POINTER(U64),
+                                    ctypes.POINTER(U64)]
     _lib = L
     return L

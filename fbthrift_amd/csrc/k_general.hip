@@ -29,6 +29,8 @@ __global__ void result_init_kernel(DevResult* res, uint64_t n) {
   res->total_bytes = 0;
   res->n_records = n;
   res->n_irregular = 0;
+  res->first_start = kNone;
+  res->pad2 = 0;
 }
 
 __device__ __forceinline__ Reader make_reader(const DecodeArgs& a, uint64_t start) {
@@ -272,8 +274,8 @@ hipError_t launch_general_encode(const EncodeArgs& a, int protocol, uint64_t n_b
   } else {
     hipLaunchKernelGGL(encode_size_kernel<TGPU_PROTOCOL_COMPACT>, grid, dim3(256), 0, stream, a);
   }
-  const hipError_t e = launch_scan_tiles(a.block_sums, n_blocks, a.scan_part, a.res, a.offs, a.n,
-                                         stream);
+  const hipError_t e = launch_scan_tiles(a.block_sums, n_blocks, a.scan_part, &a.res->total_bytes,
+                                         a.offs + a.n, stream);
   if (e != hipSuccess) return e;
   if (protocol == TGPU_PROTOCOL_BINARY) {
     hipLaunchKernelGGL(encode_write_kernel<TGPU_PROTOCOL_BINARY>, grid, dim3(256), 0, stream, a);
@@ -292,8 +294,8 @@ hipError_t launch_general_size(const EncodeArgs& a, int protocol, uint64_t n_blo
   } else {
     hipLaunchKernelGGL(encode_size_kernel<TGPU_PROTOCOL_COMPACT>, grid, dim3(256), 0, stream, a);
   }
-  const hipError_t e = launch_scan_tiles(a.block_sums, n_blocks, a.scan_part, a.res, a.offs, a.n,
-                                         stream);
+  const hipError_t e = launch_scan_tiles(a.block_sums, n_blocks, a.scan_part, &a.res->total_bytes,
+                                         a.offs + a.n, stream);
   if (e != hipSuccess) return e;
   return launch_size_offsets(a, n_blocks, stream);
 }

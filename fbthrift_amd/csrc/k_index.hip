@@ -1,0 +1,325 @@
+// k_index.hip — record index of an unindexed stream: the bulk form of the
+// reference's file-reading loop `while (!cursor.isAtEnd()) deserialize<T>(c)`
+// (Serializer.h:97-100), which is sequential because record k+1 starts where
+// record k's readNoXfer stopped. Here the dependency is broken by speculation:
+//
+//   1. index_spec_kernel — one lane per chunk of `chunk` bytes. The lane tries
+//      candidate starts (chunk 0 of a non-speculative call: `begin` only) and
+//      accepts the first from which records parse back to back to the chunk's
+//      end, the first record in the canonical form (tgpu_program.h) and the
+//      rest canonical or, failing that, read by the general reader (exact
+//      readNoXfer consumption, tgpu_device.h). Result per chunk: s (first
+//      start), e (first start at or past the chunk's end), cnt (records).
+//   2. index_flag_kernel + scan + index_list_kernel — chunks whose link is
+//      broken (s[j] != e[j-1], or nothing accepted) in ascending order.
+//   3. index_fix_kernel — one lane walks the broken links in order from the
+//      true start, re-parses each with the general reader and follows the
+//      cascade until the chain agrees again; the first reader error ends the
+//      stream exactly where the reference would throw.
+//   4. scan of the per-chunk counts, index_emit_kernel writes every start
+//      (one lane per chunk, re-walking its chain), index_finish_kernel writes
+//      the end, the status and (decode) pads the index to the requested count.
+// Speculation only decides speed: every chunk the result uses was either
+// parsed from its verified true start or is linked to one by s[j] == e[j-1].
+#include "tgpu_program.h"
+
+namespace tgpu {
+namespace {
+
+constexpr uint64_t kNo = ~0ull;        // no start found / unset
+constexpr uint64_t kErr = ~0ull - 1;   // chain ended in a reader error
+constexpr uint32_t kPosCap = 0x7fffff00u;
+
+__device__ __forceinline__ dev::Reader reader_at(const IndexArgs& a, uint64_t pos) {
+  dev::Reader r;
+  r.p = a.in;
+  r.pos = pos;
+  r.end = a.in_len;
+  r.height = (int64_t)(a.height ? a.height : a.max_depth) + 1;
+  r.string_limit = a.string_limit;
+  r.container_limit = a.container_limit;
+  r.max_depth = a.max_depth;
+  r.err = 0;
+  r.err_off = 0;
+  r.has_bool = false;
+  r.bool_val = false;
+  return r;
+}
+
+struct Chain {
+  uint64_t end;    // first record start >= hi (or the failing record's start)
+  uint64_t count;  // records parsed
+  int32_t code;    // reader error (0: none)
+  uint64_t err_off;
+};
+
+// Records back to back from p while p < hi. canonical_first: the first record
+// must match the program (speculation); returns false if it does not.
+// emit: record starts written to emit[0..) (at most emit_cap).
+template <int P>
+__device__ bool chain(const IndexArgs& a, uint64_t p, uint64_t hi, bool canonical_first,
+                      uint8_t* scratch, Chain& out, uint64_t* emit, uint64_t emit_cap,
+                      uint64_t max_count) {
+  out.count = 0;
+  out.code = 0;
+  out.err_off = 0;
+  const prog::Ctx pc{0, nullptr, 0, a.string_limit, a.container_limit};
+  while (p < hi && out.count < max_count) {
+    uint64_t q = 0;
+    bool ok = false;
+    if (a.prog && p < a.in_len) {
+      const uint64_t avail = a.in_len - p;
+      const prog::HbmSrc src{a.in + p, (uint32_t)(avail < kPosCap ? avail : kPosCap)};
+      uint32_t rel = 0;
+      ok = prog::run_program<false>(a.prog, src, pc, rel, src.avail, nullptr);
+      q = p + rel;
+    }
+    if (!ok) {
+      // speculation: a candidate start must open with a canonical record
+      // (schemas without a program: any record the reader accepts)
+      if (canonical_first && out.count == 0 && a.prog) return false;
+      dev::Reader r = reader_at(a, p);
+      dev::read_record<P>(r, a.sc, scratch, nullptr, kDiscardArena);
+      if (!r.ok()) {
+        if (canonical_first && out.count == 0) return false;
+        out.code = r.err;
+        out.err_off = r.err_off;
+        out.end = p;
+        return true;
+      }
+      q = r.pos;
+    }
+    if (emit && out.count < emit_cap) emit[out.count] = p;
+    ++out.count;
+    p = q;
+  }
+  out.end = p;
+  return true;
+}
+
+__device__ __forceinline__ uint64_t chunk_lo(const IndexArgs& a, uint64_t j) {
+  return a.begin + j * a.chunk;
+}
+__device__ __forceinline__ uint64_t chunk_hi(const IndexArgs& a, uint64_t j) {
+  const uint64_t h = a.begin + (j + 1) * a.chunk;
+  return h < a.end ? h : a.end;
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void index_spec_kernel(IndexArgs a) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= a.n_chunks) return;
+  uint8_t* scratch = a.scratch + j * a.rec_size;
+  const uint64_t lo = chunk_lo(a, j), hi = chunk_hi(a, j);
+  Chain c;
+  if (j == 0 && !a.speculative) {
+    chain<P>(a, a.begin, hi, false, scratch, c, nullptr, 0, kNo);
+    a.s[0] = a.begin;
+    a.e[0] = c.code ? kErr : c.end;
+    a.cnt[j] = c.count;
+    return;
+  }
+  const uint64_t w = j == 0 ? a.chunk : a.window;  // a shard's first record may start late
+  const uint64_t last = lo + w < hi ? lo + w : hi;
+  for (uint64_t cand = lo; cand < last; ++cand) {
+    if (chain<P>(a, cand, hi, true, scratch, c, nullptr, 0, kNo) && c.code == 0) {
+      a.s[j] = cand;
+      a.e[j] = c.end;
+      a.cnt[j] = c.count;
+      return;
+    }
+  }
+  a.s[j] = kNo;
+  a.e[j] = kNo;
+  a.cnt[j] = 0;
+}
+
+__device__ __forceinline__ bool link_broken(const IndexArgs& a, uint64_t j) {
+  const uint64_t e = a.e[j];
+  if (e == kNo || e == kErr) return true;
+  if (j == 0) return a.s[0] == kNo;
+  return a.s[j] != a.e[j - 1];
+}
+
+__global__ __launch_bounds__(256) void index_flag_kernel(IndexArgs a) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j < a.n_chunks) a.base[j] = link_broken(a, j) ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void index_list_kernel(IndexArgs a) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j < a.n_chunks && link_broken(a, j)) a.bad[a.base[j]] = j;
+}
+
+// One lane: repair the chain (see header). scal[1] = chunks in effect.
+template <int P>
+__global__ void index_fix_kernel(IndexArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint64_t C = a.n_chunks;
+  a.scal[2] = kNo;
+  a.scal[1] = C;
+  uint64_t T0 = a.begin, j0 = 0;
+  if (a.speculative) {
+    // the first chunk with a speculated start opens the range (a record may
+    // cover the first chunks entirely); none at all: no record starts here
+    while (j0 < C && a.s[j0] == kNo) ++j0;
+    if (j0 == C) {
+      a.scal[1] = 0;
+      return;
+    }
+    T0 = a.s[j0];
+    for (uint64_t i = 0; i < j0; ++i) {
+      a.s[i] = T0;
+      a.e[i] = T0;
+      a.cnt[i] = 0;
+    }
+  }
+  const uint64_t m = a.scal[0];
+  uint64_t next = 0;  // chunks below are final
+  uint8_t* scratch = a.scratch;
+  for (uint64_t k = 0; k < m; ++k) {
+    uint64_t j = a.bad[k];
+    if (j < next || j < j0) continue;
+    uint64_t T = j == 0 ? T0 : a.e[j - 1];
+    for (;;) {
+      const uint64_t hi = chunk_hi(a, j);
+      if (T >= hi) {  // no record starts inside this chunk
+        a.s[j] = T;
+        a.e[j] = T;
+        a.cnt[j] = 0;
+      } else {
+        Chain c;
+        chain<P>(a, T, hi, false, scratch, c, nullptr, 0, kNo);
+        a.s[j] = T;
+        a.cnt[j] = c.count;
+        if (c.code) {
+          a.e[j] = c.end;
+          a.scal[1] = j + 1;
+          a.scal[2] = j;
+          a.scal[3] = c.count;
+          a.scal[4] = c.end;
+          a.res->code = c.code;
+          a.res->fail_offset = c.err_off;
+          return;
+        }
+        a.e[j] = c.end;
+      }
+      T = a.e[j];
+      if (j + 1 < C && (a.s[j + 1] != T || a.e[j + 1] == kNo || a.e[j + 1] == kErr)) {
+        ++j;
+        continue;
+      }
+      break;
+    }
+    next = j + 1;
+  }
+}
+
+__global__ __launch_bounds__(256) void index_prep_kernel(IndexArgs a) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j < a.n_chunks) a.base[j] = j < a.scal[1] ? a.cnt[j] : 0;
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void index_emit_kernel(IndexArgs a) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= a.scal[1]) return;
+  const uint64_t b = a.base[j];
+  const uint64_t n = a.cnt[j];
+  if (n == 0 || b > a.max_records) return;
+  const uint64_t cap = a.max_records + 1 - b;
+  Chain c;
+  chain<P>(a, a.s[j], kNo, false, a.scratch + j * a.rec_size, c, a.offs + b, cap, n);
+}
+
+// total records; end of the last one; status; decode padding of the index.
+__global__ void index_finish_kernel(IndexArgs a, unsigned long long* total_out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint64_t ce = a.scal[1];
+  uint64_t total = 0, end = a.begin;
+  if (ce) {
+    total = a.base[ce - 1] + a.cnt[ce - 1];
+    end = a.e[ce - 1];
+  }
+  DevResult* res = a.res;
+  res->first_start = ce ? a.s[0] : kNo;
+  if (a.scal[2] != kNo && ce) {  // reader error: total = records before it
+    res->first_fail = total;
+    end = a.scal[4];
+  } else if (!ce) {
+    end = a.speculative ? kNo : a.begin;  // no record starts in the range
+  }
+  res->n_records = total;
+  res->total_bytes = end;
+  if (total <= a.max_records) a.offs[total] = end;
+  *total_out = total;
+}
+
+// offs[total+1 .. fill_to] = offs[total]: records past the stream's end (or
+// its first bad record) re-read that position, so the decoder reports them
+// exactly (underflow / the same error) without a host round trip.
+__global__ __launch_bounds__(256) void index_pad_kernel(IndexArgs a,
+                                                        const unsigned long long* total_p) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t total = *total_p;
+  if (i > total && i <= a.fill_to && total <= a.max_records) a.offs[i] = a.offs[total];
+}
+
+__global__ __launch_bounds__(256) void index_empty_kernel(DevResult* res, uint64_t* offs,
+                                                          uint64_t pos, uint64_t fill_to) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i <= fill_to) offs[i] = pos;
+  if (i == 0) {
+    res->n_records = 0;
+    res->total_bytes = pos;
+    res->first_start = kNo;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_index_empty(DevResult* res, uint64_t* offs, uint64_t pos, uint64_t fill_to,
+                              hipStream_t stream) {
+  hipLaunchKernelGGL(index_empty_kernel, dim3((uint32_t)((fill_to + 256) / 256)), dim3(256), 0,
+                     stream, res, offs, pos, fill_to);
+  return hipGetLastError();
+}
+
+uint64_t index_chunk_bytes(uint64_t span) {
+  // ~1k+ chunks keep the chip busy; chunks stay >= 1 KiB so a chunk holds
+  // several records and speculation has a long chain to confirm
+  uint64_t c = 4096;
+  while (c > 1024 && span / c < 4096) c >>= 1;
+  return c;
+}
+
+hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream) {
+  const uint64_t C = a.n_chunks;
+  const dim3 g((uint32_t)((C + 255) / 256)), b(256);
+  if (a.protocol == TGPU_PROTOCOL_BINARY)
+    hipLaunchKernelGGL(index_spec_kernel<TGPU_PROTOCOL_BINARY>, g, b, 0, stream, a);
+  else
+    hipLaunchKernelGGL(index_spec_kernel<TGPU_PROTOCOL_COMPACT>, g, b, 0, stream, a);
+  hipLaunchKernelGGL(index_flag_kernel, g, b, 0, stream, a);
+  hipError_t e = launch_scan_tiles(a.base, C, a.part, a.scal, nullptr, stream);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(index_list_kernel, g, b, 0, stream, a);
+  if (a.protocol == TGPU_PROTOCOL_BINARY)
+    hipLaunchKernelGGL(index_fix_kernel<TGPU_PROTOCOL_BINARY>, dim3(1), dim3(64), 0, stream, a);
+  else
+    hipLaunchKernelGGL(index_fix_kernel<TGPU_PROTOCOL_COMPACT>, dim3(1), dim3(64), 0, stream, a);
+  hipLaunchKernelGGL(index_prep_kernel, g, b, 0, stream, a);
+  e = launch_scan_tiles(a.base, C, a.part, nullptr, nullptr, stream);
+  if (e != hipSuccess) return e;
+  if (a.protocol == TGPU_PROTOCOL_BINARY)
+    hipLaunchKernelGGL(index_emit_kernel<TGPU_PROTOCOL_BINARY>, g, b, 0, stream, a);
+  else
+    hipLaunchKernelGGL(index_emit_kernel<TGPU_PROTOCOL_COMPACT>, g, b, 0, stream, a);
+  hipLaunchKernelGGL(index_finish_kernel, dim3(1), dim3(64), 0, stream, a, a.scal + 5);
+  if (a.fill_to > 0)
+    hipLaunchKernelGGL(index_pad_kernel, dim3((uint32_t)((a.fill_to + 256) / 256)), b, 0, stream,
+                       a, a.scal + 5);
+  return hipGetLastError();
+}
+
+}  // namespace tgpu

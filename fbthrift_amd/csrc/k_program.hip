@@ -22,209 +22,13 @@
 #include <cstdio>
 #include <cstdlib>
 
-#include "tgpu_device.h"
+#include "tgpu_program.h"
 
 namespace tgpu {
 namespace {
 
 constexpr uint32_t kPT = 256;               // records per tile = threads per workgroup
 constexpr uint32_t kWireCap = 26 * 1024;    // default LDS bytes for one tile's wire bytes
-
-__device__ __forceinline__ uint64_t win8(const uint32_t* w32, uint32_t p) {
-  const uint32_t d = p >> 2, s = p & 3;
-  const uint32_t W0 = w32[d], W1 = w32[d + 1], W2 = w32[d + 2];
-  const uint32_t lo = __builtin_amdgcn_alignbyte(W1, W0, s);
-  const uint32_t hi = __builtin_amdgcn_alignbyte(W2, W1, s);
-  return ((uint64_t)hi << 32) | lo;
-}
-
-__device__ __forceinline__ uint64_t bswap_n(uint64_t x, uint32_t width) {
-  // the first `width` bytes of x (little-endian packed) as a big-endian number
-  const uint64_t b = __builtin_bswap64(x);
-  return width == 8 ? b : (b >> (64 - 8 * width));
-}
-
-// LEB128 at p (VarintUtils-inl.h:94-134): up to 8 bytes from one window,
-// 9-10 byte i64 varints byte-wise. Returns false (irregular) on anything the
-// fast path does not take (past `end`, more than ceil(bits/7) bytes).
-__device__ __forceinline__ bool read_varint(const uint32_t* w32, uint32_t& p, uint32_t end,
-                                            uint32_t bits, uint64_t& v) {
-  const uint64_t w = win8(w32, p);
-  const uint64_t stop = ~w & 0x8080808080808080ull;
-  if (stop) {
-    const uint32_t len = ((uint32_t)__builtin_ctzll(stop) >> 3) + 1;
-    if (p + len > end || (bits == 32 && len > 5)) return false;
-    uint64_t x = (len == 8 ? w : (w & ((1ull << (8 * len)) - 1))) & 0x7f7f7f7f7f7f7f7full;
-    x = ((x & 0x7f007f007f007f00ull) >> 1) | (x & 0x007f007f007f007full);
-    x = ((x & 0x3fff00003fff0000ull) >> 2) | (x & 0x00003fff00003fffull);
-    x = ((x & 0x0fffffff00000000ull) >> 4) | (x & 0x000000000fffffffull);
-    v = bits == 32 ? (x & 0xffffffffull) : x;
-    p += len;
-    return true;
-  }
-  if (bits == 32) return false;
-  // i64 varint of 9 or 10 bytes: 8 continuation bytes so far
-  uint64_t x = 0;
-  for (uint32_t i = 0; i < 10; ++i) {
-    if (p + i >= end) return false;
-    const uint64_t b = (win8(w32, p + i) & 0xff);
-    x |= (b & 0x7f) << (7 * i);
-    if (!(b & 0x80)) {
-      v = x;
-      p += i + 1;
-      return true;
-    }
-  }
-  return false;
-}
-
-__device__ __forceinline__ void store_n(uint8_t* dst, uint64_t v, uint32_t width) {
-  switch (width) {
-    case 8: *(uint64_t*)dst = v; break;
-    case 4: *(uint32_t*)dst = (uint32_t)v; break;
-    case 2: *(uint16_t*)dst = (uint16_t)v; break;
-    default: *dst = (uint8_t)v; break;
-  }
-}
-
-__device__ __forceinline__ uint64_t unzigzag(uint64_t z, uint32_t bits) {
-  if (bits == 32) {
-    const uint32_t n = (uint32_t)z;
-    return (uint64_t)(int64_t)(int32_t)((n >> 1) ^ (0u - (n & 1)));
-  }
-  return (z >> 1) ^ (0ull - (z & 1));
-}
-
-struct Ctx {
-  const uint32_t* w32;   // LDS wire tile
-  uint64_t gbase;        // stream offset of LDS byte 0
-  uint8_t* arena;
-  uint64_t arena_cap;
-  int32_t string_limit, container_limit;
-};
-
-// Runs the program over [p, end) (LDS positions); writes into rec (LDS).
-// PP: the program in LDS (VProgram*) or in HBM read through the scalar cache
-// (const VProgram* __restrict__ kernel argument).
-template <class PP>
-__device__ bool run_program(PP P, const Ctx& c, uint32_t p, uint32_t end, uint8_t* rec) {
-  const bool compact = P->protocol == TGPU_PROTOCOL_COMPACT;
-  const uint32_t n_ops = P->n_ops;
-  for (uint32_t k = 0; k < n_ops; ++k) {
-    const VOp op = P->ops[k];
-    switch (op.kind) {
-      case VOP_CONST: {
-        if (p + op.hdr_len > end) return false;
-        const uint32_t lo = (uint32_t)win8(c.w32, p);
-        const uint32_t mask = op.hdr_len >= 4 ? 0xffffffffu : ((1u << (8 * op.hdr_len)) - 1);
-        if ((lo ^ op.hdr) & mask) return false;
-        p += op.hdr_len;
-        break;
-      }
-      case VOP_CBOOL: {
-        if (p + op.hdr_len > end) return false;
-        const uint32_t lo = (uint32_t)win8(c.w32, p);
-        const uint32_t mask = (op.hdr_len >= 4 ? 0xffffffffu : ((1u << (8 * op.hdr_len)) - 1)) & ~0xfu;
-        const uint32_t ct = lo & 0xf;
-        if (((lo ^ op.hdr) & mask) || (ct != 1 && ct != 2)) return false;
-        rec[op.member] = ct == 1 ? 1 : 0;
-        p += op.hdr_len;
-        break;
-      }
-      case VOP_FIXED: {
-        if (p + op.width > end) return false;
-        const uint64_t v = bswap_n(win8(c.w32, p), op.width);
-        if (op.is_bool && v > 1) return false;  // readBool throws: general path
-        store_n(rec + op.member, v, op.width);
-        p += op.width;
-        break;
-      }
-      case VOP_VARINT: {
-        uint64_t z;
-        if (!read_varint(c.w32, p, end, op.bits, z)) return false;
-        store_n(rec + op.member, unzigzag(z, op.bits), op.width);
-        break;
-      }
-      case VOP_STRING: {
-        int64_t len;
-        if (compact) {
-          uint64_t z;
-          if (!read_varint(c.w32, p, end, 32, z)) return false;
-          len = (int32_t)(uint32_t)z;
-        } else {
-          if (p + 4 > end) return false;
-          len = (int32_t)(uint32_t)bswap_n(win8(c.w32, p), 4);
-          p += 4;
-        }
-        if (len < 0 || (c.string_limit > 0 && len > c.string_limit) || p + len > end) return false;
-        tgpu_span* sp = (tgpu_span*)(rec + op.member);
-        sp->offset = len ? c.gbase + p : 0;
-        sp->length = (uint32_t)len;
-        sp->reserved = 0;
-        p += (uint32_t)len;
-        break;
-      }
-      case VOP_LIST: {
-        int64_t n;
-        if (compact) {
-          if (p + 1 > end) return false;
-          const uint32_t b = (uint32_t)(win8(c.w32, p) & 0xff);
-          const uint32_t ct = b & 0xf;
-          const bool ok_ct = op.elem_ttype == TGPU_T_BOOL ? (ct == 1 || ct == 2) : ct == op.elem_ct;
-          if (!ok_ct) return false;
-          ++p;
-          n = b >> 4;
-          if (n == 15) {
-            uint64_t z;
-            if (!read_varint(c.w32, p, end, 32, z)) return false;
-            n = (int32_t)(uint32_t)z;
-          }
-        } else {
-          if (p + 5 > end) return false;
-          const uint64_t w = win8(c.w32, p);
-          if ((w & 0xff) != op.elem_ttype) return false;
-          n = (int32_t)(uint32_t)bswap_n(w >> 8, 4);
-          p += 5;
-        }
-        if (n < 0 || (c.container_limit && n > c.container_limit) || n > (int64_t)(end - p))
-          return false;
-        const uint64_t scale = compact ? 8 : 1;
-        const uint64_t aoff = scale * (c.gbase + p);
-        const uint32_t es = op.width;
-        if (n && (!c.arena || aoff + (uint64_t)n * es > c.arena_cap)) return false;
-        for (int64_t i = 0; i < n; ++i) {
-          uint64_t v;
-          if (op.elem_kind == VEL_VARINT) {
-            uint64_t z;
-            if (!read_varint(c.w32, p, end, op.bits, z)) return false;
-            v = unzigzag(z, op.bits);
-          } else {
-            const uint32_t wb = op.elem_kind == VEL_BOOL ? 1 : es;
-            if (p + wb > end) return false;
-            v = bswap_n(win8(c.w32, p), wb);
-            if (op.elem_kind == VEL_BOOL) {
-              if (compact) v = v == 1;
-              else if (v > 1) return false;
-            }
-            p += wb;
-          }
-          store_n(c.arena + aoff + (uint64_t)i * es, v, es);
-        }
-        tgpu_span* sp = (tgpu_span*)(rec + op.member);
-        sp->offset = n ? aoff : 0;
-        sp->length = (uint32_t)n;
-        sp->reserved = 0;
-        break;
-      }
-      case VOP_ISSET:
-        break;
-      default:
-        return false;
-    }
-    if (op.isset != 0xffff) rec[op.isset] = 1;
-  }
-  return p == end;
-}
 
 template <bool kSProg, bool kDirect>
 __global__ __launch_bounds__(kPT) void program_decode_kernel(DecodeArgs a,
@@ -280,13 +84,14 @@ __global__ __launch_bounds__(kPT) void program_decode_kernel(DecodeArgs a,
       const uint64_t s = a.offs[r0 + r], e = a.offs[r0 + r + 1];
       ok = s >= t0 && e >= s && e <= t1;
       if (ok) {
-        Ctx c{(const uint32_t*)wire, t0 - sh, a.arena, a.arena_cap, a.string_limit,
-              a.container_limit};
+        const prog::Ctx c{t0 - sh, a.arena, a.arena_cap, a.string_limit, a.container_limit};
+        const prog::LdsSrc src{(const uint32_t*)wire};
+        uint32_t p = (uint32_t)(s - t0) + sh;
+        const uint32_t pe = (uint32_t)(e - t0) + sh;
         if (kSProg)
-          ok = run_program(pp, c, (uint32_t)(s - t0) + sh, (uint32_t)(e - t0) + sh, rec);
+          ok = prog::run_program<true>(pp, src, c, p, pe, rec) && p == pe;
         else
-          ok = run_program((const VProgram*)P, c, (uint32_t)(s - t0) + sh,
-                           (uint32_t)(e - t0) + sh, rec);
+          ok = prog::run_program<true>((const VProgram*)P, src, c, p, pe, rec) && p == pe;
       }
     }
     if (!ok) {

@@ -353,7 +353,8 @@ __global__ __launch_bounds__(256) void scan_tiles_reduce(const unsigned long lon
 }
 
 __global__ __launch_bounds__(1024) void scan_tiles_top(unsigned long long* part, uint64_t np,
-                                                       DevResult* res, uint64_t* offs, uint64_t n) {
+                                                       unsigned long long* total1,
+                                                       uint64_t* total2) {
   __shared__ unsigned long long sm[1024];
   const uint64_t per = (np + 1023) / 1024;
   const uint64_t b = threadIdx.x * per, e = min(np, b + per);
@@ -374,8 +375,8 @@ __global__ __launch_bounds__(1024) void scan_tiles_top(unsigned long long* part,
     run += v;
   }
   if (threadIdx.x == 1023) {
-    res->total_bytes = sm[1023];
-    offs[n] = sm[1023];
+    if (total1) *total1 = sm[1023];
+    if (total2) *total2 = sm[1023];
   }
 }
 
@@ -403,10 +404,10 @@ __global__ __launch_bounds__(256) void scan_tiles_apply(unsigned long long* __re
 }  // namespace
 
 hipError_t launch_scan_tiles(unsigned long long* sums, uint64_t nb, unsigned long long* part,
-                             DevResult* res, uint64_t* offs, uint64_t n, hipStream_t stream) {
+                             unsigned long long* total1, uint64_t* total2, hipStream_t stream) {
   const uint64_t np = (nb + kScanChunk - 1) / kScanChunk;
   hipLaunchKernelGGL(scan_tiles_reduce, dim3((uint32_t)np), dim3(256), 0, stream, sums, nb, part);
-  hipLaunchKernelGGL(scan_tiles_top, dim3(1), dim3(1024), 0, stream, part, np, res, offs, n);
+  hipLaunchKernelGGL(scan_tiles_top, dim3(1), dim3(1024), 0, stream, part, np, total1, total2);
   hipLaunchKernelGGL(scan_tiles_apply, dim3((uint32_t)np), dim3(256), 0, stream, sums, nb, part);
   return hipGetLastError();
 }
@@ -423,7 +424,8 @@ hipError_t launch_program_encode(const EncodeArgs& a, const VProgram* d_prog,
   const uint64_t tiles = (a.n + kET - 1) / kET;
   const uint32_t rt = (kET * a.rec_size + 16 + 15) & ~15u;
   hipLaunchKernelGGL(program_size_kernel, dim3((uint32_t)tiles), dim3(kET), rt, stream, a, d_prog);
-  hipError_t e = launch_scan_tiles(a.block_sums, tiles, part, a.res, a.offs, a.n, stream);
+  hipError_t e = launch_scan_tiles(a.block_sums, tiles, part, &a.res->total_bytes, a.offs + a.n,
+                                   stream);
   if (e != hipSuccess || size_only) return e;
   hipLaunchKernelGGL(program_write_kernel, dim3((uint32_t)tiles), dim3(kET), rt + kOutCap + 32,
                      stream, a, d_prog);

@@ -37,7 +37,11 @@ struct tgpu_context {
   uint64_t* d_offs = nullptr;
   unsigned long long* d_block_sums = nullptr;
   unsigned long long* d_scan_part = nullptr;  // partial sums of the tile scan
+  uint64_t* d_irr = nullptr;                  // program decode: irregular record list
   uint64_t reserved = 0;  // records
+  // stream indexer workspace (per chunk)
+  uint8_t* d_index = nullptr;
+  uint64_t index_bytes = 0;
   int last_op = 0;        // 1 decode, 2 encode
 };
 
@@ -382,9 +386,11 @@ int ensure_workspace(tgpu_context* ctx, uint64_t n) {
   if (ctx->d_offs) (void)hipFree(ctx->d_offs);
   if (ctx->d_block_sums) (void)hipFree(ctx->d_block_sums);
   if (ctx->d_scan_part) (void)hipFree(ctx->d_scan_part);
+  if (ctx->d_irr) (void)hipFree(ctx->d_irr);
   ctx->d_offs = nullptr;
   ctx->d_block_sums = nullptr;
   ctx->d_scan_part = nullptr;
+  ctx->d_irr = nullptr;
   ctx->reserved = 0;
   const uint64_t tiles = (want + 255) / 256;
   if (hipMalloc(&ctx->d_offs, (want + 1) * sizeof(uint64_t)) != hipSuccess) return TGPU_ERR_HIP;
@@ -393,6 +399,7 @@ int ensure_workspace(tgpu_context* ctx, uint64_t n) {
   if (hipMalloc(&ctx->d_scan_part, (scan_tiles_parts(tiles) + 1) * sizeof(unsigned long long)) !=
       hipSuccess)
     return TGPU_ERR_HIP;
+  if (hipMalloc(&ctx->d_irr, want * sizeof(uint64_t)) != hipSuccess) return TGPU_ERR_HIP;
   ctx->reserved = want;
   return TGPU_OK;
 }
@@ -400,6 +407,82 @@ int ensure_workspace(tgpu_context* ctx, uint64_t n) {
 DevSchema dev_schema(const tgpu_schema* s) {
   return DevSchema{s->d_structs, s->d_fields, (uint32_t)s->structs.size(),
                    (uint32_t)s->fields.size()};
+}
+
+// Indexed decode (a.offs = record starts): compiled-program fast path, then
+// the general decoder for the records it hands over; general decoder only
+// when the schema has no program or the limits forbid its fast path (a list
+// depth of 1 must be allowed: the program never skips, so max_depth is not
+// reached otherwise).
+hipError_t launch_indexed_decode(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                                 const DecodeArgs& a, hipStream_t s) {
+  const int32_t height = a.height ? a.height : a.max_depth;
+  if (schema->has_prog[protocol] && height >= 2 && a.max_depth >= 2) {
+    hipError_t e = launch_program_decode(a, schema->d_prog[protocol], a.rec_size, ctx->d_irr,
+                                         &ctx->d_res->n_irregular, s);
+    if (e == hipSuccess)
+      e = launch_general_decode_list(a, protocol, ctx->d_irr, &ctx->d_res->n_irregular, s);
+    return e;
+  }
+  return launch_general_decode(a, protocol, s);
+}
+
+// Stream index into offs (max_records + 1 entries); see launch_index_stream.
+// Returns a TGPU_ERR_* for host-side failures; HIP launch errors go to `e`.
+int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, const uint8_t* in,
+                 uint64_t in_len, uint64_t begin, uint64_t end, int speculative, uint64_t* offs,
+                 uint64_t max_records, uint64_t fill_to, const tgpu_limits* limits,
+                 hipStream_t s, hipError_t& e) {
+  IndexArgs x{};
+  x.sc = dev_schema(schema);
+  x.in = in;
+  x.in_len = in_len;
+  x.begin = begin;
+  x.end = end;
+  x.speculative = speculative;
+  x.protocol = protocol;
+  x.chunk = index_chunk_bytes(end > begin ? end - begin : 0);
+  x.window = (uint32_t)std::min<uint64_t>(x.chunk, 1024);
+  x.rec_size = schema->structs[0].size;
+  x.n_chunks = end > begin ? (end - begin + x.chunk - 1) / x.chunk : 0;
+  x.string_limit = limits ? limits->string_limit : 0;
+  x.container_limit = limits ? limits->container_limit : 0;
+  x.max_depth = limits ? limits->max_depth : 12000;
+  x.height = limits ? limits->height : 0;
+  const int32_t height = x.height ? x.height : x.max_depth;
+  x.prog = schema->has_prog[protocol] && height >= 2 && x.max_depth >= 2
+               ? schema->d_prog[protocol] : nullptr;
+  x.offs = offs;
+  x.max_records = max_records;
+  x.fill_to = fill_to;
+  x.res = ctx->d_res;
+  const uint64_t C = std::max<uint64_t>(x.n_chunks, 1);
+  const uint64_t rs = (x.rec_size + 7) & ~7u;
+  const uint64_t parts = scan_tiles_parts(C) + 1;
+  const uint64_t need = 8 * (5 * C + parts + 8) + C * rs;
+  if (need > ctx->index_bytes) {
+    if (ctx->d_index) (void)hipFree(ctx->d_index);
+    ctx->d_index = nullptr;
+    ctx->index_bytes = 0;
+    if (hipMalloc(&ctx->d_index, need) != hipSuccess) return TGPU_ERR_HIP;
+    ctx->index_bytes = need;
+  }
+  uint64_t* w = (uint64_t*)ctx->d_index;
+  x.s = w;
+  x.e = w + C;
+  x.cnt = (unsigned long long*)(w + 2 * C);
+  x.base = (unsigned long long*)(w + 3 * C);
+  x.bad = (unsigned long long*)(w + 4 * C);
+  x.part = (unsigned long long*)(w + 5 * C);
+  x.scal = (unsigned long long*)(w + 5 * C + parts);
+  x.scratch = (uint8_t*)(w + 5 * C + parts + 8);
+  if (x.n_chunks == 0) {
+    // nothing starts in [begin, end): the index is just the end position
+    if (e == hipSuccess) e = launch_index_empty(x.res, offs, x.begin, fill_to, s);
+    return TGPU_OK;
+  }
+  if (e == hipSuccess) e = launch_index_stream(x, s);
+  return TGPU_OK;
 }
 
 }  // namespace
@@ -546,6 +629,8 @@ void tgpu_context_destroy(tgpu_context* c) {
   if (c->d_offs) (void)hipFree(c->d_offs);
   if (c->d_block_sums) (void)hipFree(c->d_block_sums);
   if (c->d_scan_part) (void)hipFree(c->d_scan_part);
+  if (c->d_irr) (void)hipFree(c->d_irr);
+  if (c->d_index) (void)hipFree(c->d_index);
   delete c;
 }
 
@@ -750,24 +835,22 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   } else if (n) {
     if (offsets) {
       a.offs = offsets;
-      a.check_index = 1;
-      // compiled-program fast path; a list depth of 1 must be allowed by the
-      // limits (the program never skips, so max_depth is not reached)
-      const int32_t height = a.height ? a.height : a.max_depth;
-      if (schema->has_prog[protocol] && height >= 2 && a.max_depth >= 2) {
-        if (e == hipSuccess)
-          e = launch_program_decode(a, schema->d_prog[protocol], a.rec_size, ctx->d_offs,
-                                    &ctx->d_res->n_irregular, s);
-        if (e == hipSuccess)
-          e = launch_general_decode_list(a, protocol, ctx->d_offs, &ctx->d_res->n_irregular, s);
-      } else if (e == hipSuccess) {
-        e = launch_general_decode(a, protocol, s);
-      }
     } else {
+      // unindexed: build the record index on the device first (k_index.hip);
+      // records past the stream's end / its first bad record re-read that
+      // position, so the decoder reports them exactly
       a.offs = ctx->d_offs;
-      a.check_index = 0;
-      if (e == hipSuccess) e = launch_serial_decode(a, protocol, false, 0, s);
+      if (e == hipSuccess) {
+        const int irc = launch_index(ctx, schema, protocol, a.in, in_len, 0, in_len, 0, ctx->d_offs,
+                                     n, n, limits, s, e);
+        if (irc) {
+          fill_status(st, irc, 0, 0);
+          return irc;
+        }
+      }
     }
+    a.check_index = 1;
+    if (e == hipSuccess) e = launch_indexed_decode(ctx, schema, protocol, a, s);
   }
   if (e == hipSuccess && n) e = launch_decode_finish(a, protocol, fixed, s);
   ctx->last_op = 1;
@@ -781,6 +864,54 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
     return tgpu_context_wait(ctx, stream, st ? st : &tmp, n_decoded, consumed);
   }
   return TGPU_OK;
+}
+
+int tgpu_index_stream(tgpu_context* ctx, const tgpu_schema* schema, int protocol, const void* in,
+                      uint64_t in_len, uint64_t begin, uint64_t end, int speculative,
+                      uint64_t* offsets, uint64_t max_records, const tgpu_limits* limits,
+                      void* stream, tgpu_status* st, uint64_t* n_records, uint64_t* first_start,
+                      uint64_t* last_end) {
+  if (!ctx || !schema || !offsets ||
+      (protocol != TGPU_PROTOCOL_BINARY && protocol != TGPU_PROTOCOL_COMPACT) ||
+      (!in && in_len) || begin > end || end > in_len) {
+    fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+    return TGPU_ERR_INVALID_ARGUMENT;
+  }
+  const hipStream_t s = (hipStream_t)stream;
+  (void)hipGetLastError();  // drop a stale error left by another library
+  hipError_t e = launch_result_init(ctx->d_res, 0, s);
+  const int rc = launch_index(ctx, schema, protocol, (const uint8_t*)in, in_len, begin, end,
+                              speculative, offsets, max_records, 0, limits, s, e);
+  if (rc) {
+    fill_status(st, rc, 0, 0);
+    return rc;
+  }
+  ctx->last_op = 3;
+  if (e != hipSuccess) {
+    fill_status(st, TGPU_ERR_HIP, 0, 0);
+    if (st) st->reserved = (int32_t)e;
+    return TGPU_ERR_HIP;
+  }
+  if (!st && !n_records && !first_start && !last_end) return TGPU_OK;
+  e = hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    fill_status(st, TGPU_ERR_HIP, 0, 0);
+    if (st) st->reserved = (int32_t)e;
+    return TGPU_ERR_HIP;
+  }
+  const DevResult& r = *ctx->h_res;
+  int code = r.code;
+  uint64_t rec = code ? r.first_fail : r.n_records, off = code ? r.fail_offset : 0;
+  if (!code && r.n_records > max_records) {
+    code = TGPU_ERR_OUTPUT_OVERFLOW;
+    rec = max_records;
+  }
+  fill_status(st, code, rec, off);
+  if (n_records) *n_records = r.n_records;
+  if (first_start) *first_start = r.first_start;
+  if (last_end) *last_end = r.total_bytes;
+  return code;
 }
 
 }  // extern "C"

@@ -490,7 +490,11 @@ __device__ void read_list(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8
     if (r.end - r.pos < (uint64_t)(uint32_t)n) return r.fail(TGPU_ERR_TRUNCATED, r.pos);
     const uint32_t es = scalar_size(f.elem_ttype);
     const uint64_t aoff = Pr::kArenaScale * r.pos;
-    if (n > 0) {
+    if (n > 0 && !arena && arena_cap == kDiscardArena) {
+      // measuring only (stream indexer): validate and consume, store nothing
+      uint8_t tmp[8];
+      for (int32_t i = 0; i < n && r.ok(); ++i) Pr::read_scalar(r, f.elem_ttype, tmp);
+    } else if (n > 0) {
       if (!arena) return r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
       // the list is resized to n before the element reads
       sp.offset = aoff;

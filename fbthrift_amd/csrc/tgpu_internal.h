@@ -22,6 +22,9 @@ constexpr int kMaxTemplateItems = 96;
 // Nesting supported by the general device reader/writer.
 constexpr int kMaxSchemaDepth = 8;
 constexpr int kMaxSkipDepth = 32;
+// arena == nullptr with this capacity: list elements are read and validated
+// but not stored (the stream indexer measures records without output).
+constexpr uint64_t kDiscardArena = ~0ull;
 
 // One step of the canonical Binary wire template of a fixed-layout schema
 // (every field unqualified, fixed width; nested structs flattened). The item
@@ -130,6 +133,8 @@ struct DevResult {
   unsigned long long total_bytes;      // encode: output size; decode: consumed
   unsigned long long n_records;
   unsigned long long n_irregular;      // program path: records sent to the general decoder
+  unsigned long long first_start;      // stream index: first record start found
+  unsigned long long pad2;
 };
 
 struct DevSchema {
@@ -209,10 +214,11 @@ hipError_t launch_general_size(const EncodeArgs& a, int protocol,
 hipError_t launch_encode_finish(const EncodeArgs& a, int protocol,
                                 uint64_t fixed_len, hipStream_t stream);
 hipError_t launch_result_init(DevResult* res, uint64_t n, hipStream_t stream);
-// Exclusive scan of nb per-tile byte counts in place; total -> res->total_bytes
-// and offs[n]. `part` holds scan_tiles_parts(nb) entries.
+// Exclusive scan of nb per-tile byte counts in place; the total goes to
+// *total1 and *total2 (either may be null). `part` holds scan_tiles_parts(nb)
+// entries.
 hipError_t launch_scan_tiles(unsigned long long* sums, uint64_t nb, unsigned long long* part,
-                             DevResult* res, uint64_t* offs, uint64_t n, hipStream_t stream);
+                             unsigned long long* total1, uint64_t* total2, hipStream_t stream);
 uint64_t scan_tiles_parts(uint64_t nb);
 // Compiled-program encode (all-unqualified schemas): size pass, tile scan and,
 // unless size_only, the write pass. a.offs receives sizes then start offsets
@@ -221,6 +227,44 @@ bool program_encode_fits(uint32_t rec_size);
 hipError_t launch_program_encode(const EncodeArgs& a, const VProgram* d_prog,
                                  unsigned long long* part, bool size_only, hipStream_t stream);
 hipError_t launch_size_offsets(const EncodeArgs& a, uint64_t n_blocks, hipStream_t stream);
+
+// ---- stream indexer (k_index.hip) -------------------------------------------
+// Finds the start of every record beginning in [begin, end) of an unindexed
+// stream: lanes speculate record starts per chunk, a serial pass repairs the
+// chunk chain where speculation was wrong, the starts are emitted in order.
+struct IndexArgs {
+  DevSchema sc;
+  const uint8_t* in;
+  uint64_t in_len;
+  uint64_t begin, end;
+  int32_t speculative;
+  int32_t protocol;
+  uint64_t chunk;      // bytes of record starts per chunk
+  uint32_t window;     // candidate starts tried per chunk
+  uint32_t rec_size;
+  uint64_t n_chunks;
+  int32_t string_limit, container_limit, max_depth, height;
+  const VProgram* prog;  // canonical-form program (nullptr: general reader only)
+  // per chunk: speculated/verified first start, end of the chain, record count
+  uint64_t* s;
+  uint64_t* e;
+  unsigned long long* cnt;
+  unsigned long long* base;  // flags, then exclusive record-count prefix
+  unsigned long long* bad;   // chunks whose chain link failed (in order)
+  unsigned long long* part;  // scan partials
+  unsigned long long* scal;  // [0] bad count, [1] chunks in effect, [2] error chunk,
+                             // [3] records before the error in it, [4] error record start
+  uint8_t* scratch;          // n_chunks * rec_size: general-reader output (discarded)
+  uint64_t* offs;            // record starts (max_records + 1)
+  uint64_t max_records;
+  uint64_t fill_to;          // decode: offs[total+1 .. fill_to] = last end
+  DevResult* res;
+};
+uint64_t index_chunk_bytes(uint64_t span);
+hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream);
+// Empty range: offs[0..fill_to] = pos, no records.
+hipError_t launch_index_empty(DevResult* res, uint64_t* offs, uint64_t pos, uint64_t fill_to,
+                              hipStream_t stream);
 
 }  // namespace tgpu
 

@@ -255,5 +255,35 @@ class BatchSerializer:
         return records, arena, st, n_dec.value, consumed.value
 
 
+    # -- stream index -------------------------------------------------------
+    def index_stream(self, gschema, wire, begin=0, end=None, speculative=False,
+                     max_records=None, offsets=None, limits=None, stream=None, check=True):
+        """Record starts of an unindexed stream (tgpu_index_stream): the records
+        beginning in [begin, end) of `wire` (a uint8 device tensor; records may
+        run past `end`). Returns (offsets[:n+1], n, first_start, last_end,
+        status); raises on a reader error when `check`."""
+        import torch
+
+        end = wire.numel() if end is None else end
+        if max_records is None:
+            max_records = max(end - begin, 0)
+        if offsets is None:
+            offsets = torch.empty(max_records + 1, dtype=torch.int64, device=wire.device)
+        lim = None
+        if limits is not None:
+            lim = _lib.Limits(*limits) if not isinstance(limits, _lib.Limits) else limits
+        st = _lib.Status()
+        n, first, last = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.lib().tgpu_index_stream(
+            self.context().handle, gschema.handle, self.protocol, _ptr(wire), wire.numel(),
+            begin, end, 1 if speculative else 0, _ptr(offsets), max_records,
+            ctypes.byref(lim) if lim is not None else None, _stream(stream), ctypes.byref(st),
+            ctypes.byref(n), ctypes.byref(first), ctypes.byref(last))
+        if check:
+            raise_for_status(st)
+        k = min(n.value, max_records)
+        return offsets[: k + 1], n.value, first.value, last.value, st
+
+
 BinarySerializer = BatchSerializer(PROTOCOL_BINARY)
 CompactSerializer = BatchSerializer(PROTOCOL_COMPACT)

@@ -18,6 +18,9 @@
  *  tgpu_encode_batch
  *      N x Serializer<R,W>::serialize(obj, &queue) appending to one IOBufQueue
  *      (thrift/lib/cpp2/protocol/Serializer.h:136-148) i.e. N x T::write<P>.
+ *  tgpu_index_stream
+ *      the record boundaries that repeated deserialize<T>(Cursor&) walks over
+ *      a concatenated stream (Serializer.h:97-100), found in parallel.
  *  tgpu_decode_batch
  *      N x Serializer<R,W>::deserialize<T>(Cursor&) over a concatenated record
  *      stream (Serializer.h:97-100, :192-204), i.e. N x T::readNoXfer<P>.
@@ -274,6 +277,33 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema,
                       uint64_t list_arena_capacity, const tgpu_limits* limits,
                       void* stream, tgpu_status* st, uint64_t* n_decoded,
                       uint64_t* consumed);
+
+/* ---- stream index ----------------------------------------------------- */
+/*
+ * Record index of an unindexed stream — the bulk form of the file-reading
+ * loop `while (!cursor.isAtEnd()) deserialize<T>(cursor)` over back-to-back
+ * records (thrift/lib/cpp2/protocol/Serializer.h:97-100): the start of every
+ * record that begins in [begin, end) of in[0..in_len). Records may run past
+ * `end` up to in_len (a shard's overlap with the next shard).
+ *
+ * begin must be a record boundary, unless `speculative` is set: then the first
+ * record start at or after begin is discovered (*first_start) — one shard of
+ * a file split by bytes, whose first boundary is confirmed by the previous
+ * shard's *last_end (the only exchange between shards).
+ *
+ * offsets (device, max_records + 1 entries) receives the starts, then the end
+ * of the last record. Errors: the first record the reader rejects ends the
+ * index with that record's exact reference status (st->record = its index,
+ * offsets[st->record] = its start); more than max_records records ->
+ * TGPU_ERR_OUTPUT_OVERFLOW with *n_records = the number found; speculative
+ * call with no record start in the first chunk -> TGPU_ERR_UNSUPPORTED.
+ * Blocking when st != NULL (then n_records / first_start / last_end are filled).
+ */
+int tgpu_index_stream(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                      const void* in, uint64_t in_len, uint64_t begin, uint64_t end,
+                      int speculative, uint64_t* offsets, uint64_t max_records,
+                      const tgpu_limits* limits, void* stream, tgpu_status* st,
+                      uint64_t* n_records, uint64_t* first_start, uint64_t* last_end);
 
 #ifdef __cplusplus
 } /* extern "C" */

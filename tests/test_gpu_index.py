@@ -1,0 +1,159 @@
+"""Stream index (tgpu_index_stream) and the unindexed decode built on it:
+record boundaries of back-to-back records found in parallel must equal the
+sequential reference walk (repeated deserialize<T>(Cursor&)) — the oracle's
+record offsets — including speculative shards of a stream split by bytes,
+records longer than an index chunk, non-canonical records and a malformed
+record in the middle of a long stream."""
+import numpy as np
+import pytest
+
+import datagen
+import helpers
+from fbthrift_amd.schema import Schema
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _t(a, dev):
+    import torch
+
+    a = np.frombuffer(bytes(a), np.uint8) if isinstance(a, (bytes, bytearray)) else a
+    a = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+    if a.size == 0:
+        a = np.zeros(1, np.uint8)
+    return torch.from_numpy(a.copy()).to(dev)
+
+
+def _ser(protocol):
+    from fbthrift_amd.serializer import BinarySerializer, CompactSerializer
+
+    return BinarySerializer if protocol == 0 else CompactSerializer
+
+
+def _gs(schema):
+    from fbthrift_amd.serializer import GpuSchema
+
+    return GpuSchema(schema)
+
+
+def _stream(sname, proto, n, seed=0, max_len=None):
+    table = datagen.SCHEMAS[sname]
+    schema = Schema.from_table(table)
+    if max_len is None:
+        gen = {"mixed": datagen.gen_mixed, "nested": datagen.gen_nested,
+               "scalars": datagen.gen_scalars, "sparse": datagen.gen_sparse}[sname]
+        vals = datagen.flatten_values(table, [gen(i + seed) for i in range(n)])
+        rec, sarena, larena = helpers.pack(schema, vals, n)
+    else:  # mixed with long strings
+        rng = np.random.default_rng(seed)
+        r = np.zeros(n, dtype=schema.dtype())
+        for k in range(4):
+            r["f%d" % (k + 1)] = rng.integers(-2**31, 2**31 - 1, n, dtype=np.int32)
+        lens = rng.integers(0, max_len + 1, (n, 2))
+        sarena = rng.integers(0, 256, max(int(lens.sum()), 1), dtype=np.uint8)
+        off = 0
+        for i in range(n):
+            for k in range(2):
+                r["f%d" % (k + 5)][i]["offset"] = off
+                r["f%d" % (k + 5)][i]["length"] = lens[i, k]
+                off += int(lens[i, k])
+        r["__isset"] = 1
+        rec, larena = r.view(np.uint8), None
+    st, wire, offs = oracle.encode(schema, proto, rec, n, sarena, larena)
+    assert st.code == 0
+    return schema, wire, offs.astype(np.uint64)
+
+
+@pytest.mark.parametrize("name", helpers.case_names())
+def test_index_golden(gpu, name):
+    c = helpers.Case(name)
+    offs, n, first, last, st = _ser(c.protocol).index_stream(_gs(c.schema), _t(c.wire, gpu))
+    assert st.code == 0 and n == c.n and first == 0 and last == len(c.wire)
+    assert np.array_equal(offs.cpu().numpy().astype(np.uint64), c.offsets.astype(np.uint64))
+
+
+@pytest.mark.parametrize("sname,proto", [("mixed", 2), ("mixed", 0), ("nested", 0),
+                                         ("nested", 2), ("scalars", 2), ("sparse", 2)])
+def test_index_and_unindexed_decode_large(gpu, sname, proto):
+    """100k-record streams: index == oracle offsets; unindexed decode ==
+    oracle decode (records, consumed)."""
+    n = 100_000 if sname in ("mixed", "nested") else 30_000
+    schema, wire, woffs = _stream(sname, proto, n)
+    gs = _gs(schema)
+    w = _t(wire, gpu)
+    offs, got, first, last, st = _ser(proto).index_stream(gs, w)
+    assert (st.code, got, first, last) == (0, n, 0, len(wire))
+    assert np.array_equal(offs.cpu().numpy().astype(np.uint64), woffs)
+    rec, arena, st2, nd, cons = _ser(proto).deserialize_status(gs, w[: len(wire)], n)
+    ost, orec, oarena, ond, ocons = oracle.decode(schema, proto, wire, n)
+    assert st2.as_tuple() == ost.as_tuple() and st2.code == 0
+    assert (nd, cons) == (ond, ocons) == (n, len(wire))
+    assert np.array_equal(rec.cpu().numpy(), orec)
+
+
+@pytest.mark.parametrize("proto", [2, 0])
+@pytest.mark.parametrize("max_len", [30, 3000])
+def test_index_speculative_shards(gpu, proto, max_len):
+    """The stream split into byte ranges at arbitrary positions: each range
+    indexed speculatively finds the first record start at/after its begin,
+    exactly the oracle's, and its last_end is the next range's first start."""
+    n = 40_000 if max_len == 30 else 3000
+    schema, wire, woffs = _stream("mixed", proto, n, seed=5, max_len=max_len)
+    gs = _gs(schema)
+    w = _t(wire, gpu)
+    L = len(wire)
+    cuts = [0] + sorted(np.random.default_rng(1).integers(1, L, 6).tolist()) + [L]
+    prev_last = None
+    for b, e in zip(cuts[:-1], cuts[1:]):
+        offs, got, first, last, st = _ser(proto).index_stream(
+            gs, w[:L], begin=b, end=e, speculative=b > 0)
+        inside = woffs[(woffs >= b) & (woffs < e)]
+        want_last = woffs[np.searchsorted(woffs, e)] if e < L else L
+        if inside.size == 0:
+            # no record starts in this range (a record covers it): nothing found
+            assert st.code == 0 and got == 0
+            continue
+        assert st.code == 0, st.as_tuple()
+        assert first == inside[0] and got == inside.size and last == want_last
+        assert np.array_equal(offs.cpu().numpy()[:-1].astype(np.uint64), inside)
+        if prev_last is not None:
+            assert prev_last == first
+        prev_last = last
+
+
+def test_index_error_mid_stream(gpu):
+    """A malformed record deep in a long unindexed stream: index and decode
+    both report the reference status at that record; records before it are
+    decoded exactly."""
+    proto = 2
+    n = 50_000
+    schema, wire, woffs = _stream("mixed", proto, n, seed=9)
+    bad = 37_123
+    w = bytearray(wire)
+    w[int(woffs[bad])] = 0x1E  # field header with ctype 14: "don't know what type"
+    wire = bytes(w)
+    gs = _gs(schema)
+    t = _t(wire, gpu)
+    offs, got, first, last, st = _ser(proto).index_stream(gs, t, check=False)
+    ost, orec, _, ond, ocons = oracle.decode(schema, proto, wire, n)
+    assert ost.code != 0 and ost.record == bad
+    assert st.as_tuple() == ost.as_tuple()
+    assert got == bad and last == woffs[bad]
+    rec, arena, gst, nd, cons = _ser(proto).deserialize_status(gs, t, n)
+    assert gst.as_tuple() == ost.as_tuple() and (nd, cons) == (ond, ocons)
+    k = bad * schema.record_size
+    assert np.array_equal(rec.cpu().numpy()[:k], orec[:k])
+
+
+def test_unindexed_decode_past_end(gpu):
+    """Asking for more records than the stream holds: the first missing
+    record underflows exactly like the reference's cursor."""
+    proto = 2
+    n = 5000
+    schema, wire, woffs = _stream("mixed", proto, n, seed=3)
+    gs = _gs(schema)
+    rec, arena, gst, nd, cons = _ser(proto).deserialize_status(gs, _t(wire, gpu), n + 7)
+    ost, orec, _, ond, ocons = oracle.decode(schema, proto, wire, n + 7)
+    assert gst.as_tuple() == ost.as_tuple() and gst.record == n
+    assert (nd, cons) == (ond, ocons)

@@ -198,8 +198,6 @@ def test_config_shapes_roundtrip(gpu, sname, proto):
     assert bytes(_np(wire)) == want
     assert np.array_equal(_np(offs).astype(np.uint64), woffs)
     for indexed in (True, False):
-        if not indexed and n > 20_000:
-            continue  # the unindexed variable-length path is serial (one lane)
         gst, grec, garena, gnd, gcons = gpu_decode(schema, proto, want, n,
                                                    woffs if indexed else None, dev=gpu)
         ost, orec, oarena, _, _ = oracle.decode(schema, proto, want, n,
@@ -321,3 +319,27 @@ def test_program_encode_output_overflow(gpu, proto):
     s = ei.value.status
     assert (s.code, s.record, s.byte_offset) == (21, k, int(woffs[k]))
     assert bytes(_np(out)[: int(woffs[k])]) == want[: int(woffs[k])]
+
+
+@pytest.mark.parametrize("proto", [0, 2])
+def test_program_decode_oversized_tiles(gpu, proto):
+    """Indexed decode where a few tiles are far above the batch's mean size
+    (the LDS wire tile is sized from the mean): those tiles go through the
+    general decoder, the rest through the program path; == oracle."""
+    n = 6000
+    schema, rec, sarena = _long_string_records(n, 99, 12)
+    r = rec.view(schema.dtype())
+    big = np.zeros(0, np.uint8)
+    off = sarena.size
+    for i in range(1000, 1100):
+        r["f5"][i]["offset"] = off + big.size
+        r["f5"][i]["length"] = 3000
+        big = np.concatenate([big, np.full(3000, i % 251, np.uint8)])
+    sarena = np.concatenate([sarena, big])
+    st, want, woffs = oracle.encode(schema, proto, r.view(np.uint8), n, sarena, None)
+    assert st.code == 0
+    gst, grec, _, gnd, gcons = gpu_decode(schema, proto, want, n, woffs, dev=gpu)
+    ost, orec, _, ond, ocons = oracle.decode(schema, proto, want, n, offsets=woffs)
+    assert gst.as_tuple() == ost.as_tuple() and gst.code == 0
+    assert (gnd, gcons) == (ond, ocons) == (n, len(want))
+    assert np.array_equal(grec, orec)
