@@ -94,6 +94,7 @@ def cpu_baseline(seconds=12.0):
 
 class Workload:
     """One BASELINE config: resident inputs, one encode+decode step, checks."""
+    total_wire_bytes = None  # whole-job bytes per direction (default: per rank x world)
 
     def timed_step(self, ev):
         ev[0].record(self.stream)
@@ -101,6 +102,11 @@ class Workload:
         ev[1].record(self.stream)
         self.decode()
         ev[2].record(self.stream)
+
+    def check_timed(self):
+        st, nd, consumed = self.S.context().wait()
+        if st.code or consumed != self.wire_bytes:
+            raise RuntimeError("timed decode failed: %s" % (st.as_tuple(),))
 
 
 class Flat8(Workload):
@@ -255,7 +261,169 @@ class Nested(VarLen):
     span_offsets, elem_width = (8,), 4
 
 
-WORKLOADS = {2: Flat8, 3: Mixed, 4: Nested}
+class FileShards(Mixed):
+    """Config 5: one Compact file of {4 x i32, 2 x string} records, split by
+    BYTES across the ranks (64 Mi records encoded per rank, weak scaling).
+
+    Step: every rank encodes its 64 Mi records (its part of the file, in file
+    order); the file's byte ranges are redistributed so rank k holds
+    [B_k, B_{k+1} + overlap) (all_to_all over RCCL; nothing at N=1); rank k
+    indexes its range speculatively (tgpu_index_stream: rank 0 from the
+    file's first byte) and confirms its first record start against rank
+    k-1's last end (fbthrift_amd/shard.py: all-gather of 5 int64 per rank,
+    re-index on disagreement); then it decodes the records that start in its
+    range. Checked after warm-up: per-rank record counts sum to the file's,
+    every decoded record equals the generator's record of the same global
+    index, and re-encoding the decoded records reproduces the range's bytes.
+    """
+    name = ("config 5: Compact protocol, {4 x i32, 2 x string[0..32]} file split by bytes "
+            "across GPUs, encode + boundary discovery + decode")
+    dec_kernel = "program_decode_kernel"
+    overlap = 1 << 20
+
+    def __init__(self, n, rank, dev):
+        import torch
+        import torch.distributed as dist
+
+        super().__init__(n, rank, dev)
+        self.rank, self.dev = rank, dev
+        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.enc = self.wire  # this rank's part of the file (in file order)
+        self.enc_offs = self.offs
+        sizes = self._gather([self.wire_bytes])
+        self.file_off = sum(r[0] for r in sizes[:rank])
+        self.file_len = sum(r[0] for r in sizes)
+        self.total_wire_bytes = self.file_len
+        from fbthrift_amd import shard
+
+        self.ranges = shard.byte_ranges(self.file_len, self.world)
+        self.enc_ranges = []
+        off = 0
+        for r in sizes:
+            self.enc_ranges.append((off, off + r[0]))
+            off += r[0]
+        b, e = self.ranges[rank]
+        self.need = (b, min(e + self.overlap, self.file_len))
+        # N=1: the file is this rank's encode output itself
+        self.buf = self.wire if self.world == 1 else torch.empty(
+            self.need[1] - self.need[0] + 16, dtype=torch.uint8, device=dev)
+        self.idx = torch.empty(self.n * 2 + 2, dtype=torch.int64, device=dev)
+        self.back = torch.empty(self.n * 2 * self.record_bytes, dtype=torch.uint8, device=dev)
+        self.n_local = 0
+
+    # ---- collectives ---------------------------------------------------------
+    def _gather(self, vals):
+        import torch
+        import torch.distributed as dist
+
+        if self.world_size() == 1:
+            return [list(vals)]
+        t = torch.tensor(vals, dtype=torch.int64, device=self.dev)
+        out = [torch.empty_like(t) for _ in range(self.world_size())]
+        dist.all_gather(out, t)
+        return [[int(x) for x in o.tolist()] for o in out]
+
+    @staticmethod
+    def world_size():
+        import torch.distributed as dist
+
+        return dist.get_world_size() if dist.is_initialized() else 1
+
+    def redistribute(self):
+        """File bytes [need) of every rank from the ranks that encoded them."""
+        import torch
+        import torch.distributed as dist
+
+        lo, hi = self.need
+        if self.world == 1:
+            return
+        mine = self.enc_ranges[self.rank]
+        send, send_sizes, recv_sizes = [], [], []
+        for d in range(self.world):
+            b, e = self.ranges[d]
+            nlo, nhi = b, min(e + self.overlap, self.file_len)
+            a0, a1 = max(mine[0], nlo), min(mine[1], nhi)
+            if a1 > a0:
+                send.append(self.wire[a0 - mine[0]: a1 - mine[0]])
+            send_sizes.append(max(a1 - a0, 0))
+            s0, s1 = self.enc_ranges[d]
+            r0, r1 = max(s0, lo), min(s1, hi)
+            recv_sizes.append(max(r1 - r0, 0))
+        inp = torch.cat(send) if send else torch.empty(0, dtype=torch.uint8, device=self.dev)
+        dist.all_to_all_single(self.buf[: hi - lo], inp, recv_sizes, send_sizes)
+
+    def decode(self):
+        from fbthrift_amd import shard
+
+        self.redistribute()
+        lo, hi = self.need
+        b, e = self.ranges[self.rank]
+        local = self.buf[: hi - lo]
+        cap = self.idx.numel() - 1
+
+        def index_fn(begin, speculative):
+            _, n, first, last, st = self.S.index_stream(
+                self.gs, local, begin=begin - lo, end=e - lo, speculative=speculative,
+                max_records=cap, offsets=self.idx)
+            if n == 0:
+                return 0, shard.NONE, shard.NONE
+            return n, first + lo, last + lo
+
+        n, first, last, base, rounds = shard.exchange_boundaries(
+            index_fn, self.rank, self.world, b, e, self._gather)
+        self.n_local, self.first, self.last, self.base, self.rounds = n, first, last, base, rounds
+        if n:
+            self.S.deserialize(self.gs, local, n, offsets=self.idx[: n + 1],
+                               records=self.back[: n * self.record_bytes], sync=False)
+
+    def check_timed(self):
+        if self.n_local:
+            st, nd, consumed = self.S.context().wait()
+            if st.code or consumed != self.last - self.first:
+                raise RuntimeError("timed decode failed: %s" % (st.as_tuple(),))
+
+    def verify(self):
+        import ctypes
+
+        import torch
+
+        import datagen
+
+        self.check_timed()
+        counts = self._gather([self.n_local])
+        total = sum(c[0] for c in counts)
+        if total != self.n * self.world:
+            raise RuntimeError("records found %d != %d" % (total, self.n * self.world))
+        n, rs = self.n_local, self.record_bytes
+        if n == 0:
+            return
+        lib = ctypes.CDLL(os.path.join(ROOT, "tools", "build", "libtgpu_datagen.so"))
+        want = torch.empty(n * rs, dtype=torch.uint8, device=self.dev)
+        side = torch.empty(n * 64, dtype=torch.uint8, device=self.dev)
+        if lib.tgpu_gen_mixed(ctypes.c_uint64(datagen.SEED), ctypes.c_uint64(self.base),
+                              ctypes.c_uint64(n), ctypes.c_void_p(want.data_ptr()),
+                              ctypes.c_void_p(side.data_ptr()),
+                              ctypes.c_void_p(self.stream.cuda_stream)):
+            raise RuntimeError("generator failed")
+        a, b = want.view(n, rs), self.back[: n * rs].view(n, rs)
+        for lo, hi in self.fixed_ranges:
+            if not torch.equal(a[:, lo:hi], b[:, lo:hi]):
+                raise RuntimeError("decoded records differ from the generator's")
+        lo = self.need[0]
+        local = self.buf[: self.need[1] - lo]
+        again, offs2 = self.S.serialize(self.gs, self.back[: n * rs], n, string_base=local)
+        if not torch.equal(again, local[self.first - lo: self.last - lo]):
+            raise RuntimeError("re-encoded records differ from the file's bytes")
+        del want, side, again, offs2
+
+    def algorithmic(self):
+        # per rank, per step: encode as config 3; decode reads its range once
+        # for the index and once for the decode and writes the records
+        dec_bytes = 2 * (self.last - self.first) + self.n_local * self.record_bytes
+        return dec_bytes, self.n * self.record_bytes + self.side_bytes + self.wire_bytes
+
+
+WORKLOADS = {2: Flat8, 3: Mixed, 4: Nested, 5: FileShards}
 
 
 def main():
@@ -303,9 +471,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    st, nd, consumed = wl.S.context().wait()
-    if st.code or consumed != wl.wire_bytes:
-        raise RuntimeError("timed decode failed: %s" % (st.as_tuple(),))
+    wl.check_timed()
     enc_ms = [e[0].elapsed_time(e[1]) for e in evs]
     dec_ms = [e[1].elapsed_time(e[2]) for e in evs]
     if world > 1:
@@ -313,7 +479,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    value = 2.0 * wl.wire_bytes * args.steps * world / elapsed / 2**30
+    job_bytes = wl.total_wire_bytes or wl.wire_bytes * world
+    value = 2.0 * job_bytes * args.steps / elapsed / 2**30
     dec_avg = sum(dec_ms) / len(dec_ms) / 1e3
     enc_avg = sum(enc_ms) / len(enc_ms) / 1e3
     dec_alg, enc_alg = wl.algorithmic()

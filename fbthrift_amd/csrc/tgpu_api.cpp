@@ -441,10 +441,7 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   x.end = end;
   x.speculative = speculative;
   x.protocol = protocol;
-  x.chunk = index_chunk_bytes(end > begin ? end - begin : 0);
-  x.window = (uint32_t)std::min<uint64_t>(x.chunk, 1024);
   x.rec_size = schema->structs[0].size;
-  x.n_chunks = end > begin ? (end - begin + x.chunk - 1) / x.chunk : 0;
   x.string_limit = limits ? limits->string_limit : 0;
   x.container_limit = limits ? limits->container_limit : 0;
   x.max_depth = limits ? limits->max_depth : 12000;
@@ -452,6 +449,9 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   const int32_t height = x.height ? x.height : x.max_depth;
   x.prog = schema->has_prog[protocol] && height >= 2 && x.max_depth >= 2
                ? schema->d_prog[protocol] : nullptr;
+  x.chunk = index_chunk_bytes(end > begin ? end - begin : 0, x.prog != nullptr);
+  x.window = (uint32_t)std::min<uint64_t>(x.chunk, 1024);
+  x.n_chunks = end > begin ? (end - begin + x.chunk - 1) / x.chunk : 0;
   x.offs = offs;
   x.max_records = max_records;
   x.fill_to = fill_to;
@@ -459,7 +459,8 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   const uint64_t C = std::max<uint64_t>(x.n_chunks, 1);
   const uint64_t rs = (x.rec_size + 7) & ~7u;
   const uint64_t parts = scan_tiles_parts(C) + 1;
-  const uint64_t need = 8 * (5 * C + parts + 8) + C * rs;
+  const uint64_t lane_words = x.chunk == index_tile_bytes() ? C * index_tile_lanes() : 0;
+  const uint64_t need = 8 * (8 * C + parts + 8) + C * rs + 4 * lane_words;
   if (need > ctx->index_bytes) {
     if (ctx->d_index) (void)hipFree(ctx->d_index);
     ctx->d_index = nullptr;
@@ -473,9 +474,13 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   x.cnt = (unsigned long long*)(w + 2 * C);
   x.base = (unsigned long long*)(w + 3 * C);
   x.bad = (unsigned long long*)(w + 4 * C);
-  x.part = (unsigned long long*)(w + 5 * C);
-  x.scal = (unsigned long long*)(w + 5 * C + parts);
-  x.scratch = (uint8_t*)(w + 5 * C + parts + 8);
+  x.pf = w + 5 * C;
+  x.ep = w + 6 * C;
+  x.ec = (unsigned long long*)(w + 7 * C);
+  x.part = (unsigned long long*)(w + 8 * C);
+  x.scal = (unsigned long long*)(w + 8 * C + parts);
+  x.scratch = (uint8_t*)(w + 8 * C + parts + 8);
+  x.lanes = (uint32_t*)(x.scratch + C * rs);
   if (x.n_chunks == 0) {
     // nothing starts in [begin, end): the index is just the end position
     if (e == hipSuccess) e = launch_index_empty(x.res, offs, x.begin, fill_to, s);

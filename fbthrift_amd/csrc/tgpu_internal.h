@@ -249,6 +249,10 @@ struct IndexArgs {
   uint64_t* s;
   uint64_t* e;
   unsigned long long* cnt;
+  uint64_t* pf;              // speculation: where the program stopped (partial chain)
+  uint64_t* ep;              // emit: where the program stopped (kNo: done)
+  unsigned long long* ec;    // emit: starts written before it stopped
+  uint32_t* lanes;           // LDS tiles: per-lane (start, count) of the speculation pass
   unsigned long long* base;  // flags, then exclusive record-count prefix
   unsigned long long* bad;   // chunks whose chain link failed (in order)
   unsigned long long* part;  // scan partials
@@ -260,7 +264,9 @@ struct IndexArgs {
   uint64_t fill_to;          // decode: offs[total+1 .. fill_to] = last end
   DevResult* res;
 };
-uint64_t index_chunk_bytes(uint64_t span);
+uint64_t index_chunk_bytes(uint64_t span, bool tiles);
+uint64_t index_tile_bytes();
+uint64_t index_tile_lanes();
 hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream);
 // Empty range: offs[0..fill_to] = pos, no records.
 hipError_t launch_index_empty(DevResult* res, uint64_t* offs, uint64_t pos, uint64_t fill_to,

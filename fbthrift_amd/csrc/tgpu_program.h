@@ -118,8 +118,8 @@ struct Ctx {
 // PP: the program in LDS (VProgram*) or in HBM read through the scalar cache
 // (const VProgram* __restrict__ kernel argument).
 template <bool kStore, class PP, class Src>
-__device__ bool run_program(PP P, const Src& src, const Ctx& c, uint32_t& pos, uint32_t end,
-                            uint8_t* rec) {
+__device__ __forceinline__ bool run_program(PP P, const Src& src, const Ctx& c, uint32_t& pos,
+                                            uint32_t end, uint8_t* rec) {
   const bool compact = P->protocol == TGPU_PROTOCOL_COMPACT;
   const uint32_t n_ops = P->n_ops;
   uint32_t p = pos;

@@ -98,7 +98,7 @@ def test_index_speculative_shards(gpu, proto, max_len):
     """The stream split into byte ranges at arbitrary positions: each range
     indexed speculatively finds the first record start at/after its begin,
     exactly the oracle's, and its last_end is the next range's first start."""
-    n = 40_000 if max_len == 30 else 3000
+    n = 200_000 if max_len == 30 else 3000
     schema, wire, woffs = _stream("mixed", proto, n, seed=5, max_len=max_len)
     gs = _gs(schema)
     w = _t(wire, gpu)
