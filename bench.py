@@ -174,6 +174,11 @@ class VarLen(Workload):
         self.S = CompactSerializer if self.protocol == 2 else BinarySerializer
         schema = Schema.from_table(datagen.SCHEMAS[self.schema])
         self.gs = GpuSchema(schema)
+        # the schema compiler's kernels (tgpu_jit.cpp), compiled up front like
+        # the reference's generated code; TGPU_JIT=0 keeps the interpreter
+        if os.environ.get("TGPU_JIT", "") != "0" and self.gs.compile(self.protocol):
+            self.dec_kernel, self.enc_kernel = "tgpu_jit_decode", "tgpu_jit_write"
+            self.index_kernel = "tgpu_jit_index_spec"
         self.n = n
         self.record_bytes = rs = schema.record_size
         self.S.context().reserve(n)
@@ -248,6 +253,7 @@ class Mixed(VarLen):
     schema, protocol = "mixed", 2
     default_records = 1 << 26
     dec_kernel, enc_kernel = "program_decode_kernel", "program_write_kernel"
+    index_kernel = "index_tile_spec_kernel"
     fixed_ranges = [(0, 16), (48, 54)]
     span_offsets, elem_width = (16, 32), 1
 
@@ -278,7 +284,6 @@ class FileShards(Mixed):
     """
     name = ("config 5: Compact protocol, {4 x i32, 2 x string[0..32]} file split by bytes "
             "across GPUs, encode + boundary discovery + decode")
-    dec_kernel = "program_decode_kernel"
     overlap = 1 << 20
 
     def __init__(self, n, rank, dev):

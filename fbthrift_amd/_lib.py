@@ -64,7 +64,7 @@ EXPORTS = [
     "tgpu_schema_create", "tgpu_schema_destroy", "tgpu_schema_record_size",
     "tgpu_schema_fixed_wire_size", "tgpu_context_create", "tgpu_context_destroy",
     "tgpu_context_reserve", "tgpu_context_wait", "tgpu_encode_batch", "tgpu_encoded_size",
-    "tgpu_decode_batch", "tgpu_index_stream",
+    "tgpu_decode_batch", "tgpu_index_stream", "tgpu_schema_compile", "tgpu_schema_compile_check",
 ]
 
 _lib = None
@@ -117,5 +117,10 @@ def lib():
                                     ctypes.POINTER(Limits), P, ctypes.POINTER(Status),
                                     ctypes.POINTER(U64), ctypes.POINTER(U64),
                                     ctypes.POINTER(U64)]
+    L.tgpu_schema_compile.restype = I32
+    L.tgpu_schema_compile.argtypes = [P, I32]
+    L.tgpu_schema_compile_check.restype = I32
+    L.tgpu_schema_compile_check.argtypes = [P, U32, P, U32, I32, ctypes.c_char_p,
+                                            ctypes.c_char_p, U64]
     _lib = L
     return L

@@ -21,16 +21,20 @@
 //      the end, the status and (decode) pads the index to the requested count.
 // Speculation only decides speed: every chunk the result uses was either
 // parsed from its verified true start or is linked to one by s[j] == e[j-1].
-#include "tgpu_program.h"
+#include "tgpu_device.h"
+#include "tgpu_prog_kernels.h"
 
 namespace tgpu {
 namespace {
 
-constexpr uint64_t kNo = ~0ull;        // no start found / unset
-constexpr uint64_t kErr = ~0ull - 1;   // chain ended in a reader error
-constexpr uint64_t kPartial = ~0ull - 2;  // program stopped: general reader continues
-constexpr uint64_t kLanesValid = ~0ull - 3;  // pf: the tile's per-lane results are current
-constexpr uint32_t kPosCap = 0x7fffff00u;
+using prog::chunk_hi;
+using prog::chunk_lo;
+using prog::kErr;
+using prog::kNo;
+using prog::kPartial;
+using prog::kPosCap;
+using prog::kTile;
+using prog::kTileLanes;
 
 __device__ __forceinline__ dev::Reader reader_at(const IndexArgs& a, uint64_t pos) {
   dev::Reader r;
@@ -73,7 +77,7 @@ __device__ bool chain(const IndexArgs& a, uint64_t p, uint64_t hi, bool canonica
       const uint64_t avail = a.in_len - p;
       const prog::HbmSrc src{a.in + p, (uint32_t)(avail < kPosCap ? avail : kPosCap)};
       uint32_t rel = 0;
-      ok = prog::run_program<false>(a.prog, src, pc, rel, src.avail, nullptr);
+      ok = prog::run_program<false>(prog::DynProg{a.prog}, src, pc, rel, src.avail, nullptr);
       q = p + rel;
     }
     if (!ok) {
@@ -117,7 +121,7 @@ __device__ __forceinline__ uint64_t prog_chain(const IndexArgs& a, uint64_t& p, 
     const uint64_t avail = a.in_len - p;
     const prog::HbmSrc src{a.in + p, (uint32_t)(avail < kPosCap ? avail : kPosCap)};
     uint32_t rel = 0;
-    if (!prog::run_program<false>(a.prog, src, pc, rel, src.avail, nullptr)) {
+    if (!prog::run_program<false>(prog::DynProg{a.prog}, src, pc, rel, src.avail, nullptr)) {
       stuck = true;
       break;
     }
@@ -126,14 +130,6 @@ __device__ __forceinline__ uint64_t prog_chain(const IndexArgs& a, uint64_t& p, 
     p += rel;
   }
   return count;
-}
-
-__device__ __forceinline__ uint64_t chunk_lo(const IndexArgs& a, uint64_t j) {
-  return a.begin + j * a.chunk;
-}
-__device__ __forceinline__ uint64_t chunk_hi(const IndexArgs& a, uint64_t j) {
-  const uint64_t h = a.begin + (j + 1) * a.chunk;
-  return h < a.end ? h : a.end;
 }
 
 // Speculation, program-only (schemas with a program). A chain the program
@@ -240,329 +236,17 @@ __global__ __launch_bounds__(256) void index_spec_general_kernel(IndexArgs a) {
   a.cnt[j] = 0;
 }
 
-// ---- LDS tiles (schemas with a program) --------------------------------------
-// A chunk is a tile of kTile bytes handled by one workgroup: the tile (plus
-// kOver bytes for the records that straddle its end) is staged in LDS with
-// coalesced 16-byte loads; lane k speculates the first record start in its
-// kSub-byte slice and chains to the slice's end; the lanes' links are then
-// repaired inside the workgroup (lane k restarts from lane k-1's end until
-// no lane changes), so the tile behaves like one chunk of the lane path:
-// (first start, end, count). A tile any lane could not finish with the
-// program is handed to the general-reader kernels whole (kPartial).
-constexpr uint32_t kTileLanes = 256;
-constexpr uint32_t kSub = 64;
-constexpr uint32_t kTile = kTileLanes * kSub;
-constexpr uint32_t kOver = 4096;
-constexpr uint32_t kTileLds = kTile + kOver + 32;
-
-// LDS window with HBM fallback past the staged bytes (positions relative to
-// the 16-byte aligned tile base)
-struct TileSrc {
-  const uint32_t* w32;
-  uint32_t lds_len;
-  prog::HbmSrc g;
-  __device__ __forceinline__ uint64_t win8(uint32_t p) const {
-    if (p + 12 <= lds_len) return prog::LdsSrc{w32}.win8(p);
-    return g.win8(p);
-  }
-};
-
-struct TileLane {
-  uint32_t s, e, c;  // first start, end, count (tile-relative); s == kNoPos: none
-  bool stuck;
-};
-constexpr uint32_t kNoPos = 0xffffffffu;
-
-// Cheap rejection of a candidate start before running the program: the byte
-// after the first header's value must be the second header (first ops
-// CONST, VARINT|FIXED, CONST — every schema whose first two fields are
-// unqualified scalars). Never rejects a canonical record start.
-__device__ __forceinline__ bool quick_reject(const VProgram* __restrict__ P, const TileSrc& src,
-                                             uint32_t cand) {
-  if (P->n_ops < 3 || P->ops[0].kind != VOP_CONST || P->ops[2].kind != VOP_CONST) return false;
-  const uint32_t h0len = P->ops[0].hdr_len;
-  const VOp v = P->ops[1];
-  const uint64_t w = src.win8(cand + h0len);
-  uint32_t len;
-  if (v.kind == VOP_VARINT) {
-    const uint64_t stop = ~w & 0x8080808080808080ull;
-    if (!stop) return false;
-    len = ((uint32_t)__builtin_ctzll(stop) >> 3) + 1;
-  } else if (v.kind == VOP_FIXED) {
-    len = v.width;
-  } else {
-    return false;
-  }
-  if (len >= 8) return false;
-  return ((w >> (8 * len)) & 0xff) != (P->ops[2].hdr & 0xff);
-}
-
-// chain of canonical records from x while position < hi (tile-relative)
-__device__ __forceinline__ void tile_chain(const VProgram* __restrict__ P, const TileSrc& src,
-                                           const prog::Ctx& pc, uint32_t x, uint32_t hi,
-                                           uint32_t end, TileLane& L, uint64_t* emit) {
-  L.s = x;
-  L.c = 0;
-  L.stuck = false;
-  uint32_t p = x;
-  while (p < hi) {
-    uint32_t q = p;
-    if (!prog::run_program<false>(P, src, pc, q, end, nullptr)) {
-      L.stuck = true;
-      break;
-    }
-    if (emit) emit[L.c] = p;
-    ++L.c;
-    p = q;
-  }
-  L.e = p;
-}
-
-// Stages the tile, speculates and repairs the lanes' chains. entry: the
-// tile's known first start (tile-relative; kNoPos: speculate lane 0 too).
-// Returns false when the tile needs the general reader. *first: the tile's
-// first record start (kNoPos: none).
-__device__ __forceinline__ bool tile_resolve(const IndexArgs& a, uint64_t j, uint8_t* lds, uint32_t entry,
-                             TileLane& L, uint32_t& sh, uint32_t& first, uint32_t* E,
-                             int* flag) {
-  const uint64_t lo = chunk_lo(a, j);
-  const uint64_t hi_abs = chunk_hi(a, j);
-  const uint8_t* g = a.in + lo;
-  sh = (uint32_t)((uintptr_t)g & 15);
-  const uint8_t* gb = g - sh;
-  const uint64_t avail64 = a.in_len - lo + sh;
-  const uint32_t avail = (uint32_t)(avail64 < kPosCap ? avail64 : kPosCap);
-  const uint32_t staged = avail < kTile + kOver + 16 ? avail : kTile + kOver + 16;
-  const uint32_t nvec = (staged + 15) >> 4;
-  for (uint32_t i = threadIdx.x; i < nvec; i += kTileLanes)
-    ((uint4*)lds)[i] = ((const uint4*)gb)[i];
-  __syncthreads();
-  const TileSrc src{(const uint32_t*)lds, staged & ~3u, prog::HbmSrc{gb, avail}};
-  const prog::Ctx pc{0, nullptr, 0, a.string_limit, a.container_limit};
-  const uint32_t thi = sh + (uint32_t)(hi_abs - lo);  // tile end (relative)
-  const uint32_t k = threadIdx.x;
-  const uint32_t sub_lo = sh + k * kSub;
-  const uint32_t sub_hi = sub_lo + kSub < thi ? sub_lo + kSub : thi;
-  L.s = kNoPos;
-  L.e = kNoPos;
-  L.c = 0;
-  L.stuck = false;
-  if (k == 0 && entry != kNoPos) {
-    tile_chain(a.prog, src, pc, entry, sub_hi > entry ? sub_hi : entry, avail, L, nullptr);
-    if (entry >= sub_hi) {  // the entry lies past lane 0's slice
-      L.s = entry;
-      L.e = entry;
-    }
-  } else if (sub_lo < thi) {
-    // candidates: bytes equal to the first header byte that survive
-    // quick_reject (divergent but cheap); the chain from a candidate runs
-    // outside the search so all lanes of the wave run it together
-    const uint32_t h0 = a.prog->ops[0].kind == VOP_CONST ? (a.prog->ops[0].hdr & 0xff) : 0x100;
-    // bytes of the slice equal to h0, all eight 8-byte groups loaded at once
-    uint64_t mk[kSub / 8];
-#pragma unroll
-    for (uint32_t i = 0; i < kSub / 8; ++i) {
-      const uint32_t base = sub_lo + 8 * i;
-      uint64_t m = 0;
-      if (base < sub_hi) {
-        m = 0x8080808080808080ull;
-        if (h0 < 0x100) {
-          const uint64_t x = src.win8(base) ^ (h0 * 0x0101010101010101ull);
-          m = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
-        }
-      }
-      mk[i] = m;
-    }
-    uint32_t from = sub_lo;
-    bool need = true;
-    while (need) {
-      uint32_t cand = kNoPos;
-#pragma unroll
-      for (uint32_t i = 0; i < kSub / 8; ++i) {
-        uint64_t m = mk[i];
-        while (m && cand == kNoPos) {
-          const uint32_t c = sub_lo + 8 * i + ((uint32_t)__builtin_ctzll(m) >> 3);
-          m &= m - 1;
-          if (c < from || c >= sub_hi) continue;
-          if (quick_reject(a.prog, src, c)) continue;
-          cand = c;
-        }
-      }
-      if (cand == kNoPos) break;  // no record start in this slice
-      TileLane t;
-      tile_chain(a.prog, src, pc, cand, sub_hi, avail, t, nullptr);
-      if (t.c) {
-        L = t;
-        need = false;
-      } else {
-        from = cand + 1;
-      }
-    }
-  }
-  // the tile's first start: the first lane that found one
-  __shared__ uint32_t first_lane;
-  if (k == 0) first_lane = kTileLanes;
-  __syncthreads();
-  if (L.s != kNoPos) atomicMin(&first_lane, k);
-  __syncthreads();
-  const uint32_t f = first_lane;
-  if (f == kTileLanes) {
-    first = kNoPos;
-    return true;
-  }
-  // lanes before it: no record starts there
-  __shared__ uint32_t fs;
-  if (k == f) fs = L.s;
-  __syncthreads();
-  if (k < f) {
-    L.s = L.e = fs;
-    L.c = 0;
-    L.stuck = false;
-  }
-  first = fs;
-  // repair: lane k restarts from lane k-1's end until nothing changes
-  for (uint32_t it = 0; it <= kTileLanes; ++it) {
-    E[k] = L.e;
-    __syncthreads();
-    int changed = 0;
-    if (k > f) {
-      const uint32_t x = E[k - 1];
-      if (x != kNoPos && (x != L.s || L.e == kNoPos)) {
-        if (x >= sub_hi) {
-          L.s = L.e = x;
-          L.c = 0;
-          L.stuck = false;
-        } else {
-          tile_chain(a.prog, src, pc, x, sub_hi, avail, L, nullptr);
-        }
-        changed = 1;
-      }
-    }
-    if (!__syncthreads_or(changed)) break;
-  }
-  *flag = 0;
-  __syncthreads();
-  if (L.stuck || L.e == kNoPos) *flag = 1;
-  __syncthreads();
-  return *flag == 0;
-}
-
+// ---- LDS tiles (schemas with a program; tgpu_prog_kernels.h) ---------------
 __global__ __launch_bounds__(kTileLanes) void index_tile_spec_kernel(IndexArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kTileLds];
-  __shared__ uint32_t E[kTileLanes];
-  __shared__ int flag;
-  __shared__ unsigned long long csum;
-  const uint64_t j = blockIdx.x;
-  const uint32_t entry = (j == 0 && !a.speculative) ? 0u : kNoPos;  // + sh below
-  TileLane L;
-  uint32_t sh, first;
-  // tile 0 of a non-speculative call starts at begin exactly (relative 0 + sh)
-  uint32_t ent = entry;
-  if (ent != kNoPos) ent = (uint32_t)((uintptr_t)(a.in + chunk_lo(a, j)) & 15);
-  const bool ok = tile_resolve(a, j, lds, ent, L, sh, first, E, &flag);
-  const uint64_t lo = chunk_lo(a, j);
-  if (threadIdx.x == 0) csum = 0;
-  __syncthreads();
-  if (ok && first != kNoPos) atomicAdd(&csum, (unsigned long long)L.c);
-  __syncthreads();
-  // per-lane starts/counts for the emit pass (valid while the tile keeps this
-  // start: pf[j] == kLanesValid)
-  if (ok && first != kNoPos)
-    a.lanes[j * kTileLanes + threadIdx.x] = (L.s & 0xffffu) | ((uint32_t)L.c << 16);
-  if (threadIdx.x == kTileLanes - 1) {
-    if (first == kNoPos) {
-      a.s[j] = kNo;
-      a.e[j] = kNo;
-      a.cnt[j] = 0;
-    } else if (!ok) {
-      // the general reader walks the whole tile from its (speculated) start
-      a.s[j] = lo - sh + first;
-      a.e[j] = kPartial;
-      a.pf[j] = lo - sh + first;
-      a.cnt[j] = 0;
-    } else {
-      a.s[j] = lo - sh + first;
-      a.e[j] = lo - sh + L.e;
-      a.cnt[j] = csum;
-      a.pf[j] = kLanesValid;
-    }
-  }
+  __shared__ __attribute__((aligned(16))) uint8_t lds[prog::kTileLds];
+  __shared__ prog::IndexTileShared sm;
+  prog::index_spec_tile(a, prog::DynProg{a.prog}, lds, sm);
 }
 
-// Emit for a tile whose first start is verified (a.s[j]); records starting in
-// the tile get their starts written at offs[base[j] ..]. A tile the program
-// cannot finish goes to index_emit_cont_kernel whole.
 __global__ __launch_bounds__(kTileLanes) void index_tile_emit_kernel(IndexArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kTileLds];
-  __shared__ uint32_t E[kTileLanes];
-  __shared__ int flag;
-  __shared__ unsigned long long part[4];
-  const uint64_t j = blockIdx.x;
-  if (threadIdx.x == 0) a.ep[j] = kNo;
-  if (j >= a.scal[1] || a.cnt[j] == 0) return;
-  const uint64_t lo = chunk_lo(a, j);
-  const uint32_t sh0 = (uint32_t)((uintptr_t)(a.in + lo) & 15);
-  const uint64_t sj = a.s[j];
-  const uint32_t ent = (uint32_t)(sj - lo) + sh0;
-  TileLane L;
-  uint32_t sh, first;
-  bool ok;
-  if (a.pf[j] == kLanesValid) {
-    // the speculation pass's lane results still hold: stage the tile only
-    const uint8_t* g = a.in + lo;
-    sh = sh0;
-    const uint8_t* gb = g - sh;
-    const uint64_t av = a.in_len - lo + sh;
-    const uint32_t avail = (uint32_t)(av < kPosCap ? av : kPosCap);
-    const uint32_t staged = avail < kTile + kOver + 16 ? avail : kTile + kOver + 16;
-    const uint32_t nvec = (staged + 15) >> 4;
-    for (uint32_t i = threadIdx.x; i < nvec; i += kTileLanes)
-      ((uint4*)lds)[i] = ((const uint4*)gb)[i];
-    const uint32_t v = a.lanes[j * kTileLanes + threadIdx.x];
-    L.s = v & 0xffffu;
-    L.c = v >> 16;
-    first = ent;
-    ok = true;
-    __syncthreads();
-  } else {
-    ok = tile_resolve(a, j, lds, ent, L, sh, first, E, &flag);
-  }
-  const uint64_t b = a.base[j];
-  if (!ok) {
-    if (threadIdx.x == 0) {
-      a.ep[j] = sj;
-      a.ec[j] = 0;
-    }
-    return;
-  }
-  // lane k's records go after the records of lanes < k
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  unsigned long long x = L.c;
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned long long y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) part[wid] = x;
-  __syncthreads();
-  unsigned long long pre = x - L.c;
-  for (int w = 0; w < wid; ++w) pre += part[w];
-  if (L.c == 0) return;
-  // re-walk this lane's records, writing absolute starts
-  const uint64_t gb = lo - sh;
-  uint32_t p = L.s;
-  const uint8_t* g = a.in + gb;
-  const uint64_t avail64 = a.in_len - gb;
-  const uint32_t avail = (uint32_t)(avail64 < kPosCap ? avail64 : kPosCap);
-  const uint32_t staged = avail < kTile + kOver + 16 ? avail : kTile + kOver + 16;
-  const TileSrc src{(const uint32_t*)lds, staged & ~3u, prog::HbmSrc{g, avail}};
-  const prog::Ctx pc{0, nullptr, 0, a.string_limit, a.container_limit};
-  for (uint32_t i = 0; i < L.c; ++i) {
-    const uint64_t idx = b + pre + i;
-    if (idx <= a.max_records) a.offs[idx] = gb + p;
-    uint32_t q = p;
-    prog::run_program<false>(a.prog, src, pc, q, avail, nullptr);
-    p = q;
-  }
+  __shared__ __attribute__((aligned(16))) uint8_t lds[prog::kTileLds];
+  __shared__ prog::IndexTileShared sm;
+  prog::index_emit_tile(a, prog::DynProg{a.prog}, lds, sm);
 }
 
 __device__ __forceinline__ bool link_broken(const IndexArgs& a, uint64_t j) {
@@ -752,12 +436,17 @@ uint64_t index_chunk_bytes(uint64_t span, bool tiles) {
   return c;
 }
 
-hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream) {
+hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const JitKernels* jit) {
   const uint64_t C = a.n_chunks;
   const dim3 g((uint32_t)((C + 255) / 256)), b(256);
   const bool bin = a.protocol == TGPU_PROTOCOL_BINARY;
   if (a.prog && a.chunk == kTile) {
-    hipLaunchKernelGGL(index_tile_spec_kernel, dim3((uint32_t)C), dim3(kTileLanes), 0, stream, a);
+    if (jit) {
+      const hipError_t e = jit_launch_index(jit, false, a, C, stream);
+      if (e != hipSuccess) return e;
+    } else {
+      hipLaunchKernelGGL(index_tile_spec_kernel, dim3((uint32_t)C), dim3(kTileLanes), 0, stream, a);
+    }
     if (bin)
       hipLaunchKernelGGL(index_cont_kernel<TGPU_PROTOCOL_BINARY>, g, b, 0, stream, a);
     else
@@ -784,7 +473,10 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream) {
   hipLaunchKernelGGL(index_prep_kernel, g, b, 0, stream, a);
   e = launch_scan_tiles(a.base, C, a.part, nullptr, nullptr, stream);
   if (e != hipSuccess) return e;
-  if (a.prog && a.chunk == kTile)
+  if (a.prog && a.chunk == kTile && jit) {
+    e = jit_launch_index(jit, true, a, C, stream);
+    if (e != hipSuccess) return e;
+  } else if (a.prog && a.chunk == kTile)
     hipLaunchKernelGGL(index_tile_emit_kernel, dim3((uint32_t)C), dim3(kTileLanes), 0, stream, a);
   else
     hipLaunchKernelGGL(index_emit_kernel, g, b, 0, stream, a);

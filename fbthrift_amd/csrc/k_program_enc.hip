@@ -18,263 +18,20 @@
 //      its record into an LDS output tile (records past the LDS cap go to HBM
 //      directly); the tile leaves with coalesced 16-byte stores (byte stores
 //      only on the two edge chunks shared with the neighbouring tiles).
-#include "tgpu_device.h"
+#include "tgpu_prog_kernels.h"
 
 namespace tgpu {
 namespace {
 
-constexpr uint32_t kET = 256;               // records per tile = threads per workgroup
-constexpr uint32_t kOutCap = 24 * 1024;     // LDS bytes for one tile's wire output
-
-__device__ __forceinline__ uint32_t varint_len(uint64_t v) {
-  const uint32_t bits = 64 - (uint32_t)__builtin_clzll(v | 1);
-  return (bits + 6) / 7;
-}
-
-__device__ __forceinline__ uint64_t load_member(const uint8_t* p, uint32_t width) {
-  switch (width) {
-    case 8: return *(const uint64_t*)p;
-    case 4: return *(const uint32_t*)p;
-    case 2: return *(const uint16_t*)p;
-    default: return *p;
-  }
-}
-
-// zigzag of a signed member of `width` bytes, as i32 (bits 32) or i64
-__device__ __forceinline__ uint64_t zz_member(uint64_t raw, uint32_t width, uint32_t bits) {
-  int64_t v;
-  switch (width) {
-    case 2: v = (int16_t)(uint16_t)raw; break;
-    case 4: v = (int32_t)(uint32_t)raw; break;
-    default: v = (int64_t)raw; break;
-  }
-  if (bits == 32) return dev::i32_to_zz((int32_t)v);
-  return dev::i64_to_zz(v);
-}
-
-// ---- record size ------------------------------------------------------------
-// Bytes T::write emits for the record at `rec`; ok = false where the writer
-// would throw or abort (the finish kernel re-derives the exact code).
-__device__ uint64_t program_size(const VProgram* __restrict__ P, const uint8_t* rec,
-                                 const uint8_t* __restrict__ lbase, bool& ok) {
-  const bool compact = P->protocol == TGPU_PROTOCOL_COMPACT;
-  const uint32_t n_ops = P->n_ops;
-  uint64_t n = 0;
-  for (uint32_t k = 0; k < n_ops; ++k) {
-    const VOp op = P->ops[k];
-    switch (op.kind) {
-      case VOP_CONST:
-        n += op.hdr_len;
-        break;
-      case VOP_CBOOL:
-        if (rec[op.member] > 1) ok = false;
-        n += op.hdr_len;
-        break;
-      case VOP_FIXED:
-        if (op.is_bool && rec[op.member] > 1) ok = false;
-        n += op.width;
-        break;
-      case VOP_VARINT:
-        n += varint_len(zz_member(load_member(rec + op.member, op.width), op.width, op.bits));
-        break;
-      case VOP_STRING: {
-        const uint32_t len = ((const tgpu_span*)(rec + op.member))->length;
-        if (len > 0x7fffffffu) ok = false;
-        n += (compact ? varint_len(len) : 4) + (uint64_t)len;
-        break;
-      }
-      case VOP_LIST: {
-        const tgpu_span sp = *(const tgpu_span*)(rec + op.member);
-        const uint32_t len = sp.length;
-        if (len > 0x7fffffffu) {
-          ok = false;
-          break;
-        }
-        n += compact ? (len <= 14 ? 1 : 1 + varint_len(len)) : 5;
-        const uint8_t* e = lbase + sp.offset;
-        if (op.elem_kind == VEL_VARINT) {
-          for (uint32_t i = 0; i < len; ++i)
-            n += varint_len(zz_member(load_member(e + (uint64_t)i * op.width, op.width), op.width,
-                                      op.bits));
-        } else if (op.elem_kind == VEL_BOOL) {
-          for (uint32_t i = 0; i < len; ++i)
-            if (e[i] > 1) ok = false;
-          n += len;
-        } else {
-          n += (uint64_t)len * op.width;
-        }
-        break;
-      }
-      default:
-        break;
-    }
-  }
-  return n;
-}
-
-// ---- record emission ----------------------------------------------------------
-// Sinks: the LDS output tile (position q relative to the tile's LDS base) or
-// HBM directly (q relative to the record's HBM start).
-struct LdsSink {
-  uint8_t* base;
-  __device__ __forceinline__ void put(uint32_t q, uint32_t b) const { base[q] = (uint8_t)b; }
-};
-struct HbmSink {
-  uint8_t* base;
-  __device__ __forceinline__ void put(uint32_t q, uint32_t b) const { base[q] = (uint8_t)b; }
-};
-
-template <class Sink>
-__device__ __forceinline__ uint32_t put_be(const Sink& s, uint32_t q, uint64_t v, uint32_t n) {
-  for (uint32_t i = 0; i < n; ++i) s.put(q + i, (uint32_t)(v >> (8 * (n - 1 - i))));
-  return q + n;
-}
-template <class Sink>
-__device__ __forceinline__ uint32_t put_varint(const Sink& s, uint32_t q, uint64_t v) {
-  while (v & ~0x7full) {
-    s.put(q++, (uint32_t)((v & 0x7f) | 0x80));
-    v >>= 7;
-  }
-  s.put(q++, (uint32_t)v);
-  return q;
-}
-// len bytes from HBM (any alignment): aligned dword loads, bytes out
-template <class Sink>
-__device__ __forceinline__ uint32_t put_bytes(const Sink& s, uint32_t q,
-                                              const uint8_t* __restrict__ src, uint32_t len) {
-  if (!len) return q;
-  const uintptr_t a = (uintptr_t)src;
-  const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
-  uint32_t sh = (uint32_t)(a & 3);
-  uint32_t i = 0;
-  while (i < len) {
-    const uint32_t word = *w++;
-    for (uint32_t b = sh; b < 4 && i < len; ++b, ++i) s.put(q + i, (word >> (8 * b)) & 0xff);
-    sh = 0;
-  }
-  return q + len;
-}
-
-template <class Sink>
-__device__ void program_emit(const VProgram* __restrict__ P, const uint8_t* rec,
-                             const uint8_t* __restrict__ sbase, const uint8_t* __restrict__ lbase,
-                             const Sink& s) {
-  const bool compact = P->protocol == TGPU_PROTOCOL_COMPACT;
-  const uint32_t n_ops = P->n_ops;
-  uint32_t q = 0;
-  for (uint32_t k = 0; k < n_ops; ++k) {
-    const VOp op = P->ops[k];
-    switch (op.kind) {
-      case VOP_CONST:
-        for (uint32_t i = 0; i < op.hdr_len; ++i) s.put(q + i, (op.hdr >> (8 * i)) & 0xff);
-        q += op.hdr_len;
-        break;
-      case VOP_CBOOL: {
-        // the bool's value rides in the header's type nibble (CT_BOOLEAN_TRUE/FALSE)
-        const uint32_t h = op.hdr | (rec[op.member] ? 1u : 2u);
-        for (uint32_t i = 0; i < op.hdr_len; ++i) s.put(q + i, (h >> (8 * i)) & 0xff);
-        q += op.hdr_len;
-        break;
-      }
-      case VOP_FIXED:
-        q = put_be(s, q, load_member(rec + op.member, op.width), op.width);
-        break;
-      case VOP_VARINT:
-        q = put_varint(s, q, zz_member(load_member(rec + op.member, op.width), op.width, op.bits));
-        break;
-      case VOP_STRING: {
-        const tgpu_span sp = *(const tgpu_span*)(rec + op.member);
-        q = compact ? put_varint(s, q, sp.length) : put_be(s, q, sp.length, 4);
-        q = put_bytes(s, q, sbase + sp.offset, sp.length);
-        break;
-      }
-      case VOP_LIST: {
-        const tgpu_span sp = *(const tgpu_span*)(rec + op.member);
-        const uint32_t len = sp.length;
-        if (compact) {
-          if (len <= 14) {
-            s.put(q++, (len << 4) | op.elem_ct);
-          } else {
-            s.put(q++, 0xf0 | op.elem_ct);
-            q = put_varint(s, q, len);
-          }
-        } else {
-          s.put(q++, op.elem_ttype);
-          q = put_be(s, q, len, 4);
-        }
-        const uint8_t* e = lbase + sp.offset;
-        if (op.elem_kind == VEL_VARINT) {
-          for (uint32_t i = 0; i < len; ++i)
-            q = put_varint(s, q, zz_member(load_member(e + (uint64_t)i * op.width, op.width),
-                                           op.width, op.bits));
-        } else if (op.elem_kind == VEL_BOOL) {
-          for (uint32_t i = 0; i < len; ++i) s.put(q++, compact ? (e[i] ? 1u : 2u) : e[i]);
-        } else {
-          for (uint32_t i = 0; i < len; ++i)
-            q = put_be(s, q, load_member(e + (uint64_t)i * op.width, op.width), op.width);
-        }
-        break;
-      }
-      default:
-        break;
-    }
-  }
-}
-
-// ---- block helpers (256 threads) --------------------------------------------
-__device__ __forceinline__ unsigned long long wave_incl_scan(unsigned long long x) {
-  const int lane = threadIdx.x & 63;
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned long long y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  return x;
-}
-
-// exclusive scan across the block; *total = block sum (all threads)
-__device__ __forceinline__ unsigned long long block_exscan256(unsigned long long v,
-                                                              unsigned long long* part,
-                                                              unsigned long long* total) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const unsigned long long x = wave_incl_scan(v);
-  if (lane == 63) part[wid] = x;
-  __syncthreads();
-  unsigned long long pre = 0;
-  for (int w = 0; w < wid; ++w) pre += part[w];
-  *total = part[0] + part[1] + part[2] + part[3];
-  return pre + x - v;
-}
-
-// Records [r0, r0+nrec) of stride S into LDS; returns the 16-byte phase.
-__device__ __forceinline__ uint32_t stage_records(const uint8_t* recs, uint64_t r0, uint32_t nrec,
-                                                  uint32_t S, uint8_t* rtile) {
-  const uint8_t* g = recs + r0 * S;
-  const uint32_t sh = (uint32_t)((uintptr_t)g & 15);
-  const uint4* src = (const uint4*)(g - sh);
-  const uint32_t nvec = (nrec * S + sh + 15) >> 4;
-  for (uint32_t i = threadIdx.x; i < nvec; i += kET) ((uint4*)rtile)[i] = src[i];
-  return sh;
-}
+using prog::block_exscan256;
+using prog::kET;
+using prog::kOutCap;
 
 __global__ __launch_bounds__(kET) void program_size_kernel(EncodeArgs a,
                                                            const VProgram* __restrict__ P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ unsigned long long part[4];
-  const uint64_t r0 = (uint64_t)blockIdx.x * kET;
-  const uint32_t S = a.rec_size;
-  const uint32_t nrec = (uint32_t)min((uint64_t)kET, a.n - r0);
-  const uint32_t sh = stage_records(a.recs, r0, nrec, S, smem);
-  __syncthreads();
-  unsigned long long sz = 0;
-  if (threadIdx.x < nrec) {
-    bool ok = true;
-    sz = program_size(P, smem + sh + threadIdx.x * S, a.lbase, ok);
-    if (!ok) atomicMin(&a.res->first_fail, (unsigned long long)(r0 + threadIdx.x));
-    a.offs[r0 + threadIdx.x] = sz;
-  }
-  unsigned long long total;
-  (void)block_exscan256(sz, part, &total);
-  if (threadIdx.x == 0) a.block_sums[blockIdx.x] = total;
+  prog::size_tile(a, prog::DynProg{P}, a.rec_size, smem, part);
 }
 
 __global__ __launch_bounds__(kET) void program_write_kernel(EncodeArgs a,
@@ -282,56 +39,7 @@ __global__ __launch_bounds__(kET) void program_write_kernel(EncodeArgs a,
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ unsigned long long part[4];
   __shared__ unsigned int lds_end;
-  const uint64_t r0 = (uint64_t)blockIdx.x * kET;
-  const uint32_t S = a.rec_size;
-  const uint32_t nrec = (uint32_t)min((uint64_t)kET, a.n - r0);
-  uint8_t* rtile = smem;
-  uint8_t* otile = smem + ((kET * S + 16 + 15) & ~15u);
-  const uint32_t rsh = stage_records(a.recs, r0, nrec, S, rtile);
-  const uint32_t r = threadIdx.x;
-  const unsigned long long sz = r < nrec ? a.offs[r0 + r] : 0;
-  unsigned long long tile_total;
-  const unsigned long long rel = block_exscan256(sz, part, &tile_total);
-  const unsigned long long tile_base = a.block_sums[blockIdx.x];
-  if (r == 0) lds_end = (unsigned int)min(tile_total, (unsigned long long)kOutCap);
-  __syncthreads();  // record tile staged, lds_end initialised
-  uint8_t* gtile = a.out + tile_base;
-  const uint32_t osh = (uint32_t)((uintptr_t)gtile & 15);
-  bool fits = false;
-  if (r < nrec) {
-    const unsigned long long start = tile_base + rel;
-    a.offs[r0 + r] = start;
-    if (start + sz > a.cap) {
-      atomicMin(&a.res->first_fail, (unsigned long long)(r0 + r));
-      atomicMin(&lds_end, (unsigned int)min(rel, (unsigned long long)kOutCap));
-    } else {
-      fits = rel + sz <= kOutCap;
-      if (!fits) atomicMin(&lds_end, (unsigned int)rel);
-    }
-  }
-  __syncthreads();
-  if (r < nrec) {
-    const uint8_t* rec = rtile + rsh + r * S;
-    if (fits && rel + sz <= lds_end) {
-      program_emit(P, rec, a.sbase, a.lbase, LdsSink{otile + osh + (uint32_t)rel});
-    } else if (tile_base + rel + sz <= a.cap) {
-      program_emit(P, rec, a.sbase, a.lbase, HbmSink{gtile + rel});
-    }
-  }
-  __syncthreads();
-  // LDS tile [osh, osh + lds_end) -> HBM [gtile, gtile + lds_end)
-  const uint32_t end = osh + lds_end;
-  const uint32_t nvec = (end + 15) >> 4;
-  uint8_t* gb = gtile - osh;
-  for (uint32_t i = threadIdx.x; i < nvec; i += kET) {
-    const uint32_t lo = i << 4, hi = lo + 16;
-    if (lo >= osh && hi <= end) {
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      __builtin_nontemporal_store(((const u32x4*)otile)[i], (u32x4*)gb + i);
-    } else {
-      for (uint32_t b = (lo < osh ? osh : lo); b < (hi < end ? hi : end); ++b) gb[b] = otile[b];
-    }
-  }
+  prog::write_tile(a, prog::DynProg{P}, a.rec_size, smem, part, &lds_end);
 }
 
 // ---- scan of per-tile sums (exclusive, in place; total -> res, offs[n]) ----
@@ -419,14 +127,23 @@ bool program_encode_fits(uint32_t rec_size) {
 }
 
 hipError_t launch_program_encode(const EncodeArgs& a, const VProgram* d_prog,
-                                 unsigned long long* part, bool size_only, hipStream_t stream) {
+                                 unsigned long long* part, bool size_only, hipStream_t stream,
+                                 const JitKernels* jit) {
   if (a.n == 0) return hipSuccess;
   const uint64_t tiles = (a.n + kET - 1) / kET;
   const uint32_t rt = (kET * a.rec_size + 16 + 15) & ~15u;
-  hipLaunchKernelGGL(program_size_kernel, dim3((uint32_t)tiles), dim3(kET), rt, stream, a, d_prog);
-  hipError_t e = launch_scan_tiles(a.block_sums, tiles, part, &a.res->total_bytes, a.offs + a.n,
-                                   stream);
+  hipError_t e;
+  if (jit) {
+    e = jit_launch_encode(jit, false, a, tiles, rt, stream);
+  } else {
+    hipLaunchKernelGGL(program_size_kernel, dim3((uint32_t)tiles), dim3(kET), rt, stream, a,
+                       d_prog);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess)
+    e = launch_scan_tiles(a.block_sums, tiles, part, &a.res->total_bytes, a.offs + a.n, stream);
   if (e != hipSuccess || size_only) return e;
+  if (jit) return jit_launch_encode(jit, true, a, tiles, rt + kOutCap + 32, stream);
   hipLaunchKernelGGL(program_write_kernel, dim3((uint32_t)tiles), dim3(kET), rt + kOutCap + 32,
                      stream, a, d_prog);
   return hipGetLastError();

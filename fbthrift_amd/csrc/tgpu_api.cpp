@@ -404,6 +404,14 @@ int ensure_workspace(tgpu_context* ctx, uint64_t n) {
   return TGPU_OK;
 }
 
+// The schema's compiled kernels for `protocol` (tgpu_jit.cpp policy), or
+// nullptr: the interpreting kernels run.
+const JitKernels* schema_jit(const tgpu_schema* s, int protocol, int group, uint64_t records,
+                             uint64_t bytes) {
+  if (!s->has_prog[protocol]) return nullptr;
+  return jit_kernels(s->prog[protocol], s->device, group, records, bytes, false);
+}
+
 DevSchema dev_schema(const tgpu_schema* s) {
   return DevSchema{s->d_structs, s->d_fields, (uint32_t)s->structs.size(),
                    (uint32_t)s->fields.size()};
@@ -419,7 +427,8 @@ hipError_t launch_indexed_decode(tgpu_context* ctx, const tgpu_schema* schema, i
   const int32_t height = a.height ? a.height : a.max_depth;
   if (schema->has_prog[protocol] && height >= 2 && a.max_depth >= 2) {
     hipError_t e = launch_program_decode(a, schema->d_prog[protocol], a.rec_size, ctx->d_irr,
-                                         &ctx->d_res->n_irregular, s);
+                                         &ctx->d_res->n_irregular, s,
+                                         schema_jit(schema, protocol, JIT_DECODE, a.n, 0));
     if (e == hipSuccess)
       e = launch_general_decode_list(a, protocol, ctx->d_irr, &ctx->d_res->n_irregular, s);
     return e;
@@ -486,7 +495,8 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
     if (e == hipSuccess) e = launch_index_empty(x.res, offs, x.begin, fill_to, s);
     return TGPU_OK;
   }
-  if (e == hipSuccess) e = launch_index_stream(x, s);
+  if (e == hipSuccess)
+    e = launch_index_stream(x, s, x.prog ? schema_jit(schema, protocol, JIT_INDEX, 0, end - begin) : nullptr);
   return TGPU_OK;
 }
 
@@ -609,6 +619,32 @@ void tgpu_schema_destroy(tgpu_schema* s) {
 
 uint32_t tgpu_schema_record_size(const tgpu_schema* s) { return s ? s->structs[0].size : 0; }
 
+int tgpu_schema_compile(const tgpu_schema* s, int protocol) {
+  if (!s || (protocol != TGPU_PROTOCOL_BINARY && protocol != TGPU_PROTOCOL_COMPACT))
+    return TGPU_ERR_INVALID_ARGUMENT;
+  if (!s->has_prog[protocol]) return TGPU_ERR_UNSUPPORTED;
+  for (int group : {JIT_DECODE, JIT_ENCODE, JIT_INDEX})
+    if (!jit_kernels(s->prog[protocol], s->device, group, 0, 0, true)) return TGPU_ERR_UNSUPPORTED;
+  return TGPU_OK;
+}
+
+int tgpu_schema_compile_check(const tgpu_struct_desc* structs, uint32_t n_structs,
+                              const tgpu_field_desc* fields, uint32_t n_fields, int protocol,
+                              const char* arch, char* log, uint64_t log_capacity) {
+  if (!structs || n_structs == 0 || (!fields && n_fields) ||
+      (protocol != TGPU_PROTOCOL_BINARY && protocol != TGPU_PROTOCOL_COMPACT))
+    return TGPU_ERR_INVALID_ARGUMENT;
+  bool has_lists = false;
+  const int rc = validate(structs, n_structs, fields, n_fields, 0, 0, has_lists);
+  if (rc) return rc;
+  tgpu_schema h;  // host tables only: nothing is uploaded
+  h.structs.assign(structs, structs + n_structs);
+  h.fields.assign(fields, fields + n_fields);
+  VProgram P{};
+  if (!build_program(h, protocol, P)) return TGPU_ERR_UNSUPPORTED;
+  return jit_compile_check(P, arch, log, log_capacity);
+}
+
 uint64_t tgpu_schema_fixed_wire_size(const tgpu_schema* s, int protocol) {
   return (s && protocol == TGPU_PROTOCOL_BINARY && s->fixed_binary) ? s->tmpl.wire_len : 0;
 }
@@ -714,7 +750,8 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
     a.scan_part = ctx->d_scan_part;
     if (e == hipSuccess && n) {
       if (schema->has_prog[protocol] && program_encode_fits(rs))
-        e = launch_program_encode(a, schema->d_prog[protocol], ctx->d_scan_part, false, s);
+        e = launch_program_encode(a, schema->d_prog[protocol], ctx->d_scan_part, false, s,
+                                  schema_jit(schema, protocol, JIT_ENCODE, n, 0));
       else
         e = launch_general_encode(a, protocol, nb, s);
     }
@@ -770,7 +807,8 @@ int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   hipError_t e = launch_result_init(ctx->d_res, n, s);
   if (e == hipSuccess && n) {
     if (schema->has_prog[protocol] && program_encode_fits(a.rec_size)) {
-      e = launch_program_encode(a, schema->d_prog[protocol], ctx->d_scan_part, true, s);
+      e = launch_program_encode(a, schema->d_prog[protocol], ctx->d_scan_part, true, s,
+                                schema_jit(schema, protocol, JIT_ENCODE, n, 0));
       if (e == hipSuccess) e = launch_size_offsets(a, (n + 255) / 256, s);
     } else {
       e = launch_general_size(a, protocol, (n + 255) / 256, s);

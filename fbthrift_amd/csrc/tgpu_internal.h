@@ -2,10 +2,25 @@
 // kernels of the bulk Thrift record codec. Not part of the public ABI.
 #pragma once
 
+#ifdef __HIPCC_RTC__
+// Runtime-compiled schema kernels (tgpu_jit.cpp): hipRTC has no libc headers,
+// so the fixed-width types are declared here with the host's LP64 widths.
+typedef signed char int8_t;
+typedef short int16_t;
+typedef int int32_t;
+typedef long int64_t;
+typedef unsigned char uint8_t;
+typedef unsigned short uint16_t;
+typedef unsigned int uint32_t;
+typedef unsigned long uint64_t;
+typedef unsigned long uintptr_t;
+#include "thrift_gpu.h"
+#else
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/thrift_gpu.h"
+#endif
 
 namespace tgpu {
 
@@ -173,61 +188,6 @@ struct EncodeArgs {
   DevResult* res;
 };
 
-// Launchers (defined in the .hip files; all asynchronous on `stream`).
-// `t` is the host copy (launch geometry), `d_t` the device copy the kernels read.
-hipError_t launch_fixed_binary_decode(const FixedTemplate* t, const FixedTemplate* d_t,
-                                      const uint8_t* in, uint64_t n, uint8_t* out,
-                                      DevResult* res, hipStream_t stream);
-hipError_t launch_fixed_binary_encode(const FixedTemplate* t, const FixedTemplate* d_t,
-                                      const uint8_t* recs, uint64_t n, uint8_t* out,
-                                      uint64_t* offsets, DevResult* res,
-                                      hipStream_t stream);
-// Word-gather variants (S % 8 == 0, record buffer 8-byte aligned).
-hipError_t launch_plan_binary_decode(const FixedPlan* p, const FixedPlan* d_p,
-                                     const uint8_t* in, uint64_t n, uint8_t* out,
-                                     DevResult* res, hipStream_t stream);
-hipError_t launch_plan_binary_encode(const FixedPlan* p, const FixedPlan* d_p,
-                                     const uint8_t* recs, uint64_t n, uint8_t* out,
-                                     uint64_t* offsets, DevResult* res,
-                                     hipStream_t stream);
-hipError_t launch_general_decode(const DecodeArgs& a, int protocol,
-                                 hipStream_t stream);
-// Compiled-program fast path over an indexed stream (a.offs): canonical records
-// are decoded from an LDS-staged tile; the others are appended to `irregular`
-// (count in *n_irregular) and decoded by launch_general_decode_list.
-hipError_t launch_program_decode(const DecodeArgs& a, const VProgram* d_prog,
-                                 uint32_t rec_size, uint64_t* irregular,
-                                 unsigned long long* n_irregular, hipStream_t stream);
-hipError_t launch_general_decode_list(const DecodeArgs& a, int protocol,
-                                      const uint64_t* list,
-                                      const unsigned long long* n_list,
-                                      hipStream_t stream);
-hipError_t launch_serial_decode(const DecodeArgs& a, int protocol,
-                                bool from_irregular, uint64_t fixed_len,
-                                hipStream_t stream);
-hipError_t launch_decode_finish(const DecodeArgs& a, int protocol,
-                                uint64_t fixed_len, hipStream_t stream);
-hipError_t launch_general_encode(const EncodeArgs& a, int protocol,
-                                 uint64_t n_blocks, hipStream_t stream);
-hipError_t launch_general_size(const EncodeArgs& a, int protocol,
-                               uint64_t n_blocks, hipStream_t stream);
-hipError_t launch_encode_finish(const EncodeArgs& a, int protocol,
-                                uint64_t fixed_len, hipStream_t stream);
-hipError_t launch_result_init(DevResult* res, uint64_t n, hipStream_t stream);
-// Exclusive scan of nb per-tile byte counts in place; the total goes to
-// *total1 and *total2 (either may be null). `part` holds scan_tiles_parts(nb)
-// entries.
-hipError_t launch_scan_tiles(unsigned long long* sums, uint64_t nb, unsigned long long* part,
-                             unsigned long long* total1, uint64_t* total2, hipStream_t stream);
-uint64_t scan_tiles_parts(uint64_t nb);
-// Compiled-program encode (all-unqualified schemas): size pass, tile scan and,
-// unless size_only, the write pass. a.offs receives sizes then start offsets
-// (size_only: sizes, tile sums scanned; launch_size_offsets finishes them).
-bool program_encode_fits(uint32_t rec_size);
-hipError_t launch_program_encode(const EncodeArgs& a, const VProgram* d_prog,
-                                 unsigned long long* part, bool size_only, hipStream_t stream);
-hipError_t launch_size_offsets(const EncodeArgs& a, uint64_t n_blocks, hipStream_t stream);
-
 // ---- stream indexer (k_index.hip) -------------------------------------------
 // Finds the start of every record beginning in [begin, end) of an unindexed
 // stream: lanes speculate record starts per chunk, a serial pass repairs the
@@ -264,13 +224,91 @@ struct IndexArgs {
   uint64_t fill_to;          // decode: offs[total+1 .. fill_to] = last end
   DevResult* res;
 };
+
+#ifndef __HIPCC_RTC__
+// Launchers (defined in the .hip files; all asynchronous on `stream`).
+// `t` is the host copy (launch geometry), `d_t` the device copy the kernels read.
+hipError_t launch_fixed_binary_decode(const FixedTemplate* t, const FixedTemplate* d_t,
+                                      const uint8_t* in, uint64_t n, uint8_t* out,
+                                      DevResult* res, hipStream_t stream);
+hipError_t launch_fixed_binary_encode(const FixedTemplate* t, const FixedTemplate* d_t,
+                                      const uint8_t* recs, uint64_t n, uint8_t* out,
+                                      uint64_t* offsets, DevResult* res,
+                                      hipStream_t stream);
+// Word-gather variants (S % 8 == 0, record buffer 8-byte aligned).
+hipError_t launch_plan_binary_decode(const FixedPlan* p, const FixedPlan* d_p,
+                                     const uint8_t* in, uint64_t n, uint8_t* out,
+                                     DevResult* res, hipStream_t stream);
+hipError_t launch_plan_binary_encode(const FixedPlan* p, const FixedPlan* d_p,
+                                     const uint8_t* recs, uint64_t n, uint8_t* out,
+                                     uint64_t* offsets, DevResult* res,
+                                     hipStream_t stream);
+hipError_t launch_general_decode(const DecodeArgs& a, int protocol,
+                                 hipStream_t stream);
+// Compiled-program fast path over an indexed stream (a.offs): canonical records
+// are decoded from an LDS-staged tile; the others are appended to `irregular`
+// (count in *n_irregular) and decoded by launch_general_decode_list.
+// ---- schema compiler (tgpu_jit.cpp) ------------------------------------------
+// Kernels generated and compiled for one program (nullptr: not compiled —
+// policy or failure; the interpreting kernels run instead).
+struct JitKernels;
+enum JitGroup { JIT_DECODE = 0, JIT_ENCODE = 1, JIT_INDEX = 2 };
+const JitKernels* jit_kernels(const VProgram& prog, int device, int group, uint64_t records,
+                              uint64_t bytes, bool force);
+int jit_compile_check(const VProgram& P, const char* arch, char* log, uint64_t log_cap);
+hipError_t jit_launch_decode(const JitKernels* J, const DecodeArgs& a, uint64_t grid,
+                             uint32_t cap, uint32_t lds, uint64_t* irr, unsigned long long* nirr,
+                             hipStream_t s);
+hipError_t jit_launch_encode(const JitKernels* J, bool write, const EncodeArgs& a, uint64_t grid,
+                             uint32_t lds, hipStream_t s);
+hipError_t jit_launch_index(const JitKernels* J, bool emit, const IndexArgs& a, uint64_t grid,
+                            hipStream_t s);
+
+// jit: the schema's compiled kernels (nullptr: interpret d_prog).
+hipError_t launch_program_decode(const DecodeArgs& a, const VProgram* d_prog,
+                                 uint32_t rec_size, uint64_t* irregular,
+                                 unsigned long long* n_irregular, hipStream_t stream,
+                                 const JitKernels* jit);
+hipError_t launch_general_decode_list(const DecodeArgs& a, int protocol,
+                                      const uint64_t* list,
+                                      const unsigned long long* n_list,
+                                      hipStream_t stream);
+hipError_t launch_serial_decode(const DecodeArgs& a, int protocol,
+                                bool from_irregular, uint64_t fixed_len,
+                                hipStream_t stream);
+hipError_t launch_decode_finish(const DecodeArgs& a, int protocol,
+                                uint64_t fixed_len, hipStream_t stream);
+hipError_t launch_general_encode(const EncodeArgs& a, int protocol,
+                                 uint64_t n_blocks, hipStream_t stream);
+hipError_t launch_general_size(const EncodeArgs& a, int protocol,
+                               uint64_t n_blocks, hipStream_t stream);
+hipError_t launch_encode_finish(const EncodeArgs& a, int protocol,
+                                uint64_t fixed_len, hipStream_t stream);
+hipError_t launch_result_init(DevResult* res, uint64_t n, hipStream_t stream);
+// Exclusive scan of nb per-tile byte counts in place; the total goes to
+// *total1 and *total2 (either may be null). `part` holds scan_tiles_parts(nb)
+// entries.
+hipError_t launch_scan_tiles(unsigned long long* sums, uint64_t nb, unsigned long long* part,
+                             unsigned long long* total1, uint64_t* total2, hipStream_t stream);
+uint64_t scan_tiles_parts(uint64_t nb);
+// Compiled-program encode (all-unqualified schemas): size pass, tile scan and,
+// unless size_only, the write pass. a.offs receives sizes then start offsets
+// (size_only: sizes, tile sums scanned; launch_size_offsets finishes them).
+bool program_encode_fits(uint32_t rec_size);
+hipError_t launch_program_encode(const EncodeArgs& a, const VProgram* d_prog,
+                                 unsigned long long* part, bool size_only, hipStream_t stream,
+                                 const JitKernels* jit);
+hipError_t launch_size_offsets(const EncodeArgs& a, uint64_t n_blocks, hipStream_t stream);
+
+// ---- stream indexer (k_index.hip) launchers
 uint64_t index_chunk_bytes(uint64_t span, bool tiles);
 uint64_t index_tile_bytes();
 uint64_t index_tile_lanes();
-hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream);
+hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const JitKernels* jit);
 // Empty range: offs[0..fill_to] = pos, no records.
 hipError_t launch_index_empty(DevResult* res, uint64_t* offs, uint64_t pos, uint64_t fill_to,
                               hipStream_t stream);
+#endif  // !__HIPCC_RTC__
 
 }  // namespace tgpu
 

@@ -1,0 +1,749 @@
+// tgpu_prog_kernels.h — bodies of the compiled-program kernels, templated on
+// the program accessor (tgpu_program.h). The AOT library instantiates them
+// with DynProg (k_program.hip, k_program_enc.hip, k_index.hip); the schema
+// kernels generated at run time instantiate them with the schema's ops as
+// compile-time constants (tgpu_jit.cpp). Not part of the public ABI.
+//
+//   decode_tile  indexed decode of one 256-record tile (configs 3, 4)
+//   size_tile    encode pass 1: per-record wire size + tile sum
+//   write_tile   encode pass 3: records -> LDS output tile -> HBM
+//   index_spec_tile / index_emit_tile  stream index over one LDS tile
+#pragma once
+
+#include "tgpu_program.h"
+
+namespace tgpu {
+namespace prog {
+
+constexpr uint32_t kPT = 256;            // decode: records per tile = threads per workgroup
+constexpr uint32_t kET = 256;            // encode: records per tile = threads per workgroup
+constexpr uint32_t kOutCap = 24 * 1024;  // encode: LDS bytes for one tile's wire output
+
+// ---- block helpers (256 threads) --------------------------------------------
+__device__ __forceinline__ unsigned long long wave_incl_scan(unsigned long long x) {
+  const int lane = threadIdx.x & 63;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  return x;
+}
+
+// exclusive scan across the block; *total = block sum (all threads)
+__device__ __forceinline__ unsigned long long block_exscan256(unsigned long long v,
+                                                              unsigned long long* part,
+                                                              unsigned long long* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const unsigned long long x = wave_incl_scan(v);
+  if (lane == 63) part[wid] = x;
+  __syncthreads();
+  unsigned long long pre = 0;
+  for (int w = 0; w < wid; ++w) pre += part[w];
+  *total = part[0] + part[1] + part[2] + part[3];
+  return pre + x - v;
+}
+
+// ================================================================ decode ======
+// One lane runs the program over one record of the tile:
+//   * the tile's bytes [offs[r0], offs[r0+256]) go HBM -> LDS with coalesced
+//     16-byte loads (a tile larger than wire_cap falls back);
+//   * each lane reads its record from LDS through 8-byte windows, decodes
+//     varints branch-free, and writes the record into an LDS record tile
+//     (strings become zero-copy views; list elements go to the arena);
+//   * the record tile goes LDS -> HBM with coalesced 16-byte stores.
+// A record that deviates from the canonical form in any way is NOT decided
+// here: its index is appended to `irr` and the general decoder (full
+// readNoXfer semantics, tgpu_device.h) decodes it.
+// smem: wire_cap + 32 bytes of wire tile, then kPT * S + 16 record tile.
+template <class PP>
+__device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, uint32_t S,
+                                            uint32_t wire_cap, uint64_t* __restrict__ irr,
+                                            unsigned long long* __restrict__ nirr,
+                                            uint8_t* smem) {
+  uint8_t* wire = smem;
+  uint8_t* rtile = smem + wire_cap + 32;
+  const uint64_t r0 = (uint64_t)blockIdx.x * kPT;
+  const uint32_t nrec = (uint32_t)min((uint64_t)kPT, a.n - r0);
+  const uint64_t t0 = a.offs[r0], t1 = a.offs[r0 + nrec];
+  const bool tile_ok = t1 >= t0 && t1 <= a.in_len && (t1 - t0) + 16 <= wire_cap;
+  uint32_t sh = 0;
+  if (tile_ok) {
+    const uint8_t* g = a.in + t0;
+    sh = (uint32_t)((uintptr_t)g & 15);
+    const uint4* src = (const uint4*)(g - sh);
+    const uint32_t nvec = (uint32_t)((t1 - t0) + sh + 15) >> 4;
+    for (uint32_t i = threadIdx.x; i < nvec; i += kPT) ((uint4*)wire)[i] = src[i];
+  }
+  uint8_t* gout = a.recs + r0 * S;
+  const uint32_t osh = (uint32_t)((uintptr_t)gout & 15);
+  {
+    const uint4 z = {0u, 0u, 0u, 0u};
+    const uint32_t nz = (kPT * S + osh + 15) >> 4;
+    for (uint32_t i = threadIdx.x; i < nz; i += kPT) ((uint4*)rtile)[i] = z;
+  }
+  __syncthreads();
+
+  const uint32_t r = threadIdx.x;
+  if (r < nrec) {
+    uint8_t* rec = rtile + osh + r * S;
+    bool ok = tile_ok;
+    if (ok) {
+      const uint64_t s = a.offs[r0 + r], e = a.offs[r0 + r + 1];
+      ok = s >= t0 && e >= s && e <= t1;
+      if (ok) {
+        const Ctx c{t0 - sh, a.arena, a.arena_cap, a.string_limit, a.container_limit};
+        const LdsSrc src{(const uint32_t*)wire};
+        uint32_t p = (uint32_t)(s - t0) + sh;
+        const uint32_t pe = (uint32_t)(e - t0) + sh;
+        ok = run_program<true>(P, src, c, p, pe, rec) && p == pe;
+      }
+    }
+    if (!ok) {
+      const unsigned long long k = atomicAdd(nirr, 1ull);
+      irr[k] = r0 + r;
+    }
+  }
+  __syncthreads();
+  // record tile -> HBM
+  const uint32_t end = osh + nrec * S;
+  const uint32_t nvec = (end + 15) >> 4;
+  uint8_t* base = gout - osh;
+  for (uint32_t i = threadIdx.x; i < nvec; i += kPT) {
+    const uint32_t lo = i << 4, hi = lo + 16;
+    if (lo >= osh && hi <= end) {
+      ((uint4*)base)[i] = ((const uint4*)rtile)[i];
+    } else {
+      for (uint32_t b = (lo < osh ? osh : lo); b < (hi < end ? hi : end); ++b) base[b] = rtile[b];
+    }
+  }
+}
+
+// ================================================================ encode ======
+__device__ __forceinline__ uint32_t varint_len(uint64_t v) {
+  const uint32_t bits = 64 - (uint32_t)__builtin_clzll(v | 1);
+  return (bits + 6) / 7;
+}
+
+__device__ __forceinline__ uint64_t load_member(const uint8_t* p, uint32_t width) {
+  switch (width) {
+    case 8: return *(const uint64_t*)p;
+    case 4: return *(const uint32_t*)p;
+    case 2: return *(const uint16_t*)p;
+    default: return *p;
+  }
+}
+
+// zigzag of a signed member of `width` bytes, as i32 (bits 32) or i64
+__device__ __forceinline__ uint64_t zz_member(uint64_t raw, uint32_t width, uint32_t bits) {
+  int64_t v;
+  switch (width) {
+    case 2: v = (int16_t)(uint16_t)raw; break;
+    case 4: v = (int32_t)(uint32_t)raw; break;
+    default: v = (int64_t)raw; break;
+  }
+  if (bits == 32) return i32_to_zz((int32_t)v);
+  return i64_to_zz(v);
+}
+
+// Bytes T::write emits for the record at `rec`; ok = false where the writer
+// would throw or abort (the finish kernel re-derives the exact code).
+template <class PP>
+__device__ __forceinline__ uint64_t program_size(const PP& P, const uint8_t* rec,
+                                                 const uint8_t* __restrict__ lbase, bool& ok) {
+  const bool compact = P.protocol() == TGPU_PROTOCOL_COMPACT;
+  uint64_t n = 0;
+  all_ops(P, [&](const VOp op) {
+    switch (op.kind) {
+      case VOP_CONST:
+        n += op.hdr_len;
+        break;
+      case VOP_CBOOL:
+        if (rec[op.member] > 1) ok = false;
+        n += op.hdr_len;
+        break;
+      case VOP_FIXED:
+        if (op.is_bool && rec[op.member] > 1) ok = false;
+        n += op.width;
+        break;
+      case VOP_VARINT:
+        n += varint_len(zz_member(load_member(rec + op.member, op.width), op.width, op.bits));
+        break;
+      case VOP_STRING: {
+        const uint32_t len = ((const tgpu_span*)(rec + op.member))->length;
+        if (len > 0x7fffffffu) ok = false;
+        n += (compact ? varint_len(len) : 4) + (uint64_t)len;
+        break;
+      }
+      case VOP_LIST: {
+        const tgpu_span sp = *(const tgpu_span*)(rec + op.member);
+        const uint32_t len = sp.length;
+        if (len > 0x7fffffffu) {
+          ok = false;
+          break;
+        }
+        n += compact ? (len <= 14 ? 1 : 1 + varint_len(len)) : 5;
+        const uint8_t* e = lbase + sp.offset;
+        if (op.elem_kind == VEL_VARINT) {
+          for (uint32_t i = 0; i < len; ++i)
+            n += varint_len(zz_member(load_member(e + (uint64_t)i * op.width, op.width), op.width,
+                                      op.bits));
+        } else if (op.elem_kind == VEL_BOOL) {
+          for (uint32_t i = 0; i < len; ++i)
+            if (e[i] > 1) ok = false;
+          n += len;
+        } else {
+          n += (uint64_t)len * op.width;
+        }
+        break;
+      }
+      default:
+        break;
+    }
+    return true;
+  });
+  return n;
+}
+
+// Sinks: the LDS output tile (position q relative to the tile's LDS base) or
+// HBM directly (q relative to the record's HBM start).
+struct ByteSink {
+  uint8_t* base;
+  __device__ __forceinline__ void put(uint32_t q, uint32_t b) const { base[q] = (uint8_t)b; }
+};
+
+template <class Sink>
+__device__ __forceinline__ uint32_t put_be(const Sink& s, uint32_t q, uint64_t v, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) s.put(q + i, (uint32_t)(v >> (8 * (n - 1 - i))));
+  return q + n;
+}
+template <class Sink>
+__device__ __forceinline__ uint32_t put_varint(const Sink& s, uint32_t q, uint64_t v) {
+  while (v & ~0x7full) {
+    s.put(q++, (uint32_t)((v & 0x7f) | 0x80));
+    v >>= 7;
+  }
+  s.put(q++, (uint32_t)v);
+  return q;
+}
+// len bytes from HBM (any alignment): aligned dword loads, bytes out
+template <class Sink>
+__device__ __forceinline__ uint32_t put_bytes(const Sink& s, uint32_t q,
+                                              const uint8_t* __restrict__ src, uint32_t len) {
+  if (!len) return q;
+  const uintptr_t a = (uintptr_t)src;
+  const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
+  uint32_t sh = (uint32_t)(a & 3);
+  uint32_t i = 0;
+  while (i < len) {
+    const uint32_t word = *w++;
+    for (uint32_t b = sh; b < 4 && i < len; ++b, ++i) s.put(q + i, (word >> (8 * b)) & 0xff);
+    sh = 0;
+  }
+  return q + len;
+}
+
+template <class PP, class Sink>
+__device__ __forceinline__ void program_emit(const PP& P, const uint8_t* rec,
+                                             const uint8_t* __restrict__ sbase,
+                                             const uint8_t* __restrict__ lbase, const Sink& s) {
+  const bool compact = P.protocol() == TGPU_PROTOCOL_COMPACT;
+  uint32_t q = 0;
+  all_ops(P, [&](const VOp op) {
+    switch (op.kind) {
+      case VOP_CONST:
+        for (uint32_t i = 0; i < op.hdr_len; ++i) s.put(q + i, (op.hdr >> (8 * i)) & 0xff);
+        q += op.hdr_len;
+        break;
+      case VOP_CBOOL: {
+        // the bool's value rides in the header's type nibble (CT_BOOLEAN_TRUE/FALSE)
+        const uint32_t h = op.hdr | (rec[op.member] ? 1u : 2u);
+        for (uint32_t i = 0; i < op.hdr_len; ++i) s.put(q + i, (h >> (8 * i)) & 0xff);
+        q += op.hdr_len;
+        break;
+      }
+      case VOP_FIXED:
+        q = put_be(s, q, load_member(rec + op.member, op.width), op.width);
+        break;
+      case VOP_VARINT:
+        q = put_varint(s, q, zz_member(load_member(rec + op.member, op.width), op.width, op.bits));
+        break;
+      case VOP_STRING: {
+        const tgpu_span sp = *(const tgpu_span*)(rec + op.member);
+        q = compact ? put_varint(s, q, sp.length) : put_be(s, q, sp.length, 4);
+        q = put_bytes(s, q, sbase + sp.offset, sp.length);
+        break;
+      }
+      case VOP_LIST: {
+        const tgpu_span sp = *(const tgpu_span*)(rec + op.member);
+        const uint32_t len = sp.length;
+        if (compact) {
+          if (len <= 14) {
+            s.put(q++, (len << 4) | op.elem_ct);
+          } else {
+            s.put(q++, 0xf0 | op.elem_ct);
+            q = put_varint(s, q, len);
+          }
+        } else {
+          s.put(q++, op.elem_ttype);
+          q = put_be(s, q, len, 4);
+        }
+        const uint8_t* e = lbase + sp.offset;
+        if (op.elem_kind == VEL_VARINT) {
+          for (uint32_t i = 0; i < len; ++i)
+            q = put_varint(s, q, zz_member(load_member(e + (uint64_t)i * op.width, op.width),
+                                           op.width, op.bits));
+        } else if (op.elem_kind == VEL_BOOL) {
+          for (uint32_t i = 0; i < len; ++i) s.put(q++, compact ? (e[i] ? 1u : 2u) : e[i]);
+        } else {
+          for (uint32_t i = 0; i < len; ++i)
+            q = put_be(s, q, load_member(e + (uint64_t)i * op.width, op.width), op.width);
+        }
+        break;
+      }
+      default:
+        break;
+    }
+    return true;
+  });
+}
+
+// Records [r0, r0+nrec) of stride S into LDS; returns the 16-byte phase.
+__device__ __forceinline__ uint32_t stage_records(const uint8_t* recs, uint64_t r0, uint32_t nrec,
+                                                  uint32_t S, uint8_t* rtile) {
+  const uint8_t* g = recs + r0 * S;
+  const uint32_t sh = (uint32_t)((uintptr_t)g & 15);
+  const uint4* src = (const uint4*)(g - sh);
+  const uint32_t nvec = (nrec * S + sh + 15) >> 4;
+  for (uint32_t i = threadIdx.x; i < nvec; i += kET) ((uint4*)rtile)[i] = src[i];
+  return sh;
+}
+
+// Pass 1: record tile HBM -> LDS; each lane sizes its record; sizes ->
+// a.offs[i]; tile sum -> block_sums[t]; validation failures -> first_fail.
+template <class PP>
+__device__ __forceinline__ void size_tile(const EncodeArgs& a, const PP& P, uint32_t S,
+                                          uint8_t* smem, unsigned long long* part) {
+  const uint64_t r0 = (uint64_t)blockIdx.x * kET;
+  const uint32_t nrec = (uint32_t)min((uint64_t)kET, a.n - r0);
+  const uint32_t sh = stage_records(a.recs, r0, nrec, S, smem);
+  __syncthreads();
+  unsigned long long sz = 0;
+  if (threadIdx.x < nrec) {
+    bool ok = true;
+    sz = program_size(P, smem + sh + threadIdx.x * S, a.lbase, ok);
+    if (!ok) atomicMin(&a.res->first_fail, (unsigned long long)(r0 + threadIdx.x));
+    a.offs[r0 + threadIdx.x] = sz;
+  }
+  unsigned long long total;
+  (void)block_exscan256(sz, part, &total);
+  if (threadIdx.x == 0) a.block_sums[blockIdx.x] = total;
+}
+
+// Pass 3: record tile -> LDS again, block exclusive scan of the sizes gives
+// each lane its position in the tile; the lane emits its record into an LDS
+// output tile (records past the LDS cap go to HBM directly); the tile leaves
+// with coalesced 16-byte stores (byte stores only on the two edge chunks
+// shared with the neighbouring tiles).
+template <class PP>
+__device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uint32_t S,
+                                           uint8_t* smem, unsigned long long* part,
+                                           unsigned int* lds_end_p) {
+  const uint64_t r0 = (uint64_t)blockIdx.x * kET;
+  const uint32_t nrec = (uint32_t)min((uint64_t)kET, a.n - r0);
+  uint8_t* rtile = smem;
+  uint8_t* otile = smem + ((kET * S + 16 + 15) & ~15u);
+  const uint32_t rsh = stage_records(a.recs, r0, nrec, S, rtile);
+  const uint32_t r = threadIdx.x;
+  const unsigned long long sz = r < nrec ? a.offs[r0 + r] : 0;
+  unsigned long long tile_total;
+  const unsigned long long rel = block_exscan256(sz, part, &tile_total);
+  const unsigned long long tile_base = a.block_sums[blockIdx.x];
+  unsigned int& lds_end = *lds_end_p;
+  if (r == 0) lds_end = (unsigned int)min(tile_total, (unsigned long long)kOutCap);
+  __syncthreads();  // record tile staged, lds_end initialised
+  uint8_t* gtile = a.out + tile_base;
+  const uint32_t osh = (uint32_t)((uintptr_t)gtile & 15);
+  bool fits = false;
+  if (r < nrec) {
+    const unsigned long long start = tile_base + rel;
+    a.offs[r0 + r] = start;
+    if (start + sz > a.cap) {
+      atomicMin(&a.res->first_fail, (unsigned long long)(r0 + r));
+      atomicMin(&lds_end, (unsigned int)min(rel, (unsigned long long)kOutCap));
+    } else {
+      fits = rel + sz <= kOutCap;
+      if (!fits) atomicMin(&lds_end, (unsigned int)rel);
+    }
+  }
+  __syncthreads();
+  if (r < nrec) {
+    const uint8_t* rec = rtile + rsh + r * S;
+    if (fits && rel + sz <= lds_end) {
+      program_emit(P, rec, a.sbase, a.lbase, ByteSink{otile + osh + (uint32_t)rel});
+    } else if (tile_base + rel + sz <= a.cap) {
+      program_emit(P, rec, a.sbase, a.lbase, ByteSink{gtile + rel});
+    }
+  }
+  __syncthreads();
+  // LDS tile [osh, osh + lds_end) -> HBM [gtile, gtile + lds_end)
+  const uint32_t end = osh + lds_end;
+  const uint32_t nvec = (end + 15) >> 4;
+  uint8_t* gb = gtile - osh;
+  for (uint32_t i = threadIdx.x; i < nvec; i += kET) {
+    const uint32_t lo = i << 4, hi = lo + 16;
+    if (lo >= osh && hi <= end) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      __builtin_nontemporal_store(((const u32x4*)otile)[i], (u32x4*)gb + i);
+    } else {
+      for (uint32_t b = (lo < osh ? osh : lo); b < (hi < end ? hi : end); ++b) gb[b] = otile[b];
+    }
+  }
+}
+
+// ================================================================= index ======
+// A chunk is a tile of kTile bytes handled by one workgroup: the tile (plus
+// kOver bytes for the records that straddle its end) is staged in LDS with
+// coalesced 16-byte loads; lane k speculates the first record start in its
+// kSub-byte slice and chains to the slice's end; the lanes' links are then
+// repaired inside the workgroup (lane k restarts from lane k-1's end until
+// no lane changes), so the tile behaves like one chunk of the lane path:
+// (first start, end, count). A tile any lane could not finish with the
+// program is handed to the general-reader kernels whole (kPartial).
+constexpr uint64_t kNo = ~0ull;             // no start found / unset
+constexpr uint64_t kErr = ~0ull - 1;        // chain ended in a reader error
+constexpr uint64_t kPartial = ~0ull - 2;    // program stopped: general reader continues
+constexpr uint64_t kLanesValid = ~0ull - 3; // pf: the tile's per-lane results are current
+constexpr uint32_t kPosCap = 0x7fffff00u;
+constexpr uint32_t kTileLanes = 256;
+constexpr uint32_t kSub = 64;
+constexpr uint32_t kTile = kTileLanes * kSub;
+constexpr uint32_t kOver = 4096;
+constexpr uint32_t kTileLds = kTile + kOver + 32;
+constexpr uint32_t kNoPos = 0xffffffffu;
+
+__device__ __forceinline__ uint64_t chunk_lo(const IndexArgs& a, uint64_t j) {
+  return a.begin + j * a.chunk;
+}
+__device__ __forceinline__ uint64_t chunk_hi(const IndexArgs& a, uint64_t j) {
+  const uint64_t h = a.begin + (j + 1) * a.chunk;
+  return h < a.end ? h : a.end;
+}
+
+// LDS window with HBM fallback past the staged bytes (positions relative to
+// the 16-byte aligned tile base)
+// (the HBM path is rare — records straddling the staged bytes — and kept out
+// of line: inlined at every window of an unrolled program it multiplies the
+// schema compiler's code size and compile time)
+__device__ __attribute__((noinline)) uint64_t hbm_win8(const HbmSrc g, uint32_t p) {
+  return g.win8(p);
+}
+struct TileSrc {
+  const uint32_t* w32;
+  uint32_t lds_len;
+  HbmSrc g;
+  __device__ __forceinline__ uint64_t win8(uint32_t p) const {
+    if (p + 12 <= lds_len) return LdsSrc{w32}.win8(p);
+    return hbm_win8(g, p);
+  }
+};
+
+struct TileLane {
+  uint32_t s, e, c;  // first start, end, count (tile-relative); s == kNoPos: none
+  bool stuck;
+};
+
+// Cheap rejection of a candidate start before running the program: the byte
+// after the first header's value must be the second header (first ops
+// CONST, VARINT|FIXED, CONST — every schema whose first two fields are
+// unqualified scalars). Never rejects a canonical record start.
+template <class PP>
+__device__ __forceinline__ bool quick_reject(const PP& P, const TileSrc& src, uint32_t cand) {
+  if (P.n_ops() < 3) return false;
+  const VOp o0 = P.op(0), v = P.op(1), o2 = P.op(2);
+  if (o0.kind != VOP_CONST || o2.kind != VOP_CONST) return false;
+  const uint64_t w = src.win8(cand + o0.hdr_len);
+  uint32_t len;
+  if (v.kind == VOP_VARINT) {
+    const uint64_t stop = ~w & 0x8080808080808080ull;
+    if (!stop) return false;
+    len = ((uint32_t)__builtin_ctzll(stop) >> 3) + 1;
+  } else if (v.kind == VOP_FIXED) {
+    len = v.width;
+  } else {
+    return false;
+  }
+  if (len >= 8) return false;
+  return ((w >> (8 * len)) & 0xff) != (o2.hdr & 0xff);
+}
+
+// chain of canonical records from x while position < hi (tile-relative)
+template <class PP>
+__device__ __forceinline__ void tile_chain(const PP& P, const TileSrc& src, const Ctx& pc,
+                                           uint32_t x, uint32_t hi, uint32_t end, TileLane& L) {
+  L.s = x;
+  L.c = 0;
+  L.stuck = false;
+  uint32_t p = x;
+  while (p < hi) {
+    uint32_t q = p;
+    if (!run_program<false>(P, src, pc, q, end, nullptr)) {
+      L.stuck = true;
+      break;
+    }
+    ++L.c;
+    p = q;
+  }
+  L.e = p;
+}
+
+// Stages the tile, speculates and repairs the lanes' chains. entry: the
+// tile's known first start (tile-relative; kNoPos: speculate lane 0 too).
+// Returns false when the tile needs the general reader. *first: the tile's
+// first record start (kNoPos: none).
+template <class PP>
+__device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, uint64_t j,
+                                             uint8_t* lds, uint32_t entry, TileLane& L,
+                                             uint32_t& sh, uint32_t& first, uint32_t* E, int* flag,
+                                             uint32_t* first_lane, uint32_t* fs_p) {
+  const uint64_t lo = chunk_lo(a, j);
+  const uint64_t hi_abs = chunk_hi(a, j);
+  const uint8_t* g = a.in + lo;
+  sh = (uint32_t)((uintptr_t)g & 15);
+  const uint8_t* gb = g - sh;
+  const uint64_t avail64 = a.in_len - lo + sh;
+  const uint32_t avail = (uint32_t)(avail64 < kPosCap ? avail64 : kPosCap);
+  const uint32_t staged = avail < kTile + kOver + 16 ? avail : kTile + kOver + 16;
+  const uint32_t nvec = (staged + 15) >> 4;
+  for (uint32_t i = threadIdx.x; i < nvec; i += kTileLanes)
+    ((uint4*)lds)[i] = ((const uint4*)gb)[i];
+  __syncthreads();
+  const TileSrc src{(const uint32_t*)lds, staged & ~3u, HbmSrc{gb, avail}};
+  const Ctx pc{0, nullptr, 0, a.string_limit, a.container_limit};
+  const uint32_t thi = sh + (uint32_t)(hi_abs - lo);  // tile end (relative)
+  const uint32_t k = threadIdx.x;
+  const uint32_t sub_lo = sh + k * kSub;
+  const uint32_t sub_hi = sub_lo + kSub < thi ? sub_lo + kSub : thi;
+  L.s = kNoPos;
+  L.e = kNoPos;
+  L.c = 0;
+  L.stuck = false;
+  if (k == 0 && entry != kNoPos) {
+    tile_chain(P, src, pc, entry, sub_hi > entry ? sub_hi : entry, avail, L);
+    if (entry >= sub_hi) {  // the entry lies past lane 0's slice
+      L.s = entry;
+      L.e = entry;
+    }
+  } else if (sub_lo < thi) {
+    // candidates: bytes equal to the first header byte that survive
+    // quick_reject (divergent but cheap); the chain from a candidate runs
+    // outside the search so all lanes of the wave run it together
+    const VOp o0 = P.op(0);
+    const uint32_t h0 = o0.kind == VOP_CONST ? (o0.hdr & 0xff) : 0x100;
+    // bytes of the slice equal to h0, all eight 8-byte groups loaded at once
+    uint64_t mk[kSub / 8];
+#pragma unroll
+    for (uint32_t i = 0; i < kSub / 8; ++i) {
+      const uint32_t base = sub_lo + 8 * i;
+      uint64_t m = 0;
+      if (base < sub_hi) {
+        m = 0x8080808080808080ull;
+        if (h0 < 0x100) {
+          const uint64_t x = src.win8(base) ^ (h0 * 0x0101010101010101ull);
+          m = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
+        }
+      }
+      mk[i] = m;
+    }
+    uint32_t from = sub_lo;
+    bool need = true;
+    while (need) {
+      uint32_t cand = kNoPos;
+#pragma unroll
+      for (uint32_t i = 0; i < kSub / 8; ++i) {
+        uint64_t m = mk[i];
+        while (m && cand == kNoPos) {
+          const uint32_t c = sub_lo + 8 * i + ((uint32_t)__builtin_ctzll(m) >> 3);
+          m &= m - 1;
+          if (c < from || c >= sub_hi) continue;
+          if (quick_reject(P, src, c)) continue;
+          cand = c;
+        }
+      }
+      if (cand == kNoPos) break;  // no record start in this slice
+      TileLane t;
+      tile_chain(P, src, pc, cand, sub_hi, avail, t);
+      if (t.c) {
+        L = t;
+        need = false;
+      } else {
+        from = cand + 1;
+      }
+    }
+  }
+  // the tile's first start: the first lane that found one
+  if (k == 0) *first_lane = kTileLanes;
+  __syncthreads();
+  if (L.s != kNoPos) atomicMin(first_lane, k);
+  __syncthreads();
+  const uint32_t f = *first_lane;
+  if (f == kTileLanes) {
+    first = kNoPos;
+    return true;
+  }
+  // lanes before it: no record starts there
+  if (k == f) *fs_p = L.s;
+  __syncthreads();
+  const uint32_t fs = *fs_p;
+  if (k < f) {
+    L.s = L.e = fs;
+    L.c = 0;
+    L.stuck = false;
+  }
+  first = fs;
+  // repair: lane k restarts from lane k-1's end until nothing changes
+  for (uint32_t it = 0; it <= kTileLanes; ++it) {
+    E[k] = L.e;
+    __syncthreads();
+    int changed = 0;
+    if (k > f) {
+      const uint32_t x = E[k - 1];
+      if (x != kNoPos && (x != L.s || L.e == kNoPos)) {
+        if (x >= sub_hi) {
+          L.s = L.e = x;
+          L.c = 0;
+          L.stuck = false;
+        } else {
+          tile_chain(P, src, pc, x, sub_hi, avail, L);
+        }
+        changed = 1;
+      }
+    }
+    if (!__syncthreads_or(changed)) break;
+  }
+  *flag = 0;
+  __syncthreads();
+  if (L.stuck || L.e == kNoPos) *flag = 1;
+  __syncthreads();
+  return *flag == 0;
+}
+
+struct IndexTileShared {
+  uint32_t E[kTileLanes];
+  int flag;
+  uint32_t first_lane, fs;
+  unsigned long long csum;
+  unsigned long long part[4];
+};
+
+template <class PP>
+__device__ __forceinline__ void index_spec_tile(const IndexArgs& a, const PP& P, uint8_t* lds,
+                                                IndexTileShared& sm) {
+  const uint64_t j = blockIdx.x;
+  const uint64_t lo = chunk_lo(a, j);
+  // tile 0 of a non-speculative call starts at begin exactly (relative 0 + sh)
+  const uint32_t ent = (j == 0 && !a.speculative) ? (uint32_t)((uintptr_t)(a.in + lo) & 15)
+                                                  : kNoPos;
+  TileLane L;
+  uint32_t sh, first;
+  const bool ok = tile_resolve(a, P, j, lds, ent, L, sh, first, sm.E, &sm.flag, &sm.first_lane,
+                               &sm.fs);
+  if (threadIdx.x == 0) sm.csum = 0;
+  __syncthreads();
+  if (ok && first != kNoPos) atomicAdd(&sm.csum, (unsigned long long)L.c);
+  __syncthreads();
+  // per-lane starts/counts for the emit pass (valid while the tile keeps this
+  // start: pf[j] == kLanesValid)
+  if (ok && first != kNoPos)
+    a.lanes[j * kTileLanes + threadIdx.x] = (L.s & 0xffffu) | ((uint32_t)L.c << 16);
+  if (threadIdx.x == kTileLanes - 1) {
+    if (first == kNoPos) {
+      a.s[j] = kNo;
+      a.e[j] = kNo;
+      a.cnt[j] = 0;
+    } else if (!ok) {
+      // the general reader walks the whole tile from its (speculated) start
+      a.s[j] = lo - sh + first;
+      a.e[j] = kPartial;
+      a.pf[j] = lo - sh + first;
+      a.cnt[j] = 0;
+    } else {
+      a.s[j] = lo - sh + first;
+      a.e[j] = lo - sh + L.e;
+      a.cnt[j] = sm.csum;
+      a.pf[j] = kLanesValid;
+    }
+  }
+}
+
+// Emit for a tile whose first start is verified (a.s[j]); records starting in
+// the tile get their starts written at offs[base[j] ..]. A tile the program
+// cannot finish goes to index_emit_cont_kernel whole.
+template <class PP>
+__device__ __forceinline__ void index_emit_tile(const IndexArgs& a, const PP& P, uint8_t* lds,
+                                                IndexTileShared& sm) {
+  const uint64_t j = blockIdx.x;
+  if (threadIdx.x == 0) a.ep[j] = kNo;
+  if (j >= a.scal[1] || a.cnt[j] == 0) return;
+  const uint64_t lo = chunk_lo(a, j);
+  const uint32_t sh0 = (uint32_t)((uintptr_t)(a.in + lo) & 15);
+  const uint64_t sj = a.s[j];
+  const uint32_t ent = (uint32_t)(sj - lo) + sh0;
+  TileLane L;
+  uint32_t sh, first;
+  bool ok;
+  if (a.pf[j] == kLanesValid) {
+    // the speculation pass's lane results still hold: stage the tile only
+    const uint8_t* g = a.in + lo;
+    sh = sh0;
+    const uint8_t* gb = g - sh;
+    const uint64_t av = a.in_len - lo + sh;
+    const uint32_t avail = (uint32_t)(av < kPosCap ? av : kPosCap);
+    const uint32_t staged = avail < kTile + kOver + 16 ? avail : kTile + kOver + 16;
+    const uint32_t nvec = (staged + 15) >> 4;
+    for (uint32_t i = threadIdx.x; i < nvec; i += kTileLanes)
+      ((uint4*)lds)[i] = ((const uint4*)gb)[i];
+    const uint32_t v = a.lanes[j * kTileLanes + threadIdx.x];
+    L.s = v & 0xffffu;
+    L.c = v >> 16;
+    first = ent;
+    ok = true;
+    __syncthreads();
+  } else {
+    ok = tile_resolve(a, P, j, lds, ent, L, sh, first, sm.E, &sm.flag, &sm.first_lane, &sm.fs);
+  }
+  const uint64_t b = a.base[j];
+  if (!ok) {
+    if (threadIdx.x == 0) {
+      a.ep[j] = sj;
+      a.ec[j] = 0;
+    }
+    return;
+  }
+  // lane k's records go after the records of lanes < k
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const unsigned long long x = wave_incl_scan(L.c);
+  if (lane == 63) sm.part[wid] = x;
+  __syncthreads();
+  unsigned long long pre = x - L.c;
+  for (int w = 0; w < wid; ++w) pre += sm.part[w];
+  if (L.c == 0) return;
+  // re-walk this lane's records, writing absolute starts
+  const uint64_t gb = lo - sh;
+  uint32_t p = L.s;
+  const uint8_t* g = a.in + gb;
+  const uint64_t avail64 = a.in_len - gb;
+  const uint32_t avail = (uint32_t)(avail64 < kPosCap ? avail64 : kPosCap);
+  const uint32_t staged = avail < kTile + kOver + 16 ? avail : kTile + kOver + 16;
+  const TileSrc src{(const uint32_t*)lds, staged & ~3u, HbmSrc{g, avail}};
+  const Ctx pc{0, nullptr, 0, a.string_limit, a.container_limit};
+  for (uint32_t i = 0; i < L.c; ++i) {
+    const uint64_t idx = b + pre + i;
+    if (idx <= a.max_records) a.offs[idx] = gb + p;
+    uint32_t q = p;
+    run_program<false>(P, src, pc, q, avail, nullptr);
+    p = q;
+  }
+}
+
+}  // namespace prog
+}  // namespace tgpu

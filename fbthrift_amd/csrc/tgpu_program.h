@@ -1,6 +1,6 @@
-// tgpu_program.h — the compiled-record-program interpreter shared by the
-// indexed decode (k_program.hip, bytes staged in LDS) and the stream indexer
-// (k_index.hip, bytes read from HBM). Not part of the public ABI.
+// tgpu_program.h — the compiled-record-program codec shared by the indexed
+// decode, the variable-length encode and the stream indexer. Not part of the
+// public ABI.
 //
 // A VProgram (tgpu_api.cpp build_program) is the canonical wire form of one
 // record of an all-unqualified schema: the header the generated readNoXfer
@@ -9,12 +9,47 @@
 // that follows. run_program either accepts a record in exactly that form or
 // reports it irregular (never an error): irregular records go to the general
 // reader (tgpu_device.h), which has the full readNoXfer semantics.
+//
+// The program reaches the code through an accessor:
+//   DynProg  — a device-resident VProgram read through the scalar cache; one
+//              build of the kernels interprets any schema (the AOT library);
+//   a static accessor (kStatic) — the same ops as compile-time constants, in
+//              kernels the library generates and compiles for one schema at
+//              run time (tgpu_jit.cpp), the way the reference's thrift1
+//              compiler emits one readNoXfer/write per struct
+//              (deserialize_struct.whisker:19-160, serialize_struct.whisker:40-67):
+//              the op loop unrolls and every header, width and offset folds.
 #pragma once
 
-#include "tgpu_device.h"
+#include "tgpu_internal.h"
 
 namespace tgpu {
 namespace prog {
+
+// ---- program accessors --------------------------------------------------------
+struct DynProg {
+  static constexpr bool kStatic = false;
+  static constexpr uint32_t kN = 0;
+  const VProgram* __restrict__ p;
+  __device__ __forceinline__ uint32_t n_ops() const { return p->n_ops; }
+  __device__ __forceinline__ uint32_t protocol() const { return p->protocol; }
+  __device__ __forceinline__ VOp op(uint32_t k) const { return p->ops[k]; }
+};
+
+// f(op) for every op in order; stops at the first op for which f returns false.
+template <class PP, class F>
+__device__ __forceinline__ bool all_ops(const PP& P, F&& f) {
+  if constexpr (PP::kStatic) {
+#pragma unroll
+    for (uint32_t k = 0; k < PP::kN; ++k)
+      if (!f(P.op(k))) return false;
+  } else {
+    const uint32_t n = P.n_ops();
+    for (uint32_t k = 0; k < n; ++k)
+      if (!f(P.op(k))) return false;
+  }
+  return true;
+}
 
 // ---- byte sources: 8 bytes at position p, little-endian packed -------------
 struct LdsSrc {
@@ -104,6 +139,13 @@ __device__ __forceinline__ uint64_t unzigzag(uint64_t z, uint32_t bits) {
   }
   return (z >> 1) ^ (0ull - (z & 1));
 }
+// VarintUtils-inl.h:630-636
+__device__ __forceinline__ uint32_t i32_to_zz(int32_t n) {
+  return ((uint32_t)n << 1) ^ (uint32_t)(n >> 31);
+}
+__device__ __forceinline__ uint64_t i64_to_zz(int64_t n) {
+  return ((uint64_t)n << 1) ^ (uint64_t)(n >> 63);
+}
 
 struct Ctx {
   uint64_t gbase;  // stream offset of source position 0
@@ -112,140 +154,143 @@ struct Ctx {
   int32_t string_limit, container_limit;
 };
 
-// Runs the program from p over at most [p, end). On success p is the end of
-// the record. kStore: write members / isset / spans into rec and list
-// elements into the arena; otherwise only measure and validate.
-// PP: the program in LDS (VProgram*) or in HBM read through the scalar cache
-// (const VProgram* __restrict__ kernel argument).
-template <bool kStore, class PP, class Src>
-__device__ __forceinline__ bool run_program(PP P, const Src& src, const Ctx& c, uint32_t& pos,
-                                            uint32_t end, uint8_t* rec) {
-  const bool compact = P->protocol == TGPU_PROTOCOL_COMPACT;
-  const uint32_t n_ops = P->n_ops;
-  uint32_t p = pos;
-  for (uint32_t k = 0; k < n_ops; ++k) {
-    const VOp op = P->ops[k];
-    switch (op.kind) {
-      case VOP_CONST: {
-        if (p + op.hdr_len > end) return false;
-        const uint32_t lo = (uint32_t)src.win8(p);
-        const uint32_t mask = op.hdr_len >= 4 ? 0xffffffffu : ((1u << (8 * op.hdr_len)) - 1);
-        if ((lo ^ op.hdr) & mask) return false;
-        p += op.hdr_len;
-        break;
-      }
-      case VOP_CBOOL: {
-        if (p + op.hdr_len > end) return false;
-        const uint32_t lo = (uint32_t)src.win8(p);
-        const uint32_t mask = (op.hdr_len >= 4 ? 0xffffffffu : ((1u << (8 * op.hdr_len)) - 1)) & ~0xfu;
-        const uint32_t ct = lo & 0xf;
-        if (((lo ^ op.hdr) & mask) || (ct != 1 && ct != 2)) return false;
-        if (kStore) rec[op.member] = ct == 1 ? 1 : 0;
-        p += op.hdr_len;
-        break;
-      }
-      case VOP_FIXED: {
-        if (p + op.width > end) return false;
-        const uint64_t v = bswap_n(src.win8(p), op.width);
-        if (op.is_bool && v > 1) return false;  // readBool throws: general path
-        if (kStore) store_n(rec + op.member, v, op.width);
-        p += op.width;
-        break;
-      }
-      case VOP_VARINT: {
+// One op of the program at p (bounded by end); false = irregular.
+template <bool kStore, class Src>
+__device__ __forceinline__ bool run_op(const VOp op, const bool compact, const Src& src,
+                                       const Ctx& c, uint32_t& p, uint32_t end, uint8_t* rec) {
+  switch (op.kind) {
+    case VOP_CONST: {
+      if (p + op.hdr_len > end) return false;
+      const uint32_t lo = (uint32_t)src.win8(p);
+      const uint32_t mask = op.hdr_len >= 4 ? 0xffffffffu : ((1u << (8 * op.hdr_len)) - 1);
+      if ((lo ^ op.hdr) & mask) return false;
+      p += op.hdr_len;
+      break;
+    }
+    case VOP_CBOOL: {
+      if (p + op.hdr_len > end) return false;
+      const uint32_t lo = (uint32_t)src.win8(p);
+      const uint32_t mask = (op.hdr_len >= 4 ? 0xffffffffu : ((1u << (8 * op.hdr_len)) - 1)) & ~0xfu;
+      const uint32_t ct = lo & 0xf;
+      if (((lo ^ op.hdr) & mask) || (ct != 1 && ct != 2)) return false;
+      if (kStore) rec[op.member] = ct == 1 ? 1 : 0;
+      p += op.hdr_len;
+      break;
+    }
+    case VOP_FIXED: {
+      if (p + op.width > end) return false;
+      const uint64_t v = bswap_n(src.win8(p), op.width);
+      if (op.is_bool && v > 1) return false;  // readBool throws: general path
+      if (kStore) store_n(rec + op.member, v, op.width);
+      p += op.width;
+      break;
+    }
+    case VOP_VARINT: {
+      uint64_t z;
+      if (!read_varint(src, p, end, op.bits, z)) return false;
+      if (kStore) store_n(rec + op.member, unzigzag(z, op.bits), op.width);
+      break;
+    }
+    case VOP_STRING: {
+      int64_t len;
+      if (compact) {
         uint64_t z;
-        if (!read_varint(src, p, end, op.bits, z)) return false;
-        if (kStore) store_n(rec + op.member, unzigzag(z, op.bits), op.width);
-        break;
+        if (!read_varint(src, p, end, 32, z)) return false;
+        len = (int32_t)(uint32_t)z;
+      } else {
+        if (p + 4 > end) return false;
+        len = (int32_t)(uint32_t)bswap_n(src.win8(p), 4);
+        p += 4;
       }
-      case VOP_STRING: {
-        int64_t len;
-        if (compact) {
+      if (len < 0 || (c.string_limit > 0 && len > c.string_limit) || len > (int64_t)(end - p))
+        return false;
+      if (kStore) {
+        tgpu_span* sp = (tgpu_span*)(rec + op.member);
+        sp->offset = len ? c.gbase + p : 0;
+        sp->length = (uint32_t)len;
+        sp->reserved = 0;
+      }
+      p += (uint32_t)len;
+      break;
+    }
+    case VOP_LIST: {
+      int64_t n;
+      if (compact) {
+        if (p + 1 > end) return false;
+        const uint32_t b = (uint32_t)(src.win8(p) & 0xff);
+        const uint32_t ct = b & 0xf;
+        const bool ok_ct = op.elem_ttype == TGPU_T_BOOL ? (ct == 1 || ct == 2) : ct == op.elem_ct;
+        if (!ok_ct) return false;
+        ++p;
+        n = b >> 4;
+        if (n == 15) {
           uint64_t z;
           if (!read_varint(src, p, end, 32, z)) return false;
-          len = (int32_t)(uint32_t)z;
-        } else {
-          if (p + 4 > end) return false;
-          len = (int32_t)(uint32_t)bswap_n(src.win8(p), 4);
-          p += 4;
+          n = (int32_t)(uint32_t)z;
         }
-        if (len < 0 || (c.string_limit > 0 && len > c.string_limit) || len > (int64_t)(end - p))
-          return false;
-        if (kStore) {
-          tgpu_span* sp = (tgpu_span*)(rec + op.member);
-          sp->offset = len ? c.gbase + p : 0;
-          sp->length = (uint32_t)len;
-          sp->reserved = 0;
-        }
-        p += (uint32_t)len;
-        break;
+      } else {
+        if (p + 5 > end) return false;
+        const uint64_t w = src.win8(p);
+        if ((w & 0xff) != op.elem_ttype) return false;
+        n = (int32_t)(uint32_t)bswap_n(w >> 8, 4);
+        p += 5;
       }
-      case VOP_LIST: {
-        int64_t n;
-        if (compact) {
-          if (p + 1 > end) return false;
-          const uint32_t b = (uint32_t)(src.win8(p) & 0xff);
-          const uint32_t ct = b & 0xf;
-          const bool ok_ct = op.elem_ttype == TGPU_T_BOOL ? (ct == 1 || ct == 2) : ct == op.elem_ct;
-          if (!ok_ct) return false;
-          ++p;
-          n = b >> 4;
-          if (n == 15) {
-            uint64_t z;
-            if (!read_varint(src, p, end, 32, z)) return false;
-            n = (int32_t)(uint32_t)z;
-          }
-        } else {
-          if (p + 5 > end) return false;
-          const uint64_t w = src.win8(p);
-          if ((w & 0xff) != op.elem_ttype) return false;
-          n = (int32_t)(uint32_t)bswap_n(w >> 8, 4);
-          p += 5;
-        }
-        if (n < 0 || (c.container_limit && n > c.container_limit) || n > (int64_t)(end - p))
-          return false;
-        const uint64_t scale = compact ? 8 : 1;
-        const uint64_t aoff = scale * (c.gbase + p);
-        const uint32_t es = op.width;
-        if (kStore && n && (!c.arena || aoff + (uint64_t)n * es > c.arena_cap)) return false;
-        if (!kStore && op.elem_kind == VEL_FIXED) {
-          if ((uint64_t)n * es > end - p) return false;
-          p += (uint32_t)n * es;
-        } else {
-          for (int64_t i = 0; i < n; ++i) {
-            uint64_t v;
-            if (op.elem_kind == VEL_VARINT) {
-              uint64_t z;
-              if (!read_varint(src, p, end, op.bits, z)) return false;
-              v = unzigzag(z, op.bits);
-            } else {
-              const uint32_t wb = op.elem_kind == VEL_BOOL ? 1 : es;
-              if (p + wb > end) return false;
-              v = bswap_n(src.win8(p), wb);
-              if (op.elem_kind == VEL_BOOL) {
-                if (compact) v = v == 1;
-                else if (v > 1) return false;
-              }
-              p += wb;
-            }
-            if (kStore) store_n(c.arena + aoff + (uint64_t)i * es, v, es);
-          }
-        }
-        if (kStore) {
-          tgpu_span* sp = (tgpu_span*)(rec + op.member);
-          sp->offset = n ? aoff : 0;
-          sp->length = (uint32_t)n;
-          sp->reserved = 0;
-        }
-        break;
-      }
-      case VOP_ISSET:
-        break;
-      default:
+      if (n < 0 || (c.container_limit && n > c.container_limit) || n > (int64_t)(end - p))
         return false;
+      const uint64_t scale = compact ? 8 : 1;
+      const uint64_t aoff = scale * (c.gbase + p);
+      const uint32_t es = op.width;
+      if (kStore && n && (!c.arena || aoff + (uint64_t)n * es > c.arena_cap)) return false;
+      if (!kStore && op.elem_kind == VEL_FIXED) {
+        if ((uint64_t)n * es > end - p) return false;
+        p += (uint32_t)n * es;
+      } else {
+        for (int64_t i = 0; i < n; ++i) {
+          uint64_t v;
+          if (op.elem_kind == VEL_VARINT) {
+            uint64_t z;
+            if (!read_varint(src, p, end, op.bits, z)) return false;
+            v = unzigzag(z, op.bits);
+          } else {
+            const uint32_t wb = op.elem_kind == VEL_BOOL ? 1 : es;
+            if (p + wb > end) return false;
+            v = bswap_n(src.win8(p), wb);
+            if (op.elem_kind == VEL_BOOL) {
+              if (compact) v = v == 1;
+              else if (v > 1) return false;
+            }
+            p += wb;
+          }
+          if (kStore) store_n(c.arena + aoff + (uint64_t)i * es, v, es);
+        }
+      }
+      if (kStore) {
+        tgpu_span* sp = (tgpu_span*)(rec + op.member);
+        sp->offset = n ? aoff : 0;
+        sp->length = (uint32_t)n;
+        sp->reserved = 0;
+      }
+      break;
     }
-    if (kStore && op.isset != 0xffff) rec[op.isset] = 1;
+    case VOP_ISSET:
+      break;
+    default:
+      return false;
   }
+  if (kStore && op.isset != 0xffff) rec[op.isset] = 1;
+  return true;
+}
+
+// Runs the program from pos over at most [pos, end). On success pos is the
+// end of the record. kStore: write members / isset / spans into rec and list
+// elements into the arena; otherwise only measure and validate.
+template <bool kStore, class PP, class Src>
+__device__ __forceinline__ bool run_program(const PP& P, const Src& src, const Ctx& c,
+                                            uint32_t& pos, uint32_t end, uint8_t* rec) {
+  const bool compact = P.protocol() == TGPU_PROTOCOL_COMPACT;
+  uint32_t p = pos;
+  if (!all_ops(P, [&](const VOp op) { return run_op<kStore>(op, compact, src, c, p, end, rec); }))
+    return false;
   pos = p;
   return true;
 }

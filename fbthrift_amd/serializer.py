@@ -96,11 +96,28 @@ class GpuSchema:
     def fixed_wire_size(self, protocol):
         return _lib.lib().tgpu_schema_fixed_wire_size(self.handle, protocol)
 
+    def compile(self, protocol):
+        """Compiles the schema's kernels for `protocol` now (tgpu_schema_compile);
+        True when compiled kernels will be used, False when the schema has no
+        canonical program or the compiler is unavailable (interpreted)."""
+        return _lib.lib().tgpu_schema_compile(self.handle, protocol) == 0
+
     def __del__(self):
         h = getattr(self, "handle", None)
         if h is not None and _lib._lib is not None:
             _lib.lib().tgpu_schema_destroy(h)
             self.handle = None
+
+
+def compile_check(schema, protocol, arch="gfx950"):
+    """Generates and compiles `schema`'s kernels for `arch` without a GPU
+    (tgpu_schema_compile_check). Returns (code, compiler log)."""
+    structs, ns, fields, nf = schema.descriptors()
+    log = ctypes.create_string_buffer(1 << 16)
+    rc = _lib.lib().tgpu_schema_compile_check(ctypes.addressof(structs), ns,
+                                              ctypes.addressof(fields), nf, protocol,
+                                              arch.encode(), log, len(log))
+    return rc, log.value.decode(errors="replace")
 
 
 class Context:

@@ -52,8 +52,10 @@
 #ifndef THRIFT_GPU_H_
 #define THRIFT_GPU_H_
 
+#ifndef __HIPCC_RTC__ /* runtime-compiled device code declares its own types */
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -218,6 +220,27 @@ uint32_t tgpu_schema_record_size(const tgpu_schema* schema);
 /* Canonical wire length of every record if it is fixed for `protocol`
  * (Binary with only fixed-width fields), else 0. */
 uint64_t tgpu_schema_fixed_wire_size(const tgpu_schema* schema, int protocol);
+
+/*
+ * Compiles the schema's record codec for `protocol` into specialized gfx950
+ * kernels now (hipRTC) — the run-time counterpart of the reference's per-type
+ * code generation (thrift1 emitting T::readNoXfer / T::write,
+ * deserialize_struct.whisker:19-160, serialize_struct.whisker:40-67). Without
+ * this call the library compiles on the first batch of >= 64 Ki records and
+ * interprets the schema below that (env TGPU_JIT=1: compile on first use,
+ * TGPU_JIT=0: never). Results are identical either way.
+ * Returns TGPU_OK, or TGPU_ERR_UNSUPPORTED when the schema has no canonical
+ * record program for the protocol (optional fields, maps, ...) or the
+ * compiler is unavailable (the interpreting kernels are used).
+ */
+int tgpu_schema_compile(const tgpu_schema* schema, int protocol);
+/* Diagnostics: generates and compiles the kernels of the schema given by the
+ * tables (as for tgpu_schema_create) for `arch` (e.g. "gfx950"; NULL =
+ * gfx950) without loading them — needs no GPU. The compiler log goes to
+ * log[0..log_capacity) (may be NULL). */
+int tgpu_schema_compile_check(const tgpu_struct_desc* structs, uint32_t n_structs,
+                              const tgpu_field_desc* fields, uint32_t n_fields, int protocol,
+                              const char* arch, char* log, uint64_t log_capacity);
 
 /* ---- context ---------------------------------------------------------- */
 int tgpu_context_create(tgpu_context** out);

@@ -20,3 +20,12 @@ def gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+@pytest.fixture(params=["interp", "jit"])
+def codec(request, monkeypatch):
+    """Runs a GPU test through both program paths of libtgpu: the library's
+    interpreting kernels (TGPU_JIT=0) and the per-schema kernels the schema
+    compiler generates (TGPU_JIT=1, tgpu_jit.cpp)."""
+    monkeypatch.setenv("TGPU_JIT", "1" if request.param == "jit" else "0")
+    return request.param

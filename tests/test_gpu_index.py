@@ -66,7 +66,7 @@ def _stream(sname, proto, n, seed=0, max_len=None):
 
 
 @pytest.mark.parametrize("name", helpers.case_names())
-def test_index_golden(gpu, name):
+def test_index_golden(gpu, codec, name):
     c = helpers.Case(name)
     offs, n, first, last, st = _ser(c.protocol).index_stream(_gs(c.schema), _t(c.wire, gpu))
     assert st.code == 0 and n == c.n and first == 0 and last == len(c.wire)
@@ -75,7 +75,7 @@ def test_index_golden(gpu, name):
 
 @pytest.mark.parametrize("sname,proto", [("mixed", 2), ("mixed", 0), ("nested", 0),
                                          ("nested", 2), ("scalars", 2), ("sparse", 2)])
-def test_index_and_unindexed_decode_large(gpu, sname, proto):
+def test_index_and_unindexed_decode_large(gpu, codec, sname, proto):
     """100k-record streams: index == oracle offsets; unindexed decode ==
     oracle decode (records, consumed)."""
     n = 100_000 if sname in ("mixed", "nested") else 30_000
@@ -94,7 +94,7 @@ def test_index_and_unindexed_decode_large(gpu, sname, proto):
 
 @pytest.mark.parametrize("proto", [2, 0])
 @pytest.mark.parametrize("max_len", [30, 3000])
-def test_index_speculative_shards(gpu, proto, max_len):
+def test_index_speculative_shards(gpu, codec, proto, max_len):
     """The stream split into byte ranges at arbitrary positions: each range
     indexed speculatively finds the first record start at/after its begin,
     exactly the oracle's, and its last_end is the next range's first start."""
@@ -122,7 +122,7 @@ def test_index_speculative_shards(gpu, proto, max_len):
         prev_last = last
 
 
-def test_index_error_mid_stream(gpu):
+def test_index_error_mid_stream(gpu, codec):
     """A malformed record deep in a long unindexed stream: index and decode
     both report the reference status at that record; records before it are
     decoded exactly."""

@@ -54,7 +54,7 @@ def gpu_decode(schema, protocol, stream, n, offsets=None, limits=None, dev=None)
 
 @pytest.mark.parametrize("name", helpers.case_names())
 @pytest.mark.parametrize("indexed", [False, True])
-def test_decode_golden(gpu, name, indexed):
+def test_decode_golden(gpu, codec, name, indexed):
     c = helpers.Case(name)
     offs = c.offsets if indexed else None
     st, rec, arena, nd, cons = gpu_decode(c.schema, c.protocol, c.wire, c.n, offs, dev=gpu)
@@ -68,7 +68,7 @@ def test_decode_golden(gpu, name, indexed):
 
 
 @pytest.mark.parametrize("name", helpers.case_names())
-def test_encode_golden(gpu, name):
+def test_encode_golden(gpu, codec, name):
     c = helpers.Case(name)
     rec, sarena, larena = helpers.pack(c.schema, c.values, c.n)
     gs = _gschema(c.schema)
@@ -83,7 +83,7 @@ def test_encode_golden(gpu, name):
 
 
 @pytest.mark.parametrize("case", corpus.cases(), ids=lambda c: c[0])
-def test_corpus_status_parity(gpu, case):
+def test_corpus_status_parity(gpu, codec, case):
     name, proto, table, stream, n, limits, expected = case
     schema = Schema.from_table(table)
     st, rec, arena, nd, cons = gpu_decode(schema, proto, stream, n, None, limits, dev=gpu)
@@ -92,6 +92,13 @@ def test_corpus_status_parity(gpu, case):
     assert (nd, cons) == (ond, ocons)
     k = (nd + (1 if st.code else 0)) * schema.record_size  # failing record is partial in both
     assert np.array_equal(rec[:k], orec[:k])
+
+
+@pytest.mark.parametrize("name,protocol", [("mixed", 2), ("nested", 0), ("scalars", 2)])
+def test_schema_compiles_on_device(gpu, name, protocol):
+    """The schema compiler loads its kernels on the GPU (so the TGPU_JIT=1
+    runs above exercise them, not the interpreter)."""
+    assert _gschema(Schema.from_table(datagen.SCHEMAS[name])).compile(protocol)
 
 
 def _flat8(n, first=0):

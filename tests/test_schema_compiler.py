@@ -1,0 +1,26 @@
+"""The schema compiler (tgpu_jit.cpp) on a GPU-less host: the kernels it
+generates for a schema compile for gfx950 with hipRTC (all three kernel
+groups: decode, encode, index); schemas without a canonical record program
+(optional fields) are refused — they run on the general reader. GPU parity of
+the compiled kernels is in test_gpu_parity.py (TGPU_JIT=1 runs). Compiles
+cost seconds each, so the CPU suite covers the three BASELINE config schemas
+in their benchmarked protocol plus the bool/long-form-id heavy 'scalars'."""
+import pytest
+
+import helpers
+from fbthrift_amd.schema import Schema
+from fbthrift_amd.serializer import compile_check
+
+M = helpers.manifest()["schemas"]
+
+
+@pytest.mark.parametrize("name,protocol", [("flat8", 0), ("mixed", 2), ("nested", 0),
+                                           ("scalars", 2)])
+def test_schema_kernels_compile(name, protocol):
+    rc, log = compile_check(Schema.from_table(M[name]), protocol)
+    assert rc == 0, log
+
+
+def test_optional_fields_have_no_program():
+    rc, _ = compile_check(Schema.from_table(M["sparse"]), 2)
+    assert rc == 22  # TGPU_ERR_UNSUPPORTED: no canonical program, general reader path
