@@ -8,16 +8,15 @@
 // (BinaryProtocol-inl.h:41-67 / CompactProtocol-inl.h:133-180) then its value
 // (BinaryProtocol-inl.h:120-222 / CompactProtocol-inl.h:252-373).
 //
-// Three launches, one record per lane, 256-record tiles:
-//   1. program_size_kernel  — record tile HBM -> LDS (16-byte loads); each
-//      lane sizes its record; sizes -> out_offsets[i]; tile sum -> sums[t];
+// One record per lane, 256-record tiles (bodies in tgpu_prog_kernels.h):
+//   1. program_size_kernel — record tile HBM -> LDS; each lane sizes its
+//      record; sizes -> out_offsets[i]; tile sum -> block_sums[t];
 //      validation failures (validate_bool, > INT32_MAX sizes) -> first_fail.
-//   2. scan of the tile sums (scan_tiles_*: reduce, top-level scan, apply).
-//   3. program_write_kernel — record tile -> LDS again, block exclusive scan
-//      of the sizes gives each lane its position in the tile; the lane emits
-//      its record into an LDS output tile (records past the LDS cap go to HBM
-//      directly); the tile leaves with coalesced 16-byte stores (byte stores
-//      only on the two edge chunks shared with the neighbouring tiles).
+//   2. scan_tiles_* — exclusive scan of the tile sums (tile stream offsets).
+//   3. program_write_kernel — record tile -> LDS again, block scan of the
+//      sizes, records emitted into a zero-filled LDS output tile a dword at a
+//      time, coalesced 16-byte stores; out_offsets receives every start.
+// tgpu_encoded_size stops after 2.
 #include "tgpu_prog_kernels.h"
 
 namespace tgpu {
@@ -37,9 +36,8 @@ __global__ __launch_bounds__(kET) void program_size_kernel(EncodeArgs a,
 __global__ __launch_bounds__(kET) void program_write_kernel(EncodeArgs a,
                                                             const VProgram* __restrict__ P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  __shared__ unsigned long long part[4];
-  __shared__ unsigned int lds_end;
-  prog::write_tile(a, prog::DynProg{P}, a.rec_size, smem, part, &lds_end);
+  __shared__ prog::EncodeShared sm;
+  prog::write_tile(a, prog::DynProg{P}, a.rec_size, smem, sm);
 }
 
 // ---- scan of per-tile sums (exclusive, in place; total -> res, offs[n]) ----
@@ -143,9 +141,10 @@ hipError_t launch_program_encode(const EncodeArgs& a, const VProgram* d_prog,
   if (e == hipSuccess)
     e = launch_scan_tiles(a.block_sums, tiles, part, &a.res->total_bytes, a.offs + a.n, stream);
   if (e != hipSuccess || size_only) return e;
-  if (jit) return jit_launch_encode(jit, true, a, tiles, rt + kOutCap + 32, stream);
-  hipLaunchKernelGGL(program_write_kernel, dim3((uint32_t)tiles), dim3(kET), rt + kOutCap + 32,
-                     stream, a, d_prog);
+  const uint32_t lds = rt + kOutCap + 32;
+  if (jit) return jit_launch_encode(jit, true, a, tiles, lds, stream);
+  hipLaunchKernelGGL(program_write_kernel, dim3((uint32_t)tiles), dim3(kET), lds, stream, a,
+                     d_prog);
   return hipGetLastError();
 }
 

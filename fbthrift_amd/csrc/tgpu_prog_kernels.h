@@ -145,6 +145,29 @@ __device__ __forceinline__ uint64_t zz_member(uint64_t raw, uint32_t width, uint
   return i64_to_zz(v);
 }
 
+// list elements of `width` bytes from HBM, kElemBatch loads in flight
+#ifndef TGPU_ELEM_BATCH
+#define TGPU_ELEM_BATCH 8
+#endif
+template <class F>
+__device__ __forceinline__ void for_elems(const uint8_t* __restrict__ e, uint32_t len,
+                                          uint32_t width, F&& f) {
+  constexpr uint32_t B = TGPU_ELEM_BATCH;
+  if constexpr (B == 1) {
+    for (uint32_t i = 0; i < len; ++i) f(load_member(e + (uint64_t)i * width, width));
+  } else {
+    for (uint32_t i0 = 0; i0 < len; i0 += B) {
+      uint64_t v[B];
+#pragma unroll
+      for (uint32_t k = 0; k < B; ++k)
+        v[k] = i0 + k < len ? load_member(e + (uint64_t)(i0 + k) * width, width) : 0;
+#pragma unroll
+      for (uint32_t k = 0; k < B; ++k)
+        if (i0 + k < len) f(v[k]);
+    }
+  }
+}
+
 // Bytes T::write emits for the record at `rec`; ok = false where the writer
 // would throw or abort (the finish kernel re-derives the exact code).
 template <class PP>
@@ -184,12 +207,13 @@ __device__ __forceinline__ uint64_t program_size(const PP& P, const uint8_t* rec
         n += compact ? (len <= 14 ? 1 : 1 + varint_len(len)) : 5;
         const uint8_t* e = lbase + sp.offset;
         if (op.elem_kind == VEL_VARINT) {
-          for (uint32_t i = 0; i < len; ++i)
-            n += varint_len(zz_member(load_member(e + (uint64_t)i * op.width, op.width), op.width,
-                                      op.bits));
+          for_elems(e, len, op.width, [&](uint64_t x) {
+            n += varint_len(zz_member(x, op.width, op.bits));
+          });
         } else if (op.elem_kind == VEL_BOOL) {
-          for (uint32_t i = 0; i < len; ++i)
-            if (e[i] > 1) ok = false;
+          for_elems(e, len, 1, [&](uint64_t x) {
+            if (x > 1) ok = false;
+          });
           n += len;
         } else {
           n += (uint64_t)len * op.width;
@@ -204,73 +228,133 @@ __device__ __forceinline__ uint64_t program_size(const PP& P, const uint8_t* rec
   return n;
 }
 
-// Sinks: the LDS output tile (position q relative to the tile's LDS base) or
-// HBM directly (q relative to the record's HBM start).
+// ---- record emission ----------------------------------------------------------
+// A sink appends little-endian packed bytes, at most 4 per put:
+//   WordSink — the zero-filled LDS output tile: bytes gather in a 64-bit
+//              accumulator and leave a dword at a time (ds_write_b32 for
+//              dwords the record owns, ds_or_b32 for the first and last ones,
+//              which it may share with its neighbours);
+//   ByteSink — HBM directly, a byte at a time (records past the LDS tile).
+struct WordSink {
+  uint32_t* w32;
+  uint64_t acc;
+  uint32_t wpos, nb;  // acc holds the bytes of dword wpos on (nb valid, incl. the lead-in)
+  bool first;
+  __device__ __forceinline__ WordSink(uint32_t* tile, uint32_t q)
+      : w32(tile), acc(0), wpos(q >> 2), nb(q & 3), first(true) {}
+  __device__ __forceinline__ void put(uint32_t v, uint32_t n) {
+    if (n < 4) v &= (1u << (8 * n)) - 1;  // callers may pass bytes past n
+    acc |= (uint64_t)v << (8 * nb);
+    nb += n;
+    if (nb >= 4) {
+      if (first) atomicOr(&w32[wpos], (uint32_t)acc);
+      else w32[wpos] = (uint32_t)acc;
+      first = false;
+      acc >>= 32;
+      ++wpos;
+      nb -= 4;
+    }
+  }
+  __device__ __forceinline__ void finish() {
+    if (nb) atomicOr(&w32[wpos], (uint32_t)acc);
+  }
+};
 struct ByteSink {
   uint8_t* base;
-  __device__ __forceinline__ void put(uint32_t q, uint32_t b) const { base[q] = (uint8_t)b; }
+  uint32_t q;
+  __device__ __forceinline__ ByteSink(uint8_t* b) : base(b), q(0) {}
+  __device__ __forceinline__ void put(uint32_t v, uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i) base[q + i] = (uint8_t)(v >> (8 * i));
+    q += n;
+  }
+  __device__ __forceinline__ void finish() {}
 };
 
+// n <= 8 little-endian packed bytes
 template <class Sink>
-__device__ __forceinline__ uint32_t put_be(const Sink& s, uint32_t q, uint64_t v, uint32_t n) {
-  for (uint32_t i = 0; i < n; ++i) s.put(q + i, (uint32_t)(v >> (8 * (n - 1 - i))));
-  return q + n;
-}
-template <class Sink>
-__device__ __forceinline__ uint32_t put_varint(const Sink& s, uint32_t q, uint64_t v) {
-  while (v & ~0x7full) {
-    s.put(q++, (uint32_t)((v & 0x7f) | 0x80));
-    v >>= 7;
+__device__ __forceinline__ void put8(Sink& s, uint64_t v, uint32_t n) {
+  if (n <= 4) {
+    s.put((uint32_t)v, n);
+  } else {
+    s.put((uint32_t)v, 4);
+    s.put((uint32_t)(v >> 32), n - 4);
   }
-  s.put(q++, (uint32_t)v);
-  return q;
 }
-// len bytes from HBM (any alignment): aligned dword loads, bytes out
+// big-endian n-byte value (BinaryProtocol-inl.h:120-161 writeBE)
 template <class Sink>
-__device__ __forceinline__ uint32_t put_bytes(const Sink& s, uint32_t q,
-                                              const uint8_t* __restrict__ src, uint32_t len) {
-  if (!len) return q;
+__device__ __forceinline__ void put_be(Sink& s, uint64_t v, uint32_t n) {
+  put8(s, __builtin_bswap64(v) >> (64 - 8 * n), n);
+}
+// LEB128 (VarintUtils-inl.h:545-620): the first 8 bytes of the encoding are
+// the 7-bit groups spread into bytes plus continuation bits, no loop
+template <class Sink>
+__device__ __forceinline__ void put_varint(Sink& s, uint64_t v) {
+  const uint32_t len = varint_len(v);
+  uint64_t x = v & 0x00ffffffffffffffull;
+  x = (x & 0x000000000fffffffull) | ((x & 0x00fffffff0000000ull) << 4);
+  x = (x & 0x00003fff00003fffull) | ((x & 0x0fffc0000fffc000ull) << 2);
+  x = (x & 0x007f007f007f007full) | ((x & 0x3f803f803f803f80ull) << 1);
+  if (len <= 8) {
+    x |= 0x8080808080808080ull & ((1ull << (8 * (len - 1))) - 1);
+    put8(s, x, len);
+  } else {
+    put8(s, x | 0x8080808080808080ull, 8);
+    const uint32_t b8 = (uint32_t)((v >> 56) & 0x7f), b9 = (uint32_t)(v >> 63);
+    s.put(len == 10 ? (b8 | 0x80u | (b9 << 8)) : b8, len - 8);
+  }
+}
+// len bytes from HBM (any alignment): aligned dword loads, issued 8 at a
+// time before any is used (one memory round trip per 32 bytes, not per dword)
+template <class Sink>
+__device__ __forceinline__ void put_bytes(Sink& s, const uint8_t* __restrict__ src, uint32_t len) {
+  if (!len) return;
   const uintptr_t a = (uintptr_t)src;
   const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
   uint32_t sh = (uint32_t)(a & 3);
-  uint32_t i = 0;
-  while (i < len) {
-    const uint32_t word = *w++;
-    for (uint32_t b = sh; b < 4 && i < len; ++b, ++i) s.put(q + i, (word >> (8 * b)) & 0xff);
-    sh = 0;
+  uint32_t left = len;
+  while (left) {
+    const uint32_t need = (sh + left + 3) >> 2;  // dwords still to read
+    uint32_t v[8];
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) v[i] = i < need ? w[i] : 0u;
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i) {
+      if (i < need && left) {
+        const uint32_t take = 4 - sh < left ? 4 - sh : left;
+        s.put(v[i] >> (8 * sh), take);
+        left -= take;
+        sh = 0;
+      }
+    }
+    w += 8;
   }
-  return q + len;
 }
 
 template <class PP, class Sink>
 __device__ __forceinline__ void program_emit(const PP& P, const uint8_t* rec,
                                              const uint8_t* __restrict__ sbase,
-                                             const uint8_t* __restrict__ lbase, const Sink& s) {
+                                             const uint8_t* __restrict__ lbase, Sink& s) {
   const bool compact = P.protocol() == TGPU_PROTOCOL_COMPACT;
-  uint32_t q = 0;
   all_ops(P, [&](const VOp op) {
     switch (op.kind) {
       case VOP_CONST:
-        for (uint32_t i = 0; i < op.hdr_len; ++i) s.put(q + i, (op.hdr >> (8 * i)) & 0xff);
-        q += op.hdr_len;
+        put8(s, op.hdr, op.hdr_len);
         break;
-      case VOP_CBOOL: {
+      case VOP_CBOOL:
         // the bool's value rides in the header's type nibble (CT_BOOLEAN_TRUE/FALSE)
-        const uint32_t h = op.hdr | (rec[op.member] ? 1u : 2u);
-        for (uint32_t i = 0; i < op.hdr_len; ++i) s.put(q + i, (h >> (8 * i)) & 0xff);
-        q += op.hdr_len;
+        put8(s, op.hdr | (rec[op.member] ? 1u : 2u), op.hdr_len);
         break;
-      }
       case VOP_FIXED:
-        q = put_be(s, q, load_member(rec + op.member, op.width), op.width);
+        put_be(s, load_member(rec + op.member, op.width), op.width);
         break;
       case VOP_VARINT:
-        q = put_varint(s, q, zz_member(load_member(rec + op.member, op.width), op.width, op.bits));
+        put_varint(s, zz_member(load_member(rec + op.member, op.width), op.width, op.bits));
         break;
       case VOP_STRING: {
         const tgpu_span sp = *(const tgpu_span*)(rec + op.member);
-        q = compact ? put_varint(s, q, sp.length) : put_be(s, q, sp.length, 4);
-        q = put_bytes(s, q, sbase + sp.offset, sp.length);
+        if (compact) put_varint(s, sp.length);
+        else put_be(s, sp.length, 4);
+        put_bytes(s, sbase + sp.offset, sp.length);
         break;
       }
       case VOP_LIST: {
@@ -278,25 +362,24 @@ __device__ __forceinline__ void program_emit(const PP& P, const uint8_t* rec,
         const uint32_t len = sp.length;
         if (compact) {
           if (len <= 14) {
-            s.put(q++, (len << 4) | op.elem_ct);
+            s.put((len << 4) | op.elem_ct, 1);
           } else {
-            s.put(q++, 0xf0 | op.elem_ct);
-            q = put_varint(s, q, len);
+            s.put(0xf0 | op.elem_ct, 1);
+            put_varint(s, len);
           }
         } else {
-          s.put(q++, op.elem_ttype);
-          q = put_be(s, q, len, 4);
+          s.put(op.elem_ttype, 1);
+          put_be(s, len, 4);
         }
         const uint8_t* e = lbase + sp.offset;
         if (op.elem_kind == VEL_VARINT) {
-          for (uint32_t i = 0; i < len; ++i)
-            q = put_varint(s, q, zz_member(load_member(e + (uint64_t)i * op.width, op.width),
-                                           op.width, op.bits));
+          for_elems(e, len, op.width, [&](uint64_t x) {
+            put_varint(s, zz_member(x, op.width, op.bits));
+          });
         } else if (op.elem_kind == VEL_BOOL) {
-          for (uint32_t i = 0; i < len; ++i) s.put(q++, compact ? (e[i] ? 1u : 2u) : e[i]);
+          for_elems(e, len, 1, [&](uint64_t x) { s.put(compact ? (x ? 1u : 2u) : (uint32_t)x, 1); });
         } else {
-          for (uint32_t i = 0; i < len; ++i)
-            q = put_be(s, q, load_member(e + (uint64_t)i * op.width, op.width), op.width);
+          for_elems(e, len, op.width, [&](uint64_t x) { put_be(s, x, op.width); });
         }
         break;
       }
@@ -305,6 +388,23 @@ __device__ __forceinline__ void program_emit(const PP& P, const uint8_t* rec,
     }
     return true;
   });
+  s.finish();
+}
+
+// A record past the tile's LDS output cap goes straight to HBM, a byte at a
+// time (rare; out of line so the common path stays small).
+#ifdef TGPU_INLINE_HBM_EMIT
+#define TGPU_HBM_EMIT_ATTR __forceinline__
+#else
+#define TGPU_HBM_EMIT_ATTR __attribute__((noinline))
+#endif
+template <class PP>
+__device__ TGPU_HBM_EMIT_ATTR void emit_to_hbm(const PP P, const uint8_t* rec,
+                                                      const uint8_t* __restrict__ sbase,
+                                                      const uint8_t* __restrict__ lbase,
+                                                      uint8_t* dst) {
+  ByteSink b(dst);
+  program_emit(P, rec, sbase, lbase, b);
 }
 
 // Records [r0, r0+nrec) of stride S into LDS; returns the 16-byte phase.
@@ -339,15 +439,24 @@ __device__ __forceinline__ void size_tile(const EncodeArgs& a, const PP& P, uint
   if (threadIdx.x == 0) a.block_sums[blockIdx.x] = total;
 }
 
-// Pass 3: record tile -> LDS again, block exclusive scan of the sizes gives
-// each lane its position in the tile; the lane emits its record into an LDS
-// output tile (records past the LDS cap go to HBM directly); the tile leaves
-// with coalesced 16-byte stores (byte stores only on the two edge chunks
-// shared with the neighbouring tiles).
+// Pass 3 of the encode: the record tile goes HBM -> LDS again, the sizes of
+// pass 1 (a.offs) are scanned inside the block and offset by the tile's
+// stream offset (a.block_sums after the tile scan); every lane emits its
+// record into the zero-filled LDS output tile a dword at a time (records past
+// the LDS cap go to HBM directly); the tile leaves with coalesced 16-byte
+// stores (byte stores only on the two edge chunks shared with the
+// neighbouring tiles). a.offs receives every record's start.
+// (A single-pass variant with decoupled look-back was measured slower here:
+// its ticket counter alone — one atomic per tile on one address — cost
+// 1.5 ms on 256 Ki tiles, and the look-back wait another 1.4 ms.)
+struct EncodeShared {
+  unsigned long long part[4];
+  unsigned int lds_end;
+};
+
 template <class PP>
 __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uint32_t S,
-                                           uint8_t* smem, unsigned long long* part,
-                                           unsigned int* lds_end_p) {
+                                           uint8_t* smem, EncodeShared& sm) {
   const uint64_t r0 = (uint64_t)blockIdx.x * kET;
   const uint32_t nrec = (uint32_t)min((uint64_t)kET, a.n - r0);
   uint8_t* rtile = smem;
@@ -356,37 +465,47 @@ __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uin
   const uint32_t r = threadIdx.x;
   const unsigned long long sz = r < nrec ? a.offs[r0 + r] : 0;
   unsigned long long tile_total;
-  const unsigned long long rel = block_exscan256(sz, part, &tile_total);
+  const unsigned long long rel = block_exscan256(sz, sm.part, &tile_total);
   const unsigned long long tile_base = a.block_sums[blockIdx.x];
-  unsigned int& lds_end = *lds_end_p;
-  if (r == 0) lds_end = (unsigned int)min(tile_total, (unsigned long long)kOutCap);
-  __syncthreads();  // record tile staged, lds_end initialised
   uint8_t* gtile = a.out + tile_base;
   const uint32_t osh = (uint32_t)((uintptr_t)gtile & 15);
+  {  // zero the part of the output tile the records will OR into
+    const uint4 z = {0u, 0u, 0u, 0u};
+    const uint32_t nz =
+        (osh + (uint32_t)min(tile_total, (unsigned long long)kOutCap) + 4 + 15) >> 4;
+    for (uint32_t i = threadIdx.x; i < nz; i += kET) ((uint4*)otile)[i] = z;
+  }
+  if (r == 0) sm.lds_end = (unsigned int)min(tile_total, (unsigned long long)kOutCap);
+  __syncthreads();  // record tile staged, output tile zeroed, lds_end initialised
   bool fits = false;
   if (r < nrec) {
     const unsigned long long start = tile_base + rel;
     a.offs[r0 + r] = start;
     if (start + sz > a.cap) {
       atomicMin(&a.res->first_fail, (unsigned long long)(r0 + r));
-      atomicMin(&lds_end, (unsigned int)min(rel, (unsigned long long)kOutCap));
+      atomicMin(&sm.lds_end, (unsigned int)min(rel, (unsigned long long)kOutCap));
     } else {
       fits = rel + sz <= kOutCap;
-      if (!fits) atomicMin(&lds_end, (unsigned int)rel);
+      if (!fits) atomicMin(&sm.lds_end, (unsigned int)rel);
     }
   }
   __syncthreads();
   if (r < nrec) {
     const uint8_t* rec = rtile + rsh + r * S;
-    if (fits && rel + sz <= lds_end) {
-      program_emit(P, rec, a.sbase, a.lbase, ByteSink{otile + osh + (uint32_t)rel});
+    if (fits && rel + sz <= sm.lds_end) {
+#ifdef TGPU_LDS_BYTE_SINK
+      ByteSink w(otile + osh + (uint32_t)rel);
+#else
+      WordSink w((uint32_t*)otile, osh + (uint32_t)rel);
+#endif
+      program_emit(P, rec, a.sbase, a.lbase, w);
     } else if (tile_base + rel + sz <= a.cap) {
-      program_emit(P, rec, a.sbase, a.lbase, ByteSink{gtile + rel});
+      emit_to_hbm(P, rec, a.sbase, a.lbase, gtile + rel);
     }
   }
   __syncthreads();
   // LDS tile [osh, osh + lds_end) -> HBM [gtile, gtile + lds_end)
-  const uint32_t end = osh + lds_end;
+  const uint32_t end = osh + sm.lds_end;
   const uint32_t nvec = (end + 15) >> 4;
   uint8_t* gb = gtile - osh;
   for (uint32_t i = threadIdx.x; i < nvec; i += kET) {
