@@ -88,7 +88,7 @@ uint32_t program_decode_wire_cap(const DecodeArgs& a) {
 }
 
 uint32_t program_decode_lds(uint32_t wire_cap, uint32_t rec_size) {
-  return wire_cap + 32 + ((kPT * rec_size + 16 + 15) & ~15u);
+  return prog::decode_wire_region(wire_cap) + ((kPT * rec_size + 16 + 15) & ~15u);
 }
 
 hipError_t launch_program_decode(const DecodeArgs& a, const VProgram* d_prog, uint32_t rec_size,

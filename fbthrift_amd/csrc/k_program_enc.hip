@@ -129,7 +129,7 @@ hipError_t launch_program_encode(const EncodeArgs& a, const VProgram* d_prog,
                                  const JitKernels* jit) {
   if (a.n == 0) return hipSuccess;
   const uint64_t tiles = (a.n + kET - 1) / kET;
-  const uint32_t rt = (kET * a.rec_size + 16 + 15) & ~15u;
+  const uint32_t rt = prog::enc_record_region(a.rec_size);
   hipError_t e;
   if (jit) {
     e = jit_launch_encode(jit, false, a, tiles, rt, stream);
