@@ -43,7 +43,15 @@ struct tgpu_context {
   uint8_t* d_index = nullptr;
   uint64_t index_bytes = 0;
   int last_op = 0;        // 1 decode, 2 encode
+  void* host_pipe = nullptr;  // tgpu_host.cpp: streams + chunk buffers of the host path
 };
+
+namespace tgpu {
+void* context_host_pipe(tgpu_context* c) {
+  if (!c->host_pipe) c->host_pipe = host_pipe_create();
+  return c->host_pipe;
+}
+}  // namespace tgpu
 
 namespace {
 
@@ -665,6 +673,7 @@ int tgpu_context_create(tgpu_context** out) {
 
 void tgpu_context_destroy(tgpu_context* c) {
   if (!c) return;
+  if (c->host_pipe) host_pipe_destroy(c->host_pipe);
   if (c->d_res) (void)hipFree(c->d_res);
   if (c->h_res) (void)hipHostFree(c->h_res);
   if (c->d_offs) (void)hipFree(c->d_offs);

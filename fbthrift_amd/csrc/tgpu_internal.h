@@ -300,6 +300,11 @@ hipError_t launch_program_encode(const EncodeArgs& a, const VProgram* d_prog,
                                  const JitKernels* jit);
 hipError_t launch_size_offsets(const EncodeArgs& a, uint64_t n_blocks, hipStream_t stream);
 
+// ---- host-memory pipeline (tgpu_host.cpp) -------------------------------------
+void* host_pipe_create();
+void host_pipe_destroy(void* pipe);
+void* context_host_pipe(tgpu_context* ctx);  // created on first use, owned by ctx
+
 // ---- stream indexer (k_index.hip) launchers
 uint64_t index_chunk_bytes(uint64_t span, bool tiles);
 uint64_t index_tile_bytes();

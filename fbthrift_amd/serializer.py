@@ -69,6 +69,15 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else None
 
 
+def _hptr(a):
+    """Address of a host buffer (numpy array or CPU tensor)."""
+    return a.ctypes.data if hasattr(a, "ctypes") else a.data_ptr()
+
+
+def _hlen(a):
+    return a.nbytes if hasattr(a, "nbytes") else a.numel() * a.element_size()
+
+
 def _stream(stream):
     import torch
 
@@ -271,6 +280,38 @@ class BatchSerializer:
             ctypes.byref(n_dec), ctypes.byref(consumed))
         return records, arena, st, n_dec.value, consumed.value
 
+
+    # -- host memory ----------------------------------------------------------
+    def deserialize_host(self, gschema, wire, n, records=None, chunk=0, limits=None):
+        """Host-memory decode (tgpu_decode_host): `wire` and `records` are host
+        buffers (numpy uint8 arrays or CPU tensors, pinned or pageable); the
+        batch is pipelined through the GPU in chunks of `chunk` records.
+        Returns (records, status, n_decoded, consumed) without raising."""
+        import numpy as np
+
+        if records is None:
+            records = np.zeros(max(n * gschema.record_size, 1), np.uint8)
+        lim = _lib.Limits(*limits) if limits is not None else None
+        st = _lib.Status()
+        n_dec, consumed = ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.lib().tgpu_decode_host(
+            self.context().handle, gschema.handle, self.protocol, _hptr(wire), _hlen(wire), n,
+            _hptr(records), chunk, ctypes.byref(lim) if lim is not None else None,
+            ctypes.byref(st), ctypes.byref(n_dec), ctypes.byref(consumed))
+        return records, st, n_dec.value, consumed.value
+
+    def serialize_host(self, gschema, records, n, out=None, chunk=0):
+        """Host-memory encode (tgpu_encode_host) of n records held in host
+        memory into `out` (allocated when None). Returns (out, status, size)."""
+        import numpy as np
+
+        if out is None:
+            out = np.zeros(max(n * gschema.fixed_wire_size(self.protocol), 1), np.uint8)
+        st, size = _lib.Status(), ctypes.c_uint64()
+        _lib.lib().tgpu_encode_host(self.context().handle, gschema.handle, self.protocol,
+                                    _hptr(records), n, _hptr(out), _hlen(out), chunk,
+                                    ctypes.byref(st), ctypes.byref(size))
+        return out, st, size.value
 
     # -- stream index -------------------------------------------------------
     def index_stream(self, gschema, wire, begin=0, end=None, speculative=False,

@@ -301,6 +301,28 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema,
                       void* stream, tgpu_status* st, uint64_t* n_decoded,
                       uint64_t* consumed);
 
+/* ---- host-memory batches ---------------------------------------------- */
+/*
+ * The same calls for data that starts and ends in HOST memory (an IOBuf's
+ * bytes, a host record array): Serializer::deserialize / ::serialize over a
+ * host buffer (Serializer.h:62-72, :136-148), N records at a time. The batch
+ * is cut into chunks of chunk_records records (0 = 4 Mi) that are pipelined
+ * over three streams (copy in, kernels, copy out overlapping), so the rate is
+ * the PCIe rate. Host buffers may be pinned (fastest) or pageable (pinned in
+ * place for the call). Blocking; results and status exactly as for
+ * tgpu_decode_batch / tgpu_encode_batch on the whole batch.
+ * Scope: schemas with a fixed canonical Binary record length
+ * (tgpu_schema_fixed_wire_size != 0); others -> TGPU_ERR_UNSUPPORTED.
+ */
+int tgpu_decode_host(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                     const void* host_in, uint64_t in_len, uint64_t n_records,
+                     void* host_records, uint64_t chunk_records, const tgpu_limits* limits,
+                     tgpu_status* st, uint64_t* n_decoded, uint64_t* consumed);
+int tgpu_encode_host(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                     const void* host_records, uint64_t n_records, void* host_out,
+                     uint64_t out_capacity, uint64_t chunk_records, tgpu_status* st,
+                     uint64_t* out_size);
+
 /* ---- stream index ----------------------------------------------------- */
 /*
  * Record index of an unindexed stream — the bulk form of the file-reading
