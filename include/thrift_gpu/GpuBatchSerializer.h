@@ -254,6 +254,33 @@ class GpuBatchSerializer {
     return consumed;
   }
 
+  /* Host-memory forms (the reference's callers hold IOBuf / host objects,
+   * Serializer.h:62-72,136-148): records and bytes stay in host memory and
+   * are pipelined through the GPU in chunks (tgpu_decode_host /
+   * tgpu_encode_host; fixed-length Binary record schemas). */
+  uint64_t deserializeHost(const void* in, uint64_t len, uint64_t n, void* records,
+                           uint64_t chunk_records = 0) {
+    tgpu_status st{};
+    uint64_t done = 0, consumed = 0;
+    tgpu_decode_host(ctx_, schema_.get(), Protocol::kId, in, len, n, records, chunk_records,
+                     &limits_, &st, &done, &consumed);
+    if (st.code != TGPU_OK) rethrow(st);
+    return consumed;
+  }
+  uint64_t serializeHost(const void* records, uint64_t n, void* out, uint64_t capacity,
+                         uint64_t chunk_records = 0) {
+    tgpu_status st{};
+    uint64_t size = 0;
+    tgpu_encode_host(ctx_, schema_.get(), Protocol::kId, records, n, out, capacity,
+                     chunk_records, &st, &size);
+    if (st.code != TGPU_OK) rethrow(st);
+    return size;
+  }
+  /* Generates and compiles the schema's kernels now (tgpu_schema_compile):
+   * the run-time counterpart of thrift1 emitting T::readNoXfer / T::write.
+   * False when the schema runs on the interpreting kernels instead. */
+  bool compile() { return tgpu_schema_compile(schema_.get(), Protocol::kId) == TGPU_OK; }
+
   /* Asynchronous forms: enqueue on the stream; collect with wait(). */
   void serializeAsync(const void* records, uint64_t n, void* out, uint64_t capacity,
                       uint64_t* offsets = nullptr, const void* string_base = nullptr,
