@@ -274,11 +274,10 @@ class FileShards(Mixed):
     Step: every rank encodes its 64 Mi records (its part of the file, in file
     order); the file's byte ranges are redistributed so rank k holds
     [B_k, B_{k+1} + overlap) (all_to_all over RCCL; nothing at N=1); rank k
-    indexes its range speculatively (tgpu_index_stream: rank 0 from the
-    file's first byte) and confirms its first record start against rank
-    k-1's last end (fbthrift_amd/shard.py: all-gather of 5 int64 per rank,
-    re-index on disagreement); then it decodes the records that start in its
-    range. Checked after warm-up: per-rank record counts sum to the file's,
+    indexes and decodes its range in one call (tgpu_decode_stream,
+    speculative: rank 0 from the file's first byte) and confirms its first
+    record start against rank k-1's last end (fbthrift_amd/shard.py:
+    all-gather of 5 int64 per rank, redone on disagreement). Checked after warm-up: per-rank record counts sum to the file's,
     every decoded record equals the generator's record of the same global
     index, and re-encoding the decoded records reproduces the range's bytes.
     """
@@ -291,6 +290,9 @@ class FileShards(Mixed):
         import torch.distributed as dist
 
         super().__init__(n, rank, dev)
+        # the decode call is the fused index + decode (tgpu_decode_stream)
+        self.dec_kernel = ("tgpu_jit_index_decode" if self.dec_kernel.startswith("tgpu_jit")
+                           else "index_tile_decode_kernel")
         self.rank, self.dev = rank, dev
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.enc = self.wire  # this rank's part of the file (in file order)
@@ -365,11 +367,15 @@ class FileShards(Mixed):
         b, e = self.ranges[self.rank]
         local = self.buf[: hi - lo]
         cap = self.idx.numel() - 1
+        self.status = None
 
         def index_fn(begin, speculative):
-            _, n, first, last, st = self.S.index_stream(
+            # fused index + decode of the records that start in [begin, e)
+            # (tgpu_decode_stream); a re-run after the exchange replaces them
+            recs, _, _, n, first, last, st = self.S.decode_stream(
                 self.gs, local, begin=begin - lo, end=e - lo, speculative=speculative,
-                max_records=cap, offsets=self.idx)
+                max_records=cap, offsets=self.idx, records=self.back)
+            self.status = st
             if n == 0:
                 return 0, shard.NONE, shard.NONE
             return n, first + lo, last + lo
@@ -377,15 +383,11 @@ class FileShards(Mixed):
         n, first, last, base, rounds = shard.exchange_boundaries(
             index_fn, self.rank, self.world, b, e, self._gather)
         self.n_local, self.first, self.last, self.base, self.rounds = n, first, last, base, rounds
-        if n:
-            self.S.deserialize(self.gs, local, n, offsets=self.idx[: n + 1],
-                               records=self.back[: n * self.record_bytes], sync=False)
 
     def check_timed(self):
-        if self.n_local:
-            st, nd, consumed = self.S.context().wait()
-            if st.code or consumed != self.last - self.first:
-                raise RuntimeError("timed decode failed: %s" % (st.as_tuple(),))
+        if self.n_local and (self.status is None or self.status.code):
+            raise RuntimeError("timed decode failed: %s" % (
+                self.status.as_tuple() if self.status is not None else None,))
 
     def verify(self):
         import ctypes
@@ -422,9 +424,10 @@ class FileShards(Mixed):
         del want, side, again, offs2
 
     def algorithmic(self):
-        # per rank, per step: encode as config 3; decode reads its range once
-        # for the index and once for the decode and writes the records
-        dec_bytes = 2 * (self.last - self.first) + self.n_local * self.record_bytes
+        # per rank, per step: encode as config 3; decode (index + records in
+        # one call) must read its range once and write the records (the
+        # speculation pass's second read is overhead, not algorithmic)
+        dec_bytes = (self.last - self.first) + self.n_local * self.record_bytes
         return dec_bytes, self.n * self.record_bytes + self.side_bytes + self.wire_bytes
 
 

@@ -65,7 +65,7 @@ EXPORTS = [
     "tgpu_schema_fixed_wire_size", "tgpu_context_create", "tgpu_context_destroy",
     "tgpu_context_reserve", "tgpu_context_wait", "tgpu_encode_batch", "tgpu_encoded_size",
     "tgpu_decode_batch", "tgpu_index_stream", "tgpu_schema_compile", "tgpu_schema_compile_check",
-    "tgpu_decode_host", "tgpu_encode_host",
+    "tgpu_decode_host", "tgpu_encode_host", "tgpu_decode_stream",
 ]
 
 _lib = None
@@ -130,5 +130,10 @@ def lib():
     L.tgpu_encode_host.restype = I32
     L.tgpu_encode_host.argtypes = [P, P, I32, P, U64, P, U64, U64, ctypes.POINTER(Status),
                                    ctypes.POINTER(U64)]
+    L.tgpu_decode_stream.restype = I32
+    L.tgpu_decode_stream.argtypes = [P, P, I32, P, U64, U64, U64, I32, P, U64, P, P, U64,
+                                     ctypes.POINTER(Limits), P, ctypes.POINTER(Status),
+                                     ctypes.POINTER(U64), ctypes.POINTER(U64),
+                                     ctypes.POINTER(U64)]
     _lib = L
     return L

@@ -129,6 +129,24 @@ __global__ void decode_finish_kernel(DecodeArgs a, uint64_t fixed_len) {
   }
 }
 
+// After a fused index + decode of a stream range (tgpu_decode_stream): the
+// index left n_records / total_bytes / first_start (and a reader error's
+// code); a record it accepted that the decode could not store (list arena
+// overflow) is re-diagnosed here and ends the range.
+template <int P>
+__global__ void stream_decode_finish_kernel(DecodeArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  DevResult* res = a.res;
+  const uint64_t f = res->first_fail;
+  if (f < res->n_records) {
+    const Reader r = decode_one<P>(a, f);
+    res->code = r.ok() ? TGPU_ERR_INDEX_MISMATCH : r.err;
+    res->fail_offset = r.ok() ? r.pos : r.err_off;
+    res->n_records = f;
+    res->total_bytes = a.offs[f];
+  }
+}
+
 // ------------------------------------------------------------------ encode --
 template <int P>
 __device__ __forceinline__ Writer size_one(const EncodeArgs& a, uint64_t i) {
@@ -262,6 +280,16 @@ hipError_t launch_decode_finish(const DecodeArgs& a, int protocol, uint64_t fixe
   else
     hipLaunchKernelGGL(decode_finish_kernel<TGPU_PROTOCOL_COMPACT>, dim3(1), dim3(64), 0, stream, a,
                        fixed_len);
+  return hipGetLastError();
+}
+
+hipError_t launch_stream_decode_finish(const DecodeArgs& a, int protocol, hipStream_t stream) {
+  if (protocol == TGPU_PROTOCOL_BINARY)
+    hipLaunchKernelGGL(stream_decode_finish_kernel<TGPU_PROTOCOL_BINARY>, dim3(1), dim3(64), 0,
+                       stream, a);
+  else
+    hipLaunchKernelGGL(stream_decode_finish_kernel<TGPU_PROTOCOL_COMPACT>, dim3(1), dim3(64), 0,
+                       stream, a);
   return hipGetLastError();
 }
 

@@ -246,7 +246,14 @@ __global__ __launch_bounds__(kTileLanes) void index_tile_spec_kernel(IndexArgs a
 __global__ __launch_bounds__(kTileLanes) void index_tile_emit_kernel(IndexArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[prog::kTileLds];
   __shared__ prog::IndexTileShared sm;
-  prog::index_emit_tile(a, prog::DynProg{a.prog}, lds, sm);
+  prog::index_emit_tile<false>(a, prog::DynProg{a.prog}, lds, sm, nullptr);
+}
+
+__global__ __launch_bounds__(kTileLanes) void index_tile_decode_kernel(IndexArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[prog::kTileLds];
+  __shared__ __attribute__((aligned(16))) uint8_t rtile[prog::kRecTileBytes + 32];
+  __shared__ prog::IndexTileShared sm;
+  prog::index_emit_tile<true>(a, prog::DynProg{a.prog}, lds, sm, rtile);
 }
 
 __device__ __forceinline__ bool link_broken(const IndexArgs& a, uint64_t j) {
@@ -368,6 +375,22 @@ __global__ __launch_bounds__(256) void index_emit_cont_kernel(IndexArgs a) {
   Chain c;
   chain<P>(a, a.ep[j], kNo, false, a.scratch + j * a.rec_size, c, a.offs + b,
            a.max_records + 1 - b, n);
+  if (a.recs)  // fused decode: these records take the general decoder
+    for (uint64_t i = 0; i < c.count && b + i < a.n_decode; ++i)
+      a.irr[atomicAdd(a.nirr, 1ull)] = b + i;
+}
+
+// Fused decode: a stream that ends (or fails) before n_decode records hands
+// its first missing record to the general decoder, which reports it exactly
+// (underflow, or the reader error the index stopped at).
+__global__ void index_decode_tail_kernel(IndexArgs a, const unsigned long long* total_p) {
+  if (threadIdx.x || blockIdx.x) return;
+  const uint64_t total = *total_p;
+  // decode_batch: the first missing record fails (underflow or the reader
+  // error); a stream range: only a reader error's record (partially decoded
+  // like the reference leaves it)
+  if (total < a.n_decode && (a.decode_tail || a.scal[2] != kNo))
+    a.irr[atomicAdd(a.nirr, 1ull)] = total;
 }
 
 // total records; end of the last one; status; decode padding of the index.
@@ -436,13 +459,16 @@ uint64_t index_chunk_bytes(uint64_t span, bool tiles) {
   return c;
 }
 
-hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const JitKernels* jit) {
+hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const JitKernels* jit,
+                               bool* fused) {
+  const bool decode = a.recs && a.prog && a.chunk == kTile;
+  if (fused) *fused = decode;
   const uint64_t C = a.n_chunks;
   const dim3 g((uint32_t)((C + 255) / 256)), b(256);
   const bool bin = a.protocol == TGPU_PROTOCOL_BINARY;
   if (a.prog && a.chunk == kTile) {
     if (jit) {
-      const hipError_t e = jit_launch_index(jit, false, a, C, stream);
+      const hipError_t e = jit_launch_index(jit, 0, a, C, stream);
       if (e != hipSuccess) return e;
     } else {
       hipLaunchKernelGGL(index_tile_spec_kernel, dim3((uint32_t)C), dim3(kTileLanes), 0, stream, a);
@@ -473,18 +499,24 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
   hipLaunchKernelGGL(index_prep_kernel, g, b, 0, stream, a);
   e = launch_scan_tiles(a.base, C, a.part, nullptr, nullptr, stream);
   if (e != hipSuccess) return e;
+  IndexArgs x = a;
+  if (!decode) x.recs = nullptr;
   if (a.prog && a.chunk == kTile && jit) {
-    e = jit_launch_index(jit, true, a, C, stream);
+    e = jit_launch_index(jit, decode ? 2 : 1, x, C, stream);
     if (e != hipSuccess) return e;
+  } else if (decode) {
+    hipLaunchKernelGGL(index_tile_decode_kernel, dim3((uint32_t)C), dim3(kTileLanes), 0, stream, x);
   } else if (a.prog && a.chunk == kTile)
-    hipLaunchKernelGGL(index_tile_emit_kernel, dim3((uint32_t)C), dim3(kTileLanes), 0, stream, a);
+    hipLaunchKernelGGL(index_tile_emit_kernel, dim3((uint32_t)C), dim3(kTileLanes), 0, stream, x);
   else
     hipLaunchKernelGGL(index_emit_kernel, g, b, 0, stream, a);
   if (bin)
-    hipLaunchKernelGGL(index_emit_cont_kernel<TGPU_PROTOCOL_BINARY>, g, b, 0, stream, a);
+    hipLaunchKernelGGL(index_emit_cont_kernel<TGPU_PROTOCOL_BINARY>, g, b, 0, stream, x);
   else
-    hipLaunchKernelGGL(index_emit_cont_kernel<TGPU_PROTOCOL_COMPACT>, g, b, 0, stream, a);
+    hipLaunchKernelGGL(index_emit_cont_kernel<TGPU_PROTOCOL_COMPACT>, g, b, 0, stream, x);
   hipLaunchKernelGGL(index_finish_kernel, dim3(1), dim3(64), 0, stream, a, a.scal + 5);
+  if (decode)
+    hipLaunchKernelGGL(index_decode_tail_kernel, dim3(1), dim3(64), 0, stream, x, a.scal + 5);
   if (a.fill_to > 0)
     hipLaunchKernelGGL(index_pad_kernel, dim3((uint32_t)((a.fill_to + 256) / 256)), b, 0, stream,
                        a, a.scal + 5);

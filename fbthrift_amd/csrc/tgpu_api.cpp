@@ -446,10 +446,15 @@ hipError_t launch_indexed_decode(tgpu_context* ctx, const tgpu_schema* schema, i
 
 // Stream index into offs (max_records + 1 entries); see launch_index_stream.
 // Returns a TGPU_ERR_* for host-side failures; HIP launch errors go to `e`.
+// dec (optional): decode the records during the index when the tile path
+// allows it (*fused set); records [0, dec->n) into dec->recs / dec->arena,
+// leftovers to ctx->d_irr for the general decoder.
 int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, const uint8_t* in,
                  uint64_t in_len, uint64_t begin, uint64_t end, int speculative, uint64_t* offs,
                  uint64_t max_records, uint64_t fill_to, const tgpu_limits* limits,
-                 hipStream_t s, hipError_t& e) {
+                 hipStream_t s, hipError_t& e, const DecodeArgs* dec = nullptr,
+                 bool* fused = nullptr) {
+  if (fused) *fused = false;
   IndexArgs x{};
   x.sc = dev_schema(schema);
   x.in = in;
@@ -473,6 +478,15 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   x.max_records = max_records;
   x.fill_to = fill_to;
   x.res = ctx->d_res;
+  if (dec) {
+    x.recs = dec->recs;
+    x.arena = dec->arena;
+    x.arena_cap = dec->arena_cap;
+    x.n_decode = dec->n;
+    x.irr = ctx->d_irr;
+    x.nirr = &ctx->d_res->n_irregular;
+    x.decode_tail = fill_to > 0;
+  }
   const uint64_t C = std::max<uint64_t>(x.n_chunks, 1);
   const uint64_t rs = (x.rec_size + 7) & ~7u;
   const uint64_t parts = scan_tiles_parts(C) + 1;
@@ -504,7 +518,10 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
     return TGPU_OK;
   }
   if (e == hipSuccess)
-    e = launch_index_stream(x, s, x.prog ? schema_jit(schema, protocol, JIT_INDEX, 0, end - begin) : nullptr);
+    e = launch_index_stream(x, s,
+                            x.prog ? schema_jit(schema, protocol, JIT_INDEX, 0, end - begin)
+                                   : nullptr,
+                            fused);
   return TGPU_OK;
 }
 
@@ -873,6 +890,7 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   (void)hipGetLastError();  // drop a stale error left by another library
   hipError_t e = launch_result_init(ctx->d_res, n, s);
   uint64_t fixed = 0;
+  bool fused = false;
   if (n && protocol == TGPU_PROTOCOL_BINARY && schema->fixed_binary && !offsets &&
       in_len >= n * (uint64_t)schema->tmpl.wire_len) {
     fixed = schema->tmpl.wire_len;
@@ -893,8 +911,10 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
       // position, so the decoder reports them exactly
       a.offs = ctx->d_offs;
       if (e == hipSuccess) {
+        // the index tiles decode their records as they find them (fused);
+        // whatever they leave goes to the general decoder below
         const int irc = launch_index(ctx, schema, protocol, a.in, in_len, 0, in_len, 0, ctx->d_offs,
-                                     n, n, limits, s, e);
+                                     n, n, limits, s, e, &a, &fused);
         if (irc) {
           fill_status(st, irc, 0, 0);
           return irc;
@@ -902,7 +922,10 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
       }
     }
     a.check_index = 1;
-    if (e == hipSuccess) e = launch_indexed_decode(ctx, schema, protocol, a, s);
+    if (e == hipSuccess && fused)
+      e = launch_general_decode_list(a, protocol, ctx->d_irr, &ctx->d_res->n_irregular, s);
+    else if (e == hipSuccess)
+      e = launch_indexed_decode(ctx, schema, protocol, a, s);
   }
   if (e == hipSuccess && n) e = launch_decode_finish(a, protocol, fixed, s);
   ctx->last_op = 1;
@@ -916,6 +939,101 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
     return tgpu_context_wait(ctx, stream, st ? st : &tmp, n_decoded, consumed);
   }
   return TGPU_OK;
+}
+
+int tgpu_decode_stream(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                       const void* in, uint64_t in_len, uint64_t begin, uint64_t end,
+                       int speculative, uint64_t* offsets, uint64_t max_records, void* records,
+                       void* list_arena, uint64_t list_arena_capacity,
+                       const tgpu_limits* limits, void* stream, tgpu_status* st,
+                       uint64_t* n_records, uint64_t* first_start, uint64_t* last_end) {
+  if (!ctx || !schema || !offsets || (max_records && !records) ||
+      (protocol != TGPU_PROTOCOL_BINARY && protocol != TGPU_PROTOCOL_COMPACT) ||
+      (!in && in_len) || begin > end || end > in_len ||
+      ((uintptr_t)records) % schema->structs[0].align) {
+    fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+    return TGPU_ERR_INVALID_ARGUMENT;
+  }
+  const hipStream_t s = (hipStream_t)stream;
+  int rc = ensure_workspace(ctx, max_records + 1);
+  if (rc) {
+    fill_status(st, rc, 0, 0);
+    return rc;
+  }
+  DecodeArgs a{};
+  a.sc = dev_schema(schema);
+  a.in = (const uint8_t*)in;
+  a.in_len = in_len;
+  a.n = max_records;
+  a.offs = offsets;
+  a.recs = (uint8_t*)records;
+  a.arena = (uint8_t*)list_arena;
+  a.arena_cap = list_arena_capacity;
+  a.string_limit = limits ? limits->string_limit : 0;
+  a.container_limit = limits ? limits->container_limit : 0;
+  a.max_depth = limits ? limits->max_depth : 12000;
+  a.height = limits ? limits->height : 0;
+  a.rec_size = schema->structs[0].size;
+  // lengths come from the same reader that found them; the failing record's
+  // successor has no start to check against
+  a.check_index = 0;
+  a.res = ctx->d_res;
+  (void)hipGetLastError();  // drop a stale error left by another library
+  hipError_t e = launch_result_init(ctx->d_res, 0, s);
+  bool fused = false;
+  rc = launch_index(ctx, schema, protocol, a.in, in_len, begin, end, speculative, offsets,
+                    max_records, 0, limits, s, e, max_records ? &a : nullptr, &fused);
+  if (rc) {
+    fill_status(st, rc, 0, 0);
+    return rc;
+  }
+  if (e == hipSuccess && fused) {
+    e = launch_general_decode_list(a, protocol, ctx->d_irr, &ctx->d_res->n_irregular, s);
+    if (e == hipSuccess) e = launch_stream_decode_finish(a, protocol, s);
+  } else if (e == hipSuccess && max_records) {
+    // the range was indexed without the tile path: decode the records found
+    e = hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess) {
+      const DevResult r = *ctx->h_res;
+      uint64_t m = std::min<uint64_t>(r.n_records, max_records);
+      if (r.code && r.n_records < max_records) m += 1;  // the failing record, partially
+      if (m) {
+        DecodeArgs b = a;
+        b.n = m;
+        e = launch_general_decode(b, protocol, s);
+      }
+      // the index's result stands (same records, same first failure)
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(ctx->d_res, ctx->h_res, sizeof(DevResult), hipMemcpyHostToDevice, s);
+    }
+  }
+  ctx->last_op = 3;
+  if (e != hipSuccess) {
+    fill_status(st, TGPU_ERR_HIP, 0, 0);
+    if (st) st->reserved = (int32_t)e;
+    return TGPU_ERR_HIP;
+  }
+  if (!st && !n_records && !first_start && !last_end) return TGPU_OK;
+  e = hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) {
+    fill_status(st, TGPU_ERR_HIP, 0, 0);
+    if (st) st->reserved = (int32_t)e;
+    return TGPU_ERR_HIP;
+  }
+  const DevResult& r = *ctx->h_res;
+  int code = r.code;
+  uint64_t rec = code ? r.first_fail : r.n_records, off = code ? r.fail_offset : 0;
+  if (!code && r.n_records > max_records) {
+    code = TGPU_ERR_OUTPUT_OVERFLOW;
+    rec = max_records;
+  }
+  fill_status(st, code, rec, off);
+  if (n_records) *n_records = r.n_records;
+  if (first_start) *first_start = r.first_start;
+  if (last_end) *last_end = r.total_bytes;
+  return code;
 }
 
 int tgpu_index_stream(tgpu_context* ctx, const tgpu_schema* schema, int protocol, const void* in,

@@ -223,6 +223,17 @@ struct IndexArgs {
   uint64_t max_records;
   uint64_t fill_to;          // decode: offs[total+1 .. fill_to] = last end
   DevResult* res;
+  // fused decode (index tiles decode their records as they emit the starts;
+  // recs == nullptr: index only): records [0, n_decode) of stride rec_size,
+  // list arena, and the list of records left to the general decoder
+  uint8_t* recs;
+  uint8_t* arena;
+  uint64_t arena_cap;
+  uint64_t n_decode;
+  uint64_t* irr;
+  unsigned long long* nirr;
+  int32_t decode_tail;  // a stream shorter than n_decode: its first missing record fails
+  int32_t pad_;
 };
 
 #ifndef __HIPCC_RTC__
@@ -261,7 +272,8 @@ hipError_t jit_launch_decode(const JitKernels* J, const DecodeArgs& a, uint64_t 
                              hipStream_t s);
 hipError_t jit_launch_encode(const JitKernels* J, bool write, const EncodeArgs& a, uint64_t grid,
                              uint32_t lds, hipStream_t s);
-hipError_t jit_launch_index(const JitKernels* J, bool emit, const IndexArgs& a, uint64_t grid,
+// which: 0 speculation, 1 emit, 2 emit + fused decode
+hipError_t jit_launch_index(const JitKernels* J, int which, const IndexArgs& a, uint64_t grid,
                             hipStream_t s);
 
 // jit: the schema's compiled kernels (nullptr: interpret d_prog).
@@ -309,7 +321,14 @@ void* context_host_pipe(tgpu_context* ctx);  // created on first use, owned by c
 uint64_t index_chunk_bytes(uint64_t span, bool tiles);
 uint64_t index_tile_bytes();
 uint64_t index_tile_lanes();
-hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const JitKernels* jit);
+// Returns (in *fused) whether the records were decoded during the index
+// (a.recs set and the LDS-tile path taken); otherwise the caller decodes them
+// from the index.
+hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const JitKernels* jit,
+                               bool* fused);
+// After a fused index + decode over a stream range: re-diagnoses a record
+// the index accepted but the decode could not store (list arena overflow).
+hipError_t launch_stream_decode_finish(const DecodeArgs& a, int protocol, hipStream_t stream);
 // Empty range: offs[0..fill_to] = pos, no records.
 hipError_t launch_index_empty(DevResult* res, uint64_t* offs, uint64_t pos, uint64_t fill_to,
                               hipStream_t stream);

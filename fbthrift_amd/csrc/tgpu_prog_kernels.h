@@ -688,6 +688,13 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
     // outside the search so all lanes of the wave run it together
     const VOp o0 = P.op(0);
     const uint32_t h0 = o0.kind == VOP_CONST ? (o0.hdr & 0xff) : 0x100;
+    // every record ends with its STOP byte, so every record start but the
+    // range's first is preceded by it: candidates are h0 bytes after a STOP
+    // byte (a necessary condition — it only prunes; for the mixed schema,
+    // whose four int headers all equal h0, it removes ~3 of 4 candidates)
+    const VOp ol = P.op(P.n_ops() - 1);
+    const uint32_t stop =
+        (ol.kind == VOP_CONST && ol.hdr_len) ? ((ol.hdr >> (8 * (ol.hdr_len - 1))) & 0xff) : 0x100;
     // bytes of the slice equal to h0, all eight 8-byte groups loaded at once
     uint64_t mk[kSub / 8];
 #pragma unroll
@@ -699,6 +706,13 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
         if (h0 < 0x100) {
           const uint64_t x = src.win8(base) ^ (h0 * 0x0101010101010101ull);
           m = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
+        }
+        if (stop < 0x100 && base > 0) {
+          const uint64_t y = src.win8(base - 1) ^ (stop * 0x0101010101010101ull);
+          uint64_t z = (y - 0x0101010101010101ull) & ~y & 0x8080808080808080ull;
+          // the range's first byte has no predecessor inside the range
+          if (j == 0 && sh >= base && sh < base + 8) z |= 0x80ull << (8 * (sh - base));
+          m &= z;
         }
       }
       mk[i] = m;
@@ -827,9 +841,18 @@ __device__ __forceinline__ void index_spec_tile(const IndexArgs& a, const PP& P,
 // Emit for a tile whose first start is verified (a.s[j]); records starting in
 // the tile get their starts written at offs[base[j] ..]. A tile the program
 // cannot finish goes to index_emit_cont_kernel whole.
-template <class PP>
+// kDecode (fused index + decode, a.recs set): the walk that finds each start
+// also decodes the record (the same program, storing) into an LDS record
+// tile (zero-filled = default-initialized records) that leaves with
+// coalesced 16-byte stores; records past the LDS tile go to HBM directly;
+// a record the program cannot store (list arena overflow) is queued for the
+// general decoder. This removes the decode pass's second read of the wire
+// and of the index.
+constexpr uint32_t kRecTileBytes = 18 * 1024;
+
+template <bool kDecode, class PP>
 __device__ __forceinline__ void index_emit_tile(const IndexArgs& a, const PP& P, uint8_t* lds,
-                                                IndexTileShared& sm) {
+                                                IndexTileShared& sm, uint8_t* rtile) {
   const uint64_t j = blockIdx.x;
   if (threadIdx.x == 0) a.ep[j] = kNo;
   if (j >= a.scal[1] || a.cnt[j] == 0) return;
@@ -875,22 +898,80 @@ __device__ __forceinline__ void index_emit_tile(const IndexArgs& a, const PP& P,
   __syncthreads();
   unsigned long long pre = x - L.c;
   for (int w = 0; w < wid; ++w) pre += sm.part[w];
-  if (L.c == 0) return;
-  // re-walk this lane's records, writing absolute starts
   const uint64_t gb = lo - sh;
-  uint32_t p = L.s;
   const uint8_t* g = a.in + gb;
   const uint64_t avail64 = a.in_len - gb;
   const uint32_t avail = (uint32_t)(avail64 < kPosCap ? avail64 : kPosCap);
   const uint32_t staged = avail < kTile + kOver + 16 ? avail : kTile + kOver + 16;
   const TileSrc src{(const uint32_t*)lds, staged & ~3u, HbmSrc{g, avail}};
-  const Ctx pc{0, nullptr, 0, a.string_limit, a.container_limit};
-  for (uint32_t i = 0; i < L.c; ++i) {
-    const uint64_t idx = b + pre + i;
-    if (idx <= a.max_records) a.offs[idx] = gb + p;
-    uint32_t q = p;
-    run_program<false>(P, src, pc, q, avail, nullptr);
-    p = q;
+  if constexpr (!kDecode) {
+    if (L.c == 0) return;
+    // re-walk this lane's records, writing absolute starts
+    const Ctx pc{0, nullptr, 0, a.string_limit, a.container_limit};
+    uint32_t p = L.s;
+    for (uint32_t i = 0; i < L.c; ++i) {
+      const uint64_t idx = b + pre + i;
+      if (idx <= a.max_records) a.offs[idx] = gb + p;
+      uint32_t q = p;
+      run_program<false>(P, src, pc, q, avail, nullptr);
+      p = q;
+    }
+  } else {
+    const uint32_t S = a.rec_size;
+    // the tile's records [b, b + m) that are decoded: below n_decode
+    const uint64_t tile_n = sm.part[0] + sm.part[1] + sm.part[2] + sm.part[3];
+    const uint64_t m = b >= a.n_decode ? 0 : min(tile_n, a.n_decode - b);
+    const uint32_t cap_recs = kRecTileBytes / S;
+    const uint32_t in_lds = (uint32_t)min(m, (uint64_t)cap_recs);
+    uint8_t* gout = a.recs + b * S;
+    const uint32_t osh = (uint32_t)((uintptr_t)gout & 15);
+    {
+      const uint4 z = {0u, 0u, 0u, 0u};
+      const uint32_t nz = (osh + in_lds * S + 15) >> 4;
+      for (uint32_t i = threadIdx.x; i < nz; i += kTileLanes) ((uint4*)rtile)[i] = z;
+    }
+    __syncthreads();
+    const Ctx pc{gb, a.arena, a.arena_cap, a.string_limit, a.container_limit};
+    uint32_t p = L.s;
+    for (uint32_t i = 0; i < L.c; ++i) {
+      const uint64_t t = pre + i, idx = b + t;
+      if (idx <= a.max_records) a.offs[idx] = gb + p;
+      uint32_t q = p;
+      if (t < m) {
+        uint8_t* rec;
+        if (t < in_lds) {
+          rec = rtile + osh + t * S;
+        } else {
+          rec = a.recs + idx * S;
+          for (uint32_t k = 0; k < S; ++k) rec[k] = 0;
+        }
+        if (!run_program<true>(P, src, pc, q, avail, rec)) {
+          // the program cannot store it (list arena): the general decoder
+          // redoes the record from its start; the walk continues with the
+          // measured length
+          a.irr[atomicAdd(a.nirr, 1ull)] = idx;
+          q = p;
+          run_program<false>(P, src, pc, q, avail, nullptr);
+        }
+      } else {
+        run_program<false>(P, src, pc, q, avail, nullptr);
+      }
+      p = q;
+    }
+    __syncthreads();
+    // record tile -> HBM
+    const uint32_t end = osh + in_lds * S;
+    const uint32_t nvec = (end + 15) >> 4;
+    uint8_t* base = gout - osh;
+    for (uint32_t i = threadIdx.x; i < nvec; i += kTileLanes) {
+      const uint32_t lo16 = i << 4, hi16 = lo16 + 16;
+      if (lo16 >= osh && hi16 <= end) {
+        ((uint4*)base)[i] = ((const uint4*)rtile)[i];
+      } else {
+        for (uint32_t k = (lo16 < osh ? osh : lo16); k < (hi16 < end ? hi16 : end); ++k)
+          base[k] = rtile[k];
+      }
+    }
   }
 }
 

@@ -281,6 +281,37 @@ class BatchSerializer:
         return records, arena, st, n_dec.value, consumed.value
 
 
+    def decode_stream(self, gschema, wire, begin=0, end=None, speculative=False,
+                      max_records=None, offsets=None, records=None, arena=None, limits=None,
+                      stream=None):
+        """Index + decode of the records beginning in [begin, end) of an
+        unindexed stream (tgpu_decode_stream). Returns (records, arena,
+        offsets, n, first_start, last_end, status) without raising."""
+        import torch
+
+        end = wire.numel() if end is None else end
+        if max_records is None:
+            max_records = max(end - begin, 0)
+        dev = wire.device
+        if offsets is None:
+            offsets = torch.empty(max_records + 1, dtype=torch.int64, device=dev)
+        if records is None:
+            records = torch.zeros(max(max_records * gschema.record_size, 1), dtype=torch.uint8,
+                                  device=dev)
+        cap = self.arena_bytes(gschema, wire.numel())
+        if arena is None and cap:
+            arena = torch.zeros(cap, dtype=torch.uint8, device=dev)
+        lim = _lib.Limits(*limits) if limits is not None else None
+        st = _lib.Status()
+        n, first, last = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.lib().tgpu_decode_stream(
+            self.context().handle, gschema.handle, self.protocol, _ptr(wire), wire.numel(),
+            begin, end, 1 if speculative else 0, _ptr(offsets), max_records, _ptr(records),
+            _ptr(arena), arena.numel() if arena is not None else 0,
+            ctypes.byref(lim) if lim is not None else None, _stream(stream), ctypes.byref(st),
+            ctypes.byref(n), ctypes.byref(first), ctypes.byref(last))
+        return records, arena, offsets, n.value, first.value, last.value, st
+
     # -- host memory ----------------------------------------------------------
     def deserialize_host(self, gschema, wire, n, records=None, chunk=0, limits=None):
         """Host-memory decode (tgpu_decode_host): `wire` and `records` are host

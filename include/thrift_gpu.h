@@ -350,6 +350,24 @@ int tgpu_index_stream(tgpu_context* ctx, const tgpu_schema* schema, int protocol
                       const tgpu_limits* limits, void* stream, tgpu_status* st,
                       uint64_t* n_records, uint64_t* first_start, uint64_t* last_end);
 
+/*
+ * Index + decode in one pass: the records that begin in [begin, end) of an
+ * unindexed stream (as tgpu_index_stream, incl. a speculative shard) are
+ * decoded into records[0..n) while their starts are found — the whole file
+ * loop `while (!cursor.isAtEnd()) deserialize<T>(cursor)`
+ * (Serializer.h:97-100) over a byte range. offsets (max_records + 1) receives
+ * the starts and the end as for tgpu_index_stream; list_arena as for
+ * tgpu_decode_batch (capacity in_len Binary / 8 * in_len Compact). A record
+ * the reader rejects ends the range with its status and is partially
+ * decoded like the reference leaves it. Blocking when st != NULL.
+ */
+int tgpu_decode_stream(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                       const void* in, uint64_t in_len, uint64_t begin, uint64_t end,
+                       int speculative, uint64_t* offsets, uint64_t max_records,
+                       void* records, void* list_arena, uint64_t list_arena_capacity,
+                       const tgpu_limits* limits, void* stream, tgpu_status* st,
+                       uint64_t* n_records, uint64_t* first_start, uint64_t* last_end);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -157,3 +157,77 @@ def test_unindexed_decode_past_end(gpu):
     ost, orec, _, ond, ocons = oracle.decode(schema, proto, wire, n + 7)
     assert gst.as_tuple() == ost.as_tuple() and gst.record == n
     assert (nd, cons) == (ond, ocons)
+
+
+@pytest.mark.parametrize("n", [5000, 120_000])
+def test_unindexed_decode_past_end_large(gpu, codec, n):
+    """Same past-the-end rule on a stream long enough for the fused index +
+    decode tiles (the first missing record is handed to the general decoder)."""
+    proto = 2
+    schema, wire, woffs = _stream("mixed", proto, n, seed=4)
+    gs = _gs(schema)
+    rec, arena, gst, nd, cons = _ser(proto).deserialize_status(gs, _t(wire, gpu), n + 3)
+    ost, orec, _, ond, ocons = oracle.decode(schema, proto, wire, n + 3)
+    assert gst.as_tuple() == ost.as_tuple() and gst.record == n
+    assert (nd, cons) == (ond, ocons)
+    assert np.array_equal(rec.cpu().numpy()[: n * schema.record_size], orec[: n * schema.record_size])
+
+
+@pytest.mark.parametrize("sname,proto", [("mixed", 2), ("nested", 0), ("nested", 2),
+                                         ("scalars", 2), ("sparse", 2)])
+def test_decode_stream_whole(gpu, codec, sname, proto):
+    """tgpu_decode_stream over a whole stream: starts == oracle offsets, records
+    and list arena == oracle decode."""
+    n = 100_000 if sname in ("mixed", "nested") else 30_000
+    schema, wire, woffs = _stream(sname, proto, n, seed=2)
+    gs = _gs(schema)
+    w = _t(wire, gpu)
+    rec, arena, offs, got, first, last, st = _ser(proto).decode_stream(gs, w[: len(wire)],
+                                                                       max_records=n)
+    assert (st.code, got, first, last) == (0, n, 0, len(wire)), st.as_tuple()
+    assert np.array_equal(offs.cpu().numpy()[: n + 1].astype(np.uint64), woffs)
+    ost, orec, oarena, _, _ = oracle.decode(schema, proto, wire, n)
+    assert np.array_equal(rec.cpu().numpy()[: n * schema.record_size], orec)
+    if arena is not None:
+        k = min(arena.numel(), oarena.size)
+        assert np.array_equal(arena.cpu().numpy()[:k], oarena[:k])
+
+
+@pytest.mark.parametrize("proto", [2, 0])
+def test_decode_stream_speculative_shards(gpu, codec, proto):
+    """Each byte range of a stream cut at arbitrary positions, decoded
+    speculatively, holds exactly the oracle's records that start in it."""
+    n = 200_000
+    schema, wire, woffs = _stream("mixed", proto, n, seed=6, max_len=30)
+    gs = _gs(schema)
+    w = _t(wire, gpu)
+    L = len(wire)
+    ost, orec, _, _, _ = oracle.decode(schema, proto, wire, n)
+    S = schema.record_size
+    cuts = [0] + sorted(np.random.default_rng(3).integers(1, L, 5).tolist()) + [L]
+    for b, e in zip(cuts[:-1], cuts[1:]):
+        rec, arena, offs, got, first, last, st = _ser(proto).decode_stream(
+            gs, w[:L], begin=b, end=e, speculative=b > 0, max_records=n)
+        i0 = int(np.searchsorted(woffs, b))
+        i1 = int(np.searchsorted(woffs[:n], e))
+        assert st.code == 0 and got == i1 - i0, st.as_tuple()
+        if got:
+            assert first == woffs[i0]
+            assert np.array_equal(rec.cpu().numpy()[: got * S], orec[i0 * S: i1 * S])
+
+
+def test_decode_stream_error_mid_stream(gpu, codec):
+    proto = 2
+    n = 60_000
+    schema, wire, woffs = _stream("mixed", proto, n, seed=11)
+    bad = 41_000
+    w = bytearray(wire)
+    w[int(woffs[bad])] = 0x1E  # ctype 14: "don't know what type"
+    wire = bytes(w)
+    gs = _gs(schema)
+    rec, arena, offs, got, first, last, st = _ser(proto).decode_stream(gs, _t(wire, gpu),
+                                                                       max_records=n)
+    ost, orec, _, ond, ocons = oracle.decode(schema, proto, wire, n)
+    assert st.as_tuple() == ost.as_tuple() and got == bad
+    k = bad * schema.record_size
+    assert np.array_equal(rec.cpu().numpy()[:k], orec[:k])
