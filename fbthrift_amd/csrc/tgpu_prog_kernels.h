@@ -254,61 +254,60 @@ __device__ __forceinline__ uint64_t program_size(const PP& P, const uint8_t* rec
 }
 
 // ---- record emission ----------------------------------------------------------
-// A sink appends little-endian packed bytes, at most 4 per put:
-//   WordSink — the zero-filled LDS output tile: bytes gather in a 64-bit
-//              accumulator and leave a dword at a time (ds_write_b32 for
-//              dwords the record owns, ds_or_b32 for the first and last ones,
-//              which it may share with its neighbours);
+// A sink appends little-endian packed bytes: put(v, n <= 4), put64(v, n <= 8)
+// (bytes of v past n are ignored).
+//   OrSink   — the zero-filled LDS output tile: every put ORs its bytes into
+//              the (up to three) dwords they cover with ds_or_b32 — no
+//              branches, no per-lane state beyond the position; bytes a
+//              record shares a dword with its neighbour merge by the OR.
 //   ByteSink — HBM directly, a byte at a time (records past the LDS tile).
-struct WordSink {
+// (A dword-assembling sink that flushed full dwords measured ~25 % slower:
+// its per-put flush branch left the unrolled emitter with thousands of
+// divergent basic blocks and SGPR spills.)
+struct OrSink {
   uint32_t* w32;
-  uint64_t acc;
-  uint32_t wpos, nb;  // acc holds the bytes of dword wpos on (nb valid, incl. the lead-in)
-  bool first;
-  __device__ __forceinline__ WordSink(uint32_t* tile, uint32_t q)
-      : w32(tile), acc(0), wpos(q >> 2), nb(q & 3), first(true) {}
+  uint32_t q;
+  __device__ __forceinline__ OrSink(uint32_t* tile, uint32_t pos) : w32(tile), q(pos) {}
+  __device__ __forceinline__ void put64(uint64_t v, uint32_t n) {
+    if (n < 8) v &= (1ull << (8 * n)) - 1;
+    const uint32_t d = q >> 2, sh = 8 * (q & 3);
+    const uint64_t lo = v << sh;
+    const uint32_t hi = sh ? (uint32_t)(v >> (64 - sh)) : 0u;
+    atomicOr(&w32[d], (uint32_t)lo);
+    atomicOr(&w32[d + 1], (uint32_t)(lo >> 32));
+    atomicOr(&w32[d + 2], hi);
+    q += n;
+  }
   __device__ __forceinline__ void put(uint32_t v, uint32_t n) {
-    if (n < 4) v &= (1u << (8 * n)) - 1;  // callers may pass bytes past n
-    acc |= (uint64_t)v << (8 * nb);
-    nb += n;
-    if (nb >= 4) {
-      if (first) atomicOr(&w32[wpos], (uint32_t)acc);
-      else w32[wpos] = (uint32_t)acc;
-      first = false;
-      acc >>= 32;
-      ++wpos;
-      nb -= 4;
-    }
+    if (n < 4) v &= (1u << (8 * n)) - 1;
+    const uint32_t d = q >> 2, sh = 8 * (q & 3);
+    const uint64_t x = (uint64_t)v << sh;
+    atomicOr(&w32[d], (uint32_t)x);
+    atomicOr(&w32[d + 1], (uint32_t)(x >> 32));
+    q += n;
   }
-  __device__ __forceinline__ void finish() {
-    if (nb) atomicOr(&w32[wpos], (uint32_t)acc);
-  }
+  __device__ __forceinline__ void finish() {}
 };
 struct ByteSink {
   uint8_t* base;
   uint32_t q;
   __device__ __forceinline__ ByteSink(uint8_t* b) : base(b), q(0) {}
-  __device__ __forceinline__ void put(uint32_t v, uint32_t n) {
+  __device__ __forceinline__ void put64(uint64_t v, uint32_t n) {
     for (uint32_t i = 0; i < n; ++i) base[q + i] = (uint8_t)(v >> (8 * i));
     q += n;
   }
+  __device__ __forceinline__ void put(uint32_t v, uint32_t n) { put64(v, n); }
   __device__ __forceinline__ void finish() {}
 };
 
-// n <= 8 little-endian packed bytes
 template <class Sink>
 __device__ __forceinline__ void put8(Sink& s, uint64_t v, uint32_t n) {
-  if (n <= 4) {
-    s.put((uint32_t)v, n);
-  } else {
-    s.put((uint32_t)v, 4);
-    s.put((uint32_t)(v >> 32), n - 4);
-  }
+  s.put64(v, n);
 }
 // big-endian n-byte value (BinaryProtocol-inl.h:120-161 writeBE)
 template <class Sink>
 __device__ __forceinline__ void put_be(Sink& s, uint64_t v, uint32_t n) {
-  put8(s, __builtin_bswap64(v) >> (64 - 8 * n), n);
+  s.put64(__builtin_bswap64(v) >> (64 - 8 * n), n);
 }
 // LEB128 (VarintUtils-inl.h:545-620): the first 8 bytes of the encoding are
 // the 7-bit groups spread into bytes plus continuation bits, no loop
@@ -321,9 +320,9 @@ __device__ __forceinline__ void put_varint(Sink& s, uint64_t v) {
   x = (x & 0x007f007f007f007full) | ((x & 0x3f803f803f803f80ull) << 1);
   if (len <= 8) {
     x |= 0x8080808080808080ull & ((1ull << (8 * (len - 1))) - 1);
-    put8(s, x, len);
+    s.put64(x, len);
   } else {
-    put8(s, x | 0x8080808080808080ull, 8);
+    s.put64(x | 0x8080808080808080ull, 8);
     const uint32_t b8 = (uint32_t)((v >> 56) & 0x7f), b9 = (uint32_t)(v >> 63);
     s.put(len == 10 ? (b8 | 0x80u | (b9 << 8)) : b8, len - 8);
   }
@@ -344,7 +343,7 @@ __device__ __forceinline__ void put_bytes(Sink& s, const uint8_t* __restrict__ s
     for (uint32_t i = 0; i < 8; ++i) v[i] = i < need ? w[i] : 0u;
 #pragma unroll
     for (uint32_t i = 0; i < 8; ++i) {
-      if (i < need && left) {
+      if (i < need) {
         const uint32_t take = 4 - sh < left ? 4 - sh : left;
         s.put(v[i] >> (8 * sh), take);
         left -= take;
@@ -523,11 +522,7 @@ __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uin
   if (r < nrec) {
     const uint8_t* rec = rtile + rsh + r * S;
     if (fits && rel + sz <= sm.lds_end) {
-#ifdef TGPU_LDS_BYTE_SINK
-      ByteSink w(otile + osh + (uint32_t)rel);
-#else
-      WordSink w((uint32_t*)otile, osh + (uint32_t)rel);
-#endif
+      OrSink w((uint32_t*)otile, osh + (uint32_t)rel);
       program_emit(P, rec, a.sbase, a.lbase, w);
     } else if (tile_base + rel + sz <= a.cap) {
       emit_to_hbm(P, rec, a.sbase, a.lbase, gtile + rel);
