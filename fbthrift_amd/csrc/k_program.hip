@@ -74,17 +74,30 @@ __global__ __launch_bounds__(256) void general_decode_list_kernel(DecodeArgs a,
 
 }  // namespace
 
-// LDS wire tile of the indexed decode: the batch's mean tile + 30 % + 1 KiB
-// headroom (A/B winner over a fixed 26 KiB, profiles/r01_kbench_prog.log;
-// TGPU_PROG_DECODE=2: + 12 % + 512 B); a tile beyond it takes the general
-// decoder.
-uint32_t program_decode_wire_cap(const DecodeArgs& a) {
-  int capmode = 1;
-  if (const char* e = getenv("TGPU_PROG_DECODE")) capmode = atoi(e);
-  const double mean = (double)a.in_len / (double)(a.n ? a.n : 1);
-  const double want = capmode == 2 ? 1.12 * kPT * mean + 512.0 : 1.3 * kPT * mean + 1024.0;
-  uint32_t cap = (uint32_t)(want < 4096.0 ? 4096.0 : (want > 40960.0 ? 40960.0 : want));
-  return (cap + 15) & ~15u;
+// LDS wire tile of the indexed decode, sized for occupancy: the kernel is
+// latency-bound, so the cap is the largest that still lets the most
+// workgroups share a CU while holding a tile of >= 1.04 x the batch's mean
+// tile + 256 B (the rare larger tile takes the general decoder); within that,
+// at most 1.12 x mean + 512 B. (A/B on MI355X, tools/kbench_prog.py: config 3
+// 1.64 -> 1.45 ms going from the old fixed 1.3 x mean + 1 KiB to 5
+// workgroups/CU.) TGPU_PROG_DECODE="factor,pad" overrides the upper bound.
+uint32_t program_decode_wire_cap(const DecodeArgs& a, uint32_t rec_size) {
+  double factor = 1.12, pad = 512.0;
+  if (const char* e = getenv("TGPU_PROG_DECODE")) sscanf(e, "%lf,%lf", &factor, &pad);
+  const double mean = (double)a.in_len / (double)(a.n ? a.n : 1) * kPT;
+  const double lo = 1.04 * mean + 256.0, hi = std::max(factor * mean + pad, lo);
+  const uint32_t rt = (kPT * rec_size + 16 + 15) & ~15u;
+  double cap = hi;
+  for (uint32_t w = 8; w >= 1; --w) {
+    // wire bytes that fit w workgroups (the region is whole 4 KiB staging rounds)
+    const double room = std::floor((163840.0 / w - rt) / 4096.0) * 4096.0 - 32.0;
+    if (room >= lo) {
+      cap = std::min(room, hi);
+      break;
+    }
+  }
+  cap = cap < 4096.0 ? 4096.0 : (cap > 40960.0 ? 40960.0 : cap);
+  return ((uint32_t)cap) & ~15u;
 }
 
 uint32_t program_decode_lds(uint32_t wire_cap, uint32_t rec_size) {
@@ -95,7 +108,7 @@ hipError_t launch_program_decode(const DecodeArgs& a, const VProgram* d_prog, ui
                                  uint64_t* irregular, unsigned long long* n_irregular,
                                  hipStream_t stream, const JitKernels* jit) {
   if (a.n == 0) return hipSuccess;
-  const uint32_t cap = program_decode_wire_cap(a);
+  const uint32_t cap = program_decode_wire_cap(a, rec_size);
   const uint64_t tiles = (a.n + kPT - 1) / kPT;
   const uint32_t lds = program_decode_lds(cap, rec_size);
   if (jit) return jit_launch_decode(jit, a, tiles, cap, lds, irregular, n_irregular, stream);

@@ -142,7 +142,8 @@ hipError_t launch_program_encode(const EncodeArgs& a, const VProgram* d_prog,
     e = launch_scan_tiles(a.block_sums, tiles, part, &a.res->total_bytes, a.offs + a.n, stream);
   if (e != hipSuccess || size_only) return e;
   const uint32_t lds = rt + kOutCap + 32;
-  if (jit) return jit_launch_encode(jit, true, a, tiles, lds, stream);
+  // the compiled write kernel reads records from HBM: output tile only
+  if (jit) return jit_launch_encode(jit, true, a, tiles, kOutCap + 32, stream);
   hipLaunchKernelGGL(program_write_kernel, dim3((uint32_t)tiles), dim3(kET), lds, stream, a,
                      d_prog);
   return hipGetLastError();

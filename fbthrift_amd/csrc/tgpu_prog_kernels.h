@@ -90,6 +90,7 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
     const uint32_t nvec = (uint32_t)((t1 - t0) + sh + 15) >> 4;
     // LDS DMA (global_load_lds_dwordx4): the bytes go HBM -> LDS without
     // registers; lanes past the tile re-read its last vector into the slack
+    // (measured faster than masking them off)
     const uint32_t wave = threadIdx.x >> 6;
     for (uint32_t k = 0; k * kPT < nvec; ++k) {
       const uint32_t i = k * kPT + threadIdx.x;
@@ -454,12 +455,13 @@ __device__ __forceinline__ void size_tile(const EncodeArgs& a, const PP& P, uint
                                           uint8_t* smem, unsigned long long* part) {
   const uint64_t r0 = (uint64_t)blockIdx.x * kET;
   const uint32_t nrec = (uint32_t)min((uint64_t)kET, a.n - r0);
+  const uint8_t* recs = smem;
   const uint32_t sh = stage_records(a.recs, r0, nrec, S, smem);
   __syncthreads();
   unsigned long long sz = 0;
   if (threadIdx.x < nrec) {
     bool ok = true;
-    sz = program_size(P, smem + sh + threadIdx.x * S, a.lbase, ok);
+    sz = program_size(P, recs + sh + threadIdx.x * S, a.lbase, ok);
     if (!ok) atomicMin(&a.res->first_fail, (unsigned long long)(r0 + threadIdx.x));
     a.offs[r0 + threadIdx.x] = sz;
   }
@@ -488,9 +490,22 @@ __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uin
                                            uint8_t* smem, EncodeShared& sm) {
   const uint64_t r0 = (uint64_t)blockIdx.x * kET;
   const uint32_t nrec = (uint32_t)min((uint64_t)kET, a.n - r0);
-  uint8_t* rtile = smem;
-  uint8_t* otile = smem + enc_record_region(S);
-  const uint32_t rsh = stage_records(a.recs, r0, nrec, S, rtile);
+  // compiled programs read their record's members straight from HBM (the
+  // unrolled loads issue together; no LDS record tile, so 6 instead of 4
+  // workgroups fit a CU: config 3 encode -9 %, config 4 -21 %); the
+  // interpreter's op-by-op loads need the LDS-staged tile
+  uint8_t* rtile;
+  uint8_t* otile;
+  uint32_t rsh;
+  if constexpr (PP::kStatic) {
+    rtile = (uint8_t*)a.recs + r0 * S;
+    otile = smem;
+    rsh = 0;
+  } else {
+    rtile = smem;
+    otile = smem + enc_record_region(S);
+    rsh = stage_records(a.recs, r0, nrec, S, rtile);
+  }
   const uint32_t r = threadIdx.x;
   const unsigned long long sz = r < nrec ? a.offs[r0 + r] : 0;
   unsigned long long tile_total;
