@@ -663,7 +663,7 @@ template <class PP>
 __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, uint64_t j,
                                              uint8_t* lds, uint32_t entry, TileLane& L,
                                              uint32_t& sh, uint32_t& first, uint32_t* E, int* flag,
-                                             uint32_t* first_lane, uint32_t* fs_p) {
+                                             uint32_t* first_lane, uint32_t* fs_p, uint8_t* cmask) {
   const uint64_t lo = chunk_lo(a, j);
   const uint64_t hi_abs = chunk_hi(a, j);
   const uint8_t* g = a.in + lo;
@@ -682,6 +682,43 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
   const uint32_t k = threadIdx.x;
   const uint32_t sub_lo = sh + k * kSub;
   const uint32_t sub_hi = sub_lo + kSub < thi ? sub_lo + kSub : thi;
+  // candidate starts of the whole tile, one bit per byte, computed
+  // cooperatively: thread t owns 8-byte groups t, t + 256, ... (consecutive
+  // threads read consecutive LDS words: no bank conflicts, where one slice
+  // per lane read words 16 apart — 32-way conflicts). A candidate is a byte
+  // equal to the program's first header byte (h0) preceded by its STOP byte:
+  // every record ends with STOP, so every record start but the range's first
+  // is preceded by it (a necessary condition: it only prunes; for the mixed
+  // schema, whose four int headers all equal h0, it removes ~3 of 4).
+  {
+    const VOp o0 = P.op(0);
+    const uint32_t h0 = o0.kind == VOP_CONST ? (o0.hdr & 0xff) : 0x100;
+    const VOp ol = P.op(P.n_ops() - 1);
+    const uint32_t stop =
+        (ol.kind == VOP_CONST && ol.hdr_len) ? ((ol.hdr >> (8 * (ol.hdr_len - 1))) & 0xff) : 0x100;
+    const uint32_t ngroups = (thi + 7) >> 3;
+    for (uint32_t g = threadIdx.x; g < ngroups; g += kTileLanes) {
+      const uint32_t base = g << 3;
+      uint64_t m = 0x8080808080808080ull;
+      const uint64_t w = src.win8(base);
+      if (h0 < 0x100) {
+        const uint64_t x = w ^ (h0 * 0x0101010101010101ull);
+        m = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
+      }
+      if (stop < 0x100) {
+        // byte i of y = the byte before position base + i
+        const uint64_t y = (base ? src.win8(base - 1) : (w << 8)) ^ (stop * 0x0101010101010101ull);
+        uint64_t z = (y - 0x0101010101010101ull) & ~y & 0x8080808080808080ull;
+        if (!base) z |= 0x80ull;  // position 0: predecessor not staged
+        // the range's first byte has no predecessor inside the range
+        if (j == 0 && sh >= base && sh < base + 8) z |= 0x80ull << (8 * (sh - base));
+        m &= z;
+      }
+      cmask[g] = (uint8_t)((((m >> 7) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
+    }
+    for (uint32_t g = ngroups + threadIdx.x; g < ngroups + 9; g += kTileLanes) cmask[g] = 0;
+  }
+  __syncthreads();
   L.s = kNoPos;
   L.e = kNoPos;
   L.c = 0;
@@ -693,54 +730,25 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
       L.e = entry;
     }
   } else if (sub_lo < thi) {
-    // candidates: bytes equal to the first header byte that survive
-    // quick_reject (divergent but cheap); the chain from a candidate runs
-    // outside the search so all lanes of the wave run it together
-    const VOp o0 = P.op(0);
-    const uint32_t h0 = o0.kind == VOP_CONST ? (o0.hdr & 0xff) : 0x100;
-    // every record ends with its STOP byte, so every record start but the
-    // range's first is preceded by it: candidates are h0 bytes after a STOP
-    // byte (a necessary condition — it only prunes; for the mixed schema,
-    // whose four int headers all equal h0, it removes ~3 of 4 candidates)
-    const VOp ol = P.op(P.n_ops() - 1);
-    const uint32_t stop =
-        (ol.kind == VOP_CONST && ol.hdr_len) ? ((ol.hdr >> (8 * (ol.hdr_len - 1))) & 0xff) : 0x100;
-    // bytes of the slice equal to h0, all eight 8-byte groups loaded at once
-    uint64_t mk[kSub / 8];
+    // this lane's slice [sub_lo, sub_hi) as 64 candidate bits (cmask);
+    // candidates that survive quick_reject are chained in order (divergent
+    // but cheap); the chain runs outside the search so all lanes of the
+    // wave run it together
+    const uint32_t g0 = sub_lo >> 3, off = sub_lo & 7;
+    uint64_t lo8 = 0;
 #pragma unroll
-    for (uint32_t i = 0; i < kSub / 8; ++i) {
-      const uint32_t base = sub_lo + 8 * i;
-      uint64_t m = 0;
-      if (base < sub_hi) {
-        m = 0x8080808080808080ull;
-        if (h0 < 0x100) {
-          const uint64_t x = src.win8(base) ^ (h0 * 0x0101010101010101ull);
-          m = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
-        }
-        if (stop < 0x100 && base > 0) {
-          const uint64_t y = src.win8(base - 1) ^ (stop * 0x0101010101010101ull);
-          uint64_t z = (y - 0x0101010101010101ull) & ~y & 0x8080808080808080ull;
-          // the range's first byte has no predecessor inside the range
-          if (j == 0 && sh >= base && sh < base + 8) z |= 0x80ull << (8 * (sh - base));
-          m &= z;
-        }
-      }
-      mk[i] = m;
-    }
-    uint32_t from = sub_lo;
+    for (uint32_t i = 0; i < 8; ++i) lo8 |= (uint64_t)cmask[g0 + i] << (8 * i);
+    uint64_t cm = (lo8 >> off) | (off ? ((uint64_t)cmask[g0 + 8] << (64 - off)) : 0);
+    if (sub_hi - sub_lo < 64) cm &= (1ull << (sub_hi - sub_lo)) - 1;
     bool need = true;
     while (need) {
       uint32_t cand = kNoPos;
-#pragma unroll
-      for (uint32_t i = 0; i < kSub / 8; ++i) {
-        uint64_t m = mk[i];
-        while (m && cand == kNoPos) {
-          const uint32_t c = sub_lo + 8 * i + ((uint32_t)__builtin_ctzll(m) >> 3);
-          m &= m - 1;
-          if (c < from || c >= sub_hi) continue;
-          if (quick_reject(P, src, c)) continue;
-          cand = c;
-        }
+      while (cm) {
+        const uint32_t c = sub_lo + (uint32_t)__builtin_ctzll(cm);
+        cm &= cm - 1;
+        if (quick_reject(P, src, c)) continue;
+        cand = c;
+        break;
       }
       if (cand == kNoPos) break;  // no record start in this slice
       TileLane t;
@@ -748,8 +756,6 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
       if (t.c) {
         L = t;
         need = false;
-      } else {
-        from = cand + 1;
       }
     }
   }
@@ -801,6 +807,7 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
 }
 
 struct IndexTileShared {
+  uint8_t cmask[kTile / 8 + 16];  // candidate bits of the tile (one per byte)
   uint32_t E[kTileLanes];
   int flag;
   uint32_t first_lane, fs;
@@ -819,7 +826,7 @@ __device__ __forceinline__ void index_spec_tile(const IndexArgs& a, const PP& P,
   TileLane L;
   uint32_t sh, first;
   const bool ok = tile_resolve(a, P, j, lds, ent, L, sh, first, sm.E, &sm.flag, &sm.first_lane,
-                               &sm.fs);
+                               &sm.fs, sm.cmask);
   if (threadIdx.x == 0) sm.csum = 0;
   __syncthreads();
   if (ok && first != kNoPos) atomicAdd(&sm.csum, (unsigned long long)L.c);
@@ -858,7 +865,7 @@ __device__ __forceinline__ void index_spec_tile(const IndexArgs& a, const PP& P,
 // a record the program cannot store (list arena overflow) is queued for the
 // general decoder. This removes the decode pass's second read of the wire
 // and of the index.
-constexpr uint32_t kRecTileBytes = 18 * 1024;
+constexpr uint32_t kRecTileBytes = 16 * 1024;  // keeps the fused tile kernel at 4 workgroups/CU
 
 template <bool kDecode, class PP>
 __device__ __forceinline__ void index_emit_tile(const IndexArgs& a, const PP& P, uint8_t* lds,
@@ -891,7 +898,8 @@ __device__ __forceinline__ void index_emit_tile(const IndexArgs& a, const PP& P,
     ok = true;
     __syncthreads();
   } else {
-    ok = tile_resolve(a, P, j, lds, ent, L, sh, first, sm.E, &sm.flag, &sm.first_lane, &sm.fs);
+    ok = tile_resolve(a, P, j, lds, ent, L, sh, first, sm.E, &sm.flag, &sm.first_lane, &sm.fs,
+                      sm.cmask);
   }
   const uint64_t b = a.base[j];
   if (!ok) {
