@@ -47,6 +47,7 @@ struct tgpu_context {
 };
 
 namespace tgpu {
+bool schema_has_lists(const tgpu_schema* s) { return s->has_lists; }
 void* context_host_pipe(tgpu_context* c) {
   if (!c->host_pipe) c->host_pipe = host_pipe_create();
   return c->host_pipe;

@@ -8,12 +8,13 @@
 // directions and the CUs all busy). The bulk rate is bounded by PCIe, not
 // by the kernels: DESIGN.md §6.1 has the measured numbers.
 //
-// Scope: schemas whose records have a fixed canonical Binary length (the
+// The chunk pipeline needs records of a fixed canonical Binary length (the
 // fixed-layout path: BASELINE configs 1/2), where chunk boundaries are known
 // without parsing. A chunk whose decode does not end exactly on its boundary
 // (a non-canonical record changed the lengths, or a malformed record) is
 // redone with the whole rest of the stream resident, so results and errors
-// are exactly the single-call ones.
+// are exactly the single-call ones. Variable-length streams (no lists) take
+// that resident path from the start: copy in, fused index + decode, copy out.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -216,7 +217,10 @@ int tgpu_decode_host(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
   }
   const uint64_t L = tgpu_schema_fixed_wire_size(schema, protocol);
   const uint32_t S = tgpu_schema_record_size(schema);
-  if (!L) {
+  // variable-length records without lists: one resident decode (below) of
+  // the whole stream; string spans index the host stream like the device's.
+  // Lists would need a host list arena in the ABI: not supported here.
+  if (!L && schema_has_lists(schema)) {
     set_status(st, TGPU_ERR_UNSUPPORTED, 0, 0);
     return TGPU_ERR_UNSUPPORTED;
   }
@@ -228,7 +232,7 @@ int tgpu_decode_host(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
   const uint64_t chunk = chunk_records ? chunk_records : kDefaultChunk;
   PinGuard pin_in(h_in, in_len), pin_out(h_records, n * S);
   // the pipelined part: whole records the stream holds at the canonical length
-  const uint64_t fast_n = std::min<uint64_t>(n, in_len / L);
+  const uint64_t fast_n = L ? std::min<uint64_t>(n, in_len / L) : 0;
   uint64_t bad = ~0ull, done = 0;
   int rc = TGPU_OK;
   if (fast_n)

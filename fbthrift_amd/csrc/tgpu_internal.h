@@ -316,6 +316,7 @@ hipError_t launch_size_offsets(const EncodeArgs& a, uint64_t n_blocks, hipStream
 void* host_pipe_create();
 void host_pipe_destroy(void* pipe);
 void* context_host_pipe(tgpu_context* ctx);  // created on first use, owned by ctx
+bool schema_has_lists(const tgpu_schema* schema);
 
 // ---- stream indexer (k_index.hip) launchers
 uint64_t index_chunk_bytes(uint64_t span, bool tiles);

@@ -311,8 +311,10 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema,
  * the PCIe rate. Host buffers may be pinned (fastest) or pageable (pinned in
  * place for the call). Blocking; results and status exactly as for
  * tgpu_decode_batch / tgpu_encode_batch on the whole batch.
- * Scope: schemas with a fixed canonical Binary record length
- * (tgpu_schema_fixed_wire_size != 0); others -> TGPU_ERR_UNSUPPORTED.
+ * Scope: tgpu_encode_host needs a fixed canonical Binary record length
+ * (tgpu_schema_fixed_wire_size != 0); tgpu_decode_host also takes
+ * variable-length schemas without lists (decoded resident in one pass; string
+ * spans are offsets into host_in). Others -> TGPU_ERR_UNSUPPORTED.
  */
 int tgpu_decode_host(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
                      const void* host_in, uint64_t in_len, uint64_t n_records,

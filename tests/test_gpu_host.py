@@ -98,3 +98,29 @@ def test_host_encode_bad_bool_and_overflow(gpu):
     out, st, size = BinarySerializer.serialize_host(gs, rec[: 2000 * rec.size // n], 2000, out,
                                                     chunk=300)
     assert st.code == 21 and st.record == 1000 and size == 1000 * L  # TGPU_ERR_OUTPUT_OVERFLOW
+
+
+def test_host_decode_variable_length(gpu):
+    """Compact {4 x i32, 2 x string} stream in host memory (no index): records
+    equal the oracle's, string spans index the host stream; a schema with
+    lists is refused (no host list arena in the ABI)."""
+    import helpers
+
+    from fbthrift_amd.serializer import CompactSerializer, GpuSchema
+
+    table = datagen.SCHEMAS["mixed"]
+    schema = Schema.from_table(table)
+    n = 50_000
+    vals = datagen.flatten_values(table, [datagen.gen_mixed(i) for i in range(n)])
+    rec, sarena, _ = helpers.pack(schema, vals, n)
+    st, wire, offs = oracle.encode(schema, 2, rec, n, sarena)
+    assert st.code == 0
+    gs = GpuSchema(schema)
+    back, st, nd, cons = CompactSerializer.deserialize_host(
+        gs, np.frombuffer(wire, np.uint8).copy(), n)
+    ost, orec, _, ond, ocons = oracle.decode(schema, 2, wire, n)
+    assert st.as_tuple() == ost.as_tuple() and (nd, cons) == (ond, ocons) == (n, len(wire))
+    assert np.array_equal(back, orec)
+    ng = GpuSchema(Schema.from_table(datagen.SCHEMAS["nested"]))
+    _, st, _, _ = CompactSerializer.deserialize_host(ng, np.zeros(100, np.uint8), 1)
+    assert st.code == 22  # TGPU_ERR_UNSUPPORTED
