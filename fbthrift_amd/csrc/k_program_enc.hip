@@ -149,4 +149,15 @@ hipError_t launch_program_encode(const EncodeArgs& a, const VProgram* d_prog,
   return hipGetLastError();
 }
 
+hipError_t launch_program_write_fixed(const EncodeArgs& a, const VProgram* d_prog,
+                                      hipStream_t stream, const JitKernels* jit) {
+  if (a.n == 0) return hipSuccess;
+  const uint64_t tiles = (a.n + kET - 1) / kET;
+  const uint32_t rt = prog::enc_record_region(a.rec_size);
+  if (jit) return jit_launch_encode(jit, true, a, tiles, kOutCap + 32, stream);
+  hipLaunchKernelGGL(program_write_kernel, dim3((uint32_t)tiles), dim3(kET), rt + kOutCap + 32,
+                     stream, a, d_prog);
+  return hipGetLastError();
+}
+
 }  // namespace tgpu

@@ -421,6 +421,15 @@ const JitKernels* schema_jit(const tgpu_schema* s, int protocol, int group, uint
   return jit_kernels(s->prog[protocol], s->device, group, records, bytes, false);
 }
 
+// Fixed-layout Binary schemas: the compiled program kernels instead of the
+// word-gather plan kernels (TGPU_FIXED_PATH=jit; A/B).
+const JitKernels* fixed_jit(const tgpu_schema* s, int protocol, int group, uint64_t n) {
+  const char* e = getenv("TGPU_FIXED_PATH");
+  if (!e || strcmp(e, "jit") != 0) return nullptr;
+  if (!s->has_prog[protocol] || 256ull * s->tmpl.wire_len > 24 * 1024) return nullptr;
+  return jit_kernels(s->prog[protocol], s->device, group, n, 0, false);
+}
+
 DevSchema dev_schema(const tgpu_schema* s) {
   return DevSchema{s->d_structs, s->d_fields, (uint32_t)s->structs.size(),
                    (uint32_t)s->fields.size()};
@@ -759,7 +768,13 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   if (protocol == TGPU_PROTOCOL_BINARY && schema->fixed_binary &&
       n * schema->tmpl.wire_len <= out_capacity) {
     fixed = schema->tmpl.wire_len;
-    if (e == hipSuccess && schema->has_plan && ((uintptr_t)records & 7) == 0)
+    const JitKernels* fj = fixed_jit(schema, protocol, JIT_ENCODE, n);
+    if (e == hipSuccess && fj) {
+      EncodeArgs f = a;
+      f.fixed_len = fixed;
+      f.offs = out_offsets;
+      e = launch_program_write_fixed(f, schema->d_prog[protocol], s, fj);
+    } else if (e == hipSuccess && schema->has_plan && ((uintptr_t)records & 7) == 0)
       e = launch_plan_binary_encode(&schema->plan, schema->d_plan, a.recs, n, a.out, out_offsets,
                                     ctx->d_res, s);
     else if (e == hipSuccess)
@@ -895,7 +910,13 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   if (n && protocol == TGPU_PROTOCOL_BINARY && schema->fixed_binary && !offsets &&
       in_len >= n * (uint64_t)schema->tmpl.wire_len) {
     fixed = schema->tmpl.wire_len;
-    if (e == hipSuccess && schema->has_plan && ((uintptr_t)records & 7) == 0)
+    const JitKernels* fj = fixed_jit(schema, protocol, JIT_DECODE, n);
+    if (e == hipSuccess && fj) {
+      DecodeArgs f = a;
+      f.fixed_len = fixed;
+      e = launch_program_decode(f, schema->d_prog[protocol], a.rec_size, ctx->d_irr,
+                                &ctx->d_res->n_irregular, s, fj);
+    } else if (e == hipSuccess && schema->has_plan && ((uintptr_t)records & 7) == 0)
       e = launch_plan_binary_decode(&schema->plan, schema->d_plan, a.in, n, a.recs, ctx->d_res, s);
     else if (e == hipSuccess)
       e = launch_fixed_binary_decode(&schema->tmpl, schema->d_tmpl, a.in, n, a.recs, ctx->d_res,

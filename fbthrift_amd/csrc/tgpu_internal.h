@@ -171,6 +171,8 @@ struct DecodeArgs {
   uint32_t rec_size;
   int check_index;  // offsets were supplied by the caller: verify lengths
   DevResult* res;
+  uint64_t fixed_len;  // program decode of a fixed-layout stream: record i at i * fixed_len
+                       // (offs unused; a non-canonical record latches first_irregular)
 };
 
 struct EncodeArgs {
@@ -186,6 +188,7 @@ struct EncodeArgs {
   unsigned long long* scan_part;  // scan_tiles_parts(tiles) partial sums
   uint32_t rec_size;
   DevResult* res;
+  uint64_t fixed_len;  // program write of a fixed-layout schema: record i at i * fixed_len
 };
 
 // ---- stream indexer (k_index.hip) -------------------------------------------
@@ -311,6 +314,10 @@ hipError_t launch_program_encode(const EncodeArgs& a, const VProgram* d_prog,
                                  unsigned long long* part, bool size_only, hipStream_t stream,
                                  const JitKernels* jit);
 hipError_t launch_size_offsets(const EncodeArgs& a, uint64_t n_blocks, hipStream_t stream);
+// Fixed-layout schemas through the compiled program kernels (a.fixed_len set):
+// no size pass; offsets (when a.offs) are i * fixed_len.
+hipError_t launch_program_write_fixed(const EncodeArgs& a, const VProgram* d_prog,
+                                      hipStream_t stream, const JitKernels* jit);
 
 // ---- host-memory pipeline (tgpu_host.cpp) -------------------------------------
 void* host_pipe_create();

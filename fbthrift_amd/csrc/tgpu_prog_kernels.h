@@ -80,7 +80,8 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
   uint8_t* rtile = smem + decode_wire_region(wire_cap);
   const uint64_t r0 = (uint64_t)blockIdx.x * kPT;
   const uint32_t nrec = (uint32_t)min((uint64_t)kPT, a.n - r0);
-  const uint64_t t0 = a.offs[r0], t1 = a.offs[r0 + nrec];
+  const uint64_t L = a.fixed_len;
+  const uint64_t t0 = L ? r0 * L : a.offs[r0], t1 = L ? (r0 + nrec) * L : a.offs[r0 + nrec];
   const bool tile_ok = t1 >= t0 && t1 <= a.in_len && (t1 - t0) + 16 <= wire_cap;
   uint32_t sh = 0;
   if (tile_ok) {
@@ -114,7 +115,7 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
     uint8_t* rec = rtile + osh + r * S;
     bool ok = tile_ok;
     if (ok) {
-      const uint64_t s = a.offs[r0 + r], e = a.offs[r0 + r + 1];
+      const uint64_t s = L ? t0 + r * L : a.offs[r0 + r], e = L ? s + L : a.offs[r0 + r + 1];
       ok = s >= t0 && e >= s && e <= t1;
       if (ok) {
         const Ctx c{t0 - sh, a.arena, a.arena_cap, a.string_limit, a.container_limit};
@@ -125,8 +126,12 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
       }
     }
     if (!ok) {
-      const unsigned long long k = atomicAdd(nirr, 1ull);
-      irr[k] = r0 + r;
+      if (L) {  // positions past it are unknown: the serial reader takes over
+        atomicMin(&a.res->first_irregular, (unsigned long long)(r0 + r));
+      } else {
+        const unsigned long long k = atomicAdd(nirr, 1ull);
+        irr[k] = r0 + r;
+      }
     }
   }
   __syncthreads();
@@ -507,10 +512,20 @@ __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uin
     rsh = stage_records(a.recs, r0, nrec, S, rtile);
   }
   const uint32_t r = threadIdx.x;
-  const unsigned long long sz = r < nrec ? a.offs[r0 + r] : 0;
-  unsigned long long tile_total;
-  const unsigned long long rel = block_exscan256(sz, sm.part, &tile_total);
-  const unsigned long long tile_base = a.block_sums[blockIdx.x];
+  unsigned long long sz, tile_total, rel, tile_base;
+  if (a.fixed_len) {
+    // fixed layout: every record is fixed_len bytes; the size pass only
+    // validates (validate_bool -> first_fail)
+    sz = r < nrec ? a.fixed_len : 0;
+    tile_total = (unsigned long long)nrec * a.fixed_len;
+    rel = (unsigned long long)r * a.fixed_len;
+    tile_base = r0 * a.fixed_len;
+    if (a.offs && r == 0 && r0 + nrec == a.n) a.offs[a.n] = a.n * a.fixed_len;
+  } else {
+    sz = r < nrec ? a.offs[r0 + r] : 0;
+    rel = block_exscan256(sz, sm.part, &tile_total);
+    tile_base = a.block_sums[blockIdx.x];
+  }
   uint8_t* gtile = a.out + tile_base;
   const uint32_t osh = (uint32_t)((uintptr_t)gtile & 15);
   {  // zero the part of the output tile the records will OR into
@@ -524,7 +539,7 @@ __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uin
   bool fits = false;
   if (r < nrec) {
     const unsigned long long start = tile_base + rel;
-    a.offs[r0 + r] = start;
+    if (a.offs) a.offs[r0 + r] = start;
     if (start + sz > a.cap) {
       atomicMin(&a.res->first_fail, (unsigned long long)(r0 + r));
       atomicMin(&sm.lds_end, (unsigned int)min(rel, (unsigned long long)kOutCap));
@@ -536,6 +551,11 @@ __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uin
   __syncthreads();
   if (r < nrec) {
     const uint8_t* rec = rtile + rsh + r * S;
+    if (a.fixed_len) {  // the validation the size pass does otherwise (validate_bool)
+      bool ok = true;
+      (void)program_size(P, rec, a.lbase, ok);
+      if (!ok) atomicMin(&a.res->first_fail, (unsigned long long)(r0 + r));
+    }
     if (fits && rel + sz <= sm.lds_end) {
       OrSink w((uint32_t*)otile, osh + (uint32_t)rel);
       program_emit(P, rec, a.sbase, a.lbase, w);
