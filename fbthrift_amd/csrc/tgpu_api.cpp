@@ -127,7 +127,9 @@ int validate(const tgpu_struct_desc* s, uint32_t ns, const tgpu_field_desc* f, u
     const tgpu_field_desc& fd = f[sd.first_field + k];
     for (uint32_t j = 0; j < k; ++j)
       if (f[sd.first_field + j].id == fd.id) return TGPU_ERR_INVALID_ARGUMENT;
-    if (fd.qualifier > TGPU_OPTIONAL) return TGPU_ERR_UNSUPPORTED;
+    if (fd.qualifier > TGPU_TERSE) return TGPU_ERR_UNSUPPORTED;
+    // a terse struct's emptiness is its fields' (thrift::empty): not supported
+    if (fd.qualifier == TGPU_TERSE && fd.ttype == TGPU_T_STRUCT) return TGPU_ERR_UNSUPPORTED;
     if (fd.isset_offset >= sd.size) return TGPU_ERR_INVALID_ARGUMENT;
     uint32_t sz;
     if (is_scalar(fd.ttype)) {

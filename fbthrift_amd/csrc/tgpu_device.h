@@ -642,6 +642,17 @@ __device__ __forceinline__ void write_scalar(Writer& w, uint32_t t, const uint8_
   }
 }
 
+// op::isEmpty of a terse member (Clear.h:98-127): scalars by identity with
+// the intrinsic default (all bits zero), strings/containers by length.
+__device__ __forceinline__ bool terse_empty(const tgpu_field_desc& f, const uint8_t* m) {
+  if (is_scalar(f.ttype)) {
+    uint32_t any = 0;
+    for (uint32_t b = 0; b < scalar_size(f.ttype); ++b) any |= m[b];
+    return any == 0;
+  }
+  return ((const tgpu_span*)m)->length == 0;
+}
+
 struct WriteFrame {
   uint32_t si;
   uint32_t obj;
@@ -667,6 +678,7 @@ __device__ void write_record(Writer& w, const DevSchema& sc, const uint8_t* rec,
     const uint8_t* obj = rec + fr.obj;
     if (f.qualifier == TGPU_OPTIONAL && !obj[f.isset_offset]) continue;
     const uint8_t* m = obj + f.member_offset;
+    if (f.qualifier == TGPU_TERSE && terse_empty(f, m)) continue;
     if (P == TGPU_PROTOCOL_BINARY) {
       w.put(f.ttype);
       w.put_be((uint16_t)f.id, 2);

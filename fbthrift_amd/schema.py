@@ -21,12 +21,15 @@ NP_SCALAR = {T_BOOL: np.uint8, T_BYTE: np.int8, T_I16: np.int16, T_I32: np.int32
 SPAN = np.dtype([("offset", "<u8"), ("length", "<u4"), ("reserved", "<u4")])
 
 OPTIONAL = 1
+TERSE = 2  # @thrift.TerseWrite: written only when not empty (op::isEmpty)
 
 
 class Field:
-    def __init__(self, id, ttype, elem_ttype=0, optional=False, struct=None, name=None):
+    def __init__(self, id, ttype, elem_ttype=0, optional=False, struct=None, name=None,
+                 qualifier=None):
         self.id, self.ttype, self.elem_ttype = int(id), int(ttype), int(elem_ttype)
-        self.optional, self.struct = bool(optional), struct
+        self.qualifier = int(qualifier) if qualifier is not None else (OPTIONAL if optional else 0)
+        self.optional, self.struct = self.qualifier == OPTIONAL, struct
         self.name = name or "f%d" % self.id
 
 
@@ -108,7 +111,7 @@ class Schema:
             for k, f in enumerate(s.fields):
                 fd = fields[j]
                 fd.id, fd.ttype, fd.elem_ttype = f.id, f.ttype, f.elem_ttype
-                fd.qualifier = OPTIONAL if f.optional else 0
+                fd.qualifier = f.qualifier
                 fd.member_offset = self.member[(si, k)]
                 fd.isset_offset = self.isset[(si, k)]
                 fd.struct_index = self._index[id(f.struct)] if f.ttype == T_STRUCT else -1
@@ -146,7 +149,7 @@ class Schema:
         for si, rows in enumerate(table):
             for fid, tt, et, q, sub in rows:
                 structs[si].fields.append(
-                    Field(fid, tt, et, optional=q == OPTIONAL,
+                    Field(fid, tt, et, qualifier=q,
                           struct=structs[sub] if tt == T_STRUCT else None))
         return cls(structs[0])
 

@@ -95,6 +95,11 @@ enum tgpu_ttype {
 enum tgpu_qualifier {
   TGPU_UNQUALIFIED = 0, /* always written, isset set on read */
   TGPU_OPTIONAL = 1,    /* written only when isset != 0 */
+  /* @thrift.TerseWrite: written only when not empty (op::isEmpty,
+     thrift/lib/cpp2/op/detail/Clear.h:98-127 via fields.whisker:84): a
+     scalar whose bits are not all zero (-0.0 is written), a non-empty
+     string/list/set; read like an unqualified field. Not for struct fields. */
+  TGPU_TERSE = 2,
 };
 
 /*

@@ -135,6 +135,20 @@ uint32_t scalar_size(uint8_t t) {
   }
 }
 
+// op::isEmpty (thrift/lib/cpp2/op/detail/Clear.h:98-127) of a terse member:
+// scalars compare identical (bitwise) to the intrinsic default, so -0.0 is
+// not empty; strings and containers are empty when they have no elements.
+bool terse_empty(const tgpu_field_desc& f, const uint8_t* m) {
+  if (is_scalar(f.ttype)) {
+    for (uint32_t b = 0; b < scalar_size(f.ttype); ++b)
+      if (m[b]) return false;
+    return true;
+  }
+  uint32_t len;
+  std::memcpy(&len, m + 8, 4);  // tgpu_span.length
+  return len == 0;
+}
+
 // ================================================================ readers ===
 struct Limits {
   int32_t string_limit = 0, container_limit = 0, max_depth = 12000, height = 0;
@@ -696,6 +710,7 @@ struct BinaryWriter {
       const tgpu_field_desc& f = ec.sc->f[sd.first_field + k];
       if (f.qualifier == TGPU_OPTIONAL && !obj[f.isset_offset]) continue;
       const uint8_t* m = obj + f.member_offset;
+      if (f.qualifier == TGPU_TERSE && terse_empty(f, m)) continue;  // fields.whisker:84
       s.put(f.ttype);  // writeFieldBegin: byte type + BE i16 id
       s.putBE((uint16_t)f.id, 2);
       if (is_scalar(f.ttype)) {
@@ -751,6 +766,7 @@ struct CompactWriter {
       const tgpu_field_desc& f = ec.sc->f[sd.first_field + k];
       if (f.qualifier == TGPU_OPTIONAL && !obj[f.isset_offset]) continue;
       const uint8_t* m = obj + f.member_offset;
+      if (f.qualifier == TGPU_TERSE && terse_empty(f, m)) continue;  // fields.whisker:84
       if (f.ttype == TGPU_T_BOOL) {  // bool value rides in the header
         const uint8_t b = load_bool_checked(m, s.pos);
         fieldHeader(b ? 1 : 2, f.id, last);
