@@ -91,7 +91,8 @@ int layout_struct(tgpu_struct_desc* s, uint32_t ns, tgpu_field_desc* f, uint32_t
     uint32_t sz, al;
     if (is_scalar(fd.ttype)) {
       sz = al = scalar_size(fd.ttype);
-    } else if (fd.ttype == TGPU_T_STRING || fd.ttype == TGPU_T_LIST || fd.ttype == TGPU_T_SET) {
+    } else if (fd.ttype == TGPU_T_STRING || fd.ttype == TGPU_T_LIST || fd.ttype == TGPU_T_SET ||
+               fd.ttype == TGPU_T_MAP) {
       sz = 16;
       al = 8;
     } else if (fd.ttype == TGPU_T_STRUCT) {
@@ -138,6 +139,10 @@ int validate(const tgpu_struct_desc* s, uint32_t ns, const tgpu_field_desc* f, u
       sz = 16;
     } else if (fd.ttype == TGPU_T_LIST || fd.ttype == TGPU_T_SET) {
       if (!is_scalar(fd.elem_ttype)) return TGPU_ERR_UNSUPPORTED;
+      has_lists = true;
+      sz = 16;
+    } else if (fd.ttype == TGPU_T_MAP) {
+      if (!is_scalar(fd.elem_ttype) || !is_scalar(fd.val_ttype)) return TGPU_ERR_UNSUPPORTED;
       has_lists = true;
       sz = 16;
     } else if (fd.ttype == TGPU_T_STRUCT) {

@@ -502,13 +502,17 @@ __device__ void read_list(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8
       *(tgpu_span*)m = sp;
       int32_t i = 0;
       for (; i < n; ++i) {
+        // read first: a truncated stream fails as the reader does, and an
+        // element that was read always fits an arena of the documented size
         const uint64_t at = aoff + (uint64_t)i * es;
+        uint8_t tmp[8];
+        Pr::read_scalar(r, f.elem_ttype, tmp);
+        if (!r.ok()) break;
         if (at + es > arena_cap) {
           r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
           break;
         }
-        Pr::read_scalar(r, f.elem_ttype, arena + at);
-        if (!r.ok()) break;
+        for (uint32_t b = 0; b < es; ++b) arena[at + b] = tmp[b];
       }
       if (!r.ok()) {
         // leftover elements are value-initialized (protocol_methods.h:441-451)
@@ -518,6 +522,65 @@ __device__ void read_list(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8
           for (uint32_t b = 0; b < es; ++b) arena[at + b] = 0;
         }
       }
+    }
+  }
+  if (r.ok()) r.ascend();
+}
+
+// protocol_methods<map>::read (protocol_methods.h:640-677): reset to empty,
+// readMapBegin, skip_n on a key/value type mismatch of a non-empty map,
+// canReadNElements(n, {k, v}) = n * 2 bytes left, then the pairs in wire
+// order, packed {key, value} at the arena offset. A failing pair is not
+// inserted (EncodeHelpers.h:188-205): the map keeps the pairs before it.
+// Pair i's slot ends within scale x (the end of pair i on the wire), so a
+// pair that was read always fits an arena of the documented size.
+template <int P>
+__device__ void read_map(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8_t* arena,
+                         uint64_t arena_cap) {
+  using Pr = Proto<P>;
+  tgpu_span sp{0, 0, 0};
+  *(tgpu_span*)m = sp;
+  uint32_t rk = 0, rv = 0;
+  int32_t n = 0;
+  Pr::map_begin(r, rk, rv, n);
+  if (!r.ok()) return;
+  if (n > 0 && (rk != f.elem_ttype || rv != f.val_ttype)) {
+    // skip_n(protocol, n, {k, v}) with depth 0 (Protocol.h:317-344)
+    if (0 >= r.max_depth) return r.fail(TGPU_ERR_DEPTH_LIMIT, r.pos);
+    const uint32_t fk = Pr::fixed_in_container(rk), fv = Pr::fixed_in_container(rv);
+    if (fk && fv) {
+      r.skip_bytes((uint64_t)(fk + fv) * (uint32_t)n);
+    } else {
+      for (int32_t i = 0; i < n && r.ok(); ++i) {
+        skip<P>(r, rk, 1);
+        if (r.ok()) skip<P>(r, rv, 1);
+      }
+    }
+  } else {
+    if ((r.end - r.pos) / 2 < (uint64_t)(uint32_t)n) return r.fail(TGPU_ERR_TRUNCATED, r.pos);
+    const uint32_t ks = scalar_size(f.elem_ttype), ps = ks + scalar_size(f.val_ttype);
+    const uint64_t aoff = Pr::kArenaScale * r.pos;
+    const bool discard = !arena && arena_cap == kDiscardArena;
+    if (n > 0 && !arena && !discard) return r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
+    int32_t i = 0;
+    for (; i < n; ++i) {
+      uint8_t pr[16];
+      Pr::read_scalar(r, f.elem_ttype, pr);
+      if (!r.ok()) break;
+      Pr::read_scalar(r, f.val_ttype, pr + ks);
+      if (!r.ok()) break;
+      if (discard) continue;
+      const uint64_t at = aoff + (uint64_t)i * ps;
+      if (at + ps > arena_cap) {
+        r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
+        break;
+      }
+      for (uint32_t b = 0; b < ps; ++b) arena[at + b] = pr[b];
+    }
+    if (i > 0 && !discard) {
+      sp.offset = aoff;
+      sp.length = (uint32_t)i;
+      *(tgpu_span*)m = sp;
     }
   }
   if (r.ok()) r.ascend();
@@ -572,6 +635,8 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, uint8_
       fr.fidx = (uint32_t)hit;
       st[sp++] = ReadFrame{(uint32_t)f.struct_index, fr.obj + f.member_offset, 0, 0};
       continue;  // isset set when the nested STOP is reached
+    } else if (f.ttype == TGPU_T_MAP) {
+      read_map<P>(r, f, m, arena, arena_cap);
     } else {
       read_list<P>(r, f, m, arena, arena_cap);
     }
@@ -706,6 +771,26 @@ __device__ void write_record(Writer& w, const DevSchema& sc, const uint8_t* rec,
     } else if (f.ttype == TGPU_T_STRUCT) {
       if (sp == kMaxSchemaDepth) return w.fail(TGPU_ERR_UNSUPPORTED, w.pos);
       st[sp++] = WriteFrame{(uint32_t)f.struct_index, fr.obj + f.member_offset, 0, 0};
+    } else if (f.ttype == TGPU_T_MAP) {
+      // writeMapBegin (BinaryProtocol-inl.h:69-80, CompactProtocol-inl.h:182-201)
+      const tgpu_span sp_ = *(const tgpu_span*)m;
+      if (sp_.length > 0x7fffffffu) return w.fail(TGPU_ERR_WRITE_SIZE_LIMIT, w.pos);
+      if (P == TGPU_PROTOCOL_BINARY) {
+        w.put(f.elem_ttype);
+        w.put(f.val_ttype);
+        w.put_be(sp_.length, 4);
+      } else if (sp_.length == 0) {
+        w.put(0);
+      } else {
+        w.varint(sp_.length);
+        w.put((ttype_to_ctype(f.elem_ttype) << 4) | ttype_to_ctype(f.val_ttype));
+      }
+      const uint32_t ks = scalar_size(f.elem_ttype), ps = ks + scalar_size(f.val_ttype);
+      const uint8_t* e = lbase + sp_.offset;
+      for (uint32_t i = 0; i < sp_.length && w.ok(); ++i) {
+        write_scalar<P>(w, f.elem_ttype, e + (uint64_t)i * ps);
+        write_scalar<P>(w, f.val_ttype, e + (uint64_t)i * ps + ks);
+      }
     } else {  // list / set of scalars
       const tgpu_span sp_ = *(const tgpu_span*)m;
       if (sp_.length > 0x7fffffffu) return w.fail(TGPU_ERR_WRITE_SIZE_LIMIT, w.pos);

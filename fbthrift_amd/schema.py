@@ -13,7 +13,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import (T_BOOL, T_BYTE, T_DOUBLE, T_FLOAT, T_I16, T_I32, T_I64, T_LIST,
-                   T_SET, T_STRING, T_STRUCT)
+                   T_MAP, T_SET, T_STRING, T_STRUCT)
 
 SCALAR = {T_BOOL: 1, T_BYTE: 1, T_I16: 2, T_I32: 4, T_FLOAT: 4, T_I64: 8, T_DOUBLE: 8}
 NP_SCALAR = {T_BOOL: np.uint8, T_BYTE: np.int8, T_I16: np.int16, T_I32: np.int32,
@@ -26,8 +26,9 @@ TERSE = 2  # @thrift.TerseWrite: written only when not empty (op::isEmpty)
 
 class Field:
     def __init__(self, id, ttype, elem_ttype=0, optional=False, struct=None, name=None,
-                 qualifier=None):
+                 qualifier=None, val_ttype=0):
         self.id, self.ttype, self.elem_ttype = int(id), int(ttype), int(elem_ttype)
+        self.val_ttype = int(val_ttype)  # T_MAP: value type (elem_ttype = key type)
         self.qualifier = int(qualifier) if qualifier is not None else (OPTIONAL if optional else 0)
         self.optional, self.struct = self.qualifier == OPTIONAL, struct
         self.name = name or "f%d" % self.id
@@ -74,7 +75,7 @@ class Schema:
             for k, f in enumerate(s.fields):
                 if f.ttype in SCALAR:
                     sz = al = SCALAR[f.ttype]
-                elif f.ttype in (T_STRING, T_LIST, T_SET):
+                elif f.ttype in (T_STRING, T_LIST, T_SET, T_MAP):
                     sz, al = 16, 8
                 elif f.ttype == T_STRUCT:
                     sub = self._index[id(f.struct)]
@@ -112,6 +113,7 @@ class Schema:
                 fd = fields[j]
                 fd.id, fd.ttype, fd.elem_ttype = f.id, f.ttype, f.elem_ttype
                 fd.qualifier = f.qualifier
+                fd.val_ttype = f.val_ttype
                 fd.member_offset = self.member[(si, k)]
                 fd.isset_offset = self.isset[(si, k)]
                 fd.struct_index = self._index[id(f.struct)] if f.ttype == T_STRUCT else -1
@@ -126,7 +128,7 @@ class Schema:
             names.append(f.name)
             if f.ttype in SCALAR:
                 formats.append(NP_SCALAR[f.ttype])
-            elif f.ttype in (T_STRING, T_LIST, T_SET):
+            elif f.ttype in (T_STRING, T_LIST, T_SET, T_MAP):
                 formats.append(SPAN)
             else:
                 formats.append(self.dtype(self._index[id(f.struct)]))
@@ -144,13 +146,16 @@ class Schema:
     @classmethod
     def from_table(cls, table):
         """Builds a Schema from the tests/golden manifest form: a list of
-        structs, each a list of [id, ttype, elem_ttype, qualifier, struct_index]."""
+        structs, each a list of [id, ttype, elem_ttype, qualifier, struct_index]
+        (+ val_ttype for a map)."""
         structs = [Struct("S%d" % i, []) for i in range(len(table))]
         for si, rows in enumerate(table):
-            for fid, tt, et, q, sub in rows:
+            for row in rows:
+                fid, tt, et, q, sub = row[:5]
                 structs[si].fields.append(
                     Field(fid, tt, et, qualifier=q,
-                          struct=structs[sub] if tt == T_STRUCT else None))
+                          struct=structs[sub] if tt == T_STRUCT else None,
+                          val_ttype=row[5] if len(row) > 5 else 0))
         return cls(structs[0])
 
 

@@ -106,8 +106,11 @@ enum tgpu_qualifier {
  * One field of a struct, in IDL declaration order (= serialization order,
  * thrift/compiler/generate/t_whisker_generator.cc:231-236).
  *   ttype        T_BOOL..T_FLOAT scalar, T_STRING (binary/string), T_STRUCT,
- *                T_LIST or T_SET of a scalar element type.
- *   elem_ttype   element type for T_LIST/T_SET (scalar), else 0.
+ *                T_LIST or T_SET of a scalar element type, T_MAP of scalar
+ *                key and value types.
+ *   elem_ttype   element type for T_LIST/T_SET, key type for T_MAP (scalar),
+ *                else 0.
+ *   val_ttype    value type for T_MAP (scalar), else 0.
  *   struct_index nested struct (index into the schema's struct table) for
  *                T_STRUCT, else -1.
  */
@@ -116,7 +119,8 @@ typedef struct tgpu_field_desc {
   uint8_t ttype;
   uint8_t elem_ttype;
   uint8_t qualifier;
-  uint8_t reserved0[3];
+  uint8_t val_ttype;
+  uint8_t reserved0[2];
   uint32_t member_offset;
   uint32_t isset_offset;
   int32_t struct_index;
@@ -132,7 +136,7 @@ typedef struct tgpu_struct_desc {
 } tgpu_struct_desc;
 
 /*
- * Device form of a string/binary or list/set member (16 bytes, align 8).
+ * Device form of a string/binary, list/set or map member (16 bytes, align 8).
  * Decode: a string's `offset` is relative to the decoded input stream `in`
  *         (zero-copy view, ExternalBufferSharing::SHARE_EXTERNAL_BUFFER,
  *         thrift/lib/cpp2/protocol/Protocol.h:96-99); a list's `offset` is
@@ -140,6 +144,13 @@ typedef struct tgpu_struct_desc {
  *         little-endian layout. Empty strings/lists decode to {0, 0}.
  * Encode: a string's `offset` is relative to `string_base`, a list's to
  *         `list_base`; `length` is bytes (string) or elements (list).
+ * Map:    `length` = pairs, in wire order, packed {key, value} (stride key
+ *         size + value size, no padding) from `offset`. Inserting the
+ *         pairs in order with emplace (the first of equal keys wins) gives
+ *         the reference's std::map (deserialize_known_length_map,
+ *         thrift/lib/cpp2/op/detail/EncodeHelpers.h:188-205); a map whose
+ *         read fails keeps the pairs read before the failure. Encode writes
+ *         the pairs in the order given (sorted keys = std::map's order).
  */
 typedef struct tgpu_span {
   uint64_t offset;

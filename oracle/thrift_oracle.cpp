@@ -541,9 +541,13 @@ void readList(R& r, const tgpu_field_desc& f, uint8_t* member, DecodeCtx& dc) {
     int32_t i = 0;
     try {
       for (; i < n; ++i) {
+        // read first: truncation fails as the reader does (the arena always
+        // holds an element that was read when sized as documented)
         const uint64_t at = aoff + (uint64_t)i * es;
+        uint8_t tmp[8];
+        r.readScalar(f.elem_ttype, tmp);
         if (at + es > dc.arena_cap) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
-        r.readScalar(f.elem_ttype, dc.arena + at);
+        std::memcpy(dc.arena + at, tmp, es);
       }
     } catch (const OErr&) {
       // protocol_methods.h:441-451: leftover elements are value-initialized
@@ -556,6 +560,50 @@ void readList(R& r, const tgpu_field_desc& f, uint8_t* member, DecodeCtx& dc) {
     }
   }
   r.height.ascend();  // readListEnd
+}
+
+template <class R>
+void readMap(R& r, const tgpu_field_desc& f, uint8_t* member, DecodeCtx& dc) {
+  // protocol_methods<map>::read (protocol_methods.h:640-677); the member is
+  // reset first (deserialize_field.whisker:44-47). Pairs in wire order, packed
+  // {key, value} at the arena offset. deserialize_known_length_map
+  // (EncodeHelpers.h:188-205) inserts a pair only once both reads succeeded:
+  // a failing map keeps the complete pairs before the failure.
+  tgpu_span span{0, 0, 0};
+  std::memcpy(member, &span, sizeof(span));
+  uint8_t kv[2];
+  int32_t n;
+  r.readMapBegin(kv[0], kv[1], n);
+  if (n > 0 && (kv[0] != f.elem_ttype || kv[1] != f.val_ttype)) {
+    r.skip_n((uint32_t)n, kv, 2, 0);
+  } else {
+    if (!r.c.canAdvance((uint64_t)(uint32_t)n * 2)) fail(TGPU_ERR_TRUNCATED, r.c.pos);
+    const uint32_t ks = scalar_size(f.elem_ttype), ps = ks + scalar_size(f.val_ttype);
+    const uint64_t aoff = R::kArenaScale * r.c.pos;
+    if (n > 0 && !dc.arena) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
+    int32_t i = 0;
+    try {
+      for (; i < n; ++i) {
+        uint8_t pr[16];
+        r.readScalar(f.elem_ttype, pr);
+        r.readScalar(f.val_ttype, pr + ks);
+        const uint64_t at = aoff + (uint64_t)i * ps;
+        if (at + ps > dc.arena_cap) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
+        std::memcpy(dc.arena + at, pr, ps);
+      }
+    } catch (const OErr&) {
+      if (i > 0) {
+        span = tgpu_span{aoff, (uint32_t)i, 0};
+        std::memcpy(member, &span, sizeof(span));
+      }
+      throw;
+    }
+    if (n > 0) {
+      span = tgpu_span{aoff, (uint32_t)n, 0};
+      std::memcpy(member, &span, sizeof(span));
+    }
+  }
+  r.height.ascend();  // readMapEnd
 }
 
 template <class R>
@@ -593,6 +641,8 @@ void readStruct(R& r, uint32_t si, uint8_t* obj, DecodeCtx& dc) {
       readStruct(r, (uint32_t)f->struct_index, m, dc);  // merges into member
     } else if (f->ttype == TGPU_T_LIST || f->ttype == TGPU_T_SET) {
       readList(r, *f, m, dc);
+    } else if (f->ttype == TGPU_T_MAP) {
+      readMap(r, *f, m, dc);
     }
     obj[f->isset_offset] = 1;  // __isset.set(idx, true)
   }
@@ -704,6 +754,16 @@ struct BinaryWriter {
       default: s.putBE(ld<uint64_t>(p), 8); break;
     }
   }
+  // encodeMapElements: key then value per pair, in the given order
+  // (protocol_methods.h:693-701).
+  void pairs(const EncodeCtx& ec, const tgpu_field_desc& f, const tgpu_span& sp) {
+    const uint32_t ks = scalar_size(f.elem_ttype), ps = ks + scalar_size(f.val_ttype);
+    const uint8_t* e = ec.lbase + sp.offset;
+    for (uint32_t i = 0; i < sp.length; ++i) {
+      scalar(f.elem_ttype, e + (uint64_t)i * ps);
+      scalar(f.val_ttype, e + (uint64_t)i * ps + ks);
+    }
+  }
   void structure(const EncodeCtx& ec, uint32_t si, const uint8_t* obj) {
     const tgpu_struct_desc& sd = ec.sc->s[si];
     for (uint32_t k = 0; k < sd.num_fields; ++k) {
@@ -722,6 +782,13 @@ struct BinaryWriter {
         s.putBytes(ec.sbase + sp.offset, sp.length);
       } else if (f.ttype == TGPU_T_STRUCT) {
         structure(ec, (uint32_t)f.struct_index, m);
+      } else if (f.ttype == TGPU_T_MAP) {  // writeMapBegin (BinaryProtocol-inl.h:69-80)
+        const tgpu_span sp = ld<tgpu_span>(m);
+        if (sp.length > 0x7fffffffu) fail(TGPU_ERR_WRITE_SIZE_LIMIT, s.pos);  // checked_container_size
+        s.put(f.elem_ttype);
+        s.put(f.val_ttype);
+        s.putBE(sp.length, 4);
+        pairs(ec, f, sp);
       } else {  // list/set: writeListBegin + writeArithmeticVector (BinaryProtocol.cpp:95-117)
         const tgpu_span sp = ld<tgpu_span>(m);
         if (sp.length > 0x7fffffffu) fail(TGPU_ERR_WRITE_SIZE_LIMIT, s.pos);
@@ -759,6 +826,16 @@ struct CompactWriter {
       default: s.putBE(ld<uint64_t>(p), 8); break;  // double, BE (v2)
     }
   }
+  // encodeMapElements: key then value per pair, in the given order
+  // (protocol_methods.h:693-701).
+  void pairs(const EncodeCtx& ec, const tgpu_field_desc& f, const tgpu_span& sp) {
+    const uint32_t ks = scalar_size(f.elem_ttype), ps = ks + scalar_size(f.val_ttype);
+    const uint8_t* e = ec.lbase + sp.offset;
+    for (uint32_t i = 0; i < sp.length; ++i) {
+      scalar(f.elem_ttype, e + (uint64_t)i * ps);
+      scalar(f.val_ttype, e + (uint64_t)i * ps + ks);
+    }
+  }
   void structure(const EncodeCtx& ec, uint32_t si, const uint8_t* obj) {
     const tgpu_struct_desc& sd = ec.sc->s[si];
     int16_t last = 0;  // writeStructBegin pushes lastFieldId_ and resets it
@@ -782,6 +859,16 @@ struct CompactWriter {
         s.putBytes(ec.sbase + sp.offset, sp.length);
       } else if (f.ttype == TGPU_T_STRUCT) {
         structure(ec, (uint32_t)f.struct_index, m);
+      } else if (f.ttype == TGPU_T_MAP) {  // writeMapBegin (:182-201)
+        const tgpu_span sp = ld<tgpu_span>(m);
+        if (sp.length > 0x7fffffffu) fail(TGPU_ERR_WRITE_SIZE_LIMIT, s.pos);
+        if (sp.length == 0) {
+          s.put(0);
+        } else {
+          s.varint(sp.length);
+          s.put((uint8_t)((ttypeToCType(f.elem_ttype) << 4) | ttypeToCType(f.val_ttype)));
+        }
+        pairs(ec, f, sp);
       } else {  // writeCollectionBegin (:209-224)
         const tgpu_span sp = ld<tgpu_span>(m);
         if (sp.length > 0x7fffffffu) fail(TGPU_ERR_WRITE_SIZE_LIMIT, s.pos);

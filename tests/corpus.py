@@ -149,9 +149,77 @@ def cases():
     goodc = W(C).field(I64, 1).i64(1).stop().bytes()
     badc = W(C).field(I64, 1).raw(b"\xff" * 10).stop().bytes()
     out.append(("compact_mid_failure", C, two, goodc * 7 + badc + goodc, 9, None, VARINT))
+    out += map_cases()
     return out
 
 
 def nested_record(proto, height, levels, ttype):
     import wire
     return wire.nested(proto, height, levels, ttype)
+
+
+MAP_SCHEMA = [[[1, MAP, I32, 0, -1, I64], [2, I32, 0, 0, -1]]]
+BMAP_SCHEMA = [[[1, MAP, BOOL, 0, -1, BYTE]]]
+
+
+def map_cases():
+    """protocol_methods<map>::read (protocol_methods.h:640-677) and
+    readMapBegin (BinaryProtocol-inl.h:439-451, CompactProtocol-inl.h:615-650)."""
+    out = []
+    for p, pn in ((B, "binary"), (C, "compact")):
+        def m(n, kt=I32, vt=I64, pairs=None):
+            w = W(p).field(MAP, 1).map_begin(kt, vt, n)
+            for k, v in (pairs if pairs is not None else [(j, -j) for j in range(n)]):
+                (w.i32 if kt == I32 else w.i64)(k)
+                (w.i64 if vt == I64 else w.i32)(v)
+            return w
+
+        full = m(5).field(I32, 2).i32(9).stop().bytes()
+        out.append(("%s_map_ok" % pn, p, MAP_SCHEMA, full, 1, None, OK))
+        out.append(("%s_map_empty" % pn, p, MAP_SCHEMA, m(0).field(I32, 2).i32(1).stop().bytes(),
+                    1, None, OK))
+        # key/value type mismatch of a non-empty map: skip_n, member left empty
+        mm = m(3, I64, I32).field(I32, 2).i32(4).stop().bytes()
+        out.append(("%s_map_type_mismatch" % pn, p, MAP_SCHEMA, mm, 1, None, OK))
+        # cut inside a pair: the map keeps the complete pairs (EncodeHelpers.h:188-205)
+        hdr = len(W(p).field(MAP, 1).map_begin(I32, I64, 5).bytes())
+        for cut in range(hdr, len(full) - 4):
+            code = TRUNC if cut - hdr < 10 else UNDERFLOW
+            out.append(("%s_map_cut_%d" % (pn, cut), p, MAP_SCHEMA, full[:cut], 1, None, code))
+        out.append(("%s_map_limit" % pn, p, MAP_SCHEMA, full, 1, (0, 4, 12000, 0), LIMIT))
+        out.append(("%s_map_limit_ok" % pn, p, MAP_SCHEMA, full, 1, (0, 5, 12000, 0), OK))
+        # each map counts as one level of nesting (descend in readMapBegin;
+        # generated struct reads do not descend): a map of maps under an
+        # unknown id, skipped with height 1
+        mm2 = W(p).field(MAP, 9).map_begin(I32, MAP, 1).i32(1).map_begin(I32, I32, 1) \
+            .i32(2).i32(3).field(I32, 2).i32(1).stop().bytes()
+        out.append(("%s_map_height" % pn, p, MAP_SCHEMA, mm2, 1, (0, 0, 12000, 1), DEPTH))
+        out.append(("%s_map_height_ok" % pn, p, MAP_SCHEMA, mm2, 1, (0, 0, 12000, 2), OK))
+        # skipped (unknown id) map
+        sk = W(p).field(MAP, 9).map_begin(I32, STR, 2).i32(1).string(b"ab").i32(2) \
+            .string(b"").field(I32, 2).i32(3).stop().bytes()
+        out.append(("%s_map_skipped" % pn, p, MAP_SCHEMA, sk, 1, None, OK))
+    # negative sizes
+    out.append(("binary_map_negative", B, MAP_SCHEMA,
+                b"\x0d\x00\x01\x08\x0a\xff\xff\xff\xff\x00", 1, None, NEG))
+    out.append(("compact_map_negative", C, MAP_SCHEMA,
+                b"\x1b" + varint(0x80000000) + b"\x56\x00", 1, None, NEG))
+    # canReadNElements(n, {k, v}): 2 bytes per pair must remain
+    out.append(("compact_map_cant_read", C, MAP_SCHEMA, b"\x1b\x05\x56" + b"\x00" * 9, 1, None,
+                TRUNC))
+    out.append(("compact_map_can_read", C, MAP_SCHEMA,
+                b"\x1b\x05\x56" + b"\x02\x01" * 5 + b"\x00", 1, None, OK))
+    # a key/value nibble >= 14 is a bad type (getType, CompactProtocol-inl.h:783-791)
+    out.append(("compact_map_bad_type", C, MAP_SCHEMA, b"\x1b\x01\x5e\x00\x00\x00", 1, None,
+                BADT))
+    # Compact empty map: no kv byte, whatever follows is the next field
+    out.append(("compact_map_empty_no_kv", C, MAP_SCHEMA, b"\x1b\x00\x15\x04\x00", 1, None,
+                OK))
+    # bools in maps: Binary rejects bytes >= 2, Compact takes == 1 as true
+    for v, code in ((1, OK), (2, BOOLV)):
+        wb = W(B).field(MAP, 1).map_begin(BOOL, BYTE, 1).byte(v).byte(7).stop().bytes()
+        out.append(("binary_map_bool_%d" % v, B, BMAP_SCHEMA, wb, 1, None, code))
+    for v in (1, 2, 0x42):
+        wc = W(C).field(MAP, 1).map_begin(BOOL, BYTE, 1).byte(v).byte(7).stop().bytes()
+        out.append(("compact_map_bool_%d" % v, C, BMAP_SCHEMA, wc, 1, None, OK))
+    return out

@@ -12,6 +12,7 @@ import numpy as np
 # TType values (thrift/lib/cpp/protocol/TType.h:31-51)
 T_BOOL, T_BYTE, T_DOUBLE, T_I16, T_I32, T_I64 = 2, 3, 4, 6, 8, 10
 T_STRING, T_STRUCT, T_LIST, T_SET, T_FLOAT = 11, 12, 15, 14, 19
+T_MAP = 13
 
 M64 = (1 << 64) - 1
 SEED = 0x1729
@@ -85,6 +86,15 @@ SCHEMAS = {
     ],
     # optional fields + ids that force Compact long-form headers (negative,
     # gaps > 15, descending declaration order).
+    # maps of scalars ([id, T_MAP, key type, qualifier, -1, value type]),
+    # nested in a struct field too; an optional map
+    "maps": [
+        [[1, T_MAP, T_I32, 0, -1, T_I64], [2, T_MAP, T_I16, 0, -1, T_DOUBLE],
+         [3, T_MAP, T_BOOL, 0, -1, T_BYTE], [4, T_I32, 0, 0, -1],
+         [5, T_MAP, T_I64, 1, -1, T_FLOAT], [6, T_STRUCT, 0, 0, 1],
+         [7, T_MAP, T_BYTE, 0, -1, T_BOOL]],
+        [[1, T_MAP, T_I32, 0, -1, T_I32], [2, T_I64, 0, 0, -1]],
+    ],
     "sparse": [[[5, T_I32, 0, 1, -1], [-3, T_I64, 0, 0, -1], [40, T_STRING, 0, 1, -1],
                 [300, T_BOOL, 0, 0, -1], [20, T_DOUBLE, 0, 1, -1], [21, T_I16, 0, 0, -1]]],
 }
@@ -185,6 +195,29 @@ def gen_sparse(i):
     ]
 
 
+def gen_maps(i):
+    """Pairs in wire order; keys may repeat (the wire allows it, the reader
+    keeps them all in the span form); sizes cross the 1-byte varint at 127."""
+    i8, i16, i32, i64, dbl, flt, strs = interesting()
+    r = [splitmix64_at(SEED + 21, 16 * i + k) for k in range(16)]
+    big = i % 50 == 7
+
+    def n(k, m):
+        return 130 if big and k == 0 else r[k] % m
+
+    m1 = [(s32(splitmix64_at(SEED + 22, 256 * i + j)) % 1000 - 500,
+           s64(splitmix64_at(SEED + 23, 256 * i + j))) for j in range(n(0, 20))]
+    m2 = [(i16[(i + j) % len(i16)], dbl[(i + 3 * j) % len(dbl)]) for j in range(n(1, 9))]
+    m3 = [(bool((r[5] >> j) & 1), i8[(i + j) % len(i8)]) for j in range(n(2, 3))]
+    m5 = ([(i64[(i + j) % len(i64)], flt[(i + j) % len(flt)]) for j in range(n(3, 6))]
+          if r[6] & 1 else None)
+    inner = [[(s32(splitmix64_at(SEED + 24, 64 * i + j)), j - 3) for j in range(n(4, 5))],
+             s64(r[7])]
+    m7 = [(s64(splitmix64_at(SEED + 25, 64 * i + j)) % 256 - 128, bool(j & 1))
+          for j in range(n(8, 4))]
+    return [m1, m2, m3, s32(r[9]), m5, inner, m7]
+
+
 ORIGINAL = [True, False, 50, 1200, 1300, 1600, 1.0, [0], b"def", [0]]
 UPDATED = [True, False, False, True, False, 50, 1100, 1200, 1300, 1400, 1500,
            1600, 1.0, b"abc", [0], [1], b"def", b"ghi", [0], [1]]
@@ -212,7 +245,8 @@ def flatten_values(schema, records):
         return v
 
     def walk(sidx, vals, prefix):
-        for k, (fid, ttype, elem, qual, sub) in enumerate(schema[sidx]):
+        for k, row in enumerate(schema[sidx]):
+            fid, ttype, elem, qual, sub = row[:5]
             v = vals[k] if vals is not None else None
             key = "%s%d" % (prefix, k)
             put(key + ".set", 0 if v is None else 1)
@@ -221,6 +255,12 @@ def flatten_values(schema, records):
             elif ttype == T_STRING:
                 put(key + ".len", 0 if v is None else len(v))
                 out.setdefault(key + ".data", []).extend(v or b"")
+            elif ttype == T_MAP:
+                put(key + ".count", 0 if v is None else len(v))
+                out.setdefault(key + ".keys", []).extend(
+                    [scalar_repr(elem, a) for a, _ in (v or [])])
+                out.setdefault(key + ".vals", []).extend(
+                    [scalar_repr(row[5], b) for _, b in (v or [])])
             elif ttype in (T_LIST, T_SET):
                 put(key + ".count", 0 if v is None else len(v))
                 out.setdefault(key + ".elems", []).extend(
@@ -253,8 +293,10 @@ def flatten_values(schema, records):
             arrays[key] = np.array(lst, dtype=np.uint32)
         elif kind == "data":
             arrays[key] = np.array(lst, dtype=np.uint8)
-        elif kind == "elems":
+        elif kind in ("elems", "keys"):
             arrays[key] = np.array(lst, dtype=dt[f[2]])
+        elif kind == "vals":
+            arrays[key] = np.array(lst, dtype=dt[f[5]])
         else:
             arrays[key] = np.array(lst, dtype=dt[f[1]])
     return arrays

@@ -74,6 +74,13 @@ def write_value(p, ttype, elem, sidx, schema, v):
         p.writeString(v)
     elif ttype == T_STRUCT:
         write_struct(p, schema, sidx, v)
+    elif ttype == T_MAP:
+        kt, vt = elem
+        p.writeMapBegin(kt, vt, len(v))
+        for a, b in v:
+            write_value(p, kt, 0, -1, schema, a)
+            write_value(p, vt, 0, -1, schema, b)
+        p.writeMapEnd()
     elif ttype in (T_LIST, T_SET):
         (p.writeListBegin if ttype == T_LIST else p.writeSetBegin)(elem, len(v))
         for e in v:
@@ -85,12 +92,13 @@ def write_value(p, ttype, elem, sidx, schema, v):
 
 def write_struct(p, schema, sidx, vals):
     p.writeStructBegin("S%d" % sidx)
-    for (fid, ttype, elem, qual, sub), v in zip(schema[sidx], vals):
+    for row, v in zip(schema[sidx], vals):
+        fid, ttype, elem, qual, sub = row[:5]
         if v is None:
             assert qual == 1
             continue
         p.writeFieldBegin("f", ttype, fid)
-        write_value(p, ttype, elem, sub, schema, v)
+        write_value(p, ttype, (elem, row[5]) if ttype == T_MAP else elem, sub, schema, v)
         p.writeFieldEnd()
     p.writeFieldStop()
     p.writeStructEnd()
@@ -122,6 +130,8 @@ CASES = [
     ("scalars_compact", "scalars", "compact", gen_scalars, 300),
     ("sparse_binary", "sparse", "binary", gen_sparse, 200),
     ("sparse_compact", "sparse", "compact", gen_sparse, 200),
+    ("maps_binary", "maps", "binary", gen_maps, 300),
+    ("maps_compact", "maps", "compact", gen_maps, 300),
     ("original_compact", "original", "compact", lambda i: ORIGINAL, 1),
     ("original_binary", "original", "binary", lambda i: ORIGINAL, 1),
     ("updated_compact", "updated", "compact", lambda i: UPDATED, 1),

@@ -12,7 +12,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, GOLDEN)
 
 from fbthrift_amd.schema import SCALAR, Schema  # noqa: E402
-from fbthrift_amd._lib import T_LIST, T_SET, T_STRING, T_STRUCT  # noqa: E402
+from fbthrift_amd._lib import T_LIST, T_MAP, T_SET, T_STRING, T_STRUCT  # noqa: E402
 
 PROTO = {"binary": 0, "compact": 2}
 ELEM_NP = {2: np.uint8, 3: np.int8, 6: np.int16, 8: np.int32, 10: np.int64, 4: np.uint64,
@@ -100,6 +100,18 @@ def pack(schema, values, n):
             el = values[key + ".elems"]
             larena.append(np.ascontiguousarray(el).view(np.uint8))
             lpos += int(cnt.sum()) * es
+        elif f.ttype == T_MAP:
+            # packed {key, value} pairs (the tgpu_span map form)
+            cnt = values[key + ".count"].astype(np.uint64)
+            ks, vs = SCALAR[f.elem_ttype], SCALAR[f.val_ttype]
+            tot = int(cnt.sum())
+            kb = np.ascontiguousarray(values[key + ".keys"]).view(np.uint8).reshape(tot, ks)
+            vb = np.ascontiguousarray(values[key + ".vals"]).view(np.uint8).reshape(tot, vs)
+            starts = lpos + (ks + vs) * np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.uint64)
+            arr[f.name]["offset"] = np.where(cnt > 0, starts, 0)
+            arr[f.name]["length"] = cnt
+            larena.append(np.concatenate([kb, vb], axis=1).reshape(-1))
+            lpos += tot * (ks + vs)
     s = np.concatenate(sarena) if sarena else np.zeros(0, np.uint8)
     l = np.concatenate(larena) if larena else np.zeros(0, np.uint8)
     return rec.view(np.uint8).reshape(-1), s, l
@@ -136,6 +148,15 @@ def unpack(schema, rec_bytes, n, wire, arena):
             parts = [ar[o:o + l * es] for o, l in zip(sp["offset"].tolist(), sp["length"].tolist())]
             el = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
             out[key + ".elems"] = el.view(ELEM_NP[f.elem_ttype])
+        elif f.ttype == T_MAP:
+            sp = arr[f.name]
+            ks, vs = SCALAR[f.elem_ttype], SCALAR[f.val_ttype]
+            out[key + ".count"] = sp["length"].astype(np.uint32)
+            parts = [ar[o:o + l * (ks + vs)] for o, l in
+                     zip(sp["offset"].tolist(), sp["length"].tolist())]
+            pr = (np.concatenate(parts) if parts else np.zeros(0, np.uint8)).reshape(-1, ks + vs)
+            out[key + ".keys"] = np.ascontiguousarray(pr[:, :ks]).view(ELEM_NP[f.elem_ttype]).reshape(-1)
+            out[key + ".vals"] = np.ascontiguousarray(pr[:, ks:]).view(ELEM_NP[f.val_ttype]).reshape(-1)
     return out
 
 
