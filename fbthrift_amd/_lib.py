@@ -22,7 +22,7 @@ CODES = {
     0: "OK", 1: "UNDERFLOW", 2: "INVALID_VARINT", 3: "BOOL_VALUE",
     4: "INVALID_SKIP_TYPE", 5: "TRUNCATED", 6: "NEGATIVE_SIZE", 7: "SIZE_LIMIT",
     8: "DEPTH_LIMIT", 9: "BAD_TYPE", 10: "INVALID_BOOL_WRITE",
-    11: "WRITE_SIZE_LIMIT", 20: "INDEX_MISMATCH", 21: "OUTPUT_OVERFLOW",
+    11: "WRITE_SIZE_LIMIT", 12: "UNION_MISSING_STOP", 20: "INDEX_MISMATCH", 21: "OUTPUT_OVERFLOW",
     22: "UNSUPPORTED", 23: "INVALID_ARGUMENT", 24: "HIP",
 }
 CODE = {v: k for k, v in CODES.items()}
@@ -38,7 +38,8 @@ class FieldDesc(ctypes.Structure):
 
 class StructDesc(ctypes.Structure):
     _fields_ = [("first_field", ctypes.c_uint32), ("num_fields", ctypes.c_uint32),
-                ("size", ctypes.c_uint32), ("align", ctypes.c_uint32)]
+                ("size", ctypes.c_uint32), ("align", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32)]
 
 
 class Limits(ctypes.Structure):
@@ -55,7 +56,7 @@ class Status(ctypes.Structure):
         return (self.code, self.exc_class, self.tproto_type, self.record, self.byte_offset)
 
 
-assert ctypes.sizeof(FieldDesc) == 24 and ctypes.sizeof(StructDesc) == 16
+assert ctypes.sizeof(FieldDesc) == 24 and ctypes.sizeof(StructDesc) == 20
 assert ctypes.sizeof(Status) == 32
 
 # Every symbol declared in include/thrift_gpu.h (checked by tests/test_abi.py).

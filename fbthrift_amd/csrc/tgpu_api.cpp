@@ -124,8 +124,11 @@ int validate(const tgpu_struct_desc* s, uint32_t ns, const tgpu_field_desc* f, u
   if ((uint64_t)sd.first_field + sd.num_fields > nf || sd.size == 0 || sd.align == 0 ||
       sd.size % sd.align)
     return TGPU_ERR_INVALID_ARGUMENT;
+  if (sd.flags & ~(uint32_t)TGPU_STRUCT_UNION) return TGPU_ERR_UNSUPPORTED;
   for (uint32_t k = 0; k < sd.num_fields; ++k) {
     const tgpu_field_desc& fd = f[sd.first_field + k];
+    if ((sd.flags & TGPU_STRUCT_UNION) && fd.qualifier != TGPU_UNQUALIFIED)
+      return TGPU_ERR_UNSUPPORTED;
     for (uint32_t j = 0; j < k; ++j)
       if (f[sd.first_field + j].id == fd.id) return TGPU_ERR_INVALID_ARGUMENT;
     if (fd.qualifier > TGPU_TERSE) return TGPU_ERR_UNSUPPORTED;
@@ -164,6 +167,7 @@ int validate(const tgpu_struct_desc* s, uint32_t ns, const tgpu_field_desc* f, u
 bool build_template(const tgpu_schema& sc, uint32_t si, uint32_t base, FixedTemplate& t,
                     uint32_t& wire) {
   const tgpu_struct_desc& sd = sc.structs[si];
+  if (sd.flags & TGPU_STRUCT_UNION) return false;
   for (uint32_t k = 0; k < sd.num_fields; ++k) {
     const tgpu_field_desc& fd = sc.fields[sd.first_field + k];
     if (fd.qualifier != TGPU_UNQUALIFIED) return false;
@@ -236,6 +240,7 @@ VOp make_op(uint8_t kind) {
 // each value's encoding.
 bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, VProgram& P) {
   const tgpu_struct_desc& sd = sc.structs[si];
+  if (sd.flags & TGPU_STRUCT_UNION) return false;
   int32_t prev = 0;
   for (uint32_t k = 0; k < sd.num_fields; ++k) {
     const tgpu_field_desc& f = sc.fields[sd.first_field + k];
@@ -375,6 +380,7 @@ void classify(int code, int32_t* exc, int32_t* tp) {
     case TGPU_OK: e = TGPU_EXC_NONE; break;
     case TGPU_ERR_UNDERFLOW: case TGPU_ERR_INVALID_VARINT: e = TGPU_EXC_OUT_OF_RANGE; break;
     case TGPU_ERR_BOOL_VALUE: case TGPU_ERR_INVALID_SKIP_TYPE: case TGPU_ERR_TRUNCATED:
+    case TGPU_ERR_UNION_MISSING_STOP:
       e = TGPU_EXC_PROTOCOL; t = 1; break;
     case TGPU_ERR_NEGATIVE_SIZE: e = TGPU_EXC_PROTOCOL; t = 2; break;
     case TGPU_ERR_SIZE_LIMIT: case TGPU_ERR_WRITE_SIZE_LIMIT: e = TGPU_EXC_PROTOCOL; t = 3; break;
@@ -562,6 +568,7 @@ const char* tgpu_code_name(int code) {
     case TGPU_ERR_BAD_TYPE: return "BAD_TYPE";
     case TGPU_ERR_INVALID_BOOL_WRITE: return "INVALID_BOOL_WRITE";
     case TGPU_ERR_WRITE_SIZE_LIMIT: return "WRITE_SIZE_LIMIT";
+    case TGPU_ERR_UNION_MISSING_STOP: return "UNION_MISSING_STOP";
     case TGPU_ERR_INDEX_MISMATCH: return "INDEX_MISMATCH";
     case TGPU_ERR_OUTPUT_OVERFLOW: return "OUTPUT_OVERFLOW";
     case TGPU_ERR_UNSUPPORTED: return "UNSUPPORTED";

@@ -465,7 +465,12 @@ struct ReadFrame {
   uint32_t obj;  // byte offset of the struct inside the record
   int32_t prev;  // Compact delta base
   uint32_t fidx; // field being read into (for isset after a nested struct)
+  uint32_t nread;  // fields read or skipped (a union takes one)
 };
+
+__device__ __forceinline__ void zero_bytes(uint8_t* p, uint32_t n) {
+  for (uint32_t b = 0; b < n; ++b) p[b] = 0;
+}
 
 template <int P>
 __device__ void read_list(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8_t* arena,
@@ -592,13 +597,17 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, uint8_
   using Pr = Proto<P>;
   ReadFrame st[kMaxSchemaDepth];
   int sp = 0;
-  st[sp++] = ReadFrame{0, 0, 0, 0};
+  st[sp++] = ReadFrame{0, 0, 0, 0, 0};
   while (sp > 0 && r.ok()) {
     ReadFrame& fr = st[sp - 1];
+    const tgpu_struct_desc sd = sc.s[fr.si];
+    const bool un = sd.flags & TGPU_STRUCT_UNION;
     uint32_t wt = 0;
     int32_t id = 0;
     if (!Pr::field_header(r, fr.prev, wt, id)) {
       if (!r.ok()) return;
+      // a union with no field is cleared (deserialize_union.whisker:26-28)
+      if (un && fr.nread == 0) zero_bytes(rec + fr.obj, sd.size);
       // STOP: struct done; mark the parent's field set
       --sp;
       if (sp > 0) {
@@ -608,8 +617,10 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, uint8_
       }
       continue;
     }
+    // a union's one field must be followed by STOP (throwUnionMissingStop)
+    if (un && fr.nread) return r.fail(TGPU_ERR_UNION_MISSING_STOP, r.pos);
+    ++fr.nread;
     fr.prev = id;
-    const tgpu_struct_desc sd = sc.s[fr.si];
     int32_t hit = -1;
     for (uint32_t k = 0; k < sd.num_fields; ++k) {
       if (sc.f[sd.first_field + k].id == id) {
@@ -623,6 +634,10 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, uint8_
     }
     const tgpu_field_desc f = sc.f[hit];
     uint8_t* m = rec + fr.obj + f.member_offset;
+    if (un) {  // field_ref().emplace(): a fresh member becomes active
+      zero_bytes(rec + fr.obj, sd.size);
+      rec[fr.obj + f.isset_offset] = 1;
+    }
     if (is_scalar(f.ttype)) {
       Pr::read_scalar(r, f.ttype, m);
     } else if (f.ttype == TGPU_T_STRING) {
@@ -633,7 +648,7 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, uint8_
     } else if (f.ttype == TGPU_T_STRUCT) {
       if (sp == kMaxSchemaDepth) return r.fail(TGPU_ERR_UNSUPPORTED, r.pos);
       fr.fidx = (uint32_t)hit;
-      st[sp++] = ReadFrame{(uint32_t)f.struct_index, fr.obj + f.member_offset, 0, 0};
+      st[sp++] = ReadFrame{(uint32_t)f.struct_index, fr.obj + f.member_offset, 0, 0, 0};
       continue;  // isset set when the nested STOP is reached
     } else if (f.ttype == TGPU_T_MAP) {
       read_map<P>(r, f, m, arena, arena_cap);
@@ -723,18 +738,38 @@ struct WriteFrame {
   uint32_t obj;
   uint32_t k;     // next field index within the struct
   int32_t last;   // Compact lastFieldId_
+  uint32_t end;   // one past the last field to write
 };
+
+// The fields a struct writes: all of them, or for a union its active member
+// only (serialize_union.whisker:52-66): the first whose isset byte is set.
+__device__ __forceinline__ WriteFrame write_frame(const DevSchema& sc, const uint8_t* rec,
+                                                  uint32_t si, uint32_t obj) {
+  const tgpu_struct_desc sd = sc.s[si];
+  WriteFrame w{si, obj, 0, 0, sd.num_fields};
+  if (sd.flags & TGPU_STRUCT_UNION) {
+    w.k = sd.num_fields;
+    for (uint32_t k = 0; k < sd.num_fields; ++k) {
+      if (rec[obj + sc.f[sd.first_field + k].isset_offset]) {
+        w.k = k;
+        w.end = k + 1;
+        break;
+      }
+    }
+  }
+  return w;
+}
 
 template <int P>
 __device__ void write_record(Writer& w, const DevSchema& sc, const uint8_t* rec,
                              const uint8_t* sbase, const uint8_t* lbase) {
   WriteFrame st[kMaxSchemaDepth];
   int sp = 0;
-  st[sp++] = WriteFrame{0, 0, 0, 0};
+  st[sp++] = write_frame(sc, rec, 0, 0);
   while (sp > 0 && w.ok()) {
     WriteFrame& fr = st[sp - 1];
     const tgpu_struct_desc sd = sc.s[fr.si];
-    if (fr.k == sd.num_fields) {
+    if (fr.k >= fr.end) {
       w.put(0);  // writeFieldStop (T_STOP / CT_STOP are both 0)
       --sp;
       continue;
@@ -770,7 +805,7 @@ __device__ void write_record(Writer& w, const DevSchema& sc, const uint8_t* rec,
       w.bytes(sbase + sp_.offset, sp_.length);
     } else if (f.ttype == TGPU_T_STRUCT) {
       if (sp == kMaxSchemaDepth) return w.fail(TGPU_ERR_UNSUPPORTED, w.pos);
-      st[sp++] = WriteFrame{(uint32_t)f.struct_index, fr.obj + f.member_offset, 0, 0};
+      st[sp++] = write_frame(sc, rec, (uint32_t)f.struct_index, fr.obj + f.member_offset);
     } else if (f.ttype == TGPU_T_MAP) {
       // writeMapBegin (BinaryProtocol-inl.h:69-80, CompactProtocol-inl.h:182-201)
       const tgpu_span sp_ = *(const tgpu_span*)m;

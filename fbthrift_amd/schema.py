@@ -35,8 +35,9 @@ class Field:
 
 
 class Struct:
-    def __init__(self, name, fields):
+    def __init__(self, name, fields, union=False):
         self.name, self.fields = name, list(fields)
+        self.union = bool(union)  # TGPU_STRUCT_UNION
 
 
 class Schema:
@@ -109,6 +110,7 @@ class Schema:
             structs[si].num_fields = len(s.fields)
             structs[si].size = self.size[si]
             structs[si].align = self.align[si]
+            structs[si].flags = 1 if s.union else 0
             for k, f in enumerate(s.fields):
                 fd = fields[j]
                 fd.id, fd.ttype, fd.elem_ttype = f.id, f.ttype, f.elem_ttype
@@ -147,10 +149,11 @@ class Schema:
     def from_table(cls, table):
         """Builds a Schema from the tests/golden manifest form: a list of
         structs, each a list of [id, ttype, elem_ttype, qualifier, struct_index]
-        (+ val_ttype for a map)."""
-        structs = [Struct("S%d" % i, []) for i in range(len(table))]
-        for si, rows in enumerate(table):
-            for row in rows:
+        (+ val_ttype for a map); a union is {"union": true, "fields": [...]}."""
+        structs = [Struct("S%d" % i, [], union=isinstance(e, dict) and e.get("union"))
+                   for i, e in enumerate(table)]
+        for si, e in enumerate(table):
+            for row in (e["fields"] if isinstance(e, dict) else e):
                 fid, tt, et, q, sub = row[:5]
                 structs[si].fields.append(
                     Field(fid, tt, et, qualifier=q,

@@ -127,13 +127,25 @@ typedef struct tgpu_field_desc {
   uint32_t reserved1;
 } tgpu_field_desc; /* 24 bytes */
 
+/* Struct flags. */
+enum tgpu_struct_flags {
+  /* A Thrift union (deserialize_union.whisker / serialize_union.whisker):
+     each member has its own slot and isset byte; the active member is the
+     one whose isset byte is set (at most one on read, the first set one is
+     written). Reading a member first clears the whole union (emplace), an
+     immediate STOP clears it (apache::thrift::clear), a second field is
+     TGPU_ERR_UNION_MISSING_STOP. Members must be unqualified. */
+  TGPU_STRUCT_UNION = 1,
+};
+
 /* A struct = a contiguous run of fields. Struct 0 is the record (root) type. */
 typedef struct tgpu_struct_desc {
   uint32_t first_field;
   uint32_t num_fields;
   uint32_t size;  /* sizeof(record), multiple of align */
   uint32_t align;
-} tgpu_struct_desc;
+  uint32_t flags; /* tgpu_struct_flags */
+} tgpu_struct_desc; /* 20 bytes */
 
 /*
  * Device form of a string/binary, list/set or map member (16 bytes, align 8).
@@ -183,6 +195,8 @@ enum tgpu_code {
   TGPU_ERR_SIZE_LIMIT = 7,       /* SIZE_LIMIT */
   TGPU_ERR_DEPTH_LIMIT = 8,      /* DEPTH_LIMIT */
   TGPU_ERR_BAD_TYPE = 9,         /* UNKNOWN: Compact "don't know what type" */
+  TGPU_ERR_UNION_MISSING_STOP = 12, /* INVALID_DATA: throwUnionMissingStop
+                                       (TProtocolException.cpp:23-27) */
   /* writer-side: the reference aborts the process (validate_bool,
      thrift/lib/cpp2/protocol/Protocol.h:126-163) or throws SIZE_LIMIT */
   TGPU_ERR_INVALID_BOOL_WRITE = 10,

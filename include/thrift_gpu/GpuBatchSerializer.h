@@ -139,9 +139,11 @@ inline void check(int rc, const char* what) {
 struct FieldSpec {
   int16_t id;
   uint8_t ttype;
-  uint8_t elem_ttype = 0;
+  uint8_t elem_ttype = 0;  /* list/set element, map key */
   bool optional = false;
   int32_t struct_index = -1;
+  uint8_t val_ttype = 0;   /* map value */
+  uint8_t qualifier = 0;   /* TGPU_TERSE etc.; `optional` wins when set */
 };
 
 /* Owns a tgpu_schema. Structs are given as lists of FieldSpec (struct 0 =
@@ -150,18 +152,23 @@ struct FieldSpec {
  * alignment, trailing isset bytes; strings/lists as tgpu_span). */
 class GpuSchema {
  public:
-  explicit GpuSchema(const std::vector<std::vector<FieldSpec>>& structs) {
-    for (const auto& s : structs) {
+  /* unions[i] marks struct i as a Thrift union (may be shorter than structs). */
+  explicit GpuSchema(const std::vector<std::vector<FieldSpec>>& structs,
+                     const std::vector<bool>& unions = {}) {
+    for (size_t i = 0; i < structs.size(); ++i) {
+      const auto& s = structs[i];
       tgpu_struct_desc d{};
       d.first_field = static_cast<uint32_t>(fields_.size());
       d.num_fields = static_cast<uint32_t>(s.size());
+      d.flags = (i < unions.size() && unions[i]) ? TGPU_STRUCT_UNION : 0u;
       structs_.push_back(d);
       for (const FieldSpec& f : s) {
         tgpu_field_desc fd{};
         fd.id = f.id;
         fd.ttype = f.ttype;
         fd.elem_ttype = f.elem_ttype;
-        fd.qualifier = f.optional ? TGPU_OPTIONAL : TGPU_UNQUALIFIED;
+        fd.val_ttype = f.val_ttype;
+        fd.qualifier = f.optional ? TGPU_OPTIONAL : f.qualifier;
         fd.struct_index = f.struct_index;
         fields_.push_back(fd);
       }

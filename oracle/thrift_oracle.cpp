@@ -31,7 +31,8 @@ void classify(int code, int32_t* exc, int32_t* tp) {
     case TGPU_ERR_INVALID_VARINT: e = TGPU_EXC_OUT_OF_RANGE; break;
     case TGPU_ERR_BOOL_VALUE:
     case TGPU_ERR_INVALID_SKIP_TYPE:
-    case TGPU_ERR_TRUNCATED: e = TGPU_EXC_PROTOCOL; t = 1; break;  // INVALID_DATA
+    case TGPU_ERR_TRUNCATED:
+    case TGPU_ERR_UNION_MISSING_STOP: e = TGPU_EXC_PROTOCOL; t = 1; break;  // INVALID_DATA
     case TGPU_ERR_NEGATIVE_SIZE: e = TGPU_EXC_PROTOCOL; t = 2; break;
     case TGPU_ERR_SIZE_LIMIT:
     case TGPU_ERR_WRITE_SIZE_LIMIT: e = TGPU_EXC_PROTOCOL; t = 3; break;
@@ -609,11 +610,20 @@ void readMap(R& r, const tgpu_field_desc& f, uint8_t* member, DecodeCtx& dc) {
 template <class R>
 void readStruct(R& r, uint32_t si, uint8_t* obj, DecodeCtx& dc) {
   const tgpu_struct_desc& sd = dc.sc->s[si];
+  // A union (deserialize_union.whisker:19-60): an immediate STOP clears it,
+  // one field (read or skipped), then the STOP is required.
+  const bool un = sd.flags & TGPU_STRUCT_UNION;
   int16_t prev = 0;
+  bool first = true;
   while (true) {
     uint8_t wt;
     int16_t id;
-    if (!r.readFieldHeader(prev, wt, id)) break;
+    if (!r.readFieldHeader(prev, wt, id)) {
+      if (un && first) std::memset(obj, 0, sd.size);  // apache::thrift::clear
+      break;
+    }
+    if (un && !first) fail(TGPU_ERR_UNION_MISSING_STOP, r.c.pos);  // throwUnionMissingStop
+    first = false;
     prev = id;
     const tgpu_field_desc* f = nullptr;
     for (uint32_t k = 0; k < sd.num_fields; ++k) {
@@ -630,6 +640,10 @@ void readStruct(R& r, uint32_t si, uint8_t* obj, DecodeCtx& dc) {
       continue;
     }
     uint8_t* m = obj + f->member_offset;
+    if (un) {  // field_ref().emplace(): the union now holds a fresh member
+      std::memset(obj, 0, sd.size);
+      obj[f->isset_offset] = 1;
+    }
     if (is_scalar(f->ttype)) {
       r.readScalar(f->ttype, m);
     } else if (f->ttype == TGPU_T_STRING) {
@@ -728,6 +742,21 @@ struct EncodeCtx {
   const uint8_t* lbase;
 };
 
+// A union writes its active member only (serialize_union.whisker:52-66,
+// switch (getType())): the first member whose isset byte is set, or none.
+void union_range(const EncodeCtx& ec, const tgpu_struct_desc& sd, const uint8_t* obj,
+                 uint32_t& k0, uint32_t& k1) {
+  if (!(sd.flags & TGPU_STRUCT_UNION)) return;
+  k0 = k1 = sd.num_fields;
+  for (uint32_t k = 0; k < sd.num_fields; ++k) {
+    if (obj[ec.sc->f[sd.first_field + k].isset_offset]) {
+      k0 = k;
+      k1 = k + 1;
+      return;
+    }
+  }
+}
+
 uint8_t load_bool_checked(const uint8_t* p, uint64_t off) {
   // validate_bool (Protocol.h:126-163): LOG(FATAL) on a byte not in {0,1}.
   if (*p > 1) fail(TGPU_ERR_INVALID_BOOL_WRITE, off);
@@ -766,7 +795,9 @@ struct BinaryWriter {
   }
   void structure(const EncodeCtx& ec, uint32_t si, const uint8_t* obj) {
     const tgpu_struct_desc& sd = ec.sc->s[si];
-    for (uint32_t k = 0; k < sd.num_fields; ++k) {
+    uint32_t k0 = 0, k1 = sd.num_fields;
+    union_range(ec, sd, obj, k0, k1);
+    for (uint32_t k = k0; k < k1; ++k) {
       const tgpu_field_desc& f = ec.sc->f[sd.first_field + k];
       if (f.qualifier == TGPU_OPTIONAL && !obj[f.isset_offset]) continue;
       const uint8_t* m = obj + f.member_offset;
@@ -839,7 +870,9 @@ struct CompactWriter {
   void structure(const EncodeCtx& ec, uint32_t si, const uint8_t* obj) {
     const tgpu_struct_desc& sd = ec.sc->s[si];
     int16_t last = 0;  // writeStructBegin pushes lastFieldId_ and resets it
-    for (uint32_t k = 0; k < sd.num_fields; ++k) {
+    uint32_t k0 = 0, k1 = sd.num_fields;
+    union_range(ec, sd, obj, k0, k1);
+    for (uint32_t k = k0; k < k1; ++k) {
       const tgpu_field_desc& f = ec.sc->f[sd.first_field + k];
       if (f.qualifier == TGPU_OPTIONAL && !obj[f.isset_offset]) continue;
       const uint8_t* m = obj + f.member_offset;

@@ -150,6 +150,7 @@ def cases():
     badc = W(C).field(I64, 1).raw(b"\xff" * 10).stop().bytes()
     out.append(("compact_mid_failure", C, two, goodc * 7 + badc + goodc, 9, None, VARINT))
     out += map_cases()
+    out += union_cases()
     return out
 
 
@@ -222,4 +223,61 @@ def map_cases():
     for v in (1, 2, 0x42):
         wc = W(C).field(MAP, 1).map_begin(BOOL, BYTE, 1).byte(v).byte(7).stop().bytes()
         out.append(("compact_map_bool_%d" % v, C, BMAP_SCHEMA, wc, 1, None, OK))
+    return out
+
+
+# {1: i32, 2: U} with union U {1: i64, 2: string, 3: Inner{1: i32}}
+UNION_SCHEMA = [[[1, I32, 0, 0, -1], [2, STRUCT, 0, 0, 1]],
+                {"union": True, "fields": [[1, I64, 0, 0, -1], [2, STR, 0, 0, -1],
+                                           [3, STRUCT, 0, 0, 2]]},
+                [[1, I32, 0, 0, -1]]]
+ROOT_UNION = [{"union": True, "fields": [[1, I64, 0, 0, -1], [2, I32, 0, 0, -1]]}]
+UNION_MISSING_STOP = 12
+
+
+def union_cases():
+    """deserialize_union.whisker:19-60: STOP first clears the union, one field
+    (read, or skipped when unknown / of another type) then STOP, else
+    throwUnionMissingStop (TProtocolException.cpp:23-27, INVALID_DATA)."""
+    out = []
+    for p, pn in ((B, "binary"), (C, "compact")):
+        def rec(*union_fields, tail=True):
+            w = W(p).field(I32, 1).i32(7).field(STRUCT, 2).struct_begin()
+            for f in union_fields:
+                f(w)
+            w.struct_end()
+            if tail:
+                w.field(I32, 1).i32(8)
+            return w.stop().bytes()
+
+        i64 = lambda w: w.field(I64, 1).i64(-5)
+        s = lambda w: w.field(STR, 2).string(b"abc")
+        inner = lambda w: w.field(STRUCT, 3).struct_begin().field(I32, 1).i32(4).struct_end()
+        unk = lambda w: w.field(I32, 9).i32(1)
+        wrong = lambda w: w.field(I32, 2).i32(3)  # member 2 is a string
+        for name, fields, code in (("one", (i64,), OK), ("string", (s,), OK),
+                                   ("struct", (inner,), OK), ("empty", (), OK),
+                                   ("two", (i64, s), UNION_MISSING_STOP),
+                                   ("unknown", (unk,), OK),
+                                   ("unknown_then_field", (unk, i64), UNION_MISSING_STOP),
+                                   ("type_mismatch", (wrong,), OK),
+                                   ("mismatch_then_field", (wrong, s), UNION_MISSING_STOP)):
+            out.append(("%s_union_%s" % (pn, name), p, UNION_SCHEMA, rec(*fields), 1, None, code))
+        # the union field twice: the second read replaces (emplace) or clears (STOP)
+        twice = W(p).field(STRUCT, 2).struct_begin()
+        i64(twice)
+        twice.struct_end().field(STRUCT, 2).struct_begin()
+        s(twice)
+        out.append(("%s_union_twice" % pn, p, UNION_SCHEMA, twice.struct_end().stop().bytes(), 1,
+                    None, OK))
+        cleared = W(p).field(STRUCT, 2).struct_begin()
+        s(cleared)
+        cleared.struct_end().field(STRUCT, 2).struct_begin().struct_end()
+        out.append(("%s_union_cleared" % pn, p, UNION_SCHEMA, cleared.stop().bytes(), 1, None, OK))
+        # a root union, back to back
+        r1 = W(p).field(I32, 2).i32(-9).stop().bytes()
+        r2 = W(p).stop().bytes()
+        r3 = W(p).field(I64, 1).i64(1).field(I32, 2).i32(2).stop().bytes()
+        out.append(("%s_root_union" % pn, p, ROOT_UNION, r1 + r2 + r1, 3, None, OK))
+        out.append(("%s_root_union_two" % pn, p, ROOT_UNION, r1 + r3, 2, None, UNION_MISSING_STOP))
     return out

@@ -95,9 +95,30 @@ SCHEMAS = {
          [7, T_MAP, T_BYTE, 0, -1, T_BOOL]],
         [[1, T_MAP, T_I32, 0, -1, T_I32], [2, T_I64, 0, 0, -1]],
     ],
+    # unions (TGPU_STRUCT_UNION): one active member or none; a union member
+    # that is a struct holding a map; a union of the root struct twice
+    "unions": [
+        [[1, T_I32, 0, 0, -1], [2, T_STRUCT, 0, 0, 1], [3, T_STRUCT, 0, 0, 1],
+         [4, T_I64, 0, 0, -1]],
+        {"union": True, "fields": [
+            [1, T_I64, 0, 0, -1], [2, T_STRING, 0, 0, -1], [3, T_DOUBLE, 0, 0, -1],
+            [4, T_STRUCT, 0, 0, 2], [5, T_LIST, T_I32, 0, -1], [6, T_BOOL, 0, 0, -1],
+            [20, T_MAP, T_I16, 0, -1, T_I16]]},
+        [[1, T_I32, 0, 0, -1], [2, T_MAP, T_I16, 0, -1, T_I16]],
+    ],
     "sparse": [[[5, T_I32, 0, 1, -1], [-3, T_I64, 0, 0, -1], [40, T_STRING, 0, 1, -1],
                 [300, T_BOOL, 0, 0, -1], [20, T_DOUBLE, 0, 1, -1], [21, T_I16, 0, 0, -1]]],
 }
+
+
+def rows(schema, si):
+    """The field rows of struct si (a union is {"union": true, "fields": rows})."""
+    e = schema[si]
+    return e["fields"] if isinstance(e, dict) else e
+
+
+def is_union(schema, si):
+    return isinstance(schema[si], dict) and bool(schema[si].get("union"))
 
 
 # ------------------------------------------------------------ value models --
@@ -218,6 +239,32 @@ def gen_maps(i):
     return [m1, m2, m3, s32(r[9]), m5, inner, m7]
 
 
+def gen_unions(i):
+    """Two unions per record, each with member (i + j) % 8 active (7 = empty)."""
+    r = [splitmix64_at(SEED + 31, 8 * i + k) for k in range(8)]
+
+    def union(j):
+        k = (i + j) % 8
+        v = [None] * 7
+        if k == 0:
+            v[0] = s64(r[j])
+        elif k == 1:
+            v[1] = bytes([97 + (i + t) % 26 for t in range(r[j] % 12)])
+        elif k == 2:
+            v[2] = bits_to_double(finite_bits(r[j]))
+        elif k == 3:
+            v[3] = [s32(r[j]), [(t - 5, t * 3) for t in range(r[j] % 4)]]
+        elif k == 4:
+            v[4] = [s32(splitmix64_at(SEED + 32, 16 * i + t)) for t in range(r[j] % 6)]
+        elif k == 5:
+            v[5] = bool(r[j] & 1)
+        elif k == 6:
+            v[6] = [(t, -t) for t in range(r[j] % 3)]
+        return v
+
+    return [s32(r[5]), union(0), union(3), s64(r[6])]
+
+
 ORIGINAL = [True, False, 50, 1200, 1300, 1600, 1.0, [0], b"def", [0]]
 UPDATED = [True, False, False, True, False, 50, 1100, 1200, 1300, 1400, 1500,
            1600, 1.0, b"abc", [0], [1], b"def", b"ghi", [0], [1]]
@@ -245,7 +292,7 @@ def flatten_values(schema, records):
         return v
 
     def walk(sidx, vals, prefix):
-        for k, row in enumerate(schema[sidx]):
+        for k, row in enumerate(rows(schema, sidx)):
             fid, ttype, elem, qual, sub = row[:5]
             v = vals[k] if vals is not None else None
             key = "%s%d" % (prefix, k)
@@ -278,7 +325,7 @@ def flatten_values(schema, records):
         sidx, ft = 0, None
         parts = path.split("/")
         for j, part in enumerate(parts):
-            f = schema[sidx][int(part)]
+            f = rows(schema, sidx)[int(part)]
             ft = f
             if j < len(parts) - 1:
                 sidx = f[4]

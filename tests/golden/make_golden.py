@@ -92,10 +92,10 @@ def write_value(p, ttype, elem, sidx, schema, v):
 
 def write_struct(p, schema, sidx, vals):
     p.writeStructBegin("S%d" % sidx)
-    for row, v in zip(schema[sidx], vals):
+    for row, v in zip(rows(schema, sidx), vals):
         fid, ttype, elem, qual, sub = row[:5]
         if v is None:
-            assert qual == 1
+            assert qual == 1 or is_union(schema, sidx)
             continue
         p.writeFieldBegin("f", ttype, fid)
         write_value(p, ttype, (elem, row[5]) if ttype == T_MAP else elem, sub, schema, v)
@@ -132,6 +132,8 @@ CASES = [
     ("sparse_compact", "sparse", "compact", gen_sparse, 200),
     ("maps_binary", "maps", "binary", gen_maps, 300),
     ("maps_compact", "maps", "compact", gen_maps, 300),
+    ("unions_binary", "unions", "binary", gen_unions, 200),
+    ("unions_compact", "unions", "compact", gen_unions, 200),
     ("original_compact", "original", "compact", lambda i: ORIGINAL, 1),
     ("original_binary", "original", "binary", lambda i: ORIGINAL, 1),
     ("updated_compact", "updated", "compact", lambda i: UPDATED, 1),
