@@ -11,6 +11,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libtgpu.so")
 
 PROTOCOL_BINARY = 0
 PROTOCOL_COMPACT = 2
+PROTOCOL_COMPACT_V1 = 0x102  # CompactV1Protocol (doubles little-endian)
 
 # TType (thrift/lib/cpp/protocol/TType.h:31-51)
 T_STOP, T_VOID, T_BOOL, T_BYTE, T_DOUBLE = 0, 1, 2, 3, 4

@@ -252,44 +252,28 @@ hipError_t launch_result_init(DevResult* res, uint64_t n, hipStream_t stream) {
 
 hipError_t launch_general_decode(const DecodeArgs& a, int protocol, hipStream_t stream) {
   const uint32_t g = grid_for(a.n);
-  if (protocol == TGPU_PROTOCOL_BINARY)
-    hipLaunchKernelGGL(general_decode_kernel<TGPU_PROTOCOL_BINARY>, dim3(g), dim3(256), 0, stream,
-                       a);
-  else
-    hipLaunchKernelGGL(general_decode_kernel<TGPU_PROTOCOL_COMPACT>, dim3(g), dim3(256), 0, stream,
-                       a);
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(general_decode_kernel<P_>, dim3(g), dim3(256), 0, stream,
+                       a));
   return hipGetLastError();
 }
 
 hipError_t launch_serial_decode(const DecodeArgs& a, int protocol, bool from_irregular,
                                 uint64_t fixed_len, hipStream_t stream) {
-  if (protocol == TGPU_PROTOCOL_BINARY)
-    hipLaunchKernelGGL(serial_decode_kernel<TGPU_PROTOCOL_BINARY>, dim3(1), dim3(64), 0, stream, a,
-                       (int)from_irregular, fixed_len);
-  else
-    hipLaunchKernelGGL(serial_decode_kernel<TGPU_PROTOCOL_COMPACT>, dim3(1), dim3(64), 0, stream, a,
-                       (int)from_irregular, fixed_len);
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(serial_decode_kernel<P_>, dim3(1), dim3(64), 0, stream, a,
+                       (int)from_irregular, fixed_len));
   return hipGetLastError();
 }
 
 hipError_t launch_decode_finish(const DecodeArgs& a, int protocol, uint64_t fixed_len,
                                 hipStream_t stream) {
-  if (protocol == TGPU_PROTOCOL_BINARY)
-    hipLaunchKernelGGL(decode_finish_kernel<TGPU_PROTOCOL_BINARY>, dim3(1), dim3(64), 0, stream, a,
-                       fixed_len);
-  else
-    hipLaunchKernelGGL(decode_finish_kernel<TGPU_PROTOCOL_COMPACT>, dim3(1), dim3(64), 0, stream, a,
-                       fixed_len);
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(decode_finish_kernel<P_>, dim3(1), dim3(64), 0, stream, a,
+                       fixed_len));
   return hipGetLastError();
 }
 
 hipError_t launch_stream_decode_finish(const DecodeArgs& a, int protocol, hipStream_t stream) {
-  if (protocol == TGPU_PROTOCOL_BINARY)
-    hipLaunchKernelGGL(stream_decode_finish_kernel<TGPU_PROTOCOL_BINARY>, dim3(1), dim3(64), 0,
-                       stream, a);
-  else
-    hipLaunchKernelGGL(stream_decode_finish_kernel<TGPU_PROTOCOL_COMPACT>, dim3(1), dim3(64), 0,
-                       stream, a);
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(stream_decode_finish_kernel<P_>, dim3(1), dim3(64), 0,
+                       stream, a));
   return hipGetLastError();
 }
 
@@ -297,19 +281,11 @@ hipError_t launch_general_encode(const EncodeArgs& a, int protocol, uint64_t n_b
                                  hipStream_t stream) {
   if (a.n == 0) return hipSuccess;
   const dim3 grid((uint32_t)n_blocks);
-  if (protocol == TGPU_PROTOCOL_BINARY) {
-    hipLaunchKernelGGL(encode_size_kernel<TGPU_PROTOCOL_BINARY>, grid, dim3(256), 0, stream, a);
-  } else {
-    hipLaunchKernelGGL(encode_size_kernel<TGPU_PROTOCOL_COMPACT>, grid, dim3(256), 0, stream, a);
-  }
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_size_kernel<P_>, grid, dim3(256), 0, stream, a));
   const hipError_t e = launch_scan_tiles(a.block_sums, n_blocks, a.scan_part, &a.res->total_bytes,
                                          a.offs + a.n, stream);
   if (e != hipSuccess) return e;
-  if (protocol == TGPU_PROTOCOL_BINARY) {
-    hipLaunchKernelGGL(encode_write_kernel<TGPU_PROTOCOL_BINARY>, grid, dim3(256), 0, stream, a);
-  } else {
-    hipLaunchKernelGGL(encode_write_kernel<TGPU_PROTOCOL_COMPACT>, grid, dim3(256), 0, stream, a);
-  }
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_write_kernel<P_>, grid, dim3(256), 0, stream, a));
   return hipGetLastError();
 }
 
@@ -317,11 +293,7 @@ hipError_t launch_general_size(const EncodeArgs& a, int protocol, uint64_t n_blo
                                hipStream_t stream) {
   if (a.n == 0) return hipSuccess;
   const dim3 grid((uint32_t)n_blocks);
-  if (protocol == TGPU_PROTOCOL_BINARY) {
-    hipLaunchKernelGGL(encode_size_kernel<TGPU_PROTOCOL_BINARY>, grid, dim3(256), 0, stream, a);
-  } else {
-    hipLaunchKernelGGL(encode_size_kernel<TGPU_PROTOCOL_COMPACT>, grid, dim3(256), 0, stream, a);
-  }
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_size_kernel<P_>, grid, dim3(256), 0, stream, a));
   const hipError_t e = launch_scan_tiles(a.block_sums, n_blocks, a.scan_part, &a.res->total_bytes,
                                          a.offs + a.n, stream);
   if (e != hipSuccess) return e;
@@ -336,12 +308,8 @@ hipError_t launch_size_offsets(const EncodeArgs& a, uint64_t n_blocks, hipStream
 
 hipError_t launch_encode_finish(const EncodeArgs& a, int protocol, uint64_t fixed_len,
                                 hipStream_t stream) {
-  if (protocol == TGPU_PROTOCOL_BINARY)
-    hipLaunchKernelGGL(encode_finish_kernel<TGPU_PROTOCOL_BINARY>, dim3(1), dim3(64), 0, stream, a,
-                       fixed_len);
-  else
-    hipLaunchKernelGGL(encode_finish_kernel<TGPU_PROTOCOL_COMPACT>, dim3(1), dim3(64), 0, stream, a,
-                       fixed_len);
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_finish_kernel<P_>, dim3(1), dim3(64), 0, stream, a,
+                       fixed_len));
   return hipGetLastError();
 }
 

@@ -465,7 +465,6 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
   if (fused) *fused = decode;
   const uint64_t C = a.n_chunks;
   const dim3 g((uint32_t)((C + 255) / 256)), b(256);
-  const bool bin = a.protocol == TGPU_PROTOCOL_BINARY;
   if (a.prog && a.chunk == kTile) {
     if (jit) {
       const hipError_t e = jit_launch_index(jit, 0, a, C, stream);
@@ -473,29 +472,18 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
     } else {
       hipLaunchKernelGGL(index_tile_spec_kernel, dim3((uint32_t)C), dim3(kTileLanes), 0, stream, a);
     }
-    if (bin)
-      hipLaunchKernelGGL(index_cont_kernel<TGPU_PROTOCOL_BINARY>, g, b, 0, stream, a);
-    else
-      hipLaunchKernelGGL(index_cont_kernel<TGPU_PROTOCOL_COMPACT>, g, b, 0, stream, a);
+    TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_cont_kernel<P_>, g, b, 0, stream, a));
   } else if (a.prog) {
     hipLaunchKernelGGL(index_spec_kernel, g, b, 0, stream, a);
-    if (bin)
-      hipLaunchKernelGGL(index_cont_kernel<TGPU_PROTOCOL_BINARY>, g, b, 0, stream, a);
-    else
-      hipLaunchKernelGGL(index_cont_kernel<TGPU_PROTOCOL_COMPACT>, g, b, 0, stream, a);
-  } else if (bin) {
-    hipLaunchKernelGGL(index_spec_general_kernel<TGPU_PROTOCOL_BINARY>, g, b, 0, stream, a);
+    TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_cont_kernel<P_>, g, b, 0, stream, a));
   } else {
-    hipLaunchKernelGGL(index_spec_general_kernel<TGPU_PROTOCOL_COMPACT>, g, b, 0, stream, a);
+    TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_spec_general_kernel<P_>, g, b, 0, stream, a));
   }
   hipLaunchKernelGGL(index_flag_kernel, g, b, 0, stream, a);
   hipError_t e = launch_scan_tiles(a.base, C, a.part, a.scal, nullptr, stream);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(index_list_kernel, g, b, 0, stream, a);
-  if (bin)
-    hipLaunchKernelGGL(index_fix_kernel<TGPU_PROTOCOL_BINARY>, dim3(1), dim3(64), 0, stream, a);
-  else
-    hipLaunchKernelGGL(index_fix_kernel<TGPU_PROTOCOL_COMPACT>, dim3(1), dim3(64), 0, stream, a);
+  TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_fix_kernel<P_>, dim3(1), dim3(64), 0, stream, a));
   hipLaunchKernelGGL(index_prep_kernel, g, b, 0, stream, a);
   e = launch_scan_tiles(a.base, C, a.part, nullptr, nullptr, stream);
   if (e != hipSuccess) return e;
@@ -510,10 +498,7 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
     hipLaunchKernelGGL(index_tile_emit_kernel, dim3((uint32_t)C), dim3(kTileLanes), 0, stream, x);
   else
     hipLaunchKernelGGL(index_emit_kernel, g, b, 0, stream, a);
-  if (bin)
-    hipLaunchKernelGGL(index_emit_cont_kernel<TGPU_PROTOCOL_BINARY>, g, b, 0, stream, x);
-  else
-    hipLaunchKernelGGL(index_emit_cont_kernel<TGPU_PROTOCOL_COMPACT>, g, b, 0, stream, x);
+  TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_emit_cont_kernel<P_>, g, b, 0, stream, x));
   hipLaunchKernelGGL(index_finish_kernel, dim3(1), dim3(64), 0, stream, a, a.scal + 5);
   if (decode)
     hipLaunchKernelGGL(index_decode_tail_kernel, dim3(1), dim3(64), 0, stream, x, a.scal + 5);

@@ -121,12 +121,8 @@ hipError_t launch_general_decode_list(const DecodeArgs& a, int protocol, const u
                                       const unsigned long long* n_list, hipStream_t stream) {
   const uint64_t b = (a.n + 255) / 256;
   const uint32_t g = (uint32_t)(b < 2048 ? (b ? b : 1) : 2048);
-  if (protocol == TGPU_PROTOCOL_BINARY)
-    hipLaunchKernelGGL(general_decode_list_kernel<TGPU_PROTOCOL_BINARY>, dim3(g), dim3(256), 0,
-                       stream, a, list, n_list);
-  else
-    hipLaunchKernelGGL(general_decode_list_kernel<TGPU_PROTOCOL_COMPACT>, dim3(g), dim3(256), 0,
-                       stream, a, list, n_list);
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(general_decode_list_kernel<P_>, dim3(g), dim3(256), 0,
+                       stream, a, list, n_list));
   return hipGetLastError();
 }
 

@@ -26,6 +26,7 @@ struct tgpu_schema {
   FixedPlan plan{};
   FixedPlan* d_plan = nullptr;
   bool has_prog[3] = {false, false, false};  // compiled programs by protocol id
+  bool has_double = false;  // any double member/element (CompactV1 differs there)
   VProgram prog[3]{};
   VProgram* d_prog[3] = {nullptr, nullptr, nullptr};
 };
@@ -48,6 +49,22 @@ struct tgpu_context {
 
 namespace tgpu {
 bool schema_has_lists(const tgpu_schema* s) { return s->has_lists; }
+
+bool valid_protocol(int p) {
+  return p == TGPU_PROTOCOL_BINARY || p == TGPU_PROTOCOL_COMPACT || p == TGPU_PROTOCOL_COMPACT_V1;
+}
+// The record program that runs `protocol`: CompactV1 differs from Compact
+// only in the byte order of doubles (CompactV1Protocol-inl.h:36-41,73-79), so
+// a schema without doubles runs Compact's program; with doubles, none (the
+// general kernels, instantiated for CompactV1).
+int prog_protocol(const tgpu_schema* s, int protocol) {
+  if (protocol == TGPU_PROTOCOL_COMPACT_V1) return s->has_double ? -1 : TGPU_PROTOCOL_COMPACT;
+  return protocol;
+}
+bool has_prog(const tgpu_schema* s, int protocol) {
+  const int q = prog_protocol(s, protocol);
+  return q >= 0 && s->has_prog[q];
+}
 void* context_host_pipe(tgpu_context* c) {
   if (!c->host_pipe) c->host_pipe = host_pipe_create();
   return c->host_pipe;
@@ -430,8 +447,8 @@ int ensure_workspace(tgpu_context* ctx, uint64_t n) {
 // nullptr: the interpreting kernels run.
 const JitKernels* schema_jit(const tgpu_schema* s, int protocol, int group, uint64_t records,
                              uint64_t bytes) {
-  if (!s->has_prog[protocol]) return nullptr;
-  return jit_kernels(s->prog[protocol], s->device, group, records, bytes, false);
+  if (!has_prog(s, protocol)) return nullptr;
+  return jit_kernels(s->prog[prog_protocol(s, protocol)], s->device, group, records, bytes, false);
 }
 
 // Fixed-layout Binary schemas: the compiled program kernels instead of the
@@ -439,8 +456,8 @@ const JitKernels* schema_jit(const tgpu_schema* s, int protocol, int group, uint
 const JitKernels* fixed_jit(const tgpu_schema* s, int protocol, int group, uint64_t n) {
   const char* e = getenv("TGPU_FIXED_PATH");
   if (!e || strcmp(e, "jit") != 0) return nullptr;
-  if (!s->has_prog[protocol] || 256ull * s->tmpl.wire_len > 24 * 1024) return nullptr;
-  return jit_kernels(s->prog[protocol], s->device, group, n, 0, false);
+  if (!has_prog(s, protocol) || 256ull * s->tmpl.wire_len > 24 * 1024) return nullptr;
+  return jit_kernels(s->prog[prog_protocol(s, protocol)], s->device, group, n, 0, false);
 }
 
 DevSchema dev_schema(const tgpu_schema* s) {
@@ -456,8 +473,8 @@ DevSchema dev_schema(const tgpu_schema* s) {
 hipError_t launch_indexed_decode(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
                                  const DecodeArgs& a, hipStream_t s) {
   const int32_t height = a.height ? a.height : a.max_depth;
-  if (schema->has_prog[protocol] && height >= 2 && a.max_depth >= 2) {
-    hipError_t e = launch_program_decode(a, schema->d_prog[protocol], a.rec_size, ctx->d_irr,
+  if (has_prog(schema, protocol) && height >= 2 && a.max_depth >= 2) {
+    hipError_t e = launch_program_decode(a, schema->d_prog[prog_protocol(schema, protocol)], a.rec_size, ctx->d_irr,
                                          &ctx->d_res->n_irregular, s,
                                          schema_jit(schema, protocol, JIT_DECODE, a.n, 0));
     if (e == hipSuccess)
@@ -492,8 +509,8 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   x.max_depth = limits ? limits->max_depth : 12000;
   x.height = limits ? limits->height : 0;
   const int32_t height = x.height ? x.height : x.max_depth;
-  x.prog = schema->has_prog[protocol] && height >= 2 && x.max_depth >= 2
-               ? schema->d_prog[protocol] : nullptr;
+  x.prog = has_prog(schema, protocol) && height >= 2 && x.max_depth >= 2
+               ? schema->d_prog[prog_protocol(schema, protocol)] : nullptr;
   x.chunk = index_chunk_bytes(end > begin ? end - begin : 0, x.prog != nullptr);
   x.window = (uint32_t)std::min<uint64_t>(x.chunk, 1024);
   x.n_chunks = end > begin ? (end - begin + x.chunk - 1) / x.chunk : 0;
@@ -605,7 +622,14 @@ int tgpu_schema_create(const tgpu_struct_desc* structs, uint32_t n_structs,
   s->structs.assign(structs, structs + n_structs);
   s->fields.assign(fields, fields + n_fields);
   s->has_lists = has_lists;
-  for (uint32_t k = 0; k < n_fields; ++k) s->has_strings |= fields[k].ttype == TGPU_T_STRING;
+  for (uint32_t k = 0; k < n_fields; ++k) {
+    const tgpu_field_desc& f = fields[k];
+    s->has_strings |= f.ttype == TGPU_T_STRING;
+    s->has_double |= f.ttype == TGPU_T_DOUBLE ||
+                     ((f.ttype == TGPU_T_LIST || f.ttype == TGPU_T_SET || f.ttype == TGPU_T_MAP) &&
+                      f.elem_ttype == TGPU_T_DOUBLE) ||
+                     (f.ttype == TGPU_T_MAP && f.val_ttype == TGPU_T_DOUBLE);
+  }
   (void)hipGetDevice(&s->device);
   if (hipMalloc(&s->d_structs, sizeof(tgpu_struct_desc) * n_structs) != hipSuccess ||
       hipMalloc(&s->d_fields, sizeof(tgpu_field_desc) * std::max(n_fields, 1u)) != hipSuccess) {
@@ -669,11 +693,11 @@ void tgpu_schema_destroy(tgpu_schema* s) {
 uint32_t tgpu_schema_record_size(const tgpu_schema* s) { return s ? s->structs[0].size : 0; }
 
 int tgpu_schema_compile(const tgpu_schema* s, int protocol) {
-  if (!s || (protocol != TGPU_PROTOCOL_BINARY && protocol != TGPU_PROTOCOL_COMPACT))
+  if (!s || !valid_protocol(protocol))
     return TGPU_ERR_INVALID_ARGUMENT;
-  if (!s->has_prog[protocol]) return TGPU_ERR_UNSUPPORTED;
+  if (!has_prog(s, protocol)) return TGPU_ERR_UNSUPPORTED;
   for (int group : {JIT_DECODE, JIT_ENCODE, JIT_INDEX})
-    if (!jit_kernels(s->prog[protocol], s->device, group, 0, 0, true)) return TGPU_ERR_UNSUPPORTED;
+    if (!jit_kernels(s->prog[prog_protocol(s, protocol)], s->device, group, 0, 0, true)) return TGPU_ERR_UNSUPPORTED;
   return TGPU_OK;
 }
 
@@ -681,7 +705,7 @@ int tgpu_schema_compile_check(const tgpu_struct_desc* structs, uint32_t n_struct
                               const tgpu_field_desc* fields, uint32_t n_fields, int protocol,
                               const char* arch, char* log, uint64_t log_capacity) {
   if (!structs || n_structs == 0 || (!fields && n_fields) ||
-      (protocol != TGPU_PROTOCOL_BINARY && protocol != TGPU_PROTOCOL_COMPACT))
+      !valid_protocol(protocol))
     return TGPU_ERR_INVALID_ARGUMENT;
   bool has_lists = false;
   const int rc = validate(structs, n_structs, fields, n_fields, 0, 0, has_lists);
@@ -689,8 +713,12 @@ int tgpu_schema_compile_check(const tgpu_struct_desc* structs, uint32_t n_struct
   tgpu_schema h;  // host tables only: nothing is uploaded
   h.structs.assign(structs, structs + n_structs);
   h.fields.assign(fields, fields + n_fields);
+  for (uint32_t k = 0; k < n_fields; ++k)
+    h.has_double |= fields[k].ttype == TGPU_T_DOUBLE || fields[k].elem_ttype == TGPU_T_DOUBLE ||
+                    fields[k].val_ttype == TGPU_T_DOUBLE;
+  const int q = prog_protocol(&h, protocol);
   VProgram P{};
-  if (!build_program(h, protocol, P)) return TGPU_ERR_UNSUPPORTED;
+  if (q < 0 || !build_program(h, q, P)) return TGPU_ERR_UNSUPPORTED;
   return jit_compile_check(P, arch, log, log_capacity);
 }
 
@@ -754,7 +782,7 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
                       const void* records, uint64_t n, const void* string_base,
                       const void* list_base, void* out, uint64_t out_capacity,
                       uint64_t* out_offsets, void* stream, tgpu_status* st, uint64_t* out_size) {
-  if (!ctx || !schema || (protocol != TGPU_PROTOCOL_BINARY && protocol != TGPU_PROTOCOL_COMPACT) ||
+  if (!ctx || !schema || !valid_protocol(protocol) ||
       (n && (!records || !out))) {
     fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
     return TGPU_ERR_INVALID_ARGUMENT;
@@ -787,7 +815,7 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
       EncodeArgs f = a;
       f.fixed_len = fixed;
       f.offs = out_offsets;
-      e = launch_program_write_fixed(f, schema->d_prog[protocol], s, fj);
+      e = launch_program_write_fixed(f, schema->d_prog[prog_protocol(schema, protocol)], s, fj);
     } else if (e == hipSuccess && schema->has_plan && ((uintptr_t)records & 7) == 0)
       e = launch_plan_binary_encode(&schema->plan, schema->d_plan, a.recs, n, a.out, out_offsets,
                                     ctx->d_res, s);
@@ -805,8 +833,8 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
     a.block_sums = ctx->d_block_sums;
     a.scan_part = ctx->d_scan_part;
     if (e == hipSuccess && n) {
-      if (schema->has_prog[protocol] && program_encode_fits(rs))
-        e = launch_program_encode(a, schema->d_prog[protocol], ctx->d_scan_part, false, s,
+      if (has_prog(schema, protocol) && program_encode_fits(rs))
+        e = launch_program_encode(a, schema->d_prog[prog_protocol(schema, protocol)], ctx->d_scan_part, false, s,
                                   schema_jit(schema, protocol, JIT_ENCODE, n, 0));
       else
         e = launch_general_encode(a, protocol, nb, s);
@@ -833,7 +861,7 @@ int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol
                       const void* records, uint64_t n, const void* list_base,
                       uint64_t* out_offsets, void* stream, tgpu_status* st, uint64_t* total) {
   if (!ctx || !schema || !out_offsets ||
-      (protocol != TGPU_PROTOCOL_BINARY && protocol != TGPU_PROTOCOL_COMPACT) ||
+      !valid_protocol(protocol) ||
       (n && !records) || ((uintptr_t)records) % schema->structs[0].align) {
     fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
     return TGPU_ERR_INVALID_ARGUMENT;
@@ -862,8 +890,8 @@ int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   (void)hipGetLastError();  // drop a stale error left by another library
   hipError_t e = launch_result_init(ctx->d_res, n, s);
   if (e == hipSuccess && n) {
-    if (schema->has_prog[protocol] && program_encode_fits(a.rec_size)) {
-      e = launch_program_encode(a, schema->d_prog[protocol], ctx->d_scan_part, true, s,
+    if (has_prog(schema, protocol) && program_encode_fits(a.rec_size)) {
+      e = launch_program_encode(a, schema->d_prog[prog_protocol(schema, protocol)], ctx->d_scan_part, true, s,
                                 schema_jit(schema, protocol, JIT_ENCODE, n, 0));
       if (e == hipSuccess) e = launch_size_offsets(a, (n + 255) / 256, s);
     } else {
@@ -888,7 +916,7 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
                       uint64_t in_len, const uint64_t* offsets, uint64_t n, void* records,
                       void* list_arena, uint64_t list_arena_capacity, const tgpu_limits* limits,
                       void* stream, tgpu_status* st, uint64_t* n_decoded, uint64_t* consumed) {
-  if (!ctx || !schema || (protocol != TGPU_PROTOCOL_BINARY && protocol != TGPU_PROTOCOL_COMPACT) ||
+  if (!ctx || !schema || !valid_protocol(protocol) ||
       (n && (!records || (!in && in_len)))) {
     fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
     return TGPU_ERR_INVALID_ARGUMENT;
@@ -928,7 +956,7 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
     if (e == hipSuccess && fj) {
       DecodeArgs f = a;
       f.fixed_len = fixed;
-      e = launch_program_decode(f, schema->d_prog[protocol], a.rec_size, ctx->d_irr,
+      e = launch_program_decode(f, schema->d_prog[prog_protocol(schema, protocol)], a.rec_size, ctx->d_irr,
                                 &ctx->d_res->n_irregular, s, fj);
     } else if (e == hipSuccess && schema->has_plan && ((uintptr_t)records & 7) == 0)
       e = launch_plan_binary_decode(&schema->plan, schema->d_plan, a.in, n, a.recs, ctx->d_res, s);
@@ -984,7 +1012,7 @@ int tgpu_decode_stream(tgpu_context* ctx, const tgpu_schema* schema, int protoco
                        const tgpu_limits* limits, void* stream, tgpu_status* st,
                        uint64_t* n_records, uint64_t* first_start, uint64_t* last_end) {
   if (!ctx || !schema || !offsets || (max_records && !records) ||
-      (protocol != TGPU_PROTOCOL_BINARY && protocol != TGPU_PROTOCOL_COMPACT) ||
+      !valid_protocol(protocol) ||
       (!in && in_len) || begin > end || end > in_len ||
       ((uintptr_t)records) % schema->structs[0].align) {
     fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
@@ -1078,7 +1106,7 @@ int tgpu_index_stream(tgpu_context* ctx, const tgpu_schema* schema, int protocol
                       void* stream, tgpu_status* st, uint64_t* n_records, uint64_t* first_start,
                       uint64_t* last_end) {
   if (!ctx || !schema || !offsets ||
-      (protocol != TGPU_PROTOCOL_BINARY && protocol != TGPU_PROTOCOL_COMPACT) ||
+      !valid_protocol(protocol) ||
       (!in && in_len) || begin > end || end > in_len) {
     fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
     return TGPU_ERR_INVALID_ARGUMENT;

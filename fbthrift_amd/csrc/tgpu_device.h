@@ -351,6 +351,21 @@ struct Proto<TGPU_PROTOCOL_COMPACT> {
   }
 };
 
+// ----------------------------------------------------------- Compact V1 ----
+// CompactV1Protocol.h: the Compact reader with readDouble as readLE
+// (CompactV1Protocol-inl.h:73-79); skip, sizes and everything else inherited.
+template <>
+struct Proto<TGPU_PROTOCOL_COMPACT_V1> : Proto<TGPU_PROTOCOL_COMPACT> {
+  static __device__ __forceinline__ void read_scalar(Reader& r, uint32_t t, uint8_t* dst) {
+    if (t == TGPU_T_DOUBLE) {
+      const uint64_t v = __builtin_bswap64(r.readBE(8));
+      if (r.ok()) *(uint64_t*)dst = v;
+      return;
+    }
+    Proto<TGPU_PROTOCOL_COMPACT>::read_scalar(r, t, dst);
+  }
+};
+
 // -------------------------------------------------------------------- skip --
 // Iterative skip with an explicit frame stack (no recursion on the GPU).
 // Frame kinds: struct (Binary: no delta; Compact: last field id), list/set
@@ -717,7 +732,10 @@ __device__ __forceinline__ void write_scalar(Writer& w, uint32_t t, const uint8_
       case TGPU_T_I32: w.varint(i32_to_zz(*(const int32_t*)p)); break;
       case TGPU_T_I64: w.varint(i64_to_zz(*(const int64_t*)p)); break;
       case TGPU_T_FLOAT: w.put_be(*(const uint32_t*)p, 4); break;
-      default: w.put_be(*(const uint64_t*)p, 8); break;
+      default:  // double: BE, CompactV1 LE (CompactV1Protocol-inl.h:36-41)
+        if (P == TGPU_PROTOCOL_COMPACT_V1) w.put_be(__builtin_bswap64(*(const uint64_t*)p), 8);
+        else w.put_be(*(const uint64_t*)p, 8);
+        break;
     }
   }
 }

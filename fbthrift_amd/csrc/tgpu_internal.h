@@ -22,6 +22,22 @@ typedef unsigned long uintptr_t;
 #include "../../include/thrift_gpu.h"
 #endif
 
+// Runs `stmt` with the protocol as the constant P_ (a kernel template
+// argument): Binary, Compact, or CompactV1.
+#define TGPU_BY_PROTOCOL(proto, ...)                                    \
+  do {                                                                  \
+    if ((proto) == TGPU_PROTOCOL_BINARY) {                              \
+      constexpr int P_ = TGPU_PROTOCOL_BINARY;                          \
+      __VA_ARGS__;                                                      \
+    } else if ((proto) == TGPU_PROTOCOL_COMPACT_V1) {                   \
+      constexpr int P_ = TGPU_PROTOCOL_COMPACT_V1;                      \
+      __VA_ARGS__;                                                      \
+    } else {                                                            \
+      constexpr int P_ = TGPU_PROTOCOL_COMPACT;                         \
+      __VA_ARGS__;                                                      \
+    }                                                                   \
+  } while (0)
+
 namespace tgpu {
 
 // Records per workgroup tile in the fixed-layout Binary kernels. 256 records x

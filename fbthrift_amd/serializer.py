@@ -13,7 +13,7 @@ raises AbortError where the reference calls LOG(FATAL) (Protocol.h:126-163).
 import ctypes
 
 from . import _lib
-from ._lib import PROTOCOL_BINARY, PROTOCOL_COMPACT
+from ._lib import PROTOCOL_BINARY, PROTOCOL_COMPACT, PROTOCOL_COMPACT_V1
 
 
 class TProtocolException(Exception):
@@ -227,7 +227,7 @@ class BatchSerializer:
     def arena_bytes(self, gschema, in_len):
         if not gschema.has_lists:
             return 0
-        return in_len * (8 if self.protocol == PROTOCOL_COMPACT else 1)
+        return in_len * (1 if self.protocol == PROTOCOL_BINARY else 8)
 
     def deserialize(self, gschema, wire, n, offsets=None, limits=None, records=None,
                     arena=None, stream=None, sync=True):
@@ -376,3 +376,4 @@ class BatchSerializer:
 
 BinarySerializer = BatchSerializer(PROTOCOL_BINARY)
 CompactSerializer = BatchSerializer(PROTOCOL_COMPACT)
+CompactV1Serializer = BatchSerializer(PROTOCOL_COMPACT_V1)

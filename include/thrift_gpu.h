@@ -67,6 +67,10 @@ extern "C" {
 enum tgpu_protocol {
   TGPU_PROTOCOL_BINARY = 0,
   TGPU_PROTOCOL_COMPACT = 2,
+  /* CompactV1ProtocolReader/Writer (thrift/lib/cpp2/protocol/
+     CompactV1Protocol.h, -inl.h:36-41,73-79): Compact with doubles written
+     little-endian. It has no PROTOCOL_TYPES id; this value is the library's. */
+  TGPU_PROTOCOL_COMPACT_V1 = 0x102,
 };
 
 /* Wire types: thrift/lib/cpp/protocol/TType.h:31-51 (same numeric values). */
@@ -318,7 +322,7 @@ int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol
  * deserialize<T>(Cursor&). Records are default-initialized (zero, isset 0)
  * before reading. List elements are written to list_arena (capacity
  * list_arena_capacity bytes; required size: in_len for Binary,
- * 8 * in_len for Compact, 0 when the schema has no lists).
+ * 8 * in_len for Compact/CompactV1, 0 when the schema has no lists/maps).
  * limits may be NULL (reference defaults).
  * If st != NULL the call waits and fills st, *n_decoded (records fully
  * decoded before the first failure) and *consumed (bytes consumed by them).

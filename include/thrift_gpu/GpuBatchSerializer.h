@@ -59,6 +59,11 @@ struct CompactProtocol {
   using ProtocolWriter = apache::thrift::CompactProtocolWriter;
   static constexpr int kId = TGPU_PROTOCOL_COMPACT;
 };
+struct CompactV1Protocol {
+  using ProtocolReader = apache::thrift::CompactV1ProtocolReader;
+  using ProtocolWriter = apache::thrift::CompactV1ProtocolWriter;
+  static constexpr int kId = TGPU_PROTOCOL_COMPACT_V1;
+};
 #else
 /* Same type codes as thrift/lib/cpp/protocol/TProtocolException.h:41-51. */
 class TProtocolException : public std::runtime_error {
@@ -90,6 +95,9 @@ struct BinaryProtocol {
 };
 struct CompactProtocol {
   static constexpr int kId = TGPU_PROTOCOL_COMPACT;
+};
+struct CompactV1Protocol {  /* CompactV1Protocol.h: doubles little-endian */
+  static constexpr int kId = TGPU_PROTOCOL_COMPACT_V1;
 };
 #endif
 
@@ -322,6 +330,7 @@ class GpuBatchSerializer {
 
 using BinaryBatchSerializer = GpuBatchSerializer<BinaryProtocol>;
 using CompactBatchSerializer = GpuBatchSerializer<CompactProtocol>;
+using CompactV1BatchSerializer = GpuBatchSerializer<CompactV1Protocol>;
 
 }  // namespace apache::thrift::gpu
 

@@ -114,7 +114,7 @@ def decode(schema, protocol, wire, n, offsets=None, limits=None, arena_cap=None)
     w = _u8(wire)
     rec = np.zeros(max(n * schema.record_size, 1), np.uint8)
     if arena_cap is None:
-        arena_cap = w.size * (8 if protocol == 2 else 1)
+        arena_cap = w.size * (1 if protocol == 0 else 8)
     arena = np.zeros(max(arena_cap, 1), np.uint8)
     offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
     lim = Limits(*limits) if limits is not None else None

@@ -509,6 +509,18 @@ struct CompactReader {
   static constexpr uint64_t kArenaScale = 8;
 };
 
+// ---- CompactV1 (CompactV1Protocol.h): readDouble is readLE (-inl.h:73-79) --
+struct CompactV1Reader : CompactReader {
+  void readScalar(uint8_t t, uint8_t* dst) {
+    if (t == TGPU_T_DOUBLE) {
+      const uint64_t v = __builtin_bswap64((uint64_t)c.readBE<int64_t>());
+      std::memcpy(dst, &v, 8);
+      return;
+    }
+    CompactReader::readScalar(t, dst);
+  }
+};
+
 // ---- generated readNoXfer restated, table-driven (TableBasedSerializerImpl.h
 // :695-767 has the same contract; deserialize_struct.whisker:19-160) --------
 struct DecodeCtx {
@@ -834,8 +846,10 @@ struct BinaryWriter {
   }
 };
 
-// CompactProtocolWriter (CompactProtocol-inl.h:91-383).
-struct CompactWriter {
+// CompactProtocolWriter (CompactProtocol-inl.h:91-383); kV1: CompactV1
+// (CompactV1Protocol-inl.h:36-41, doubles little-endian).
+template <bool kV1>
+struct CompactWriterT {
   Sink s;
   void fieldHeader(uint8_t ctype, int16_t id, int16_t& last) {  // :133-160
     if (id > last && id - last <= 15) {
@@ -854,7 +868,9 @@ struct CompactWriter {
       case TGPU_T_I32: s.varint(i32ToZigzag(ld<int32_t>(p))); break;
       case TGPU_T_I64: s.varint(i64ToZigzag(ld<int64_t>(p))); break;
       case TGPU_T_FLOAT: s.putBE(ld<uint32_t>(p), 4); break;
-      default: s.putBE(ld<uint64_t>(p), 8); break;  // double, BE (v2)
+      default:  // double: BE (v2); V1 writes it little-endian
+        s.putBE(kV1 ? __builtin_bswap64(ld<uint64_t>(p)) : ld<uint64_t>(p), 8);
+        break;
     }
   }
   // encodeMapElements: key then value per pair, in the given order
@@ -920,6 +936,9 @@ struct CompactWriter {
     s.put(0);  // writeFieldStop
   }
 };
+
+using CompactWriter = CompactWriterT<false>;
+using CompactV1Writer = CompactWriterT<true>;
 
 template <class W>
 int encode_impl(const Schema& sc, const uint8_t* recs, uint64_t n,
@@ -1000,6 +1019,9 @@ int oracle_encode_batch(const tgpu_struct_desc* structs, uint32_t n_structs,
   if (protocol == TGPU_PROTOCOL_COMPACT)
     return encode_impl<CompactWriter>(sc, rec, n_records, sb, lb, (uint8_t*)out,
                                       out_capacity, out_offsets, st, out_size);
+  if (protocol == TGPU_PROTOCOL_COMPACT_V1)
+    return encode_impl<CompactV1Writer>(sc, rec, n_records, sb, lb, (uint8_t*)out,
+                                        out_capacity, out_offsets, st, out_size);
   set_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
   return TGPU_ERR_INVALID_ARGUMENT;
 }
@@ -1025,6 +1047,11 @@ int oracle_decode_batch(const tgpu_struct_desc* structs, uint32_t n_structs,
                                       (uint8_t*)records, (uint8_t*)list_arena,
                                       list_arena_capacity, lim, st, n_decoded,
                                       consumed);
+  if (protocol == TGPU_PROTOCOL_COMPACT_V1)
+    return decode_impl<CompactV1Reader>(sc, p, in_len, offsets, n_records,
+                                        (uint8_t*)records, (uint8_t*)list_arena,
+                                        list_arena_capacity, lim, st, n_decoded,
+                                        consumed);
   set_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
   return TGPU_ERR_INVALID_ARGUMENT;
 }

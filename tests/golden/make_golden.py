@@ -110,6 +110,10 @@ def serialize(proto, schema, records):
         t = TTransport.TMemoryBuffer()
         p = (TBinaryProtocol.TBinaryProtocol(t) if proto == "binary"
              else TCompactProtocol.TCompactProtocol(t))
+        if proto == "compact_v1":
+            # version 1 of the Compact protocol: doubles in native (LE) order
+            # (TCompactProtocol.py VERSION_LOW vs VERSION_DOUBLE_BE)
+            p._TCompactProtocol__version = TCompactProtocol.TCompactProtocol.VERSION_LOW
         write_struct(p, schema, 0, rec)
         b = t.getvalue()
         chunks.append(b)
@@ -134,6 +138,11 @@ CASES = [
     ("maps_compact", "maps", "compact", gen_maps, 300),
     ("unions_binary", "unions", "binary", gen_unions, 200),
     ("unions_compact", "unions", "compact", gen_unions, 200),
+    ("scalars_compact_v1", "scalars", "compact_v1", gen_scalars, 300),
+    ("nested_compact_v1", "nested", "compact_v1", gen_nested, 500),
+    ("maps_compact_v1", "maps", "compact_v1", gen_maps, 100),
+    ("unions_compact_v1", "unions", "compact_v1", gen_unions, 100),
+    ("flat8_compact_v1", "flat8", "compact_v1", gen_flat8, 300),
     ("original_compact", "original", "compact", lambda i: ORIGINAL, 1),
     ("original_binary", "original", "binary", lambda i: ORIGINAL, 1),
     ("updated_compact", "updated", "compact", lambda i: UPDATED, 1),

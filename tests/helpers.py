@@ -14,7 +14,7 @@ sys.path.insert(0, GOLDEN)
 from fbthrift_amd.schema import SCALAR, Schema  # noqa: E402
 from fbthrift_amd._lib import T_LIST, T_MAP, T_SET, T_STRING, T_STRUCT  # noqa: E402
 
-PROTO = {"binary": 0, "compact": 2}
+PROTO = {"binary": 0, "compact": 2, "compact_v1": 0x102}
 ELEM_NP = {2: np.uint8, 3: np.int8, 6: np.int16, 8: np.int32, 10: np.int64, 4: np.uint64,
            19: np.uint32}
 

@@ -1,0 +1,81 @@
+"""CompactV1 (TGPU_PROTOCOL_COMPACT_V1): CompactV1ProtocolReader/Writer,
+thrift/lib/cpp2/protocol/CompactV1Protocol.h — the Compact protocol with
+doubles written and read little-endian (CompactV1Protocol-inl.h:36-41,
+73-79); every other byte is Compact's.
+
+Golden vectors: the reference's Python TCompactProtocol at VERSION_LOW (its
+V1 double order), cases *_compact_v1 in tests/golden (decode, encode and
+encoded size on the GPU run through tests/test_gpu_parity.py's golden tests).
+"""
+import struct
+
+import numpy as np
+import pytest
+
+import datagen
+import helpers
+from fbthrift_amd.schema import Schema
+from oracle import oracle
+
+V1 = 0x102
+
+
+def test_v1_differs_from_compact_only_in_doubles():
+    """Same values, both protocols: identical record lengths, and the bytes
+    differ exactly where a double is (byte-reversed)."""
+    a, b = helpers.Case("nested_compact"), helpers.Case("nested_compact_v1")
+    n = b.n
+    assert np.array_equal(a.offsets[:n + 1], b.offsets)
+    wa, wb = a.wire[:len(b.wire)], b.wire
+    diff = [i for i in range(len(wb)) if wa[i] != wb[i]]
+    assert diff
+    # each record's inner struct holds 3 doubles after a 1-byte header
+    rec0 = wb[:int(b.offsets[1])]
+    d0 = datagen.gen_nested(0)[2][0]
+    assert struct.pack("<d", d0) in rec0 and struct.pack(">d", d0) in wa[:int(a.offsets[1])]
+
+
+def test_v1_without_doubles_is_compact():
+    a, b = helpers.Case("flat8_compact"), helpers.Case("flat8_compact_v1")
+    assert a.wire[:len(b.wire)] == b.wire
+
+
+def test_oracle_rejects_unknown_protocol():
+    schema = Schema.from_table(datagen.SCHEMAS["flat8"])
+    st, *_ = oracle.decode(schema, 3, b"\x00", 1)
+    assert st.code == 23  # INVALID_ARGUMENT
+
+
+@pytest.mark.gpu
+def test_v1_program_selection(gpu):
+    """A V1 schema without doubles runs Compact's compiled program; with
+    doubles there is none (general kernels) — tgpu_schema_compile says which."""
+    from fbthrift_amd.serializer import GpuSchema
+
+    assert GpuSchema(Schema.from_table(datagen.SCHEMAS["mixed"])).compile(V1)
+    assert not GpuSchema(Schema.from_table(datagen.SCHEMAS["nested"])).compile(V1)
+
+
+@pytest.mark.gpu
+def test_gpu_v1_large_nested_roundtrip(gpu):
+    """A larger V1 batch with doubles (general kernels, incl. the unindexed
+    stream path): GPU bytes and records equal the oracle's."""
+    import torch
+
+    from fbthrift_amd.serializer import CompactV1Serializer as S, GpuSchema
+
+    table = datagen.SCHEMAS["nested"]
+    schema = Schema.from_table(table)
+    n = 40_000
+    vals = datagen.flatten_values(table, [datagen.gen_nested(i) for i in range(n)])
+    rec, sa, la = helpers.pack(schema, vals, n)
+    ost, owire, ooffs = oracle.encode(schema, V1, rec, n, sa, la)
+    assert ost.code == 0
+    gs = GpuSchema(schema)
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x) if x.size else np.zeros(1, np.uint8)).to(gpu)
+    wire, offs = S.serialize(gs, t(rec), n, t(sa), t(la))
+    assert bytes(wire.cpu().numpy()) == owire
+    grec, garena, gst, gnd, gcons = S.deserialize_status(gs, t(np.frombuffer(owire, np.uint8).copy()), n)
+    assert gst.code == 0 and gnd == n and gcons == len(owire)
+    helpers.assert_values_equal(
+        helpers.unpack(schema, grec.cpu().numpy(), n, owire, garena.cpu().numpy()), vals)

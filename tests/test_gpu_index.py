@@ -26,7 +26,10 @@ def _t(a, dev):
 
 
 def _ser(protocol):
-    from fbthrift_amd.serializer import BinarySerializer, CompactSerializer
+    from fbthrift_amd import serializer as S
+
+    return {0: S.BinarySerializer, 2: S.CompactSerializer,
+            0x102: S.CompactV1Serializer}[protocol]
 
     return BinarySerializer if protocol == 0 else CompactSerializer
 
