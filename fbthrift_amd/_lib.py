@@ -67,7 +67,7 @@ EXPORTS = [
     "tgpu_schema_fixed_wire_size", "tgpu_context_create", "tgpu_context_destroy",
     "tgpu_context_reserve", "tgpu_context_wait", "tgpu_encode_batch", "tgpu_encoded_size",
     "tgpu_decode_batch", "tgpu_index_stream", "tgpu_schema_compile", "tgpu_schema_compile_check",
-    "tgpu_decode_host", "tgpu_encode_host", "tgpu_decode_stream",
+    "tgpu_decode_host", "tgpu_encode_host", "tgpu_decode_stream", "tgpu_transcode_batch",
 ]
 
 _lib = None
@@ -137,5 +137,9 @@ def lib():
                                      ctypes.POINTER(Limits), P, ctypes.POINTER(Status),
                                      ctypes.POINTER(U64), ctypes.POINTER(U64),
                                      ctypes.POINTER(U64)]
+    L.tgpu_transcode_batch.restype = I32
+    L.tgpu_transcode_batch.argtypes = [P, P, I32, I32, P, U64, P, U64, P, U64, P,
+                                       ctypes.POINTER(Limits), P, ctypes.POINTER(Status),
+                                       ctypes.POINTER(U64), ctypes.POINTER(U64)]
     _lib = L
     return L

@@ -45,6 +45,11 @@ struct tgpu_context {
   uint64_t index_bytes = 0;
   int last_op = 0;        // 1 decode, 2 encode
   void* host_pipe = nullptr;  // tgpu_host.cpp: streams + chunk buffers of the host path
+  // transcode: decoded records and list arena between the two passes
+  uint8_t* d_xrec = nullptr;
+  uint64_t xrec_bytes = 0;
+  uint8_t* d_xarena = nullptr;
+  uint64_t xarena_bytes = 0;
 };
 
 namespace tgpu {
@@ -750,6 +755,8 @@ void tgpu_context_destroy(tgpu_context* c) {
   if (c->d_scan_part) (void)hipFree(c->d_scan_part);
   if (c->d_irr) (void)hipFree(c->d_irr);
   if (c->d_index) (void)hipFree(c->d_index);
+  if (c->d_xrec) (void)hipFree(c->d_xrec);
+  if (c->d_xarena) (void)hipFree(c->d_xarena);
   delete c;
 }
 
@@ -1003,6 +1010,67 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
     return tgpu_context_wait(ctx, stream, st ? st : &tmp, n_decoded, consumed);
   }
   return TGPU_OK;
+}
+
+namespace {
+int grow(uint8_t*& p, uint64_t& have, uint64_t want) {
+  if (want <= have) return TGPU_OK;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  have = 0;
+  if (hipMalloc(&p, want) != hipSuccess) return TGPU_ERR_HIP;
+  have = want;
+  return TGPU_OK;
+}
+}  // namespace
+
+int tgpu_transcode_batch(tgpu_context* ctx, const tgpu_schema* schema, int from_protocol,
+                         int to_protocol, const void* in, uint64_t in_len,
+                         const uint64_t* offsets, uint64_t n, void* out, uint64_t out_capacity,
+                         uint64_t* out_offsets, const tgpu_limits* limits, void* stream,
+                         tgpu_status* st, uint64_t* n_done, uint64_t* out_size) {
+  if (n_done) *n_done = 0;
+  if (out_size) *out_size = 0;
+  if (!ctx || !schema || !valid_protocol(from_protocol) || !valid_protocol(to_protocol) ||
+      (n && (!in || !out))) {
+    fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+    return TGPU_ERR_INVALID_ARGUMENT;
+  }
+  // records and list elements stay in HBM between the passes (grow-only)
+  const uint64_t rs = schema->structs[0].size;
+  const uint64_t acap =
+      schema->has_lists ? in_len * (from_protocol == TGPU_PROTOCOL_BINARY ? 1 : 8) : 0;
+  int rc = grow(ctx->d_xrec, ctx->xrec_bytes, std::max<uint64_t>(n * rs, 16));
+  if (!rc && acap) rc = grow(ctx->d_xarena, ctx->xarena_bytes, acap);
+  if (rc) {
+    fill_status(st, rc, 0, 0);
+    return rc;
+  }
+  tgpu_status dst{};
+  uint64_t nd = 0, consumed = 0;
+  const int drc = tgpu_decode_batch(ctx, schema, from_protocol, in, in_len, offsets, n,
+                                    ctx->d_xrec, acap ? ctx->d_xarena : nullptr, acap, limits,
+                                    stream, &dst, &nd, &consumed);
+  if (drc && nd == 0 && dst.exc_class == TGPU_EXC_RUNTIME) {  // usage / HIP error
+    if (st) *st = dst;
+    return drc;
+  }
+  tgpu_status est{};
+  uint64_t total = 0;
+  const int erc = tgpu_encode_batch(ctx, schema, to_protocol, ctx->d_xrec, nd, in,
+                                    acap ? ctx->d_xarena : nullptr, out, out_capacity,
+                                    out_offsets, stream, &est, &total);
+  if (out_size) *out_size = total;
+  // the first failure in record order: an encode failure is at a record
+  // before the one the decoder rejected
+  if (erc) {
+    if (st) *st = est;
+    if (n_done) *n_done = est.record;
+    return erc;
+  }
+  if (n_done) *n_done = nd;
+  if (st) *st = dst;
+  return drc;
 }
 
 int tgpu_decode_stream(tgpu_context* ctx, const tgpu_schema* schema, int protocol,

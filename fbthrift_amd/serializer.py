@@ -280,6 +280,29 @@ class BatchSerializer:
             ctypes.byref(n_dec), ctypes.byref(consumed))
         return records, arena, st, n_dec.value, consumed.value
 
+    def transcode(self, gschema, wire, n, to_protocol, offsets=None, out=None, limits=None,
+                  stream=None):
+        """Re-encodes n records of `wire` (this serializer's protocol) into
+        `to_protocol` on the device (tgpu_transcode_batch). Returns (out,
+        out_offsets, status, n_done, out_size); never raises on data errors."""
+        import torch
+
+        dev = wire.device
+        if out is None:
+            # no wire byte grows by more than 8x in another protocol (a
+            # 1-byte Compact varint list element is 8 Binary bytes)
+            out = torch.empty(max(8 * wire.numel() + 16, 16), dtype=torch.uint8, device=dev)
+        offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        lim = _lib.Limits(*limits) if limits is not None else None
+        st = _lib.Status()
+        done, size = ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.lib().tgpu_transcode_batch(
+            self.context().handle, gschema.handle, self.protocol, to_protocol, _ptr(wire),
+            wire.numel(), _ptr(offsets), n, _ptr(out), out.numel(), _ptr(offs),
+            ctypes.byref(lim) if lim is not None else None, _stream(stream), ctypes.byref(st),
+            ctypes.byref(done), ctypes.byref(size))
+        return out, offs, st, done.value, size.value
+
 
     def decode_stream(self, gschema, wire, begin=0, end=None, speculative=False,
                       max_records=None, offsets=None, records=None, arena=None, limits=None,

@@ -335,6 +335,28 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema,
                       void* stream, tgpu_status* st, uint64_t* n_decoded,
                       uint64_t* consumed);
 
+/* ---- transcoding ------------------------------------------------------ */
+/*
+ * Re-encodes n records of a stream from one protocol into another (Binary,
+ * Compact, CompactV1 in any direction, same schema) without leaving the
+ * device: each output record is byte-identical to
+ * serialize<To>(deserialize<From>(record)) of the reference — the bulk form
+ * of the wire-to-wire transcoder (thrift/lib/cpp2/transcode/README.md:1-20,
+ * schema-driven; unknown fields are dropped as the generated codec drops
+ * them). The decoded records and list elements stay in a context workspace
+ * in HBM between the read and the write. in/offsets/limits as for
+ * tgpu_decode_batch; out/out_offsets (n+1 entries, may be NULL) as for
+ * tgpu_encode_batch. Blocking. A record the reader rejects ends the batch:
+ * the records before it are transcoded (*n_done, *out_size) and st is the
+ * reader's status for it; an output overflow reports the encoder's.
+ */
+int tgpu_transcode_batch(tgpu_context* ctx, const tgpu_schema* schema, int from_protocol,
+                         int to_protocol, const void* in, uint64_t in_len,
+                         const uint64_t* offsets, uint64_t n_records, void* out,
+                         uint64_t out_capacity, uint64_t* out_offsets,
+                         const tgpu_limits* limits, void* stream, tgpu_status* st,
+                         uint64_t* n_done, uint64_t* out_size);
+
 /* ---- host-memory batches ---------------------------------------------- */
 /*
  * The same calls for data that starts and ends in HOST memory (an IOBuf's

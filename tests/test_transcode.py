@@ -1,0 +1,119 @@
+"""Binary <-> Compact <-> CompactV1 transcoding (tgpu_transcode_batch):
+serialize<To>(deserialize<From>(record)) for every record, on the device —
+the bulk form of thrift/lib/cpp2/transcode (README.md:1-20: schema-driven
+wire-to-wire conversion).
+
+Pinned by the reference's own vectors: the golden cases of one schema were
+written by the reference's Python protocols from the same values in every
+protocol, so transcoding case X_<from> must give exactly X_<to>'s bytes.
+Unknown fields are dropped (the generated codec does not retain them):
+UpdatedStruct bytes transcoded under OriginalStruct's schema equal
+OriginalStruct written directly.
+"""
+import itertools
+
+import numpy as np
+import pytest
+
+import helpers
+from oracle import oracle
+
+PROTOS = {"binary": 0, "compact": 2, "compact_v1": 0x102}
+
+
+def _pairs():
+    """(from case, to case) golden pairs with the same schema and values."""
+    names = helpers.case_names()
+    out = []
+    for a, b in itertools.permutations(names, 2):
+        for pa in PROTOS:
+            for pb in PROTOS:
+                if a.endswith("_" + pa) and b.endswith("_" + pb):
+                    ba, bb = a[: -len(pa) - 1], b[: -len(pb) - 1]
+                    if ba == bb and pa != pb:
+                        out.append((a, b))
+    return sorted(set(out))
+
+
+PAIRS = _pairs()
+
+
+def _oracle_transcode(schema, pf, pt, wire, n):
+    st, rec, arena, nd, _ = oracle.decode(schema, pf, wire, n)
+    est, out, offs = oracle.encode(schema, pt, rec, nd, np.frombuffer(bytes(wire) or b"\0", np.uint8),
+                                   arena)
+    return st, nd, out, offs
+
+
+@pytest.mark.parametrize("src,dst", PAIRS, ids=["%s->%s" % p for p in PAIRS])
+def test_oracle_transcode_equals_reference_bytes(src, dst):
+    a, b = helpers.Case(src), helpers.Case(dst)
+    n = min(a.n, b.n)
+    wire = a.wire[: int(a.offsets[n])]
+    st, nd, out, offs = _oracle_transcode(a.schema, a.protocol, b.protocol, wire, n)
+    assert st.code == 0 and nd == n
+    assert out == b.wire[: int(b.offsets[n])]
+
+
+@pytest.mark.parametrize("proto", ["binary", "compact"])
+def test_oracle_transcode_drops_unknown_fields(proto):
+    upd, orig = helpers.Case("updated_" + proto), helpers.Case("original_" + proto)
+    for to in ("binary", "compact"):
+        st, nd, out, _ = _oracle_transcode(orig.schema, upd.protocol, PROTOS[to], upd.wire, 1)
+        assert st.code == 0 and out == helpers.Case("original_" + to).wire
+
+
+def _gpu_transcode(dev, schema, pf, pt, wire, n, out_cap=None, offsets=None):
+    import torch
+
+    from fbthrift_amd import serializer as S
+
+    ser = {0: S.BinarySerializer, 2: S.CompactSerializer, 0x102: S.CompactV1Serializer}[pf]
+    gs = S.GpuSchema(schema)
+    w = torch.from_numpy(np.frombuffer(bytes(wire) or b"\0", np.uint8).copy()).to(dev)
+    out = None if out_cap is None else torch.empty(max(out_cap, 1), dtype=torch.uint8, device=dev)
+    offs_t = None
+    if offsets is not None:
+        offs_t = torch.from_numpy(np.asarray(offsets, np.int64).copy()).to(dev)
+    out, offs, st, done, size = ser.transcode(gs, w[: len(wire)] if len(wire) else w[:0], n, pt,
+                                              offsets=offs_t, out=out)
+    return st, done, bytes(out[:size].cpu().numpy()), offs[: done + 1].cpu().numpy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("src,dst", PAIRS, ids=["%s->%s" % p for p in PAIRS])
+def test_gpu_transcode_golden(gpu, src, dst):
+    a, b = helpers.Case(src), helpers.Case(dst)
+    n = min(a.n, b.n)
+    wire = a.wire[: int(a.offsets[n])]
+    for offs in (None, a.offsets[: n + 1]):
+        st, done, out, o = _gpu_transcode(gpu, a.schema, a.protocol, b.protocol, wire, n,
+                                          offsets=offs)
+        assert st.code == 0 and done == n, st.as_tuple()
+        assert out == b.wire[: int(b.offsets[n])]
+        assert np.array_equal(o.astype(np.uint64), b.offsets[: n + 1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["maps_compact", "unions_binary", "nested_compact_v1",
+                                  "scalars_binary"])
+def test_gpu_transcode_errors_match_oracle(gpu, name):
+    """Damaged input: the reader's status, the records before it transcoded
+    (as the oracle does it); a small output: OUTPUT_OVERFLOW at the record
+    that does not fit."""
+    c = helpers.Case(name)
+    rng = np.random.default_rng(3)
+    to = 0 if c.protocol != 0 else 2
+    for trial in range(6):
+        m = np.frombuffer(c.wire, np.uint8).copy()
+        pos = rng.integers(0, m.size, 2)
+        m[pos] = rng.integers(0, 256, 2)
+        st, done, out, _ = _gpu_transcode(gpu, c.schema, c.protocol, to, m.tobytes(), c.n)
+        ost, ond, oout, _ = _oracle_transcode(c.schema, c.protocol, to, m.tobytes(), c.n)
+        assert st.as_tuple() == ost.as_tuple() and done == ond, trial
+        assert out == oout
+    full = _oracle_transcode(c.schema, c.protocol, to, c.wire, c.n)[2]
+    st, done, out, _ = _gpu_transcode(gpu, c.schema, c.protocol, to, c.wire, c.n,
+                                      out_cap=len(full) // 2)
+    assert st.code == 21 and 0 < done < c.n
+    assert out == full[: len(out)]
