@@ -445,6 +445,9 @@ def main():
     ap.add_argument("--no-copy-ceiling", action="store_true")
     ap.add_argument("--host-start", action="store_true",
                     help="also time pinned-host -> decode -> host and host -> encode -> host")
+    ap.add_argument("--transcode", action="store_true",
+                    help="also time device transcoding of the workload's stream into the "
+                         "other protocol (tgpu_transcode_batch)")
     args = ap.parse_args()
 
     import torch
@@ -520,6 +523,8 @@ def main():
     }
     if args.host_start and rank == 0:
         line["host_start"] = host_start(wl, dev)
+    if args.transcode and rank == 0:
+        line["transcode"] = transcode(wl, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == 2:
         line["cpu_baseline"] = cpu_baseline()
     if rank == 0:
@@ -583,6 +588,41 @@ def pmc_traffic(kernel, n, config=2):
         return int(d["hbm_bytes_per_record"] * n)
     except (OSError, KeyError, ValueError):
         return None
+
+
+def transcode(wl, dev, reps=5):
+    """Device-resident Binary <-> Compact transcoding of the workload's whole
+    stream (tgpu_transcode_batch: decode into an HBM workspace, re-encode);
+    rate = input wire bytes / time. Checked by transcoding back to the
+    original bytes. Secondary line, never `value`."""
+    import torch
+
+    from fbthrift_amd import serializer as S
+
+    src = wl.S
+    to = 2 if src.protocol == 0 else 0
+    dst = S.CompactSerializer if to == 2 else S.BinarySerializer
+    w = wl.wire[: wl.wire_bytes]
+    out = torch.empty(8 * wl.wire_bytes + 16, dtype=torch.uint8, device=dev)
+    res = {"from": src.protocol, "to": to}
+    best = None
+    for _ in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        _, offs, st, done, size = src.transcode(wl.gs, w, wl.n, to, out=out)
+        el = time.perf_counter() - t0
+        if st.code or done != wl.n:
+            raise RuntimeError("transcode failed: %s" % (st.as_tuple(),))
+        best = el if best is None else min(best, el)
+    back = torch.empty(wl.wire_bytes + 16, dtype=torch.uint8, device=dev)
+    _, _, st, done, bsize = dst.transcode(wl.gs, out[:size], wl.n, src.protocol, out=back)
+    if st.code or bsize != wl.wire_bytes or not torch.equal(back[:bsize], w):
+        raise RuntimeError("transcode round trip mismatch")
+    res["gibps_in"] = round(wl.wire_bytes / best / 2**30, 3)
+    res["out_bytes"] = size
+    res["ms"] = round(best * 1e3, 3)
+    res["how"] = "blocking call incl. one host sync between the passes; best of %d" % reps
+    return res
 
 
 def host_start(wl, dev):
