@@ -27,6 +27,7 @@ struct tgpu_schema {
   FixedPlan* d_plan = nullptr;
   bool has_prog[3] = {false, false, false};  // compiled programs by protocol id
   bool has_double = false;  // any double member/element (CompactV1 differs there)
+  bool str_elems = false;   // strings inside lists/sets/maps (arena scale 4 / 16)
   VProgram prog[3]{};
   VProgram* d_prog[3] = {nullptr, nullptr, nullptr};
 };
@@ -96,6 +97,8 @@ uint32_t scalar_size(uint32_t t) {
   }
 }
 uint32_t align_up(uint32_t x, uint32_t a) { return (x + a - 1) / a * a; }
+// container element types: scalars, or strings (as tgpu_span)
+bool is_elem(uint32_t t) { return is_scalar(t) || t == TGPU_T_STRING; }
 
 // Layout of struct si (memoized in `done`): declaration-order members at
 // natural alignment, then one isset byte per field (Isset.h:243-296).
@@ -163,11 +166,11 @@ int validate(const tgpu_struct_desc* s, uint32_t ns, const tgpu_field_desc* f, u
     } else if (fd.ttype == TGPU_T_STRING) {
       sz = 16;
     } else if (fd.ttype == TGPU_T_LIST || fd.ttype == TGPU_T_SET) {
-      if (!is_scalar(fd.elem_ttype)) return TGPU_ERR_UNSUPPORTED;
+      if (!is_elem(fd.elem_ttype)) return TGPU_ERR_UNSUPPORTED;
       has_lists = true;
       sz = 16;
     } else if (fd.ttype == TGPU_T_MAP) {
-      if (!is_scalar(fd.elem_ttype) || !is_scalar(fd.val_ttype)) return TGPU_ERR_UNSUPPORTED;
+      if (!is_elem(fd.elem_ttype) || !is_elem(fd.val_ttype)) return TGPU_ERR_UNSUPPORTED;
       has_lists = true;
       sz = 16;
     } else if (fd.ttype == TGPU_T_STRUCT) {
@@ -321,6 +324,7 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
     } else if (f.ttype == TGPU_T_LIST || f.ttype == TGPU_T_SET) {
       v.kind = VOP_LIST;
       const uint32_t e = f.elem_ttype;
+      if (!is_scalar(e)) return false;  // string elements: general kernels
       v.width = (uint8_t)scalar_size(e);
       v.elem_ttype = (uint8_t)e;
       v.elem_ct = (uint8_t)compact_ctype(e);
@@ -467,7 +471,7 @@ const JitKernels* fixed_jit(const tgpu_schema* s, int protocol, int group, uint6
 
 DevSchema dev_schema(const tgpu_schema* s) {
   return DevSchema{s->d_structs, s->d_fields, (uint32_t)s->structs.size(),
-                   (uint32_t)s->fields.size()};
+                   (uint32_t)s->fields.size(), s->str_elems ? 1u : 0u, 0u};
 }
 
 // Indexed decode (a.offs = record starts): compiled-program fast path, then
@@ -629,7 +633,11 @@ int tgpu_schema_create(const tgpu_struct_desc* structs, uint32_t n_structs,
   s->has_lists = has_lists;
   for (uint32_t k = 0; k < n_fields; ++k) {
     const tgpu_field_desc& f = fields[k];
-    s->has_strings |= f.ttype == TGPU_T_STRING;
+    const bool container = f.ttype == TGPU_T_LIST || f.ttype == TGPU_T_SET || f.ttype == TGPU_T_MAP;
+    const bool se = container && (f.elem_ttype == TGPU_T_STRING ||
+                                  (f.ttype == TGPU_T_MAP && f.val_ttype == TGPU_T_STRING));
+    s->str_elems |= se;
+    s->has_strings |= f.ttype == TGPU_T_STRING || se;
     s->has_double |= f.ttype == TGPU_T_DOUBLE ||
                      ((f.ttype == TGPU_T_LIST || f.ttype == TGPU_T_SET || f.ttype == TGPU_T_MAP) &&
                       f.elem_ttype == TGPU_T_DOUBLE) ||
@@ -725,6 +733,12 @@ int tgpu_schema_compile_check(const tgpu_struct_desc* structs, uint32_t n_struct
   VProgram P{};
   if (q < 0 || !build_program(h, q, P)) return TGPU_ERR_UNSUPPORTED;
   return jit_compile_check(P, arch, log, log_capacity);
+}
+
+uint32_t tgpu_schema_arena_scale(const tgpu_schema* s, int protocol) {
+  if (!s || !s->has_lists || !valid_protocol(protocol)) return 0;
+  const bool bin = protocol == TGPU_PROTOCOL_BINARY;
+  return s->str_elems ? (bin ? 4 : 16) : (bin ? 1 : 8);
 }
 
 uint64_t tgpu_schema_fixed_wire_size(const tgpu_schema* s, int protocol) {
@@ -1038,8 +1052,7 @@ int tgpu_transcode_batch(tgpu_context* ctx, const tgpu_schema* schema, int from_
   }
   // records and list elements stay in HBM between the passes (grow-only)
   const uint64_t rs = schema->structs[0].size;
-  const uint64_t acap =
-      schema->has_lists ? in_len * (from_protocol == TGPU_PROTOCOL_BINARY ? 1 : 8) : 0;
+  const uint64_t acap = in_len * tgpu_schema_arena_scale(schema, from_protocol);
   int rc = grow(ctx->d_xrec, ctx->xrec_bytes, std::max<uint64_t>(n * rs, 16));
   if (!rc && acap) rc = grow(ctx->d_xarena, ctx->xarena_bytes, acap);
   if (rc) {

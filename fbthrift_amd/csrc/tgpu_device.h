@@ -34,6 +34,10 @@ __device__ __forceinline__ uint32_t scalar_size(uint32_t t) {
          : (t == TGPU_T_I32 || t == TGPU_T_FLOAT) ? 4
                                                   : 8;
 }
+// Container elements: scalars in native layout, strings as tgpu_span.
+__device__ __forceinline__ uint32_t elem_size(uint32_t t) {
+  return t == TGPU_T_STRING ? 16 : scalar_size(t);
+}
 // CompactProtocol-inl.h:48-86
 __device__ __forceinline__ uint32_t ctype_to_ttype(uint32_t ct) {
   // packed nibble table for ct 0..13
@@ -487,9 +491,35 @@ __device__ __forceinline__ void zero_bytes(uint8_t* p, uint32_t n) {
   for (uint32_t b = 0; b < n; ++b) p[b] = 0;
 }
 
+// One container element: a scalar, or a string as a span into the stream
+// (the string field rule, Protocol.h:96-99).
+template <int P>
+__device__ __forceinline__ void read_elem(Reader& r, uint32_t t, uint8_t* dst) {
+  if (t == TGPU_T_STRING) {
+    uint64_t v = 0;
+    uint32_t l = 0;
+    Proto<P>::read_string(r, v, l);
+    if (r.ok()) {
+      const tgpu_span e{l ? v : 0, l, 0};
+      const uint8_t* b = (const uint8_t*)&e;
+      for (uint32_t k = 0; k < 16; ++k) dst[k] = b[k];
+    }
+    return;
+  }
+  Proto<P>::read_scalar(r, t, dst);
+}
+
+// Arena slots: scale x (wire position of the first element). Scalars need
+// scale 1 (Binary) / 8 (Compact); 16-byte string spans from >= 4 (Binary) or
+// >= 1 (Compact) wire bytes need 4 / 16.
+template <int P>
+__device__ __forceinline__ uint64_t arena_scale(const DevSchema& sc) {
+  return sc.str_elems ? (P == TGPU_PROTOCOL_BINARY ? 4 : 16) : Proto<P>::kArenaScale;
+}
+
 template <int P>
 __device__ void read_list(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8_t* arena,
-                          uint64_t arena_cap) {
+                          uint64_t arena_cap, uint64_t scale) {
   using Pr = Proto<P>;
   tgpu_span sp{0, 0, 0};
   *(tgpu_span*)m = sp;
@@ -508,12 +538,12 @@ __device__ void read_list(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8
     }
   } else {
     if (r.end - r.pos < (uint64_t)(uint32_t)n) return r.fail(TGPU_ERR_TRUNCATED, r.pos);
-    const uint32_t es = scalar_size(f.elem_ttype);
-    const uint64_t aoff = Pr::kArenaScale * r.pos;
+    const uint32_t es = elem_size(f.elem_ttype);
+    const uint64_t aoff = scale * r.pos;
     if (n > 0 && !arena && arena_cap == kDiscardArena) {
       // measuring only (stream indexer): validate and consume, store nothing
-      uint8_t tmp[8];
-      for (int32_t i = 0; i < n && r.ok(); ++i) Pr::read_scalar(r, f.elem_ttype, tmp);
+      uint8_t tmp[16];
+      for (int32_t i = 0; i < n && r.ok(); ++i) read_elem<P>(r, f.elem_ttype, tmp);
     } else if (n > 0) {
       if (!arena) return r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
       // the list is resized to n before the element reads
@@ -525,8 +555,8 @@ __device__ void read_list(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8
         // read first: a truncated stream fails as the reader does, and an
         // element that was read always fits an arena of the documented size
         const uint64_t at = aoff + (uint64_t)i * es;
-        uint8_t tmp[8];
-        Pr::read_scalar(r, f.elem_ttype, tmp);
+        uint8_t tmp[16];
+        read_elem<P>(r, f.elem_ttype, tmp);
         if (!r.ok()) break;
         if (at + es > arena_cap) {
           r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
@@ -556,7 +586,7 @@ __device__ void read_list(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8
 // pair that was read always fits an arena of the documented size.
 template <int P>
 __device__ void read_map(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8_t* arena,
-                         uint64_t arena_cap) {
+                         uint64_t arena_cap, uint64_t scale) {
   using Pr = Proto<P>;
   tgpu_span sp{0, 0, 0};
   *(tgpu_span*)m = sp;
@@ -578,16 +608,16 @@ __device__ void read_map(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8_
     }
   } else {
     if ((r.end - r.pos) / 2 < (uint64_t)(uint32_t)n) return r.fail(TGPU_ERR_TRUNCATED, r.pos);
-    const uint32_t ks = scalar_size(f.elem_ttype), ps = ks + scalar_size(f.val_ttype);
-    const uint64_t aoff = Pr::kArenaScale * r.pos;
+    const uint32_t ks = elem_size(f.elem_ttype), ps = ks + elem_size(f.val_ttype);
+    const uint64_t aoff = scale * r.pos;
     const bool discard = !arena && arena_cap == kDiscardArena;
     if (n > 0 && !arena && !discard) return r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
     int32_t i = 0;
     for (; i < n; ++i) {
-      uint8_t pr[16];
-      Pr::read_scalar(r, f.elem_ttype, pr);
+      uint8_t pr[32];
+      read_elem<P>(r, f.elem_ttype, pr);
       if (!r.ok()) break;
-      Pr::read_scalar(r, f.val_ttype, pr + ks);
+      read_elem<P>(r, f.val_ttype, pr + ks);
       if (!r.ok()) break;
       if (discard) continue;
       const uint64_t at = aoff + (uint64_t)i * ps;
@@ -666,9 +696,9 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, uint8_
       st[sp++] = ReadFrame{(uint32_t)f.struct_index, fr.obj + f.member_offset, 0, 0, 0};
       continue;  // isset set when the nested STOP is reached
     } else if (f.ttype == TGPU_T_MAP) {
-      read_map<P>(r, f, m, arena, arena_cap);
+      read_map<P>(r, f, m, arena, arena_cap, arena_scale<P>(sc));
     } else {
-      read_list<P>(r, f, m, arena, arena_cap);
+      read_list<P>(r, f, m, arena, arena_cap, arena_scale<P>(sc));
     }
     if (r.ok()) rec[fr.obj + f.isset_offset] = 1;
   }
@@ -738,6 +768,20 @@ __device__ __forceinline__ void write_scalar(Writer& w, uint32_t t, const uint8_
         break;
     }
   }
+}
+
+// One container element: a scalar, or a string span into string_base.
+template <int P>
+__device__ __forceinline__ void write_elem(Writer& w, uint32_t t, const uint8_t* p,
+                                           const uint8_t* sbase) {
+  if (t != TGPU_T_STRING) return write_scalar<P>(w, t, p);
+  tgpu_span e;
+  uint8_t* b = (uint8_t*)&e;
+  for (uint32_t k = 0; k < 16; ++k) b[k] = p[k];
+  if (e.length > 0x7fffffffu) return w.fail(TGPU_ERR_WRITE_SIZE_LIMIT, w.pos);  // checkBinarySize
+  if (P == TGPU_PROTOCOL_BINARY) w.put_be(e.length, 4);
+  else w.varint(e.length);
+  w.bytes(sbase + e.offset, e.length);
 }
 
 // op::isEmpty of a terse member (Clear.h:98-127): scalars by identity with
@@ -838,11 +882,11 @@ __device__ void write_record(Writer& w, const DevSchema& sc, const uint8_t* rec,
         w.varint(sp_.length);
         w.put((ttype_to_ctype(f.elem_ttype) << 4) | ttype_to_ctype(f.val_ttype));
       }
-      const uint32_t ks = scalar_size(f.elem_ttype), ps = ks + scalar_size(f.val_ttype);
+      const uint32_t ks = elem_size(f.elem_ttype), ps = ks + elem_size(f.val_ttype);
       const uint8_t* e = lbase + sp_.offset;
       for (uint32_t i = 0; i < sp_.length && w.ok(); ++i) {
-        write_scalar<P>(w, f.elem_ttype, e + (uint64_t)i * ps);
-        write_scalar<P>(w, f.val_ttype, e + (uint64_t)i * ps + ks);
+        write_elem<P>(w, f.elem_ttype, e + (uint64_t)i * ps, sbase);
+        if (w.ok()) write_elem<P>(w, f.val_ttype, e + (uint64_t)i * ps + ks, sbase);
       }
     } else {  // list / set of scalars
       const tgpu_span sp_ = *(const tgpu_span*)m;
@@ -859,9 +903,10 @@ __device__ void write_record(Writer& w, const DevSchema& sc, const uint8_t* rec,
           w.varint(sp_.length);
         }
       }
-      const uint32_t es = scalar_size(f.elem_ttype);
+      const uint32_t es = elem_size(f.elem_ttype);
       const uint8_t* e = lbase + sp_.offset;
-      for (uint32_t i = 0; i < sp_.length && w.ok(); ++i) write_scalar<P>(w, f.elem_ttype, e + (uint64_t)i * es);
+      for (uint32_t i = 0; i < sp_.length && w.ok(); ++i)
+        write_elem<P>(w, f.elem_ttype, e + (uint64_t)i * es, sbase);
     }
   }
 }

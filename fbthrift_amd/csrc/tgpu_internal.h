@@ -172,6 +172,8 @@ struct DevSchema {
   const tgpu_struct_desc* s;
   const tgpu_field_desc* f;
   uint32_t ns, nf;
+  uint32_t str_elems;  // some list/set/map holds strings: arena scale 4 / 16
+  uint32_t pad_;
 };
 
 struct DecodeArgs {

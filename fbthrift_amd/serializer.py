@@ -225,9 +225,8 @@ class BatchSerializer:
 
     # -- decode ---------------------------------------------------------------
     def arena_bytes(self, gschema, in_len):
-        if not gschema.has_lists:
-            return 0
-        return in_len * (1 if self.protocol == PROTOCOL_BINARY else 8)
+        """List arena a decode of in_len bytes needs (tgpu_schema_arena_scale)."""
+        return in_len * _lib.lib().tgpu_schema_arena_scale(gschema.handle, self.protocol)
 
     def deserialize(self, gschema, wire, n, offsets=None, limits=None, records=None,
                     arena=None, stream=None, sync=True):

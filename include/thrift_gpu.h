@@ -110,11 +110,12 @@ enum tgpu_qualifier {
  * One field of a struct, in IDL declaration order (= serialization order,
  * thrift/compiler/generate/t_whisker_generator.cc:231-236).
  *   ttype        T_BOOL..T_FLOAT scalar, T_STRING (binary/string), T_STRUCT,
- *                T_LIST or T_SET of a scalar element type, T_MAP of scalar
- *                key and value types.
- *   elem_ttype   element type for T_LIST/T_SET, key type for T_MAP (scalar),
- *                else 0.
- *   val_ttype    value type for T_MAP (scalar), else 0.
+ *                T_LIST or T_SET of a scalar or string element type, T_MAP
+ *                of scalar or string key and value types.
+ *   elem_ttype   element type for T_LIST/T_SET, key type for T_MAP, else 0.
+ *   val_ttype    value type for T_MAP, else 0.
+ * A string inside a container is a tgpu_span (like a string field); the
+ * list arena then needs tgpu_schema_arena_scale bytes per input byte.
  *   struct_index nested struct (index into the schema's struct table) for
  *                T_STRUCT, else -1.
  */
@@ -251,6 +252,11 @@ int tgpu_schema_create(const tgpu_struct_desc* structs, uint32_t n_structs,
 void tgpu_schema_destroy(tgpu_schema* schema);
 /* sizeof(record) of the root struct. */
 uint32_t tgpu_schema_record_size(const tgpu_schema* schema);
+/* List arena bytes a decode needs per input byte: 0 without lists/sets/
+ * maps; 1 Binary / 8 Compact for scalar elements; 4 Binary / 16 Compact
+ * when some container holds strings (16-byte spans). */
+uint32_t tgpu_schema_arena_scale(const tgpu_schema* schema, int protocol);
+
 /* Canonical wire length of every record if it is fixed for `protocol`
  * (Binary with only fixed-width fields), else 0. */
 uint64_t tgpu_schema_fixed_wire_size(const tgpu_schema* schema, int protocol);
@@ -321,8 +327,9 @@ int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol
  * means records are read back to back from offset 0 like repeated
  * deserialize<T>(Cursor&). Records are default-initialized (zero, isset 0)
  * before reading. List elements are written to list_arena (capacity
- * list_arena_capacity bytes; required size: in_len for Binary,
- * 8 * in_len for Compact/CompactV1, 0 when the schema has no lists/maps).
+ * list_arena_capacity bytes; required size: in_len x tgpu_schema_arena_scale
+ * — in_len Binary / 8 * in_len Compact for scalar elements, 0 without
+ * lists/sets/maps).
  * limits may be NULL (reference defaults).
  * If st != NULL the call waits and fills st, *n_decoded (records fully
  * decoded before the first failure) and *consumed (bytes consumed by them).

@@ -114,7 +114,11 @@ def decode(schema, protocol, wire, n, offsets=None, limits=None, arena_cap=None)
     w = _u8(wire)
     rec = np.zeros(max(n * schema.record_size, 1), np.uint8)
     if arena_cap is None:
-        arena_cap = w.size * (1 if protocol == 0 else 8)
+        str_elems = any(f.ttype in (13, 14, 15) and (f.elem_ttype == 11 or
+                                                      (f.ttype == 13 and f.val_ttype == 11))
+                        for st_ in schema.structs for f in st_.fields)
+        arena_cap = w.size * ((4 if protocol == 0 else 16) if str_elems else
+                              (1 if protocol == 0 else 8))
     arena = np.zeros(max(arena_cap, 1), np.uint8)
     offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
     lim = Limits(*limits) if limits is not None else None

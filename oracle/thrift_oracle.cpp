@@ -527,7 +527,31 @@ struct DecodeCtx {
   const Schema* sc;
   uint8_t* arena;
   uint64_t arena_cap;
+  uint64_t scale;  // arena bytes per wire byte: 1/8, or 4/16 with string elements
 };
+
+bool has_string_elems(const Schema& sc) {
+  for (uint32_t k = 0; k < sc.nf; ++k) {
+    const tgpu_field_desc& f = sc.f[k];
+    const bool container = f.ttype == TGPU_T_LIST || f.ttype == TGPU_T_SET || f.ttype == TGPU_T_MAP;
+    if (container && (f.elem_ttype == TGPU_T_STRING ||
+                      (f.ttype == TGPU_T_MAP && f.val_ttype == TGPU_T_STRING)))
+      return true;
+  }
+  return false;
+}
+
+uint32_t elem_size(uint8_t t) { return t == TGPU_T_STRING ? 16 : scalar_size(t); }
+
+// A container element: a scalar, or a string as a span into the stream.
+template <class R>
+void readElem(R& r, uint8_t t, uint8_t* dst) {
+  if (t != TGPU_T_STRING) return r.readScalar(t, dst);
+  tgpu_span sp{0, 0, 0};
+  r.readString(sp.offset, sp.length);
+  if (sp.length == 0) sp.offset = 0;
+  std::memcpy(dst, &sp, sizeof(sp));
+}
 
 template <class R>
 void readList(R& r, const tgpu_field_desc& f, uint8_t* member, DecodeCtx& dc) {
@@ -542,8 +566,8 @@ void readList(R& r, const tgpu_field_desc& f, uint8_t* member, DecodeCtx& dc) {
     r.skip_n((uint32_t)n, &reported, 1, 0);
   } else {
     if (!r.c.canAdvance((uint64_t)(uint32_t)n)) fail(TGPU_ERR_TRUNCATED, r.c.pos);  // canReadNElements
-    const uint32_t es = scalar_size(f.elem_ttype);
-    const uint64_t aoff = R::kArenaScale * r.c.pos;
+    const uint32_t es = elem_size(f.elem_ttype);
+    const uint64_t aoff = dc.scale * r.c.pos;
     if (n > 0) {
       if (!dc.arena) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
       // resizeWithoutInitialization(out, n) happens before the element reads
@@ -557,8 +581,8 @@ void readList(R& r, const tgpu_field_desc& f, uint8_t* member, DecodeCtx& dc) {
         // read first: truncation fails as the reader does (the arena always
         // holds an element that was read when sized as documented)
         const uint64_t at = aoff + (uint64_t)i * es;
-        uint8_t tmp[8];
-        r.readScalar(f.elem_ttype, tmp);
+        uint8_t tmp[16];
+        readElem(r, f.elem_ttype, tmp);
         if (at + es > dc.arena_cap) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
         std::memcpy(dc.arena + at, tmp, es);
       }
@@ -591,15 +615,15 @@ void readMap(R& r, const tgpu_field_desc& f, uint8_t* member, DecodeCtx& dc) {
     r.skip_n((uint32_t)n, kv, 2, 0);
   } else {
     if (!r.c.canAdvance((uint64_t)(uint32_t)n * 2)) fail(TGPU_ERR_TRUNCATED, r.c.pos);
-    const uint32_t ks = scalar_size(f.elem_ttype), ps = ks + scalar_size(f.val_ttype);
-    const uint64_t aoff = R::kArenaScale * r.c.pos;
+    const uint32_t ks = elem_size(f.elem_ttype), ps = ks + elem_size(f.val_ttype);
+    const uint64_t aoff = dc.scale * r.c.pos;
     if (n > 0 && !dc.arena) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
     int32_t i = 0;
     try {
       for (; i < n; ++i) {
-        uint8_t pr[16];
-        r.readScalar(f.elem_ttype, pr);
-        r.readScalar(f.val_ttype, pr + ks);
+        uint8_t pr[32];
+        readElem(r, f.elem_ttype, pr);
+        readElem(r, f.val_ttype, pr + ks);
         const uint64_t at = aoff + (uint64_t)i * ps;
         if (at + ps > dc.arena_cap) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
         std::memcpy(dc.arena + at, pr, ps);
@@ -683,7 +707,8 @@ int decode_impl(const Schema& sc, const uint8_t* in, uint64_t in_len,
                 const uint64_t* offsets, uint64_t n, uint8_t* recs,
                 uint8_t* arena, uint64_t arena_cap, const Limits& lim,
                 tgpu_status* st, uint64_t* n_dec, uint64_t* consumed) {
-  DecodeCtx dc{&sc, arena, arena_cap};
+  DecodeCtx dc{&sc, arena, arena_cap,
+               has_string_elems(sc) ? (R::kArenaScale == 1 ? 4u : 16u) : R::kArenaScale};
   uint64_t pos = offsets ? offsets[0] : 0;
   const uint32_t rs = sc.s[0].size;
   for (uint64_t i = 0; i < n; ++i) {
@@ -786,6 +811,7 @@ T ld(const uint8_t* p) {
 // (serialize_struct.whisker:40-67; gen/module_types_tcc.h:106-121).
 struct BinaryWriter {
   Sink s;
+  void stringLen(uint32_t n) { s.putBE(n, 4); }
   void scalar(uint8_t t, const uint8_t* p) {
     switch (t) {
       case TGPU_T_BOOL: s.put(load_bool_checked(p, s.pos)); break;
@@ -798,12 +824,21 @@ struct BinaryWriter {
   // encodeMapElements: key then value per pair, in the given order
   // (protocol_methods.h:693-701).
   void pairs(const EncodeCtx& ec, const tgpu_field_desc& f, const tgpu_span& sp) {
-    const uint32_t ks = scalar_size(f.elem_ttype), ps = ks + scalar_size(f.val_ttype);
+    const uint32_t ks = elem_size(f.elem_ttype), ps = ks + elem_size(f.val_ttype);
     const uint8_t* e = ec.lbase + sp.offset;
     for (uint32_t i = 0; i < sp.length; ++i) {
-      scalar(f.elem_ttype, e + (uint64_t)i * ps);
-      scalar(f.val_ttype, e + (uint64_t)i * ps + ks);
+      elem(ec, f.elem_ttype, e + (uint64_t)i * ps);
+      elem(ec, f.val_ttype, e + (uint64_t)i * ps + ks);
     }
+  }
+  // a container element: scalar, or a string span into string_base
+  // (writeBinary: checkBinarySize then the length and bytes)
+  void elem(const EncodeCtx& ec, uint8_t t, const uint8_t* p) {
+    if (t != TGPU_T_STRING) return scalar(t, p);
+    const tgpu_span sp = ld<tgpu_span>(p);
+    if (sp.length > 0x7fffffffu) fail(TGPU_ERR_WRITE_SIZE_LIMIT, s.pos);
+    stringLen(sp.length);
+    s.putBytes(ec.sbase + sp.offset, sp.length);
   }
   void structure(const EncodeCtx& ec, uint32_t si, const uint8_t* obj) {
     const tgpu_struct_desc& sd = ec.sc->s[si];
@@ -837,9 +872,9 @@ struct BinaryWriter {
         if (sp.length > 0x7fffffffu) fail(TGPU_ERR_WRITE_SIZE_LIMIT, s.pos);
         s.put(f.elem_ttype);
         s.putBE(sp.length, 4);
-        const uint32_t es = scalar_size(f.elem_ttype);
+        const uint32_t es = elem_size(f.elem_ttype);
         for (uint32_t i = 0; i < sp.length; ++i)
-          scalar(f.elem_ttype, ec.lbase + sp.offset + (uint64_t)i * es);
+          elem(ec, f.elem_ttype, ec.lbase + sp.offset + (uint64_t)i * es);
       }
     }
     s.put(TGPU_T_STOP);  // writeFieldStop
@@ -851,6 +886,7 @@ struct BinaryWriter {
 template <bool kV1>
 struct CompactWriterT {
   Sink s;
+  void stringLen(uint32_t n) { s.varint(n); }
   void fieldHeader(uint8_t ctype, int16_t id, int16_t& last) {  // :133-160
     if (id > last && id - last <= 15) {
       s.put((uint8_t)(((id - last) << 4) | ctype));
@@ -876,12 +912,21 @@ struct CompactWriterT {
   // encodeMapElements: key then value per pair, in the given order
   // (protocol_methods.h:693-701).
   void pairs(const EncodeCtx& ec, const tgpu_field_desc& f, const tgpu_span& sp) {
-    const uint32_t ks = scalar_size(f.elem_ttype), ps = ks + scalar_size(f.val_ttype);
+    const uint32_t ks = elem_size(f.elem_ttype), ps = ks + elem_size(f.val_ttype);
     const uint8_t* e = ec.lbase + sp.offset;
     for (uint32_t i = 0; i < sp.length; ++i) {
-      scalar(f.elem_ttype, e + (uint64_t)i * ps);
-      scalar(f.val_ttype, e + (uint64_t)i * ps + ks);
+      elem(ec, f.elem_ttype, e + (uint64_t)i * ps);
+      elem(ec, f.val_ttype, e + (uint64_t)i * ps + ks);
     }
+  }
+  // a container element: scalar, or a string span into string_base
+  // (writeBinary: checkBinarySize then the length and bytes)
+  void elem(const EncodeCtx& ec, uint8_t t, const uint8_t* p) {
+    if (t != TGPU_T_STRING) return scalar(t, p);
+    const tgpu_span sp = ld<tgpu_span>(p);
+    if (sp.length > 0x7fffffffu) fail(TGPU_ERR_WRITE_SIZE_LIMIT, s.pos);
+    stringLen(sp.length);
+    s.putBytes(ec.sbase + sp.offset, sp.length);
   }
   void structure(const EncodeCtx& ec, uint32_t si, const uint8_t* obj) {
     const tgpu_struct_desc& sd = ec.sc->s[si];
@@ -928,9 +973,9 @@ struct CompactWriterT {
           s.put((uint8_t)(0xf0 | ct));
           s.varint(sp.length);
         }
-        const uint32_t es = scalar_size(f.elem_ttype);
+        const uint32_t es = elem_size(f.elem_ttype);
         for (uint32_t i = 0; i < sp.length; ++i)
-          scalar(f.elem_ttype, ec.lbase + sp.offset + (uint64_t)i * es);
+          elem(ec, f.elem_ttype, ec.lbase + sp.offset + (uint64_t)i * es);
       }
     }
     s.put(0);  // writeFieldStop

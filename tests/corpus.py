@@ -151,6 +151,7 @@ def cases():
     out.append(("compact_mid_failure", C, two, goodc * 7 + badc + goodc, 9, None, VARINT))
     out += map_cases()
     out += union_cases()
+    out += string_elem_cases()
     return out
 
 
@@ -280,4 +281,28 @@ def union_cases():
         r3 = W(p).field(I64, 1).i64(1).field(I32, 2).i32(2).stop().bytes()
         out.append(("%s_root_union" % pn, p, ROOT_UNION, r1 + r2 + r1, 3, None, OK))
         out.append(("%s_root_union_two" % pn, p, ROOT_UNION, r1 + r3, 2, None, UNION_MISSING_STOP))
+    return out
+
+
+LSTR = [[[1, LIST, STR, 0, -1], [2, MAP, STR, 0, -1, I32], [3, I32, 0, 0, -1]]]
+
+
+def string_elem_cases():
+    """Strings inside containers: each element read as a string field is
+    (readString: size checks, canAdvance -> TRUNCATED), the container's
+    canReadNElements counts one byte per element (two per pair)."""
+    out = []
+    for p, pn in ((B, "binary"), (C, "compact")):
+        ok = W(p).field(LIST, 1).list_begin(STR, 3).string(b"ab").string(b"").string(b"xyz") \
+            .field(MAP, 2).map_begin(STR, I32, 2).string(b"k").i32(1).string(b"").i32(-2) \
+            .field(I32, 3).i32(5).stop().bytes()
+        out.append(("%s_strlist_ok" % pn, p, LSTR, ok, 1, None, OK))
+        for cut in range(3, len(ok) - 1, 2):
+            out.append(("%s_strlist_cut_%d" % (pn, cut), p, LSTR, ok[:cut], 1, None, None))
+        out.append(("%s_strlist_limit" % pn, p, LSTR, ok, 1, (2, 0, 12000, 0), LIMIT))
+        # a list of i32 where strings are expected: skipped, no error
+        mm = W(p).field(LIST, 1).list_begin(I32, 2).i32(1).i32(2).stop().bytes()
+        out.append(("%s_strlist_mismatch" % pn, p, LSTR, mm, 1, None, OK))
+    neg = W(B).field(LIST, 1).list_begin(STR, 1).raw(b"\xff\xff\xff\xfe").stop().bytes()
+    out.append(("binary_strlist_negative", B, LSTR, neg, 1, None, NEG))
     return out

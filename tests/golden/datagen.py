@@ -106,6 +106,13 @@ SCHEMAS = {
             [20, T_MAP, T_I16, 0, -1, T_I16]]},
         [[1, T_I32, 0, 0, -1], [2, T_MAP, T_I16, 0, -1, T_I16]],
     ],
+    # strings inside containers (tgpu_span elements)
+    "strcont": [
+        [[1, T_LIST, T_STRING, 0, -1], [2, T_MAP, T_STRING, 0, -1, T_I64],
+         [3, T_MAP, T_I32, 0, -1, T_STRING], [4, T_SET, T_STRING, 0, -1],
+         [5, T_STRING, 0, 0, -1], [6, T_MAP, T_STRING, 0, -1, T_STRING],
+         [7, T_LIST, T_I16, 0, -1]],
+    ],
     "sparse": [[[5, T_I32, 0, 1, -1], [-3, T_I64, 0, 0, -1], [40, T_STRING, 0, 1, -1],
                 [300, T_BOOL, 0, 0, -1], [20, T_DOUBLE, 0, 1, -1], [21, T_I16, 0, 0, -1]]],
 }
@@ -265,6 +272,23 @@ def gen_unions(i):
     return [s32(r[5]), union(0), union(3), s64(r[6])]
 
 
+def gen_strcont(i):
+    r = [splitmix64_at(SEED + 41, 16 * i + k) for k in range(16)]
+
+    def word(k, j):
+        x = splitmix64_at(SEED + 42, 64 * i + 8 * k + j)
+        return bytes(97 + (x >> (5 * t)) % 26 for t in range(x % 9))
+
+    big = i % 40 == 11
+    return [[word(0, j) for j in range(20 if big else r[0] % 6)],
+            [(word(1, j), s64(r[1 + j % 3])) for j in range(r[4] % 4)],
+            [(s32(r[5]) + j, word(2, j)) for j in range(r[6] % 4)],
+            [word(3, j) for j in range(r[7] % 3)],
+            word(4, 0),
+            [(word(5, j), word(6, j)) for j in range(r[8] % 3)],
+            [j - 2 for j in range(r[9] % 5)]]
+
+
 ORIGINAL = [True, False, 50, 1200, 1300, 1600, 1.0, [0], b"def", [0]]
 UPDATED = [True, False, False, True, False, 50, 1100, 1200, 1300, 1400, 1500,
            1600, 1.0, b"abc", [0], [1], b"def", b"ghi", [0], [1]]
@@ -291,6 +315,15 @@ def flatten_values(schema, records):
             return int(bool(v))
         return v
 
+    def column(key, t, items):
+        # container elements: scalars as one column; strings as
+        # <key>.len (u32 per element) + <key>.data (bytes)
+        if t == T_STRING:
+            out.setdefault(key + ".len", []).extend(len(e) for e in items)
+            out.setdefault(key + ".data", []).extend(b for e in items for b in e)
+        else:
+            out.setdefault(key, []).extend(scalar_repr(t, e) for e in items)
+
     def walk(sidx, vals, prefix):
         for k, row in enumerate(rows(schema, sidx)):
             fid, ttype, elem, qual, sub = row[:5]
@@ -304,14 +337,11 @@ def flatten_values(schema, records):
                 out.setdefault(key + ".data", []).extend(v or b"")
             elif ttype == T_MAP:
                 put(key + ".count", 0 if v is None else len(v))
-                out.setdefault(key + ".keys", []).extend(
-                    [scalar_repr(elem, a) for a, _ in (v or [])])
-                out.setdefault(key + ".vals", []).extend(
-                    [scalar_repr(row[5], b) for _, b in (v or [])])
+                column(key + ".keys", elem, [a for a, _ in (v or [])])
+                column(key + ".vals", row[5], [b for _, b in (v or [])])
             elif ttype in (T_LIST, T_SET):
                 put(key + ".count", 0 if v is None else len(v))
-                out.setdefault(key + ".elems", []).extend(
-                    [scalar_repr(elem, e) for e in (v or [])])
+                column(key + ".elems", elem, v or [])
             else:
                 put(key + ".val", 0 if v is None else scalar_repr(ttype, v))
 
@@ -333,7 +363,7 @@ def flatten_values(schema, records):
 
     for key, lst in out.items():
         path, kind = key.rsplit(".", 1)
-        f = ftype(path)
+        f = ftype(path) if kind in ("elems", "keys", "vals", "val") else None
         if kind in ("set",):
             arrays[key] = np.array(lst, dtype=np.uint8)
         elif kind in ("len", "count"):

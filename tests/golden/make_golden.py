@@ -138,6 +138,8 @@ CASES = [
     ("maps_compact", "maps", "compact", gen_maps, 300),
     ("unions_binary", "unions", "binary", gen_unions, 200),
     ("unions_compact", "unions", "compact", gen_unions, 200),
+    ("strcont_binary", "strcont", "binary", gen_strcont, 200),
+    ("strcont_compact", "strcont", "compact", gen_strcont, 200),
     ("scalars_compact_v1", "scalars", "compact_v1", gen_scalars, 300),
     ("nested_compact_v1", "nested", "compact_v1", gen_nested, 500),
     ("maps_compact_v1", "maps", "compact_v1", gen_maps, 100),

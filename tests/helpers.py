@@ -67,11 +67,36 @@ def _view(rec, schema, path):
         si = schema.struct_index(f.struct)
 
 
+SPAN_NP = np.dtype([("offset", "<u8"), ("length", "<u4"), ("reserved", "<u4")])
+
+
+def _esize(t):
+    return 16 if t == T_STRING else SCALAR[t]
+
+
 def pack(schema, values, n):
     """Columnar values -> (records u8 array, string arena, list arena)."""
     rec = np.zeros(n, dtype=schema.dtype())
     sarena, larena = [], []
-    spos, lpos = 0, 0
+    pos = {"s": 0, "l": 0}
+
+    def strings(lens, data):
+        """Spans of consecutive strings appended to the string arena."""
+        lens = np.asarray(lens, dtype=np.uint64)
+        starts = pos["s"] + np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+        sarena.append(np.asarray(data, dtype=np.uint8))
+        pos["s"] += int(lens.sum())
+        return np.where(lens > 0, starts, 0), lens
+
+    def column(key, t, total):
+        """(total, element size) bytes of one element column."""
+        if t == T_STRING:
+            off, lens = strings(values[key + ".len"], values[key + ".data"])
+            sp = np.zeros(total, SPAN_NP)
+            sp["offset"], sp["length"] = off, lens
+            return sp.view(np.uint8).reshape(total, 16)
+        return np.ascontiguousarray(values[key]).view(np.uint8).reshape(total, SCALAR[t])
+
     for path, f in _paths(schema):
         key = _key(path)
         arr, f, si, k = _view(rec, schema, path)
@@ -85,33 +110,24 @@ def pack(schema, values, n):
             else:
                 arr[f.name] = v
         elif f.ttype == T_STRING:
-            lens = values[key + ".len"].astype(np.uint64)
-            starts = spos + np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
-            arr[f.name]["offset"] = np.where(lens > 0, starts, 0)
-            arr[f.name]["length"] = lens
-            sarena.append(values[key + ".data"].astype(np.uint8))
-            spos += int(lens.sum())
-        elif f.ttype in (T_LIST, T_SET):
+            off, lens = strings(values[key + ".len"], values[key + ".data"])
+            arr[f.name]["offset"], arr[f.name]["length"] = off, lens
+        elif f.ttype in (T_LIST, T_SET, T_MAP):
             cnt = values[key + ".count"].astype(np.uint64)
-            es = SCALAR[f.elem_ttype]
-            starts = lpos + es * np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.uint64)
-            arr[f.name]["offset"] = np.where(cnt > 0, starts, 0)
-            arr[f.name]["length"] = cnt
-            el = values[key + ".elems"]
-            larena.append(np.ascontiguousarray(el).view(np.uint8))
-            lpos += int(cnt.sum()) * es
-        elif f.ttype == T_MAP:
-            # packed {key, value} pairs (the tgpu_span map form)
-            cnt = values[key + ".count"].astype(np.uint64)
-            ks, vs = SCALAR[f.elem_ttype], SCALAR[f.val_ttype]
             tot = int(cnt.sum())
-            kb = np.ascontiguousarray(values[key + ".keys"]).view(np.uint8).reshape(tot, ks)
-            vb = np.ascontiguousarray(values[key + ".vals"]).view(np.uint8).reshape(tot, vs)
-            starts = lpos + (ks + vs) * np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.uint64)
+            if f.ttype == T_MAP:
+                # packed {key, value} pairs (the tgpu_span map form)
+                el = np.concatenate([column(key + ".keys", f.elem_ttype, tot),
+                                     column(key + ".vals", f.val_ttype, tot)], axis=1)
+                es = _esize(f.elem_ttype) + _esize(f.val_ttype)
+            else:
+                el = column(key + ".elems", f.elem_ttype, tot)
+                es = _esize(f.elem_ttype)
+            starts = pos["l"] + es * np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.uint64)
             arr[f.name]["offset"] = np.where(cnt > 0, starts, 0)
             arr[f.name]["length"] = cnt
-            larena.append(np.concatenate([kb, vb], axis=1).reshape(-1))
-            lpos += tot * (ks + vs)
+            larena.append(el.reshape(-1))
+            pos["l"] += tot * es
     s = np.concatenate(sarena) if sarena else np.zeros(0, np.uint8)
     l = np.concatenate(larena) if larena else np.zeros(0, np.uint8)
     return rec.view(np.uint8).reshape(-1), s, l
@@ -125,6 +141,20 @@ def unpack(schema, rec_bytes, n, wire, arena):
     w = np.frombuffer(bytes(wire), dtype=np.uint8)
     ar = np.ascontiguousarray(arena).view(np.uint8).reshape(-1)
     out = {}
+
+    def strings(key, offs, lens):
+        out[key + ".len"] = np.asarray(lens, dtype=np.uint32)
+        parts = [w[o:o + l] for o, l in zip(np.asarray(offs).tolist(), np.asarray(lens).tolist())]
+        out[key + ".data"] = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+
+    def column(key, t, b):
+        """b: (total, element size) bytes of one element column."""
+        if t == T_STRING:
+            sp = np.ascontiguousarray(b).reshape(-1).view(SPAN_NP)
+            strings(key, sp["offset"], sp["length"])
+        else:
+            out[key] = np.ascontiguousarray(b).reshape(-1).view(ELEM_NP[t])
+
     for path, f in _paths(schema):
         key = _key(path)
         arr, f, si, k = _view(rec, schema, path)
@@ -138,25 +168,19 @@ def unpack(schema, rec_bytes, n, wire, arena):
             out[key + ".val"] = v.copy()
         elif f.ttype == T_STRING:
             sp = arr[f.name]
-            out[key + ".len"] = sp["length"].astype(np.uint32)
-            parts = [w[o:o + l] for o, l in zip(sp["offset"].tolist(), sp["length"].tolist())]
-            out[key + ".data"] = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
-        elif f.ttype in (T_LIST, T_SET):
+            strings(key, sp["offset"], sp["length"])
+        elif f.ttype in (T_LIST, T_SET, T_MAP):
             sp = arr[f.name]
-            es = SCALAR[f.elem_ttype]
+            ks = _esize(f.elem_ttype)
+            es = ks + (_esize(f.val_ttype) if f.ttype == T_MAP else 0)
             out[key + ".count"] = sp["length"].astype(np.uint32)
             parts = [ar[o:o + l * es] for o, l in zip(sp["offset"].tolist(), sp["length"].tolist())]
-            el = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
-            out[key + ".elems"] = el.view(ELEM_NP[f.elem_ttype])
-        elif f.ttype == T_MAP:
-            sp = arr[f.name]
-            ks, vs = SCALAR[f.elem_ttype], SCALAR[f.val_ttype]
-            out[key + ".count"] = sp["length"].astype(np.uint32)
-            parts = [ar[o:o + l * (ks + vs)] for o, l in
-                     zip(sp["offset"].tolist(), sp["length"].tolist())]
-            pr = (np.concatenate(parts) if parts else np.zeros(0, np.uint8)).reshape(-1, ks + vs)
-            out[key + ".keys"] = np.ascontiguousarray(pr[:, :ks]).view(ELEM_NP[f.elem_ttype]).reshape(-1)
-            out[key + ".vals"] = np.ascontiguousarray(pr[:, ks:]).view(ELEM_NP[f.val_ttype]).reshape(-1)
+            el = (np.concatenate(parts) if parts else np.zeros(0, np.uint8)).reshape(-1, es)
+            if f.ttype == T_MAP:
+                column(key + ".keys", f.elem_ttype, el[:, :ks])
+                column(key + ".vals", f.val_ttype, el[:, ks:])
+            else:
+                column(key + ".elems", f.elem_ttype, el)
     return out
 
 

@@ -28,8 +28,8 @@ T_MAP, T_I32, T_STRING, T_LIST = 13, 8, 11, 15
 
 @pytest.mark.gpu
 def test_map_schema_validation(gpu):
-    """Maps of scalar keys and values only; anything else is UNSUPPORTED."""
-    for kt, vt, ok in ((8, 10, True), (2, 3, True), (11, 8, False), (8, 15, False),
+    """Maps of scalar or string keys and values; anything else is UNSUPPORTED."""
+    for kt, vt, ok in ((8, 10, True), (2, 3, True), (11, 8, True), (12, 8, False), (8, 15, False),
                        (8, 0, False)):
         s = Schema(Struct("S", [Field(1, T_MAP, kt, val_ttype=vt)]))
         structs, ns, fields, nf = s.descriptors()
