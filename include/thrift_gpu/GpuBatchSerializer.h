@@ -291,6 +291,25 @@ class GpuBatchSerializer {
     if (st.code != TGPU_OK) rethrow(st);
     return size;
   }
+  /* Re-encodes n records of `in` (this serializer's protocol) into protocol
+   * To (tgpu_transcode_batch): serialize<To>(deserialize<From>(record)) per
+   * record without leaving the device. Returns the output size; throws on
+   * the first record the reader rejects (records before it are written). */
+  template <class To>
+  uint64_t transcode(const void* in, uint64_t len, uint64_t n, void* out, uint64_t capacity,
+                     uint64_t* out_offsets = nullptr, const uint64_t* offsets = nullptr) {
+    tgpu_status st{};
+    uint64_t done = 0, size = 0;
+    tgpu_transcode_batch(ctx_, schema_.get(), Protocol::kId, To::kId, in, len, offsets, n, out,
+                         capacity, out_offsets, &limits_, stream_, &st, &done, &size);
+    if (st.code != TGPU_OK) rethrow(st);
+    return size;
+  }
+  /* List arena bytes deserialize() needs for `len` input bytes. */
+  uint64_t arenaBytes(uint64_t len) const {
+    return len * tgpu_schema_arena_scale(schema_.get(), Protocol::kId);
+  }
+
   /* Generates and compiles the schema's kernels now (tgpu_schema_compile):
    * the run-time counterpart of thrift1 emitting T::readNoXfer / T::write.
    * False when the schema runs on the interpreting kernels instead. */

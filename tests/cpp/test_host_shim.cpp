@@ -95,6 +95,31 @@ int main() {
     ser.compile();  // fixed-layout schema: compiled or interpreted, same results
   }
 
+  // Transcoding (tgpu_transcode_batch): Binary -> Compact equals the Compact
+  // serializer's bytes, and Compact -> Binary gives the original stream back.
+  {
+    BinaryBatchSerializer bin(flat);
+    CompactBatchSerializer cmp(flat);
+    const uint64_t bbytes = bin.serialize(d_rec, n, d_wire, n * 89);
+    uint8_t* d_c1 = dev_alloc<uint8_t>(n * 89 * 2);
+    uint8_t* d_c2 = dev_alloc<uint8_t>(n * 89 * 2);
+    uint8_t* d_b2 = dev_alloc<uint8_t>(n * 89);
+    const uint64_t cbytes = bin.transcode<CompactProtocol>(d_wire, bbytes, n, d_c1, n * 178);
+    CHECK(cmp.serialize(d_rec, n, d_c2, n * 178) == cbytes);
+    std::vector<uint8_t> c1(cbytes), c2(cbytes), b1(bbytes), b2(bbytes);
+    CHECK(hipMemcpy(c1.data(), d_c1, cbytes, hipMemcpyDeviceToHost) == hipSuccess);
+    CHECK(hipMemcpy(c2.data(), d_c2, cbytes, hipMemcpyDeviceToHost) == hipSuccess);
+    CHECK(c1 == c2);
+    CHECK(cmp.transcode<BinaryProtocol>(d_c1, cbytes, n, d_b2, n * 89) == bbytes);
+    CHECK(hipMemcpy(b1.data(), d_wire, bbytes, hipMemcpyDeviceToHost) == hipSuccess);
+    CHECK(hipMemcpy(b2.data(), d_b2, bbytes, hipMemcpyDeviceToHost) == hipSuccess);
+    CHECK(b1 == b2);
+    CHECK(bin.arenaBytes(1000) == 0);  // no lists or maps
+    (void)hipFree(d_c1);
+    (void)hipFree(d_c2);
+    (void)hipFree(d_b2);
+  }
+
   // Binary readBool: a byte >= 2 throws TProtocolException(INVALID_DATA)
   // (BinaryProtocol-inl.h:489-495; BinaryProtocolTest.cpp:30-41).
   GpuSchema wb({{{1, TGPU_T_I64}, {2, TGPU_T_BOOL}, {3, TGPU_T_I32}}});
