@@ -517,6 +517,10 @@ __device__ __forceinline__ uint64_t arena_scale(const DevSchema& sc) {
   return sc.str_elems ? (P == TGPU_PROTOCOL_BINARY ? 4 : 16) : Proto<P>::kArenaScale;
 }
 
+__device__ __forceinline__ bool at_ok(uint64_t aoff, int32_t i, uint32_t es, uint64_t cap) {
+  return aoff + ((uint64_t)i + 1) * es <= cap;
+}
+
 template <int P>
 __device__ void read_list(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8_t* arena,
                           uint64_t arena_cap, uint64_t scale) {
@@ -565,11 +569,27 @@ __device__ void read_list(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8
         for (uint32_t b = 0; b < es; ++b) arena[at + b] = tmp[b];
       }
       if (!r.ok()) {
-        // leftover elements are value-initialized (protocol_methods.h:441-451)
-        for (; i < n; ++i) {
-          const uint64_t at = aoff + (uint64_t)i * es;
-          if (at + es > arena_cap) break;
-          for (uint32_t b = 0; b < es; ++b) arena[at + b] = 0;
+        if (f.ttype == TGPU_T_SET) {
+          // deserialize_known_length_set (EncodeHelpers.h:248-259): an element
+          // is inserted once read — the set keeps the complete ones
+          sp.length = (uint32_t)i;
+          if (!i) sp.offset = 0;
+          *(tgpu_span*)m = sp;
+        } else if (f.elem_ttype == TGPU_T_STRING) {
+          // non-trivial elements: reserve + emplace_back_default + read
+          // (protocol_methods.h:374-386,458-461): the failing element is
+          // in the list, empty (readString throws before assigning)
+          if (at_ok(aoff, i, es, arena_cap))
+            for (uint32_t b = 0; b < es; ++b) arena[aoff + (uint64_t)i * es + b] = 0;
+          sp.length = (uint32_t)(i + 1);
+          *(tgpu_span*)m = sp;
+        } else {
+          // leftover elements are value-initialized (protocol_methods.h:441-451)
+          for (; i < n; ++i) {
+            const uint64_t at = aoff + (uint64_t)i * es;
+            if (at + es > arena_cap) break;
+            for (uint32_t b = 0; b < es; ++b) arena[at + b] = 0;
+          }
         }
       }
     }

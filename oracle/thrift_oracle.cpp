@@ -587,11 +587,27 @@ void readList(R& r, const tgpu_field_desc& f, uint8_t* member, DecodeCtx& dc) {
         std::memcpy(dc.arena + at, tmp, es);
       }
     } catch (const OErr&) {
-      // protocol_methods.h:441-451: leftover elements are value-initialized
-      for (; i < n; ++i) {
-        const uint64_t at = aoff + (uint64_t)i * es;
-        if (at + es > dc.arena_cap) break;
-        std::memset(dc.arena + at, 0, es);
+      if (f.ttype == TGPU_T_SET) {
+        // deserialize_known_length_set (EncodeHelpers.h:248-259, std::set):
+        // an element is inserted once read — the complete ones remain
+        span.length = (uint32_t)i;
+        if (!i) span.offset = 0;
+        std::memcpy(member, &span, sizeof(span));
+      } else if (f.elem_ttype == TGPU_T_STRING) {
+        // non-trivial elements: reserve + emplace_back_default + read
+        // (protocol_methods.h:374-386,458-461): the failing element is in
+        // the list, empty
+        if (aoff + ((uint64_t)i + 1) * es <= dc.arena_cap)
+          std::memset(dc.arena + aoff + (uint64_t)i * es, 0, es);
+        span.length = (uint32_t)(i + 1);
+        std::memcpy(member, &span, sizeof(span));
+      } else {
+        // protocol_methods.h:441-451: leftover elements are value-initialized
+        for (; i < n; ++i) {
+          const uint64_t at = aoff + (uint64_t)i * es;
+          if (at + es > dc.arena_cap) break;
+          std::memset(dc.arena + at, 0, es);
+        }
       }
       throw;
     }
