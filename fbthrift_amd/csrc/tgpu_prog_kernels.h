@@ -110,6 +110,15 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
   }
   __syncthreads();
 
+  // Binary lists: elements converted in place in the wire tile (an element's
+  // arena slot is its own wire bytes), then the whole tile goes to the arena
+  // with coalesced 16-byte stores (arena and stream 16-byte congruent; arena
+  // bytes outside spans are unspecified). Config 4 decode: per-element 4-byte
+  // stores 2.27 ms, whole-tile copy 1.82 ms, each lane copying its own lists
+  // with 16-byte stores 3.15 ms.
+  const bool stage_lists = P.has_lists() && P.protocol() == TGPU_PROTOCOL_BINARY && tile_ok &&
+                           a.arena && t1 <= a.arena_cap &&
+                           (((uintptr_t)a.arena - (uintptr_t)a.in) & 15) == 0;
   const uint32_t r = threadIdx.x;
   if (r < nrec) {
     uint8_t* rec = rtile + osh + r * S;
@@ -118,7 +127,8 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
       const uint64_t s = L ? t0 + r * L : a.offs[r0 + r], e = L ? s + L : a.offs[r0 + r + 1];
       ok = s >= t0 && e >= s && e <= t1;
       if (ok) {
-        const Ctx c{t0 - sh, a.arena, a.arena_cap, a.string_limit, a.container_limit};
+        const Ctx c{t0 - sh, a.arena, a.arena_cap, a.string_limit, a.container_limit,
+                    stage_lists ? wire : nullptr};
         const LdsSrc src{(const uint32_t*)wire};
         uint32_t p = (uint32_t)(s - t0) + sh;
         const uint32_t pe = (uint32_t)(e - t0) + sh;
@@ -135,6 +145,18 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
     }
   }
   __syncthreads();
+  if (stage_lists) {  // converted wire tile -> arena [t0, t1), coalesced
+    const uint32_t wend = sh + (uint32_t)(t1 - t0);
+    uint8_t* ab = a.arena + t0 - sh;
+    for (uint32_t i = threadIdx.x; i < ((wend + 15) >> 4); i += kPT) {
+      const uint32_t lo = i << 4, hi = lo + 16;
+      if (lo >= sh && hi <= wend) {
+        ((uint4*)ab)[i] = ((const uint4*)wire)[i];
+      } else {
+        for (uint32_t b = (lo < sh ? sh : lo); b < (hi < wend ? hi : wend); ++b) ab[b] = wire[b];
+      }
+    }
+  }
   // record tile -> HBM
   const uint32_t end = osh + nrec * S;
   const uint32_t nvec = (end + 15) >> 4;

@@ -33,6 +33,7 @@ struct DynProg {
   const VProgram* __restrict__ p;
   __device__ __forceinline__ uint32_t n_ops() const { return p->n_ops; }
   __device__ __forceinline__ uint32_t protocol() const { return p->protocol; }
+  __device__ __forceinline__ bool has_lists() const { return p->has_list != 0; }
   __device__ __forceinline__ VOp op(uint32_t k) const { return p->ops[k]; }
 };
 
@@ -152,6 +153,10 @@ struct Ctx {
   uint8_t* arena;
   uint64_t arena_cap;
   int32_t string_limit, container_limit;
+  // Binary decode tile: list elements are converted in place in the LDS
+  // wire tile (an element's arena slot is its own wire bytes, scale 1) and
+  // the tile is copied to the arena with coalesced stores afterwards
+  uint8_t* lds_wire;
 };
 
 // One op of the program at p (bounded by end); false = irregular.
@@ -259,9 +264,12 @@ __device__ __forceinline__ bool run_op(const VOp op, const bool compact, const S
               if (compact) v = v == 1;
               else if (v > 1) return false;
             }
+            if (kStore && c.lds_wire) store_n(c.lds_wire + p, v, wb);  // in place (wb == es)
             p += wb;
           }
-          if (kStore) store_n(c.arena + aoff + (uint64_t)i * es, v, es);
+#ifndef TGPU_NO_ARENA_STORE  // A/B only (tools/kbench_jit.py): cost of the element stores
+          if (kStore && !c.lds_wire) store_n(c.arena + aoff + (uint64_t)i * es, v, es);
+#endif
         }
       }
       if (kStore) {

@@ -329,7 +329,8 @@ int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol
  * before reading. List elements are written to list_arena (capacity
  * list_arena_capacity bytes; required size: in_len x tgpu_schema_arena_scale
  * — in_len Binary / 8 * in_len Compact for scalar elements, 0 without
- * lists/sets/maps).
+ * lists/sets/maps). Bytes of list_arena outside the records' spans are
+ * unspecified (a Binary decode may copy whole wire tiles there).
  * limits may be NULL (reference defaults).
  * If st != NULL the call waits and fills st, *n_decoded (records fully
  * decoded before the first failure) and *consumed (bytes consumed by them).

@@ -191,3 +191,10 @@ def assert_values_equal(got, want):
         assert g.shape == w.shape, (k, g.shape, w.shape)
         assert np.array_equal(g.view(np.uint8) if g.dtype.kind == "f" else g,
                               w.view(np.uint8) if w.dtype.kind == "f" else w), k
+
+
+def assert_arena_equal(schema, rec_bytes, n, wire, got_arena, want_arena):
+    """The list arena bytes the records' spans reference are equal (bytes of
+    the arena outside the spans are unspecified)."""
+    assert_values_equal(unpack(schema, rec_bytes, n, wire, got_arena),
+                        unpack(schema, rec_bytes, n, wire, want_arena))

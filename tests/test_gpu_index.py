@@ -192,8 +192,7 @@ def test_decode_stream_whole(gpu, codec, sname, proto):
     ost, orec, oarena, _, _ = oracle.decode(schema, proto, wire, n)
     assert np.array_equal(rec.cpu().numpy()[: n * schema.record_size], orec)
     if arena is not None:
-        k = min(arena.numel(), oarena.size)
-        assert np.array_equal(arena.cpu().numpy()[:k], oarena[:k])
+        helpers.assert_arena_equal(schema, orec, n, wire, arena.cpu().numpy(), oarena)
 
 
 @pytest.mark.parametrize("proto", [2, 0])

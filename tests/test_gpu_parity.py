@@ -65,8 +65,7 @@ def test_decode_golden(gpu, codec, name, indexed):
     assert nd == c.n and cons == len(c.wire)
     ost, orec, oarena, _, _ = oracle.decode(c.schema, c.protocol, c.wire, c.n, offsets=offs)
     assert np.array_equal(rec[: c.n * c.schema.record_size], orec[: c.n * c.schema.record_size])
-    k = min(arena.size, oarena.size)
-    assert np.array_equal(arena[:k], oarena[:k])
+    helpers.assert_arena_equal(c.schema, orec, c.n, c.wire, arena, oarena)
     helpers.assert_values_equal(helpers.unpack(c.schema, rec, c.n, c.wire, arena), c.values)
 
 
@@ -214,8 +213,7 @@ def test_config_shapes_roundtrip(gpu, sname, proto):
                                                 offsets=woffs if indexed else None)
         assert gst.code == 0 and gcons == len(want)
         assert np.array_equal(grec, orec)
-        k = min(garena.size, oarena.size)
-        assert np.array_equal(garena[:k], oarena[:k])
+        helpers.assert_arena_equal(schema, orec, n, want, garena, oarena)
 
 
 @pytest.mark.parametrize("case", [c for c in corpus.cases() if c[4] == 1], ids=lambda c: c[0])
@@ -264,8 +262,7 @@ def test_program_path_with_irregular_records(gpu, name, every):
     assert st.as_tuple() == ost.as_tuple()
     assert st.code == 0 and cons == ocons == len(stream)
     assert np.array_equal(rec, orec)
-    k = min(arena.size, oarena.size)
-    assert np.array_equal(arena[:k], oarena[:k])
+    helpers.assert_arena_equal(c.schema, orec, c.n, stream, arena, oarena)
 
 
 def _long_string_records(n, seed, max_len):
