@@ -17,6 +17,9 @@
 //      sizes, records emitted into a zero-filled LDS output tile a dword at a
 //      time, coalesced 16-byte stores; out_offsets receives every start.
 // tgpu_encoded_size stops after 2.
+#include <cstdlib>
+#include <cstring>
+
 #include "tgpu_prog_kernels.h"
 
 namespace tgpu {
@@ -124,6 +127,16 @@ bool program_encode_fits(uint32_t rec_size) {
   return kET * rec_size + 32 <= 32 * 1024;  // record tile + 24 KiB output tile <= 64 KiB LDS
 }
 
+// LDS of the compiled write kernel's element stage: prog::kElemStage, or a
+// "#define TGPU_ELEM_STAGE n" in TGPU_JIT_DEFINES (A/B runs, tools/kbench_jit.py)
+static uint32_t elem_stage_bytes() {
+  uint32_t n = prog::kElemStage;
+  if (const char* d = getenv("TGPU_JIT_DEFINES")) {
+    if (const char* k = strstr(d, "TGPU_ELEM_STAGE")) n = (uint32_t)strtoul(k + 15, nullptr, 10);
+  }
+  return n;
+}
+
 hipError_t launch_program_encode(const EncodeArgs& a, const VProgram* d_prog,
                                  unsigned long long* part, bool size_only, hipStream_t stream,
                                  const JitKernels* jit) {
@@ -142,8 +155,9 @@ hipError_t launch_program_encode(const EncodeArgs& a, const VProgram* d_prog,
     e = launch_scan_tiles(a.block_sums, tiles, part, &a.res->total_bytes, a.offs + a.n, stream);
   if (e != hipSuccess || size_only) return e;
   const uint32_t lds = rt + kOutCap + 32;
-  // the compiled write kernel reads records from HBM: output tile only
-  if (jit) return jit_launch_encode(jit, true, a, tiles, kOutCap + 32, stream);
+  // the compiled write kernel reads records from HBM: output tile (+ the
+  // list element stage, prog::kElemStage)
+  if (jit) return jit_launch_encode(jit, true, a, tiles, kOutCap + 32 + elem_stage_bytes(), stream);
   hipLaunchKernelGGL(program_write_kernel, dim3((uint32_t)tiles), dim3(kET), lds, stream, a,
                      d_prog);
   return hipGetLastError();

@@ -213,7 +213,11 @@ __device__ __forceinline__ void for_elems(const uint8_t* __restrict__ e, uint32_
       uint64_t v[B];
 #pragma unroll
       for (uint32_t k = 0; k < B; ++k)
+#ifndef TGPU_NO_ELEM_LOAD  // A/B only (tools/kbench_jit.py --no-check): cost of the loads
         v[k] = i0 + k < len ? load_member(e + (uint64_t)(i0 + k) * width, width) : 0;
+#else
+        v[k] = i0 + k;
+#endif
 #pragma unroll
       for (uint32_t k = 0; k < B; ++k)
         if (i0 + k < len) f(v[k]);
@@ -510,7 +514,16 @@ __device__ __forceinline__ void size_tile(const EncodeArgs& a, const PP& P, uint
 struct EncodeShared {
   unsigned long long part[4];
   unsigned int lds_end;
+  unsigned long long elo, ehi;  // the tile's list elements in list_base
 };
+
+// Encode, compiled programs: the tile's list elements are staged in LDS with
+// coalesced 16-byte loads when their extent in list_base fits kElemStage
+// bytes (each lane's own 4-byte element loads cost 1.0 of config 4's 2.5 ms).
+#ifndef TGPU_ELEM_STAGE
+#define TGPU_ELEM_STAGE 0
+#endif
+constexpr uint32_t kElemStage = TGPU_ELEM_STAGE;
 
 template <class PP>
 __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uint32_t S,
@@ -534,6 +547,10 @@ __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uin
     rsh = stage_records(a.recs, r0, nrec, S, rtile);
   }
   const uint32_t r = threadIdx.x;
+  if (kElemStage > 0 && r == 0) {
+    sm.elo = ~0ull;
+    sm.ehi = 0;
+  }
   unsigned long long sz, tile_total, rel, tile_base;
   if (a.fixed_len) {
     // fixed layout: every record is fixed_len bytes; the size pass only
@@ -550,6 +567,46 @@ __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uin
   }
   uint8_t* gtile = a.out + tile_base;
   const uint32_t osh = (uint32_t)((uintptr_t)gtile & 15);
+  const uint8_t* lbase = a.lbase;
+  if constexpr (PP::kStatic && kElemStage > 0) {
+    if (P.has_lists()) {
+      // extent of the tile's elements (block barrier in the exscan above
+      // orders thread 0's init before the atomics)
+      unsigned long long lo = ~0ull, hi = 0;
+      if (r < nrec) {
+        const uint8_t* rec = rtile + r * S;
+        all_ops(P, [&](const VOp op) {
+          if (op.kind == VOP_LIST) {
+            const tgpu_span sp = *(const tgpu_span*)(rec + op.member);
+            if (sp.length) {
+              lo = min(lo, (unsigned long long)sp.offset);
+              hi = max(hi, (unsigned long long)sp.offset + (unsigned long long)sp.length * op.width);
+            }
+          }
+          return true;
+        });
+      }
+      if (lo != ~0ull) {
+        atomicMin(&sm.elo, lo);
+        atomicMax(&sm.ehi, hi);
+      }
+      __syncthreads();
+      const unsigned long long elo = sm.elo, ehi = sm.ehi;
+      if (elo < ehi) {
+        const uintptr_t g0 = ((uintptr_t)a.lbase + elo) & ~(uintptr_t)15;
+        const uint32_t nvec = (uint32_t)(((uintptr_t)a.lbase + ehi - g0 + 15) >> 4);
+        if (nvec * 16 <= kElemStage) {
+          uint8_t* stage = smem + kOutCap + 32;
+          for (uint32_t i = threadIdx.x; i < nvec; i += kET)
+            ((uint4*)stage)[i] = ((const uint4*)g0)[i];
+          // a flat (generic) address into the LDS aperture, computed in 64-bit
+          // integers so element offsets added later stay inside it
+          const uintptr_t sg = (uintptr_t)(void*)stage;
+          lbase = (const uint8_t*)(sg - (g0 - (uintptr_t)a.lbase));
+        }
+      }
+    }
+  }
   {  // zero the part of the output tile the records will OR into
     const uint4 z = {0u, 0u, 0u, 0u};
     const uint32_t nz =
@@ -580,7 +637,7 @@ __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uin
     }
     if (fits && rel + sz <= sm.lds_end) {
       OrSink w((uint32_t*)otile, osh + (uint32_t)rel);
-      program_emit(P, rec, a.sbase, a.lbase, w);
+      program_emit(P, rec, a.sbase, lbase, w);
     } else if (tile_base + rel + sz <= a.cap) {
       emit_to_hbm(P, rec, a.sbase, a.lbase, gtile + rel);
     }

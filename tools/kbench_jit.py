@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--var", nargs="*", default=[""])
     ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--no-check", action="store_true",
+                    help="timing-only variants (e.g. TGPU_NO_ELEM_LOAD) change the output")
     args = ap.parse_args()
     import torch
 
@@ -40,7 +42,7 @@ def main():
                 torch.cuda.synchronize()
                 enc[v].append(ev[0].elapsed_time(ev[1]))
                 dec[v].append(ev[1].elapsed_time(ev[2]))
-            if rnd == 0:
+            if rnd == 0 and not args.no_check:
                 wl.check_timed()
                 got = (wl.wire.clone(), wl.back.clone())
                 if ref is None:
