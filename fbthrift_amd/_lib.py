@@ -68,7 +68,7 @@ EXPORTS = [
     "tgpu_context_reserve", "tgpu_context_wait", "tgpu_encode_batch", "tgpu_encoded_size",
     "tgpu_decode_batch", "tgpu_index_stream", "tgpu_schema_compile", "tgpu_schema_compile_check",
     "tgpu_decode_host", "tgpu_encode_host", "tgpu_decode_stream", "tgpu_transcode_batch",
-    "tgpu_schema_arena_scale",
+    "tgpu_schema_arena_scale", "tgpu_decode_host_ex", "tgpu_encode_host_ex",
 ]
 
 _lib = None
@@ -138,6 +138,13 @@ def lib():
                                      ctypes.POINTER(Limits), P, ctypes.POINTER(Status),
                                      ctypes.POINTER(U64), ctypes.POINTER(U64),
                                      ctypes.POINTER(U64)]
+    L.tgpu_decode_host_ex.restype = I32
+    L.tgpu_decode_host_ex.argtypes = [P, P, I32, P, U64, U64, P, P, U64, ctypes.POINTER(Limits),
+                                      ctypes.POINTER(Status), ctypes.POINTER(U64),
+                                      ctypes.POINTER(U64)]
+    L.tgpu_encode_host_ex.restype = I32
+    L.tgpu_encode_host_ex.argtypes = [P, P, I32, P, U64, P, U64, P, U64, P, U64, P,
+                                      ctypes.POINTER(Status), ctypes.POINTER(U64)]
     L.tgpu_schema_arena_scale.restype = ctypes.c_uint32
     L.tgpu_schema_arena_scale.argtypes = [P, I32]
     L.tgpu_transcode_batch.restype = I32

@@ -328,4 +328,104 @@ int tgpu_encode_host(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
   return TGPU_OK;
 }
 
+// ---- any schema: one resident pass (copy in, device call, copy out) -------
+namespace {
+struct DevBuf {
+  uint8_t* p = nullptr;
+  bool alloc(uint64_t n) { return hipMalloc(&p, std::max<uint64_t>(n, 16)) == hipSuccess; }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+};
+}  // namespace
+
+int tgpu_decode_host_ex(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                        const void* h_in, uint64_t in_len, uint64_t n, void* h_records,
+                        void* h_arena, uint64_t arena_capacity, const tgpu_limits* limits,
+                        tgpu_status* st, uint64_t* n_decoded, uint64_t* consumed) {
+  if (n_decoded) *n_decoded = 0;
+  if (consumed) *consumed = 0;
+  if (!ctx || !schema || (n && (!h_in || !h_records)) || (arena_capacity && !h_arena)) {
+    set_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+    return TGPU_ERR_INVALID_ARGUMENT;
+  }
+  const uint32_t S = tgpu_schema_record_size(schema);
+  PinGuard pin_in(h_in, in_len), pin_rec(h_records, n * S), pin_ar(h_arena, arena_capacity);
+  DevBuf din, drec, dar;
+  if (!din.alloc(in_len) || !drec.alloc(n * S) || (arena_capacity && !dar.alloc(arena_capacity))) {
+    set_status(st, TGPU_ERR_HIP, 0, 0);
+    return TGPU_ERR_HIP;
+  }
+  tgpu_status cs{};
+  uint64_t nd = 0, cons = 0;
+  int code = TGPU_ERR_HIP;
+  if (hipMemcpy(din.p, h_in, in_len, hipMemcpyHostToDevice) == hipSuccess) {
+    code = tgpu_decode_batch(ctx, schema, protocol, din.p, in_len, nullptr, n, drec.p,
+                             arena_capacity ? dar.p : nullptr, arena_capacity, limits, nullptr,
+                             &cs, &nd, &cons);
+    // the records before the failure and the partial failing one go back,
+    // and the arena (its bytes outside the spans are unspecified)
+    const uint64_t back = std::min<uint64_t>(n, nd + (code ? 1 : 0));
+    if (code != TGPU_ERR_HIP &&
+        (hipMemcpy(h_records, drec.p, back * S, hipMemcpyDeviceToHost) != hipSuccess ||
+         (arena_capacity &&
+          hipMemcpy(h_arena, dar.p, arena_capacity, hipMemcpyDeviceToHost) != hipSuccess)))
+      code = TGPU_ERR_HIP;
+  }
+  if (code == TGPU_ERR_HIP) {
+    set_status(st, TGPU_ERR_HIP, 0, 0);
+    return TGPU_ERR_HIP;
+  }
+  if (st) *st = cs;
+  if (n_decoded) *n_decoded = nd;
+  if (consumed) *consumed = cons;
+  return code;
+}
+
+int tgpu_encode_host_ex(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                        const void* h_records, uint64_t n, const void* h_strings,
+                        uint64_t strings_len, const void* h_lists, uint64_t lists_len,
+                        void* h_out, uint64_t out_capacity, uint64_t* h_out_offsets,
+                        tgpu_status* st, uint64_t* out_size) {
+  if (out_size) *out_size = 0;
+  if (!ctx || !schema || (n && (!h_records || !h_out)) || (strings_len && !h_strings) ||
+      (lists_len && !h_lists)) {
+    set_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+    return TGPU_ERR_INVALID_ARGUMENT;
+  }
+  const uint32_t S = tgpu_schema_record_size(schema);
+  PinGuard pin_rec(h_records, n * S), pin_s(h_strings, strings_len), pin_l(h_lists, lists_len),
+      pin_out(h_out, out_capacity);
+  DevBuf drec, dstr, dlist, dout, doffs;
+  if (!drec.alloc(n * S) || !dstr.alloc(strings_len) || !dlist.alloc(lists_len) ||
+      !dout.alloc(out_capacity) || (h_out_offsets && !doffs.alloc((n + 1) * 8))) {
+    set_status(st, TGPU_ERR_HIP, 0, 0);
+    return TGPU_ERR_HIP;
+  }
+  if (hipMemcpy(drec.p, h_records, n * S, hipMemcpyHostToDevice) != hipSuccess ||
+      (strings_len && hipMemcpy(dstr.p, h_strings, strings_len, hipMemcpyHostToDevice) != hipSuccess) ||
+      (lists_len && hipMemcpy(dlist.p, h_lists, lists_len, hipMemcpyHostToDevice) != hipSuccess)) {
+    set_status(st, TGPU_ERR_HIP, 0, 0);
+    return TGPU_ERR_HIP;
+  }
+  tgpu_status cs{};
+  uint64_t size = 0;
+  int code = tgpu_encode_batch(ctx, schema, protocol, drec.p, n, dstr.p, dlist.p, dout.p,
+                               out_capacity, h_out_offsets ? (uint64_t*)doffs.p : nullptr,
+                               nullptr, &cs, &size);
+  if (code != TGPU_ERR_HIP &&
+      (hipMemcpy(h_out, dout.p, std::min(size, out_capacity), hipMemcpyDeviceToHost) !=
+           hipSuccess ||
+       (h_out_offsets && code == TGPU_OK &&
+        hipMemcpy(h_out_offsets, doffs.p, (n + 1) * 8, hipMemcpyDeviceToHost) != hipSuccess)))
+    code = TGPU_ERR_HIP;
+  if (code == TGPU_ERR_HIP) {
+    set_status(st, TGPU_ERR_HIP, 0, 0);
+    return TGPU_ERR_HIP;
+  }
+  if (st) *st = cs;
+  if (out_size) *out_size = size;
+  return code;
+}
+
 }  // extern "C"

@@ -353,6 +353,44 @@ class BatchSerializer:
             ctypes.byref(st), ctypes.byref(n_dec), ctypes.byref(consumed))
         return records, st, n_dec.value, consumed.value
 
+    def deserialize_host_ex(self, gschema, wire, n, limits=None):
+        """Host-memory decode of any schema (tgpu_decode_host_ex, one resident
+        pass). Returns (records, arena, status, n_decoded, consumed); spans
+        index `wire` (strings) and `arena` (list elements)."""
+        import numpy as np
+
+        records = np.zeros(max(n * gschema.record_size, 1), np.uint8)
+        cap = self.arena_bytes(gschema, _hlen(wire))
+        arena = np.zeros(max(cap, 1), np.uint8)
+        lim = _lib.Limits(*limits) if limits is not None else None
+        st = _lib.Status()
+        n_dec, consumed = ctypes.c_uint64(), ctypes.c_uint64()
+        _lib.lib().tgpu_decode_host_ex(
+            self.context().handle, gschema.handle, self.protocol, _hptr(wire), _hlen(wire), n,
+            _hptr(records), _hptr(arena) if cap else None, cap,
+            ctypes.byref(lim) if lim is not None else None, ctypes.byref(st),
+            ctypes.byref(n_dec), ctypes.byref(consumed))
+        return records, arena, st, n_dec.value, consumed.value
+
+    def serialize_host_ex(self, gschema, records, n, strings=None, lists=None, out=None):
+        """Host-memory encode of any schema (tgpu_encode_host_ex). Returns
+        (out, offsets, status, size)."""
+        import numpy as np
+
+        if out is None:
+            total = _hlen(records) + (_hlen(strings) if strings is not None else 0) + \
+                (_hlen(lists) if lists is not None else 0)
+            out = np.zeros(max(8 * total + 16, 16), np.uint8)
+        offs = np.zeros(n + 1, np.uint64)
+        st, size = _lib.Status(), ctypes.c_uint64()
+        _lib.lib().tgpu_encode_host_ex(
+            self.context().handle, gschema.handle, self.protocol, _hptr(records), n,
+            _hptr(strings) if strings is not None else None,
+            _hlen(strings) if strings is not None else 0,
+            _hptr(lists) if lists is not None else None, _hlen(lists) if lists is not None else 0,
+            _hptr(out), _hlen(out), offs.ctypes.data, ctypes.byref(st), ctypes.byref(size))
+        return out, offs, st, size.value
+
     def serialize_host(self, gschema, records, n, out=None, chunk=0):
         """Host-memory encode (tgpu_encode_host) of n records held in host
         memory into `out` (allocated when None). Returns (out, status, size)."""

@@ -389,6 +389,28 @@ int tgpu_encode_host(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
                      uint64_t out_capacity, uint64_t chunk_records, tgpu_status* st,
                      uint64_t* out_size);
 
+/*
+ * Host-memory batches of ANY schema (lists, sets, maps, strings, unions):
+ * one resident pass — the host buffers are copied to the device, the
+ * device call runs, the outputs come back (PCIe-bound; pageable buffers are
+ * pinned in place for the call). Results and status exactly as for
+ * tgpu_decode_batch / tgpu_encode_batch. Decode: string spans are offsets
+ * into host_in, list spans into host_arena (capacity as for the device
+ * arena: in_len x tgpu_schema_arena_scale; may be NULL/0 without lists).
+ * Encode: spans are relative to host_strings / host_lists; host_out_offsets
+ * (n+1 entries) may be NULL. Blocking.
+ */
+int tgpu_decode_host_ex(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                        const void* host_in, uint64_t in_len, uint64_t n_records,
+                        void* host_records, void* host_arena, uint64_t arena_capacity,
+                        const tgpu_limits* limits, tgpu_status* st, uint64_t* n_decoded,
+                        uint64_t* consumed);
+int tgpu_encode_host_ex(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                        const void* host_records, uint64_t n_records, const void* host_strings,
+                        uint64_t strings_len, const void* host_lists, uint64_t lists_len,
+                        void* host_out, uint64_t out_capacity, uint64_t* host_out_offsets,
+                        tgpu_status* st, uint64_t* out_size);
+
 /* ---- stream index ----------------------------------------------------- */
 /*
  * Record index of an unindexed stream — the bulk form of the file-reading

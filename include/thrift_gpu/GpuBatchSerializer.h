@@ -291,6 +291,28 @@ class GpuBatchSerializer {
     if (st.code != TGPU_OK) rethrow(st);
     return size;
   }
+  /* Host-memory forms for any schema (tgpu_decode_host_ex /
+   * tgpu_encode_host_ex): one resident pass through the GPU. */
+  uint64_t deserializeHostEx(const void* in, uint64_t len, uint64_t n, void* records,
+                             void* arena = nullptr, uint64_t arena_capacity = 0) {
+    tgpu_status st{};
+    uint64_t done = 0, consumed = 0;
+    tgpu_decode_host_ex(ctx_, schema_.get(), Protocol::kId, in, len, n, records, arena,
+                        arena_capacity, &limits_, &st, &done, &consumed);
+    if (st.code != TGPU_OK) rethrow(st);
+    return consumed;
+  }
+  uint64_t serializeHostEx(const void* records, uint64_t n, const void* strings,
+                           uint64_t strings_len, const void* lists, uint64_t lists_len,
+                           void* out, uint64_t capacity, uint64_t* out_offsets = nullptr) {
+    tgpu_status st{};
+    uint64_t size = 0;
+    tgpu_encode_host_ex(ctx_, schema_.get(), Protocol::kId, records, n, strings, strings_len,
+                        lists, lists_len, out, capacity, out_offsets, &st, &size);
+    if (st.code != TGPU_OK) rethrow(st);
+    return size;
+  }
+
   /* Re-encodes n records of `in` (this serializer's protocol) into protocol
    * To (tgpu_transcode_batch): serialize<To>(deserialize<From>(record)) per
    * record without leaving the device. Returns the output size; throws on

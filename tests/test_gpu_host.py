@@ -124,3 +124,34 @@ def test_host_decode_variable_length(gpu):
     ng = GpuSchema(Schema.from_table(datagen.SCHEMAS["nested"]))
     _, st, _, _ = CompactSerializer.deserialize_host(ng, np.zeros(100, np.uint8), 1)
     assert st.code == 22  # TGPU_ERR_UNSUPPORTED
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["nested_binary", "maps_compact", "strcont_binary",
+                                  "unions_compact", "scalars_compact_v1"])
+def test_host_ex_any_schema(gpu, name):
+    """tgpu_decode_host_ex / tgpu_encode_host_ex: host buffers, any schema;
+    records, spans and bytes equal the oracle's (damaged input too)."""
+    import helpers
+    from fbthrift_amd import serializer as S
+    from oracle import oracle
+
+    c = helpers.Case(name)
+    ser = {0: S.BinarySerializer, 2: S.CompactSerializer, 0x102: S.CompactV1Serializer}[c.protocol]
+    gs = S.GpuSchema(c.schema)
+    wire = np.frombuffer(c.wire, np.uint8).copy()
+    rec, arena, st, nd, cons = ser.deserialize_host_ex(gs, wire, c.n)
+    assert st.code == 0 and nd == c.n and cons == len(c.wire)
+    ost, orec, oarena, _, _ = oracle.decode(c.schema, c.protocol, c.wire, c.n)
+    assert np.array_equal(rec[: c.n * c.schema.record_size], orec[: c.n * c.schema.record_size])
+    helpers.assert_values_equal(helpers.unpack(c.schema, rec, c.n, c.wire, arena), c.values)
+    # encode from host records + host string / list arenas
+    prec, sa, la = helpers.pack(c.schema, c.values, c.n)
+    out, offs, est, size = ser.serialize_host_ex(gs, prec, c.n, strings=sa, lists=la)
+    assert est.code == 0 and bytes(out[:size]) == c.wire
+    assert np.array_equal(offs, c.offsets)
+    m = wire.copy()
+    m[len(m) // 2] ^= 0x5A
+    rec, arena, st, nd, cons = ser.deserialize_host_ex(gs, m, c.n)
+    ost, orec, oarena, ond, ocons = oracle.decode(c.schema, c.protocol, m, c.n)
+    assert st.as_tuple() == ost.as_tuple() and (nd, cons) == (ond, ocons)
