@@ -361,18 +361,45 @@ __device__ __forceinline__ void put_varint(Sink& s, uint64_t v) {
 }
 // len bytes from HBM (any alignment): aligned dword loads, issued 8 at a
 // time before any is used (one memory round trip per 32 bytes, not per dword)
+// The first batch of a string's dwords, loaded ahead (compiled programs
+// issue every string's first batch before emitting anything, so the lanes'
+// string loads overlap instead of each waiting behind the previous ops).
+struct StrPrefetch {
+  uint32_t v[8];
+};
+__device__ __forceinline__ void str_prefetch(StrPrefetch& f, const uint8_t* __restrict__ src,
+                                             uint32_t len) {
+  const uintptr_t a = (uintptr_t)src;
+  const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t need = ((uint32_t)(a & 3) + len + 3) >> 2;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i) f.v[i] = i < need ? w[i] : 0u;
+}
+
 template <class Sink>
-__device__ __forceinline__ void put_bytes(Sink& s, const uint8_t* __restrict__ src, uint32_t len) {
+__device__ __forceinline__ void put_bytes(Sink& s, const uint8_t* __restrict__ src, uint32_t len,
+                                          const StrPrefetch* pf = nullptr) {
   if (!len) return;
   const uintptr_t a = (uintptr_t)src;
   const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
   uint32_t sh = (uint32_t)(a & 3);
   uint32_t left = len;
+  bool first = true;
   while (left) {
     const uint32_t need = (sh + left + 3) >> 2;  // dwords still to read
     uint32_t v[8];
+    if (pf && first) {
 #pragma unroll
-    for (uint32_t i = 0; i < 8; ++i) v[i] = i < need ? w[i] : 0u;
+      for (uint32_t i = 0; i < 8; ++i) v[i] = pf->v[i];
+    } else {
+#pragma unroll
+#ifndef TGPU_NO_STR_LOAD  // A/B only (tools/kbench_jit.py --no-check): cost of the loads
+      for (uint32_t i = 0; i < 8; ++i) v[i] = i < need ? w[i] : 0u;
+#else
+      for (uint32_t i = 0; i < 8; ++i) v[i] = i;
+#endif
+    }
+    first = false;
 #pragma unroll
     for (uint32_t i = 0; i < 8; ++i) {
       if (i < need) {
@@ -386,11 +413,31 @@ __device__ __forceinline__ void put_bytes(Sink& s, const uint8_t* __restrict__ s
   }
 }
 
+// String ops whose first batch is loaded before any emission (A/B knob, off:
+// measured slower on config 3 — 5.62 ms with 4, 4.84 ms with 1, vs 3.81 ms —
+// the held batches cost registers/occupancy; strings' loads themselves cost
+// 0.86 ms of the encode, A/B TGPU_NO_STR_LOAD).
+#ifndef TGPU_STR_PREFETCH
+#define TGPU_STR_PREFETCH 0
+#endif
 template <class PP, class Sink>
 __device__ __forceinline__ void program_emit(const PP& P, const uint8_t* rec,
                                              const uint8_t* __restrict__ sbase,
                                              const uint8_t* __restrict__ lbase, Sink& s) {
   const bool compact = P.protocol() == TGPU_PROTOCOL_COMPACT;
+  constexpr uint32_t kPf = PP::kStatic ? TGPU_STR_PREFETCH : 0;
+  StrPrefetch pf[kPf > 0 ? kPf : 1];
+  uint32_t npf = 0, ipf = 0;
+  if constexpr (kPf > 0) {
+    all_ops(P, [&](const VOp op) {
+      if (op.kind == VOP_STRING && npf < kPf) {
+        const tgpu_span sp = *(const tgpu_span*)(rec + op.member);
+        str_prefetch(pf[npf], sbase + sp.offset, sp.length);
+        ++npf;
+      }
+      return true;
+    });
+  }
   all_ops(P, [&](const VOp op) {
     switch (op.kind) {
       case VOP_CONST:
@@ -410,7 +457,9 @@ __device__ __forceinline__ void program_emit(const PP& P, const uint8_t* rec,
         const tgpu_span sp = *(const tgpu_span*)(rec + op.member);
         if (compact) put_varint(s, sp.length);
         else put_be(s, sp.length, 4);
-        put_bytes(s, sbase + sp.offset, sp.length);
+        const StrPrefetch* f = ipf < npf ? &pf[ipf] : nullptr;
+        ++ipf;
+        put_bytes(s, sbase + sp.offset, sp.length, f);
         break;
       }
       case VOP_LIST: {
