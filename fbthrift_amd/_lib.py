@@ -68,8 +68,13 @@ EXPORTS = [
     "tgpu_context_reserve", "tgpu_context_wait", "tgpu_encode_batch", "tgpu_encoded_size",
     "tgpu_decode_batch", "tgpu_index_stream", "tgpu_schema_compile", "tgpu_schema_compile_check",
     "tgpu_decode_host", "tgpu_encode_host", "tgpu_decode_stream", "tgpu_transcode_batch",
-    "tgpu_schema_arena_scale", "tgpu_decode_host_ex", "tgpu_encode_host_ex",
+    "tgpu_schema_arena_scale", "tgpu_decode_host_ex", "tgpu_encode_host_ex", "tgpu_skim_batch",
 ]
+
+# tgpu_skim_field as a numpy record (16 bytes).
+SKIM_FIELDS = [("id", "<i2"), ("ttype", "u1"), ("flags", "u1"), ("length", "<u4"),
+               ("offset", "<u8")]
+SKIM_BOOL, SKIM_TRUE = 1, 2
 
 _lib = None
 
@@ -121,6 +126,9 @@ def lib():
                                     ctypes.POINTER(Limits), P, ctypes.POINTER(Status),
                                     ctypes.POINTER(U64), ctypes.POINTER(U64),
                                     ctypes.POINTER(U64)]
+    L.tgpu_skim_batch.restype = I32
+    L.tgpu_skim_batch.argtypes = [P, I32, P, U64, P, U64, P, U32, P, ctypes.POINTER(Limits), P,
+                                  ctypes.POINTER(Status), ctypes.POINTER(U64)]
     L.tgpu_schema_compile.restype = I32
     L.tgpu_schema_compile.argtypes = [P, I32]
     L.tgpu_schema_compile_check.restype = I32

@@ -1181,6 +1181,45 @@ int tgpu_decode_stream(tgpu_context* ctx, const tgpu_schema* schema, int protoco
   return code;
 }
 
+int tgpu_skim_batch(tgpu_context* ctx, int protocol, const void* in, uint64_t in_len,
+                    const uint64_t* offsets, uint64_t n, tgpu_skim_field* fields,
+                    uint32_t max_fields, uint32_t* field_counts, const tgpu_limits* limits,
+                    void* stream, tgpu_status* st, uint64_t* n_done) {
+  if (!ctx || !valid_protocol(protocol) ||
+      (n && (!offsets || !field_counts || (max_fields && !fields) || (!in && in_len)))) {
+    fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+    return TGPU_ERR_INVALID_ARGUMENT;
+  }
+  const hipStream_t s = (hipStream_t)stream;
+  SkimArgs a{};
+  a.in = (const uint8_t*)in;
+  a.in_len = in_len;
+  a.offs = offsets;
+  a.n = n;
+  a.fields = fields;
+  a.counts = field_counts;
+  a.max_fields = max_fields;
+  a.string_limit = limits ? limits->string_limit : 0;
+  a.container_limit = limits ? limits->container_limit : 0;
+  a.max_depth = limits ? limits->max_depth : 12000;
+  a.height = limits ? limits->height : 0;
+  a.res = ctx->d_res;
+  (void)hipGetLastError();
+  hipError_t e = launch_result_init(ctx->d_res, n, s);
+  if (e == hipSuccess) e = launch_skim(a, protocol, s);
+  ctx->last_op = 1;
+  if (e != hipSuccess) {
+    fill_status(st, TGPU_ERR_HIP, 0, 0);
+    if (st) st->reserved = (int32_t)e;
+    return TGPU_ERR_HIP;
+  }
+  if (st || n_done) {
+    tgpu_status tmp;
+    return tgpu_context_wait(ctx, stream, st ? st : &tmp, n_done, nullptr);
+  }
+  return TGPU_OK;
+}
+
 int tgpu_index_stream(tgpu_context* ctx, const tgpu_schema* schema, int protocol, const void* in,
                       uint64_t in_len, uint64_t begin, uint64_t end, int speculative,
                       uint64_t* offsets, uint64_t max_records, const tgpu_limits* limits,

@@ -193,6 +193,19 @@ struct DecodeArgs {
                        // (offs unused; a non-canonical record latches first_irregular)
 };
 
+// Schemaless skim of an indexed stream (k_skim.hip, tgpu_skim_batch).
+struct SkimArgs {
+  const uint8_t* in;
+  uint64_t in_len;
+  const uint64_t* offs;  // n+1 record starts
+  uint64_t n;
+  tgpu_skim_field* fields;
+  uint32_t* counts;
+  uint32_t max_fields;
+  int32_t string_limit, container_limit, max_depth, height;
+  DevResult* res;
+};
+
 struct EncodeArgs {
   DevSchema sc;
   const uint8_t* recs;
@@ -306,6 +319,7 @@ hipError_t launch_general_decode_list(const DecodeArgs& a, int protocol,
                                       const uint64_t* list,
                                       const unsigned long long* n_list,
                                       hipStream_t stream);
+hipError_t launch_skim(const SkimArgs& a, int protocol, hipStream_t stream);
 hipError_t launch_serial_decode(const DecodeArgs& a, int protocol,
                                 bool from_irregular, uint64_t fixed_len,
                                 hipStream_t stream);

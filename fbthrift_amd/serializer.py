@@ -434,6 +434,42 @@ class BatchSerializer:
         return offsets[: k + 1], n.value, first.value, last.value, st
 
 
+    # -- schemaless skim ----------------------------------------------------
+    def skim(self, wire, offsets, n=None, max_fields=16, limits=None, stream=None, check=True):
+        """Top-level fields of records [0, n) of an indexed stream
+        (tgpu_skim_batch): `wire` a uint8 device tensor, `offsets` its n+1
+        record starts (device int64). Returns (fields, counts, n_done,
+        status): fields a uint8 device tensor of n * max_fields
+        tgpu_skim_field entries (skim_records() views it as numpy records),
+        counts an int32 device tensor of each record's field count."""
+        import torch
+
+        if n is None:
+            n = offsets.numel() - 1
+        fields = torch.zeros(max(n * max_fields * 16, 16), dtype=torch.uint8, device=wire.device)
+        counts = torch.zeros(max(n, 1), dtype=torch.int32, device=wire.device)
+        lim = None
+        if limits is not None:
+            lim = _lib.Limits(*limits) if not isinstance(limits, _lib.Limits) else limits
+        st, done = _lib.Status(), ctypes.c_uint64()
+        _lib.lib().tgpu_skim_batch(
+            self.context().handle, self.protocol, _ptr(wire), wire.numel(), _ptr(offsets), n,
+            _ptr(fields), max_fields, _ptr(counts),
+            ctypes.byref(lim) if lim is not None else None, _stream(stream), ctypes.byref(st),
+            ctypes.byref(done))
+        if check:
+            raise_for_status(st)
+        return fields, counts[:n], done.value, st
+
+
+def skim_records(fields, n, max_fields):
+    """tgpu_skim_field entries (uint8 tensor or array) as a numpy record
+    array of shape (n, max_fields)."""
+    import numpy as np
+
+    a = fields.cpu().numpy() if hasattr(fields, "cpu") else np.asarray(fields)
+    return a[: n * max_fields * 16].view(np.dtype(_lib.SKIM_FIELDS)).reshape(n, max_fields)
+
 BinarySerializer = BatchSerializer(PROTOCOL_BINARY)
 CompactSerializer = BatchSerializer(PROTOCOL_COMPACT)
 CompactV1Serializer = BatchSerializer(PROTOCOL_COMPACT_V1)

@@ -456,6 +456,45 @@ int tgpu_decode_stream(tgpu_context* ctx, const tgpu_schema* schema, int protoco
                        const tgpu_limits* limits, void* stream, tgpu_status* st,
                        uint64_t* n_records, uint64_t* first_start, uint64_t* last_end);
 
+/*
+ * Schemaless skim: one entry per top-level field of every record, in wire
+ * order — the parse loop of protocol::parseObject
+ * (thrift/lib/cpp2/protocol/detail/Object.h:416-432) with each value kept as
+ * its encoded bytes instead of materialized, as the masked parse stores an
+ * excluded field (setMaskedDataFull, detail/FieldMaskUtil.h:373-388:
+ * wireType + the bytes apache::thrift::skip passes over). Bool fields are
+ * read (parseValueWithMask, FieldMaskUtil.h:441-450): Compact carries the
+ * value in the field header, so its encoded value is empty and the value is
+ * in `flags`.
+ *   offset  absolute byte position of the value in `in` (after the header)
+ *   length  bytes of the value (what skip consumed)
+ *   flags   TGPU_SKIM_BOOL | (value ? TGPU_SKIM_TRUE : 0) for T_BOOL
+ */
+typedef struct tgpu_skim_field {
+  int16_t id;
+  uint8_t ttype; /* wire TType (Compact types mapped to TType) */
+  uint8_t flags;
+  uint32_t length;
+  uint64_t offset;
+} tgpu_skim_field;
+
+enum { TGPU_SKIM_BOOL = 1, TGPU_SKIM_TRUE = 2 };
+
+/*
+ * Skims records [0, n) of an indexed stream (offsets: device, n + 1 entries,
+ * e.g. from tgpu_index_stream with a field-less schema). Record i's fields go
+ * to fields[i * max_fields ...] (device); field_counts[i] (device) receives
+ * its total number of fields — entries past max_fields are counted but not
+ * stored. Errors as tgpu_decode_batch: the first record (in record order)
+ * the reader rejects, or whose end disagrees with offsets[i + 1]
+ * (TGPU_ERR_INDEX_MISMATCH), is reported with the reference's status; n_done
+ * = records before it. Blocking when st != NULL.
+ */
+int tgpu_skim_batch(tgpu_context* ctx, int protocol, const void* in, uint64_t in_len,
+                    const uint64_t* offsets, uint64_t n_records, tgpu_skim_field* fields,
+                    uint32_t max_fields, uint32_t* field_counts, const tgpu_limits* limits,
+                    void* stream, tgpu_status* st, uint64_t* n_done);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -155,3 +155,29 @@ def write_varint(value):
     out = np.zeros(16, np.uint8)
     n = lib().oracle_write_varint(value, _p(out))
     return out[:n].tobytes()
+
+
+SKIM_DTYPE = np.dtype([("id", "<i2"), ("ttype", "u1"), ("flags", "u1"), ("length", "<u4"),
+                       ("offset", "<u8")])
+
+
+def skim(protocol, wire, offsets, n=None, max_fields=16, limits=None):
+    """Schemaless skim (oracle_skim_batch): returns (status, fields (n,
+    max_fields) SKIM_DTYPE records, counts uint32[n], n_done)."""
+    w = _u8(wire)
+    offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = offs.size - 1 if n is None else n
+    fields = np.zeros((max(n, 1), max(max_fields, 1)), SKIM_DTYPE)
+    counts = np.zeros(max(n, 1), np.uint32)
+    L = lib()
+    L.oracle_skim_batch.restype = ctypes.c_int
+    L.oracle_skim_batch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                                    ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                    ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_void_p]
+    lim = Limits(*limits) if limits is not None else None
+    st, done = Status(), ctypes.c_uint64()
+    L.oracle_skim_batch(protocol, _p(w), w.size, _p(offs), n, fields.ctypes.data, max_fields,
+                        counts.ctypes.data, ctypes.byref(lim) if lim else None,
+                        ctypes.byref(st), ctypes.byref(done))
+    return st, fields[:n, :max_fields], counts[:n], done.value

@@ -1167,6 +1167,77 @@ int64_t oracle_skip_value(int protocol, const void* in, uint64_t in_len, uint64_
   }
 }
 
+// Schemaless skim: the field loop of protocol::parseObject
+// (protocol/detail/Object.h:416-432) keeping each value as the bytes
+// apache::thrift::skip passes over (setMaskedDataFull,
+// protocol/detail/FieldMaskUtil.h:373-388); bools are read
+// (FieldMaskUtil.h:441-450). Sequential, record by record; stops at the
+// first record the reader rejects or whose end disagrees with offsets[i+1].
+extern "C++" template <class R>
+int skim_impl(const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n,
+              tgpu_skim_field* fields, uint32_t max_fields, uint32_t* counts,
+              const Limits& lim, tgpu_status* st, uint64_t* n_done) {
+  for (uint64_t i = 0; i < n; ++i) {
+    R r;
+    r.c = Cursor{in, offsets[i], in_len};
+    r.lim = lim;
+    r.height.h = lim.initial_height();
+    uint32_t count = 0;
+    try {
+      if (offsets[i] > in_len || offsets[i + 1] < offsets[i])
+        fail(TGPU_ERR_INDEX_MISMATCH, offsets[i]);
+      int16_t prev = 0;
+      while (true) {
+        uint8_t wt;
+        int16_t id;
+        if (!r.readFieldHeader(prev, wt, id)) break;
+        prev = id;
+        const uint64_t off = r.c.pos;
+        uint8_t flags = 0;
+        if (wt == TGPU_T_BOOL) flags = TGPU_SKIM_BOOL | (r.readBool() ? TGPU_SKIM_TRUE : 0);
+        else r.skip(wt, 0);
+        if (count < max_fields) {
+          tgpu_skim_field& f = fields[i * (uint64_t)max_fields + count];
+          f.id = id;
+          f.ttype = wt;
+          f.flags = flags;
+          f.length = (uint32_t)(r.c.pos - off);
+          f.offset = off;
+        }
+        ++count;
+      }
+      counts[i] = count;
+      if (r.c.pos != offsets[i + 1]) fail(TGPU_ERR_INDEX_MISMATCH, r.c.pos);
+    } catch (const OErr& e) {
+      set_status(st, e.code, i, e.off);
+      if (n_done) *n_done = i;
+      return e.code;
+    }
+  }
+  set_status(st, TGPU_OK, n, 0);
+  if (n_done) *n_done = n;
+  return TGPU_OK;
+}
+
+int oracle_skim_batch(int protocol, const void* in, uint64_t in_len, const uint64_t* offsets,
+                      uint64_t n_records, tgpu_skim_field* fields, uint32_t max_fields,
+                      uint32_t* field_counts, const tgpu_limits* limits, tgpu_status* st,
+                      uint64_t* n_done) {
+  const Limits lim = to_limits(limits);
+  auto p = (const uint8_t*)in;
+  if (protocol == TGPU_PROTOCOL_BINARY)
+    return skim_impl<BinaryReader>(p, in_len, offsets, n_records, fields, max_fields,
+                                   field_counts, lim, st, n_done);
+  if (protocol == TGPU_PROTOCOL_COMPACT)
+    return skim_impl<CompactReader>(p, in_len, offsets, n_records, fields, max_fields,
+                                    field_counts, lim, st, n_done);
+  if (protocol == TGPU_PROTOCOL_COMPACT_V1)
+    return skim_impl<CompactV1Reader>(p, in_len, offsets, n_records, fields, max_fields,
+                                      field_counts, lim, st, n_done);
+  set_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+  return TGPU_ERR_INVALID_ARGUMENT;
+}
+
 int oracle_read_varint(const void* in, uint64_t len, int bits, uint64_t* value,
                        uint64_t* consumed) {
   Cursor c{(const uint8_t*)in, 0, len};

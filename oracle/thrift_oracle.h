@@ -54,6 +54,14 @@ int64_t oracle_skip_value(int protocol, const void* in, uint64_t in_len,
                           uint64_t pos, int ttype, int32_t max_depth,
                           int32_t height);
 
+/* Schemaless skim (tgpu_skim_batch semantics): per record the top-level
+ * fields as (id, wire type, bool flags, value offset, value length). */
+int oracle_skim_batch(int protocol, const void* in, uint64_t in_len,
+                      const uint64_t* offsets, uint64_t n_records,
+                      tgpu_skim_field* fields, uint32_t max_fields,
+                      uint32_t* field_counts, const tgpu_limits* limits,
+                      tgpu_status* st, uint64_t* n_done);
+
 /* Varint / zigzag primitives (VarintUtils-inl.h restated) for unit tests. */
 int oracle_read_varint(const void* in, uint64_t len, int bits,
                        uint64_t* value, uint64_t* consumed);
