@@ -33,16 +33,25 @@ __device__ __forceinline__ Reader skim_reader(const SkimArgs& a, uint64_t start)
 }
 
 // Skims record i into its field slots; returns the reader (error latched).
+// The reader walks `src` (the stream, or an LDS copy of bytes
+// [base, base + src_len) of it) in positions relative to `base`; stored
+// offsets and error offsets are absolute.
 template <int P>
-__device__ Reader skim_one(const SkimArgs& a, uint64_t i, bool store) {
+__device__ Reader skim_one(const SkimArgs& a, uint64_t i, bool store, const uint8_t* src,
+                           uint64_t base, uint64_t src_len) {
+  // slot k of record i at fields[k * n + i] (field-major: a wave's k-th
+  // stores are 64 consecutive entries)
+  tgpu_skim_field* out = a.fields + i;
   using Pr = Proto<P>;
   const uint64_t start = a.offs[i];
-  Reader r = skim_reader(a, start);
+  Reader r = skim_reader(a, start - base);
+  r.p = src;
+  r.end = src_len;
   if (start > a.in_len || a.offs[i + 1] < start) {
-    r.fail(TGPU_ERR_INDEX_MISMATCH, start);
+    r.fail(TGPU_ERR_INDEX_MISMATCH, start - base);
+    r.err_off += base;
     return r;
   }
-  tgpu_skim_field* out = a.fields + i * (uint64_t)a.max_fields;
   uint32_t count = 0;
   int32_t prev = 0;
   while (r.ok()) {
@@ -53,7 +62,9 @@ __device__ Reader skim_one(const SkimArgs& a, uint64_t i, bool store) {
     const uint64_t off = r.pos;
     uint32_t flags = 0;
     if (wt == TGPU_T_BOOL) flags = TGPU_SKIM_BOOL | (Pr::read_bool(r) ? TGPU_SKIM_TRUE : 0);
-    else skip<P>(r, wt, 0);
+    // leaves inline (skip's explicit stack lives in scratch); structs and
+    // containers take the full skip
+    else if (r.max_depth <= 0 || !Pr::skip_leaf(r, wt)) skip<P>(r, wt, 0);
     if (!r.ok()) break;
     if (store && count < a.max_fields) {
       tgpu_skim_field f;
@@ -61,23 +72,57 @@ __device__ Reader skim_one(const SkimArgs& a, uint64_t i, bool store) {
       f.ttype = (uint8_t)wt;
       f.flags = (uint8_t)flags;
       f.length = (uint32_t)(r.pos - off);
-      f.offset = off;
-      out[count] = f;
+      f.offset = off + base;
+      out[(uint64_t)count * a.n] = f;
     }
     ++count;
   }
   if (store) a.counts[i] = count;
-  if (r.ok() && r.pos != a.offs[i + 1]) r.fail(TGPU_ERR_INDEX_MISMATCH, r.pos);
+  if (r.ok() && r.pos + base != a.offs[i + 1]) r.fail(TGPU_ERR_INDEX_MISMATCH, r.pos);
+  r.pos += base;
+  r.err_off += base;
   return r;
 }
 
 template <int P>
+__device__ __forceinline__ Reader skim_global(const SkimArgs& a, uint64_t i, bool store) {
+  return skim_one<P>(a, i, store, a.in, 0, a.in_len);
+}
+
+// One 256-record tile per workgroup: the tile's wire bytes
+// [offs[r0], offs[r1]) are copied to LDS with 16-byte loads when they fit
+// (kSkimTile), and each lane parses its record there; a record whose parse
+// fails on the copy (damaged input, a length running off the tile) is parsed
+// again from HBM, so every status is the stream's own. Tiles too large for
+// LDS parse from HBM directly.
+constexpr uint32_t kSkimTile = 32768;
+
+template <int P>
 __global__ __launch_bounds__(256) void skim_kernel(SkimArgs a) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-    const Reader r = skim_one<P>(a, i, true);
-    if (!r.ok()) atomicMin(&a.res->first_fail, (unsigned long long)i);
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kSkimTile + 16];
+  const uint64_t r0 = (uint64_t)blockIdx.x * 256;
+  const uint64_t r1 = min(r0 + 256, a.n);
+  const uint64_t b0 = a.offs[r0], b1 = a.offs[r1];
+  const uint64_t a0 = b0 & ~15ull;
+  const bool staged = b0 <= b1 && b1 <= a.in_len && b1 - a0 <= kSkimTile;
+  if (staged) {
+    const uint32_t nbytes = (uint32_t)(b1 - a0);
+    const uint32_t nvec = (nbytes + 15) >> 4;
+    for (uint32_t v = threadIdx.x; v < nvec; v += 256) {
+      const uint64_t g = a0 + 16ull * v;
+      if (g + 16 <= a.in_len) {
+        *(uint4*)(tile + 16 * v) = *(const uint4*)(a.in + g);
+      } else {
+        for (uint32_t b = 0; b < 16 && g + b < a.in_len; ++b) tile[16 * v + b] = a.in[g + b];
+      }
+    }
   }
+  __syncthreads();
+  const uint64_t i = r0 + threadIdx.x;
+  if (i >= a.n) return;
+  Reader r = staged ? skim_one<P>(a, i, true, tile, a0, b1 - a0) : skim_global<P>(a, i, true);
+  if (staged && !r.ok()) r = skim_global<P>(a, i, true);
+  if (!r.ok()) atomicMin(&a.res->first_fail, (unsigned long long)i);
 }
 
 template <int P>
@@ -86,7 +131,7 @@ __global__ void skim_finish_kernel(SkimArgs a) {
   DevResult* res = a.res;
   const uint64_t f = res->first_fail;
   if (f < a.n) {
-    const Reader r = skim_one<P>(a, f, false);
+    const Reader r = skim_global<P>(a, f, false);
     res->code = r.ok() ? TGPU_ERR_INDEX_MISMATCH : r.err;
     res->fail_offset = r.ok() ? r.pos : r.err_off;
     res->n_records = f;
@@ -98,17 +143,14 @@ __global__ void skim_finish_kernel(SkimArgs a) {
   }
 }
 
-uint32_t skim_grid(uint64_t n) {
-  const uint64_t b = (n + 255) / 256;
-  return (uint32_t)(b < 8192 ? (b ? b : 1) : 8192);
-}
-
 }  // namespace
 
 hipError_t launch_skim(const SkimArgs& a, int protocol, hipStream_t stream) {
-  if (a.n)
-    TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(skim_kernel<P_>, dim3(skim_grid(a.n)), dim3(256),
-                                                  0, stream, a));
+  if (a.n) {
+    const uint32_t g = (uint32_t)((a.n + 255) / 256);
+    TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(skim_kernel<P_>, dim3(g), dim3(256), 0, stream,
+                                                  a));
+  }
   TGPU_BY_PROTOCOL(protocol,
                    hipLaunchKernelGGL(skim_finish_kernel<P_>, dim3(1), dim3(64), 0, stream, a));
   return hipGetLastError();

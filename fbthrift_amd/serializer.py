@@ -463,12 +463,13 @@ class BatchSerializer:
 
 
 def skim_records(fields, n, max_fields):
-    """tgpu_skim_field entries (uint8 tensor or array) as a numpy record
-    array of shape (n, max_fields)."""
+    """Field-major tgpu_skim_field entries (uint8 tensor or array) as a numpy
+    record array of shape (n, max_fields): [i, k] = field k of record i."""
     import numpy as np
 
     a = fields.cpu().numpy() if hasattr(fields, "cpu") else np.asarray(fields)
-    return a[: n * max_fields * 16].view(np.dtype(_lib.SKIM_FIELDS)).reshape(n, max_fields)
+    a = a[: n * max_fields * 16].view(np.dtype(_lib.SKIM_FIELDS))
+    return a.reshape(max_fields, n).T
 
 BinarySerializer = BatchSerializer(PROTOCOL_BINARY)
 CompactSerializer = BatchSerializer(PROTOCOL_COMPACT)

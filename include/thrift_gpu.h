@@ -482,10 +482,12 @@ enum { TGPU_SKIM_BOOL = 1, TGPU_SKIM_TRUE = 2 };
 
 /*
  * Skims records [0, n) of an indexed stream (offsets: device, n + 1 entries,
- * e.g. from tgpu_index_stream with a field-less schema). Record i's fields go
- * to fields[i * max_fields ...] (device); field_counts[i] (device) receives
- * its total number of fields — entries past max_fields are counted but not
- * stored. Errors as tgpu_decode_batch: the first record (in record order)
+ * e.g. from tgpu_index_stream with a field-less schema). fields (device,
+ * max_fields * n_records entries) is field-major: the k-th field of record i
+ * is fields[k * n_records + i] (so a wavefront's k-th stores are contiguous);
+ * field_counts[i] (device) receives the record's total number of fields —
+ * fields past max_fields are counted but not stored, slots past the count
+ * are left untouched. Errors as tgpu_decode_batch: the first record (in record order)
  * the reader rejects, or whose end disagrees with offsets[i + 1]
  * (TGPU_ERR_INDEX_MISMATCH), is reported with the reference's status; n_done
  * = records before it. Blocking when st != NULL.

@@ -167,7 +167,7 @@ def skim(protocol, wire, offsets, n=None, max_fields=16, limits=None):
     w = _u8(wire)
     offs = np.ascontiguousarray(offsets, dtype=np.uint64)
     n = offs.size - 1 if n is None else n
-    fields = np.zeros((max(n, 1), max(max_fields, 1)), SKIM_DTYPE)
+    fields = np.zeros((max(max_fields, 1), max(n, 1)), SKIM_DTYPE)  # field-major
     counts = np.zeros(max(n, 1), np.uint32)
     L = lib()
     L.oracle_skim_batch.restype = ctypes.c_int
@@ -180,4 +180,4 @@ def skim(protocol, wire, offsets, n=None, max_fields=16, limits=None):
     L.oracle_skim_batch(protocol, _p(w), w.size, _p(offs), n, fields.ctypes.data, max_fields,
                         counts.ctypes.data, ctypes.byref(lim) if lim else None,
                         ctypes.byref(st), ctypes.byref(done))
-    return st, fields[:n, :max_fields], counts[:n], done.value
+    return st, fields[:max_fields, :n].T, counts[:n], done.value

@@ -1197,7 +1197,7 @@ int skim_impl(const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint6
         if (wt == TGPU_T_BOOL) flags = TGPU_SKIM_BOOL | (r.readBool() ? TGPU_SKIM_TRUE : 0);
         else r.skip(wt, 0);
         if (count < max_fields) {
-          tgpu_skim_field& f = fields[i * (uint64_t)max_fields + count];
+          tgpu_skim_field& f = fields[(uint64_t)count * n + i];
           f.id = id;
           f.ttype = wt;
           f.flags = flags;
