@@ -660,7 +660,7 @@ def skim(wl, dev, reps=10):
     for _ in range(reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        wl.S.skim(w, offs, wl.n, max_fields=nf, check=False)
+        wl.S.skim(w, offs, wl.n, max_fields=nf, check=False, fields=fields, counts=counts)
         e1.record()
         torch.cuda.synchronize()
         times.append(e0.elapsed_time(e1) / 1e3)

@@ -9,6 +9,8 @@
 // (tgpu_device.h), so depth / size / varint / bool errors are the ones the
 // decoder reports for the same bytes. The first failing record in record
 // order is re-diagnosed by one lane and published like a decode result.
+#include <cstdlib>
+
 #include "tgpu_device.h"
 
 namespace tgpu {
@@ -94,10 +96,8 @@ __device__ __forceinline__ Reader skim_global(const SkimArgs& a, uint64_t i, boo
 // (kSkimTile), and each lane parses its record there; a record whose parse
 // fails on the copy (damaged input, a length running off the tile) is parsed
 // again from HBM, so every status is the stream's own. Tiles too large for
-// LDS parse from HBM directly.
-constexpr uint32_t kSkimTile = 32768;
-
-template <int P>
+// LDS parse from HBM directly. kSkimTile: LDS bytes of the wire copy.
+template <int P, uint32_t kSkimTile>
 __global__ __launch_bounds__(256) void skim_kernel(SkimArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t tile[kSkimTile + 16];
   const uint64_t r0 = (uint64_t)blockIdx.x * 256;
@@ -145,11 +145,23 @@ __global__ void skim_finish_kernel(SkimArgs a) {
 
 }  // namespace
 
+// Wire copy per 256-record tile: 24 KB (6 workgroups per CU; a config-2 tile
+// is 22.8 KB) unless the stream's mean tile is larger, then 32 KB (4 per CU).
+// Measured on MI355X (tools/skim_ab.py): 24 KB beats 32 KB on configs 2-4
+// even where a share of the tiles overflows to HBM parsing (config 4: 1.52
+// vs 1.96 ms), and 16 KB gains nothing on config 3. TGPU_SKIM_TILE=24|32
+// forces one (A/B).
 hipError_t launch_skim(const SkimArgs& a, int protocol, hipStream_t stream) {
   if (a.n) {
     const uint32_t g = (uint32_t)((a.n + 255) / 256);
-    TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(skim_kernel<P_>, dim3(g), dim3(256), 0, stream,
-                                                  a));
+    uint32_t kb = a.in_len / a.n * 256 <= 24560 ? 24 : 32;
+    if (const char* e = getenv("TGPU_SKIM_TILE")) kb = (uint32_t)atoi(e);
+    if (kb == 24)
+      TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL((skim_kernel<P_, 24560>), dim3(g), dim3(256),
+                                                    0, stream, a));
+    else
+      TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL((skim_kernel<P_, 32752>), dim3(g), dim3(256),
+                                                    0, stream, a));
   }
   TGPU_BY_PROTOCOL(protocol,
                    hipLaunchKernelGGL(skim_finish_kernel<P_>, dim3(1), dim3(64), 0, stream, a));

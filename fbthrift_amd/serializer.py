@@ -435,19 +435,25 @@ class BatchSerializer:
 
 
     # -- schemaless skim ----------------------------------------------------
-    def skim(self, wire, offsets, n=None, max_fields=16, limits=None, stream=None, check=True):
+    def skim(self, wire, offsets, n=None, max_fields=16, limits=None, stream=None, check=True,
+             fields=None, counts=None):
         """Top-level fields of records [0, n) of an indexed stream
         (tgpu_skim_batch): `wire` a uint8 device tensor, `offsets` its n+1
         record starts (device int64). Returns (fields, counts, n_done,
         status): fields a uint8 device tensor of n * max_fields
         tgpu_skim_field entries (skim_records() views it as numpy records),
-        counts an int32 device tensor of each record's field count."""
+        counts an int32 device tensor of each record's field count. `fields`
+        / `counts` may be given (preallocated, reused across calls)."""
         import torch
 
         if n is None:
             n = offsets.numel() - 1
-        fields = torch.zeros(max(n * max_fields * 16, 16), dtype=torch.uint8, device=wire.device)
-        counts = torch.zeros(max(n, 1), dtype=torch.int32, device=wire.device)
+        if fields is None:
+            fields = torch.zeros(max(n * max_fields * 16, 16), dtype=torch.uint8,
+                                 device=wire.device)
+        if counts is None:
+            counts = torch.zeros(max(n, 1), dtype=torch.int32, device=wire.device)
+        assert fields.numel() >= n * max_fields * 16 and counts.numel() >= n
         lim = None
         if limits is not None:
             lim = _lib.Limits(*limits) if not isinstance(limits, _lib.Limits) else limits
