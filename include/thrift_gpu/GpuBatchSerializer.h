@@ -327,6 +327,19 @@ class GpuBatchSerializer {
     if (st.code != TGPU_OK) rethrow(st);
     return size;
   }
+  /* Schemaless skim of n indexed records (tgpu_skim_batch): the field loop
+   * of protocol::parseObject with every value kept as its encoded bytes
+   * (protocol/detail/FieldMaskUtil.h:373-388). fields: max_fields * n
+   * entries, field-major (fields[k * n + i] = field k of record i); counts:
+   * n. Device pointers. Throws on the first record the reader rejects. */
+  void skim(const void* in, uint64_t len, const uint64_t* offsets, uint64_t n,
+            tgpu_skim_field* fields, uint32_t max_fields, uint32_t* counts) {
+    tgpu_status st{};
+    uint64_t done = 0;
+    tgpu_skim_batch(ctx_, Protocol::kId, in, len, offsets, n, fields, max_fields, counts,
+                    &limits_, stream_, &st, &done);
+    if (st.code != TGPU_OK) rethrow(st);
+  }
   /* List arena bytes deserialize() needs for `len` input bytes. */
   uint64_t arenaBytes(uint64_t len) const {
     return len * tgpu_schema_arena_scale(schema_.get(), Protocol::kId);

@@ -120,6 +120,36 @@ int main() {
     (void)hipFree(d_b2);
   }
 
+  // Schemaless skim (tgpu_skim_batch): field k of record i is an i64 whose
+  // 8 value bytes follow its 3-byte header at i * 89 + 11 k.
+  {
+    BinaryBatchSerializer bin(flat);
+    CHECK(bin.serialize(d_rec, n, d_wire, n * 89) == n * 89);
+    std::vector<uint64_t> ho(n + 1);
+    for (uint64_t i = 0; i <= n; ++i) ho[i] = i * 89;
+    uint64_t* d_offs = dev_alloc<uint64_t>(n + 1);
+    tgpu_skim_field* d_f = dev_alloc<tgpu_skim_field>(8 * n);
+    uint32_t* d_cnt = dev_alloc<uint32_t>(n);
+    CHECK(hipMemcpy(d_offs, ho.data(), (n + 1) * 8, hipMemcpyHostToDevice) == hipSuccess);
+    bin.skim(d_wire, n * 89, d_offs, n, d_f, 8, d_cnt);
+    std::vector<tgpu_skim_field> f(8 * n);
+    std::vector<uint32_t> cnt(n);
+    CHECK(hipMemcpy(f.data(), d_f, 8 * n * sizeof(tgpu_skim_field), hipMemcpyDeviceToHost) ==
+          hipSuccess);
+    CHECK(hipMemcpy(cnt.data(), d_cnt, n * 4, hipMemcpyDeviceToHost) == hipSuccess);
+    for (uint64_t i = 0; i < n; i += 997) {
+      CHECK(cnt[i] == 8);
+      for (int k = 0; k < 8; ++k) {
+        const tgpu_skim_field& e = f[k * n + i];
+        CHECK(e.id == k + 1 && e.ttype == TGPU_T_I64 && e.length == 8);
+        CHECK(e.offset == i * 89 + 11 * k + 3);
+      }
+    }
+    (void)hipFree(d_offs);
+    (void)hipFree(d_f);
+    (void)hipFree(d_cnt);
+  }
+
   // Binary readBool: a byte >= 2 throws TProtocolException(INVALID_DATA)
   // (BinaryProtocol-inl.h:489-495; BinaryProtocolTest.cpp:30-41).
   GpuSchema wb({{{1, TGPU_T_I64}, {2, TGPU_T_BOOL}, {3, TGPU_T_I32}}});
