@@ -69,13 +69,14 @@ __device__ Reader skim_one(const SkimArgs& a, uint64_t i, bool store, const uint
     else if (r.max_depth <= 0 || !Pr::skip_leaf(r, wt)) skip<P>(r, wt, 0);
     if (!r.ok()) break;
     if (store && count < a.max_fields) {
-      tgpu_skim_field f;
-      f.id = (int16_t)id;
-      f.ttype = (uint8_t)wt;
-      f.flags = (uint8_t)flags;
-      f.length = (uint32_t)(r.pos - off);
-      f.offset = off + base;
-      out[(uint64_t)count * a.n] = f;
+      // one 16-byte entry {id, ttype, flags | length | offset}
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const uint64_t o = off + base;
+      const u32x4 e = {(uint32_t)(uint16_t)id | (wt << 16) | (flags << 24),
+                       (uint32_t)(r.pos - off), (uint32_t)o, (uint32_t)(o >> 32)};
+      u32x4* dst = (u32x4*)(out + (uint64_t)count * a.n);
+      if (a.nt_stores) __builtin_nontemporal_store(e, dst);
+      else *dst = e;
     }
     ++count;
   }

@@ -1186,7 +1186,8 @@ int tgpu_skim_batch(tgpu_context* ctx, int protocol, const void* in, uint64_t in
                     uint32_t max_fields, uint32_t* field_counts, const tgpu_limits* limits,
                     void* stream, tgpu_status* st, uint64_t* n_done) {
   if (!ctx || !valid_protocol(protocol) ||
-      (n && (!offsets || !field_counts || (max_fields && !fields) || (!in && in_len)))) {
+      (n && (!offsets || !field_counts || (max_fields && !fields) || (!in && in_len))) ||
+      ((uintptr_t)fields & 15)) {
     fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
     return TGPU_ERR_INVALID_ARGUMENT;
   }
@@ -1204,6 +1205,7 @@ int tgpu_skim_batch(tgpu_context* ctx, int protocol, const void* in, uint64_t in
   a.max_depth = limits ? limits->max_depth : 12000;
   a.height = limits ? limits->height : 0;
   a.res = ctx->d_res;
+  a.nt_stores = getenv("TGPU_SKIM_NT") ? atoi(getenv("TGPU_SKIM_NT")) : 1;
   (void)hipGetLastError();
   hipError_t e = launch_result_init(ctx->d_res, n, s);
   if (e == hipSuccess) e = launch_skim(a, protocol, s);

@@ -204,6 +204,7 @@ struct SkimArgs {
   uint32_t max_fields;
   int32_t string_limit, container_limit, max_depth, height;
   DevResult* res;
+  int nt_stores;  // entries stored non-temporally (never re-read here)
 };
 
 struct EncodeArgs {

@@ -483,7 +483,7 @@ enum { TGPU_SKIM_BOOL = 1, TGPU_SKIM_TRUE = 2 };
 /*
  * Skims records [0, n) of an indexed stream (offsets: device, n + 1 entries,
  * e.g. from tgpu_index_stream with a field-less schema). fields (device,
- * max_fields * n_records entries) is field-major: the k-th field of record i
+ * 16-byte aligned, max_fields * n_records entries) is field-major: the k-th field of record i
  * is fields[k * n_records + i] (so a wavefront's k-th stores are contiguous);
  * field_counts[i] (device) receives the record's total number of fields —
  * fields past max_fields are counted but not stored, slots past the count
