@@ -440,8 +440,9 @@ class BatchSerializer:
         """Top-level fields of records [0, n) of an indexed stream
         (tgpu_skim_batch): `wire` a uint8 device tensor, `offsets` its n+1
         record starts (device int64). Returns (fields, counts, n_done,
-        status): fields a uint8 device tensor of n * max_fields
-        tgpu_skim_field entries (skim_records() views it as numpy records),
+        status): fields a uint8 device tensor of max_fields * n
+        tgpu_skim_field entries, field-major (skim_records() views it as a
+        numpy (n, max_fields) record array),
         counts an int32 device tensor of each record's field count. `fields`
         / `counts` may be given (preallocated, reused across calls)."""
         import torch
@@ -466,6 +467,21 @@ class BatchSerializer:
         if check:
             raise_for_status(st)
         return fields, counts[:n], done.value, st
+
+    def skim_stream(self, wire, max_fields=16, limits=None, stream=None):
+        """Skim of an unindexed stream of back-to-back records (a file): the
+        record index is found first without a schema (tgpu_index_stream with
+        a field-less struct: every record walked by the reader's skip), then
+        tgpu_skim_batch runs over it. Returns (offsets[:n+1], fields, counts,
+        n); raises on the first record the reader rejects."""
+        from .schema import Schema, Struct
+
+        if getattr(self, "_any_schema", None) is None:
+            self._any_schema = GpuSchema(Schema(Struct("Any", [])))
+        offs, n, _, _, _ = self.index_stream(self._any_schema, wire, limits=limits, stream=stream)
+        fields, counts, _, _ = self.skim(wire, offs, n, max_fields=max_fields, limits=limits,
+                                         stream=stream)
+        return offs, fields, counts, n
 
 
 def skim_records(fields, n, max_fields):

@@ -223,3 +223,27 @@ def test_oracle_skim_status_is_schemaless_decode_status(case):
         assert dst.code == 0 and (st.code, st.byte_offset) == (3, 3), name
         return
     assert st.as_tuple() == dst.as_tuple(), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["flat8_binary", "mixed_compact", "nested_binary",
+                                  "maps_compact_v1", "unions_compact"])
+def test_gpu_skim_stream(gpu, name):
+    """Unindexed stream: schemaless index, then skim — the golden index and
+    the oracle's entries."""
+    import torch
+
+    from fbthrift_amd import serializer as S
+
+    c = helpers.Case(name)
+    ser = {0: S.BinarySerializer, 2: S.CompactSerializer, 0x102: S.CompactV1Serializer}[c.protocol]
+    w = torch.from_numpy(np.frombuffer(c.wire, np.uint8).copy()).to(gpu)
+    offs, fields, counts, n = ser.skim_stream(w, max_fields=32)
+    assert n == c.n
+    assert np.array_equal(offs.cpu().numpy().astype(np.uint64), c.offsets)
+    ost, ofields, ocounts, _ = oracle.skim(c.protocol, c.wire, c.offsets, c.n, 32)
+    got = S.skim_records(fields, n, 32)
+    cnt = counts.cpu().numpy()
+    assert np.array_equal(cnt, ocounts)
+    for i in range(n):
+        assert np.array_equal(got[i, :cnt[i]], ofields[i, :cnt[i]])
