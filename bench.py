@@ -309,8 +309,7 @@ class FileShards(Mixed):
         for r in sizes:
             self.enc_ranges.append((off, off + r[0]))
             off += r[0]
-        b, e = self.ranges[rank]
-        self.need = (b, min(e + self.overlap, self.file_len))
+        self.need = shard.need_range(self.ranges, self.overlap, self.file_len, rank)
         # N=1: the file is this rank's encode output itself
         self.buf = self.wire if self.world == 1 else torch.empty(
             self.need[1] - self.need[0] + 16, dtype=torch.uint8, device=dev)
@@ -320,15 +319,11 @@ class FileShards(Mixed):
 
     # ---- collectives ---------------------------------------------------------
     def _gather(self, vals):
-        import torch
         import torch.distributed as dist
 
-        if self.world_size() == 1:
-            return [list(vals)]
-        t = torch.tensor(vals, dtype=torch.int64, device=self.dev)
-        out = [torch.empty_like(t) for _ in range(self.world_size())]
-        dist.all_gather(out, t)
-        return [[int(x) for x in o.tolist()] for o in out]
+        from fbthrift_amd import shard
+
+        return shard.tensor_gather(dist.all_gather, self.dev, self.world_size())(vals)
 
     @staticmethod
     def world_size():
@@ -338,26 +333,14 @@ class FileShards(Mixed):
 
     def redistribute(self):
         """File bytes [need) of every rank from the ranks that encoded them."""
-        import torch
         import torch.distributed as dist
 
-        lo, hi = self.need
+        from fbthrift_amd import shard
+
         if self.world == 1:
             return
-        mine = self.enc_ranges[self.rank]
-        send, send_sizes, recv_sizes = [], [], []
-        for d in range(self.world):
-            b, e = self.ranges[d]
-            nlo, nhi = b, min(e + self.overlap, self.file_len)
-            a0, a1 = max(mine[0], nlo), min(mine[1], nhi)
-            if a1 > a0:
-                send.append(self.wire[a0 - mine[0]: a1 - mine[0]])
-            send_sizes.append(max(a1 - a0, 0))
-            s0, s1 = self.enc_ranges[d]
-            r0, r1 = max(s0, lo), min(s1, hi)
-            recv_sizes.append(max(r1 - r0, 0))
-        inp = torch.cat(send) if send else torch.empty(0, dtype=torch.uint8, device=self.dev)
-        dist.all_to_all_single(self.buf[: hi - lo], inp, recv_sizes, send_sizes)
+        shard.redistribute(self.wire, self.enc_ranges, self.ranges, self.overlap, self.file_len,
+                           self.rank, self.buf, dist.all_to_all_single)
 
     def decode(self):
         from fbthrift_amd import shard

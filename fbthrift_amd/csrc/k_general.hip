@@ -30,43 +30,14 @@ __global__ void result_init_kernel(DevResult* res, uint64_t n) {
   res->n_records = n;
   res->n_irregular = 0;
   res->first_start = kNone;
-  res->pad2 = 0;
+  res->n_deep = 0;
+  res->n_deep_chunks = 0;
 }
 
-__device__ __forceinline__ Reader make_reader(const DecodeArgs& a, uint64_t start) {
-  Reader r;
-  r.p = a.in;
-  r.pos = start;
-  r.end = a.in_len;
-  r.height = (int64_t)(a.height ? a.height : a.max_depth) + 1;
-  r.string_limit = a.string_limit;
-  r.container_limit = a.container_limit;
-  r.max_depth = a.max_depth;
-  r.err = 0;
-  r.err_off = 0;
-  r.has_bool = false;
-  r.bool_val = false;
-  return r;
-}
-
-// Parses record i (record buffer zeroed first). Returns the reader.
+// Parses record i (record buffer zeroed first); lane: deep-pass lane or -1.
 template <int P>
-__device__ Reader decode_one(const DecodeArgs& a, uint64_t i) {
-  uint8_t* rec = a.recs + i * a.rec_size;
-  if ((a.rec_size & 7) == 0) {
-    for (uint32_t b = 0; b < a.rec_size; b += 8) *(uint64_t*)(rec + b) = 0;
-  } else {
-    for (uint32_t b = 0; b < a.rec_size; ++b) rec[b] = 0;
-  }
-  const uint64_t start = a.offs[i];
-  Reader r = make_reader(a, start);
-  if (start > a.in_len || (a.check_index && a.offs[i + 1] < start)) {
-    r.fail(TGPU_ERR_INDEX_MISMATCH, start);
-    return r;
-  }
-  read_record<P>(r, a.sc, rec, a.arena, a.arena_cap);
-  if (r.ok() && a.check_index && r.pos != a.offs[i + 1]) r.fail(TGPU_ERR_INDEX_MISMATCH, r.pos);
-  return r;
+__device__ __forceinline__ Reader decode_one(const DecodeArgs& a, uint64_t i, int lane = 0) {
+  return decode_record<P>(a, i, lane);
 }
 
 // Indexed streams: one lane per record, records independent.
@@ -74,7 +45,21 @@ template <int P>
 __global__ __launch_bounds__(256) void general_decode_kernel(DecodeArgs a) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-    const Reader r = decode_one<P>(a, i);
+    const Reader r = decode_one<P>(a, i, -1);
+    if (!r.ok()) defer_or_fail(r, a.deep, &a.res->first_fail, i);
+  }
+}
+
+// The records the bulk passes deferred (a skip nested past the private
+// frames): each lane keeps max_depth frames in HBM.
+template <int P>
+__global__ __launch_bounds__(64) void deep_decode_kernel(DecodeArgs a) {
+  const uint32_t lane = blockIdx.x * 64 + threadIdx.x;
+  if (lane >= a.deep.lanes) return;
+  const uint64_t m = *a.deep.count;
+  for (uint64_t k = lane; k < m; k += a.deep.lanes) {
+    const uint64_t i = a.deep.list[k];
+    const Reader r = decode_one<P>(a, i, (int)lane);
     if (!r.ok()) atomicMin(&a.res->first_fail, (unsigned long long)i);
   }
 }
@@ -264,14 +249,25 @@ hipError_t launch_serial_decode(const DecodeArgs& a, int protocol, bool from_irr
   return hipGetLastError();
 }
 
+hipError_t launch_deep_decode(const DecodeArgs& a, int protocol, hipStream_t stream) {
+  if (!a.deep.lanes) return hipSuccess;
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(deep_decode_kernel<P_>, dim3((a.deep.lanes + 63) / 64),
+                                                dim3(64), 0, stream, a));
+  return hipGetLastError();
+}
+
 hipError_t launch_decode_finish(const DecodeArgs& a, int protocol, uint64_t fixed_len,
                                 hipStream_t stream) {
+  const hipError_t e = launch_deep_decode(a, protocol, stream);
+  if (e != hipSuccess) return e;
   TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(decode_finish_kernel<P_>, dim3(1), dim3(64), 0, stream, a,
                        fixed_len));
   return hipGetLastError();
 }
 
 hipError_t launch_stream_decode_finish(const DecodeArgs& a, int protocol, hipStream_t stream) {
+  const hipError_t e = launch_deep_decode(a, protocol, stream);
+  if (e != hipSuccess) return e;
   TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(stream_decode_finish_kernel<P_>, dim3(1), dim3(64), 0,
                        stream, a));
   return hipGetLastError();

@@ -36,19 +36,11 @@ using prog::kPosCap;
 using prog::kTile;
 using prog::kTileLanes;
 
-__device__ __forceinline__ dev::Reader reader_at(const IndexArgs& a, uint64_t pos) {
-  dev::Reader r;
-  r.p = a.in;
-  r.pos = pos;
-  r.end = a.in_len;
-  r.height = (int64_t)(a.height ? a.height : a.max_depth) + 1;
-  r.string_limit = a.string_limit;
-  r.container_limit = a.container_limit;
-  r.max_depth = a.max_depth;
-  r.err = 0;
-  r.err_off = 0;
-  r.has_bool = false;
-  r.bool_val = false;
+// lane >= 0: the deep-pass lane whose HBM skip frames the reader may use.
+__device__ __forceinline__ dev::Reader reader_at(const IndexArgs& a, uint64_t pos, int lane) {
+  dev::Reader r = dev::make_reader(a.in, pos, a.in_len, a.string_limit, a.container_limit,
+                                   a.max_depth, a.height);
+  if (lane >= 0) dev::attach_slab(r, a.deep, (uint32_t)lane);
   return r;
 }
 
@@ -62,10 +54,13 @@ struct Chain {
 // Records back to back from p while p < hi. canonical_first: the first record
 // must match the program (speculation); returns false if it does not.
 // emit: record starts written to emit[0..) (at most emit_cap).
+// A record nested past the private skip frames (lane < 0) ends the chain
+// with out.code = kErrDeep: speculation treats it as a failed chain (the
+// repair lane, which has HBM frames, walks it), emission defers the chunk.
 template <int P>
 __device__ bool chain(const IndexArgs& a, uint64_t p, uint64_t hi, bool canonical_first,
                       uint8_t* scratch, Chain& out, uint64_t* emit, uint64_t emit_cap,
-                      uint64_t max_count) {
+                      uint64_t max_count, int lane = -1) {
   out.count = 0;
   out.code = 0;
   out.err_off = 0;
@@ -84,7 +79,7 @@ __device__ bool chain(const IndexArgs& a, uint64_t p, uint64_t hi, bool canonica
       // speculation: a candidate start must open with a canonical record
       // (schemas without a program: any record the reader accepts)
       if (canonical_first && out.count == 0 && a.prog) return false;
-      dev::Reader r = reader_at(a, p);
+      dev::Reader r = reader_at(a, p, lane);
       dev::read_record<P>(r, a.sc, scratch, nullptr, kDiscardArena);
       if (!r.ok()) {
         if (canonical_first && out.count == 0) return false;
@@ -312,7 +307,7 @@ __global__ void index_fix_kernel(IndexArgs a) {
         a.pf[j] = 0;
       } else {
         Chain c;
-        chain<P>(a, T, hi, false, scratch, c, nullptr, 0, kNo);
+        chain<P>(a, T, hi, false, scratch, c, nullptr, 0, kNo, 0);
         a.s[j] = T;
         a.cnt[j] = c.count;
         a.pf[j] = 0;
@@ -365,19 +360,38 @@ __global__ __launch_bounds__(256) void index_emit_kernel(IndexArgs a) {
   }
 }
 
+// Emission of chunk j's chain from where the program stopped (ep[j]) with
+// the general reader; lane >= 0: deep pass (HBM skip frames).
 template <int P>
-__global__ __launch_bounds__(256) void index_emit_cont_kernel(IndexArgs a) {
-  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= a.n_chunks || a.ep[j] == kNo) return;
+__device__ __forceinline__ void emit_cont(const IndexArgs& a, uint64_t j, int lane) {
   const uint64_t b = a.base[j] + a.ec[j];
   const uint64_t n = a.cnt[j] - a.ec[j];
   if (b > a.max_records) return;
   Chain c;
   chain<P>(a, a.ep[j], kNo, false, a.scratch + j * a.rec_size, c, a.offs + b,
-           a.max_records + 1 - b, n);
+           a.max_records + 1 - b, n, lane);
+  if (c.code == kErrDeep) {  // the deep pass re-walks the whole chain
+    a.deep_chunks[atomicAdd(&a.res->n_deep_chunks, 1ull)] = j;
+    return;
+  }
   if (a.recs)  // fused decode: these records take the general decoder
     for (uint64_t i = 0; i < c.count && b + i < a.n_decode; ++i)
       a.irr[atomicAdd(a.nirr, 1ull)] = b + i;
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void index_emit_cont_kernel(IndexArgs a) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= a.n_chunks || a.ep[j] == kNo) return;
+  emit_cont<P>(a, j, -1);
+}
+
+template <int P>
+__global__ __launch_bounds__(64) void index_deep_emit_kernel(IndexArgs a) {
+  const uint32_t lane = blockIdx.x * 64 + threadIdx.x;
+  if (lane >= a.deep.lanes) return;
+  const uint64_t m = a.res->n_deep_chunks;
+  for (uint64_t k = lane; k < m; k += a.deep.lanes) emit_cont<P>(a, a.deep_chunks[k], (int)lane);
 }
 
 // Fused decode: a stream that ends (or fails) before n_decode records hands
@@ -499,6 +513,10 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
   else
     hipLaunchKernelGGL(index_emit_kernel, g, b, 0, stream, a);
   TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_emit_cont_kernel<P_>, g, b, 0, stream, x));
+  if (a.deep.lanes)
+    TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_deep_emit_kernel<P_>,
+                                                    dim3((a.deep.lanes + 63) / 64), dim3(64), 0,
+                                                    stream, x));
   hipLaunchKernelGGL(index_finish_kernel, dim3(1), dim3(64), 0, stream, a, a.scal + 5);
   if (decode)
     hipLaunchKernelGGL(index_decode_tail_kernel, dim3(1), dim3(64), 0, stream, x, a.scal + 5);

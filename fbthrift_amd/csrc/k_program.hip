@@ -47,28 +47,8 @@ __global__ __launch_bounds__(256) void general_decode_list_kernel(DecodeArgs a,
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < m; k += stride) {
     const uint64_t i = list[k];
-    uint8_t* rec = a.recs + i * a.rec_size;
-    for (uint32_t b = 0; b < a.rec_size; ++b) rec[b] = 0;
-    const uint64_t start = a.offs[i];
-    dev::Reader r;
-    r.p = a.in;
-    r.pos = start;
-    r.end = a.in_len;
-    r.height = (int64_t)(a.height ? a.height : a.max_depth) + 1;
-    r.string_limit = a.string_limit;
-    r.container_limit = a.container_limit;
-    r.max_depth = a.max_depth;
-    r.err = 0;
-    r.err_off = 0;
-    r.has_bool = false;
-    r.bool_val = false;
-    if (start > a.in_len || (a.check_index && a.offs[i + 1] < start)) {
-      r.fail(TGPU_ERR_INDEX_MISMATCH, start);
-    } else {
-      dev::read_record<Pr>(r, a.sc, rec, a.arena, a.arena_cap);
-      if (r.ok() && a.check_index && r.pos != a.offs[i + 1]) r.fail(TGPU_ERR_INDEX_MISMATCH, r.pos);
-    }
-    if (!r.ok()) atomicMin(&a.res->first_fail, (unsigned long long)i);
+    const dev::Reader r = dev::decode_record<Pr>(a, i, -1);
+    if (!r.ok()) dev::defer_or_fail(r, a.deep, &a.res->first_fail, i);
   }
 }
 

@@ -18,37 +18,21 @@ namespace {
 
 using namespace dev;
 
-__device__ __forceinline__ Reader skim_reader(const SkimArgs& a, uint64_t start) {
-  Reader r;
-  r.p = a.in;
-  r.pos = start;
-  r.end = a.in_len;
-  r.height = (int64_t)(a.height ? a.height : a.max_depth) + 1;
-  r.string_limit = a.string_limit;
-  r.container_limit = a.container_limit;
-  r.max_depth = a.max_depth;
-  r.err = 0;
-  r.err_off = 0;
-  r.has_bool = false;
-  r.bool_val = false;
-  return r;
-}
-
 // Skims record i into its field slots; returns the reader (error latched).
 // The reader walks `src` (the stream, or an LDS copy of bytes
 // [base, base + src_len) of it) in positions relative to `base`; stored
 // offsets and error offsets are absolute.
 template <int P>
 __device__ Reader skim_one(const SkimArgs& a, uint64_t i, bool store, const uint8_t* src,
-                           uint64_t base, uint64_t src_len) {
+                           uint64_t base, uint64_t src_len, int lane) {
   // slot k of record i at fields[k * n + i] (field-major: a wave's k-th
   // stores are 64 consecutive entries)
   tgpu_skim_field* out = a.fields + i;
   using Pr = Proto<P>;
   const uint64_t start = a.offs[i];
-  Reader r = skim_reader(a, start - base);
-  r.p = src;
-  r.end = src_len;
+  Reader r = make_reader(src, start - base, src_len, a.string_limit, a.container_limit,
+                         a.max_depth, a.height);
+  if (lane >= 0) attach_slab(r, a.deep, (uint32_t)lane);
   if (start > a.in_len || a.offs[i + 1] < start) {
     r.fail(TGPU_ERR_INDEX_MISMATCH, start - base);
     r.err_off += base;
@@ -88,8 +72,9 @@ __device__ Reader skim_one(const SkimArgs& a, uint64_t i, bool store, const uint
 }
 
 template <int P>
-__device__ __forceinline__ Reader skim_global(const SkimArgs& a, uint64_t i, bool store) {
-  return skim_one<P>(a, i, store, a.in, 0, a.in_len);
+__device__ __forceinline__ Reader skim_global(const SkimArgs& a, uint64_t i, bool store,
+                                              int lane) {
+  return skim_one<P>(a, i, store, a.in, 0, a.in_len, lane);
 }
 
 // One 256-record tile per workgroup: the tile's wire bytes
@@ -121,9 +106,23 @@ __global__ __launch_bounds__(256) void skim_kernel(SkimArgs a) {
   __syncthreads();
   const uint64_t i = r0 + threadIdx.x;
   if (i >= a.n) return;
-  Reader r = staged ? skim_one<P>(a, i, true, tile, a0, b1 - a0) : skim_global<P>(a, i, true);
-  if (staged && !r.ok()) r = skim_global<P>(a, i, true);
-  if (!r.ok()) atomicMin(&a.res->first_fail, (unsigned long long)i);
+  Reader r = staged ? skim_one<P>(a, i, true, tile, a0, b1 - a0, -1)
+                    : skim_global<P>(a, i, true, -1);
+  if (staged && !r.ok() && r.err != kErrDeep) r = skim_global<P>(a, i, true, -1);
+  if (!r.ok()) defer_or_fail(r, a.deep, &a.res->first_fail, i);
+}
+
+// Records the skim deferred (a value nested past the private skip frames).
+template <int P>
+__global__ __launch_bounds__(64) void deep_skim_kernel(SkimArgs a) {
+  const uint32_t lane = blockIdx.x * 64 + threadIdx.x;
+  if (lane >= a.deep.lanes) return;
+  const uint64_t m = *a.deep.count;
+  for (uint64_t k = lane; k < m; k += a.deep.lanes) {
+    const uint64_t i = a.deep.list[k];
+    const Reader r = skim_global<P>(a, i, true, (int)lane);
+    if (!r.ok()) atomicMin(&a.res->first_fail, (unsigned long long)i);
+  }
 }
 
 template <int P>
@@ -132,7 +131,7 @@ __global__ void skim_finish_kernel(SkimArgs a) {
   DevResult* res = a.res;
   const uint64_t f = res->first_fail;
   if (f < a.n) {
-    const Reader r = skim_global<P>(a, f, false);
+    const Reader r = skim_global<P>(a, f, false, 0);
     res->code = r.ok() ? TGPU_ERR_INDEX_MISMATCH : r.err;
     res->fail_offset = r.ok() ? r.pos : r.err_off;
     res->n_records = f;
@@ -164,6 +163,10 @@ hipError_t launch_skim(const SkimArgs& a, int protocol, hipStream_t stream) {
       TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL((skim_kernel<P_, 32752>), dim3(g), dim3(256),
                                                     0, stream, a));
   }
+  if (a.deep.lanes)
+    TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(deep_skim_kernel<P_>,
+                                                  dim3((a.deep.lanes + 63) / 64), dim3(64), 0,
+                                                  stream, a));
   TGPU_BY_PROTOCOL(protocol,
                    hipLaunchKernelGGL(skim_finish_kernel<P_>, dim3(1), dim3(64), 0, stream, a));
   return hipGetLastError();

@@ -40,7 +40,12 @@ struct tgpu_context {
   unsigned long long* d_block_sums = nullptr;
   unsigned long long* d_scan_part = nullptr;  // partial sums of the tile scan
   uint64_t* d_irr = nullptr;                  // program decode: irregular record list
+  uint64_t* d_deep = nullptr;                 // records deferred to the deep pass
   uint64_t reserved = 0;  // records
+  // deep-pass skip frames (DeepArgs): slab_lanes x slab_frames, grow-only
+  uint8_t* d_slabs = nullptr;
+  uint64_t slab_frames = 0;
+  uint32_t slab_lanes = 0;
   // stream indexer workspace (per chunk)
   uint8_t* d_index = nullptr;
   uint64_t index_bytes = 0;
@@ -435,10 +440,12 @@ int ensure_workspace(tgpu_context* ctx, uint64_t n) {
   if (ctx->d_block_sums) (void)hipFree(ctx->d_block_sums);
   if (ctx->d_scan_part) (void)hipFree(ctx->d_scan_part);
   if (ctx->d_irr) (void)hipFree(ctx->d_irr);
+  if (ctx->d_deep) (void)hipFree(ctx->d_deep);
   ctx->d_offs = nullptr;
   ctx->d_block_sums = nullptr;
   ctx->d_scan_part = nullptr;
   ctx->d_irr = nullptr;
+  ctx->d_deep = nullptr;
   ctx->reserved = 0;
   const uint64_t tiles = (want + 255) / 256;
   if (hipMalloc(&ctx->d_offs, (want + 1) * sizeof(uint64_t)) != hipSuccess) return TGPU_ERR_HIP;
@@ -448,9 +455,37 @@ int ensure_workspace(tgpu_context* ctx, uint64_t n) {
       hipSuccess)
     return TGPU_ERR_HIP;
   if (hipMalloc(&ctx->d_irr, want * sizeof(uint64_t)) != hipSuccess) return TGPU_ERR_HIP;
+  if (hipMalloc(&ctx->d_deep, want * sizeof(uint64_t)) != hipSuccess) return TGPU_ERR_HIP;
   ctx->reserved = want;
   return TGPU_OK;
 }
+
+// Skip frames for the deep pass: max_depth + 2 frames per lane (the skip's
+// depth check fires first), up to kMaxDeepFrames; as many lanes (<= 256) as
+// fit 64 MiB. Deferred records are rare (a value nested past 16 levels), so
+// the pass's width only bounds its time, never its result.
+int ensure_deep(tgpu_context* ctx, int32_t max_depth) {
+  const uint64_t want = std::min<uint64_t>(std::max<int64_t>((int64_t)max_depth + 2, 1),
+                                           kMaxDeepFrames);
+  if (ctx->d_slabs && ctx->slab_frames >= want) return TGPU_OK;
+  if (ctx->d_slabs) (void)hipFree(ctx->d_slabs);
+  ctx->d_slabs = nullptr;
+  ctx->slab_frames = 0;
+  ctx->slab_lanes = 0;
+  const uint64_t frame = 12;  // sizeof(dev::SkipFrame)
+  const uint64_t lanes = std::min<uint64_t>(256, std::max<uint64_t>(1, (64ull << 20) / (want * frame)));
+  if (hipMalloc(&ctx->d_slabs, lanes * want * frame) != hipSuccess) return TGPU_ERR_HIP;
+  ctx->slab_frames = want;
+  ctx->slab_lanes = (uint32_t)lanes;
+  return TGPU_OK;
+}
+
+DeepArgs deep_args(tgpu_context* ctx) {
+  return DeepArgs{ctx->d_deep, &ctx->d_res->n_deep, ctx->d_slabs, ctx->slab_frames,
+                  ctx->slab_lanes, 0};
+}
+
+int32_t limit_depth(const tgpu_limits* limits) { return limits ? limits->max_depth : 12000; }
 
 // The schema's compiled kernels for `protocol` (tgpu_jit.cpp policy), or
 // nullptr: the interpreting kernels run.
@@ -527,6 +562,7 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   x.max_records = max_records;
   x.fill_to = fill_to;
   x.res = ctx->d_res;
+  x.deep = deep_args(ctx);
   if (dec) {
     x.recs = dec->recs;
     x.arena = dec->arena;
@@ -540,7 +576,7 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   const uint64_t rs = (x.rec_size + 7) & ~7u;
   const uint64_t parts = scan_tiles_parts(C) + 1;
   const uint64_t lane_words = x.chunk == index_tile_bytes() ? C * index_tile_lanes() : 0;
-  const uint64_t need = 8 * (8 * C + parts + 8) + C * rs + 4 * lane_words;
+  const uint64_t need = 8 * (9 * C + parts + 9) + C * rs + 4 * lane_words;
   if (need > ctx->index_bytes) {
     if (ctx->d_index) (void)hipFree(ctx->d_index);
     ctx->d_index = nullptr;
@@ -561,6 +597,7 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   x.scal = (unsigned long long*)(w + 8 * C + parts);
   x.scratch = (uint8_t*)(w + 8 * C + parts + 8);
   x.lanes = (uint32_t*)(x.scratch + C * rs);
+  x.deep_chunks = (uint64_t*)(x.lanes + lane_words + (lane_words & 1));
   if (x.n_chunks == 0) {
     // nothing starts in [begin, end): the index is just the end position
     if (e == hipSuccess) e = launch_index_empty(x.res, offs, x.begin, fill_to, s);
@@ -768,6 +805,8 @@ void tgpu_context_destroy(tgpu_context* c) {
   if (c->d_block_sums) (void)hipFree(c->d_block_sums);
   if (c->d_scan_part) (void)hipFree(c->d_scan_part);
   if (c->d_irr) (void)hipFree(c->d_irr);
+  if (c->d_deep) (void)hipFree(c->d_deep);
+  if (c->d_slabs) (void)hipFree(c->d_slabs);
   if (c->d_index) (void)hipFree(c->d_index);
   if (c->d_xrec) (void)hipFree(c->d_xrec);
   if (c->d_xarena) (void)hipFree(c->d_xarena);
@@ -948,6 +987,7 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   }
   const hipStream_t s = (hipStream_t)stream;
   int rc = ensure_workspace(ctx, n);
+  if (!rc) rc = ensure_deep(ctx, limit_depth(limits));
   if (rc) {
     fill_status(st, rc, 0, 0);
     return rc;
@@ -966,6 +1006,7 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   a.height = limits ? limits->height : 0;
   a.rec_size = schema->structs[0].size;
   a.res = ctx->d_res;
+  a.deep = deep_args(ctx);
   (void)hipGetLastError();  // drop a stale error left by another library
   hipError_t e = launch_result_init(ctx->d_res, n, s);
   uint64_t fixed = 0;
@@ -1101,6 +1142,7 @@ int tgpu_decode_stream(tgpu_context* ctx, const tgpu_schema* schema, int protoco
   }
   const hipStream_t s = (hipStream_t)stream;
   int rc = ensure_workspace(ctx, max_records + 1);
+  if (!rc) rc = ensure_deep(ctx, limit_depth(limits));
   if (rc) {
     fill_status(st, rc, 0, 0);
     return rc;
@@ -1123,6 +1165,7 @@ int tgpu_decode_stream(tgpu_context* ctx, const tgpu_schema* schema, int protoco
   // successor has no start to check against
   a.check_index = 0;
   a.res = ctx->d_res;
+  a.deep = deep_args(ctx);
   (void)hipGetLastError();  // drop a stale error left by another library
   hipError_t e = launch_result_init(ctx->d_res, 0, s);
   bool fused = false;
@@ -1147,6 +1190,7 @@ int tgpu_decode_stream(tgpu_context* ctx, const tgpu_schema* schema, int protoco
         DecodeArgs b = a;
         b.n = m;
         e = launch_general_decode(b, protocol, s);
+        if (e == hipSuccess) e = launch_deep_decode(b, protocol, s);
       }
       // the index's result stands (same records, same first failure)
       if (e == hipSuccess)
@@ -1192,6 +1236,12 @@ int tgpu_skim_batch(tgpu_context* ctx, int protocol, const void* in, uint64_t in
     return TGPU_ERR_INVALID_ARGUMENT;
   }
   const hipStream_t s = (hipStream_t)stream;
+  int rc = ensure_workspace(ctx, n);
+  if (!rc) rc = ensure_deep(ctx, limit_depth(limits));
+  if (rc) {
+    fill_status(st, rc, 0, 0);
+    return rc;
+  }
   SkimArgs a{};
   a.in = (const uint8_t*)in;
   a.in_len = in_len;
@@ -1205,6 +1255,7 @@ int tgpu_skim_batch(tgpu_context* ctx, int protocol, const void* in, uint64_t in
   a.max_depth = limits ? limits->max_depth : 12000;
   a.height = limits ? limits->height : 0;
   a.res = ctx->d_res;
+  a.deep = deep_args(ctx);
   a.nt_stores = getenv("TGPU_SKIM_NT") ? atoi(getenv("TGPU_SKIM_NT")) : 1;
   (void)hipGetLastError();
   hipError_t e = launch_result_init(ctx->d_res, n, s);
@@ -1234,6 +1285,11 @@ int tgpu_index_stream(tgpu_context* ctx, const tgpu_schema* schema, int protocol
     return TGPU_ERR_INVALID_ARGUMENT;
   }
   const hipStream_t s = (hipStream_t)stream;
+  const int drc = ensure_deep(ctx, limit_depth(limits));
+  if (drc) {
+    fill_status(st, drc, 0, 0);
+    return drc;
+  }
   (void)hipGetLastError();  // drop a stale error left by another library
   hipError_t e = launch_result_init(ctx->d_res, 0, s);
   const int rc = launch_index(ctx, schema, protocol, (const uint8_t*)in, in_len, begin, end,

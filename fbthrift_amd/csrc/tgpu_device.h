@@ -86,6 +86,9 @@ struct Reader {
   int32_t err;
   uint64_t err_off;
   bool has_bool, bool_val;  // Compact boolValue_ latch
+  // skip frames past the private kMaxSkipDepth (nullptr: kErrDeep instead)
+  uint8_t* deep;
+  uint64_t deep_cap;  // frames at `deep`
 
   __device__ __forceinline__ bool ok() const { return err == 0; }
   __device__ __forceinline__ void fail(int32_t code, uint64_t off) {
@@ -142,6 +145,28 @@ struct Reader {
   }
   __device__ __forceinline__ void ascend() { ++height; }
 };
+
+// A reader at `pos` of in[0..end) with the call's limits; height is
+// ProtocolBase::setHeight (0 = max_depth, Protocol.h:59-78) plus the root.
+__device__ __forceinline__ Reader make_reader(const uint8_t* in, uint64_t pos, uint64_t end,
+                                             int32_t string_limit, int32_t container_limit,
+                                             int32_t max_depth, int32_t height) {
+  Reader r;
+  r.p = in;
+  r.pos = pos;
+  r.end = end;
+  r.height = (int64_t)(height ? height : max_depth) + 1;
+  r.string_limit = string_limit;
+  r.container_limit = container_limit;
+  r.max_depth = max_depth;
+  r.err = 0;
+  r.err_off = 0;
+  r.has_bool = false;
+  r.bool_val = false;
+  r.deep = nullptr;
+  r.deep_cap = 0;
+  return r;
+}
 
 template <int P>
 struct Proto;
@@ -381,10 +406,17 @@ struct SkipFrame {
   int32_t depth;  // depth of the values inside this frame
 };
 
+// Frames live in the lane's private array, or all of them in the reader's
+// HBM slab when it has one (deep-pass lanes). Running out of private frames
+// is kErrDeep (the caller defers the record to the deep pass); out of slab
+// frames (past kMaxDeepFrames) TGPU_ERR_UNSUPPORTED.
 template <int P>
 __device__ void skip(Reader& r, uint32_t type, int32_t depth) {
   using Pr = Proto<P>;
-  SkipFrame st[kMaxSkipDepth];
+  SkipFrame priv[kMaxSkipDepth];
+  SkipFrame* const st = r.deep ? (SkipFrame*)r.deep : priv;
+  const uint64_t cap = r.deep ? r.deep_cap : (uint64_t)kMaxSkipDepth;
+  const int32_t full = r.deep ? TGPU_ERR_UNSUPPORTED : kErrDeep;
   int sp = 0;
   uint32_t cur = type;
   int32_t cdepth = depth;
@@ -397,7 +429,7 @@ __device__ void skip(Reader& r, uint32_t type, int32_t depth) {
         if (cur == TGPU_T_STRUCT) {
           r.descend(r.pos);  // readStructBegin
           if (!r.ok()) return;
-          if (sp == kMaxSkipDepth) return r.fail(TGPU_ERR_UNSUPPORTED, r.pos);
+          if ((uint64_t)sp >= cap) return r.fail(full, r.pos);
           st[sp++] = SkipFrame{1, 0, 0, 0, 0, cdepth + 1};
         } else if (cur == TGPU_T_LIST || cur == TGPU_T_SET || cur == TGPU_T_MAP) {
           uint32_t a = 0, b = 0;
@@ -415,7 +447,7 @@ __device__ void skip(Reader& r, uint32_t type, int32_t depth) {
             r.skip_bytes(sum * (uint64_t)(uint32_t)n);
             r.ascend();
           } else {
-            if (sp == kMaxSkipDepth) return r.fail(TGPU_ERR_UNSUPPORTED, r.pos);
+            if ((uint64_t)sp >= cap) return r.fail(full, r.pos);
             st[sp++] = SkipFrame{(uint8_t)(is_map ? 3 : 2), (uint8_t)a, (uint8_t)b, 0, n,
                                  cdepth + 2};
           }
@@ -722,6 +754,46 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, uint8_
     }
     if (r.ok()) rec[fr.obj + f.isset_offset] = 1;
   }
+}
+
+// ---------------------------------------------------------- deep passes ----
+// Lane `lane`'s HBM skip frames (DeepArgs), attached to a reader.
+__device__ __forceinline__ void attach_slab(Reader& r, const DeepArgs& d, uint32_t lane) {
+  if (!d.slabs) return;
+  r.deep = d.slabs + (uint64_t)lane * d.slab_frames * sizeof(SkipFrame);
+  r.deep_cap = d.slab_frames;
+}
+
+// A lane whose reader failed: a value nested past its private skip frames
+// defers item i to the deep pass; any other error is a real one.
+__device__ __forceinline__ void defer_or_fail(const Reader& r, const DeepArgs& d,
+                                              unsigned long long* first_fail, uint64_t i) {
+  if (r.err == kErrDeep) d.list[atomicAdd(d.count, 1ull)] = i;
+  else atomicMin(first_fail, (unsigned long long)i);
+}
+
+// Record i of an indexed stream, zeroed and then read (one readNoXfer into a
+// default-constructed T); the reader comes back with any error latched.
+// lane >= 0: the deep-pass lane whose HBM frames the skip may use.
+template <int P>
+__device__ Reader decode_record(const DecodeArgs& a, uint64_t i, int lane) {
+  uint8_t* rec = a.recs + i * a.rec_size;
+  if ((a.rec_size & 7) == 0) {
+    for (uint32_t b = 0; b < a.rec_size; b += 8) *(uint64_t*)(rec + b) = 0;
+  } else {
+    for (uint32_t b = 0; b < a.rec_size; ++b) rec[b] = 0;
+  }
+  const uint64_t start = a.offs[i];
+  Reader r = make_reader(a.in, start, a.in_len, a.string_limit, a.container_limit, a.max_depth,
+                         a.height);
+  if (lane >= 0) attach_slab(r, a.deep, (uint32_t)lane);
+  if (start > a.in_len || (a.check_index && a.offs[i + 1] < start)) {
+    r.fail(TGPU_ERR_INDEX_MISMATCH, start);
+    return r;
+  }
+  read_record<P>(r, a.sc, rec, a.arena, a.arena_cap);
+  if (r.ok() && a.check_index && r.pos != a.offs[i + 1]) r.fail(TGPU_ERR_INDEX_MISMATCH, r.pos);
+  return r;
 }
 
 // ------------------------------------------------------------------ writer --

@@ -52,7 +52,24 @@ constexpr uint32_t kMaxFixedRecord = 160;
 constexpr int kMaxTemplateItems = 96;
 // Nesting supported by the general device reader/writer.
 constexpr int kMaxSchemaDepth = 8;
-constexpr int kMaxSkipDepth = 32;
+// Skip frames a lane keeps privately. A value nested deeper is not an error:
+// the lane reports kErrDeep and its record (or index chunk) is redone by a
+// deep pass whose lanes keep max_depth frames in HBM (DeepArgs), so the skip
+// follows FLAGS_thrift_protocol_max_depth (Protocol.cpp:21-29) like the
+// reference's recursive skip (BinaryProtocol.cpp:140-143).
+constexpr int kMaxSkipDepth = 16;
+constexpr int32_t kErrDeep = 0x10000;  // internal; never reaches a tgpu_status
+// Frames of one deep-pass lane are capped (the reference's recursion would
+// exhaust a thread stack long before): deeper -> TGPU_ERR_UNSUPPORTED.
+constexpr uint64_t kMaxDeepFrames = 1ull << 22;
+struct DeepArgs {
+  uint64_t* list;               // deferred records (or index chunks)
+  unsigned long long* count;    // entries in list
+  uint8_t* slabs;               // lanes x slab_frames skip frames (dev::SkipFrame)
+  uint64_t slab_frames;
+  uint32_t lanes;
+  uint32_t pad;
+};
 // arena == nullptr with this capacity: list elements are read and validated
 // but not stored (the stream indexer measures records without output).
 constexpr uint64_t kDiscardArena = ~0ull;
@@ -165,7 +182,8 @@ struct DevResult {
   unsigned long long n_records;
   unsigned long long n_irregular;      // program path: records sent to the general decoder
   unsigned long long first_start;      // stream index: first record start found
-  unsigned long long pad2;
+  unsigned long long n_deep;           // records deferred to the deep pass
+  unsigned long long n_deep_chunks;    // index chunks deferred to the deep emit pass
 };
 
 struct DevSchema {
@@ -191,6 +209,7 @@ struct DecodeArgs {
   DevResult* res;
   uint64_t fixed_len;  // program decode of a fixed-layout stream: record i at i * fixed_len
                        // (offs unused; a non-canonical record latches first_irregular)
+  DeepArgs deep;
 };
 
 // Schemaless skim of an indexed stream (k_skim.hip, tgpu_skim_batch).
@@ -205,6 +224,7 @@ struct SkimArgs {
   int32_t string_limit, container_limit, max_depth, height;
   DevResult* res;
   int nt_stores;  // entries stored non-temporally (never re-read here)
+  DeepArgs deep;
 };
 
 struct EncodeArgs {
@@ -269,6 +289,8 @@ struct IndexArgs {
   unsigned long long* nirr;
   int32_t decode_tail;  // a stream shorter than n_decode: its first missing record fails
   int32_t pad_;
+  DeepArgs deep;        // records: fused decode deferrals; chunks: deep_chunks
+  uint64_t* deep_chunks;  // emit chains stopped by kErrDeep (count: res->n_deep_chunks)
 };
 
 #ifndef __HIPCC_RTC__
@@ -321,6 +343,8 @@ hipError_t launch_general_decode_list(const DecodeArgs& a, int protocol,
                                       const unsigned long long* n_list,
                                       hipStream_t stream);
 hipError_t launch_skim(const SkimArgs& a, int protocol, hipStream_t stream);
+// The records deferred by kErrDeep (a.deep), redone with HBM skip frames.
+hipError_t launch_deep_decode(const DecodeArgs& a, int protocol, hipStream_t stream);
 hipError_t launch_serial_decode(const DecodeArgs& a, int protocol,
                                 bool from_irregular, uint64_t fixed_len,
                                 hipStream_t stream);

@@ -26,6 +26,70 @@ def byte_ranges(total_len, world):
     return [(total_len * k // world, total_len * (k + 1) // world) for k in range(world)]
 
 
+def need_range(ranges, overlap, file_len, rank):
+    """File bytes rank `rank` must hold: its range plus `overlap` bytes of the
+    next one (the record straddling its end; overlap >= the longest record)."""
+    b, e = ranges[rank]
+    return b, min(e + overlap, file_len)
+
+
+def redistribution(enc_ranges, ranges, overlap, file_len, rank):
+    """The byte moves that turn "rank k holds the file bytes it encoded"
+    (enc_ranges[k], contiguous and in file order) into "rank k holds
+    need_range(k)". Returns (send, recv): send[d] / recv[s] = (lo, hi) file
+    offsets this rank sends to rank d / receives from rank s (lo == hi:
+    nothing). The received pieces are ascending and tile need_range(rank)."""
+    world = len(ranges)
+    mine = enc_ranges[rank]
+    lo, hi = need_range(ranges, overlap, file_len, rank)
+    send, recv = [], []
+    for d in range(world):
+        nlo, nhi = need_range(ranges, overlap, file_len, d)
+        a0, a1 = max(mine[0], nlo), min(mine[1], nhi)
+        send.append((a0, max(a0, a1)))
+        s0, s1 = enc_ranges[d]
+        r0, r1 = max(s0, lo), min(s1, hi)
+        recv.append((r0, max(r0, r1)))
+    return send, recv
+
+
+def redistribute(local, enc_ranges, ranges, overlap, file_len, rank, out, all_to_all_single):
+    """Moves the file bytes (one all-to-all; RCCL over xGMI on the GPU path,
+    gloo in the CPU tests): `local` (uint8 tensor) holds this rank's encoded
+    bytes enc_ranges[rank]; `out` receives need_range(rank). Returns the
+    filled prefix of `out`."""
+    import torch
+
+    send, recv = redistribution(enc_ranges, ranges, overlap, file_len, rank)
+    base = enc_ranges[rank][0]
+    pieces = [local[a - base: b - base] for a, b in send if b > a]
+    inp = torch.cat(pieces) if pieces else local[:0]
+    lo, hi = need_range(ranges, overlap, file_len, rank)
+    all_to_all_single(out[: hi - lo], inp, [b - a for a, b in recv], [b - a for a, b in send])
+    return out[: hi - lo]
+
+
+def tensor_gather(all_gather, device, world):
+    """all_gather(list_of_ints) over torch.distributed for
+    exchange_boundaries: one int64 tensor per rank. Positions may be NONE
+    (2**64 - 1, no record start in a range), which int64 cannot hold: it
+    travels as -1 and comes back as NONE (no real position is negative)."""
+    import torch
+
+    def gather(vals):
+        enc = [-1 if v == NONE else int(v) for v in vals]
+        if world == 1:
+            rows = [enc]
+        else:
+            t = torch.tensor(enc, dtype=torch.int64, device=device)
+            out = [torch.empty_like(t) for _ in range(world)]
+            all_gather(out, t)
+            rows = [o.tolist() for o in out]
+        return [[NONE if v == -1 else int(v) for v in r] for r in rows]
+
+    return gather
+
+
 def resolve(begins, ends, firsts, lasts):
     """Given every rank's range [begins[k], ends[k]) and its index result
     (first start, last end; NONE when no record start was found), return the

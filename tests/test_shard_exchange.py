@@ -125,3 +125,126 @@ def test_exchange_gloo(world, lie):
     assert sum(counts) == len(starts) - 1
     if lie:
         assert max(r[5] for r in res) >= 2
+
+
+# ---- the whole config-5 composition on CPU ranks ---------------------------
+# What bench.py's FileShards runs on the GPUs, with the GPU calls replaced by
+# the oracle: every rank encodes its share of a Compact file of config-3
+# records (plus a few records larger than a whole range), the byte ranges are
+# moved with all_to_all_single (shard.redistribute), each rank indexes its
+# range speculatively with the oracle's sequential record walk and the ranks
+# confirm their first record start (shard.exchange_boundaries over
+# shard.tensor_gather, NONE-safe). The per-rank record sets must be exactly a
+# whole-file sequential read's.
+GIANT = {37: 70_000, 1200: 150_000}
+OVERLAP = 1 << 18
+
+
+def _mixed_record(i):
+    import datagen
+    from wire import C, W
+
+    v = datagen.gen_mixed(i)
+    w = W(C)
+    for k in range(4):
+        w.field(8, k + 1).i32(v[k])
+    # giant payload bytes 0x0F: a candidate start inside it fails at once
+    # (Compact ctype 15, "don't know what type")
+    w.field(11, 5).string(v[4] if i not in GIANT else b"\x0f" * GIANT[i])
+    return w.field(11, 6).string(v[5]).stop().bytes()
+
+
+def _share(rank, world, n):
+    return range(n * rank // world, n * (rank + 1) // world)
+
+
+def _composition_worker(rank, world, port, n, q):
+    import hashlib
+
+    import torch
+    import torch.distributed as dist
+
+    from oracle import oracle
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        enc = b"".join(_mixed_record(i) for i in _share(rank, world, n))
+        gather = shard.tensor_gather(dist.all_gather, torch.device("cpu"), world)
+        sizes = [r[0] for r in gather([len(enc)])]
+        enc_ranges, off = [], 0
+        for s in sizes:
+            enc_ranges.append((off, off + s))
+            off += s
+        file_len = off
+        ranges = shard.byte_ranges(file_len, world)
+        lo, hi = shard.need_range(ranges, OVERLAP, file_len, rank)
+        out = torch.zeros(hi - lo + 16, dtype=torch.uint8)
+        local = shard.redistribute(torch.frombuffer(bytearray(enc), dtype=torch.uint8),
+                                   enc_ranges, ranges, OVERLAP, file_len, rank, out,
+                                   dist.all_to_all_single)
+        buf = local.numpy().copy()
+        b, e = ranges[rank]
+
+        def walk(p):
+            # records back to back from p while they start before e
+            count = 0
+            while p < e:
+                length = oracle.record_length(2, buf, p - lo)
+                if length <= 0:
+                    return None
+                p += length
+                count += 1
+            return count, p
+
+        def index_fn(begin, speculative):
+            cands = range(begin, e) if speculative else [begin]
+            for c in cands:
+                r = walk(c)
+                if r is not None and r[0] > 0:
+                    return r[0], c, r[1]
+            return 0, shard.NONE, shard.NONE
+
+        res = shard.exchange_boundaries(index_fn, rank, world, b, e, gather)
+        q.put((rank, hashlib.sha256(buf.tobytes()).hexdigest(), (lo, hi)) + tuple(res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_file_split_composition_gloo(world):
+    import hashlib
+
+    import torch.multiprocessing as mp
+
+    n = 2400
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_composition_worker, args=(r, world, port, n, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    recs = [_mixed_record(i) for i in range(n)]
+    data = b"".join(recs)
+    starts = np.concatenate([[0], np.cumsum([len(r) for r in recs])]).astype(np.int64)
+    ranges = shard.byte_ranges(len(data), world)
+    empty_ranges = 0
+    for (rank, digest, (lo, hi), cnt, first, last, base, rounds), (b, e) in zip(res, ranges):
+        assert digest == hashlib.sha256(data[lo:hi]).hexdigest()  # bytes moved right
+        inside = np.nonzero((starts[:-1] >= b) & (starts[:-1] < e))[0]
+        assert cnt == inside.size
+        assert base == int(np.count_nonzero(starts[:-1] < b))
+        if inside.size:
+            assert first == starts[inside[0]] and last == starts[inside[-1] + 1]
+        else:
+            empty_ranges += 1
+            assert first == shard.NONE
+    assert sum(r[3] for r in res) == n
+    if world == 4:
+        assert empty_ranges >= 1  # a range inside one giant record took the NONE path
