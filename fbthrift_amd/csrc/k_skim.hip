@@ -52,6 +52,11 @@ __device__ Reader skim_one(const SkimArgs& a, uint64_t i, bool store, const uint
     // containers take the full skip
     else if (r.max_depth <= 0 || !Pr::skip_leaf(r, wt)) skip<P>(r, wt, 0);
     if (!r.ok()) break;
+    // an entry's length is 32 bits: a value of 4 GiB or more is reported
+    if (r.pos - off > 0xffffffffull) {
+      r.fail(TGPU_ERR_UNSUPPORTED, off);
+      break;
+    }
     if (store && count < a.max_fields) {
       // one 16-byte entry {id, ttype, flags | length | offset}
       typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));

@@ -227,6 +227,11 @@ __device__ __forceinline__ void for_elems(const uint8_t* __restrict__ e, uint32_
 
 // Bytes T::write emits for the record at `rec`; ok = false where the writer
 // would throw or abort (the finish kernel re-derives the exact code).
+// Size of a record whose string or list length fails the writer's size check
+// (> INT32_MAX): larger than any output buffer, so the write pass never
+// emits it (emission would copy `length` bytes) and reports the record.
+constexpr uint64_t kNeverFits = 1ull << 44;
+
 template <class PP>
 __device__ __forceinline__ uint64_t program_size(const PP& P, const uint8_t* rec,
                                                  const uint8_t* __restrict__ lbase, bool& ok) {
@@ -250,7 +255,11 @@ __device__ __forceinline__ uint64_t program_size(const PP& P, const uint8_t* rec
         break;
       case VOP_STRING: {
         const uint32_t len = ((const tgpu_span*)(rec + op.member))->length;
-        if (len > 0x7fffffffu) ok = false;
+        if (len > 0x7fffffffu) {  // checkBinarySize: never emitted (see kNeverFits)
+          ok = false;
+          n += kNeverFits;
+          break;
+        }
         n += (compact ? varint_len(len) : 4) + (uint64_t)len;
         break;
       }
@@ -259,6 +268,7 @@ __device__ __forceinline__ uint64_t program_size(const PP& P, const uint8_t* rec
         const uint32_t len = sp.length;
         if (len > 0x7fffffffu) {
           ok = false;
+          n += kNeverFits;
           break;
         }
         n += compact ? (len <= 14 ? 1 : 1 + varint_len(len)) : 5;

@@ -312,9 +312,12 @@ class BatchSerializer:
         import torch
 
         end = wire.numel() if end is None else end
-        if max_records is None:
-            max_records = max(end - begin, 0)
         dev = wire.device
+        if max_records is None:
+            # a record can be one byte (STOP), so end - begin bounds the count;
+            # sizing records for that is up to 8 x S per byte: count first
+            max_records = self._count_records(gschema, wire, begin, end, speculative, limits,
+                                              stream)
         if offsets is None:
             offsets = torch.empty(max_records + 1, dtype=torch.int64, device=dev)
         if records is None:
@@ -405,6 +408,19 @@ class BatchSerializer:
         return out, st, size.value
 
     # -- stream index -------------------------------------------------------
+    def _count_records(self, gschema, wire, begin, end, speculative, limits, stream):
+        """Records beginning in [begin, end): an index into a small buffer
+        (an estimate of one record per 16 bytes) that reports the exact count
+        when it overflows (TGPU_ERR_OUTPUT_OVERFLOW), so callers that did
+        not give max_records allocate for the records found, not for one
+        record per byte."""
+        span = max(end - begin, 0)
+        guess = min(span, max(1024, span // 16))
+        _, n, _, _, st = self.index_stream(gschema, wire, begin, end, speculative,
+                                           max_records=guess, limits=limits, stream=stream,
+                                           check=False)
+        return max(n, guess)
+
     def index_stream(self, gschema, wire, begin=0, end=None, speculative=False,
                      max_records=None, offsets=None, limits=None, stream=None, check=True):
         """Record starts of an unindexed stream (tgpu_index_stream): the records
@@ -415,7 +431,8 @@ class BatchSerializer:
 
         end = wire.numel() if end is None else end
         if max_records is None:
-            max_records = max(end - begin, 0)
+            max_records = self._count_records(gschema, wire, begin, end, speculative, limits,
+                                              stream)
         if offsets is None:
             offsets = torch.empty(max_records + 1, dtype=torch.int64, device=wire.device)
         lim = None

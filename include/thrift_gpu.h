@@ -467,7 +467,8 @@ int tgpu_decode_stream(tgpu_context* ctx, const tgpu_schema* schema, int protoco
  * value in the field header, so its encoded value is empty and the value is
  * in `flags`.
  *   offset  absolute byte position of the value in `in` (after the header)
- *   length  bytes of the value (what skip consumed)
+ *   length  bytes of the value (what skip consumed); a value of 4 GiB or
+ *           more does not fit and fails the record with TGPU_ERR_UNSUPPORTED
  *   flags   TGPU_SKIM_BOOL | (value ? TGPU_SKIM_TRUE : 0) for T_BOOL
  */
 typedef struct tgpu_skim_field {

@@ -1196,6 +1196,8 @@ int skim_impl(const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint6
         uint8_t flags = 0;
         if (wt == TGPU_T_BOOL) flags = TGPU_SKIM_BOOL | (r.readBool() ? TGPU_SKIM_TRUE : 0);
         else r.skip(wt, 0);
+        // an entry's length is 32 bits: a longer value is not representable
+        if (r.c.pos - off > 0xffffffffull) fail(TGPU_ERR_UNSUPPORTED, off);
         if (count < max_fields) {
           tgpu_skim_field& f = fields[(uint64_t)count * n + i];
           f.id = id;

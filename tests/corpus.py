@@ -281,7 +281,22 @@ def union_cases():
         r3 = W(p).field(I64, 1).i64(1).field(I32, 2).i32(2).stop().bytes()
         out.append(("%s_root_union" % pn, p, ROOT_UNION, r1 + r2 + r1, 3, None, OK))
         out.append(("%s_root_union_two" % pn, p, ROOT_UNION, r1 + r3, 2, None, UNION_MISSING_STOP))
+    # thrift/test/tablebased/SerializerTest.cpp:399-418 DuplicateUnionData, the
+    # reference's one checked-in wire vector: TestStructWithUnion
+    # {1: TestUnion union_field} with TestUnion {1: string string_field,
+    # 2: float float_field} (thrift_tablebased.thrift:105-112). The union field
+    # twice, the second holding a float whose value is missing; sizeof(data)
+    # keeps the literal's NUL, so one byte of the float is present.
+    # EXPECT_THROW(..., std::out_of_range).
+    dup = (b"\x0c" b"\x00\x01" b"\x0b" b"\x00\x01" b"\x00\x00\x00\x00" b"\x00"
+           b"\x0c" b"\x00\x01" b"\x13" b"\x00\x02" b"\x00")
+    out.append(("binary_duplicate_union_data", B, DUP_UNION_SCHEMA, dup, 1, None, UNDERFLOW))
     return out
+
+
+FLOAT = 19
+DUP_UNION_SCHEMA = [[[1, STRUCT, 0, 0, 1]],
+                    {"union": True, "fields": [[1, STR, 0, 0, -1], [2, FLOAT, 0, 0, -1]]}]
 
 
 LSTR = [[[1, LIST, STR, 0, -1], [2, MAP, STR, 0, -1, I32], [3, I32, 0, 0, -1]]]
