@@ -63,33 +63,121 @@ def gen_flat8_device(n, first, dev):
     return out.view(torch.uint8).reshape(-1)
 
 
-def cpu_baseline(seconds=12.0):
-    """The oracle's codegen-equivalent Binary encode+decode (the reference's
-    generated T::write / T::readNoXfer restated, -O3 -march=native) on this
-    host's cores, over a bounded sample, same metric."""
+def cpu_threads():
+    """Host cores this process can run on: its CPU affinity, capped by the
+    cgroup's CPU quota (a GPU box shares a larger machine: nproc shows all of
+    its CPUs, the quota is this job's share). Returns (threads, detail)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = float(q) / float(period)
+    except (OSError, ValueError):
+        pass
+    threads = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    return threads, {"nproc": os.cpu_count(), "affinity": aff, "cgroup_cpu_quota": quota}
+
+
+def _timed(fn, seconds):
+    """Runs fn() until `seconds` have passed (at least twice); returns the
+    mean seconds per call and the call count."""
+    fn()
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        fn()
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            return el / reps, reps
+
+
+def cpu_baseline(wl, seconds=8.0):
+    """The oracle's codegen-equivalent encode+decode of the workload's schema
+    (the reference's generated T::write / T::readNoXfer restated for it,
+    -O3 -march=native, oracle/thrift_oracle.cpp) on this host's cores over a
+    bounded sample of the same records, same metric (2 x wire bytes / (encode
+    + decode time)); also on one core. Output formats equal the device's
+    (string spans = SHARE views, list elements into an arena). Config 5
+    decodes the way the reference reads a file: one cursor, record after
+    record (Serializer.h:97-100)."""
     import numpy as np
 
     from oracle import oracle
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    n = 1 << 22
-    recs = np.zeros(n * 72, np.uint8)
-    oracle.lib().oracle_gen_flat8(SEED, 0, n, recs.ctypes.data)
-    wire = np.zeros(n * 89, np.uint8)
-    back = np.zeros(n * 72, np.uint8)
     L = oracle.lib()
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        L.oracle_flat8_binary_encode(recs.ctypes.data, n, wire.ctypes.data, threads)
-        rc = L.oracle_flat8_binary_decode(wire.ctypes.data, n, back.ctypes.data, threads)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    assert rc == 0 and np.array_equal(back, recs)
-    gib = 2.0 * n * 89 * reps / el / 2**30
-    return {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": "%d x encode+decode of 4Mi config-2 records (%.1f s wall)" % (reps, el)}
+    threads, detail = cpu_threads()
+    cfg = wl.config_id
+    if cfg == 2:
+        n = 1 << 22
+        recs = np.zeros(n * 72, np.uint8)
+        L.oracle_gen_flat8(SEED, 0, n, recs.ctypes.data)
+        wire = np.zeros(n * 89, np.uint8)
+        back = np.zeros(n * 72, np.uint8)
+
+        def step(t):
+            L.oracle_flat8_binary_encode(recs.ctypes.data, n, wire.ctypes.data, t)
+            assert L.oracle_flat8_binary_decode(wire.ctypes.data, n, back.ctypes.data, t) == 0
+
+        def check():
+            assert np.array_equal(back, recs)
+        wire_bytes = n * 89
+    else:
+        n = min(wl.n, 1 << 22)
+        rs = wl.record_bytes
+        recs = wl.recs[: n * rs].cpu().numpy()
+        side = wl.side[: n * 64].cpu().numpy()
+        sizes = np.zeros(n, np.uint64)
+        offs = np.zeros(n + 1, np.uint64)
+        back = np.zeros(n * rs, np.uint8)
+        size_fn = L.oracle_mixed_compact_size if wl.schema == "mixed" else \
+            L.oracle_nested_binary_size
+        size_fn(recs.ctypes.data, n, sizes.ctypes.data, threads)
+        np.cumsum(sizes, out=offs[1:])
+        wire_bytes = int(offs[-1])
+        wire = np.zeros(wire_bytes + 16, np.uint8)
+        arena = np.zeros(wire_bytes + 16, np.uint8)
+        starts = np.zeros(n + 1, np.uint64)
+
+        def step(t):
+            # serializedSize pass + scan + write (one contiguous stream), then
+            # the decode
+            size_fn(recs.ctypes.data, n, sizes.ctypes.data, t)
+            np.cumsum(sizes, out=offs[1:])
+            if wl.schema == "mixed":
+                L.oracle_mixed_compact_encode(recs.ctypes.data, n, side.ctypes.data,
+                                              wire.ctypes.data, offs.ctypes.data, t)
+                if cfg == 5:
+                    got = L.oracle_mixed_compact_read_file(wire.ctypes.data, wire_bytes, n,
+                                                           back.ctypes.data, starts.ctypes.data)
+                    assert got == n
+                else:
+                    assert L.oracle_mixed_compact_decode(wire.ctypes.data, offs.ctypes.data, n,
+                                                         back.ctypes.data, t) == 0
+            else:
+                L.oracle_nested_binary_encode(recs.ctypes.data, n, side.ctypes.data,
+                                              wire.ctypes.data, offs.ctypes.data, t)
+                assert L.oracle_nested_binary_decode(wire.ctypes.data, offs.ctypes.data, n,
+                                                     back.ctypes.data, arena.ctypes.data, t) == 0
+
+        def check():
+            a, b = recs.reshape(n, rs), back.reshape(n, rs)
+            for lo, hi in wl.fixed_ranges:
+                assert np.array_equal(a[:, lo:hi], b[:, lo:hi])
+            g = wl.wire[: wire_bytes].cpu().numpy() if cfg != 5 else None
+            if g is not None:
+                assert np.array_equal(wire[:wire_bytes], g)  # same bytes as the GPU's
+    t_all, reps = _timed(lambda: step(threads), seconds)
+    check()
+    t_one, reps1 = _timed(lambda: step(1), seconds / 2)
+    gib = lambda t: round(2.0 * wire_bytes / t / 2**30, 3)
+    return {"value": gib(t_all), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "single_core": {"value": gib(t_one), "unit": "GiB/s", "cores": 1},
+            "host": detail,
+            "ns_per_record_1core": round(t_one / n * 1e9, 2),
+            "sample": "%d x encode+decode of %d config-%d records (%d + %d reps, %.1f s)" % (
+                reps + reps1, n, cfg, reps, reps1, t_all * reps + t_one * reps1)}
 
 
 class Workload:
@@ -111,6 +199,7 @@ class Workload:
 
 class Flat8(Workload):
     """Config 2: Binary, flat {1..8: i64} (72-byte records, 89-byte wire)."""
+    config_id = 2
     name = "config 2: Binary protocol, flat {1..8: i64} records, encode+decode"
     default_records = 1 << 26
     dec_kernel, enc_kernel = "plan_binary_decode_kernel", "plan_binary_encode_kernel"
@@ -249,6 +338,7 @@ class VarLen(Workload):
 
 
 class Mixed(VarLen):
+    config_id = 3
     name = "config 3: Compact protocol, {4 x i32, 2 x string[0..32]} records, indexed encode+decode"
     schema, protocol = "mixed", 2
     default_records = 1 << 26
@@ -259,6 +349,7 @@ class Mixed(VarLen):
 
 
 class Nested(VarLen):
+    config_id = 4
     name = "config 4: Binary protocol, {i64, list<i32>[0..16], inner{3 x double}}, indexed encode+decode"
     schema, protocol = "nested", 0
     default_records = 1 << 25
@@ -281,6 +372,7 @@ class FileShards(Mixed):
     every decoded record equals the generator's record of the same global
     index, and re-encoding the decoded records reproduces the range's bytes.
     """
+    config_id = 5
     name = ("config 5: Compact protocol, {4 x i32, 2 x string[0..32]} file split by bytes "
             "across GPUs, encode + boundary discovery + decode")
     overlap = 1 << 20
@@ -422,7 +514,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=2, choices=sorted(WORKLOADS))
+    ap.add_argument("--config", type=int, default=2, choices=[1] + sorted(WORKLOADS))
     ap.add_argument("--records", type=int, default=0, help="records per GPU (default: config's)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-copy-ceiling", action="store_true")
@@ -435,6 +527,9 @@ def main():
                     help="also time device transcoding of the workload's stream into the "
                          "other protocol (tgpu_transcode_batch)")
     args = ap.parse_args()
+    if args.config == 1:
+        print(json.dumps(config1()), flush=True)
+        return
 
     import torch
     import torch.distributed as dist
@@ -513,12 +608,71 @@ def main():
         line["transcode"] = transcode(wl, dev)
     if args.skim and rank == 0:
         line["skim"] = skim(wl, dev)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == 2:
-        line["cpu_baseline"] = cpu_baseline()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(wl)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def config1(n=1000, seconds=3.0):
+    """BASELINE config 1 ("thrift/perf"): Binary round trip of 1k flat
+    {8 x i64} records on the CPU — the shape of the reference's protocol
+    microbenchmarks (ThriftProtocolBenchmarks.cpp:167-219: serialize and
+    deserialize of one struct, ns/op) with the oracle's codegen-equivalent
+    T::write / T::readNoXfer on one core, values of config 2's generator.
+    The same 1k batch also goes through the C-ABI on the GPU (plumbing: a
+    1k-record call is launch-latency bound), checked byte for byte."""
+    import numpy as np
+
+    from oracle import oracle
+
+    L = oracle.lib()
+    recs = np.zeros(n * 72, np.uint8)
+    L.oracle_gen_flat8(SEED, 0, n, recs.ctypes.data)
+    wire = np.zeros(n * 89, np.uint8)
+    back = np.zeros(n * 72, np.uint8)
+    t_enc, reps_e = _timed(lambda: L.oracle_flat8_binary_encode(recs.ctypes.data, n,
+                                                                wire.ctypes.data, 1), seconds)
+    t_dec, reps_d = _timed(lambda: L.oracle_flat8_binary_decode(wire.ctypes.data, n,
+                                                                back.ctypes.data, 1), seconds)
+    assert np.array_equal(back, recs)
+    line = {"metric": "CPU Binary round trip, 1k flat {8 x i64} records (config 1)",
+            "value": round((t_enc + t_dec) / n * 1e9, 2), "unit": "ns/record",
+            "higher_is_better": False, "dtype": "u8", "data": "synthetic (config 2 generator)",
+            "config": {"workload": "config 1: thrift/perf-style CPU round trip, 1000 x flat8",
+                       "records": n, "wire_bytes_per_record": 89},
+            "encode_ns_per_record": round(t_enc / n * 1e9, 2),
+            "decode_ns_per_record": round(t_dec / n * 1e9, 2),
+            "cores": 1, "kind": "port", "reps": reps_e + reps_d}
+    try:
+        import torch
+
+        if torch.cuda.is_available():
+            from fbthrift_amd.schema import Schema
+            from fbthrift_amd.serializer import BinarySerializer as BS, GpuSchema
+            import datagen
+
+            dev = torch.device("cuda", 0)
+            gs = GpuSchema(Schema.from_table(datagen.SCHEMAS["flat8"]))
+            r = torch.from_numpy(recs).to(dev)
+
+            def gpu_round_trip():
+                w, _ = BS.serialize(gs, r, n, offsets=None)
+                out, _, _ = BS.deserialize(gs, w, n)
+                return w, out
+
+            w, out = gpu_round_trip()
+            assert np.array_equal(w.cpu().numpy(), wire) and np.array_equal(out.cpu().numpy(), recs)
+            t_gpu, reps_g = _timed(gpu_round_trip, 1.0)
+            line["gpu_plumbing"] = {"us_per_round_trip_call": round(t_gpu * 1e6, 2),
+                                    "ns_per_record": round(t_gpu / n * 1e9, 2),
+                                    "how": "tgpu_encode_batch + tgpu_decode_batch, blocking, "
+                                           "device-resident 1k batch", "reps": reps_g}
+    except Exception as e:  # a CPU-only host: the CPU line stands alone
+        line["gpu_plumbing"] = {"skipped": str(e)[:200]}
+    return line
 
 
 def copy_ceiling(dev, nbytes=4 << 30):

@@ -64,6 +64,16 @@ def lib():
         L.oracle_mixed_compact_decode.argtypes = [P, P, U64, P, I32]
         L.oracle_mixed_compact_encode.restype = I32
         L.oracle_mixed_compact_encode.argtypes = [P, U64, P, P, P, I32]
+        L.oracle_mixed_compact_size.restype = I32
+        L.oracle_mixed_compact_size.argtypes = [P, U64, P, I32]
+        L.oracle_mixed_compact_read_file.restype = U64
+        L.oracle_mixed_compact_read_file.argtypes = [P, U64, U64, P, P]
+        L.oracle_nested_binary_size.restype = I32
+        L.oracle_nested_binary_size.argtypes = [P, U64, P, I32]
+        L.oracle_nested_binary_encode.restype = I32
+        L.oracle_nested_binary_encode.argtypes = [P, U64, P, P, P, I32]
+        L.oracle_nested_binary_decode.restype = I32
+        L.oracle_nested_binary_decode.argtypes = [P, P, U64, P, P, I32]
         L.oracle_splitmix64_at.restype = U64
         L.oracle_splitmix64_at.argtypes = [U64, U64]
         L.oracle_gen_flat8.argtypes = [U64, U64, U64, P]

@@ -1391,6 +1391,187 @@ int oracle_mixed_compact_encode(const void* records, uint64_t n,
   return TGPU_OK;
 }
 
+// serializedSize of the codegen-equivalent mixed record (exact, the size
+// pass a contiguous multi-threaded encode needs): sizes[i], then the
+// exclusive prefix is the caller's (out_offsets = sizes scanned).
+int oracle_mixed_compact_size(const void* records, uint64_t n, uint64_t* sizes,
+                              int n_threads) {
+  const uint8_t* rp = (const uint8_t*)records;
+  parallel_for(n, n_threads, [&](uint64_t b, uint64_t e) {
+    for (uint64_t i = b; i < e; ++i) {
+      const uint8_t* r = rp + i * 56;
+      Sink s{nullptr, 0, 0};
+      for (int k = 0; k < 4; ++k) {
+        s.put(0x15);
+        s.varint(i32ToZigzag(ld<int32_t>(r + 4 * k)));
+      }
+      for (int k = 0; k < 2; ++k) {
+        const tgpu_span sp = ld<tgpu_span>(r + 16 + 16 * k);
+        s.put(0x18);
+        s.varint(sp.length);
+        s.pos += sp.length;
+      }
+      s.put(0);
+      sizes[i] = s.pos;
+    }
+  });
+  return TGPU_OK;
+}
+
+// ---- codegen-equivalent nested {1: i64, 2: list<i32>, 3: Inner{1..3: double}},
+// Binary (BASELINE config 4) -------------------------------------------------
+// Device layout: i64 @0; span @8; Inner @24 (f64 @24,32,40, isset @48..50);
+// isset @56..58; size 64. The generated write (serialize_struct.whisker:40-67)
+// / readNoXfer fast path (advanceToNextField, BinaryProtocol-inl.h:586-621;
+// readListBegin + readArithmeticVector, BinaryProtocol.cpp:49-72; nested
+// struct via beforeSubobject/afterSubobject) restated for this one schema.
+// List elements decode to an arena at their wire position (the device's
+// layout: scale 1 Binary), natively little-endian.
+namespace {
+inline void nested_write(Sink& s, const uint8_t* r, const uint8_t* lb) {
+  s.put(TGPU_T_I64); s.putBE(1, 2); s.putBE(ld<uint64_t>(r), 8);
+  const tgpu_span sp = ld<tgpu_span>(r + 8);
+  s.put(TGPU_T_LIST); s.putBE(2, 2); s.put(TGPU_T_I32); s.putBE(sp.length, 4);
+  if (s.out) {
+    if (s.pos + 4ull * sp.length > s.cap) fail(TGPU_ERR_OUTPUT_OVERFLOW, s.pos);
+    const uint8_t* e = lb + sp.offset;
+    uint8_t* o = s.out + s.pos;
+    for (uint32_t k = 0; k < sp.length; ++k) {
+      const uint32_t v = __builtin_bswap32(ld<uint32_t>(e + 4 * k));
+      std::memcpy(o + 4 * k, &v, 4);
+    }
+  }
+  s.pos += 4ull * sp.length;
+  s.put(TGPU_T_STRUCT); s.putBE(3, 2);
+  for (int k = 0; k < 3; ++k) {
+    s.put(TGPU_T_DOUBLE); s.putBE((uint64_t)(k + 1), 2); s.putBE(ld<uint64_t>(r + 24 + 8 * k), 8);
+  }
+  s.put(0);
+  s.put(0);
+}
+}  // namespace
+
+int oracle_nested_binary_size(const void* records, uint64_t n, uint64_t* sizes, int n_threads) {
+  const uint8_t* rp = (const uint8_t*)records;
+  parallel_for(n, n_threads, [&](uint64_t b, uint64_t e) {
+    for (uint64_t i = b; i < e; ++i)
+      sizes[i] = 57 + 4ull * ld<tgpu_span>(rp + i * 64 + 8).length;
+  });
+  return TGPU_OK;
+}
+
+int oracle_nested_binary_encode(const void* records, uint64_t n, const void* list_base,
+                                void* out, const uint64_t* offsets, int n_threads) {
+  const uint8_t* rp = (const uint8_t*)records;
+  parallel_for(n, n_threads, [&](uint64_t b, uint64_t e) {
+    for (uint64_t i = b; i < e; ++i) {
+      Sink s{(uint8_t*)out, offsets[i], offsets[n]};
+      nested_write(s, rp + i * 64, (const uint8_t*)list_base);
+    }
+  });
+  return TGPU_OK;
+}
+
+int oracle_nested_binary_decode(const void* in, const uint64_t* offsets, uint64_t n,
+                                void* records, void* arena, int n_threads) {
+  const uint8_t* p = (const uint8_t*)in;
+  uint8_t* out = (uint8_t*)records;
+  uint8_t* ar = (uint8_t*)arena;
+  int rc = TGPU_OK;
+  auto hdr = [](const uint8_t* q, uint8_t t, int id) {
+    return q[0] == t && q[1] == 0 && q[2] == (uint8_t)id;
+  };
+  parallel_for(n, n_threads, [&](uint64_t b, uint64_t e) {
+    for (uint64_t i = b; i < e; ++i) {
+      uint8_t* o = out + i * 64;
+      std::memset(o, 0, 64);
+      uint64_t pos = offsets[i];
+      const uint64_t end = offsets[n];
+      // the canonical form only (a miss is the generated _loop path: the
+      // caller uses oracle_decode_batch for irregular streams)
+      if (end - pos < 57 || !hdr(p + pos, TGPU_T_I64, 1)) { rc = TGPU_ERR_UNSUPPORTED; continue; }
+      const uint64_t v = load_be64(p + pos + 3);
+      std::memcpy(o, &v, 8);
+      o[56] = 1;
+      pos += 11;
+      if (!hdr(p + pos, TGPU_T_LIST, 2) || p[pos + 3] != TGPU_T_I32) { rc = TGPU_ERR_UNSUPPORTED; continue; }
+      uint32_t cnt;
+      std::memcpy(&cnt, p + pos + 4, 4);
+      cnt = __builtin_bswap32(cnt);
+      pos += 8;
+      if ((int32_t)cnt < 0 || end - pos < 4ull * cnt + 37) { rc = TGPU_ERR_UNSUPPORTED; continue; }
+      for (uint32_t k = 0; k < cnt; ++k) {
+        uint32_t x;
+        std::memcpy(&x, p + pos + 4 * k, 4);
+        x = __builtin_bswap32(x);
+        std::memcpy(ar + pos + 4 * k, &x, 4);
+      }
+      const tgpu_span sp{cnt ? pos : 0, cnt, 0};
+      std::memcpy(o + 8, &sp, 16);
+      o[57] = 1;
+      pos += 4ull * cnt;
+      if (!hdr(p + pos, TGPU_T_STRUCT, 3)) { rc = TGPU_ERR_UNSUPPORTED; continue; }
+      pos += 3;
+      bool ok = true;
+      for (int k = 0; k < 3 && ok; ++k) {
+        ok = hdr(p + pos, TGPU_T_DOUBLE, k + 1);
+        const uint64_t d = load_be64(p + pos + 3);
+        std::memcpy(o + 24 + 8 * k, &d, 8);
+        o[48 + k] = 1;
+        pos += 11;
+      }
+      if (!ok || p[pos] != 0 || p[pos + 1] != 0) { rc = TGPU_ERR_UNSUPPORTED; continue; }
+      o[58] = 1;
+    }
+  });
+  return rc;
+}
+
+// A file of records read the reference's way: one cursor, record after
+// record (while (!cursor.isAtEnd()) deserialize<T>(cursor), Serializer.h:97-100),
+// through the codegen-equivalent mixed reader. Writes the record starts
+// (n + 1) and returns the number of records (the stream must hold exactly
+// canonical records; 0 otherwise).
+uint64_t oracle_mixed_compact_read_file(const void* in, uint64_t in_len, uint64_t max_records,
+                                        void* records, uint64_t* offsets) {
+  const uint8_t* p = (const uint8_t*)in;
+  uint8_t* out = (uint8_t*)records;
+  uint64_t pos = 0, i = 0;
+  while (pos < in_len && i < max_records) {
+    uint8_t* o = out + i * 56;
+    std::memset(o, 0, 56);
+    CompactReader r;
+    r.c = Cursor{p, pos, in_len};
+    r.height.h = 12001;
+    offsets[i] = pos;
+    try {
+      for (int k = 0; k < 4; ++k) {
+        if (!(r.c.avail() && r.c.p[r.c.pos] == 0x15)) return 0;
+        r.c.pos++;
+        const int32_t v = zigzagToI32((uint32_t)readVarint<32>(r.c));
+        std::memcpy(o + 4 * k, &v, 4);
+        o[48 + k] = 1;
+      }
+      for (int k = 0; k < 2; ++k) {
+        if (!(r.c.avail() && r.c.p[r.c.pos] == 0x18)) return 0;
+        r.c.pos++;
+        tgpu_span sp{0, 0, 0};
+        r.readString(sp.offset, sp.length);
+        std::memcpy(o + 16 + 16 * k, &sp, 16);
+        o[52 + k] = 1;
+      }
+      if (!(r.c.avail() && r.c.p[r.c.pos] == 0)) return 0;
+      r.c.pos++;
+    } catch (const OErr&) {
+      return 0;
+    }
+    pos = r.c.pos;
+    ++i;
+  }
+  offsets[i] = pos;
+  return i;
+}
+
 // ---- generators ------------------------------------------------------------
 // Counter-based splitmix64 (Steele/Lea/Flood; the survey's PRNG, seed 0x1729 =
 // VarintUtilsTestUtil.h:59): z = seed + (index+1)*golden, then the finalizer.

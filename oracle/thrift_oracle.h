@@ -81,6 +81,16 @@ int oracle_mixed_compact_decode(const void* in, const uint64_t* offsets,
 int oracle_mixed_compact_encode(const void* records, uint64_t n_records,
                                 const void* string_base, void* out,
                                 const uint64_t* offsets, int n_threads);
+int oracle_mixed_compact_size(const void* records, uint64_t n_records, uint64_t* sizes,
+                              int n_threads);
+uint64_t oracle_mixed_compact_read_file(const void* in, uint64_t in_len, uint64_t max_records,
+                                        void* records, uint64_t* offsets);
+int oracle_nested_binary_size(const void* records, uint64_t n_records, uint64_t* sizes,
+                              int n_threads);
+int oracle_nested_binary_encode(const void* records, uint64_t n_records, const void* list_base,
+                                void* out, const uint64_t* offsets, int n_threads);
+int oracle_nested_binary_decode(const void* in, const uint64_t* offsets, uint64_t n_records,
+                                void* records, void* arena, int n_threads);
 
 /* ---- deterministic generators (shared spec with tests/golden) -------- */
 uint64_t oracle_splitmix64_at(uint64_t seed, uint64_t index);

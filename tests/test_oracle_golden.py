@@ -72,3 +72,48 @@ def test_varint_vectors():
         assert oracle.write_varint(v) == b
         rc, got, used = oracle.read_varint(b, bits)
         assert rc == 0 and got == v and used == len(b)
+
+
+def test_codegen_equivalent_paths_match_golden():
+    """The codegen-equivalent CPU paths timed as per-config baselines
+    (bench.py cpu_baseline) reproduce the golden streams and records: mixed
+    Compact (config 3/5: size, encode, indexed decode, sequential file read)
+    and nested Binary (config 4: size, encode, decode)."""
+    L = oracle.lib()
+    for name, size_fn, enc, dec in (
+            ("mixed_compact", L.oracle_mixed_compact_size, None, None),
+            ("nested_binary", L.oracle_nested_binary_size, None, None)):
+        c = helpers.Case(name)
+        rec, sarena, larena = helpers.pack(c.schema, c.values, c.n)
+        sizes = np.zeros(c.n, np.uint64)
+        size_fn(rec.ctypes.data, c.n, sizes.ctypes.data, 4)
+        offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint64)
+        assert np.array_equal(offs, c.offsets), name
+        out = np.zeros(len(c.wire), np.uint8)
+        back = np.zeros(c.n * c.schema.record_size, np.uint8)
+        if name == "mixed_compact":
+            L.oracle_mixed_compact_encode(rec.ctypes.data, c.n, sarena.ctypes.data,
+                                          out.ctypes.data, offs.ctypes.data, 4)
+            assert out.tobytes() == c.wire
+            w = np.frombuffer(c.wire, np.uint8)
+            assert L.oracle_mixed_compact_decode(w.ctypes.data, offs.ctypes.data, c.n,
+                                                 back.ctypes.data, 4) == 0
+            got = np.zeros(c.n + 1, np.uint64)
+            back2 = np.zeros_like(back)
+            assert L.oracle_mixed_compact_read_file(w.ctypes.data, w.size, c.n, back2.ctypes.data,
+                                                    got.ctypes.data) == c.n
+            assert np.array_equal(got, c.offsets) and np.array_equal(back2, back)
+            arena = oarena = None
+        else:
+            L.oracle_nested_binary_encode(rec.ctypes.data, c.n, larena.ctypes.data,
+                                          out.ctypes.data, offs.ctypes.data, 4)
+            assert out.tobytes() == c.wire
+            w = np.frombuffer(c.wire, np.uint8)
+            arena = np.zeros(len(c.wire), np.uint8)
+            assert L.oracle_nested_binary_decode(w.ctypes.data, offs.ctypes.data, c.n,
+                                                 back.ctypes.data, arena.ctypes.data, 4) == 0
+        ost, orec, oarena, _, _ = oracle.decode(c.schema, c.protocol, c.wire, c.n,
+                                                offsets=c.offsets)
+        assert np.array_equal(back, orec[: back.size]), name
+        if arena is not None:
+            helpers.assert_arena_equal(c.schema, orec, c.n, c.wire, arena, oarena)
