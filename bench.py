@@ -523,6 +523,10 @@ def main():
     ap.add_argument("--skim", action="store_true",
                     help="also time the schemaless skim of the workload's indexed stream "
                          "(tgpu_skim_batch)")
+    ap.add_argument("--irregular", action="store_true",
+                    help="config 2 only: also time decodes of streams that leave the canonical "
+                         "form (first record reordered; every record with an extra unknown "
+                         "field) against the indexed program decode")
     ap.add_argument("--transcode", action="store_true",
                     help="also time device transcoding of the workload's stream into the "
                          "other protocol (tgpu_transcode_batch)")
@@ -608,12 +612,73 @@ def main():
         line["transcode"] = transcode(wl, dev)
     if args.skim and rank == 0:
         line["skim"] = skim(wl, dev)
+    if args.irregular and rank == 0 and args.config == 2:
+        line["irregular"] = irregular(wl, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(wl)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def irregular(wl, dev, reps=3):
+    """Config 2 streams the fixed-layout kernels cannot take whole (the
+    reference reads them like any other stream): (i) the first record's
+    fields 1 and 2 swapped, (ii) every record carrying an extra unknown i32
+    field (a newer writer's schema; 96 bytes per record). Blocking decodes
+    (tgpu_decode_batch: plan kernel, then the parallel index + decode of the
+    tail), timed with HIP events around the call, each checked against the
+    records; reported beside the indexed program decode of the canonical
+    stream (offsets given) and the plan decode."""
+    import torch
+
+    n, L = wl.n, wl.L
+    canon = wl.wire[: n * L]
+    offs = torch.arange(n + 1, dtype=torch.int64, device=dev) * L
+    first = canon.clone()
+    first[0:11], first[11:22] = canon[11:22].clone(), canon[0:11].clone()
+    ex = torch.empty((n, 96), dtype=torch.uint8, device=dev)
+    c2 = canon.view(n, L)
+    ex[:, :88] = c2[:, :88]
+    ex[:, 88] = 8
+    ex[:, 89] = 0
+    ex[:, 90] = 20
+    ex[:, 91:95] = c2[:, 3:7]
+    ex[:, 95] = 0
+    every = ex.view(-1)
+    res = {"records": n}
+
+    def timed(name, wire, offsets=None, bytes_=None):
+        best = None
+        for _ in range(reps + 1):
+            wl.back.zero_()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            e0.record()
+            _, _, consumed = wl.S.deserialize(wl.gs, wire, n, offsets=offsets, records=wl.back)
+            e1.record()
+            torch.cuda.synchronize()
+            wall = time.perf_counter() - t0
+            ms = e0.elapsed_time(e1)
+            if consumed != wire.numel() or not torch.equal(wl.back, wl.recs):
+                raise RuntimeError("irregular decode %s differs" % name)
+            if best is None or ms < best[0]:
+                best = (ms, wall * 1e3)
+        res[name] = {"ms": round(best[0], 3), "wall_ms": round(best[1], 3),
+                     "wire_GiBps": round(wire.numel() / best[0] * 1e3 / 2**30, 1)}
+        print("irregular %s: %s" % (name, res[name]), file=sys.stderr, flush=True)
+
+    timed("plan_decode_canonical", canon)
+    timed("indexed_program_decode_canonical", canon, offs)
+    timed("first_record_reordered", first)
+    timed("every_record_extra_field", every)
+    base = res["indexed_program_decode_canonical"]["ms"]
+    for k in ("first_record_reordered", "every_record_extra_field"):
+        res[k]["x_indexed_program_decode"] = round(res[k]["ms"] / base, 2)
+    del first, ex, every, offs
+    return res
 
 
 def config1(n=1000, seconds=3.0):

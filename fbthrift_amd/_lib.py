@@ -34,6 +34,13 @@ class FieldDesc(ctypes.Structure):
                 ("elem_ttype", ctypes.c_uint8), ("qualifier", ctypes.c_uint8),
                 ("val_ttype", ctypes.c_uint8), ("reserved0", ctypes.c_uint8 * 2), ("member_offset", ctypes.c_uint32),
                 ("isset_offset", ctypes.c_uint32), ("struct_index", ctypes.c_int32),
+                ("type_index", ctypes.c_uint32)]
+
+
+class TypeDesc(ctypes.Structure):
+    _fields_ = [("ttype", ctypes.c_uint8), ("elem_ttype", ctypes.c_uint8),
+                ("val_ttype", ctypes.c_uint8), ("reserved0", ctypes.c_uint8),
+                ("struct_index", ctypes.c_int32), ("type_index", ctypes.c_uint32),
                 ("reserved1", ctypes.c_uint32)]
 
 
@@ -58,12 +65,13 @@ class Status(ctypes.Structure):
 
 
 assert ctypes.sizeof(FieldDesc) == 24 and ctypes.sizeof(StructDesc) == 20
+assert ctypes.sizeof(TypeDesc) == 16
 assert ctypes.sizeof(Status) == 32
 
 # Every symbol declared in include/thrift_gpu.h (checked by tests/test_abi.py).
 EXPORTS = [
     "tgpu_abi_version", "tgpu_code_name", "tgpu_code_classify", "tgpu_layout_compute",
-    "tgpu_schema_create", "tgpu_schema_destroy", "tgpu_schema_record_size",
+    "tgpu_schema_create", "tgpu_schema_create_ex", "tgpu_schema_destroy", "tgpu_schema_record_size",
     "tgpu_schema_fixed_wire_size", "tgpu_context_create", "tgpu_context_destroy",
     "tgpu_context_reserve", "tgpu_context_wait", "tgpu_encode_batch", "tgpu_encoded_size",
     "tgpu_decode_batch", "tgpu_index_stream", "tgpu_schema_compile", "tgpu_schema_compile_check",
@@ -98,6 +106,8 @@ def lib():
     L.tgpu_layout_compute.argtypes = [P, U32, P, U32]
     L.tgpu_schema_create.restype = I32
     L.tgpu_schema_create.argtypes = [P, U32, P, U32, ctypes.POINTER(P)]
+    L.tgpu_schema_create_ex.restype = I32
+    L.tgpu_schema_create_ex.argtypes = [P, U32, P, U32, P, U32, ctypes.POINTER(P)]
     L.tgpu_schema_destroy.argtypes = [P]
     L.tgpu_schema_record_size.restype = U32
     L.tgpu_schema_record_size.argtypes = [P]

@@ -114,6 +114,30 @@ __global__ void decode_finish_kernel(DecodeArgs a, uint64_t fixed_len) {
   }
 }
 
+// Status of a fixed-layout batch whose tail [rec_base, n) was indexed and
+// decoded after its first non-canonical record: `a` covers the tail (records,
+// offsets and indices relative to rec_base; offsets are absolute stream
+// positions of a stream that starts at 0).
+template <int P>
+__global__ void tail_decode_finish_kernel(DecodeArgs a, uint64_t rec_base) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  DevResult* res = a.res;
+  const uint64_t f = res->first_fail;
+  if (f < a.n) {
+    const Reader r = decode_one<P>(a, f);
+    res->code = r.ok() ? TGPU_ERR_INDEX_MISMATCH : r.err;
+    res->fail_offset = r.ok() ? r.pos : r.err_off;
+    res->first_fail = rec_base + f;
+    res->n_records = rec_base + f;
+    res->total_bytes = a.offs[f];
+  } else {
+    res->code = 0;
+    res->first_fail = kNone;
+    res->n_records = rec_base + a.n;
+    res->total_bytes = a.offs[a.n];
+  }
+}
+
 // After a fused index + decode of a stream range (tgpu_decode_stream): the
 // index left n_records / total_bytes / first_start (and a reader error's
 // code); a record it accepted that the decode could not store (list arena
@@ -270,6 +294,15 @@ hipError_t launch_stream_decode_finish(const DecodeArgs& a, int protocol, hipStr
   if (e != hipSuccess) return e;
   TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(stream_decode_finish_kernel<P_>, dim3(1), dim3(64), 0,
                        stream, a));
+  return hipGetLastError();
+}
+
+hipError_t launch_tail_decode_finish(const DecodeArgs& a, int protocol, uint64_t rec_base,
+                                     hipStream_t stream) {
+  const hipError_t e = launch_deep_decode(a, protocol, stream);
+  if (e != hipSuccess) return e;
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(tail_decode_finish_kernel<P_>, dim3(1), dim3(64), 0,
+                                                stream, a, rec_base));
   return hipGetLastError();
 }
 

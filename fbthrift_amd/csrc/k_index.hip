@@ -46,6 +46,7 @@ __device__ __forceinline__ dev::Reader reader_at(const IndexArgs& a, uint64_t po
 
 struct Chain {
   uint64_t end;    // first record start >= hi (or the failing record's start)
+  uint64_t second; // start of the chain's second record (kNo: fewer than two)
   uint64_t count;  // records parsed
   int32_t code;    // reader error (0: none)
   uint64_t err_off;
@@ -64,6 +65,7 @@ __device__ bool chain(const IndexArgs& a, uint64_t p, uint64_t hi, bool canonica
   out.count = 0;
   out.code = 0;
   out.err_off = 0;
+  out.second = kNo;
   const prog::Ctx pc{0, nullptr, 0, a.string_limit, a.container_limit};
   while (p < hi && out.count < max_count) {
     uint64_t q = 0;
@@ -80,7 +82,11 @@ __device__ bool chain(const IndexArgs& a, uint64_t p, uint64_t hi, bool canonica
       // (schemas without a program: any record the reader accepts)
       if (canonical_first && out.count == 0 && a.prog) return false;
       dev::Reader r = reader_at(a, p, lane);
-      dev::read_record<P>(r, a.sc, scratch, nullptr, kDiscardArena);
+      // measuring read: the root into scratch, nested elements into per-level
+      // slots after it (the index's scratch stride holds both)
+      const uint32_t root = (a.sc.s[0].size + 15) & ~15u;
+      dev::Arena A = dev::record_arena<P>(a.sc, nullptr, kDiscardArena, p, scratch + root);
+      dev::read_record<P>(r, a.sc, scratch, A);
       if (!r.ok()) {
         if (canonical_first && out.count == 0) return false;
         out.code = r.err;
@@ -91,6 +97,7 @@ __device__ bool chain(const IndexArgs& a, uint64_t p, uint64_t hi, bool canonica
       q = r.pos;
     }
     if (emit && out.count < emit_cap) emit[out.count] = p;
+    if (out.count == 1) out.second = p;
     ++out.count;
     p = q;
   }
@@ -209,6 +216,7 @@ __global__ __launch_bounds__(256) void index_spec_general_kernel(IndexArgs a) {
   uint8_t* scratch = a.scratch + j * a.rec_size;
   const uint64_t lo = chunk_lo(a, j), hi = chunk_hi(a, j);
   Chain c;
+  a.s2[j] = kNo;
   if (j == 0 && !a.speculative) {
     chain<P>(a, a.begin, hi, false, scratch, c, nullptr, 0, kNo);
     a.s[0] = a.begin;
@@ -223,12 +231,54 @@ __global__ __launch_bounds__(256) void index_spec_general_kernel(IndexArgs a) {
       a.s[j] = cand;
       a.e[j] = c.end;
       a.cnt[j] = c.count;
+      a.s2[j] = c.second;
       return;
     }
   }
   a.s[j] = kNo;
   a.e[j] = kNo;
   a.cnt[j] = 0;
+}
+
+// Speculation fallback for chunks in which no candidate opened a canonical
+// chain (kNo): any record the general reader accepts may open it (records
+// that left the canonical form: reordered, unknown or missing fields, as after
+// schema evolution). A candidate inside the record straddling the chunk's
+// start can parse as a record of its own and then run in step with the true
+// records; s2 (the chain's second start) lets the repair pass take such a
+// chain over in O(1) when the true start is its second record.
+template <int P>
+__global__ __launch_bounds__(256) void index_spec_fallback_kernel(IndexArgs a) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j >= a.n_chunks) return;
+  if (a.s[j] != kNo || a.e[j] != kNo) {
+    a.s2[j] = kNo;
+    return;
+  }
+  uint8_t* scratch = a.scratch + j * a.rec_size;
+  const uint64_t lo = chunk_lo(a, j), hi = chunk_hi(a, j);
+  Chain c;
+  if (j == 0 && !a.speculative) {
+    chain<P>(a, a.begin, hi, false, scratch, c, nullptr, 0, kNo);
+    a.s[0] = a.begin;
+    a.e[0] = c.code ? kErr : c.end;
+    a.cnt[0] = c.count;
+    a.s2[0] = kNo;
+    return;
+  }
+  const uint64_t w = j == 0 ? a.chunk : a.window;
+  const uint64_t last = lo + w < hi ? lo + w : hi;
+  for (uint64_t cand = lo; cand < last; ++cand) {
+    if (chain<P>(a, cand, hi, false, scratch, c, nullptr, 0, kNo) && c.code == 0 && c.count) {
+      a.s[j] = cand;
+      a.e[j] = c.end;
+      a.cnt[j] = c.count;
+      a.s2[j] = c.second;
+      a.pf[j] = 0;
+      return;
+    }
+  }
+  a.s2[j] = kNo;
 }
 
 // ---- LDS tiles (schemas with a program; tgpu_prog_kernels.h) ---------------
@@ -305,6 +355,12 @@ __global__ void index_fix_kernel(IndexArgs a) {
         a.e[j] = T;
         a.cnt[j] = 0;
         a.pf[j] = 0;
+      } else if (a.s2[j] == T && a.e[j] != kNo && a.e[j] != kErr && a.e[j] != kPartial) {
+        // the speculated chain's first record was a false start inside the
+        // record ending at T; from its second record on it is the true chain
+        a.s[j] = T;
+        a.cnt[j] -= 1;
+        a.s2[j] = kNo;
       } else {
         Chain c;
         chain<P>(a, T, hi, false, scratch, c, nullptr, 0, kNo, 0);
@@ -493,6 +549,8 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
   } else {
     TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_spec_general_kernel<P_>, g, b, 0, stream, a));
   }
+  if (a.prog)
+    TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_spec_fallback_kernel<P_>, g, b, 0, stream, a));
   hipLaunchKernelGGL(index_flag_kernel, g, b, 0, stream, a);
   hipError_t e = launch_scan_tiles(a.base, C, a.part, a.scal, nullptr, stream);
   if (e != hipSuccess) return e;

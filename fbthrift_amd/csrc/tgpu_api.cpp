@@ -2,6 +2,7 @@
 // validation/upload, the canonical Binary template, context workspaces and
 // the stream-ordered launch sequences of encode/decode.
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -14,8 +15,14 @@ using namespace tgpu;
 struct tgpu_schema {
   std::vector<tgpu_struct_desc> structs;
   std::vector<tgpu_field_desc> fields;
+  std::vector<tgpu_type_desc> types;  // nested container types
   tgpu_struct_desc* d_structs = nullptr;
   tgpu_field_desc* d_fields = nullptr;
+  tgpu_type_desc* d_types = nullptr;
+  // containers of structs / containers: per-record arena regions
+  bool nested = false;
+  uint32_t region_scale[2] = {0, 0};  // Binary, Compact (and CompactV1)
+  uint32_t nest_slot = 0;             // measuring reads: element slot bytes
   int device = 0;
   bool has_lists = false;
   bool has_strings = false;
@@ -147,20 +154,64 @@ int layout_struct(tgpu_struct_desc* s, uint32_t ns, tgpu_field_desc* f, uint32_t
   return TGPU_OK;
 }
 
-int validate(const tgpu_struct_desc* s, uint32_t ns, const tgpu_field_desc* f, uint32_t nf,
-             uint32_t si, int depth, bool& has_lists) {
-  if (si >= ns || depth > kMaxSchemaDepth) return TGPU_ERR_UNSUPPORTED;
-  const tgpu_struct_desc& sd = s[si];
-  if ((uint64_t)sd.first_field + sd.num_fields > nf || sd.size == 0 || sd.align == 0 ||
+// The schema tables a validation walks (fields' type_index / struct_index
+// into these).
+struct Tables {
+  const tgpu_struct_desc* s;
+  uint32_t ns;
+  const tgpu_field_desc* f;
+  uint32_t nf;
+  const tgpu_type_desc* t;
+  uint32_t nt;
+};
+
+struct SchemaFacts {
+  bool has_lists = false;
+  bool nested = false;  // a container holds structs or containers
+};
+
+int validate_struct(const Tables& T, uint32_t si, int depth, SchemaFacts& facts);
+
+// A container (list/set/map) description c at nesting depth `depth` (each
+// struct or container of structs/containers takes one of the device's
+// kMaxSchemaDepth frames).
+int validate_container(const Tables& T, uint32_t ttype, uint32_t elem, uint32_t val,
+                       int32_t struct_index, uint32_t type_index, int depth, SchemaFacts& facts) {
+  facts.has_lists = true;
+  if (depth >= kMaxSchemaDepth) return TGPU_ERR_UNSUPPORTED;
+  const bool is_map = ttype == TGPU_T_MAP;
+  if (ttype != TGPU_T_LIST && ttype != TGPU_T_SET && !is_map) return TGPU_ERR_INVALID_ARGUMENT;
+  if (is_map && !is_elem(elem)) return TGPU_ERR_UNSUPPORTED;  // keys: scalars, strings
+  const uint32_t v = is_map ? val : elem;
+  if (is_elem(v)) return TGPU_OK;
+  facts.nested = true;
+  if (v == TGPU_T_STRUCT) {
+    if (struct_index < 0 || (uint32_t)struct_index >= T.ns) return TGPU_ERR_INVALID_ARGUMENT;
+    return validate_struct(T, (uint32_t)struct_index, depth + 1, facts);
+  }
+  if (v == TGPU_T_LIST || v == TGPU_T_SET || v == TGPU_T_MAP) {
+    if (type_index == 0 || type_index > T.nt) return TGPU_ERR_INVALID_ARGUMENT;
+    const tgpu_type_desc& n = T.t[type_index - 1];
+    if (n.ttype != v) return TGPU_ERR_INVALID_ARGUMENT;
+    return validate_container(T, n.ttype, n.elem_ttype, n.val_ttype, n.struct_index,
+                              n.type_index, depth + 1, facts);
+  }
+  return TGPU_ERR_UNSUPPORTED;
+}
+
+int validate_struct(const Tables& T, uint32_t si, int depth, SchemaFacts& facts) {
+  if (si >= T.ns || depth > kMaxSchemaDepth - 1) return TGPU_ERR_UNSUPPORTED;
+  const tgpu_struct_desc& sd = T.s[si];
+  if ((uint64_t)sd.first_field + sd.num_fields > T.nf || sd.size == 0 || sd.align == 0 ||
       sd.size % sd.align)
     return TGPU_ERR_INVALID_ARGUMENT;
   if (sd.flags & ~(uint32_t)TGPU_STRUCT_UNION) return TGPU_ERR_UNSUPPORTED;
   for (uint32_t k = 0; k < sd.num_fields; ++k) {
-    const tgpu_field_desc& fd = f[sd.first_field + k];
+    const tgpu_field_desc& fd = T.f[sd.first_field + k];
     if ((sd.flags & TGPU_STRUCT_UNION) && fd.qualifier != TGPU_UNQUALIFIED)
       return TGPU_ERR_UNSUPPORTED;
     for (uint32_t j = 0; j < k; ++j)
-      if (f[sd.first_field + j].id == fd.id) return TGPU_ERR_INVALID_ARGUMENT;
+      if (T.f[sd.first_field + j].id == fd.id) return TGPU_ERR_INVALID_ARGUMENT;
     if (fd.qualifier > TGPU_TERSE) return TGPU_ERR_UNSUPPORTED;
     // a terse struct's emptiness is its fields' (thrift::empty): not supported
     if (fd.qualifier == TGPU_TERSE && fd.ttype == TGPU_T_STRUCT) return TGPU_ERR_UNSUPPORTED;
@@ -170,19 +221,16 @@ int validate(const tgpu_struct_desc* s, uint32_t ns, const tgpu_field_desc* f, u
       sz = scalar_size(fd.ttype);
     } else if (fd.ttype == TGPU_T_STRING) {
       sz = 16;
-    } else if (fd.ttype == TGPU_T_LIST || fd.ttype == TGPU_T_SET) {
-      if (!is_elem(fd.elem_ttype)) return TGPU_ERR_UNSUPPORTED;
-      has_lists = true;
-      sz = 16;
-    } else if (fd.ttype == TGPU_T_MAP) {
-      if (!is_elem(fd.elem_ttype) || !is_elem(fd.val_ttype)) return TGPU_ERR_UNSUPPORTED;
-      has_lists = true;
+    } else if (fd.ttype == TGPU_T_LIST || fd.ttype == TGPU_T_SET || fd.ttype == TGPU_T_MAP) {
+      const int rc = validate_container(T, fd.ttype, fd.elem_ttype, fd.val_ttype, fd.struct_index,
+                                        fd.type_index, depth, facts);
+      if (rc) return rc;
       sz = 16;
     } else if (fd.ttype == TGPU_T_STRUCT) {
-      if (fd.struct_index < 0 || (uint32_t)fd.struct_index >= ns) return TGPU_ERR_INVALID_ARGUMENT;
-      const int rc = validate(s, ns, f, nf, (uint32_t)fd.struct_index, depth + 1, has_lists);
+      if (fd.struct_index < 0 || (uint32_t)fd.struct_index >= T.ns) return TGPU_ERR_INVALID_ARGUMENT;
+      const int rc = validate_struct(T, (uint32_t)fd.struct_index, depth + 1, facts);
       if (rc) return rc;
-      sz = s[fd.struct_index].size;
+      sz = T.s[fd.struct_index].size;
     } else {
       return TGPU_ERR_UNSUPPORTED;
     }
@@ -190,6 +238,70 @@ int validate(const tgpu_struct_desc* s, uint32_t ns, const tgpu_field_desc* f, u
     if (fd.member_offset % (sz >= 8 ? 8 : sz)) return TGPU_ERR_INVALID_ARGUMENT;
   }
   return TGPU_OK;
+}
+
+int validate(const tgpu_struct_desc* s, uint32_t ns, const tgpu_field_desc* f, uint32_t nf,
+             const tgpu_type_desc* t, uint32_t nt, SchemaFacts& facts) {
+  return validate_struct(Tables{s, ns, f, nf, t, nt}, 0, 0, facts);
+}
+
+// ---- arena regions of nested schemas (thrift_gpu.h tgpu_schema_arena_scale)
+// Every arena byte of a record is charged to wire bytes of its own: an
+// element's slot (scalar, span, struct, packed pair) to the element's own
+// bytes (a struct element's own bytes can be one STOP), a container's
+// allocation padding (<= 7) to its header. The region scale is the largest
+// bytes-per-wire-byte ratio any element kind of the schema reaches.
+uint32_t min_wire(uint32_t t, bool compact) {
+  switch (t) {
+    case TGPU_T_BOOL: case TGPU_T_BYTE: return 1;
+    case TGPU_T_I16: return compact ? 1 : 2;
+    case TGPU_T_I32: return compact ? 1 : 4;
+    case TGPU_T_I64: return compact ? 1 : 8;
+    case TGPU_T_FLOAT: return 4;
+    case TGPU_T_DOUBLE: return 8;
+    case TGPU_T_STRING: return compact ? 1 : 4;
+    case TGPU_T_LIST: case TGPU_T_SET: return compact ? 1 : 5;
+    case TGPU_T_MAP: return compact ? 1 : 6;
+    default: return 1;  // struct: its STOP
+  }
+}
+uint32_t slot_bytes(const Tables& T, uint32_t t, int32_t si) {
+  if (t == TGPU_T_STRUCT) return T.s[si].size;
+  if (t == TGPU_T_STRING || t == TGPU_T_LIST || t == TGPU_T_SET || t == TGPU_T_MAP) return 16;
+  return scalar_size(t);
+}
+// arena bytes charged to one element of type t (+ padding of its own allocation)
+uint32_t charged(const Tables& T, uint32_t t, int32_t si) {
+  const bool cont = t == TGPU_T_LIST || t == TGPU_T_SET || t == TGPU_T_MAP;
+  return slot_bytes(T, t, si) + (cont ? 7 : 0);
+}
+void region_ratio(const Tables& T, uint32_t ttype, uint32_t elem, uint32_t val, int32_t si,
+                  uint32_t ti, bool compact, double& ratio, uint32_t& slot) {
+  const bool is_map = ttype == TGPU_T_MAP;
+  const uint32_t v = is_map ? val : elem;
+  const uint32_t kb = is_map ? slot_bytes(T, elem, -1) : 0;
+  const uint32_t kw = is_map ? min_wire(elem, compact) : 0;
+  ratio = std::max(ratio, (double)(kb + charged(T, v, si)) / (double)(kw + min_wire(v, compact)));
+  ratio = std::max(ratio, 7.0 / (double)min_wire(ttype, compact));  // this container's padding
+  if (v == TGPU_T_STRUCT || v == TGPU_T_LIST || v == TGPU_T_SET || v == TGPU_T_MAP)
+    slot = std::max(slot, kb + slot_bytes(T, v, si));
+  if (v == TGPU_T_LIST || v == TGPU_T_SET || v == TGPU_T_MAP) {
+    const tgpu_type_desc& n = T.t[ti - 1];
+    region_ratio(T, n.ttype, n.elem_ttype, n.val_ttype, n.struct_index, n.type_index, compact,
+                 ratio, slot);
+  }
+}
+void region_scale(const tgpu_schema& sc, bool compact, uint32_t& scale, uint32_t& slot) {
+  const Tables T{sc.structs.data(), (uint32_t)sc.structs.size(), sc.fields.data(),
+                 (uint32_t)sc.fields.size(), sc.types.data(), (uint32_t)sc.types.size()};
+  double ratio = 8.0;
+  slot = 16;
+  for (const tgpu_field_desc& f : sc.fields)
+    if (f.ttype == TGPU_T_LIST || f.ttype == TGPU_T_SET || f.ttype == TGPU_T_MAP)
+      region_ratio(T, f.ttype, f.elem_ttype, f.val_ttype, f.struct_index, f.type_index, compact,
+                   ratio, slot);
+  scale = ((uint32_t)std::ceil(ratio) + 7) & ~7u;
+  slot = (slot + 15) & ~15u;
 }
 
 // Canonical Binary wire template (BinaryProtocol-inl.h:53-67 headers/STOP,
@@ -504,9 +616,18 @@ const JitKernels* fixed_jit(const tgpu_schema* s, int protocol, int group, uint6
   return jit_kernels(s->prog[prog_protocol(s, protocol)], s->device, group, n, 0, false);
 }
 
-DevSchema dev_schema(const tgpu_schema* s) {
-  return DevSchema{s->d_structs, s->d_fields, (uint32_t)s->structs.size(),
-                   (uint32_t)s->fields.size(), s->str_elems ? 1u : 0u, 0u};
+DevSchema dev_schema(const tgpu_schema* s, int protocol) {
+  const uint32_t scale =
+      s->nested ? s->region_scale[protocol == TGPU_PROTOCOL_BINARY ? 0 : 1] : 0u;
+  return DevSchema{s->d_structs, s->d_fields, s->d_types, (uint32_t)s->structs.size(),
+                   (uint32_t)s->fields.size(), s->str_elems ? 1u : 0u, scale, s->nest_slot, 0u};
+}
+
+// Scratch bytes per record of a measuring read (stream index): the root
+// record, then one element slot per nesting level.
+uint64_t measure_scratch(const tgpu_schema* s) {
+  const uint64_t root = (s->structs[0].size + 15) & ~15ull;
+  return root + (s->nested ? (uint64_t)kMaxSchemaDepth * s->nest_slot : 0);
 }
 
 // Indexed decode (a.offs = record starts): compiled-program fast path, then
@@ -540,14 +661,16 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
                  bool* fused = nullptr) {
   if (fused) *fused = false;
   IndexArgs x{};
-  x.sc = dev_schema(schema);
+  x.sc = dev_schema(schema, protocol);
   x.in = in;
   x.in_len = in_len;
   x.begin = begin;
   x.end = end;
   x.speculative = speculative;
   x.protocol = protocol;
-  x.rec_size = schema->structs[0].size;
+  // record stride of the fused decode (schemas with a program) / scratch
+  // stride of the measuring reads
+  x.rec_size = schema->nested ? (uint32_t)measure_scratch(schema) : schema->structs[0].size;
   x.string_limit = limits ? limits->string_limit : 0;
   x.container_limit = limits ? limits->container_limit : 0;
   x.max_depth = limits ? limits->max_depth : 12000;
@@ -576,7 +699,7 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   const uint64_t rs = (x.rec_size + 7) & ~7u;
   const uint64_t parts = scan_tiles_parts(C) + 1;
   const uint64_t lane_words = x.chunk == index_tile_bytes() ? C * index_tile_lanes() : 0;
-  const uint64_t need = 8 * (9 * C + parts + 9) + C * rs + 4 * lane_words;
+  const uint64_t need = 8 * (10 * C + parts + 9) + C * rs + 4 * lane_words;
   if (need > ctx->index_bytes) {
     if (ctx->d_index) (void)hipFree(ctx->d_index);
     ctx->d_index = nullptr;
@@ -598,6 +721,7 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   x.scratch = (uint8_t*)(w + 8 * C + parts + 8);
   x.lanes = (uint32_t*)(x.scratch + C * rs);
   x.deep_chunks = (uint64_t*)(x.lanes + lane_words + (lane_words & 1));
+  x.s2 = x.deep_chunks + C;
   if (x.n_chunks == 0) {
     // nothing starts in [begin, end): the index is just the end position
     if (e == hipSuccess) e = launch_index_empty(x.res, offs, x.begin, fill_to, s);
@@ -609,6 +733,46 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
                                    : nullptr,
                             fused);
   return TGPU_OK;
+}
+
+// Blocking decode of a fixed-layout stream after the plan kernel: waits for
+// its verdict. Every record canonical: the batch is done (returns 0; the
+// finish kernel still records the result for tgpu_context_wait). Otherwise
+// the records from the first non-canonical one on are read the way an
+// unindexed stream is — parallel speculative index from its byte position
+// i * L (the bytes before it are i canonical records), the records decoded
+// with it (compiled program, general decoder for the rest) — and the status
+// is left on the device (returns 1). -1: the caller's serial fallback
+// (no program for the index); a HIP error goes to `e` (returns 0).
+int fixed_tail(tgpu_context* ctx, const tgpu_schema* schema, int protocol, const DecodeArgs& a,
+               uint64_t L, const tgpu_limits* limits, hipStream_t s, hipError_t& e) {
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return 0;
+  const uint64_t irr = ctx->h_res->first_irregular;
+  if (irr >= a.n) {
+    e = launch_decode_finish(a, protocol, L, s);
+    return 0;
+  }
+  DecodeArgs t = a;
+  t.recs = a.recs + irr * a.rec_size;
+  t.n = a.n - irr;
+  t.offs = ctx->d_offs + irr;
+  t.check_index = 1;
+  bool fused = false;
+  const int rc = launch_index(ctx, schema, protocol, a.in, a.in_len, irr * L, a.in_len, 0,
+                              ctx->d_offs + irr, t.n, t.n, limits, s, e, &t, &fused);
+  if (rc) {
+    e = hipErrorOutOfMemory;
+    return 0;
+  }
+  if (e == hipSuccess && fused)
+    e = launch_general_decode_list(t, protocol, ctx->d_irr, &ctx->d_res->n_irregular, s);
+  else if (e == hipSuccess)
+    e = launch_indexed_decode(ctx, schema, protocol, t, s);
+  if (e == hipSuccess) e = launch_tail_decode_finish(t, protocol, irr, s);
+  return 1;
 }
 
 }  // namespace
@@ -658,27 +822,48 @@ int tgpu_layout_compute(tgpu_struct_desc* structs, uint32_t n_structs, tgpu_fiel
 
 int tgpu_schema_create(const tgpu_struct_desc* structs, uint32_t n_structs,
                        const tgpu_field_desc* fields, uint32_t n_fields, tgpu_schema** out) {
-  if (!out || !structs || n_structs == 0 || (!fields && n_fields)) return TGPU_ERR_INVALID_ARGUMENT;
+  return tgpu_schema_create_ex(structs, n_structs, fields, n_fields, nullptr, 0, out);
+}
+
+int tgpu_schema_create_ex(const tgpu_struct_desc* structs, uint32_t n_structs,
+                          const tgpu_field_desc* fields, uint32_t n_fields,
+                          const tgpu_type_desc* types, uint32_t n_types, tgpu_schema** out) {
+  if (!out || !structs || n_structs == 0 || (!fields && n_fields) || (!types && n_types))
+    return TGPU_ERR_INVALID_ARGUMENT;
   *out = nullptr;
-  bool has_lists = false;
-  int rc = validate(structs, n_structs, fields, n_fields, 0, 0, has_lists);
+  SchemaFacts facts;
+  int rc = validate(structs, n_structs, fields, n_fields, types, n_types, facts);
   if (rc) return rc;
   auto* s = new (std::nothrow) tgpu_schema();
   if (!s) return TGPU_ERR_HIP;
   s->structs.assign(structs, structs + n_structs);
   s->fields.assign(fields, fields + n_fields);
-  s->has_lists = has_lists;
-  for (uint32_t k = 0; k < n_fields; ++k) {
-    const tgpu_field_desc& f = fields[k];
-    const bool container = f.ttype == TGPU_T_LIST || f.ttype == TGPU_T_SET || f.ttype == TGPU_T_MAP;
-    const bool se = container && (f.elem_ttype == TGPU_T_STRING ||
-                                  (f.ttype == TGPU_T_MAP && f.val_ttype == TGPU_T_STRING));
+  if (n_types) s->types.assign(types, types + n_types);
+  s->has_lists = facts.has_lists;
+  s->nested = facts.nested;
+  if (s->nested) {
+    uint32_t slot_b = 0, slot_c = 0;
+    region_scale(*s, false, s->region_scale[0], slot_b);
+    region_scale(*s, true, s->region_scale[1], slot_c);
+    s->nest_slot = std::max(slot_b, slot_c);
+  }
+  // element / value types anywhere: fields' and nested types'
+  auto note = [&](uint32_t ttype, uint32_t elem, uint32_t val) {
+    const bool container = ttype == TGPU_T_LIST || ttype == TGPU_T_SET || ttype == TGPU_T_MAP;
+    const bool se = container && (elem == TGPU_T_STRING ||
+                                  (ttype == TGPU_T_MAP && val == TGPU_T_STRING));
     s->str_elems |= se;
-    s->has_strings |= f.ttype == TGPU_T_STRING || se;
-    s->has_double |= f.ttype == TGPU_T_DOUBLE ||
-                     ((f.ttype == TGPU_T_LIST || f.ttype == TGPU_T_SET || f.ttype == TGPU_T_MAP) &&
-                      f.elem_ttype == TGPU_T_DOUBLE) ||
-                     (f.ttype == TGPU_T_MAP && f.val_ttype == TGPU_T_DOUBLE);
+    s->has_strings |= ttype == TGPU_T_STRING || se;
+    s->has_double |= ttype == TGPU_T_DOUBLE || (container && elem == TGPU_T_DOUBLE) ||
+                     (ttype == TGPU_T_MAP && val == TGPU_T_DOUBLE);
+  };
+  for (uint32_t k = 0; k < n_fields; ++k) note(fields[k].ttype, fields[k].elem_ttype, fields[k].val_ttype);
+  for (uint32_t k = 0; k < n_types; ++k) note(types[k].ttype, types[k].elem_ttype, types[k].val_ttype);
+  if (n_types && (hipMalloc(&s->d_types, sizeof(tgpu_type_desc) * n_types) != hipSuccess ||
+                  hipMemcpy(s->d_types, types, sizeof(tgpu_type_desc) * n_types,
+                            hipMemcpyHostToDevice) != hipSuccess)) {
+    tgpu_schema_destroy(s);
+    return TGPU_ERR_HIP;
   }
   (void)hipGetDevice(&s->device);
   if (hipMalloc(&s->d_structs, sizeof(tgpu_struct_desc) * n_structs) != hipSuccess ||
@@ -733,6 +918,7 @@ void tgpu_schema_destroy(tgpu_schema* s) {
   if (!s) return;
   if (s->d_structs) (void)hipFree(s->d_structs);
   if (s->d_fields) (void)hipFree(s->d_fields);
+  if (s->d_types) (void)hipFree(s->d_types);
   if (s->d_tmpl) (void)hipFree(s->d_tmpl);
   if (s->d_plan) (void)hipFree(s->d_plan);
   for (VProgram* p : s->d_prog)
@@ -757,8 +943,8 @@ int tgpu_schema_compile_check(const tgpu_struct_desc* structs, uint32_t n_struct
   if (!structs || n_structs == 0 || (!fields && n_fields) ||
       !valid_protocol(protocol))
     return TGPU_ERR_INVALID_ARGUMENT;
-  bool has_lists = false;
-  const int rc = validate(structs, n_structs, fields, n_fields, 0, 0, has_lists);
+  SchemaFacts facts;
+  const int rc = validate(structs, n_structs, fields, n_fields, nullptr, 0, facts);
   if (rc) return rc;
   tgpu_schema h;  // host tables only: nothing is uploaded
   h.structs.assign(structs, structs + n_structs);
@@ -775,6 +961,7 @@ int tgpu_schema_compile_check(const tgpu_struct_desc* structs, uint32_t n_struct
 uint32_t tgpu_schema_arena_scale(const tgpu_schema* s, int protocol) {
   if (!s || !s->has_lists || !valid_protocol(protocol)) return 0;
   const bool bin = protocol == TGPU_PROTOCOL_BINARY;
+  if (s->nested) return s->region_scale[bin ? 0 : 1];
   return s->str_elems ? (bin ? 4 : 16) : (bin ? 1 : 8);
 }
 
@@ -857,7 +1044,7 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   (void)hipGetLastError();  // drop a stale error left by another library
   hipError_t e = launch_result_init(ctx->d_res, n, s);
   EncodeArgs a{};
-  a.sc = dev_schema(schema);
+  a.sc = dev_schema(schema, protocol);
   a.recs = (const uint8_t*)records;
   a.n = n;
   a.sbase = (const uint8_t*)string_base;
@@ -933,7 +1120,7 @@ int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol
     return rc;
   }
   EncodeArgs a{};
-  a.sc = dev_schema(schema);
+  a.sc = dev_schema(schema, protocol);
   a.recs = (const uint8_t*)records;
   a.n = n;
   a.offs = out_offsets;
@@ -993,7 +1180,7 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
     return rc;
   }
   DecodeArgs a{};
-  a.sc = dev_schema(schema);
+  a.sc = dev_schema(schema, protocol);
   a.in = (const uint8_t*)in;
   a.in_len = in_len;
   a.n = n;
@@ -1027,6 +1214,27 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
                                      s);
     a.offs = ctx->d_offs;
     a.check_index = 0;
+    if (st || n_decoded || consumed) {
+      // blocking call: look at the plan kernel's verdict, and index + decode
+      // the tail after a non-canonical record in parallel
+      const int trc = fixed_tail(ctx, schema, protocol, a, fixed, limits, s, e);
+      if (trc >= 0) {
+        ctx->last_op = 1;
+        if (e != hipSuccess) {
+          fill_status(st, TGPU_ERR_HIP, 0, 0);
+          if (st) st->reserved = (int32_t)e;
+          return TGPU_ERR_HIP;
+        }
+        if (trc == 0) {  // every record canonical: decoded by the plan kernel
+          fill_status(st, TGPU_OK, n, 0);
+          if (n_decoded) *n_decoded = n;
+          if (consumed) *consumed = n * fixed;
+          return TGPU_OK;
+        }
+        tgpu_status tmp;
+        return tgpu_context_wait(ctx, stream, st ? st : &tmp, n_decoded, consumed);
+      }
+    }
     if (e == hipSuccess) e = launch_serial_decode(a, protocol, true, fixed, s);
   } else if (n) {
     if (offsets) {
@@ -1148,7 +1356,7 @@ int tgpu_decode_stream(tgpu_context* ctx, const tgpu_schema* schema, int protoco
     return rc;
   }
   DecodeArgs a{};
-  a.sc = dev_schema(schema);
+  a.sc = dev_schema(schema, protocol);
   a.in = (const uint8_t*)in;
   a.in_len = in_len;
   a.n = max_records;

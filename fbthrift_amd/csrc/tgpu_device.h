@@ -34,9 +34,11 @@ __device__ __forceinline__ uint32_t scalar_size(uint32_t t) {
          : (t == TGPU_T_I32 || t == TGPU_T_FLOAT) ? 4
                                                   : 8;
 }
-// Container elements: scalars in native layout, strings as tgpu_span.
+// Container elements: scalars in native layout, strings and containers as
+// tgpu_span (structs: slot_size).
 __device__ __forceinline__ uint32_t elem_size(uint32_t t) {
-  return t == TGPU_T_STRING ? 16 : scalar_size(t);
+  return (t == TGPU_T_STRING || t == TGPU_T_LIST || t == TGPU_T_SET || t == TGPU_T_MAP)
+             ? 16 : scalar_size(t);
 }
 // CompactProtocol-inl.h:48-86
 __device__ __forceinline__ uint32_t ctype_to_ttype(uint32_t ct) {
@@ -511,17 +513,60 @@ __device__ void skip(Reader& r, uint32_t type, int32_t depth) {
 }
 
 // ------------------------------------------------------------ struct read ---
-struct ReadFrame {
-  uint32_t si;
-  uint32_t obj;  // byte offset of the struct inside the record
-  int32_t prev;  // Compact delta base
-  uint32_t fidx; // field being read into (for isset after a nested struct)
-  uint32_t nread;  // fields read or skipped (a union takes one)
-};
-
 __device__ __forceinline__ void zero_bytes(uint8_t* p, uint32_t n) {
   for (uint32_t b = 0; b < n; ++b) p[b] = 0;
 }
+
+// A container's element (list/set) or key/value (map) types, from a
+// container field or from a type-table node (tgpu_type_desc).
+struct CType {
+  uint32_t ttype, elem, val;
+  int32_t si;   // struct of the elements / values (T_STRUCT)
+  uint32_t ti;  // 1 + type node of container elements / values
+};
+__device__ __forceinline__ CType ctype_of(const tgpu_field_desc& f) {
+  return CType{f.ttype, f.elem_ttype, f.val_ttype, f.struct_index, f.type_index};
+}
+__device__ __forceinline__ CType ctype_node(const DevSchema& sc, uint32_t ti) {
+  const tgpu_type_desc t = sc.t[ti - 1];
+  return CType{t.ttype, t.elem_ttype, t.val_ttype, t.struct_index, t.type_index};
+}
+__device__ __forceinline__ bool is_container(uint32_t t) {
+  return t == TGPU_T_LIST || t == TGPU_T_SET || t == TGPU_T_MAP;
+}
+__device__ __forceinline__ bool is_complex(uint32_t t) {
+  return t == TGPU_T_STRUCT || is_container(t);
+}
+// Bytes of one element / key / value in the arena.
+__device__ __forceinline__ uint32_t slot_size(const DevSchema& sc, uint32_t t, int32_t si) {
+  return t == TGPU_T_STRUCT ? sc.s[si].size : elem_size(t);
+}
+
+// Where containers put their elements (tgpu_schema_arena_scale):
+//   position rule (schemas without nested containers): scale x the wire
+//     position of the first element, so every slot is computable without a
+//     scan;
+//   record regions (nested schemas): each record's containers are allocated
+//     in wire order from scale x its start, 8-byte aligned;
+//   measure only (base null, cap kDiscardArena: the stream indexer): simple
+//     containers are validated without storing; a container of structs or
+//     containers reads each element into one reused slot per nesting level.
+struct Arena {
+  uint8_t* base;
+  uint64_t cap;
+  uint64_t scale;
+  uint64_t bump;    // next free offset (record regions)
+  bool regions;
+  uint8_t* nest;    // measure only: slots, nest_slot bytes per frame depth
+  uint32_t nest_slot;
+  __device__ __forceinline__ bool discard() const { return !base && cap == kDiscardArena; }
+  __device__ __forceinline__ uint64_t alloc(uint64_t first_elem_pos, uint64_t bytes) {
+    if (!regions) return scale * first_elem_pos;
+    const uint64_t o = bump;
+    bump = (bump + bytes + 7) & ~7ull;
+    return o;
+  }
+};
 
 // One container element: a scalar, or a string as a span into the stream
 // (the string field rule, Protocol.h:96-99).
@@ -541,9 +586,9 @@ __device__ __forceinline__ void read_elem(Reader& r, uint32_t t, uint8_t* dst) {
   Proto<P>::read_scalar(r, t, dst);
 }
 
-// Arena slots: scale x (wire position of the first element). Scalars need
-// scale 1 (Binary) / 8 (Compact); 16-byte string spans from >= 4 (Binary) or
-// >= 1 (Compact) wire bytes need 4 / 16.
+// Arena slots of the position rule: scale x (wire position of the first
+// element). Scalars need scale 1 (Binary) / 8 (Compact); 16-byte string
+// spans from >= 4 (Binary) or >= 1 (Compact) wire bytes need 4 / 16.
 template <int P>
 __device__ __forceinline__ uint64_t arena_scale(const DevSchema& sc) {
   return sc.str_elems ? (P == TGPU_PROTOCOL_BINARY ? 4 : 16) : Proto<P>::kArenaScale;
@@ -553,9 +598,11 @@ __device__ __forceinline__ bool at_ok(uint64_t aoff, int32_t i, uint32_t es, uin
   return aoff + ((uint64_t)i + 1) * es <= cap;
 }
 
+// protocol_methods<list>::read (protocol_methods.h:389-467) of scalar or
+// string elements: the member is reset, a type mismatch skips the list
+// (skip_n), canReadNElements, then the elements.
 template <int P>
-__device__ void read_list(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8_t* arena,
-                          uint64_t arena_cap, uint64_t scale) {
+__device__ void read_list(Reader& r, const CType& c, uint8_t* m, Arena& A) {
   using Pr = Proto<P>;
   tgpu_span sp{0, 0, 0};
   *(tgpu_span*)m = sp;
@@ -563,7 +610,7 @@ __device__ void read_list(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8
   int32_t n = 0;
   Pr::list_begin(r, reported, n);
   if (!r.ok()) return;
-  if (reported != f.elem_ttype) {
+  if (reported != c.elem) {
     // skip_n(protocol, n, {reported}) with depth 0
     if (0 >= r.max_depth) return r.fail(TGPU_ERR_DEPTH_LIMIT, r.pos);
     const uint32_t fs = Pr::fixed_in_container(reported);
@@ -574,14 +621,16 @@ __device__ void read_list(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8
     }
   } else {
     if (r.end - r.pos < (uint64_t)(uint32_t)n) return r.fail(TGPU_ERR_TRUNCATED, r.pos);
-    const uint32_t es = elem_size(f.elem_ttype);
-    const uint64_t aoff = scale * r.pos;
-    if (n > 0 && !arena && arena_cap == kDiscardArena) {
+    const uint32_t es = elem_size(c.elem);
+    if (n > 0 && A.discard()) {
       // measuring only (stream indexer): validate and consume, store nothing
       uint8_t tmp[16];
-      for (int32_t i = 0; i < n && r.ok(); ++i) read_elem<P>(r, f.elem_ttype, tmp);
+      for (int32_t i = 0; i < n && r.ok(); ++i) read_elem<P>(r, c.elem, tmp);
     } else if (n > 0) {
-      if (!arena) return r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
+      if (!A.base) return r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
+      uint8_t* arena = A.base;
+      const uint64_t arena_cap = A.cap;
+      const uint64_t aoff = A.alloc(r.pos, (uint64_t)(uint32_t)n * es);
       // the list is resized to n before the element reads
       sp.offset = aoff;
       sp.length = (uint32_t)n;
@@ -592,7 +641,7 @@ __device__ void read_list(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8
         // element that was read always fits an arena of the documented size
         const uint64_t at = aoff + (uint64_t)i * es;
         uint8_t tmp[16];
-        read_elem<P>(r, f.elem_ttype, tmp);
+        read_elem<P>(r, c.elem, tmp);
         if (!r.ok()) break;
         if (at + es > arena_cap) {
           r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
@@ -601,13 +650,13 @@ __device__ void read_list(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8
         for (uint32_t b = 0; b < es; ++b) arena[at + b] = tmp[b];
       }
       if (!r.ok()) {
-        if (f.ttype == TGPU_T_SET) {
+        if (c.ttype == TGPU_T_SET) {
           // deserialize_known_length_set (EncodeHelpers.h:248-259): an element
           // is inserted once read — the set keeps the complete ones
           sp.length = (uint32_t)i;
           if (!i) sp.offset = 0;
           *(tgpu_span*)m = sp;
-        } else if (f.elem_ttype == TGPU_T_STRING) {
+        } else if (c.elem == TGPU_T_STRING) {
           // non-trivial elements: reserve + emplace_back_default + read
           // (protocol_methods.h:374-386,458-461): the failing element is
           // in the list, empty (readString throws before assigning)
@@ -629,16 +678,15 @@ __device__ void read_list(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8
   if (r.ok()) r.ascend();
 }
 
-// protocol_methods<map>::read (protocol_methods.h:640-677): reset to empty,
-// readMapBegin, skip_n on a key/value type mismatch of a non-empty map,
-// canReadNElements(n, {k, v}) = n * 2 bytes left, then the pairs in wire
-// order, packed {key, value} at the arena offset. A failing pair is not
-// inserted (EncodeHelpers.h:188-205): the map keeps the pairs before it.
+// protocol_methods<map>::read (protocol_methods.h:640-677) of scalar or string
+// keys and values: reset to empty, readMapBegin, skip_n on a key/value type
+// mismatch of a non-empty map, canReadNElements(n, {k, v}) = n * 2 bytes
+// left, then the pairs in wire order, packed {key, value}. A failing pair is
+// not inserted (EncodeHelpers.h:188-205): the map keeps the pairs before it.
 // Pair i's slot ends within scale x (the end of pair i on the wire), so a
 // pair that was read always fits an arena of the documented size.
 template <int P>
-__device__ void read_map(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8_t* arena,
-                         uint64_t arena_cap, uint64_t scale) {
+__device__ void read_map(Reader& r, const CType& c, uint8_t* m, Arena& A) {
   using Pr = Proto<P>;
   tgpu_span sp{0, 0, 0};
   *(tgpu_span*)m = sp;
@@ -646,7 +694,7 @@ __device__ void read_map(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8_
   int32_t n = 0;
   Pr::map_begin(r, rk, rv, n);
   if (!r.ok()) return;
-  if (n > 0 && (rk != f.elem_ttype || rv != f.val_ttype)) {
+  if (n > 0 && (rk != c.elem || rv != c.val)) {
     // skip_n(protocol, n, {k, v}) with depth 0 (Protocol.h:317-344)
     if (0 >= r.max_depth) return r.fail(TGPU_ERR_DEPTH_LIMIT, r.pos);
     const uint32_t fk = Pr::fixed_in_container(rk), fv = Pr::fixed_in_container(rv);
@@ -660,24 +708,24 @@ __device__ void read_map(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8_
     }
   } else {
     if ((r.end - r.pos) / 2 < (uint64_t)(uint32_t)n) return r.fail(TGPU_ERR_TRUNCATED, r.pos);
-    const uint32_t ks = elem_size(f.elem_ttype), ps = ks + elem_size(f.val_ttype);
-    const uint64_t aoff = scale * r.pos;
-    const bool discard = !arena && arena_cap == kDiscardArena;
-    if (n > 0 && !arena && !discard) return r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
+    const uint32_t ks = elem_size(c.elem), ps = ks + elem_size(c.val);
+    const bool discard = A.discard();
+    if (n > 0 && !A.base && !discard) return r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
+    const uint64_t aoff = (n > 0 && !discard) ? A.alloc(r.pos, (uint64_t)(uint32_t)n * ps) : 0;
     int32_t i = 0;
     for (; i < n; ++i) {
       uint8_t pr[32];
-      read_elem<P>(r, f.elem_ttype, pr);
+      read_elem<P>(r, c.elem, pr);
       if (!r.ok()) break;
-      read_elem<P>(r, f.val_ttype, pr + ks);
+      read_elem<P>(r, c.val, pr + ks);
       if (!r.ok()) break;
       if (discard) continue;
       const uint64_t at = aoff + (uint64_t)i * ps;
-      if (at + ps > arena_cap) {
+      if (at + ps > A.cap) {
         r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
         break;
       }
-      for (uint32_t b = 0; b < ps; ++b) arena[at + b] = pr[b];
+      for (uint32_t b = 0; b < ps; ++b) A.base[at + b] = pr[b];
     }
     if (i > 0 && !discard) {
       sp.offset = aoff;
@@ -688,15 +736,177 @@ __device__ void read_map(Reader& r, const tgpu_field_desc& f, uint8_t* m, uint8_
   if (r.ok()) r.ascend();
 }
 
+// The record reader: the generated readNoXfer (deserialize_struct.whisker:
+// 19-160) as an explicit frame machine. Frames: a struct being read field by
+// field; a list/set whose elements are structs or containers; a map whose
+// values are. Their element semantics are the reference's:
+//   list  reserve + emplace_back_default + read (protocol_methods.h:374-386,
+//         458-461): the list holds the elements read plus the failing one;
+//   set   an element is inserted once read (EncodeHelpers.h:248-259);
+//   map   a pair is inserted once key and value are read (:188-205).
+enum : uint8_t { RF_STRUCT = 1, RF_LIST = 2, RF_MAP = 3 };
+struct ReadFrame {
+  uint8_t kind;
+  uint8_t is_set;
+  uint8_t etype;   // list: element type; map: value type
+  uint8_t ktype;   // map: key type
+  int32_t prev;    // struct: Compact delta base
+  int32_t si;      // struct: its index; list/map: struct of the elements / values
+  uint32_t ti;     // list/map: type node of container elements / values
+  uint32_t fidx;   // struct: field whose struct / container value is open
+  uint32_t nread;  // struct: fields read or skipped (a union takes one)
+  uint32_t n, i;   // list/map: elements, elements done
+  uint32_t es, ks; // list/map: element (pair) stride in the arena, key bytes
+  uint8_t* obj;    // struct: the object; list/map: element array
+  uint8_t* span;   // list/map: the member / element span being filled
+};
+
+__device__ __forceinline__ void set_span_len(uint8_t* m, uint8_t* arr, uint8_t* base, uint32_t len) {
+  tgpu_span sp{len ? (uint64_t)(arr - base) : 0, len, 0};
+  *(tgpu_span*)m = sp;
+}
+
+// Child value of frame p is complete (and the reader ok).
+__device__ __forceinline__ void child_done(const DevSchema& sc, ReadFrame& p, const Arena& A) {
+  if (p.kind == RF_STRUCT) {
+    p.obj[sc.f[p.fidx].isset_offset] = 1;  // __isset.set(idx, true)
+  } else {
+    ++p.i;
+    if (p.kind == RF_MAP || p.is_set) set_span_len(p.span, p.obj, A.base, p.i);
+  }
+}
+
+// Opens the container value of type c at member / element slot m: simple
+// elements are read here (returns true: done), elements that are structs
+// or containers get a frame (returns false).
 template <int P>
-__device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, uint8_t* arena,
-                            uint64_t arena_cap) {
+__device__ bool open_container(Reader& r, const DevSchema& sc, const CType& c, uint8_t* m,
+                               Arena& A, ReadFrame* st, int& sp) {
+  using Pr = Proto<P>;
+  const bool is_map = c.ttype == TGPU_T_MAP;
+  const uint32_t et = is_map ? c.val : c.elem;
+  if (!is_complex(et)) {
+    if (is_map) read_map<P>(r, c, m, A);
+    else read_list<P>(r, c, m, A);
+    return true;
+  }
+  *(tgpu_span*)m = tgpu_span{0, 0, 0};  // reset (deserialize_field.whisker:44-47)
+  uint32_t rk = 0, rv = 0;
+  int32_t n = 0;
+  if (is_map) Pr::map_begin(r, rk, rv, n);
+  else Pr::list_begin(r, rv, n);
+  if (!r.ok()) return true;
+  const bool mismatch = is_map ? (n > 0 && (rk != c.elem || rv != c.val)) : rv != c.elem;
+  if (mismatch) {
+    if (0 >= r.max_depth) {
+      r.fail(TGPU_ERR_DEPTH_LIMIT, r.pos);
+      return true;
+    }
+    for (int32_t i = 0; i < n && r.ok(); ++i) {
+      if (is_map) skip<P>(r, rk, 1);
+      if (r.ok()) skip<P>(r, rv, 1);
+    }
+    if (r.ok()) r.ascend();
+    return true;
+  }
+  if ((r.end - r.pos) / (is_map ? 2 : 1) < (uint64_t)(uint32_t)n) {
+    r.fail(TGPU_ERR_TRUNCATED, r.pos);
+    return true;
+  }
+  if (n == 0) {
+    r.ascend();
+    return true;
+  }
+  if (sp == kMaxSchemaDepth) {
+    r.fail(TGPU_ERR_UNSUPPORTED, r.pos);
+    return true;
+  }
+  const uint32_t ks = is_map ? elem_size(c.elem) : 0;
+  const uint32_t es = ks + slot_size(sc, et, c.si);
+  uint8_t* arr;
+  uint32_t stride = es;
+  if (A.discard()) {
+    arr = A.nest + (uint64_t)sp * A.nest_slot;  // one reused slot per level
+    stride = 0;
+  } else {
+    if (!A.base) {
+      r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
+      return true;
+    }
+    const uint64_t bytes = (uint64_t)(uint32_t)n * es;
+    const uint64_t aoff = A.alloc(r.pos, bytes);
+    if (aoff + bytes > A.cap) {
+      r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
+      return true;
+    }
+    arr = A.base + aoff;
+  }
+  ReadFrame& f = st[sp++];
+  f.kind = is_map ? RF_MAP : RF_LIST;
+  f.is_set = c.ttype == TGPU_T_SET;
+  f.etype = (uint8_t)et;
+  f.ktype = (uint8_t)c.elem;
+  f.si = c.si;
+  f.ti = c.ti;
+  f.n = (uint32_t)n;
+  f.i = 0;
+  f.es = stride;
+  f.ks = ks;
+  f.obj = arr;
+  f.span = m;
+  return false;
+}
+
+// Reads one record into rec (zeroed by the caller). A.bump: the record's
+// region start when A.regions.
+template <int P>
+__device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, Arena& A) {
   using Pr = Proto<P>;
   ReadFrame st[kMaxSchemaDepth];
   int sp = 0;
-  st[sp++] = ReadFrame{0, 0, 0, 0, 0};
+  {
+    ReadFrame& f = st[sp++];
+    f.kind = RF_STRUCT;
+    f.si = 0;
+    f.obj = rec;
+    f.prev = 0;
+    f.nread = 0;
+    f.fidx = 0;
+  }
   while (sp > 0 && r.ok()) {
     ReadFrame& fr = st[sp - 1];
+    if (fr.kind != RF_STRUCT) {
+      if (fr.i == fr.n) {  // readListEnd / readMapEnd
+        r.ascend();
+        --sp;
+        if (sp > 0) child_done(sc, st[sp - 1], A);
+        continue;
+      }
+      const uint32_t esz = fr.es ? fr.es : (fr.ks + slot_size(sc, fr.etype, fr.si));
+      uint8_t* el = fr.obj + (uint64_t)fr.i * fr.es;
+      zero_bytes(el, esz);  // a default-constructed element / pair
+      uint8_t* val = el;
+      if (fr.kind == RF_MAP) {
+        read_elem<P>(r, fr.ktype, el);
+        if (!r.ok()) break;
+        val = el + fr.ks;
+      } else if (!fr.is_set) {
+        set_span_len(fr.span, fr.obj, A.base, fr.i + 1);  // emplace_back_default
+      }
+      if (fr.etype == TGPU_T_STRUCT) {
+        if (sp == kMaxSchemaDepth) return r.fail(TGPU_ERR_UNSUPPORTED, r.pos);
+        ReadFrame& f = st[sp++];
+        f.kind = RF_STRUCT;
+        f.si = fr.si;
+        f.obj = val;
+        f.prev = 0;
+        f.nread = 0;
+        f.fidx = 0;
+      } else if (open_container<P>(r, sc, ctype_node(sc, fr.ti), val, A, st, sp)) {
+        if (r.ok()) child_done(sc, fr, A);
+      }
+      continue;
+    }
     const tgpu_struct_desc sd = sc.s[fr.si];
     const bool un = sd.flags & TGPU_STRUCT_UNION;
     uint32_t wt = 0;
@@ -704,14 +914,10 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, uint8_
     if (!Pr::field_header(r, fr.prev, wt, id)) {
       if (!r.ok()) return;
       // a union with no field is cleared (deserialize_union.whisker:26-28)
-      if (un && fr.nread == 0) zero_bytes(rec + fr.obj, sd.size);
-      // STOP: struct done; mark the parent's field set
+      if (un && fr.nread == 0) zero_bytes(fr.obj, sd.size);
+      // STOP: struct done
       --sp;
-      if (sp > 0) {
-        const ReadFrame& parent = st[sp - 1];
-        const tgpu_field_desc& pf = sc.f[parent.fidx];
-        rec[parent.obj + pf.isset_offset] = 1;
-      }
+      if (sp > 0) child_done(sc, st[sp - 1], A);
       continue;
     }
     // a union's one field must be followed by STOP (throwUnionMissingStop)
@@ -730,10 +936,10 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, uint8_
       continue;
     }
     const tgpu_field_desc f = sc.f[hit];
-    uint8_t* m = rec + fr.obj + f.member_offset;
+    uint8_t* m = fr.obj + f.member_offset;
     if (un) {  // field_ref().emplace(): a fresh member becomes active
-      zero_bytes(rec + fr.obj, sd.size);
-      rec[fr.obj + f.isset_offset] = 1;
+      zero_bytes(fr.obj, sd.size);
+      fr.obj[f.isset_offset] = 1;
     }
     if (is_scalar(f.ttype)) {
       Pr::read_scalar(r, f.ttype, m);
@@ -745,15 +951,37 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, uint8_
     } else if (f.ttype == TGPU_T_STRUCT) {
       if (sp == kMaxSchemaDepth) return r.fail(TGPU_ERR_UNSUPPORTED, r.pos);
       fr.fidx = (uint32_t)hit;
-      st[sp++] = ReadFrame{(uint32_t)f.struct_index, fr.obj + f.member_offset, 0, 0, 0};
+      ReadFrame& nf = st[sp++];
+      nf.kind = RF_STRUCT;
+      nf.si = f.struct_index;
+      nf.obj = m;
+      nf.prev = 0;
+      nf.nread = 0;
+      nf.fidx = 0;
       continue;  // isset set when the nested STOP is reached
-    } else if (f.ttype == TGPU_T_MAP) {
-      read_map<P>(r, f, m, arena, arena_cap, arena_scale<P>(sc));
     } else {
-      read_list<P>(r, f, m, arena, arena_cap, arena_scale<P>(sc));
+      fr.fidx = (uint32_t)hit;
+      if (!open_container<P>(r, sc, ctype_of(f), m, A, st, sp)) continue;
     }
-    if (r.ok()) rec[fr.obj + f.isset_offset] = 1;
+    if (r.ok()) fr.obj[f.isset_offset] = 1;
   }
+}
+
+// The arena of one record read: the position rule, or the record's region
+// (scale x its start) for nested schemas; `nest` = per-level element slots
+// when measuring only.
+template <int P>
+__device__ __forceinline__ Arena record_arena(const DevSchema& sc, uint8_t* base, uint64_t cap,
+                                             uint64_t start, uint8_t* nest) {
+  Arena A;
+  A.base = base;
+  A.cap = cap;
+  A.regions = sc.bump_scale != 0;
+  A.scale = A.regions ? sc.bump_scale : arena_scale<P>(sc);
+  A.bump = A.regions ? sc.bump_scale * start : 0;
+  A.nest = nest;
+  A.nest_slot = sc.nest_slot;
+  return A;
 }
 
 // ---------------------------------------------------------- deep passes ----
@@ -791,7 +1019,8 @@ __device__ Reader decode_record(const DecodeArgs& a, uint64_t i, int lane) {
     r.fail(TGPU_ERR_INDEX_MISMATCH, start);
     return r;
   }
-  read_record<P>(r, a.sc, rec, a.arena, a.arena_cap);
+  Arena A = record_arena<P>(a.sc, a.arena, a.arena_cap, start, nullptr);
+  read_record<P>(r, a.sc, rec, A);
   if (r.ok() && a.check_index && r.pos != a.offs[i + 1]) r.fail(TGPU_ERR_INDEX_MISMATCH, r.pos);
   return r;
 }
@@ -887,24 +1116,39 @@ __device__ __forceinline__ bool terse_empty(const tgpu_field_desc& f, const uint
   return ((const tgpu_span*)m)->length == 0;
 }
 
+// The record writer: the generated write (serialize_struct.whisker:40-67,
+// serialize_field.whisker:17-71) as an explicit frame machine — a struct's
+// fields in declaration order, and lists/sets/maps whose elements or values
+// are structs or containers element by element.
+enum : uint8_t { WF_STRUCT = 1, WF_LIST = 2, WF_MAP = 3 };
 struct WriteFrame {
-  uint32_t si;
-  uint32_t obj;
-  uint32_t k;     // next field index within the struct
-  int32_t last;   // Compact lastFieldId_
-  uint32_t end;   // one past the last field to write
+  uint8_t kind;
+  uint8_t etype;  // list: element type; map: value type
+  uint8_t ktype;  // map: key type
+  uint8_t pad;
+  uint32_t si;    // struct: its index; list/map: struct of the elements / values
+  uint32_t ti;    // list/map: type node of container elements / values
+  uint32_t k;     // struct: next field index; list/map: next element
+  int32_t last;   // struct: Compact lastFieldId_
+  uint32_t end;   // struct: one past the last field to write; list/map: elements
+  uint32_t es, ks;
+  const uint8_t* obj;
 };
 
 // The fields a struct writes: all of them, or for a union its active member
 // only (serialize_union.whisker:52-66): the first whose isset byte is set.
-__device__ __forceinline__ WriteFrame write_frame(const DevSchema& sc, const uint8_t* rec,
-                                                  uint32_t si, uint32_t obj) {
+__device__ __forceinline__ WriteFrame write_frame(const DevSchema& sc, uint32_t si,
+                                                  const uint8_t* obj) {
   const tgpu_struct_desc sd = sc.s[si];
-  WriteFrame w{si, obj, 0, 0, sd.num_fields};
+  WriteFrame w{};
+  w.kind = WF_STRUCT;
+  w.si = si;
+  w.obj = obj;
+  w.end = sd.num_fields;
   if (sd.flags & TGPU_STRUCT_UNION) {
     w.k = sd.num_fields;
     for (uint32_t k = 0; k < sd.num_fields; ++k) {
-      if (rec[obj + sc.f[sd.first_field + k].isset_offset]) {
+      if (obj[sc.f[sd.first_field + k].isset_offset]) {
         w.k = k;
         w.end = k + 1;
         break;
@@ -914,14 +1158,108 @@ __device__ __forceinline__ WriteFrame write_frame(const DevSchema& sc, const uin
   return w;
 }
 
+// writeListBegin / writeSetBegin / writeMapBegin (BinaryProtocol-inl.h:69-96,
+// CompactProtocol-inl.h:182-246) of a container value with `n` elements.
+template <int P>
+__device__ __forceinline__ void container_header(Writer& w, const CType& c, uint32_t n) {
+  if (c.ttype == TGPU_T_MAP) {
+    if (P == TGPU_PROTOCOL_BINARY) {
+      w.put(c.elem);
+      w.put(c.val);
+      w.put_be(n, 4);
+    } else if (n == 0) {
+      w.put(0);
+    } else {
+      w.varint(n);
+      w.put((ttype_to_ctype(c.elem) << 4) | ttype_to_ctype(c.val));
+    }
+  } else if (P == TGPU_PROTOCOL_BINARY) {
+    w.put(c.elem);
+    w.put_be(n, 4);
+  } else {
+    const uint32_t ct = ttype_to_ctype(c.elem);
+    if (n <= 14) {
+      w.put((n << 4) | ct);
+    } else {
+      w.put(0xf0 | ct);
+      w.varint(n);
+    }
+  }
+}
+
+// Writes the container value of type c held in span member m: simple
+// elements here (returns true), structs / containers as elements get a
+// frame (returns false).
+template <int P>
+__device__ bool write_container(Writer& w, const DevSchema& sc, const CType& c,
+                                const uint8_t* m, const uint8_t* sbase, const uint8_t* lbase,
+                                WriteFrame* st, int& sp) {
+  const tgpu_span sp_ = *(const tgpu_span*)m;
+  // checked_container_size: > INT32_MAX -> SIZE_LIMIT
+  if (sp_.length > 0x7fffffffu) {
+    w.fail(TGPU_ERR_WRITE_SIZE_LIMIT, w.pos);
+    return true;
+  }
+  container_header<P>(w, c, sp_.length);
+  const bool is_map = c.ttype == TGPU_T_MAP;
+  const uint32_t et = is_map ? c.val : c.elem;
+  const uint32_t ks = is_map ? elem_size(c.elem) : 0;
+  const uint8_t* e = lbase + sp_.offset;
+  if (!is_complex(et)) {
+    const uint32_t ps = ks + elem_size(et);
+    for (uint32_t i = 0; i < sp_.length && w.ok(); ++i) {
+      if (is_map) write_elem<P>(w, c.elem, e + (uint64_t)i * ps, sbase);
+      if (w.ok()) write_elem<P>(w, et, e + (uint64_t)i * ps + ks, sbase);
+    }
+    return true;
+  }
+  if (sp_.length == 0) return true;
+  if (sp == kMaxSchemaDepth) {
+    w.fail(TGPU_ERR_UNSUPPORTED, w.pos);
+    return true;
+  }
+  WriteFrame& f = st[sp++];
+  f = WriteFrame{};
+  f.kind = is_map ? WF_MAP : WF_LIST;
+  f.etype = (uint8_t)et;
+  f.ktype = (uint8_t)c.elem;
+  f.si = (uint32_t)c.si;
+  f.ti = c.ti;
+  f.k = 0;
+  f.end = sp_.length;
+  f.ks = ks;
+  f.es = ks + slot_size(sc, et, c.si);
+  f.obj = e;
+  return false;
+}
+
 template <int P>
 __device__ void write_record(Writer& w, const DevSchema& sc, const uint8_t* rec,
                              const uint8_t* sbase, const uint8_t* lbase) {
   WriteFrame st[kMaxSchemaDepth];
   int sp = 0;
-  st[sp++] = write_frame(sc, rec, 0, 0);
+  st[sp++] = write_frame(sc, 0, rec);
   while (sp > 0 && w.ok()) {
     WriteFrame& fr = st[sp - 1];
+    if (fr.kind != WF_STRUCT) {
+      if (fr.k >= fr.end) {  // lists and maps have no end marker on the wire
+        --sp;
+        continue;
+      }
+      const uint8_t* el = fr.obj + (uint64_t)fr.k++ * fr.es;
+      if (fr.kind == WF_MAP) {
+        write_elem<P>(w, fr.ktype, el, sbase);
+        if (!w.ok()) break;
+        el += fr.ks;
+      }
+      if (fr.etype == TGPU_T_STRUCT) {
+        if (sp == kMaxSchemaDepth) return w.fail(TGPU_ERR_UNSUPPORTED, w.pos);
+        st[sp++] = write_frame(sc, fr.si, el);
+      } else {
+        write_container<P>(w, sc, ctype_node(sc, fr.ti), el, sbase, lbase, st, sp);
+      }
+      continue;
+    }
     const tgpu_struct_desc sd = sc.s[fr.si];
     if (fr.k >= fr.end) {
       w.put(0);  // writeFieldStop (T_STOP / CT_STOP are both 0)
@@ -929,7 +1267,7 @@ __device__ void write_record(Writer& w, const DevSchema& sc, const uint8_t* rec,
       continue;
     }
     const tgpu_field_desc f = sc.f[sd.first_field + fr.k++];
-    const uint8_t* obj = rec + fr.obj;
+    const uint8_t* obj = fr.obj;
     if (f.qualifier == TGPU_OPTIONAL && !obj[f.isset_offset]) continue;
     const uint8_t* m = obj + f.member_offset;
     if (f.qualifier == TGPU_TERSE && terse_empty(f, m)) continue;
@@ -959,46 +1297,9 @@ __device__ void write_record(Writer& w, const DevSchema& sc, const uint8_t* rec,
       w.bytes(sbase + sp_.offset, sp_.length);
     } else if (f.ttype == TGPU_T_STRUCT) {
       if (sp == kMaxSchemaDepth) return w.fail(TGPU_ERR_UNSUPPORTED, w.pos);
-      st[sp++] = write_frame(sc, rec, (uint32_t)f.struct_index, fr.obj + f.member_offset);
-    } else if (f.ttype == TGPU_T_MAP) {
-      // writeMapBegin (BinaryProtocol-inl.h:69-80, CompactProtocol-inl.h:182-201)
-      const tgpu_span sp_ = *(const tgpu_span*)m;
-      if (sp_.length > 0x7fffffffu) return w.fail(TGPU_ERR_WRITE_SIZE_LIMIT, w.pos);
-      if (P == TGPU_PROTOCOL_BINARY) {
-        w.put(f.elem_ttype);
-        w.put(f.val_ttype);
-        w.put_be(sp_.length, 4);
-      } else if (sp_.length == 0) {
-        w.put(0);
-      } else {
-        w.varint(sp_.length);
-        w.put((ttype_to_ctype(f.elem_ttype) << 4) | ttype_to_ctype(f.val_ttype));
-      }
-      const uint32_t ks = elem_size(f.elem_ttype), ps = ks + elem_size(f.val_ttype);
-      const uint8_t* e = lbase + sp_.offset;
-      for (uint32_t i = 0; i < sp_.length && w.ok(); ++i) {
-        write_elem<P>(w, f.elem_ttype, e + (uint64_t)i * ps, sbase);
-        if (w.ok()) write_elem<P>(w, f.val_ttype, e + (uint64_t)i * ps + ks, sbase);
-      }
-    } else {  // list / set of scalars
-      const tgpu_span sp_ = *(const tgpu_span*)m;
-      if (sp_.length > 0x7fffffffu) return w.fail(TGPU_ERR_WRITE_SIZE_LIMIT, w.pos);
-      if (P == TGPU_PROTOCOL_BINARY) {
-        w.put(f.elem_ttype);
-        w.put_be(sp_.length, 4);
-      } else {
-        const uint32_t ct = ttype_to_ctype(f.elem_ttype);
-        if (sp_.length <= 14) {
-          w.put((sp_.length << 4) | ct);
-        } else {
-          w.put(0xf0 | ct);
-          w.varint(sp_.length);
-        }
-      }
-      const uint32_t es = elem_size(f.elem_ttype);
-      const uint8_t* e = lbase + sp_.offset;
-      for (uint32_t i = 0; i < sp_.length && w.ok(); ++i)
-        write_elem<P>(w, f.elem_ttype, e + (uint64_t)i * es, sbase);
+      st[sp++] = write_frame(sc, (uint32_t)f.struct_index, m);
+    } else {
+      write_container<P>(w, sc, ctype_of(f), m, sbase, lbase, st, sp);
     }
   }
 }

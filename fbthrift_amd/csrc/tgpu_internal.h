@@ -189,8 +189,11 @@ struct DevResult {
 struct DevSchema {
   const tgpu_struct_desc* s;
   const tgpu_field_desc* f;
+  const tgpu_type_desc* t;  // nested container types (type_index k -> t[k - 1])
   uint32_t ns, nf;
-  uint32_t str_elems;  // some list/set/map holds strings: arena scale 4 / 16
+  uint32_t str_elems;   // some list/set/map holds strings: arena scale 4 / 16
+  uint32_t bump_scale;  // nested schema: record regions of this scale (0: position rule)
+  uint32_t nest_slot;   // nested schema, measuring reads: element slot bytes per level
   uint32_t pad_;
 };
 
@@ -263,6 +266,7 @@ struct IndexArgs {
   // per chunk: speculated/verified first start, end of the chain, record count
   uint64_t* s;
   uint64_t* e;
+  uint64_t* s2;              // speculation: the chain's second start (kNo: none)
   unsigned long long* cnt;
   uint64_t* pf;              // speculation: where the program stopped (partial chain)
   uint64_t* ep;              // emit: where the program stopped (kNo: done)
@@ -345,6 +349,10 @@ hipError_t launch_general_decode_list(const DecodeArgs& a, int protocol,
 hipError_t launch_skim(const SkimArgs& a, int protocol, hipStream_t stream);
 // The records deferred by kErrDeep (a.deep), redone with HBM skip frames.
 hipError_t launch_deep_decode(const DecodeArgs& a, int protocol, hipStream_t stream);
+// Status of a fixed-layout batch whose tail from record rec_base was indexed
+// and decoded (a: the tail, indices relative to rec_base).
+hipError_t launch_tail_decode_finish(const DecodeArgs& a, int protocol, uint64_t rec_base,
+                                     hipStream_t stream);
 hipError_t launch_serial_decode(const DecodeArgs& a, int protocol,
                                 bool from_irregular, uint64_t fixed_len,
                                 hipStream_t stream);

@@ -24,14 +24,37 @@ OPTIONAL = 1
 TERSE = 2  # @thrift.TerseWrite: written only when not empty (op::isEmpty)
 
 
+class Type:
+    """A container type held by a container (a list/set element or a map
+    value that is itself a list, set or map): tgpu_type_desc. `struct` is
+    the struct of T_STRUCT elements / values, `inner` the Type of container
+    elements / values."""
+
+    def __init__(self, ttype, elem_ttype, val_ttype=0, struct=None, inner=None):
+        self.ttype, self.elem_ttype, self.val_ttype = int(ttype), int(elem_ttype), int(val_ttype)
+        self.struct, self.inner = struct, inner
+
+
 class Field:
+    """One field. For T_STRUCT, `struct` is the nested struct; for a list/set
+    of structs (elem_ttype T_STRUCT) or a map with struct values (val_ttype
+    T_STRUCT), `struct` is that struct; `inner` is the Type of container
+    elements / values."""
+
     def __init__(self, id, ttype, elem_ttype=0, optional=False, struct=None, name=None,
-                 qualifier=None, val_ttype=0):
+                 qualifier=None, val_ttype=0, inner=None):
         self.id, self.ttype, self.elem_ttype = int(id), int(ttype), int(elem_ttype)
         self.val_ttype = int(val_ttype)  # T_MAP: value type (elem_ttype = key type)
         self.qualifier = int(qualifier) if qualifier is not None else (OPTIONAL if optional else 0)
         self.optional, self.struct = self.qualifier == OPTIONAL, struct
+        self.inner = inner
         self.name = name or "f%d" % self.id
+
+
+def element_struct(t):
+    """The struct a container description (Field or Type) holds, if any."""
+    v = t.val_ttype if t.ttype == T_MAP else t.elem_ttype
+    return t.struct if v == T_STRUCT else None
 
 
 class Struct:
@@ -49,6 +72,18 @@ class Schema:
         self.structs = []
         index = {}
 
+        self.types, tindex = [], {}
+
+        def visit_container(t):
+            es = element_struct(t)
+            if es is not None:
+                visit(es)
+            if t.inner is not None:
+                if id(t.inner) not in tindex:
+                    tindex[id(t.inner)] = len(self.types)
+                    self.types.append(t.inner)
+                visit_container(t.inner)
+
         def visit(s):
             if id(s) in index:
                 return index[id(s)]
@@ -57,10 +92,13 @@ class Schema:
             for f in s.fields:
                 if f.ttype == T_STRUCT:
                     visit(f.struct)
+                elif f.ttype in (T_LIST, T_SET, T_MAP):
+                    visit_container(f)
             return index[id(s)]
 
         visit(root)
         self._index = index
+        self._tindex = tindex
         self._layout()
 
     # -- layout -------------------------------------------------------------
@@ -118,9 +156,37 @@ class Schema:
                 fd.val_ttype = f.val_ttype
                 fd.member_offset = self.member[(si, k)]
                 fd.isset_offset = self.isset[(si, k)]
-                fd.struct_index = self._index[id(f.struct)] if f.ttype == T_STRUCT else -1
+                fd.struct_index = self._struct_ref(f)
+                fd.type_index = self._type_ref(f)
                 j += 1
         return structs, len(self.structs), fields, nf
+
+    def _struct_ref(self, t):
+        if t.ttype == T_STRUCT or element_struct(t) is not None:
+            return self._index[id(t.struct)]
+        return -1
+
+    def _type_ref(self, t):
+        return 1 + self._tindex[id(t.inner)] if getattr(t, "inner", None) is not None else 0
+
+    def type_descriptors(self):
+        """The nested container types (tgpu_type_desc[]) for
+        tgpu_schema_create_ex: (array, count)."""
+        types = (_lib.TypeDesc * max(len(self.types), 1))()
+        for k, t in enumerate(self.types):
+            types[k].ttype, types[k].elem_ttype, types[k].val_ttype = t.ttype, t.elem_ttype, t.val_ttype
+            types[k].struct_index = self._struct_ref(t)
+            types[k].type_index = self._type_ref(t)
+        return types, len(self.types)
+
+    @property
+    def nested(self):
+        """Some container holds structs or containers (arena record regions)."""
+        def complex_(t):
+            v = t.val_ttype if t.ttype == T_MAP else t.elem_ttype
+            return v in (T_STRUCT, T_LIST, T_SET, T_MAP)
+        return any(complex_(f) for s in self.structs for f in s.fields
+                   if f.ttype in (T_LIST, T_SET, T_MAP))
 
     # -- numpy view of the record layout -------------------------------------
     def dtype(self, si=0):
@@ -149,16 +215,28 @@ class Schema:
     def from_table(cls, table):
         """Builds a Schema from the tests/golden manifest form: a list of
         structs, each a list of [id, ttype, elem_ttype, qualifier, struct_index]
-        (+ val_ttype for a map); a union is {"union": true, "fields": [...]}."""
+        (+ val_ttype for a map, + the nested container type of the elements /
+        values as [ttype, elem_ttype, val_ttype, struct_index, nested]); a
+        union is {"union": true, "fields": [...]}. struct_index names the
+        struct of a T_STRUCT field or of T_STRUCT elements / values."""
         structs = [Struct("S%d" % i, [], union=isinstance(e, dict) and e.get("union"))
                    for i, e in enumerate(table)]
+
+        def typ(spec):
+            if not spec:
+                return None
+            tt, et, vt, sub = spec[:4]
+            return Type(tt, et, vt, struct=structs[sub] if sub is not None and sub >= 0 else None,
+                        inner=typ(spec[4] if len(spec) > 4 else None))
+
         for si, e in enumerate(table):
             for row in (e["fields"] if isinstance(e, dict) else e):
                 fid, tt, et, q, sub = row[:5]
                 structs[si].fields.append(
                     Field(fid, tt, et, qualifier=q,
-                          struct=structs[sub] if tt == T_STRUCT else None,
-                          val_ttype=row[5] if len(row) > 5 else 0))
+                          struct=structs[sub] if sub is not None and sub >= 0 else None,
+                          val_ttype=row[5] if len(row) > 5 else 0,
+                          inner=typ(row[6] if len(row) > 6 else None)))
         return cls(structs[0])
 
 

@@ -91,10 +91,12 @@ class GpuSchema:
     def __init__(self, schema):
         self.schema = schema
         structs, ns, fields, nf = schema.descriptors()
-        self._keep = (structs, fields)
+        types, nt = schema.type_descriptors()
+        self._keep = (structs, fields, types)
         h = ctypes.c_void_p()
-        rc = _lib.lib().tgpu_schema_create(ctypes.addressof(structs), ns,
-                                           ctypes.addressof(fields), nf, ctypes.byref(h))
+        rc = _lib.lib().tgpu_schema_create_ex(ctypes.addressof(structs), ns,
+                                              ctypes.addressof(fields), nf,
+                                              ctypes.addressof(types), nt, ctypes.byref(h))
         if rc:
             raise TgpuError("tgpu_schema_create: %s" % _lib.CODES.get(rc, rc))
         self.handle = h

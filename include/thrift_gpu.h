@@ -110,14 +110,25 @@ enum tgpu_qualifier {
  * One field of a struct, in IDL declaration order (= serialization order,
  * thrift/compiler/generate/t_whisker_generator.cc:231-236).
  *   ttype        T_BOOL..T_FLOAT scalar, T_STRING (binary/string), T_STRUCT,
- *                T_LIST or T_SET of a scalar or string element type, T_MAP
- *                of scalar or string key and value types.
+ *                T_LIST or T_SET, T_MAP.
  *   elem_ttype   element type for T_LIST/T_SET, key type for T_MAP, else 0.
- *   val_ttype    value type for T_MAP, else 0.
+ *                A list/set element may be a scalar, a string, a struct or
+ *                itself a list/set/map; a map key is a scalar or a string.
+ *   val_ttype    value type for T_MAP (any type, like a list element), else 0.
  * A string inside a container is a tgpu_span (like a string field); the
  * list arena then needs tgpu_schema_arena_scale bytes per input byte.
- *   struct_index nested struct (index into the schema's struct table) for
- *                T_STRUCT, else -1.
+ *   struct_index the struct (index into the schema's struct table) of a
+ *                T_STRUCT field, of a list/set's T_STRUCT elements or of a
+ *                map's T_STRUCT values; else -1.
+ *   type_index   1 + index into the schema's type table (tgpu_type_desc,
+ *                tgpu_schema_create_ex) of the container that is this
+ *                list/set's element or this map's value type; 0 otherwise.
+ * Containers hold their elements in the list arena: scalars in native
+ * layout, strings and containers as tgpu_span, structs in the struct layout;
+ * a map holds packed {key, value} pairs. This is the shape of the
+ * reference's TypeInfo / ListFieldExt / MapFieldExt tables
+ * (thrift/lib/cpp2/protocol/TableBasedForwardTypes.h:37-93), which nest the
+ * same way.
  */
 typedef struct tgpu_field_desc {
   int16_t id;
@@ -129,8 +140,24 @@ typedef struct tgpu_field_desc {
   uint32_t member_offset;
   uint32_t isset_offset;
   int32_t struct_index;
-  uint32_t reserved1;
+  uint32_t type_index;
 } tgpu_field_desc; /* 24 bytes */
+
+/*
+ * A container type nested inside a container (list<list<i32>>,
+ * map<string, list<Struct>>, ...): the same description a container field
+ * carries (elem_ttype / val_ttype / struct_index / type_index as in
+ * tgpu_field_desc), for a list/set element or a map value.
+ */
+typedef struct tgpu_type_desc {
+  uint8_t ttype;      /* T_LIST, T_SET or T_MAP */
+  uint8_t elem_ttype;
+  uint8_t val_ttype;
+  uint8_t reserved0;
+  int32_t struct_index;
+  uint32_t type_index;
+  uint32_t reserved1;
+} tgpu_type_desc; /* 16 bytes */
 
 /* Struct flags. */
 enum tgpu_struct_flags {
@@ -249,12 +276,22 @@ int tgpu_layout_compute(tgpu_struct_desc* structs, uint32_t n_structs,
 int tgpu_schema_create(const tgpu_struct_desc* structs, uint32_t n_structs,
                        const tgpu_field_desc* fields, uint32_t n_fields,
                        tgpu_schema** out);
+/* The same with a table of nested container types (types[k] is referenced
+ * as type_index k + 1 by fields and by other types). */
+int tgpu_schema_create_ex(const tgpu_struct_desc* structs, uint32_t n_structs,
+                          const tgpu_field_desc* fields, uint32_t n_fields,
+                          const tgpu_type_desc* types, uint32_t n_types, tgpu_schema** out);
 void tgpu_schema_destroy(tgpu_schema* schema);
 /* sizeof(record) of the root struct. */
 uint32_t tgpu_schema_record_size(const tgpu_schema* schema);
 /* List arena bytes a decode needs per input byte: 0 without lists/sets/
  * maps; 1 Binary / 8 Compact for scalar elements; 4 Binary / 16 Compact
- * when some container holds strings (16-byte spans). */
+ * when some container holds strings (16-byte spans). A schema with
+ * containers of structs or of containers ("nested") reads each record's
+ * containers into a region of its own, scale x [record start, record end)
+ * of the arena, allocated in wire order (8-byte aligned); its scale bounds
+ * element bytes per wire byte (e.g. sizeof(struct) for a list of structs,
+ * as an element struct can be a single STOP byte on the wire). */
 uint32_t tgpu_schema_arena_scale(const tgpu_schema* schema, int protocol);
 
 /* Canonical wire length of every record if it is fixed for `protocol`

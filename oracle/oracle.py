@@ -49,6 +49,15 @@ def lib():
         L.oracle_decode_batch.argtypes = [P, U32, P, U32, I32, P, U64, P, U64, P, P, U64,
                                           ctypes.POINTER(Limits), ctypes.POINTER(Status),
                                           ctypes.POINTER(U64), ctypes.POINTER(U64)]
+        L.oracle_encode_batch_ex.restype = I32
+        L.oracle_encode_batch_ex.argtypes = [P, U32, P, U32, P, U32, I32, P, U64, P, P, P, U64, P,
+                                             ctypes.POINTER(Status), ctypes.POINTER(U64)]
+        L.oracle_decode_batch_ex.restype = I32
+        L.oracle_decode_batch_ex.argtypes = [P, U32, P, U32, P, U32, I32, P, U64, P, U64, P, P,
+                                             U64, ctypes.POINTER(Limits), ctypes.POINTER(Status),
+                                             ctypes.POINTER(U64), ctypes.POINTER(U64)]
+        L.oracle_arena_scale.restype = U32
+        L.oracle_arena_scale.argtypes = [P, U32, P, U32, P, U32, I32]
         L.oracle_record_length.restype = ctypes.c_int64
         L.oracle_record_length.argtypes = [I32, P, U64, U64, ctypes.c_int32, ctypes.c_int32]
         L.oracle_read_varint.restype = I32
@@ -96,6 +105,7 @@ def _u8(b):
 def encode(schema, protocol, records, n, string_base=None, list_base=None, cap=None):
     """Returns (status, wire bytes, offsets[n+1])."""
     structs, ns, fields, nf = schema.descriptors()
+    types, nt = schema.type_descriptors()
     rec = _u8(records)
     sb = _u8(string_base) if string_base is not None else np.zeros(1, np.uint8)
     lb = _u8(list_base) if list_base is not None else np.zeros(1, np.uint8)
@@ -103,41 +113,49 @@ def encode(schema, protocol, records, n, string_base=None, list_base=None, cap=N
         # first pass: size only
         offs = np.zeros(n + 1, np.uint64)
         st, size = Status(), ctypes.c_uint64()
-        lib().oracle_encode_batch(ctypes.addressof(structs), ns, ctypes.addressof(fields), nf,
-                                  protocol, _p(rec), n, _p(sb), _p(lb), None, 0, _p(offs),
-                                  ctypes.byref(st), ctypes.byref(size))
+        lib().oracle_encode_batch_ex(ctypes.addressof(structs), ns, ctypes.addressof(fields), nf,
+                                     ctypes.addressof(types), nt, protocol, _p(rec), n, _p(sb),
+                                     _p(lb), None, 0, _p(offs), ctypes.byref(st),
+                                     ctypes.byref(size))
         if st.code:
             return st, b"", offs
         cap = size.value
     out = np.zeros(max(cap, 1), np.uint8)
     offs = np.zeros(n + 1, np.uint64)
     st, size = Status(), ctypes.c_uint64()
-    lib().oracle_encode_batch(ctypes.addressof(structs), ns, ctypes.addressof(fields), nf,
-                              protocol, _p(rec), n, _p(sb), _p(lb), _p(out), cap, _p(offs),
-                              ctypes.byref(st), ctypes.byref(size))
+    lib().oracle_encode_batch_ex(ctypes.addressof(structs), ns, ctypes.addressof(fields), nf,
+                                 ctypes.addressof(types), nt, protocol, _p(rec), n, _p(sb),
+                                 _p(lb), _p(out), cap, _p(offs), ctypes.byref(st),
+                                 ctypes.byref(size))
     return st, out[: size.value].tobytes(), offs
 
 
 def decode(schema, protocol, wire, n, offsets=None, limits=None, arena_cap=None):
     """Returns (status, records ndarray[u8], arena ndarray[u8], n_decoded, consumed)."""
     structs, ns, fields, nf = schema.descriptors()
+    types, nt = schema.type_descriptors()
     w = _u8(wire)
     rec = np.zeros(max(n * schema.record_size, 1), np.uint8)
     if arena_cap is None:
-        str_elems = any(f.ttype in (13, 14, 15) and (f.elem_ttype == 11 or
-                                                      (f.ttype == 13 and f.val_ttype == 11))
-                        for st_ in schema.structs for f in st_.fields)
-        arena_cap = w.size * ((4 if protocol == 0 else 16) if str_elems else
-                              (1 if protocol == 0 else 8))
+        arena_cap = w.size * arena_scale(schema, protocol)
     arena = np.zeros(max(arena_cap, 1), np.uint8)
     offs = None if offsets is None else np.ascontiguousarray(offsets, dtype=np.uint64)
     lim = Limits(*limits) if limits is not None else None
     st, nd, cons = Status(), ctypes.c_uint64(), ctypes.c_uint64()
-    lib().oracle_decode_batch(ctypes.addressof(structs), ns, ctypes.addressof(fields), nf,
-                              protocol, _p(w), w.size, _p(offs), n, _p(rec), _p(arena),
+    lib().oracle_decode_batch_ex(ctypes.addressof(structs), ns, ctypes.addressof(fields), nf,
+                                 ctypes.addressof(types), nt,
+                                 protocol, _p(w), w.size, _p(offs), n, _p(rec), _p(arena),
                               arena_cap, ctypes.byref(lim) if lim else None, ctypes.byref(st),
                               ctypes.byref(nd), ctypes.byref(cons))
     return st, rec, arena, nd.value, cons.value
+
+
+def arena_scale(schema, protocol):
+    """List arena bytes per input byte (tgpu_schema_arena_scale restated)."""
+    structs, ns, fields, nf = schema.descriptors()
+    types, nt = schema.type_descriptors()
+    return lib().oracle_arena_scale(ctypes.addressof(structs), ns, ctypes.addressof(fields), nf,
+                                    ctypes.addressof(types), nt, protocol)
 
 
 def record_length(protocol, buf, pos=0, max_depth=12000, height=0):

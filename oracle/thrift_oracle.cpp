@@ -8,6 +8,7 @@
 #include "thrift_oracle.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -116,7 +117,27 @@ struct Schema {
   uint32_t ns;
   const tgpu_field_desc* f;
   uint32_t nf;
+  const tgpu_type_desc* t = nullptr;  // nested container types (type_index k -> t[k-1])
+  uint32_t nt = 0;
 };
+
+// A container's element (list/set) or key/value (map) types, from a field or
+// a nested type (TableBasedForwardTypes.h:37-93 ListFieldExt / MapFieldExt).
+struct CT {
+  uint8_t ttype, elem, val;
+  int32_t si;   // struct of T_STRUCT elements / values
+  uint32_t ti;  // 1 + nested type of container elements / values
+};
+CT ct_of(const tgpu_field_desc& f) {
+  return CT{f.ttype, f.elem_ttype, f.val_ttype, f.struct_index, f.type_index};
+}
+CT ct_node(const Schema& sc, uint32_t ti) {
+  const tgpu_type_desc& t = sc.t[ti - 1];
+  return CT{t.ttype, t.elem_ttype, t.val_ttype, t.struct_index, t.type_index};
+}
+bool is_container_t(uint8_t t) {
+  return t == TGPU_T_LIST || t == TGPU_T_SET || t == TGPU_T_MAP;
+}
 
 bool is_scalar(uint8_t t) {
   switch (t) {
@@ -528,20 +549,82 @@ struct DecodeCtx {
   uint8_t* arena;
   uint64_t arena_cap;
   uint64_t scale;  // arena bytes per wire byte: 1/8, or 4/16 with string elements
+  // nested schemas: each record's containers are allocated in wire order
+  // from scale x its start, 8-byte aligned (thrift_gpu.h
+  // tgpu_schema_arena_scale); otherwise scale x the first element's position
+  bool regions = false;
+  uint64_t bump = 0;
+  uint64_t alloc(uint64_t first_elem_pos, uint64_t bytes) {
+    if (!regions) return scale * first_elem_pos;
+    const uint64_t o = bump;
+    bump = (bump + bytes + 7) & ~7ull;
+    return o;
+  }
 };
 
 bool has_string_elems(const Schema& sc) {
-  for (uint32_t k = 0; k < sc.nf; ++k) {
-    const tgpu_field_desc& f = sc.f[k];
-    const bool container = f.ttype == TGPU_T_LIST || f.ttype == TGPU_T_SET || f.ttype == TGPU_T_MAP;
-    if (container && (f.elem_ttype == TGPU_T_STRING ||
-                      (f.ttype == TGPU_T_MAP && f.val_ttype == TGPU_T_STRING)))
-      return true;
-  }
+  auto se = [](uint8_t t, uint8_t e, uint8_t v) {
+    return is_container_t(t) && (e == TGPU_T_STRING || (t == TGPU_T_MAP && v == TGPU_T_STRING));
+  };
+  for (uint32_t k = 0; k < sc.nf; ++k)
+    if (se(sc.f[k].ttype, sc.f[k].elem_ttype, sc.f[k].val_ttype)) return true;
+  for (uint32_t k = 0; k < sc.nt; ++k)
+    if (se(sc.t[k].ttype, sc.t[k].elem_ttype, sc.t[k].val_ttype)) return true;
   return false;
 }
 
-uint32_t elem_size(uint8_t t) { return t == TGPU_T_STRING ? 16 : scalar_size(t); }
+// Scalars in native layout; strings and containers as 16-byte spans.
+uint32_t elem_size(uint8_t t) {
+  return (t == TGPU_T_STRING || is_container_t(t)) ? 16 : scalar_size(t);
+}
+uint32_t slot_size(const Schema& sc, uint8_t t, int32_t si) {
+  return t == TGPU_T_STRUCT ? sc.s[si].size : elem_size(t);
+}
+bool is_complex_t(uint8_t t) { return t == TGPU_T_STRUCT || is_container_t(t); }
+
+// ---- arena regions of nested schemas -----------------------------------------
+// Every arena byte of a record is charged to wire bytes of its own: an
+// element's slot to the element's own bytes (a struct element can be one
+// STOP byte), a container's alignment padding (<= 7) to its header. The scale
+// is the largest bytes-per-wire-byte ratio of the schema's element kinds,
+// at least 8, rounded up to a multiple of 8.
+uint32_t min_wire(uint8_t t, bool compact) {
+  switch (t) {
+    case TGPU_T_BOOL: case TGPU_T_BYTE: return 1;
+    case TGPU_T_I16: return compact ? 1 : 2;
+    case TGPU_T_I32: return compact ? 1 : 4;
+    case TGPU_T_I64: return compact ? 1 : 8;
+    case TGPU_T_FLOAT: return 4;
+    case TGPU_T_DOUBLE: return 8;
+    case TGPU_T_STRING: return compact ? 1 : 4;
+    case TGPU_T_LIST: case TGPU_T_SET: return compact ? 1 : 5;
+    case TGPU_T_MAP: return compact ? 1 : 6;
+    default: return 1;
+  }
+}
+bool nested_schema(const Schema& sc) {
+  auto nested = [](uint8_t t, uint8_t e, uint8_t v) {
+    return is_container_t(t) && is_complex_t(t == TGPU_T_MAP ? v : e);
+  };
+  for (uint32_t k = 0; k < sc.nf; ++k)
+    if (nested(sc.f[k].ttype, sc.f[k].elem_ttype, sc.f[k].val_ttype)) return true;
+  return false;
+}
+void ratio_of(const Schema& sc, const CT& c, bool compact, double& ratio) {
+  const bool is_map = c.ttype == TGPU_T_MAP;
+  const uint8_t v = is_map ? c.val : c.elem;
+  const double kb = is_map ? elem_size(c.elem) : 0, kw = is_map ? min_wire(c.elem, compact) : 0;
+  const double vb = slot_size(sc, v, c.si) + (is_container_t(v) ? 7 : 0);
+  ratio = std::max(ratio, (kb + vb) / (kw + min_wire(v, compact)));
+  ratio = std::max(ratio, 7.0 / min_wire(c.ttype, compact));
+  if (is_container_t(v)) ratio_of(sc, ct_node(sc, c.ti), compact, ratio);
+}
+uint32_t region_scale(const Schema& sc, bool compact) {
+  double ratio = 8.0;
+  for (uint32_t k = 0; k < sc.nf; ++k)
+    if (is_container_t(sc.f[k].ttype)) ratio_of(sc, ct_of(sc.f[k]), compact, ratio);
+  return ((uint32_t)std::ceil(ratio) + 7) & ~7u;
+}
 
 // A container element: a scalar, or a string as a span into the stream.
 template <class R>
@@ -554,7 +637,26 @@ void readElem(R& r, uint8_t t, uint8_t* dst) {
 }
 
 template <class R>
-void readList(R& r, const tgpu_field_desc& f, uint8_t* member, DecodeCtx& dc) {
+void readStruct(R& r, uint32_t si, uint8_t* obj, DecodeCtx& dc);
+template <class R>
+void readContainer(R& r, const CT& c, uint8_t* member, DecodeCtx& dc);
+
+inline void put_span(uint8_t* m, uint64_t off, uint32_t len) {
+  const tgpu_span sp{len ? off : 0, len, 0};
+  std::memcpy(m, &sp, sizeof(sp));
+}
+
+// A list/set element or map value of type t (struct si / nested type ti)
+// read into its slot.
+template <class R>
+void readValue(R& r, uint8_t t, int32_t si, uint32_t ti, uint8_t* dst, DecodeCtx& dc) {
+  if (t == TGPU_T_STRUCT) readStruct(r, (uint32_t)si, dst, dc);
+  else if (is_container_t(t)) readContainer(r, ct_node(*dc.sc, ti), dst, dc);
+  else readElem(r, t, dst);
+}
+
+template <class R>
+void readList(R& r, const CT& f, uint8_t* member, DecodeCtx& dc) {
   // protocol_methods<list>::read (protocol_methods.h:389-467). The member is
   // reset to empty first (deserialize_field.whisker:44-47).
   tgpu_span span{0, 0, 0};
@@ -562,12 +664,33 @@ void readList(R& r, const tgpu_field_desc& f, uint8_t* member, DecodeCtx& dc) {
   uint8_t reported;
   int32_t n;
   r.readListBegin(reported, n);
-  if (reported != f.elem_ttype) {
+  if (reported != f.elem) {
     r.skip_n((uint32_t)n, &reported, 1, 0);
+  } else if (is_complex_t(f.elem)) {
+    // structs / containers as elements: reserve + emplace_back_default +
+    // read per element (:374-386,458-461) — the list holds the elements
+    // read plus the failing one; a set inserts an element once it is read
+    // (EncodeHelpers.h:248-259)
+    if (!r.c.canAdvance((uint64_t)(uint32_t)n)) fail(TGPU_ERR_TRUNCATED, r.c.pos);
+    const uint32_t es = slot_size(*dc.sc, f.elem, f.si);
+    if (n > 0) {
+      if (!dc.arena) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
+      const uint64_t bytes = (uint64_t)(uint32_t)n * es;
+      const uint64_t aoff = dc.alloc(r.c.pos, bytes);
+      if (aoff + bytes > dc.arena_cap) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
+      const bool is_set = f.ttype == TGPU_T_SET;
+      for (int32_t i = 0; i < n; ++i) {
+        uint8_t* el = dc.arena + aoff + (uint64_t)i * es;
+        std::memset(el, 0, es);
+        if (!is_set) put_span(member, aoff, (uint32_t)(i + 1));
+        readValue(r, f.elem, f.si, f.ti, el, dc);
+        if (is_set) put_span(member, aoff, (uint32_t)(i + 1));
+      }
+    }
   } else {
     if (!r.c.canAdvance((uint64_t)(uint32_t)n)) fail(TGPU_ERR_TRUNCATED, r.c.pos);  // canReadNElements
-    const uint32_t es = elem_size(f.elem_ttype);
-    const uint64_t aoff = dc.scale * r.c.pos;
+    const uint32_t es = elem_size(f.elem);
+    const uint64_t aoff = n > 0 ? dc.alloc(r.c.pos, (uint64_t)(uint32_t)n * es) : 0;
     if (n > 0) {
       if (!dc.arena) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
       // resizeWithoutInitialization(out, n) happens before the element reads
@@ -582,7 +705,7 @@ void readList(R& r, const tgpu_field_desc& f, uint8_t* member, DecodeCtx& dc) {
         // holds an element that was read when sized as documented)
         const uint64_t at = aoff + (uint64_t)i * es;
         uint8_t tmp[16];
-        readElem(r, f.elem_ttype, tmp);
+        readElem(r, f.elem, tmp);
         if (at + es > dc.arena_cap) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
         std::memcpy(dc.arena + at, tmp, es);
       }
@@ -593,7 +716,7 @@ void readList(R& r, const tgpu_field_desc& f, uint8_t* member, DecodeCtx& dc) {
         span.length = (uint32_t)i;
         if (!i) span.offset = 0;
         std::memcpy(member, &span, sizeof(span));
-      } else if (f.elem_ttype == TGPU_T_STRING) {
+      } else if (f.elem == TGPU_T_STRING) {
         // non-trivial elements: reserve + emplace_back_default + read
         // (protocol_methods.h:374-386,458-461): the failing element is in
         // the list, empty
@@ -616,30 +739,46 @@ void readList(R& r, const tgpu_field_desc& f, uint8_t* member, DecodeCtx& dc) {
 }
 
 template <class R>
-void readMap(R& r, const tgpu_field_desc& f, uint8_t* member, DecodeCtx& dc) {
+void readMap(R& r, const CT& f, uint8_t* member, DecodeCtx& dc) {
   // protocol_methods<map>::read (protocol_methods.h:640-677); the member is
   // reset first (deserialize_field.whisker:44-47). Pairs in wire order, packed
-  // {key, value} at the arena offset. deserialize_known_length_map
-  // (EncodeHelpers.h:188-205) inserts a pair only once both reads succeeded:
-  // a failing map keeps the complete pairs before the failure.
+  // {key, value}. deserialize_known_length_map (EncodeHelpers.h:188-205)
+  // inserts a pair only once both reads succeeded: a failing map keeps the
+  // complete pairs before the failure.
   tgpu_span span{0, 0, 0};
   std::memcpy(member, &span, sizeof(span));
   uint8_t kv[2];
   int32_t n;
   r.readMapBegin(kv[0], kv[1], n);
-  if (n > 0 && (kv[0] != f.elem_ttype || kv[1] != f.val_ttype)) {
+  if (n > 0 && (kv[0] != f.elem || kv[1] != f.val)) {
     r.skip_n((uint32_t)n, kv, 2, 0);
+  } else if (is_complex_t(f.val)) {
+    if (!r.c.canAdvance((uint64_t)(uint32_t)n * 2)) fail(TGPU_ERR_TRUNCATED, r.c.pos);
+    const uint32_t ks = elem_size(f.elem), ps = ks + slot_size(*dc.sc, f.val, f.si);
+    if (n > 0) {
+      if (!dc.arena) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
+      const uint64_t bytes = (uint64_t)(uint32_t)n * ps;
+      const uint64_t aoff = dc.alloc(r.c.pos, bytes);
+      if (aoff + bytes > dc.arena_cap) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
+      for (int32_t i = 0; i < n; ++i) {
+        uint8_t* pr = dc.arena + aoff + (uint64_t)i * ps;
+        std::memset(pr, 0, ps);
+        readElem(r, f.elem, pr);
+        readValue(r, f.val, f.si, f.ti, pr + ks, dc);
+        put_span(member, aoff, (uint32_t)(i + 1));
+      }
+    }
   } else {
     if (!r.c.canAdvance((uint64_t)(uint32_t)n * 2)) fail(TGPU_ERR_TRUNCATED, r.c.pos);
-    const uint32_t ks = elem_size(f.elem_ttype), ps = ks + elem_size(f.val_ttype);
-    const uint64_t aoff = dc.scale * r.c.pos;
+    const uint32_t ks = elem_size(f.elem), ps = ks + elem_size(f.val);
+    const uint64_t aoff = n > 0 ? dc.alloc(r.c.pos, (uint64_t)(uint32_t)n * ps) : 0;
     if (n > 0 && !dc.arena) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
     int32_t i = 0;
     try {
       for (; i < n; ++i) {
         uint8_t pr[32];
-        readElem(r, f.elem_ttype, pr);
-        readElem(r, f.val_ttype, pr + ks);
+        readElem(r, f.elem, pr);
+        readElem(r, f.val, pr + ks);
         const uint64_t at = aoff + (uint64_t)i * ps;
         if (at + ps > dc.arena_cap) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
         std::memcpy(dc.arena + at, pr, ps);
@@ -657,6 +796,12 @@ void readMap(R& r, const tgpu_field_desc& f, uint8_t* member, DecodeCtx& dc) {
     }
   }
   r.height.ascend();  // readMapEnd
+}
+
+template <class R>
+void readContainer(R& r, const CT& c, uint8_t* member, DecodeCtx& dc) {
+  if (c.ttype == TGPU_T_MAP) readMap(r, c, member, dc);
+  else readList(r, c, member, dc);
 }
 
 template <class R>
@@ -705,10 +850,8 @@ void readStruct(R& r, uint32_t si, uint8_t* obj, DecodeCtx& dc) {
       std::memcpy(m, &sp, sizeof(sp));
     } else if (f->ttype == TGPU_T_STRUCT) {
       readStruct(r, (uint32_t)f->struct_index, m, dc);  // merges into member
-    } else if (f->ttype == TGPU_T_LIST || f->ttype == TGPU_T_SET) {
-      readList(r, *f, m, dc);
-    } else if (f->ttype == TGPU_T_MAP) {
-      readMap(r, *f, m, dc);
+    } else if (is_container_t(f->ttype)) {
+      readContainer(r, ct_of(*f), m, dc);
     }
     obj[f->isset_offset] = 1;  // __isset.set(idx, true)
   }
@@ -725,6 +868,10 @@ int decode_impl(const Schema& sc, const uint8_t* in, uint64_t in_len,
                 tgpu_status* st, uint64_t* n_dec, uint64_t* consumed) {
   DecodeCtx dc{&sc, arena, arena_cap,
                has_string_elems(sc) ? (R::kArenaScale == 1 ? 4u : 16u) : R::kArenaScale};
+  if (nested_schema(sc)) {
+    dc.regions = true;
+    dc.scale = region_scale(sc, R::kArenaScale != 1);
+  }
   uint64_t pos = offsets ? offsets[0] : 0;
   const uint32_t rs = sc.s[0].size;
   for (uint64_t i = 0; i < n; ++i) {
@@ -735,6 +882,7 @@ int decode_impl(const Schema& sc, const uint8_t* in, uint64_t in_len,
     r.c = Cursor{in, start, in_len};
     r.lim = lim;
     r.height.h = lim.initial_height();
+    dc.bump = dc.scale * start;  // the record's region (nested schemas)
     try {
       readStruct(r, 0, rec, dc);
     } catch (const OErr& e) {
@@ -837,14 +985,37 @@ struct BinaryWriter {
       default: s.putBE(ld<uint64_t>(p), 8); break;
     }
   }
-  // encodeMapElements: key then value per pair, in the given order
-  // (protocol_methods.h:693-701).
-  void pairs(const EncodeCtx& ec, const tgpu_field_desc& f, const tgpu_span& sp) {
-    const uint32_t ks = elem_size(f.elem_ttype), ps = ks + elem_size(f.val_ttype);
+  // writeMapBegin / writeListBegin (BinaryProtocol-inl.h:69-96)
+  void header(const CT& c, uint32_t n) {
+    if (c.ttype == TGPU_T_MAP) {
+      s.put(c.elem);
+      s.put(c.val);
+    } else {
+      s.put(c.elem);
+    }
+    s.putBE(n, 4);
+  }
+  // a list/set element or map value: a struct (the generated write), a
+  // container, or a scalar / string
+  void value(const EncodeCtx& ec, uint8_t t, int32_t si, uint32_t ti, const uint8_t* p) {
+    if (t == TGPU_T_STRUCT) structure(ec, (uint32_t)si, p);
+    else if (is_container_t(t)) container(ec, ct_node(*ec.sc, ti), p);
+    else elem(ec, t, p);
+  }
+  // protocol_methods<list/set/map>::write (protocol_methods.h:469-489,
+  // 693-701): header, then the elements (key then value per pair) in the
+  // given order
+  void container(const EncodeCtx& ec, const CT& c, const uint8_t* m) {
+    const tgpu_span sp = ld<tgpu_span>(m);
+    if (sp.length > 0x7fffffffu) fail(TGPU_ERR_WRITE_SIZE_LIMIT, s.pos);  // checked_container_size
+    header(c, sp.length);
+    const bool is_map = c.ttype == TGPU_T_MAP;
+    const uint8_t v = is_map ? c.val : c.elem;
+    const uint32_t ks = is_map ? elem_size(c.elem) : 0, ps = ks + slot_size(*ec.sc, v, c.si);
     const uint8_t* e = ec.lbase + sp.offset;
     for (uint32_t i = 0; i < sp.length; ++i) {
-      elem(ec, f.elem_ttype, e + (uint64_t)i * ps);
-      elem(ec, f.val_ttype, e + (uint64_t)i * ps + ks);
+      if (is_map) elem(ec, c.elem, e + (uint64_t)i * ps);
+      value(ec, v, c.si, c.ti, e + (uint64_t)i * ps + ks);
     }
   }
   // a container element: scalar, or a string span into string_base
@@ -876,21 +1047,8 @@ struct BinaryWriter {
         s.putBytes(ec.sbase + sp.offset, sp.length);
       } else if (f.ttype == TGPU_T_STRUCT) {
         structure(ec, (uint32_t)f.struct_index, m);
-      } else if (f.ttype == TGPU_T_MAP) {  // writeMapBegin (BinaryProtocol-inl.h:69-80)
-        const tgpu_span sp = ld<tgpu_span>(m);
-        if (sp.length > 0x7fffffffu) fail(TGPU_ERR_WRITE_SIZE_LIMIT, s.pos);  // checked_container_size
-        s.put(f.elem_ttype);
-        s.put(f.val_ttype);
-        s.putBE(sp.length, 4);
-        pairs(ec, f, sp);
-      } else {  // list/set: writeListBegin + writeArithmeticVector (BinaryProtocol.cpp:95-117)
-        const tgpu_span sp = ld<tgpu_span>(m);
-        if (sp.length > 0x7fffffffu) fail(TGPU_ERR_WRITE_SIZE_LIMIT, s.pos);
-        s.put(f.elem_ttype);
-        s.putBE(sp.length, 4);
-        const uint32_t es = elem_size(f.elem_ttype);
-        for (uint32_t i = 0; i < sp.length; ++i)
-          elem(ec, f.elem_ttype, ec.lbase + sp.offset + (uint64_t)i * es);
+      } else {  // list / set / map
+        container(ec, ct_of(f), m);
       }
     }
     s.put(TGPU_T_STOP);  // writeFieldStop
@@ -925,14 +1083,46 @@ struct CompactWriterT {
         break;
     }
   }
-  // encodeMapElements: key then value per pair, in the given order
-  // (protocol_methods.h:693-701).
-  void pairs(const EncodeCtx& ec, const tgpu_field_desc& f, const tgpu_span& sp) {
-    const uint32_t ks = elem_size(f.elem_ttype), ps = ks + elem_size(f.val_ttype);
+  // writeMapBegin (:182-201) / writeCollectionBegin (:209-224)
+  void header(const CT& c, uint32_t n) {
+    if (c.ttype == TGPU_T_MAP) {
+      if (n == 0) {
+        s.put(0);
+      } else {
+        s.varint(n);
+        s.put((uint8_t)((ttypeToCType(c.elem) << 4) | ttypeToCType(c.val)));
+      }
+      return;
+    }
+    const uint8_t ct = ttypeToCType(c.elem);
+    if (n <= 14) {
+      s.put((uint8_t)((n << 4) | ct));
+    } else {
+      s.put((uint8_t)(0xf0 | ct));
+      s.varint(n);
+    }
+  }
+  // a list/set element or map value: a struct (the generated write), a
+  // container, or a scalar / string
+  void value(const EncodeCtx& ec, uint8_t t, int32_t si, uint32_t ti, const uint8_t* p) {
+    if (t == TGPU_T_STRUCT) structure(ec, (uint32_t)si, p);
+    else if (is_container_t(t)) container(ec, ct_node(*ec.sc, ti), p);
+    else elem(ec, t, p);
+  }
+  // protocol_methods<list/set/map>::write (protocol_methods.h:469-489,
+  // 693-701): header, then the elements (key then value per pair) in the
+  // given order
+  void container(const EncodeCtx& ec, const CT& c, const uint8_t* m) {
+    const tgpu_span sp = ld<tgpu_span>(m);
+    if (sp.length > 0x7fffffffu) fail(TGPU_ERR_WRITE_SIZE_LIMIT, s.pos);  // checked_container_size
+    header(c, sp.length);
+    const bool is_map = c.ttype == TGPU_T_MAP;
+    const uint8_t v = is_map ? c.val : c.elem;
+    const uint32_t ks = is_map ? elem_size(c.elem) : 0, ps = ks + slot_size(*ec.sc, v, c.si);
     const uint8_t* e = ec.lbase + sp.offset;
     for (uint32_t i = 0; i < sp.length; ++i) {
-      elem(ec, f.elem_ttype, e + (uint64_t)i * ps);
-      elem(ec, f.val_ttype, e + (uint64_t)i * ps + ks);
+      if (is_map) elem(ec, c.elem, e + (uint64_t)i * ps);
+      value(ec, v, c.si, c.ti, e + (uint64_t)i * ps + ks);
     }
   }
   // a container element: scalar, or a string span into string_base
@@ -969,29 +1159,8 @@ struct CompactWriterT {
         s.putBytes(ec.sbase + sp.offset, sp.length);
       } else if (f.ttype == TGPU_T_STRUCT) {
         structure(ec, (uint32_t)f.struct_index, m);
-      } else if (f.ttype == TGPU_T_MAP) {  // writeMapBegin (:182-201)
-        const tgpu_span sp = ld<tgpu_span>(m);
-        if (sp.length > 0x7fffffffu) fail(TGPU_ERR_WRITE_SIZE_LIMIT, s.pos);
-        if (sp.length == 0) {
-          s.put(0);
-        } else {
-          s.varint(sp.length);
-          s.put((uint8_t)((ttypeToCType(f.elem_ttype) << 4) | ttypeToCType(f.val_ttype)));
-        }
-        pairs(ec, f, sp);
-      } else {  // writeCollectionBegin (:209-224)
-        const tgpu_span sp = ld<tgpu_span>(m);
-        if (sp.length > 0x7fffffffu) fail(TGPU_ERR_WRITE_SIZE_LIMIT, s.pos);
-        const uint8_t ct = ttypeToCType(f.elem_ttype);
-        if (sp.length <= 14) {
-          s.put((uint8_t)((sp.length << 4) | ct));
-        } else {
-          s.put((uint8_t)(0xf0 | ct));
-          s.varint(sp.length);
-        }
-        const uint32_t es = elem_size(f.elem_ttype);
-        for (uint32_t i = 0; i < sp.length; ++i)
-          elem(ec, f.elem_ttype, ec.lbase + sp.offset + (uint64_t)i * es);
+      } else {  // list / set / map
+        container(ec, ct_of(f), m);
       }
     }
     s.put(0);  // writeFieldStop
@@ -1064,13 +1233,14 @@ inline uint64_t load_be64(const uint8_t* p) {
 // ================================================================ C entry ===
 extern "C" {
 
-int oracle_encode_batch(const tgpu_struct_desc* structs, uint32_t n_structs,
+int oracle_encode_batch_ex(const tgpu_struct_desc* structs, uint32_t n_structs,
                         const tgpu_field_desc* fields, uint32_t n_fields,
+                        const tgpu_type_desc* types, uint32_t n_types,
                         int protocol, const void* records, uint64_t n_records,
                         const void* string_base, const void* list_base,
                         void* out, uint64_t out_capacity, uint64_t* out_offsets,
                         tgpu_status* st, uint64_t* out_size) {
-  Schema sc{structs, n_structs, fields, n_fields};
+  Schema sc{structs, n_structs, fields, n_fields, types, n_types};
   auto rec = (const uint8_t*)records;
   auto sb = (const uint8_t*)string_base;
   auto lb = (const uint8_t*)list_base;
@@ -1087,15 +1257,27 @@ int oracle_encode_batch(const tgpu_struct_desc* structs, uint32_t n_structs,
   return TGPU_ERR_INVALID_ARGUMENT;
 }
 
-int oracle_decode_batch(const tgpu_struct_desc* structs, uint32_t n_structs,
+int oracle_encode_batch(const tgpu_struct_desc* structs, uint32_t n_structs,
                         const tgpu_field_desc* fields, uint32_t n_fields,
+                        int protocol, const void* records, uint64_t n_records,
+                        const void* string_base, const void* list_base,
+                        void* out, uint64_t out_capacity, uint64_t* out_offsets,
+                        tgpu_status* st, uint64_t* out_size) {
+  return oracle_encode_batch_ex(structs, n_structs, fields, n_fields, nullptr, 0, protocol,
+                                records, n_records, string_base, list_base, out, out_capacity,
+                                out_offsets, st, out_size);
+}
+
+int oracle_decode_batch_ex(const tgpu_struct_desc* structs, uint32_t n_structs,
+                        const tgpu_field_desc* fields, uint32_t n_fields,
+                        const tgpu_type_desc* types, uint32_t n_types,
                         int protocol, const void* in, uint64_t in_len,
                         const uint64_t* offsets, uint64_t n_records,
                         void* records, void* list_arena,
                         uint64_t list_arena_capacity, const tgpu_limits* limits,
                         tgpu_status* st, uint64_t* n_decoded,
                         uint64_t* consumed) {
-  Schema sc{structs, n_structs, fields, n_fields};
+  Schema sc{structs, n_structs, fields, n_fields, types, n_types};
   const Limits lim = to_limits(limits);
   auto p = (const uint8_t*)in;
   if (protocol == TGPU_PROTOCOL_BINARY)
@@ -1115,6 +1297,33 @@ int oracle_decode_batch(const tgpu_struct_desc* structs, uint32_t n_structs,
                                         consumed);
   set_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
   return TGPU_ERR_INVALID_ARGUMENT;
+}
+
+int oracle_decode_batch(const tgpu_struct_desc* structs, uint32_t n_structs,
+                        const tgpu_field_desc* fields, uint32_t n_fields,
+                        int protocol, const void* in, uint64_t in_len,
+                        const uint64_t* offsets, uint64_t n_records,
+                        void* records, void* list_arena,
+                        uint64_t list_arena_capacity, const tgpu_limits* limits,
+                        tgpu_status* st, uint64_t* n_decoded,
+                        uint64_t* consumed) {
+  return oracle_decode_batch_ex(structs, n_structs, fields, n_fields, nullptr, 0, protocol, in,
+                                in_len, offsets, n_records, records, list_arena,
+                                list_arena_capacity, limits, st, n_decoded, consumed);
+}
+
+// Arena bytes per input byte a decode of this schema needs (the library's
+// tgpu_schema_arena_scale, restated).
+uint32_t oracle_arena_scale(const tgpu_struct_desc* structs, uint32_t n_structs,
+                            const tgpu_field_desc* fields, uint32_t n_fields,
+                            const tgpu_type_desc* types, uint32_t n_types, int protocol) {
+  Schema sc{structs, n_structs, fields, n_fields, types, n_types};
+  const bool bin = protocol == TGPU_PROTOCOL_BINARY;
+  bool lists = false;
+  for (uint32_t k = 0; k < n_fields; ++k) lists |= is_container_t(fields[k].ttype);
+  if (!lists) return 0;
+  if (nested_schema(sc)) return region_scale(sc, !bin);
+  return has_string_elems(sc) ? (bin ? 4 : 16) : (bin ? 1 : 8);
 }
 
 int64_t oracle_record_length(int protocol, const void* in, uint64_t in_len,

@@ -26,6 +26,22 @@ extern "C" {
 #endif
 
 /* Table-driven encode of n records (same layout/span rules as the C-ABI). */
+int oracle_encode_batch_ex(const tgpu_struct_desc* structs, uint32_t n_structs,
+                           const tgpu_field_desc* fields, uint32_t n_fields,
+                           const tgpu_type_desc* types, uint32_t n_types, int protocol,
+                           const void* records, uint64_t n_records, const void* string_base,
+                           const void* list_base, void* out, uint64_t out_capacity,
+                           uint64_t* out_offsets, tgpu_status* st, uint64_t* out_size);
+int oracle_decode_batch_ex(const tgpu_struct_desc* structs, uint32_t n_structs,
+                           const tgpu_field_desc* fields, uint32_t n_fields,
+                           const tgpu_type_desc* types, uint32_t n_types, int protocol,
+                           const void* in, uint64_t in_len, const uint64_t* offsets,
+                           uint64_t n_records, void* records, void* list_arena,
+                           uint64_t list_arena_capacity, const tgpu_limits* limits,
+                           tgpu_status* st, uint64_t* n_decoded, uint64_t* consumed);
+uint32_t oracle_arena_scale(const tgpu_struct_desc* structs, uint32_t n_structs,
+                            const tgpu_field_desc* fields, uint32_t n_fields,
+                            const tgpu_type_desc* types, uint32_t n_types, int protocol);
 int oracle_encode_batch(const tgpu_struct_desc* structs, uint32_t n_structs,
                         const tgpu_field_desc* fields, uint32_t n_fields,
                         int protocol, const void* records, uint64_t n_records,
