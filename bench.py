@@ -650,6 +650,7 @@ def irregular(wl, dev, reps=3):
     res = {"records": n}
 
     def timed(name, wire, offsets=None, bytes_=None):
+        print("irregular %s: start" % name, file=sys.stderr, flush=True)
         best = None
         for _ in range(reps + 1):
             wl.back.zero_()

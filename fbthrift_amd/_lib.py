@@ -23,7 +23,8 @@ CODES = {
     0: "OK", 1: "UNDERFLOW", 2: "INVALID_VARINT", 3: "BOOL_VALUE",
     4: "INVALID_SKIP_TYPE", 5: "TRUNCATED", 6: "NEGATIVE_SIZE", 7: "SIZE_LIMIT",
     8: "DEPTH_LIMIT", 9: "BAD_TYPE", 10: "INVALID_BOOL_WRITE",
-    11: "WRITE_SIZE_LIMIT", 12: "UNION_MISSING_STOP", 20: "INDEX_MISMATCH", 21: "OUTPUT_OVERFLOW",
+    11: "WRITE_SIZE_LIMIT", 12: "UNION_MISSING_STOP", 13: "MISSING_REQUIRED_FIELD",
+    20: "INDEX_MISMATCH", 21: "OUTPUT_OVERFLOW",
     22: "UNSUPPORTED", 23: "INVALID_ARGUMENT", 24: "HIP",
 }
 CODE = {v: k for k, v in CODES.items()}

@@ -216,7 +216,8 @@ __global__ __launch_bounds__(256) void index_spec_general_kernel(IndexArgs a) {
   uint8_t* scratch = a.scratch + j * a.rec_size;
   const uint64_t lo = chunk_lo(a, j), hi = chunk_hi(a, j);
   Chain c;
-  a.s2[j] = kNo;
+  uint64_t* starts = a.sst + j * kSpecStarts;
+  starts[0] = kNo;
   if (j == 0 && !a.speculative) {
     chain<P>(a, a.begin, hi, false, scratch, c, nullptr, 0, kNo);
     a.s[0] = a.begin;
@@ -227,14 +228,14 @@ __global__ __launch_bounds__(256) void index_spec_general_kernel(IndexArgs a) {
   const uint64_t w = j == 0 ? a.chunk : a.window;
   const uint64_t last = lo + w < hi ? lo + w : hi;
   for (uint64_t cand = lo; cand < last; ++cand) {
-    if (chain<P>(a, cand, hi, true, scratch, c, nullptr, 0, kNo) && c.code == 0) {
+    if (chain<P>(a, cand, hi, true, scratch, c, starts, kSpecStarts, kNo) && c.code == 0) {
       a.s[j] = cand;
       a.e[j] = c.end;
       a.cnt[j] = c.count;
-      a.s2[j] = c.second;
       return;
     }
   }
+  starts[0] = kNo;
   a.s[j] = kNo;
   a.e[j] = kNo;
   a.cnt[j] = 0;
@@ -245,16 +246,15 @@ __global__ __launch_bounds__(256) void index_spec_general_kernel(IndexArgs a) {
 // that left the canonical form: reordered, unknown or missing fields, as after
 // schema evolution). A candidate inside the record straddling the chunk's
 // start can parse as a record of its own and then run in step with the true
-// records; s2 (the chain's second start) lets the repair pass take such a
-// chain over in O(1) when the true start is its second record.
+// records; the chain's first kSpecStarts starts (sst) let the repair pass
+// take it over in O(1) when the true start is one of them.
 template <int P>
 __global__ __launch_bounds__(256) void index_spec_fallback_kernel(IndexArgs a) {
   const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (j >= a.n_chunks) return;
-  if (a.s[j] != kNo || a.e[j] != kNo) {
-    a.s2[j] = kNo;
-    return;
-  }
+  uint64_t* starts = a.sst + j * kSpecStarts;
+  starts[0] = kNo;
+  if (a.s[j] != kNo || a.e[j] != kNo) return;
   uint8_t* scratch = a.scratch + j * a.rec_size;
   const uint64_t lo = chunk_lo(a, j), hi = chunk_hi(a, j);
   Chain c;
@@ -263,22 +263,21 @@ __global__ __launch_bounds__(256) void index_spec_fallback_kernel(IndexArgs a) {
     a.s[0] = a.begin;
     a.e[0] = c.code ? kErr : c.end;
     a.cnt[0] = c.count;
-    a.s2[0] = kNo;
     return;
   }
   const uint64_t w = j == 0 ? a.chunk : a.window;
   const uint64_t last = lo + w < hi ? lo + w : hi;
   for (uint64_t cand = lo; cand < last; ++cand) {
-    if (chain<P>(a, cand, hi, false, scratch, c, nullptr, 0, kNo) && c.code == 0 && c.count) {
+    if (chain<P>(a, cand, hi, false, scratch, c, starts, kSpecStarts, kNo) && c.code == 0 &&
+        c.count) {
       a.s[j] = cand;
       a.e[j] = c.end;
       a.cnt[j] = c.count;
-      a.s2[j] = c.second;
       a.pf[j] = 0;
       return;
     }
   }
-  a.s2[j] = kNo;
+  starts[0] = kNo;
 }
 
 // ---- LDS tiles (schemas with a program; tgpu_prog_kernels.h) ---------------
@@ -308,14 +307,31 @@ __device__ __forceinline__ bool link_broken(const IndexArgs& a, uint64_t j) {
   return a.s[j] != a.e[j - 1];
 }
 
-__global__ __launch_bounds__(256) void index_flag_kernel(IndexArgs a) {
+__global__ __launch_bounds__(256) void index_flag_kernel(IndexArgs a, int sst_valid) {
   const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j < a.n_chunks) a.base[j] = link_broken(a, j) ? 1 : 0;
+  if (j >= a.n_chunks) return;
+  a.base[j] = link_broken(a, j) ? 1 : 0;
+  if (!sst_valid) a.sst[j * kSpecStarts] = kNo;
 }
 
 __global__ __launch_bounds__(256) void index_list_kernel(IndexArgs a) {
   const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (j < a.n_chunks && link_broken(a, j)) a.bad[a.base[j]] = j;
+}
+
+// The true start T of chunk j is one of its speculated chain's first
+// kSpecStarts starts: the chain from T is the rest of it.
+__device__ __forceinline__ bool take_over(const IndexArgs& a, uint64_t j, uint64_t T) {
+  const uint64_t* st = a.sst + j * kSpecStarts;
+  const uint64_t n = a.cnt[j] < (uint64_t)kSpecStarts ? a.cnt[j] : (uint64_t)kSpecStarts;
+  for (uint64_t m = 1; m < n; ++m) {
+    if (st[m] == T) {
+      a.s[j] = T;
+      a.cnt[j] -= m;
+      return true;
+    }
+  }
+  return false;
 }
 
 // One lane: repair the chain (see header). scal[1] = chunks in effect.
@@ -355,12 +371,10 @@ __global__ void index_fix_kernel(IndexArgs a) {
         a.e[j] = T;
         a.cnt[j] = 0;
         a.pf[j] = 0;
-      } else if (a.s2[j] == T && a.e[j] != kNo && a.e[j] != kErr && a.e[j] != kPartial) {
-        // the speculated chain's first record was a false start inside the
-        // record ending at T; from its second record on it is the true chain
-        a.s[j] = T;
-        a.cnt[j] -= 1;
-        a.s2[j] = kNo;
+      } else if (T > a.s[j] && a.sst[j * kSpecStarts] == a.s[j] && a.e[j] != kNo &&
+                 a.e[j] != kErr && a.e[j] != kPartial && take_over(a, j, T)) {
+        // the speculated chain started with false records inside the record
+        // ending at T; from T on it is the true chain
       } else {
         Chain c;
         chain<P>(a, T, hi, false, scratch, c, nullptr, 0, kNo, 0);
@@ -549,9 +563,13 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
   } else {
     TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_spec_general_kernel<P_>, g, b, 0, stream, a));
   }
-  if (a.prog)
+  // (a speculative range opens at its first program-confirmed start: a
+  // general-reader start there has no predecessor chunk to verify it)
+  if (a.prog && !a.speculative)
     TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_spec_fallback_kernel<P_>, g, b, 0, stream, a));
-  hipLaunchKernelGGL(index_flag_kernel, g, b, 0, stream, a);
+  // sst is written by the general speculation and the fallback only
+  const int sst_valid = !a.prog || !a.speculative;
+  hipLaunchKernelGGL(index_flag_kernel, g, b, 0, stream, a, sst_valid);
   hipError_t e = launch_scan_tiles(a.base, C, a.part, a.scal, nullptr, stream);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(index_list_kernel, g, b, 0, stream, a);

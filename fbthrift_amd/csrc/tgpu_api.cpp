@@ -205,14 +205,18 @@ int validate_struct(const Tables& T, uint32_t si, int depth, SchemaFacts& facts)
   if ((uint64_t)sd.first_field + sd.num_fields > T.nf || sd.size == 0 || sd.align == 0 ||
       sd.size % sd.align)
     return TGPU_ERR_INVALID_ARGUMENT;
-  if (sd.flags & ~(uint32_t)TGPU_STRUCT_UNION) return TGPU_ERR_UNSUPPORTED;
+  if (sd.flags & ~(uint32_t)(TGPU_STRUCT_UNION | TGPU_STRUCT_ENFORCE_REQUIRED))
+    return TGPU_ERR_UNSUPPORTED;
   for (uint32_t k = 0; k < sd.num_fields; ++k) {
     const tgpu_field_desc& fd = T.f[sd.first_field + k];
     if ((sd.flags & TGPU_STRUCT_UNION) && fd.qualifier != TGPU_UNQUALIFIED)
       return TGPU_ERR_UNSUPPORTED;
     for (uint32_t j = 0; j < k; ++j)
       if (T.f[sd.first_field + j].id == fd.id) return TGPU_ERR_INVALID_ARGUMENT;
-    if (fd.qualifier > TGPU_TERSE) return TGPU_ERR_UNSUPPORTED;
+    if (fd.qualifier > TGPU_REQUIRED) return TGPU_ERR_UNSUPPORTED;
+    // required fields are checked through a 64-bit per-struct mask
+    if (fd.qualifier == TGPU_REQUIRED && k >= 64 && (sd.flags & TGPU_STRUCT_ENFORCE_REQUIRED))
+      return TGPU_ERR_UNSUPPORTED;
     // a terse struct's emptiness is its fields' (thrift::empty): not supported
     if (fd.qualifier == TGPU_TERSE && fd.ttype == TGPU_T_STRUCT) return TGPU_ERR_UNSUPPORTED;
     if (fd.isset_offset >= sd.size) return TGPU_ERR_INVALID_ARGUMENT;
@@ -312,7 +316,9 @@ bool build_template(const tgpu_schema& sc, uint32_t si, uint32_t base, FixedTemp
   if (sd.flags & TGPU_STRUCT_UNION) return false;
   for (uint32_t k = 0; k < sd.num_fields; ++k) {
     const tgpu_field_desc& fd = sc.fields[sd.first_field + k];
-    if (fd.qualifier != TGPU_UNQUALIFIED) return false;
+    // a required field is written always and read like an unqualified one;
+    // a canonical record holds every field, so the enforcement never fires
+    if (fd.qualifier != TGPU_UNQUALIFIED && fd.qualifier != TGPU_REQUIRED) return false;
     if (t.n_items >= (uint32_t)kMaxTemplateItems || t.n_isset >= 64) return false;
     TemplateItem it{};
     it.wire_off = (uint16_t)wire;
@@ -386,7 +392,7 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
   int32_t prev = 0;
   for (uint32_t k = 0; k < sd.num_fields; ++k) {
     const tgpu_field_desc& f = sc.fields[sd.first_field + k];
-    if (f.qualifier != TGPU_UNQUALIFIED) return false;
+    if (f.qualifier != TGPU_UNQUALIFIED && f.qualifier != TGPU_REQUIRED) return false;
     const uint32_t member = base + f.member_offset, isset = base + f.isset_offset;
     if (member > 0xfffe || isset > 0xfffe) return false;
     VOp hdr = make_op(VOP_CONST);
@@ -528,6 +534,7 @@ void classify(int code, int32_t* exc, int32_t* tp) {
     case TGPU_ERR_NEGATIVE_SIZE: e = TGPU_EXC_PROTOCOL; t = 2; break;
     case TGPU_ERR_SIZE_LIMIT: case TGPU_ERR_WRITE_SIZE_LIMIT: e = TGPU_EXC_PROTOCOL; t = 3; break;
     case TGPU_ERR_DEPTH_LIMIT: e = TGPU_EXC_PROTOCOL; t = 8; break;
+    case TGPU_ERR_MISSING_REQUIRED_FIELD: e = TGPU_EXC_PROTOCOL; t = 6; break;
     case TGPU_ERR_BAD_TYPE: e = TGPU_EXC_PROTOCOL; t = 0; break;
     case TGPU_ERR_INVALID_BOOL_WRITE: e = TGPU_EXC_ABORT; break;
     default: break;
@@ -699,7 +706,7 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   const uint64_t rs = (x.rec_size + 7) & ~7u;
   const uint64_t parts = scan_tiles_parts(C) + 1;
   const uint64_t lane_words = x.chunk == index_tile_bytes() ? C * index_tile_lanes() : 0;
-  const uint64_t need = 8 * (10 * C + parts + 9) + C * rs + 4 * lane_words;
+  const uint64_t need = 8 * ((9 + kSpecStarts) * C + parts + 9) + C * rs + 4 * lane_words;
   if (need > ctx->index_bytes) {
     if (ctx->d_index) (void)hipFree(ctx->d_index);
     ctx->d_index = nullptr;
@@ -721,7 +728,7 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   x.scratch = (uint8_t*)(w + 8 * C + parts + 8);
   x.lanes = (uint32_t*)(x.scratch + C * rs);
   x.deep_chunks = (uint64_t*)(x.lanes + lane_words + (lane_words & 1));
-  x.s2 = x.deep_chunks + C;
+  x.sst = x.deep_chunks + C;
   if (x.n_chunks == 0) {
     // nothing starts in [begin, end): the index is just the end position
     if (e == hipSuccess) e = launch_index_empty(x.res, offs, x.begin, fill_to, s);
@@ -796,6 +803,7 @@ const char* tgpu_code_name(int code) {
     case TGPU_ERR_INVALID_BOOL_WRITE: return "INVALID_BOOL_WRITE";
     case TGPU_ERR_WRITE_SIZE_LIMIT: return "WRITE_SIZE_LIMIT";
     case TGPU_ERR_UNION_MISSING_STOP: return "UNION_MISSING_STOP";
+    case TGPU_ERR_MISSING_REQUIRED_FIELD: return "MISSING_REQUIRED_FIELD";
     case TGPU_ERR_INDEX_MISMATCH: return "INDEX_MISMATCH";
     case TGPU_ERR_OUTPUT_OVERFLOW: return "OUTPUT_OVERFLOW";
     case TGPU_ERR_UNSUPPORTED: return "UNSUPPORTED";

@@ -755,6 +755,7 @@ struct ReadFrame {
   uint32_t ti;     // list/map: type node of container elements / values
   uint32_t fidx;   // struct: field whose struct / container value is open
   uint32_t nread;  // struct: fields read or skipped (a union takes one)
+  uint64_t seen;   // struct: fields (index < 64) read by this read (required check)
   uint32_t n, i;   // list/map: elements, elements done
   uint32_t es, ks; // list/map: element (pair) stride in the arena, key bytes
   uint8_t* obj;    // struct: the object; list/map: element array
@@ -770,6 +771,8 @@ __device__ __forceinline__ void set_span_len(uint8_t* m, uint8_t* arr, uint8_t* 
 __device__ __forceinline__ void child_done(const DevSchema& sc, ReadFrame& p, const Arena& A) {
   if (p.kind == RF_STRUCT) {
     p.obj[sc.f[p.fidx].isset_offset] = 1;  // __isset.set(idx, true)
+    const uint32_t k = p.fidx - sc.s[p.si].first_field;
+    if (k < 64) p.seen |= 1ull << k;
   } else {
     ++p.i;
     if (p.kind == RF_MAP || p.is_set) set_span_len(p.span, p.obj, A.base, p.i);
@@ -872,6 +875,7 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, Arena&
     f.prev = 0;
     f.nread = 0;
     f.fidx = 0;
+    f.seen = 0;
   }
   while (sp > 0 && r.ok()) {
     ReadFrame& fr = st[sp - 1];
@@ -902,6 +906,7 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, Arena&
         f.prev = 0;
         f.nread = 0;
         f.fidx = 0;
+        f.seen = 0;
       } else if (open_container<P>(r, sc, ctype_node(sc, fr.ti), val, A, st, sp)) {
         if (r.ok()) child_done(sc, fr, A);
       }
@@ -915,6 +920,13 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, Arena&
       if (!r.ok()) return;
       // a union with no field is cleared (deserialize_union.whisker:26-28)
       if (un && fr.nread == 0) zero_bytes(fr.obj, sd.size);
+      // deprecated_enforce_required: every required field read by this
+      // read, checked after readStructEnd (deserialize_struct.whisker:116-124)
+      if (sd.flags & TGPU_STRUCT_ENFORCE_REQUIRED) {
+        for (uint32_t k = 0; k < sd.num_fields && k < 64; ++k)
+          if (sc.f[sd.first_field + k].qualifier == TGPU_REQUIRED && !((fr.seen >> k) & 1))
+            return r.fail(TGPU_ERR_MISSING_REQUIRED_FIELD, r.pos);
+      }
       // STOP: struct done
       --sp;
       if (sp > 0) child_done(sc, st[sp - 1], A);
@@ -958,12 +970,17 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, Arena&
       nf.prev = 0;
       nf.nread = 0;
       nf.fidx = 0;
+      nf.seen = 0;
       continue;  // isset set when the nested STOP is reached
     } else {
       fr.fidx = (uint32_t)hit;
       if (!open_container<P>(r, sc, ctype_of(f), m, A, st, sp)) continue;
     }
-    if (r.ok()) fr.obj[f.isset_offset] = 1;
+    if (r.ok()) {
+      fr.obj[f.isset_offset] = 1;
+      const uint32_t k = (uint32_t)hit - sd.first_field;
+      if (k < 64) fr.seen |= 1ull << k;
+    }
   }
 }
 

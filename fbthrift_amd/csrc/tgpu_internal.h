@@ -73,6 +73,8 @@ struct DeepArgs {
 // arena == nullptr with this capacity: list elements are read and validated
 // but not stored (the stream indexer measures records without output).
 constexpr uint64_t kDiscardArena = ~0ull;
+// Starts of a speculated chain kept for the repair pass (stream indexer).
+constexpr int kSpecStarts = 8;
 
 // One step of the canonical Binary wire template of a fixed-layout schema
 // (every field unqualified, fixed width; nested structs flattened). The item
@@ -266,7 +268,8 @@ struct IndexArgs {
   // per chunk: speculated/verified first start, end of the chain, record count
   uint64_t* s;
   uint64_t* e;
-  uint64_t* s2;              // speculation: the chain's second start (kNo: none)
+  uint64_t* sst;             // speculation: the chain's first kSpecStarts starts
+                             // (sst[j * kSpecStarts] == s[j] when valid)
   unsigned long long* cnt;
   uint64_t* pf;              // speculation: where the program stopped (partial chain)
   uint64_t* ep;              // emit: where the program stopped (kNo: done)

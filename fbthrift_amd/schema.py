@@ -22,6 +22,7 @@ SPAN = np.dtype([("offset", "<u8"), ("length", "<u4"), ("reserved", "<u4")])
 
 OPTIONAL = 1
 TERSE = 2  # @thrift.TerseWrite: written only when not empty (op::isEmpty)
+REQUIRED = 3  # `required`: always written; enforced on read with Struct(enforce_required)
 
 
 class Type:
@@ -58,9 +59,11 @@ def element_struct(t):
 
 
 class Struct:
-    def __init__(self, name, fields, union=False):
+    def __init__(self, name, fields, union=False, enforce_required=False):
         self.name, self.fields = name, list(fields)
         self.union = bool(union)  # TGPU_STRUCT_UNION
+        # TGPU_STRUCT_ENFORCE_REQUIRED (deprecated_enforce_required codegen)
+        self.enforce_required = bool(enforce_required)
 
 
 class Schema:
@@ -148,7 +151,7 @@ class Schema:
             structs[si].num_fields = len(s.fields)
             structs[si].size = self.size[si]
             structs[si].align = self.align[si]
-            structs[si].flags = 1 if s.union else 0
+            structs[si].flags = (1 if s.union else 0) | (2 if s.enforce_required else 0)
             for k, f in enumerate(s.fields):
                 fd = fields[j]
                 fd.id, fd.ttype, fd.elem_ttype = f.id, f.ttype, f.elem_ttype
@@ -219,7 +222,8 @@ class Schema:
         values as [ttype, elem_ttype, val_ttype, struct_index, nested]); a
         union is {"union": true, "fields": [...]}. struct_index names the
         struct of a T_STRUCT field or of T_STRUCT elements / values."""
-        structs = [Struct("S%d" % i, [], union=isinstance(e, dict) and e.get("union"))
+        structs = [Struct("S%d" % i, [], union=isinstance(e, dict) and e.get("union"),
+                          enforce_required=isinstance(e, dict) and e.get("enforce_required"))
                    for i, e in enumerate(table)]
 
         def typ(spec):

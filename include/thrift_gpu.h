@@ -104,6 +104,12 @@ enum tgpu_qualifier {
      scalar whose bits are not all zero (-0.0 is written), a non-empty
      string/list/set; read like an unqualified field. Not for struct fields. */
   TGPU_TERSE = 2,
+  /* `required`: always written; read like an unqualified field. With the
+     struct flag TGPU_STRUCT_ENFORCE_REQUIRED (the generated reader built with
+     the deprecated_enforce_required compiler option) a struct whose read
+     did not see the field fails with TGPU_ERR_MISSING_REQUIRED_FIELD
+     (deserialize_struct.whisker:116-124). Its isset byte records the read. */
+  TGPU_REQUIRED = 3,
 };
 
 /*
@@ -168,6 +174,10 @@ enum tgpu_struct_flags {
      immediate STOP clears it (apache::thrift::clear), a second field is
      TGPU_ERR_UNION_MISSING_STOP. Members must be unqualified. */
   TGPU_STRUCT_UNION = 1,
+  /* Readers check the struct's required fields (TGPU_REQUIRED): one not
+     read by this struct's read -> TGPU_ERR_MISSING_REQUIRED_FIELD, after its
+     STOP. Structs with required fields past the 64th field are rejected. */
+  TGPU_STRUCT_ENFORCE_REQUIRED = 2,
 };
 
 /* A struct = a contiguous run of fields. Struct 0 is the record (root) type. */
@@ -229,6 +239,9 @@ enum tgpu_code {
   TGPU_ERR_BAD_TYPE = 9,         /* UNKNOWN: Compact "don't know what type" */
   TGPU_ERR_UNION_MISSING_STOP = 12, /* INVALID_DATA: throwUnionMissingStop
                                        (TProtocolException.cpp:23-27) */
+  TGPU_ERR_MISSING_REQUIRED_FIELD = 13, /* MISSING_REQUIRED_FIELD:
+                                           throwMissingRequiredField
+                                           (TProtocolException.cpp:54-58) */
   /* writer-side: the reference aborts the process (validate_bool,
      thrift/lib/cpp2/protocol/Protocol.h:126-163) or throws SIZE_LIMIT */
   TGPU_ERR_INVALID_BOOL_WRITE = 10,

@@ -38,6 +38,7 @@ void classify(int code, int32_t* exc, int32_t* tp) {
     case TGPU_ERR_SIZE_LIMIT:
     case TGPU_ERR_WRITE_SIZE_LIMIT: e = TGPU_EXC_PROTOCOL; t = 3; break;
     case TGPU_ERR_DEPTH_LIMIT: e = TGPU_EXC_PROTOCOL; t = 8; break;
+    case TGPU_ERR_MISSING_REQUIRED_FIELD: e = TGPU_EXC_PROTOCOL; t = 6; break;
     case TGPU_ERR_BAD_TYPE: e = TGPU_EXC_PROTOCOL; t = 0; break;  // UNKNOWN
     case TGPU_ERR_INVALID_BOOL_WRITE: e = TGPU_EXC_ABORT; break;
     default: break;
@@ -812,6 +813,7 @@ void readStruct(R& r, uint32_t si, uint8_t* obj, DecodeCtx& dc) {
   const bool un = sd.flags & TGPU_STRUCT_UNION;
   int16_t prev = 0;
   bool first = true;
+  uint64_t seen = 0;  // the generated reader's local isset_<field> flags
   while (true) {
     uint8_t wt;
     int16_t id;
@@ -854,7 +856,16 @@ void readStruct(R& r, uint32_t si, uint8_t* obj, DecodeCtx& dc) {
       readContainer(r, ct_of(*f), m, dc);
     }
     obj[f->isset_offset] = 1;  // __isset.set(idx, true)
+    const uint32_t k = (uint32_t)(f - (dc.sc->f + sd.first_field));
+    if (k < 64) seen |= 1ull << k;
   }
+  // deprecated_enforce_required (deserialize_struct.whisker:116-124): after
+  // readStructEnd, a required field this read did not see throws
+  // MISSING_REQUIRED_FIELD
+  if (sd.flags & TGPU_STRUCT_ENFORCE_REQUIRED)
+    for (uint32_t k = 0; k < sd.num_fields && k < 64; ++k)
+      if (dc.sc->f[sd.first_field + k].qualifier == TGPU_REQUIRED && !((seen >> k) & 1))
+        fail(TGPU_ERR_MISSING_REQUIRED_FIELD, r.c.pos);
 }
 
 void init_record(const Schema& sc, uint8_t* rec) {

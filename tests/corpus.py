@@ -152,6 +152,59 @@ def cases():
     out += map_cases()
     out += union_cases()
     out += string_elem_cases()
+    out += required_cases()
+    return out
+
+
+MISSING_REQ = 13
+REQ = 3
+
+
+def _req_schema(enforce):
+    # {1: required i64, 2: i32, 3: Inner{1: required i32, 2: i32}}
+    return [{"fields": [[1, I64, 0, REQ, -1], [2, I32, 0, 0, -1], [3, STRUCT, 0, 0, 1]],
+             "enforce_required": enforce},
+            {"fields": [[1, I32, 0, REQ, -1], [2, I32, 0, 0, -1]], "enforce_required": enforce}]
+
+
+def required_cases():
+    """deserialize_struct.whisker:116-124 (deprecated_enforce_required): after
+    readStructEnd, a required field this read of the struct did not see
+    throws TProtocolException MISSING_REQUIRED_FIELD; without the option the
+    record reads normally. A field of the wrong type is skipped, so it is not
+    seen; a nested struct read twice is checked per read."""
+    out = []
+    for p, pn in ((B, "binary"), (C, "compact")):
+        def rec(f1=True, f1_type=I64, inner=((1, 5), (2, 6)), inner2=None):
+            w = W(p)
+            if f1:
+                w.field(f1_type, 1)
+                w.i64(9) if f1_type == I64 else w.i32(9)
+            w.field(I32, 2).i32(3)
+            for ins in (inner, inner2):
+                if ins is None:
+                    continue
+                w.field(STRUCT, 3).struct_begin()
+                for fid, v in ins:
+                    w.field(I32, fid).i32(v)
+                w.struct_end()
+            return w.stop().bytes()
+
+        good = rec()
+        for enforce in (True, False):
+            tag = "%s_req_%s" % (pn, "enforced" if enforce else "off")
+            sch = _req_schema(enforce)
+            for name, stream, code in (
+                    ("ok", good, OK),
+                    ("missing_root", rec(f1=False), MISSING_REQ),
+                    ("wrong_type", rec(f1_type=I32), MISSING_REQ),
+                    ("missing_inner", rec(inner=((2, 6),)), MISSING_REQ),
+                    ("inner_absent", rec(inner=None), OK),
+                    ("inner_twice_second_missing", rec(inner2=((2, 7),)), MISSING_REQ),
+                    ("third_record", good + good + rec(f1=False) + good, MISSING_REQ)):
+                n = 4 if name == "third_record" else 1
+                out.append(("%s_%s" % (tag, name), p, sch, stream, n, None,
+                            code if enforce else OK))
     return out
 
 

@@ -52,6 +52,7 @@ TBinaryProtocol, TCompactProtocol, TTransport = import_reference()
 sys.path.insert(0, HERE)
 
 from datagen import *  # noqa: F401,F403  (schemas + generators)
+import nestgen  # noqa: E402
 
 
 # ----------------------------------------------------------------- writing --
@@ -104,6 +105,51 @@ def write_struct(p, schema, sidx, vals):
     p.writeStructEnd()
 
 
+def write_spec(p, table, spec, v):
+    """A value of type `spec` (tests/golden/nestgen.py) through the
+    reference's protocol methods; structs field by field in declaration
+    order, optional fields only when set."""
+    t = spec[0]
+    if t == T_STRUCT:
+        p.writeStructBegin("S%d" % spec[1])
+        for row, x in zip(table[spec[1]], v):
+            if x is None:
+                assert row[3] == 1
+                continue
+            p.writeFieldBegin("f", row[1], row[0])
+            write_spec(p, table, nestgen.field_spec(row), x)
+            p.writeFieldEnd()
+        p.writeFieldStop()
+        p.writeStructEnd()
+    elif t == T_MAP:
+        p.writeMapBegin(spec[1][0], spec[2][0], len(v))
+        for a, b in v:
+            write_spec(p, table, spec[1], a)
+            write_spec(p, table, spec[2], b)
+        p.writeMapEnd()
+    elif t in (T_LIST, T_SET):
+        (p.writeListBegin if t == T_LIST else p.writeSetBegin)(spec[1][0], len(v))
+        for e in v:
+            write_spec(p, table, spec[1], e)
+        (p.writeListEnd if t == T_LIST else p.writeSetEnd)()
+    else:
+        write_value(p, t, 0, -1, table, v)
+
+
+def serialize_nested(proto, table, records):
+    chunks, offsets, pos = [], [0], 0
+    for rec in records:
+        t = TTransport.TMemoryBuffer()
+        p = (TBinaryProtocol.TBinaryProtocol(t) if proto == "binary"
+             else TCompactProtocol.TCompactProtocol(t))
+        write_spec(p, table, (T_STRUCT, 0), rec)
+        b = t.getvalue()
+        chunks.append(b)
+        pos += len(b)
+        offsets.append(pos)
+    return b"".join(chunks), np.array(offsets, dtype=np.uint64)
+
+
 def serialize(proto, schema, records):
     chunks, offsets, pos = [], [0], 0
     for rec in records:
@@ -151,6 +197,14 @@ CASES = [
     ("updated_binary", "updated", "binary", lambda i: UPDATED, 1),
 ]
 
+NESTED_CASES = [
+    # containers of structs / of containers (tests/golden/nestgen.py)
+    ("structlist_binary", "structlist", "binary", 400),
+    ("structlist_compact", "structlist", "compact", 400),
+    ("deepcont_binary", "deepcont", "binary", 300),
+    ("deepcont_compact", "deepcont", "compact", 300),
+]
+
 DIGESTS = [
     # name, schema, proto, generator, n: sha256 of the whole stream
     ("flat8_binary_50k", "flat8", "binary", gen_flat8, 50000),
@@ -189,6 +243,21 @@ def main():
         manifest["cases"][name] = {"schema": sch, "protocol": proto, "n": n,
                                    "bytes": len(wire),
                                    "sha256": hashlib.sha256(wire).hexdigest()}
+        print(name, n, len(wire))
+    manifest["nested_schemas"] = nestgen.NESTED_SCHEMAS
+    manifest["nested_cases"] = {}
+    for name, sch, proto, n in NESTED_CASES:
+        table = nestgen.NESTED_SCHEMAS[sch]
+        recs = [nestgen.NESTED_GENERATORS[sch](i) for i in range(n)]
+        wire, offs = serialize_nested(proto, table, recs)
+        with open(os.path.join(HERE, name + ".wire.bin"), "wb") as f:
+            f.write(wire)
+        np.save(os.path.join(HERE, name + ".offsets.npy"), offs)
+        with open(os.path.join(HERE, name + ".values.json"), "w") as f:
+            json.dump([nestgen.to_json((T_STRUCT, 0), r, table) for r in recs], f)
+        manifest["nested_cases"][name] = {"schema": sch, "protocol": proto, "n": n,
+                                          "bytes": len(wire),
+                                          "sha256": hashlib.sha256(wire).hexdigest()}
         print(name, n, len(wire))
     for name, sch, proto, gen, n in DIGESTS:
         schema = SCHEMAS[sch]
