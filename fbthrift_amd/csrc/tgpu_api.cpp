@@ -239,7 +239,9 @@ int validate_struct(const Tables& T, uint32_t si, int depth, SchemaFacts& facts)
       return TGPU_ERR_UNSUPPORTED;
     }
     if ((uint64_t)fd.member_offset + sz > sd.size) return TGPU_ERR_INVALID_ARGUMENT;
-    if (fd.member_offset % (sz >= 8 ? 8 : sz)) return TGPU_ERR_INVALID_ARGUMENT;
+    // natural alignment: a nested struct's own, else min(size, 8)
+    const uint32_t al = fd.ttype == TGPU_T_STRUCT ? T.s[fd.struct_index].align : (sz >= 8 ? 8 : sz);
+    if (fd.member_offset % al) return TGPU_ERR_INVALID_ARGUMENT;
   }
   return TGPU_OK;
 }
