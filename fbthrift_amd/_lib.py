@@ -72,7 +72,8 @@ assert ctypes.sizeof(Status) == 32
 # Every symbol declared in include/thrift_gpu.h (checked by tests/test_abi.py).
 EXPORTS = [
     "tgpu_abi_version", "tgpu_code_name", "tgpu_code_classify", "tgpu_layout_compute",
-    "tgpu_schema_create", "tgpu_schema_create_ex", "tgpu_schema_destroy", "tgpu_schema_record_size",
+    "tgpu_schema_create", "tgpu_schema_create_ex", "tgpu_schema_destroy",
+    "tgpu_encoded_size_host", "tgpu_schema_record_size",
     "tgpu_schema_fixed_wire_size", "tgpu_context_create", "tgpu_context_destroy",
     "tgpu_context_reserve", "tgpu_context_wait", "tgpu_encode_batch", "tgpu_encoded_size",
     "tgpu_decode_batch", "tgpu_index_stream", "tgpu_schema_compile", "tgpu_schema_compile_check",
@@ -164,6 +165,9 @@ def lib():
     L.tgpu_encode_host_ex.restype = I32
     L.tgpu_encode_host_ex.argtypes = [P, P, I32, P, U64, P, U64, P, U64, P, U64, P,
                                       ctypes.POINTER(Status), ctypes.POINTER(U64)]
+    L.tgpu_encoded_size_host.restype = I32
+    L.tgpu_encoded_size_host.argtypes = [P, P, I32, P, U64, P, U64, P, ctypes.POINTER(Status),
+                                         ctypes.POINTER(U64)]
     L.tgpu_schema_arena_scale.restype = ctypes.c_uint32
     L.tgpu_schema_arena_scale.argtypes = [P, I32]
     L.tgpu_transcode_batch.restype = I32

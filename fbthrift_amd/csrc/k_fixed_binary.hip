@@ -20,6 +20,7 @@
 // first such record index; the general decoder then re-reads the stream from
 // that record with the full readNoXfer semantics.
 #include "tgpu_internal.h"
+#include "tgpu_program.h"
 
 namespace tgpu {
 namespace {
@@ -65,7 +66,8 @@ __device__ __forceinline__ void zero_lds(uint8_t* p, uint32_t nbytes16) {
 
 __global__ __launch_bounds__(kBlock) void fixed_binary_decode_kernel(
     const FixedTemplate* __restrict__ tp, const uint8_t* __restrict__ in,
-    uint64_t n, uint8_t* __restrict__ out, DevResult* __restrict__ res) {
+    uint64_t n, uint8_t* __restrict__ out, DevResult* __restrict__ res, uint64_t* __restrict__ exc,
+    uint64_t exc_cap) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const FixedTemplate& t = *tp;
   const uint32_t L = t.wire_len, S = t.record_size;
@@ -82,6 +84,7 @@ __global__ __launch_bounds__(kBlock) void fixed_binary_decode_kernel(
   __syncthreads();
 
   const uint32_t r = threadIdx.x;
+  bool exception = false;
   if (r < nrec) {
     const uint32_t base = sh + r * L;
     uint8_t* orec = rec + osh + r * S;
@@ -124,8 +127,9 @@ __global__ __launch_bounds__(kBlock) void fixed_binary_decode_kernel(
       }
     }
     for (uint32_t k = 0; k < t.n_isset; ++k) orec[t.isset_off[k]] = 1;
-    if (!ok) atomicMin(&res->first_irregular, (unsigned long long)(tile0 + r));
+    exception = !ok;
   }
+  prog::note_exception(exception, tile0 + r, res, exc, exc_cap);
   __syncthreads();
   stage_out(rec + osh, out + tile0 * S, nrec * S, osh);
 }
@@ -211,11 +215,12 @@ inline uint32_t encode_lds(const FixedTemplate& t) {
 
 hipError_t launch_fixed_binary_decode(const FixedTemplate* t, const FixedTemplate* d_t,
                                       const uint8_t* in, uint64_t n, uint8_t* out,
-                                      DevResult* res, hipStream_t stream) {
+                                      DevResult* res, uint64_t* exc, uint64_t exc_cap,
+                                      hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const uint64_t blocks = (n + kTileRecords - 1) / kTileRecords;
   hipLaunchKernelGGL(fixed_binary_decode_kernel, dim3((uint32_t)blocks), dim3(kBlock),
-                     decode_lds(*t), stream, d_t, in, n, out, res);
+                     decode_lds(*t), stream, d_t, in, n, out, res, exc, exc_cap);
   return hipGetLastError();
 }
 

@@ -32,6 +32,7 @@ __global__ void result_init_kernel(DevResult* res, uint64_t n) {
   res->first_start = kNone;
   res->n_deep = 0;
   res->n_deep_chunks = 0;
+  res->first_misfit = kNone;
 }
 
 // Parses record i (record buffer zeroed first); lane: deep-pass lane or -1.
@@ -62,6 +63,43 @@ __global__ __launch_bounds__(64) void deep_decode_kernel(DecodeArgs a) {
     const Reader r = decode_one<P>(a, i, (int)lane);
     if (!r.ok()) atomicMin(&a.res->first_fail, (unsigned long long)i);
   }
+}
+
+// Fixed-stride batches (Binary, fixed-layout schema): the records the fast
+// kernel could not take (its exception list: fields reordered, a bool byte
+// above 1, ...) are read by the general reader at their stride position i * L.
+// One that reads exactly L bytes keeps every later record in place; one that
+// does not (other length, reader error, a skip nested past the private
+// frames) moves first_misfit, from where the caller re-reads the stream
+// (index or serial path), which also reports any error exactly. A list that
+// overflowed (n_irregular > cap) is left alone: first_irregular stands.
+template <int P>
+__global__ __launch_bounds__(256) void fixed_exception_kernel(DecodeArgs a, uint64_t L) {
+  const unsigned long long cnt = a.res->n_irregular;
+  if (cnt > a.exc_cap) return;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += stride) {
+    const uint64_t i = a.exc[k];
+    if (i >= a.n) continue;
+    const Reader r = decode_record<P>(a, i, -1, i * L);
+    if (!r.ok() || r.pos != i * L + L) atomicMin(&a.res->first_misfit, (unsigned long long)i);
+  }
+}
+
+__global__ void fixed_exception_resolve_kernel(DevResult* res, uint64_t cap) {
+  if (res->n_irregular <= cap) res->first_irregular = res->first_misfit;
+  res->n_irregular = 0;
+  res->first_misfit = kNone;
+}
+
+// Record 0 of a fixed-stride batch read at 0: first_misfit = 0 unless it is
+// exactly L bytes (the plan kernel's work is wasted on a stream whose stride
+// is not L, e.g. every record carrying a field the schema does not know).
+template <int P>
+__global__ void fixed_probe_kernel(DecodeArgs a, uint64_t L) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const Reader r = decode_record<P>(a, 0, -1, 0);
+  a.res->first_misfit = (r.ok() && r.pos == L) ? kNone : 0;
 }
 
 // Unindexed streams the fixed-layout path cannot take: one lane reads the
@@ -270,6 +308,21 @@ hipError_t launch_serial_decode(const DecodeArgs& a, int protocol, bool from_irr
                                 uint64_t fixed_len, hipStream_t stream) {
   TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(serial_decode_kernel<P_>, dim3(1), dim3(64), 0, stream, a,
                        (int)from_irregular, fixed_len));
+  return hipGetLastError();
+}
+
+hipError_t launch_fixed_exceptions(const DecodeArgs& a, int protocol, uint64_t L,
+                                   hipStream_t stream) {
+  const uint32_t g = grid_for(a.exc_cap < a.n ? a.exc_cap : a.n);
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(fixed_exception_kernel<P_>, dim3(g), dim3(256), 0,
+                                                stream, a, L));
+  hipLaunchKernelGGL(fixed_exception_resolve_kernel, dim3(1), dim3(1), 0, stream, a.res, a.exc_cap);
+  return hipGetLastError();
+}
+
+hipError_t launch_fixed_probe(const DecodeArgs& a, int protocol, uint64_t L, hipStream_t stream) {
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(fixed_probe_kernel<P_>, dim3(1), dim3(64), 0,
+                                                stream, a, L));
   return hipGetLastError();
 }
 

@@ -36,9 +36,24 @@ using prog::kPosCap;
 using prog::kTile;
 using prog::kTileLanes;
 
+// A speculated chain reads at most kSpecReach bytes past its chunk's end. A
+// false start can parse as a container of many elements that are true
+// records (a list<struct> count read from value bytes), which would otherwise
+// walk the rest of the stream on one lane, for every such candidate; past the
+// reach the candidate is rejected like any other that fails to read, and a
+// chunk whose true straddling record is longer than that is left to the
+// repair lane (unbounded).
+constexpr uint64_t kSpecReach = 256 * 1024;
+
+__device__ __forceinline__ uint64_t spec_limit(const IndexArgs& a, uint64_t hi) {
+  return hi + kSpecReach < a.in_len ? hi + kSpecReach : a.in_len;
+}
+
 // lane >= 0: the deep-pass lane whose HBM skip frames the reader may use.
-__device__ __forceinline__ dev::Reader reader_at(const IndexArgs& a, uint64_t pos, int lane) {
-  dev::Reader r = dev::make_reader(a.in, pos, a.in_len, a.string_limit, a.container_limit,
+// limit: the reader's end (a.in_len, or a speculated chain's reach).
+__device__ __forceinline__ dev::Reader reader_at(const IndexArgs& a, uint64_t pos, int lane,
+                                                 uint64_t limit) {
+  dev::Reader r = dev::make_reader(a.in, pos, limit, a.string_limit, a.container_limit,
                                    a.max_depth, a.height);
   if (lane >= 0) dev::attach_slab(r, a.deep, (uint32_t)lane);
   return r;
@@ -52,49 +67,64 @@ struct Chain {
   uint64_t err_off;
 };
 
+// One record at p (reader end `limit`): the program first, then (general)
+// the reader. Returns 1 (q = the next record's start), 0 (not canonical and
+// !general) or -1 (reader error in out.code / out.err_off).
+template <int P>
+__device__ __forceinline__ int one_record(const IndexArgs& a, uint64_t p, uint64_t limit,
+                                          uint8_t* scratch, int lane, bool general, uint64_t& q,
+                                          Chain& out) {
+  if (a.prog && p < limit) {
+    const prog::Ctx pc{0, nullptr, 0, a.string_limit, a.container_limit};
+    const uint64_t avail = limit - p;
+    const prog::HbmSrc src{a.in + p, (uint32_t)(avail < kPosCap ? avail : kPosCap)};
+    uint32_t rel = 0;
+    if (prog::run_program<false>(prog::DynProg{a.prog}, src, pc, rel, src.avail, nullptr)) {
+      q = p + rel;
+      return 1;
+    }
+  }
+  if (!general) return 0;
+  dev::Reader r = reader_at(a, p, lane, limit);
+  // measuring read: the root into scratch, nested elements into per-level
+  // slots after it (the index's scratch stride holds both)
+  const uint32_t root = (a.sc.s[0].size + 15) & ~15u;
+  dev::Arena A = dev::record_arena<P>(a.sc, nullptr, kDiscardArena, p, scratch + root);
+  dev::read_record<P>(r, a.sc, scratch, A);
+  if (!r.ok()) {
+    out.code = r.err;
+    out.err_off = r.err_off;
+    return -1;
+  }
+  q = r.pos;
+  return 1;
+}
+
 // Records back to back from p while p < hi. canonical_first: the first record
 // must match the program (speculation); returns false if it does not.
 // emit: record starts written to emit[0..) (at most emit_cap).
 // A record nested past the private skip frames (lane < 0) ends the chain
 // with out.code = kErrDeep: speculation treats it as a failed chain (the
 // repair lane, which has HBM frames, walks it), emission defers the chunk.
+// spec: a speculated chain (bounded reach, see kSpecReach).
 template <int P>
 __device__ bool chain(const IndexArgs& a, uint64_t p, uint64_t hi, bool canonical_first,
                       uint8_t* scratch, Chain& out, uint64_t* emit, uint64_t emit_cap,
-                      uint64_t max_count, int lane = -1) {
+                      uint64_t max_count, int lane = -1, bool spec = false) {
+  const uint64_t limit = spec ? spec_limit(a, hi) : a.in_len;
   out.count = 0;
   out.code = 0;
   out.err_off = 0;
   out.second = kNo;
-  const prog::Ctx pc{0, nullptr, 0, a.string_limit, a.container_limit};
   while (p < hi && out.count < max_count) {
     uint64_t q = 0;
-    bool ok = false;
-    if (a.prog && p < a.in_len) {
-      const uint64_t avail = a.in_len - p;
-      const prog::HbmSrc src{a.in + p, (uint32_t)(avail < kPosCap ? avail : kPosCap)};
-      uint32_t rel = 0;
-      ok = prog::run_program<false>(prog::DynProg{a.prog}, src, pc, rel, src.avail, nullptr);
-      q = p + rel;
-    }
-    if (!ok) {
-      // speculation: a candidate start must open with a canonical record
-      // (schemas without a program: any record the reader accepts)
-      if (canonical_first && out.count == 0 && a.prog) return false;
-      dev::Reader r = reader_at(a, p, lane);
-      // measuring read: the root into scratch, nested elements into per-level
-      // slots after it (the index's scratch stride holds both)
-      const uint32_t root = (a.sc.s[0].size + 15) & ~15u;
-      dev::Arena A = dev::record_arena<P>(a.sc, nullptr, kDiscardArena, p, scratch + root);
-      dev::read_record<P>(r, a.sc, scratch, A);
-      if (!r.ok()) {
-        if (canonical_first && out.count == 0) return false;
-        out.code = r.err;
-        out.err_off = r.err_off;
-        out.end = p;
-        return true;
-      }
-      q = r.pos;
+    const int got = one_record<P>(a, p, limit, scratch, lane,
+                                  !(canonical_first && out.count == 0 && a.prog), q, out);
+    if (got == 0) return false;  // speculation: the first record is not canonical
+    if (got < 0) {
+      if (canonical_first && out.count == 0) return false;
+      out.end = p;
+      return true;
     }
     if (emit && out.count < emit_cap) emit[out.count] = p;
     if (out.count == 1) out.second = p;
@@ -191,7 +221,9 @@ __global__ __launch_bounds__(256) void index_cont_kernel(IndexArgs a) {
   const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (j >= a.n_chunks || a.e[j] != kPartial) return;
   Chain c;
-  chain<P>(a, a.pf[j], chunk_hi(a, j), false, a.scratch + j * a.rec_size, c, nullptr, 0, kNo);
+  const bool verified = j == 0 && !a.speculative;
+  chain<P>(a, a.pf[j], chunk_hi(a, j), false, a.scratch + j * a.rec_size, c, nullptr, 0, kNo, -1,
+           !verified);
   if (c.code) {
     if (j == 0 && !a.speculative) {
       a.e[0] = kErr;
@@ -228,7 +260,8 @@ __global__ __launch_bounds__(256) void index_spec_general_kernel(IndexArgs a) {
   const uint64_t w = j == 0 ? a.chunk : a.window;
   const uint64_t last = lo + w < hi ? lo + w : hi;
   for (uint64_t cand = lo; cand < last; ++cand) {
-    if (chain<P>(a, cand, hi, true, scratch, c, starts, kSpecStarts, kNo) && c.code == 0) {
+    if (chain<P>(a, cand, hi, true, scratch, c, starts, kSpecStarts, kNo, -1, true) &&
+        c.code == 0) {
       a.s[j] = cand;
       a.e[j] = c.end;
       a.cnt[j] = c.count;
@@ -268,8 +301,8 @@ __global__ __launch_bounds__(256) void index_spec_fallback_kernel(IndexArgs a) {
   const uint64_t w = j == 0 ? a.chunk : a.window;
   const uint64_t last = lo + w < hi ? lo + w : hi;
   for (uint64_t cand = lo; cand < last; ++cand) {
-    if (chain<P>(a, cand, hi, false, scratch, c, starts, kSpecStarts, kNo) && c.code == 0 &&
-        c.count) {
+    if (chain<P>(a, cand, hi, false, scratch, c, starts, kSpecStarts, kNo, -1, true) &&
+        c.code == 0 && c.count) {
       a.s[j] = cand;
       a.e[j] = c.end;
       a.cnt[j] = c.count;
@@ -278,6 +311,61 @@ __global__ __launch_bounds__(256) void index_spec_fallback_kernel(IndexArgs a) {
     }
   }
   starts[0] = kNo;
+}
+
+// Parallel link repair, one lane per chunk whose speculated start s[j] is not
+// its predecessor's end T = e[j-1]. A false start inside the record straddling
+// the chunk's start parses as records of its own and soon lands on a true
+// record start, after which it runs in step with the true chain. The lane walks
+// the chain from T and the speculated chain from s[j] together (two pointers,
+// the one behind advances) until they meet: from there the speculated chain is
+// the true one, so s[j] = T and cnt[j] = records from T to the meeting point +
+// the speculated chain's records from it. If the walk from T passes the
+// chunk's end first, that walk is the chunk's chain (e[j] replaced). Chunks
+// without an accepted start are parsed from T. Every result is the chunk's
+// chain given T; index_fix_kernel then verifies the links from the true start
+// in order (a chunk whose T changes there is walked again), so this pass only
+// decides speed. A reader error leaves the chunk to index_fix_kernel.
+template <int P>
+__global__ __launch_bounds__(256) void index_merge_kernel(IndexArgs a) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j == 0 || j >= a.n_chunks) return;
+  const uint64_t T = a.e[j - 1];
+  if (T == kNo || T == kErr || T == kPartial) return;
+  const uint64_t s0 = a.s[j], e0 = a.e[j];
+  if (s0 == T || e0 == kErr || e0 == kPartial) return;
+  const bool none = s0 == kNo || e0 == kNo;
+  const uint64_t hi = chunk_hi(a, j), limit = spec_limit(a, hi);
+  uint8_t* scratch = a.scratch + j * a.rec_size;
+  uint64_t pt = T, pf = none ? kNo : s0, ct = 0, cf = 0;
+  Chain c{};
+  for (;;) {
+    if (pt == pf) break;  // met: the speculated chain from here is the true one
+    if (pt < pf) {
+      if (pt >= hi) break;  // the walk from T is the chunk's whole chain
+      uint64_t q;
+      if (one_record<P>(a, pt, limit, scratch, -1, true, q, c) < 0) return;
+      pt = q;
+      ++ct;
+    } else {
+      if (pf >= hi) {  // passed the speculated chain's end: finish from T alone
+        pf = kNo;
+        continue;
+      }
+      uint64_t q;
+      if (one_record<P>(a, pf, limit, scratch, -1, true, q, c) < 0) return;
+      pf = q;
+      ++cf;
+    }
+  }
+  if (pt == pf) {
+    a.cnt[j] = ct + (a.cnt[j] - cf);
+  } else {
+    a.cnt[j] = ct;
+    a.e[j] = pt;
+  }
+  a.s[j] = T;
+  a.pf[j] = 0;
 }
 
 // ---- LDS tiles (schemas with a program; tgpu_prog_kernels.h) ---------------
@@ -567,6 +655,7 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
   // general-reader start there has no predecessor chunk to verify it)
   if (a.prog && !a.speculative)
     TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_spec_fallback_kernel<P_>, g, b, 0, stream, a));
+  TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_merge_kernel<P_>, g, b, 0, stream, a));
   // sst is written by the general speculation and the fallback only
   const int sst_valid = !a.prog || !a.speculative;
   hipLaunchKernelGGL(index_flag_kernel, g, b, 0, stream, a, sst_valid);

@@ -23,6 +23,7 @@
 #include <cstdlib>
 
 #include "tgpu_internal.h"
+#include "tgpu_program.h"
 
 namespace tgpu {
 namespace {
@@ -81,12 +82,18 @@ __device__ __forceinline__ unsigned long long decode_word(const FixedPlan* P,
 template <uint32_t T, bool kGlds, bool kPair, bool kNT>
 __global__ __launch_bounds__(T) void plan_binary_decode_kernel(
     const FixedPlan* __restrict__ pp, const uint8_t* __restrict__ in, uint64_t n,
-    unsigned long long* __restrict__ out, DevResult* __restrict__ res) {
+    unsigned long long* __restrict__ out, DevResult* __restrict__ res, uint64_t* __restrict__ exc,
+    uint64_t exc_cap) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t L = pp->wire_len, Q = pp->n_words;
   const uint64_t tile0 = (uint64_t)blockIdx.x * T;
   const uint32_t nrec = (uint32_t)min((uint64_t)T, n - tile0);
   FixedPlan* P = (FixedPlan*)(smem + wire_region(T, L));
+  // records of the tile a word of which the plan could not take (several
+  // threads may mark one record)
+  uint8_t* bad = smem + wire_region(T, L) + sizeof(FixedPlan);
+  bad[threadIdx.x] = 0;
+  bool any_bad = false;
 
   // stage the wire tile (16-byte phase of the stream preserved)
   const uint8_t* g = in + tile0 * L;
@@ -123,7 +130,10 @@ __global__ __launch_bounds__(T) void plan_binary_decode_kernel(
       const unsigned long long v = decode_word(P, w32, sh + r * L, j, ok);
       if (kNT) __builtin_nontemporal_store(v, o + q);
       else o[q] = v;
-      if (!ok) atomicMin(&res->first_irregular, (unsigned long long)(tile0 + r));
+      if (!ok) {
+        bad[r] = 1;
+        any_bad = true;
+      }
       r += sr;
       j += sj;
       if (j >= Q) {
@@ -148,8 +158,14 @@ __global__ __launch_bounds__(T) void plan_binary_decode_kernel(
       } else {
         o[q] = v0;
       }
-      if (!ok0) atomicMin(&res->first_irregular, (unsigned long long)(tile0 + r));
-      if (!ok1) atomicMin(&res->first_irregular, (unsigned long long)(tile0 + r1));
+      if (!ok0) {
+        bad[r] = 1;
+        any_bad = true;
+      }
+      if (!ok1) {
+        bad[r1] = 1;
+        any_bad = true;
+      }
       r += sr;
       j += sj;
       if (j >= Q) {
@@ -157,6 +173,10 @@ __global__ __launch_bounds__(T) void plan_binary_decode_kernel(
         ++r;
       }
     }
+  }
+  if (__syncthreads_or(any_bad)) {
+    const uint32_t k = threadIdx.x;
+    prog::note_exception(k < nrec && bad[k], tile0 + k, res, exc, exc_cap);
   }
 }
 
@@ -312,11 +332,11 @@ EncVariant enc_variant() {
 template <uint32_t T>
 hipError_t launch_dec_T(const DecVariant& v, uint32_t lds, uint64_t blocks, hipStream_t stream,
                         const FixedPlan* d_p, const uint8_t* in, uint64_t n,
-                        unsigned long long* out, DevResult* res) {
+                        unsigned long long* out, DevResult* res, uint64_t* exc, uint64_t cap) {
 #define TGPU_DEC(G, P_, N)                                                                   \
   if (v.glds == G && v.pair == P_ && v.nt == N) {                                            \
     hipLaunchKernelGGL((plan_binary_decode_kernel<T, G, P_, N>), dim3((uint32_t)blocks),     \
-                       dim3(T), lds, stream, d_p, in, n, out, res);                          \
+                       dim3(T), lds, stream, d_p, in, n, out, res, exc, cap);                \
     return hipGetLastError();                                                                \
   }
   TGPU_DEC(0, 0, 0) TGPU_DEC(1, 0, 0) TGPU_DEC(0, 1, 0) TGPU_DEC(1, 1, 0)
@@ -328,19 +348,19 @@ hipError_t launch_dec_T(const DecVariant& v, uint32_t lds, uint64_t blocks, hipS
 }  // namespace
 
 hipError_t launch_plan_binary_decode(const FixedPlan* p, const FixedPlan* d_p, const uint8_t* in,
-                                     uint64_t n, uint8_t* out, DevResult* res,
-                                     hipStream_t stream) {
+                                     uint64_t n, uint8_t* out, DevResult* res, uint64_t* exc,
+                                     uint64_t exc_cap, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const DecVariant v = dec_variant();
   DecVariant use = v;
   if (((uintptr_t)out & 15) != 0) use.pair = 0;  // 16-byte stores need 16-byte records base
   const uint64_t blocks = (n + use.T - 1) / use.T;
-  const uint32_t lds = wire_region(use.T, p->wire_len) + (uint32_t)sizeof(FixedPlan);
+  const uint32_t lds = wire_region(use.T, p->wire_len) + (uint32_t)sizeof(FixedPlan) + use.T;
   auto* o = (unsigned long long*)out;
   switch (use.T) {
-    case 128: return launch_dec_T<128>(use, lds, blocks, stream, d_p, in, n, o, res);
-    case 512: return launch_dec_T<512>(use, lds, blocks, stream, d_p, in, n, o, res);
-    default: return launch_dec_T<256>(use, lds, blocks, stream, d_p, in, n, o, res);
+    case 128: return launch_dec_T<128>(use, lds, blocks, stream, d_p, in, n, o, res, exc, exc_cap);
+    case 512: return launch_dec_T<512>(use, lds, blocks, stream, d_p, in, n, o, res, exc, exc_cap);
+    default: return launch_dec_T<256>(use, lds, blocks, stream, d_p, in, n, o, res, exc, exc_cap);
   }
 }
 

@@ -37,6 +37,11 @@ struct tgpu_schema {
   bool str_elems = false;   // strings inside lists/sets/maps (arena scale 4 / 16)
   VProgram prog[3]{};
   VProgram* d_prog[3] = {nullptr, nullptr, nullptr};
+  // the same programs taking appended unknown fields at the root STOP
+  // (kStopSkipsUnknown): a separate variant, so the canonical kernels keep
+  // their register footprint; used where a stream is known to carry them
+  VProgram prog_tol[3]{};
+  VProgram* d_prog_tol[3] = {nullptr, nullptr, nullptr};
 };
 
 struct tgpu_context {
@@ -476,13 +481,23 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
   return true;
 }
 
-bool build_program(const tgpu_schema& sc, int proto, VProgram& P) {
+bool build_program(const tgpu_schema& sc, int proto, VProgram& P, bool tolerant = false) {
   P = VProgram{};
   P.protocol = (uint32_t)proto;
   P.rec_size = sc.structs[0].size;
   if (!emit_program(sc, 0, 0, proto, P)) return false;
   VOp stop = make_op(VOP_CONST);
   stop.hdr_len = 1;
+  const tgpu_struct_desc& root = sc.structs[0];
+  if (tolerant && root.num_fields) {
+    int32_t max_id = -32768;
+    for (uint32_t k = 0; k < root.num_fields; ++k)
+      max_id = std::max<int32_t>(max_id, sc.fields[root.first_field + k].id);
+    const int16_t last = sc.fields[root.first_field + root.num_fields - 1].id;
+    stop.elem_kind = kStopSkipsUnknown;
+    stop.member = (uint16_t)(int16_t)max_id;
+    stop.hdr = (uint32_t)(uint16_t)last << 8;
+  }
   return push_op(P, stop);
 }
 
@@ -554,6 +569,12 @@ void fill_status(tgpu_status* st, int code, uint64_t rec, uint64_t off) {
   st->byte_offset = off;
 }
 
+// Fixed-layout decodes: exception list entries read at their stride (beyond
+// it the stream is indexed from the first exception); blocking calls of at
+// least kFixedProbeMin records check record 0's length first.
+constexpr uint64_t kFixedExceptionCap = 1ull << 20;
+constexpr uint64_t kFixedProbeMin = 1ull << 16;
+
 int ensure_workspace(tgpu_context* ctx, uint64_t n) {
   if (n <= ctx->reserved && ctx->d_offs) return TGPU_OK;
   const uint64_t want = std::max<uint64_t>(n, 1024);
@@ -608,6 +629,14 @@ DeepArgs deep_args(tgpu_context* ctx) {
 
 int32_t limit_depth(const tgpu_limits* limits) { return limits ? limits->max_depth : 12000; }
 
+// TGPU_PROGRAM_TAILS=1: every decode / index uses the programs that take
+// appended unknown fields (A/B and tests; by default only the fixed-layout
+// path's probe selects them).
+bool tails_everywhere() {
+  const char* e = getenv("TGPU_PROGRAM_TAILS");
+  return e && e[0] == '1';
+}
+
 // The schema's compiled kernels for `protocol` (tgpu_jit.cpp policy), or
 // nullptr: the interpreting kernels run.
 const JitKernels* schema_jit(const tgpu_schema* s, int protocol, int group, uint64_t records,
@@ -648,9 +677,13 @@ hipError_t launch_indexed_decode(tgpu_context* ctx, const tgpu_schema* schema, i
                                  const DecodeArgs& a, hipStream_t s) {
   const int32_t height = a.height ? a.height : a.max_depth;
   if (has_prog(schema, protocol) && height >= 2 && a.max_depth >= 2) {
-    hipError_t e = launch_program_decode(a, schema->d_prog[prog_protocol(schema, protocol)], a.rec_size, ctx->d_irr,
-                                         &ctx->d_res->n_irregular, s,
-                                         schema_jit(schema, protocol, JIT_DECODE, a.n, 0));
+    const int q = prog_protocol(schema, protocol);
+    const bool tol = tails_everywhere();
+    hipError_t e = launch_program_decode(
+        a, tol ? schema->d_prog_tol[q] : schema->d_prog[q], a.rec_size, ctx->d_irr,
+        &ctx->d_res->n_irregular, s,
+        tol ? jit_kernels(schema->prog_tol[q], schema->device, JIT_DECODE, a.n, 0, false)
+            : schema_jit(schema, protocol, JIT_DECODE, a.n, 0));
     if (e == hipSuccess)
       e = launch_general_decode_list(a, protocol, ctx->d_irr, &ctx->d_res->n_irregular, s);
     return e;
@@ -667,8 +700,9 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
                  uint64_t in_len, uint64_t begin, uint64_t end, int speculative, uint64_t* offs,
                  uint64_t max_records, uint64_t fill_to, const tgpu_limits* limits,
                  hipStream_t s, hipError_t& e, const DecodeArgs* dec = nullptr,
-                 bool* fused = nullptr) {
+                 bool* fused = nullptr, bool tolerant = false) {
   if (fused) *fused = false;
+  tolerant = tolerant || tails_everywhere();
   IndexArgs x{};
   x.sc = dev_schema(schema, protocol);
   x.in = in;
@@ -685,8 +719,9 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   x.max_depth = limits ? limits->max_depth : 12000;
   x.height = limits ? limits->height : 0;
   const int32_t height = x.height ? x.height : x.max_depth;
+  const int pq = prog_protocol(schema, protocol);
   x.prog = has_prog(schema, protocol) && height >= 2 && x.max_depth >= 2
-               ? schema->d_prog[prog_protocol(schema, protocol)] : nullptr;
+               ? (tolerant ? schema->d_prog_tol[pq] : schema->d_prog[pq]) : nullptr;
   x.chunk = index_chunk_bytes(end > begin ? end - begin : 0, x.prog != nullptr);
   x.window = (uint32_t)std::min<uint64_t>(x.chunk, 1024);
   x.n_chunks = end > begin ? (end - begin + x.chunk - 1) / x.chunk : 0;
@@ -737,10 +772,13 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
     return TGPU_OK;
   }
   if (e == hipSuccess)
-    e = launch_index_stream(x, s,
-                            x.prog ? schema_jit(schema, protocol, JIT_INDEX, 0, end - begin)
-                                   : nullptr,
-                            fused);
+    e = launch_index_stream(
+        x, s,
+        !x.prog ? nullptr
+        : tolerant ? jit_kernels(schema->prog_tol[pq], schema->device, JIT_INDEX, 0, end - begin,
+                                 false)
+                   : schema_jit(schema, protocol, JIT_INDEX, 0, end - begin),
+        fused);
   return TGPU_OK;
 }
 
@@ -753,13 +791,19 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
 // with it (compiled program, general decoder for the rest) — and the status
 // is left on the device (returns 1). -1: the caller's serial fallback
 // (no program for the index); a HIP error goes to `e` (returns 0).
+// first: the batch's first record not at its stride position when already
+// known (the record-0 probe), else read from the device result.
 int fixed_tail(tgpu_context* ctx, const tgpu_schema* schema, int protocol, const DecodeArgs& a,
-               uint64_t L, const tgpu_limits* limits, hipStream_t s, hipError_t& e) {
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e != hipSuccess) return 0;
-  const uint64_t irr = ctx->h_res->first_irregular;
+               uint64_t L, const tgpu_limits* limits, hipStream_t s, hipError_t& e,
+               uint64_t first = ~0ull) {
+  uint64_t irr = first;
+  if (first == ~0ull) {
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return 0;
+    irr = ctx->h_res->first_irregular;
+  }
   if (irr >= a.n) {
     e = launch_decode_finish(a, protocol, L, s);
     return 0;
@@ -770,8 +814,11 @@ int fixed_tail(tgpu_context* ctx, const tgpu_schema* schema, int protocol, const
   t.offs = ctx->d_offs + irr;
   t.check_index = 1;
   bool fused = false;
+  // a stream off the stride from record 0 on (the probe): most likely every
+  // record carries appended fields, which the tolerant programs take
   const int rc = launch_index(ctx, schema, protocol, a.in, a.in_len, irr * L, a.in_len, 0,
-                              ctx->d_offs + irr, t.n, t.n, limits, s, e, &t, &fused);
+                              ctx->d_offs + irr, t.n, t.n, limits, s, e, &t, &fused,
+                              first == 0);
   if (rc) {
     e = hipErrorOutOfMemory;
     return 0;
@@ -890,9 +937,13 @@ int tgpu_schema_create_ex(const tgpu_struct_desc* structs, uint32_t n_structs,
   }
   for (int proto : {TGPU_PROTOCOL_BINARY, TGPU_PROTOCOL_COMPACT}) {
     if (!build_program(*s, proto, s->prog[proto])) continue;
+    build_program(*s, proto, s->prog_tol[proto], true);
     if (hipMalloc(&s->d_prog[proto], sizeof(VProgram)) != hipSuccess ||
         hipMemcpy(s->d_prog[proto], &s->prog[proto], sizeof(VProgram), hipMemcpyHostToDevice) !=
-            hipSuccess) {
+            hipSuccess ||
+        hipMalloc(&s->d_prog_tol[proto], sizeof(VProgram)) != hipSuccess ||
+        hipMemcpy(s->d_prog_tol[proto], &s->prog_tol[proto], sizeof(VProgram),
+                  hipMemcpyHostToDevice) != hipSuccess) {
       tgpu_schema_destroy(s);
       return TGPU_ERR_HIP;
     }
@@ -932,6 +983,8 @@ void tgpu_schema_destroy(tgpu_schema* s) {
   if (s->d_tmpl) (void)hipFree(s->d_tmpl);
   if (s->d_plan) (void)hipFree(s->d_plan);
   for (VProgram* p : s->d_prog)
+    if (p) (void)hipFree(p);
+  for (VProgram* p : s->d_prog_tol)
     if (p) (void)hipFree(p);
   delete s;
 }
@@ -1211,6 +1264,30 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   if (n && protocol == TGPU_PROTOCOL_BINARY && schema->fixed_binary && !offsets &&
       in_len >= n * (uint64_t)schema->tmpl.wire_len) {
     fixed = schema->tmpl.wire_len;
+    a.exc = ctx->d_irr;
+    a.exc_cap = std::min<uint64_t>(ctx->reserved, kFixedExceptionCap);
+    const bool blocking = st || n_decoded || consumed;
+    if (blocking && n >= kFixedProbeMin && e == hipSuccess) {
+      // a stream whose stride is not L from record 0 on (every record
+      // carrying an unknown field, ...): index it directly
+      e = launch_fixed_probe(a, protocol, fixed, s);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(DevResult), hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e == hipSuccess && ctx->h_res->first_misfit == 0) {
+        a.offs = ctx->d_offs;
+        const int trc = fixed_tail(ctx, schema, protocol, a, fixed, limits, s, e, 0);
+        ctx->last_op = 1;
+        if (e != hipSuccess || trc < 0) {
+          fill_status(st, TGPU_ERR_HIP, 0, 0);
+          if (st) st->reserved = (int32_t)e;
+          return TGPU_ERR_HIP;
+        }
+        tgpu_status tmp;
+        return tgpu_context_wait(ctx, stream, st ? st : &tmp, n_decoded, consumed);
+      }
+      if (e == hipSuccess) e = launch_result_init(ctx->d_res, n, s);
+    }
     const JitKernels* fj = fixed_jit(schema, protocol, JIT_DECODE, n);
     if (e == hipSuccess && fj) {
       DecodeArgs f = a;
@@ -1218,13 +1295,17 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
       e = launch_program_decode(f, schema->d_prog[prog_protocol(schema, protocol)], a.rec_size, ctx->d_irr,
                                 &ctx->d_res->n_irregular, s, fj);
     } else if (e == hipSuccess && schema->has_plan && ((uintptr_t)records & 7) == 0)
-      e = launch_plan_binary_decode(&schema->plan, schema->d_plan, a.in, n, a.recs, ctx->d_res, s);
+      e = launch_plan_binary_decode(&schema->plan, schema->d_plan, a.in, n, a.recs, ctx->d_res,
+                                    a.exc, a.exc_cap, s);
     else if (e == hipSuccess)
       e = launch_fixed_binary_decode(&schema->tmpl, schema->d_tmpl, a.in, n, a.recs, ctx->d_res,
-                                     s);
+                                     a.exc, a.exc_cap, s);
     a.offs = ctx->d_offs;
     a.check_index = 0;
-    if (st || n_decoded || consumed) {
+    // exceptions read at their stride; first_irregular becomes the first
+    // record not at its stride position
+    if (e == hipSuccess) e = launch_fixed_exceptions(a, protocol, fixed, s);
+    if (blocking) {
       // blocking call: look at the plan kernel's verdict, and index + decode
       // the tail after a non-canonical record in parallel
       const int trc = fixed_tail(ctx, schema, protocol, a, fixed, limits, s, e);

@@ -1020,18 +1020,31 @@ __device__ __forceinline__ void defer_or_fail(const Reader& r, const DeepArgs& d
 // Record i of an indexed stream, zeroed and then read (one readNoXfer into a
 // default-constructed T); the reader comes back with any error latched.
 // lane >= 0: the deep-pass lane whose HBM frames the skip may use.
+// (start: the record's position; kIndexed: a.offs[i], checked as below)
+constexpr uint64_t kIndexed = ~0ull;
 template <int P>
-__device__ Reader decode_record(const DecodeArgs& a, uint64_t i, int lane) {
+__device__ Reader decode_record(const DecodeArgs& a, uint64_t i, int lane,
+                                uint64_t at = kIndexed) {
   uint8_t* rec = a.recs + i * a.rec_size;
   if ((a.rec_size & 7) == 0) {
     for (uint32_t b = 0; b < a.rec_size; b += 8) *(uint64_t*)(rec + b) = 0;
   } else {
     for (uint32_t b = 0; b < a.rec_size; ++b) rec[b] = 0;
   }
-  const uint64_t start = a.offs[i];
+  const bool indexed = at == kIndexed;
+  const uint64_t start = indexed ? a.offs[i] : at;
   Reader r = make_reader(a.in, start, a.in_len, a.string_limit, a.container_limit, a.max_depth,
                          a.height);
   if (lane >= 0) attach_slab(r, a.deep, (uint32_t)lane);
+  if (!indexed) {
+    if (start > a.in_len) {
+      r.fail(TGPU_ERR_UNDERFLOW, start);
+      return r;
+    }
+    Arena A = record_arena<P>(a.sc, a.arena, a.arena_cap, start, nullptr);
+    read_record<P>(r, a.sc, rec, A);
+    return r;
+  }
   if (start > a.in_len || (a.check_index && a.offs[i + 1] < start)) {
     r.fail(TGPU_ERR_INDEX_MISMATCH, start);
     return r;

@@ -428,4 +428,41 @@ int tgpu_encode_host_ex(tgpu_context* ctx, const tgpu_schema* schema, int protoc
   return code;
 }
 
+int tgpu_encoded_size_host(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                           const void* h_records, uint64_t n, const void* h_lists,
+                           uint64_t lists_len, uint64_t* h_out_offsets, tgpu_status* st,
+                           uint64_t* total) {
+  if (total) *total = 0;
+  if (!ctx || !schema || (n && !h_records) || (lists_len && !h_lists)) {
+    set_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+    return TGPU_ERR_INVALID_ARGUMENT;
+  }
+  const uint32_t S = tgpu_schema_record_size(schema);
+  PinGuard pin_rec(h_records, n * S), pin_l(h_lists, lists_len);
+  DevBuf drec, dlist, doffs;
+  if (!drec.alloc(n * S) || !dlist.alloc(lists_len) || !doffs.alloc((n + 1) * 8)) {
+    set_status(st, TGPU_ERR_HIP, 0, 0);
+    return TGPU_ERR_HIP;
+  }
+  if ((n && hipMemcpy(drec.p, h_records, n * S, hipMemcpyHostToDevice) != hipSuccess) ||
+      (lists_len && hipMemcpy(dlist.p, h_lists, lists_len, hipMemcpyHostToDevice) != hipSuccess)) {
+    set_status(st, TGPU_ERR_HIP, 0, 0);
+    return TGPU_ERR_HIP;
+  }
+  tgpu_status cs{};
+  uint64_t size = 0;
+  int code = tgpu_encoded_size(ctx, schema, protocol, drec.p, n, lists_len ? dlist.p : nullptr,
+                               (uint64_t*)doffs.p, nullptr, &cs, &size);
+  if (code == TGPU_OK && h_out_offsets &&
+      hipMemcpy(h_out_offsets, doffs.p, (n + 1) * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    code = TGPU_ERR_HIP;
+  if (code == TGPU_ERR_HIP) {
+    set_status(st, TGPU_ERR_HIP, 0, 0);
+    return TGPU_ERR_HIP;
+  }
+  if (st) *st = cs;
+  if (total) *total = size;
+  return code;
+}
+
 }  // extern "C"

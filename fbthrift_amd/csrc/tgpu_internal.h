@@ -164,6 +164,12 @@ struct VOp {
   uint8_t elem_ct;    // LIST: Compact element ctype
   uint8_t is_bool;    // FIXED: Binary bool (byte must be 0/1)
 };
+// CONST op flag (elem_kind): the root record's STOP, before which fields with
+// ids above the schema's (member = the root's largest id; hdr bits 8..23 =
+// the last root field's id, Compact's delta base) are skipped when they are
+// scalars or strings — a newer writer's appended fields
+// (deserialize_struct.whisker: unknown ids go to skip).
+constexpr uint8_t kStopSkipsUnknown = 1;
 constexpr int kMaxProgramOps = 128;
 struct VProgram {
   uint32_t n_ops;
@@ -186,6 +192,7 @@ struct DevResult {
   unsigned long long first_start;      // stream index: first record start found
   unsigned long long n_deep;           // records deferred to the deep pass
   unsigned long long n_deep_chunks;    // index chunks deferred to the deep emit pass
+  unsigned long long first_misfit;     // fixed path: first exception not L bytes long
 };
 
 struct DevSchema {
@@ -213,7 +220,10 @@ struct DecodeArgs {
   int check_index;  // offsets were supplied by the caller: verify lengths
   DevResult* res;
   uint64_t fixed_len;  // program decode of a fixed-layout stream: record i at i * fixed_len
-                       // (offs unused; a non-canonical record latches first_irregular)
+                       // (offs unused; a non-canonical record latches first_irregular
+                       // and joins the exception list exc[0 .. exc_cap))
+  uint64_t* exc;
+  uint64_t exc_cap;
   DeepArgs deep;
 };
 
@@ -303,9 +313,13 @@ struct IndexArgs {
 #ifndef __HIPCC_RTC__
 // Launchers (defined in the .hip files; all asynchronous on `stream`).
 // `t` is the host copy (launch geometry), `d_t` the device copy the kernels read.
+// Fixed-layout decodes: a record they cannot take joins the exception list
+// exc[0 .. exc_cap) (count res->n_irregular, first res->first_irregular);
+// launch_fixed_exceptions then reads the listed records at their stride.
 hipError_t launch_fixed_binary_decode(const FixedTemplate* t, const FixedTemplate* d_t,
                                       const uint8_t* in, uint64_t n, uint8_t* out,
-                                      DevResult* res, hipStream_t stream);
+                                      DevResult* res, uint64_t* exc, uint64_t exc_cap,
+                                      hipStream_t stream);
 hipError_t launch_fixed_binary_encode(const FixedTemplate* t, const FixedTemplate* d_t,
                                       const uint8_t* recs, uint64_t n, uint8_t* out,
                                       uint64_t* offsets, DevResult* res,
@@ -313,7 +327,17 @@ hipError_t launch_fixed_binary_encode(const FixedTemplate* t, const FixedTemplat
 // Word-gather variants (S % 8 == 0, record buffer 8-byte aligned).
 hipError_t launch_plan_binary_decode(const FixedPlan* p, const FixedPlan* d_p,
                                      const uint8_t* in, uint64_t n, uint8_t* out,
-                                     DevResult* res, hipStream_t stream);
+                                     DevResult* res, uint64_t* exc, uint64_t exc_cap,
+                                     hipStream_t stream);
+// The fixed-layout decodes' exception records read by the general reader at
+// i * L: one that does not read exactly L bytes (or fails) moves
+// res->first_misfit; then first_irregular = the first misfit when the list was
+// complete (else it stands), n_irregular = 0. Stream-ordered, no host sync.
+hipError_t launch_fixed_exceptions(const DecodeArgs& a, int protocol, uint64_t L,
+                                   hipStream_t stream);
+// Blocking fixed-layout calls: reads record 0 at offset 0 with the general
+// reader; res->first_misfit = 0 when it is not L bytes long (or fails).
+hipError_t launch_fixed_probe(const DecodeArgs& a, int protocol, uint64_t L, hipStream_t stream);
 hipError_t launch_plan_binary_encode(const FixedPlan* p, const FixedPlan* d_p,
                                      const uint8_t* recs, uint64_t n, uint8_t* out,
                                      uint64_t* offsets, DevResult* res,

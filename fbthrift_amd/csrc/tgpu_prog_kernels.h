@@ -136,12 +136,11 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
       }
     }
     if (!ok) {
-      if (L) {  // positions past it are unknown: the serial reader takes over
-        atomicMin(&a.res->first_irregular, (unsigned long long)(r0 + r));
-      } else {
-        const unsigned long long k = atomicAdd(nirr, 1ull);
-        irr[k] = r0 + r;
-      }
+      // general decoder list; a fixed-stride batch's exception list (irr ==
+      // a.exc, read again at the stride position by fixed_exception_kernel)
+      const unsigned long long k = atomicAdd(nirr, 1ull);
+      if (!L || k < a.exc_cap) irr[k] = r0 + r;
+      if (L) atomicMin(&a.res->first_irregular, (unsigned long long)(r0 + r));
     }
   }
   __syncthreads();

@@ -26,6 +26,31 @@
 namespace tgpu {
 namespace prog {
 
+// ---- fixed-stride exceptions ----------------------------------------------------
+// A fixed-stride batch (record i at i * L): record i is one the fast kernel
+// could not take. It latches first_irregular and joins the exception list
+// (irr[0 .. cap), count in n_irregular) that fixed_exception_kernel reads at
+// the record's stride position. Called by every lane of a wave together (a
+// lane passes flag = false when it has nothing), with i increasing with the
+// lane: one atomic per wave, the lowest flagged lane's i is the minimum.
+__device__ __forceinline__ void note_exception(bool flag, uint64_t i, DevResult* res,
+                                               uint64_t* irr, uint64_t cap) {
+  const uint64_t m = __ballot(flag);
+  if (!m) return;
+  const uint32_t lane = __lane_id();
+  const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+  unsigned long long base = 0;
+  if (lane == leader) {
+    base = atomicAdd(&res->n_irregular, (unsigned long long)__popcll(m));
+    atomicMin(&res->first_irregular, (unsigned long long)i);
+  }
+  base = __shfl(base, (int)leader, 64);
+  if (flag) {
+    const uint64_t k = base + (uint64_t)__popcll(m & ((1ull << lane) - 1));
+    if (k < cap) irr[k] = i;
+  }
+}
+
 // ---- program accessors --------------------------------------------------------
 struct DynProg {
   static constexpr bool kStatic = false;
@@ -159,6 +184,99 @@ struct Ctx {
   uint8_t* lds_wire;
 };
 
+// At the root STOP (kStopSkipsUnknown) a field header instead of STOP: up to
+// kMaxUnknownTail fields with ids above the schema's, each a scalar or a
+// string within the limits, are skipped (the general reader's unknown-field
+// path, BinaryProtocol.cpp skip / Protocol.h:187-344, for these types), then
+// the STOP. Anything else is irregular (the general reader decides).
+constexpr uint32_t kMaxUnknownTail = 8;
+
+template <class Src>
+__device__ __forceinline__ bool skip_unknown_tail(const VOp op, const bool compact,
+                                                            const Src src, const Ctx c,
+                                                            uint32_t& pos, const uint32_t end) {
+  const int32_t max_id = (int16_t)op.member;
+  int32_t prev = (int16_t)(uint16_t)(op.hdr >> 8);
+  uint32_t p = pos;
+  for (uint32_t k = 0; k <= kMaxUnknownTail; ++k) {
+    if (p + 1 > end) return false;
+    const uint64_t w = src.win8(p);
+    const uint32_t b = (uint32_t)(w & 0xff);
+    if (b == 0) {  // STOP
+      pos = p + 1;
+      return true;
+    }
+    if (k == kMaxUnknownTail) return false;
+    int32_t id;
+    uint32_t t;
+    if (!compact) {
+      if (p + 3 > end) return false;
+      t = b;
+      id = (int16_t)(uint16_t)(((w >> 8) & 0xff) << 8 | ((w >> 16) & 0xff));
+      p += 3;
+    } else {
+      t = b & 0xf;
+      const uint32_t d = b >> 4;
+      ++p;
+      if (d) {
+        id = prev + (int32_t)d;
+      } else {
+        uint64_t z;
+        if (!read_varint(src, p, end, 32, z)) return false;
+        const int64_t v = (int64_t)unzigzag(z, 32);
+        if (v < -32768 || v > 32767) return false;
+        id = (int32_t)v;
+      }
+      prev = id;
+    }
+    if (id <= max_id) return false;  // a schema id (or below): not a plain append
+    int64_t n;  // value bytes
+    if (!compact) {
+      switch (t) {
+        case TGPU_T_BOOL:
+          if (p + 1 > end || (src.win8(p) & 0xff) > 1) return false;
+          n = 1;
+          break;
+        case TGPU_T_BYTE: n = 1; break;
+        case TGPU_T_I16: n = 2; break;
+        case TGPU_T_I32: case TGPU_T_FLOAT: n = 4; break;
+        case TGPU_T_I64: case TGPU_T_DOUBLE: n = 8; break;
+        case TGPU_T_STRING:
+          if (p + 4 > end) return false;
+          n = (int32_t)(uint32_t)bswap_n(src.win8(p), 4);
+          p += 4;
+          if (n < 0 || (c.string_limit > 0 && n > c.string_limit)) return false;
+          break;
+        default: return false;
+      }
+    } else {
+      switch (t) {
+        case 1: case 2: n = 0; break;  // bool in the header
+        case 3: n = 1; break;          // byte
+        case 4: case 5: case 6: {      // i16 / i32 / i64 varints
+          uint64_t z;
+          if (!read_varint(src, p, end, t == 6 ? 64 : 32, z)) return false;
+          n = 0;
+          break;
+        }
+        case 7: n = 8; break;   // double
+        case 13: n = 4; break;  // float
+        case 8: {               // binary
+          uint64_t z;
+          if (!read_varint(src, p, end, 32, z)) return false;
+          n = (int32_t)(uint32_t)z;
+          if (n < 0 || (c.string_limit > 0 && n > c.string_limit)) return false;
+          break;
+        }
+        default: return false;
+      }
+    }
+    if (n > (int64_t)(end - p)) return false;
+    p += (uint32_t)n;
+  }
+  return false;
+}
+
 // One op of the program at p (bounded by end); false = irregular.
 template <bool kStore, class Src>
 __device__ __forceinline__ bool run_op(const VOp op, const bool compact, const Src& src,
@@ -168,7 +286,11 @@ __device__ __forceinline__ bool run_op(const VOp op, const bool compact, const S
       if (p + op.hdr_len > end) return false;
       const uint32_t lo = (uint32_t)src.win8(p);
       const uint32_t mask = op.hdr_len >= 4 ? 0xffffffffu : ((1u << (8 * op.hdr_len)) - 1);
-      if ((lo ^ op.hdr) & mask) return false;
+      if ((lo ^ op.hdr) & mask) {
+        if (op.elem_kind != kStopSkipsUnknown) return false;
+        if (!skip_unknown_tail(op, compact, src, c, p, end)) return false;
+        break;
+      }
       p += op.hdr_len;
       break;
     }

@@ -461,6 +461,14 @@ int tgpu_encode_host_ex(tgpu_context* ctx, const tgpu_schema* schema, int protoc
                         void* host_out, uint64_t out_capacity, uint64_t* host_out_offsets,
                         tgpu_status* st, uint64_t* out_size);
 
+/* Exact wire size of host-memory records (tgpu_encoded_size over host
+ * buffers; host_out_offsets, n+1 entries, may be NULL): what an encode into
+ * an IOBufQueue preallocates. Blocking. */
+int tgpu_encoded_size_host(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                           const void* host_records, uint64_t n_records, const void* host_lists,
+                           uint64_t lists_len, uint64_t* host_out_offsets, tgpu_status* st,
+                           uint64_t* total);
+
 /* ---- stream index ----------------------------------------------------- */
 /*
  * Record index of an unindexed stream — the bulk form of the file-reading

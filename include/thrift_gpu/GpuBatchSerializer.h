@@ -26,6 +26,7 @@
 #ifndef THRIFT_GPU_GPU_BATCH_SERIALIZER_H_
 #define THRIFT_GPU_GPU_BATCH_SERIALIZER_H_
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <stdexcept>
@@ -33,9 +34,14 @@
 #include <utility>
 #include <vector>
 
+#include <memory>
+
 #include "../thrift_gpu.h"
+#include "HostBinding.h"
 
 #ifdef THRIFT_GPU_WITH_FBTHRIFT
+#include <folly/io/IOBuf.h>
+#include <folly/io/IOBufQueue.h>
 #include <thrift/lib/cpp/protocol/TProtocolException.h>
 #include <thrift/lib/cpp2/protocol/BinaryProtocol.h>
 #include <thrift/lib/cpp2/protocol/CompactProtocol.h>
@@ -101,6 +107,115 @@ struct CompactV1Protocol {  /* CompactV1Protocol.h: doubles little-endian */
 };
 #endif
 
+#ifdef THRIFT_GPU_WITH_FBTHRIFT
+using IOBuf = folly::IOBuf;
+using IOBufQueue = folly::IOBufQueue;
+#else
+/* Header-free stand-ins for the folly::IOBuf / IOBufQueue subset the batch
+ * entry points use (the reference's serialize / deserialize take and fill
+ * these, Serializer.h:62-72,136-148): a circular chain of byte buffers with
+ * data() / length() / next() / prependChain(), and a queue that appends
+ * through preallocate() / postallocate() and hands its chain over with
+ * move(). The batch code is written against this subset only, so the same
+ * templates instantiate with folly's types. */
+class IOBuf {
+ public:
+  static std::unique_ptr<IOBuf> copyBuffer(const void* p, size_t n) {
+    std::unique_ptr<IOBuf> b(new IOBuf());
+    b->bytes_.assign((const uint8_t*)p, (const uint8_t*)p + n);
+    return b;
+  }
+  static std::unique_ptr<IOBuf> create(size_t capacity) {
+    std::unique_ptr<IOBuf> b(new IOBuf());
+    b->bytes_.reserve(capacity);
+    return b;
+  }
+  ~IOBuf() {
+    // a chain owns its other buffers (the head is owned by its holder)
+    if (next_ != this) {
+      IOBuf* p = next_;
+      prev_->next_ = nullptr;
+      while (p) {
+        IOBuf* q = p->next_;
+        p->next_ = p->prev_ = p;
+        delete p;
+        p = q;
+      }
+    }
+  }
+  const uint8_t* data() const { return bytes_.data(); }
+  uint8_t* writableData() { return bytes_.data(); }
+  size_t length() const { return bytes_.size(); }
+  size_t capacity() const { return bytes_.capacity(); }
+  IOBuf* next() { return next_; }
+  const IOBuf* next() const { return next_; }
+  bool isChained() const { return next_ != this; }
+  /* Appends `other` (a chain) at the end of this chain. */
+  void prependChain(std::unique_ptr<IOBuf> other) {
+    IOBuf* o = other.release();
+    IOBuf* otail = o->prev_;
+    IOBuf* tail = prev_;
+    tail->next_ = o;
+    o->prev_ = tail;
+    otail->next_ = this;
+    prev_ = otail;
+  }
+  size_t computeChainDataLength() const {
+    size_t n = 0;
+    const IOBuf* b = this;
+    do {
+      n += b->length();
+      b = b->next_;
+    } while (b != this);
+    return n;
+  }
+  std::vector<uint8_t>& bytes() { return bytes_; }
+
+ private:
+  IOBuf() : next_(this), prev_(this) {}
+  std::vector<uint8_t> bytes_;
+  IOBuf* next_;
+  IOBuf* prev_;
+};
+
+class IOBufQueue {
+ public:
+  /* Writable space of at least `min` bytes at the end of the queue. */
+  std::pair<void*, size_t> preallocate(size_t min, size_t newAllocationSize) {
+    std::unique_ptr<IOBuf> b = IOBuf::create(std::max(min, newAllocationSize));
+    b->bytes().resize(b->capacity());
+    pending_ = std::move(b);
+    return {pending_->writableData(), pending_->length()};
+  }
+  /* Commits n bytes of the last preallocate(). */
+  void postallocate(size_t n) {
+    pending_->bytes().resize(n);
+    if (!head_) head_ = std::move(pending_);
+    else head_->prependChain(std::move(pending_));
+  }
+  size_t chainLength() const { return head_ ? head_->computeChainDataLength() : 0; }
+  std::unique_ptr<IOBuf> move() { return std::move(head_); }
+  const IOBuf* front() const { return head_.get(); }
+
+ private:
+  std::unique_ptr<IOBuf> head_, pending_;
+};
+#endif
+
+/* Bytes of an IOBuf chain, in order (the bytes a Cursor over it reads). */
+template <class Buf>
+std::vector<uint8_t> coalesced(const Buf* head) {
+  std::vector<uint8_t> out;
+  if (!head) return out;
+  out.reserve(head->computeChainDataLength());
+  const Buf* b = head;
+  do {
+    out.insert(out.end(), b->data(), b->data() + b->length());
+    b = b->next();
+  } while (b != head);
+  return out;
+}
+
 /* tgpu runtime failure (HIP error, bad argument, capacity) — no reference
  * counterpart. */
 class GpuBatchError : public std::runtime_error {
@@ -152,6 +267,7 @@ struct FieldSpec {
   int32_t struct_index = -1;
   uint8_t val_ttype = 0;   /* map value */
   uint8_t qualifier = 0;   /* TGPU_TERSE etc.; `optional` wins when set */
+  uint32_t type_index = 0; /* 1 + nested container type (tgpu_type_desc) */
 };
 
 /* Owns a tgpu_schema. Structs are given as lists of FieldSpec (struct 0 =
@@ -160,15 +276,21 @@ struct FieldSpec {
  * alignment, trailing isset bytes; strings/lists as tgpu_span). */
 class GpuSchema {
  public:
-  /* unions[i] marks struct i as a Thrift union (may be shorter than structs). */
+  /* unions[i] marks struct i as a Thrift union (may be shorter than structs);
+     flags[i] adds tgpu_struct_flags (e.g. TGPU_STRUCT_ENFORCE_REQUIRED);
+     types: nested container types referenced by FieldSpec::type_index. */
   explicit GpuSchema(const std::vector<std::vector<FieldSpec>>& structs,
-                     const std::vector<bool>& unions = {}) {
+                     const std::vector<bool>& unions = {},
+                     const std::vector<tgpu_type_desc>& types = {},
+                     const std::vector<uint32_t>& flags = {})
+      : types_(types) {
     for (size_t i = 0; i < structs.size(); ++i) {
       const auto& s = structs[i];
       tgpu_struct_desc d{};
       d.first_field = static_cast<uint32_t>(fields_.size());
       d.num_fields = static_cast<uint32_t>(s.size());
       d.flags = (i < unions.size() && unions[i]) ? TGPU_STRUCT_UNION : 0u;
+      if (i < flags.size()) d.flags |= flags[i];
       structs_.push_back(d);
       for (const FieldSpec& f : s) {
         tgpu_field_desc fd{};
@@ -178,15 +300,17 @@ class GpuSchema {
         fd.val_ttype = f.val_ttype;
         fd.qualifier = f.optional ? TGPU_OPTIONAL : f.qualifier;
         fd.struct_index = f.struct_index;
+        fd.type_index = f.type_index;
         fields_.push_back(fd);
       }
     }
     check(tgpu_layout_compute(structs_.data(), (uint32_t)structs_.size(), fields_.data(),
                               (uint32_t)fields_.size()),
           "tgpu_layout_compute");
-    check(tgpu_schema_create(structs_.data(), (uint32_t)structs_.size(), fields_.data(),
-                             (uint32_t)fields_.size(), &schema_),
-          "tgpu_schema_create");
+    check(tgpu_schema_create_ex(structs_.data(), (uint32_t)structs_.size(), fields_.data(),
+                                (uint32_t)fields_.size(), types_.data(),
+                                (uint32_t)types_.size(), &schema_),
+          "tgpu_schema_create_ex");
   }
   ~GpuSchema() { tgpu_schema_destroy(schema_); }
   GpuSchema(const GpuSchema&) = delete;
@@ -200,8 +324,10 @@ class GpuSchema {
   uint32_t issetOffset(uint32_t struct_index, uint32_t k) const {
     return fields_[structs_[struct_index].first_field + k].isset_offset;
   }
+  SchemaTables tables() const { return SchemaTables{structs_.data(), fields_.data(), types_.data()}; }
 
  private:
+  std::vector<tgpu_type_desc> types_;
   std::vector<tgpu_struct_desc> structs_;
   std::vector<tgpu_field_desc> fields_;
   tgpu_schema* schema_ = nullptr;
@@ -310,6 +436,59 @@ class GpuBatchSerializer {
     tgpu_encode_host_ex(ctx_, schema_.get(), Protocol::kId, records, n, strings, strings_len,
                         lists, lists_len, out, capacity, out_offsets, &st, &size);
     if (st.code != TGPU_OK) rethrow(st);
+    return size;
+  }
+
+  /* deserialize over an IOBuf chain into codegen'd objects: N x
+   * Serializer::deserialize<T>(Cursor&) (Serializer.h:62-72,97-100) with the
+   * records materialized into T (std::string / std::vector members filled
+   * with COPY semantics, Protocol.h:406-454) through `binding`. out[0..n)
+   * are default-constructed T. Returns bytes consumed; throws like the
+   * reference on the first failing record, the records before it set (the
+   * failing one partially, as the reference leaves it). */
+  template <class T>
+  uint64_t deserializeBatch(const IOBuf* buf, T* out, uint64_t n, const HostStruct& binding) {
+    const std::vector<uint8_t> in = coalesced(buf);
+    const uint32_t S = schema_.recordSize();
+    std::vector<uint8_t> recs(n * S + 16);
+    const uint64_t acap = in.size() * tgpu_schema_arena_scale(schema_.get(), Protocol::kId);
+    std::vector<uint8_t> arena(acap + 16);
+    tgpu_status st{};
+    uint64_t done = 0, consumed = 0;
+    tgpu_decode_host_ex(ctx_, schema_.get(), Protocol::kId, in.data(), in.size(), n, recs.data(),
+                        acap ? arena.data() : nullptr, acap, &limits_, &st, &done, &consumed);
+    const uint64_t m = st.code == TGPU_OK ? n : (st.exc_class == TGPU_EXC_RUNTIME ? 0 : done + 1);
+    materialize(schema_.tables(), recs.data(), std::min(m, n), S, in.data(), arena.data(),
+                binding, out, sizeof(T));
+    if (st.code != TGPU_OK) rethrow(st);
+    return consumed;
+  }
+
+  /* serialize of codegen'd objects appended to an IOBufQueue: N x
+   * Serializer::serialize(obj, &queue) (Serializer.h:136-148). The exact
+   * size is computed first (tgpu_encoded_size_host), one preallocate() of
+   * it is filled by the device encoder. Returns the bytes appended. */
+  template <class T>
+  uint64_t serializeBatch(const T* in, uint64_t n, const HostStruct& binding, IOBufQueue* out) {
+    const uint32_t S = schema_.recordSize();
+    detail::DeviceForm form = dematerialize(schema_.tables(), S, in, n, sizeof(T), binding);
+    form.strings.resize(form.strings.size() + 16);
+    form.lists.resize(form.lists.size() + 16);
+    tgpu_status st{};
+    uint64_t total = 0;
+    tgpu_encoded_size_host(ctx_, schema_.get(), Protocol::kId, form.records.data(), n,
+                           form.lists.data(), form.lists.size(), nullptr, &st, &total);
+    if (st.code != TGPU_OK) rethrow(st);
+    auto space = out->preallocate(total ? total : 1, total ? total : 1);
+    uint64_t size = 0;
+    tgpu_encode_host_ex(ctx_, schema_.get(), Protocol::kId, form.records.data(), n,
+                        form.strings.data(), form.strings.size(), form.lists.data(),
+                        form.lists.size(), space.first, space.second, nullptr, &st, &size);
+    if (st.code != TGPU_OK) {
+      out->postallocate(0);
+      rethrow(st);
+    }
+    out->postallocate(size);
     return size;
   }
 

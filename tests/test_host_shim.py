@@ -1,6 +1,9 @@
 """The C++ host mirror (include/thrift_gpu/GpuBatchSerializer.h): builds and
 links against libtgpu.so on CPU; on the GPU it round-trips a codegen-layout
-struct and rethrows the reference's exception types."""
+struct and rethrows the reference's exception types; the IOBuf batch API
+(serializeBatch / deserializeBatch) round-trips codegen'd objects with
+std::string / std::vector / std::map / std::set / nested struct members and
+matches a plain Binary writer byte for byte (tests/cpp/test_host_objects.cpp)."""
 import os
 import subprocess
 
@@ -10,11 +13,13 @@ import helpers
 
 CPP = os.path.join(helpers.ROOT, "tests", "cpp")
 BIN = os.path.join(CPP, "build", "test_host_shim")
+BIN2 = os.path.join(CPP, "build", "test_host_objects")
 
 
 def test_host_shim_builds():
     subprocess.run(["make", "-s", "-C", CPP], check=True)
     out = subprocess.run(["ldd", BIN], capture_output=True, text=True).stdout
+    assert os.path.exists(BIN2)
     assert "libtgpu.so" in out and "not found" not in out.split("libtgpu.so")[1].split("\n")[0]
 
 
@@ -24,3 +29,11 @@ def test_host_shim_runs(gpu):
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert "host shim ok" in r.stdout
+
+
+@pytest.mark.gpu
+def test_host_objects_runs(gpu):
+    subprocess.run(["make", "-s", "-C", CPP], check=True)
+    r = subprocess.run([BIN2], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "host objects ok" in r.stdout

@@ -1,10 +1,13 @@
 """Fixed-layout Binary streams (config 2's schema) that leave the canonical
 form: the reference reads them record by record like any other stream
 (reordered fields, unknown fields skipped, deserialize_struct.whisker:128-159),
-so the device must too. The plan kernel decodes the canonical prefix; from
-the first non-canonical record on, the stream is indexed and decoded in
-parallel (tgpu_api.cpp fixed_tail). Records, offsets and status are compared
-with the oracle at 1M records."""
+so the device must too. The plan kernel decodes every record at its stride
+and lists the ones it cannot take; the general reader reads those at their
+stride position (k_general.hip fixed_exception_kernel). From the first one
+that is not exactly the stride long (or fails) the stream is indexed and
+decoded in parallel (tgpu_api.cpp fixed_tail); a stream whose record 0 is
+already off the stride is indexed directly. Records, offsets and status are
+compared with the oracle at 1M records."""
 import numpy as np
 import pytest
 
@@ -109,3 +112,52 @@ def test_async_call_matches(gpu, where):
     w = wire.copy()
     w[89 * where: 89 * (where + 1)] = reordered(wire[89 * where: 89 * (where + 1)])
     run(gpu, w, n, sync=False)
+
+
+def _reorder_at(wire, idx):
+    w = wire.copy()
+    for i in idx:
+        w[89 * i: 89 * (i + 1)] = reordered(wire[89 * i: 89 * (i + 1)])
+    return w
+
+
+@pytest.mark.parametrize("sync", [True, False])
+def test_many_exceptions_same_length(gpu, sync):
+    """Every 1000th record reordered (same length): the plan kernel lists them,
+    the general reader reads each at its stride position (no re-index)."""
+    _, wire = canonical(N)
+    st, nd = run(gpu, _reorder_at(wire, range(3, N, 1000)), N, sync)
+    assert st.code == 0 and nd == N
+
+
+def test_every_record_reordered(gpu):
+    """An exception list of exactly its capacity (2^20 records)."""
+    _, wire = canonical(N)
+    w = wire.reshape(N, 89).copy()
+    w[:, 0:11], w[:, 11:22] = wire.reshape(N, 89)[:, 11:22], wire.reshape(N, 89)[:, 0:11]
+    st, nd = run(gpu, w.reshape(-1), N)
+    assert st.code == 0 and nd == N
+
+
+def test_exception_list_overflow(gpu):
+    """More exceptions than the list holds: the stream is indexed from the
+    first one."""
+    n = N + 4096
+    _, wire = canonical(n)
+    w = wire.reshape(n, 89).copy()
+    w[:, 0:11], w[:, 11:22] = wire.reshape(n, 89)[:, 11:22], wire.reshape(n, 89)[:, 0:11]
+    st, nd = run(gpu, w.reshape(-1), n)
+    assert st.code == 0 and nd == n
+
+
+@pytest.mark.parametrize("sync", [True, False])
+def test_exception_then_length_change(gpu, sync):
+    """Reordered records around a record one field longer: from the longer
+    record on the stride is wrong, so the stream is re-read from it."""
+    n = 100_000
+    _, wire = canonical(n)
+    w = _reorder_at(wire, [10, 500, 70_000])
+    extra = with_extra_field(w[89 * 5000: 89 * 5001])
+    w = np.concatenate([w[: 89 * 5000], extra, w[89 * 5001:]])
+    st, nd = run(gpu, w, n, sync)
+    assert st.code == 0 and nd == n
