@@ -527,6 +527,9 @@ def main():
                     help="config 2 only: also time decodes of streams that leave the canonical "
                          "form (first record reordered; every record with an extra unknown "
                          "field) against the indexed program decode")
+    ap.add_argument("--nested", action="store_true",
+                    help="also time a nested-container workload (list<struct>, "
+                         "list<list<i32>>; Binary; general kernels) encode + decode")
     ap.add_argument("--transcode", action="store_true",
                     help="also time device transcoding of the workload's stream into the "
                          "other protocol (tgpu_transcode_batch)")
@@ -614,12 +617,147 @@ def main():
         line["skim"] = skim(wl, dev)
     if args.irregular and rank == 0 and args.config == 2:
         line["irregular"] = irregular(wl, dev)
+    if args.nested and rank == 0:
+        del wl
+        torch.cuda.empty_cache()
+        line["nested"] = nested(dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(wl)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+# Config 4's shape with containers of structs and of containers (the nested
+# golden cases' types, tests/golden/nestgen.py): Record {1: i64 id;
+# 2: list<Item> items[0..8]; 3: list<list<i32>> grid[0..3][0..7]},
+# Item {1: i32 a; 2: i64 b; 3: double c}.
+T_I32_, T_I64_, T_DOUBLE_, T_LIST_, T_STRUCT_ = 8, 10, 4, 15, 12
+NESTED_TABLE = [
+    [[1, T_I64_, 0, 0, -1], [2, T_LIST_, T_STRUCT_, 0, 1],
+     [3, T_LIST_, T_LIST_, 0, -1, 0, [T_LIST_, T_I32_, 0, -1]]],
+    [[1, T_I32_, 0, 0, -1], [2, T_I64_, 0, 0, -1], [3, T_DOUBLE_, 0, 0, -1]],
+]
+
+
+def nested(dev, n=1 << 24, reps=5, seed=0x1729):
+    """Nested containers on the device (the general reader / writer's frame
+    machines, per-record arena regions): n records generated on the device
+    (torch, seeded), encoded from a list base holding the Item arrays, the
+    grid's row spans and the rows' i32 arrays, then decoded from the indexed
+    stream. Timed with HIP events around each call (best of `reps`); checked
+    by re-encoding the decoded records (their spans now index the decode's
+    arena) to the same bytes. Rates are wire GiB/s; the rooflines price the
+    algorithmic bytes (wire + records + element arrays) against HBM."""
+    import torch
+
+    from fbthrift_amd import serializer as SZ
+    from fbthrift_amd.schema import Schema
+
+    schema = Schema.from_table(NESTED_TABLE)
+    by_name = {st.name: k for k, st in enumerate(schema.structs)}
+    r0, r1 = by_name["S0"], by_name["S1"]
+    S, IS = schema.size[r0], schema.size[r1]
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    ni = torch.randint(0, 9, (n,), device=dev, generator=g)
+    ng = torch.randint(0, 4, (n,), device=dev, generator=g)
+    rows = int(ng.sum().item())
+    rl = torch.randint(0, 8, (rows,), device=dev, generator=g)
+    items = int(ni.sum().item())
+
+    def excl(x):
+        c = torch.cumsum(x, 0)
+        return c - x
+
+    rl8 = (rl * 4 + 7) // 8 * 8  # each row's i32 array 8-byte aligned
+    items_base = 0
+    outer_base = (items * IS + 15) // 16 * 16
+    inner_base = outer_base + rows * 16
+    total = inner_base + int(rl8.sum().item()) + 16
+    lbase = torch.zeros(total, dtype=torch.uint8, device=dev)
+    # Items
+    it = lbase[: items * IS].view(items, IS)
+    mo = lambda si, k: schema.member[(si, k)]
+    io = lambda si, k: schema.isset[(si, k)]
+    it.view(torch.int32).view(items, IS // 4)[:, mo(r1, 0) // 4] = torch.randint(
+        -2**31, 2**31 - 1, (items,), device=dev, generator=g, dtype=torch.int32)
+    it.view(torch.int64).view(items, IS // 8)[:, mo(r1, 1) // 8] = torch.randint(
+        -2**62, 2**62, (items,), device=dev, generator=g, dtype=torch.int64)
+    it.view(torch.float64).view(items, IS // 8)[:, mo(r1, 2) // 8] = torch.randn(
+        items, device=dev, generator=g, dtype=torch.float64)
+    for k in range(3):
+        it[:, io(r1, k)] = 1
+    # grid rows: spans into the i32 arrays
+    outer = lbase[outer_base: outer_base + rows * 16].view(torch.int64).view(rows, 2)
+    outer[:, 0] = inner_base + excl(rl8)
+    outer[:, 1] = rl
+    nints = int(rl8.sum().item()) // 4
+    lbase[inner_base: inner_base + nints * 4].view(torch.int32)[:] = torch.randint(
+        -2**31, 2**31 - 1, (nints,), device=dev, generator=g, dtype=torch.int32)
+    # records
+    recs = torch.zeros(n * S, dtype=torch.uint8, device=dev)
+    rv = recs.view(n, S)
+    rv.view(torch.int64).view(n, S // 8)[:, mo(r0, 0) // 8] = torch.arange(n, device=dev) * 7919
+    sp = rv.view(torch.int64).view(n, S // 8)
+    sp[:, mo(r0, 1) // 8] = items_base + excl(ni) * IS
+    sp[:, mo(r0, 1) // 8 + 1] = ni
+    sp[:, mo(r0, 2) // 8] = outer_base + excl(ng) * 16
+    sp[:, mo(r0, 2) // 8 + 1] = ng
+    for k in range(3):
+        rv[:, io(r0, k)] = 1
+    del it, outer, sp, rv
+    gs = SZ.GpuSchema(schema)
+    Ser = SZ.BinarySerializer
+    Ser.context().reserve(n)
+    offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    _, wire_bytes = Ser.encoded_size(gs, recs, n, offs, list_base=lbase)
+    wire = torch.empty(wire_bytes + 16, dtype=torch.uint8, device=dev)
+    cap = Ser.arena_bytes(gs, wire_bytes)
+    arena = torch.empty(cap + 16, dtype=torch.uint8, device=dev)
+    back = torch.empty(n * S, dtype=torch.uint8, device=dev)
+
+    def best(fn):
+        t = []
+        for _ in range(reps + 1):
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            t.append(e0.elapsed_time(e1))
+        return min(t[1:])
+
+    enc_ms = best(lambda: Ser.serialize(gs, recs, n, list_base=lbase, out=wire, offsets=offs,
+                                        sync=False))
+    dec_ms = best(lambda: Ser.deserialize(gs, wire[:wire_bytes], n, offsets=offs, records=back,
+                                          arena=arena, sync=False))
+    st, nd, consumed = Ser.context().wait()
+    if st.code or nd != n or consumed != wire_bytes:
+        raise RuntimeError("nested decode failed: %s" % (st.as_tuple(),))
+    again = torch.empty_like(wire)
+    w2, _ = Ser.serialize(gs, back, n, list_base=arena, out=again, offsets=None)
+    if w2.numel() != wire_bytes or not torch.equal(w2, wire[:wire_bytes]):
+        raise RuntimeError("nested re-encode differs")
+    elem = items * IS + rows * 16 + int(rl.sum().item()) * 4
+    alg = wire_bytes + n * S + elem  # either direction: wire + records + element arrays
+    gib = wire_bytes / 2**30
+    return {"records": n, "wire_bytes": wire_bytes, "record_bytes": S,
+            "item_bytes": IS, "items": items, "grid_rows": rows,
+            "encode_ms": round(enc_ms, 3), "decode_ms": round(dec_ms, 3),
+            "encode_GiBps": round(gib / enc_ms * 1e3, 1),
+            "decode_GiBps": round(gib / dec_ms * 1e3, 1),
+            "encode_plus_decode_GiBps": round(2 * gib / (enc_ms + dec_ms) * 1e3, 1),
+            "roofline": {"bound": "hbm", "algorithmic_bytes_per_call": alg,
+                         "decode_achieved_GBps": round(alg / dec_ms / 1e6, 1),
+                         "decode_frac": round(alg / dec_ms / 1e6 / HBM_PEAK_GBS, 4),
+                         "encode_achieved_GBps": round(alg / enc_ms / 1e6, 1),
+                         "encode_frac": round(alg / enc_ms / 1e6 / HBM_PEAK_GBS, 4),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s"},
+            "kernels": "general_decode_kernel / encode_size_kernel + encode_write_kernel "
+                       "(no program: containers of structs and of containers)"}
 
 
 def irregular(wl, dev, reps=3):
@@ -783,19 +921,21 @@ def copy_ceiling(dev, nbytes=4 << 30):
 
 def pmc_traffic(kernel, n, config=2):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
-    summary (profiles/pmc_latest.json, written by tools/pmc_summary.py from
-    separate --pmc passes, gfx950 FETCH_SIZE x2 correction applied), scaled to
+    summary (profiles/pmc_c<config>.json or, for config 2's plan kernels,
+    profiles/pmc_latest.json, written by tools/pmc_summary.py from separate
+    --pmc passes, gfx950 FETCH_SIZE x2 correction applied), scaled to
     this launch's record count; None when no summary exists."""
-    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        if d.get("config", 2) != config:
-            return None
-        d = d[kernel]
-        return int(d["hbm_bytes_per_record"] * n)
-    except (OSError, KeyError, ValueError):
-        return None
+    for name in ("pmc_c%d.json" % config, "pmc_latest.json"):
+        path = os.path.join(ROOT, "profiles", name)
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            if d.get("config", 2) != config:
+                continue
+            return int(d[kernel]["hbm_bytes_per_record"] * n)
+        except (OSError, KeyError, ValueError):
+            continue
+    return None
 
 
 def transcode(wl, dev, reps=5):

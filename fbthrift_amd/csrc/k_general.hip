@@ -11,6 +11,9 @@
 //                    the batch result.
 // All state lives in the caller's stream order; nothing is read back to the
 // host inside a call, so calls can be captured into a hipGraph.
+#include <algorithm>
+#include <cstdlib>
+
 #include "tgpu_device.h"
 
 namespace tgpu {
@@ -49,6 +52,41 @@ __global__ __launch_bounds__(256) void general_decode_kernel(DecodeArgs a) {
     const Reader r = decode_one<P>(a, i, -1);
     if (!r.ok()) defer_or_fail(r, a.deep, &a.res->first_fail, i);
   }
+}
+
+// Indexed streams, 256 records per workgroup: the tile's wire bytes
+// [offs[r0], offs[r1]) are copied to LDS with 16-byte loads when they fit
+// (tile_cap, sized by the caller from the mean record) and each lane reads
+// its record there (the general reader is byte-serial: LDS latency instead of
+// HBM's per byte); a record whose read fails on the copy is read again from
+// HBM, so every status is the stream's own; a tile too large reads from HBM.
+template <int P>
+__global__ __launch_bounds__(256) void general_decode_tile_kernel(DecodeArgs a,
+                                                                  uint32_t tile_cap) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
+  const uint64_t r0 = (uint64_t)blockIdx.x * 256;
+  const uint64_t r1 = min(r0 + 256, a.n);
+  const uint64_t b0 = a.offs[r0], b1 = a.offs[r1];
+  const uint64_t a0 = b0 & ~15ull;
+  const bool staged = b0 <= b1 && b1 <= a.in_len && b1 - a0 <= tile_cap;
+  if (staged) {
+    const uint32_t nvec = (uint32_t)((b1 - a0 + 15) >> 4);
+    for (uint32_t v = threadIdx.x; v < nvec; v += 256) {
+      const uint64_t g = a0 + 16ull * v;
+      if (g + 16 <= a.in_len) {
+        *(uint4*)(tile + 16 * v) = *(const uint4*)(a.in + g);
+      } else {
+        for (uint32_t b = 0; b < 16 && g + b < a.in_len; ++b) tile[16 * v + b] = a.in[g + b];
+      }
+    }
+  }
+  __syncthreads();
+  const uint64_t i = r0 + threadIdx.x;
+  if (i >= a.n) return;
+  Reader r = staged ? decode_record<P>(a, i, -1, kIndexed, tile, a0, b1)
+                    : decode_record<P>(a, i, -1);
+  if (staged && !r.ok() && r.err != kErrDeep) r = decode_record<P>(a, i, -1);
+  if (!r.ok()) defer_or_fail(r, a.deep, &a.res->first_fail, i);
 }
 
 // The records the bulk passes deferred (a skip nested past the private
@@ -298,6 +336,18 @@ hipError_t launch_result_init(DevResult* res, uint64_t n, hipStream_t stream) {
 }
 
 hipError_t launch_general_decode(const DecodeArgs& a, int protocol, hipStream_t stream) {
+  if (a.n == 0) return hipSuccess;
+  if (a.offs && !getenv("TGPU_GENERAL_HBM")) {
+    // LDS tile for 256 records of the stream's mean size, with slack
+    const uint64_t mean = (a.in_len + a.n - 1) / a.n;
+    const uint64_t want = ((mean * 256 * 5 / 4 + 15) & ~15ull) + 32;
+    const uint32_t cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 4096), 64 * 1024);
+    const uint64_t blocks = (a.n + 255) / 256;
+    TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(general_decode_tile_kernel<P_>,
+                                                  dim3((uint32_t)blocks), dim3(256), cap + 16,
+                                                  stream, a, cap));
+    return hipGetLastError();
+  }
   const uint32_t g = grid_for(a.n);
   TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(general_decode_kernel<P_>, dim3(g), dim3(256), 0, stream,
                        a));

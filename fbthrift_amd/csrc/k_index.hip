@@ -388,6 +388,29 @@ __global__ __launch_bounds__(kTileLanes) void index_tile_decode_kernel(IndexArgs
   prog::index_emit_tile<true>(a, prog::DynProg{a.prog}, lds, sm, rtile);
 }
 
+// Single pass (tgpu_prog_kernels.h index_onepass_tile), interpreted program.
+template <bool kDecode>
+__global__ __launch_bounds__(kTileLanes) void index_onepass_kernel(IndexArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[prog::kTileLds];
+  __shared__ __attribute__((aligned(16))) uint8_t rtile[kDecode ? prog::kRecTileBytes + 32 : 16];
+  __shared__ prog::IndexTileShared sm;
+  __shared__ prog::OnePassShared op;
+  prog::index_onepass_tile<kDecode>(a, prog::DynProg{a.prog}, lds, sm, rtile, op);
+}
+
+__global__ __launch_bounds__(256) void index_onepass_init_kernel(IndexArgs a) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (j < a.n_chunks) {
+    a.pf[j] = 0;
+    a.ep[j] = 0;
+  }
+  if (j == 0) {
+    a.scal[1] = a.n_chunks;
+    a.scal[2] = kNo;
+    for (int k = 6; k < 12; ++k) a.scal[k] = 0;
+  }
+}
+
 __device__ __forceinline__ bool link_broken(const IndexArgs& a, uint64_t j) {
   const uint64_t e = a.e[j];
   if (e == kNo || e == kErr || e == kPartial) return true;
@@ -682,12 +705,31 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
     TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_deep_emit_kernel<P_>,
                                                     dim3((a.deep.lanes + 63) / 64), dim3(64), 0,
                                                     stream, x));
+  return launch_index_finish(a, decode, stream);
+}
+
+hipError_t launch_index_finish(const IndexArgs& a, bool decode, hipStream_t stream) {
   hipLaunchKernelGGL(index_finish_kernel, dim3(1), dim3(64), 0, stream, a, a.scal + 5);
   if (decode)
-    hipLaunchKernelGGL(index_decode_tail_kernel, dim3(1), dim3(64), 0, stream, x, a.scal + 5);
+    hipLaunchKernelGGL(index_decode_tail_kernel, dim3(1), dim3(64), 0, stream, a, a.scal + 5);
   if (a.fill_to > 0)
-    hipLaunchKernelGGL(index_pad_kernel, dim3((uint32_t)((a.fill_to + 256) / 256)), b, 0, stream,
-                       a, a.scal + 5);
+    hipLaunchKernelGGL(index_pad_kernel, dim3((uint32_t)((a.fill_to + 256) / 256)), dim3(256), 0,
+                       stream, a, a.scal + 5);
+  return hipGetLastError();
+}
+
+hipError_t launch_index_onepass(const IndexArgs& a, hipStream_t stream, const JitKernels* jit) {
+  const uint64_t C = a.n_chunks;
+  if (!a.prog || a.chunk != kTile || C == 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(index_onepass_init_kernel, dim3((uint32_t)((C + 255) / 256)), dim3(256), 0,
+                     stream, a);
+  const bool decode = a.recs != nullptr;
+  if (jit) return jit_launch_index(jit, decode ? 4 : 3, a, C, stream);
+  if (decode)
+    hipLaunchKernelGGL(index_onepass_kernel<true>, dim3((uint32_t)C), dim3(kTileLanes), 0, stream, a);
+  else
+    hipLaunchKernelGGL(index_onepass_kernel<false>, dim3((uint32_t)C), dim3(kTileLanes), 0, stream,
+                       a);
   return hipGetLastError();
 }
 

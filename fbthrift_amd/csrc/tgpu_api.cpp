@@ -3,6 +3,7 @@
 // the stream-ordered launch sequences of encode/decode.
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -629,6 +630,14 @@ DeepArgs deep_args(tgpu_context* ctx) {
 
 int32_t limit_depth(const tgpu_limits* limits) { return limits ? limits->max_depth : 12000; }
 
+// TGPU_INDEX_ONEPASS=1: blocking calls try the single-pass stream index
+// first (launch_index_onepass). Off by default: it measured slower than the
+// two passes (config 5: 7.4 ms vs 3.0 + 3.0 ms).
+bool onepass_enabled() {
+  const char* e = getenv("TGPU_INDEX_ONEPASS");
+  return e && e[0] == '1';
+}
+
 // TGPU_PROGRAM_TAILS=1: every decode / index uses the programs that take
 // appended unknown fields (A/B and tests; by default only the fixed-layout
 // path's probe selects them).
@@ -700,7 +709,7 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
                  uint64_t in_len, uint64_t begin, uint64_t end, int speculative, uint64_t* offs,
                  uint64_t max_records, uint64_t fill_to, const tgpu_limits* limits,
                  hipStream_t s, hipError_t& e, const DecodeArgs* dec = nullptr,
-                 bool* fused = nullptr, bool tolerant = false) {
+                 bool* fused = nullptr, bool tolerant = false, bool may_sync = false) {
   if (fused) *fused = false;
   tolerant = tolerant || tails_everywhere();
   IndexArgs x{};
@@ -743,7 +752,7 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   const uint64_t rs = (x.rec_size + 7) & ~7u;
   const uint64_t parts = scan_tiles_parts(C) + 1;
   const uint64_t lane_words = x.chunk == index_tile_bytes() ? C * index_tile_lanes() : 0;
-  const uint64_t need = 8 * ((9 + kSpecStarts) * C + parts + 9) + C * rs + 4 * lane_words;
+  const uint64_t need = 8 * ((9 + kSpecStarts) * C + parts + 17) + C * rs + 4 * lane_words;
   if (need > ctx->index_bytes) {
     if (ctx->d_index) (void)hipFree(ctx->d_index);
     ctx->d_index = nullptr;
@@ -762,7 +771,7 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   x.ec = (unsigned long long*)(w + 7 * C);
   x.part = (unsigned long long*)(w + 8 * C);
   x.scal = (unsigned long long*)(w + 8 * C + parts);
-  x.scratch = (uint8_t*)(w + 8 * C + parts + 8);
+  x.scratch = (uint8_t*)(w + 8 * C + parts + 16);
   x.lanes = (uint32_t*)(x.scratch + C * rs);
   x.deep_chunks = (uint64_t*)(x.lanes + lane_words + (lane_words & 1));
   x.sst = x.deep_chunks + C;
@@ -771,14 +780,33 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
     if (e == hipSuccess) e = launch_index_empty(x.res, offs, x.begin, fill_to, s);
     return TGPU_OK;
   }
-  if (e == hipSuccess)
-    e = launch_index_stream(
-        x, s,
-        !x.prog ? nullptr
-        : tolerant ? jit_kernels(schema->prog_tol[pq], schema->device, JIT_INDEX, 0, end - begin,
-                                 false)
-                   : schema_jit(schema, protocol, JIT_INDEX, 0, end - begin),
-        fused);
+  const JitKernels* jit =
+      !x.prog ? nullptr
+      : tolerant ? jit_kernels(schema->prog_tol[pq], schema->device, JIT_INDEX, 0, end - begin,
+                               false)
+                 : schema_jit(schema, protocol, JIT_INDEX, 0, end - begin);
+  if (e == hipSuccess && may_sync && x.prog && x.chunk == index_tile_bytes() && onepass_enabled()) {
+    // single pass with look-back; a range it cannot finish alone (a record
+    // off the program, a record longer than a tile, ...) goes to the two-pass
+    // index below, which redoes it whole
+    e = launch_index_onepass(x, s, jit);
+    uint64_t sc[12] = {1};
+    if (e == hipSuccess) e = hipMemcpyAsync(sc, x.scal, sizeof(sc), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    const uint64_t failed = sc[7];
+    if (getenv("TGPU_ONEPASS_STATS"))  // counters with TGPU_JIT_DEFINES="#define TGPU_ONEPASS_STATS"
+      fprintf(stderr, "tgpu onepass: tiles %llu failed %llu windows %llu restarts %llu repairs %llu "
+              "failed tiles %llu\n", (unsigned long long)x.n_chunks, (unsigned long long)sc[7],
+              (unsigned long long)sc[8], (unsigned long long)sc[9], (unsigned long long)sc[10],
+              (unsigned long long)sc[11]);
+    if (e == hipSuccess && !failed) {
+      e = launch_index_finish(x, x.recs != nullptr, s);
+      if (fused) *fused = x.recs != nullptr;
+      return TGPU_OK;
+    }
+    if (e == hipSuccess && x.nirr) e = hipMemsetAsync(x.nirr, 0, sizeof(unsigned long long), s);
+  }
+  if (e == hipSuccess) e = launch_index_stream(x, s, jit, fused);
   return TGPU_OK;
 }
 
@@ -818,7 +846,7 @@ int fixed_tail(tgpu_context* ctx, const tgpu_schema* schema, int protocol, const
   // record carries appended fields, which the tolerant programs take
   const int rc = launch_index(ctx, schema, protocol, a.in, a.in_len, irr * L, a.in_len, 0,
                               ctx->d_offs + irr, t.n, t.n, limits, s, e, &t, &fused,
-                              first == 0);
+                              first == 0, true);
   if (rc) {
     e = hipErrorOutOfMemory;
     return 0;
@@ -1339,7 +1367,8 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
         // the index tiles decode their records as they find them (fused);
         // whatever they leave goes to the general decoder below
         const int irc = launch_index(ctx, schema, protocol, a.in, in_len, 0, in_len, 0, ctx->d_offs,
-                                     n, n, limits, s, e, &a, &fused);
+                                     n, n, limits, s, e, &a, &fused, false,
+                                     st || n_decoded || consumed);
         if (irc) {
           fill_status(st, irc, 0, 0);
           return irc;
@@ -1469,7 +1498,8 @@ int tgpu_decode_stream(tgpu_context* ctx, const tgpu_schema* schema, int protoco
   hipError_t e = launch_result_init(ctx->d_res, 0, s);
   bool fused = false;
   rc = launch_index(ctx, schema, protocol, a.in, in_len, begin, end, speculative, offsets,
-                    max_records, 0, limits, s, e, max_records ? &a : nullptr, &fused);
+                    max_records, 0, limits, s, e, max_records ? &a : nullptr, &fused, false,
+                    st != nullptr);
   if (rc) {
     fill_status(st, rc, 0, 0);
     return rc;
@@ -1592,7 +1622,8 @@ int tgpu_index_stream(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   (void)hipGetLastError();  // drop a stale error left by another library
   hipError_t e = launch_result_init(ctx->d_res, 0, s);
   const int rc = launch_index(ctx, schema, protocol, (const uint8_t*)in, in_len, begin, end,
-                              speculative, offsets, max_records, 0, limits, s, e);
+                              speculative, offsets, max_records, 0, limits, s, e, nullptr,
+                              nullptr, false, st || n_records || first_start || last_end);
   if (rc) {
     fill_status(st, rc, 0, 0);
     return rc;

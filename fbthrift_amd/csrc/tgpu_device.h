@@ -81,7 +81,8 @@ __device__ __forceinline__ uint64_t i64_to_zz(int64_t n) {
 
 // ------------------------------------------------------------------ reader --
 struct Reader {
-  const uint8_t* p;
+  const uint8_t* p;  // byte at stream position x: p[x - base]
+  uint64_t base;     // 0, or the stream position of an LDS copy's first byte
   uint64_t pos, end;
   int64_t height;
   int32_t string_limit, container_limit, max_depth;
@@ -104,7 +105,7 @@ struct Reader {
       fail(TGPU_ERR_UNDERFLOW, pos);
       return 0;
     }
-    return p[pos++];
+    return p[pos++ - base];
   }
   __device__ __forceinline__ uint64_t readBE(uint32_t nbytes) {
     if (end - pos < nbytes) {
@@ -113,7 +114,7 @@ struct Reader {
       return 0;
     }
     uint64_t v = 0;
-    for (uint32_t i = 0; i < nbytes; ++i) v = (v << 8) | p[pos + i];
+    for (uint32_t i = 0; i < nbytes; ++i) v = (v << 8) | p[pos - base + i];
     pos += nbytes;
     return v;
   }
@@ -135,7 +136,7 @@ struct Reader {
         fail(TGPU_ERR_UNDERFLOW, pos);
         return 0;
       }
-      const uint64_t b = p[pos++];
+      const uint64_t b = p[pos++ - base];
       r |= (b & 0x7f) << (7 * i);
       if (!(b & 0x80)) return bits < 64 ? (r & ((1ull << bits) - 1)) : r;
     }
@@ -155,6 +156,7 @@ __device__ __forceinline__ Reader make_reader(const uint8_t* in, uint64_t pos, u
                                              int32_t max_depth, int32_t height) {
   Reader r;
   r.p = in;
+  r.base = 0;
   r.pos = pos;
   r.end = end;
   r.height = (int64_t)(height ? height : max_depth) + 1;
@@ -1022,9 +1024,11 @@ __device__ __forceinline__ void defer_or_fail(const Reader& r, const DeepArgs& d
 // lane >= 0: the deep-pass lane whose HBM frames the skip may use.
 // (start: the record's position; kIndexed: a.offs[i], checked as below)
 constexpr uint64_t kIndexed = ~0ull;
+// src (optional): an LDS copy of stream bytes [base, end) to read from.
 template <int P>
 __device__ Reader decode_record(const DecodeArgs& a, uint64_t i, int lane,
-                                uint64_t at = kIndexed) {
+                                uint64_t at = kIndexed, const uint8_t* src = nullptr,
+                                uint64_t base = 0, uint64_t end = 0) {
   uint8_t* rec = a.recs + i * a.rec_size;
   if ((a.rec_size & 7) == 0) {
     for (uint32_t b = 0; b < a.rec_size; b += 8) *(uint64_t*)(rec + b) = 0;
@@ -1033,8 +1037,15 @@ __device__ Reader decode_record(const DecodeArgs& a, uint64_t i, int lane,
   }
   const bool indexed = at == kIndexed;
   const uint64_t start = indexed ? a.offs[i] : at;
-  Reader r = make_reader(a.in, start, a.in_len, a.string_limit, a.container_limit, a.max_depth,
-                         a.height);
+  Reader r = make_reader(src ? src : a.in, start, src ? end : a.in_len, a.string_limit,
+                         a.container_limit, a.max_depth, a.height);
+  if (src) {
+    r.base = base;
+    if (start < base || start > end) {  // not inside the copy: the caller reads HBM
+      r.fail(TGPU_ERR_UNDERFLOW, start);
+      return r;
+    }
+  }
   if (lane >= 0) attach_slab(r, a.deep, (uint32_t)lane);
   if (!indexed) {
     if (start > a.in_len) {

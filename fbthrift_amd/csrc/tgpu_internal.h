@@ -289,7 +289,9 @@ struct IndexArgs {
   unsigned long long* bad;   // chunks whose chain link failed (in order)
   unsigned long long* part;  // scan partials
   unsigned long long* scal;  // [0] bad count, [1] chunks in effect, [2] error chunk,
-                             // [3] records before the error in it, [4] error record start
+                             // [3] records before the error in it, [4] error record start,
+                             // [5] total, single pass: [6] ticket, [7] failed, [8..11]
+                             // look-back windows / restarts / repairs / failed tiles
   uint8_t* scratch;          // n_chunks * rec_size: general-reader output (discarded)
   uint64_t* offs;            // record starts (max_records + 1)
   uint64_t max_records;
@@ -429,6 +431,15 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
 // After a fused index + decode over a stream range: re-diagnoses a record
 // the index accepted but the decode could not store (list arena overflow).
 hipError_t launch_stream_decode_finish(const DecodeArgs& a, int protocol, hipStream_t stream);
+// The index's epilogue: total / end / status (index_finish_kernel), the
+// fused decode's missing-record hand-off and the decode padding of offs.
+hipError_t launch_index_finish(const IndexArgs& a, bool decode, hipStream_t stream);
+// Single-pass index (+ fused decode when a.recs): LDS tiles with decoupled
+// look-back; leaves a.scal[7] != 0 when some tile could not finish alone (the
+// caller then runs launch_index_stream), else the index's arrays as the
+// two-pass index leaves them before its epilogue (launch_index_finish).
+// Program schemas with kTile chunks only.
+hipError_t launch_index_onepass(const IndexArgs& a, hipStream_t stream, const JitKernels* jit);
 // Empty range: offs[0..fill_to] = pos, no records.
 hipError_t launch_index_empty(DevResult* res, uint64_t* offs, uint64_t pos, uint64_t fill_to,
                               hipStream_t stream);

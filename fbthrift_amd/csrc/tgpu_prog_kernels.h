@@ -733,7 +733,10 @@ constexpr uint32_t kPosCap = 0x7fffff00u;
 constexpr uint32_t kTileLanes = 256;
 constexpr uint32_t kSub = 64;
 constexpr uint32_t kTile = kTileLanes * kSub;
-constexpr uint32_t kOver = 4096;
+#ifndef TGPU_KOVER
+#define TGPU_KOVER 4096
+#endif
+constexpr uint32_t kOver = TGPU_KOVER;
 constexpr uint32_t kTileLds = kTile + kOver + 32;
 constexpr uint32_t kNoPos = 0xffffffffu;
 
@@ -1022,7 +1025,15 @@ __device__ __forceinline__ void index_spec_tile(const IndexArgs& a, const PP& P,
 // a record the program cannot store (list arena overflow) is queued for the
 // general decoder. This removes the decode pass's second read of the wire
 // and of the index.
-constexpr uint32_t kRecTileBytes = 16 * 1024;  // keeps the fused tile kernel at 4 workgroups/CU
+#ifndef TGPU_REC_TILE
+#define TGPU_REC_TILE (16 * 1024)
+#endif
+constexpr uint32_t kRecTileBytes = TGPU_REC_TILE;  // keeps the fused tile kernel at 4 workgroups/CU
+
+template <bool kDecode, class PP>
+__device__ __forceinline__ void emit_lanes(const IndexArgs& a, const PP& P, const uint8_t* lds,
+                                           IndexTileShared& sm, uint8_t* rtile, const TileLane& L,
+                                           uint32_t sh, uint64_t lo, uint64_t b);
 
 template <bool kDecode, class PP>
 __device__ __forceinline__ void index_emit_tile(const IndexArgs& a, const PP& P, uint8_t* lds,
@@ -1066,6 +1077,16 @@ __device__ __forceinline__ void index_emit_tile(const IndexArgs& a, const PP& P,
     }
     return;
   }
+  emit_lanes<kDecode>(a, P, lds, sm, rtile, L, sh, lo, b);
+}
+
+// The emission body of a tile whose lanes hold verified chains (L) and whose
+// first record is record b of the range: starts to offs[b ..], and (kDecode)
+// the records decoded through an LDS record tile.
+template <bool kDecode, class PP>
+__device__ __forceinline__ void emit_lanes(const IndexArgs& a, const PP& P, const uint8_t* lds,
+                                           IndexTileShared& sm, uint8_t* rtile, const TileLane& L,
+                                           uint32_t sh, uint64_t lo, uint64_t b) {
   // lane k's records go after the records of lanes < k
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const unsigned long long x = wave_incl_scan(L.c);
@@ -1148,6 +1169,287 @@ __device__ __forceinline__ void index_emit_tile(const IndexArgs& a, const PP& P,
       }
     }
   }
+}
+
+// ---- single pass: speculate, look back, emit / decode ----------------------
+// The two-pass index (spec, fix, scan, emit) reads every tile twice. Here tile
+// j (workgroup j) speculates its chain (tile_resolve), publishes it (AGG: its
+// first start s, end e and count) and looks back: predecessors are summed
+// while each one's start is its predecessor's end, down to one whose chain is
+// verified (INCL: its inclusive record prefix and end are known). Every link
+// on the way matching means every chain on the way starts at the true end of
+// a verified chain, so this tile's prefix is their sum and it is INCL. Its own
+// link broken (the chain below verified): the tile re-chains from the true
+// start (the bytes are still in LDS) — the repair the two-pass index does in
+// index_fix_kernel. A broken link further down: that tile repairs itself;
+// this one waits for it. Then the tile emits its starts and decodes its
+// records exactly like the two-pass emit tile. Anything a tile cannot do
+// alone (a record the program does not take, no record start in the tile, a
+// record end past the packed fields' range, a wait past its bound) is FAIL,
+// which every later tile inherits; the caller then runs the two-pass index.
+//
+// Each status is ONE 64-bit word written and read with relaxed agent-scope
+// atomics (sc1 stores / loads): no release / acquire, whose L2 write-back and
+// invalidate (buffer_wbl2 / buffer_inv, one per tile, with the L2 full of the
+// decode's output) made the first version 6x slower than the two passes.
+//   AGG  (a.pf[j]):  01 | cnt:15 | s - lo:15 (0x7fff: s = e) | e - lo:32
+//   FAIL (a.pf[j]):  11 | 0
+//   INCL (a.ep[j]):  1 | e - hi:23 | inclusive prefix:40
+// Tiles go in workgroup order: workgroups are dispatched in index order (per
+// XCD), so a lower tile is resident or done whenever this one runs (a ticket
+// counter — one atomic per tile on one address — cost 1.5 ms over 256 Ki
+// tiles in the encoder experiment). Every wait is bounded
+// (kOpSpinCap): a missed bound fails the pass, never hangs it. a.scal[7]: the
+// fail flag (TGPU_ONEPASS_STATS: counters in a.scal[8..11]).
+constexpr uint32_t kOpSpinCap = 1u << 20;
+constexpr uint64_t kAggTag = 1ull << 62, kFailTag = 3ull << 62, kInclTag = 1ull << 63;
+constexpr uint64_t kSSame = 0x7fff;
+
+template <class T>
+__device__ __forceinline__ uint64_t op_ld(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ void op_st(T* p, uint64_t v) {
+  __hip_atomic_store(p, (T)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// AGG word for a chain [s, e) of c records in tile [lo, hi); 0 when the
+// fields cannot hold it.
+__device__ __forceinline__ uint64_t op_agg(uint64_t lo, uint64_t s, uint64_t e, uint64_t c) {
+  if (e < lo || e - lo > 0xffffffffull || c > 0x7fff) return 0;
+  const uint64_t sr = s == e ? kSSame : s - lo;
+  if (sr > kSSame) return 0;
+  return kAggTag | (c << 47) | (sr << 32) | (e - lo);
+}
+__device__ __forceinline__ uint64_t op_incl(uint64_t hi, uint64_t e, uint64_t incl) {
+  if (e < hi || e - hi >= (1ull << 23) || incl >= (1ull << 40)) return 0;
+  return kInclTag | ((e - hi) << 40) | incl;
+}
+
+// Waits until tile k is INCL or FAIL: its INCL word, or kFailTag, or 0 after
+// the bound.
+__device__ __forceinline__ uint64_t op_wait_final(const IndexArgs& a, uint64_t k) {
+  for (uint32_t spin = 0; spin < kOpSpinCap; ++spin) {
+    const uint64_t iw = op_ld(a.ep + k);
+    if (iw) return iw;
+    if (op_ld(a.pf + k) == kFailTag) return kFailTag;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  return 0;
+}
+
+struct OnePassShared {
+  uint64_t e;       // the tile's chain end (absolute)
+  uint64_t verdict; // 1 INCL, 3 FAIL, 0: repair from `start`
+  uint64_t prefix, start;
+};
+constexpr uint64_t kOpIncl = 1, kOpFail = 3;
+
+// Wave 0: the look-back of tile j whose speculated chain starts at s, 64
+// predecessors per round trip (lane l reads tile top - l): the first lane
+// whose tile is verified (INCL) or failed stops the window; every link above
+// it (tile k's end == tile k + 1's start) must hold. Tile j's own link broken
+// while the chain below verifies: re-chain from tile j - 1's end (verdict 0).
+// A link broken further down: that tile repairs itself; wait for it and look
+// again. No verified tile in the window: its counts are summed and the window
+// moves down.
+__device__ __forceinline__ void op_look_back(const IndexArgs& a, uint64_t j, uint64_t s,
+                                             OnePassShared& op) {
+  const uint32_t l = threadIdx.x;  // 0..63
+  if (j == 0) {  // the range's first tile starts at begin (or opens a speculative range)
+    if (l == 0) {
+      op.verdict = kOpIncl;
+      op.prefix = 0;
+    }
+    return;
+  }
+  int verdict = 2;  // 0 repair, 1 incl, 2 fail, 3 look again
+  uint64_t prefix = 0, own = kNo;
+  for (uint32_t restart = 0; restart < 64; ++restart) {
+    uint64_t need = s, sum = 0;
+    own = kNo;
+    int64_t top = (int64_t)j - 1;
+    verdict = -1;
+    while (verdict < 0) {
+      const int64_t k = top - (int64_t)l;
+      const bool valid = k >= 0;
+      uint64_t iw = 0, aw = 0;
+      if (valid) {
+        iw = op_ld(a.ep + k);
+        aw = iw ? 0 : op_ld(a.pf + k);
+      }
+      for (uint32_t spin = 0; __any(valid && !iw && !aw); ++spin) {
+        if (spin >= kOpSpinCap) {
+          aw = kFailTag;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        if (valid && !iw && !aw) {
+          iw = op_ld(a.ep + k);
+          aw = iw ? 0 : op_ld(a.pf + k);
+        }
+      }
+      const bool incl = iw != 0;
+      const bool fail = !incl && aw == kFailTag;
+      const uint64_t lo = valid ? chunk_lo(a, (uint64_t)k) : 0;
+      const uint64_t hi = valid ? chunk_hi(a, (uint64_t)k) : 0;
+      const uint64_t ek = incl ? hi + ((iw >> 40) & ((1ull << 23) - 1)) : lo + (aw & 0xffffffffull);
+      const uint64_t sr = (aw >> 32) & kSSame;
+      const uint64_t sk = sr == kSSame ? ek : lo + sr;
+      const uint64_t ck = incl ? 0 : (aw >> 47) & 0x7fff;
+      // the start of tile k + 1: lane l - 1's tile (lane 0: the chain above)
+      uint64_t above = __shfl_up(sk, 1, 64);
+      if (l == 0) above = need;
+      const uint64_t stops = __ballot(valid && (incl || fail));
+      const uint32_t stop = stops ? (uint32_t)__builtin_ctzll(stops) : 64u;
+      bool broken = valid && l <= stop && !fail && ek != above;
+      if (top == (int64_t)j - 1 && l == 0 && broken) {
+        own = ek;  // tile j's own link: it re-chains from here if the rest holds
+        broken = false;
+      }
+      own = __shfl(own, 0, 64);
+      const uint64_t bm = __ballot(broken);
+      if (bm) {  // tile (top - m) + 1 starts wrong: it repairs itself
+        const uint32_t m = (uint32_t)__builtin_ctzll(bm);
+        const uint64_t kb = (uint64_t)(top - (int64_t)m) + 1;
+        uint64_t w = 0;
+        if (l == 0) w = op_wait_final(a, kb);
+        w = __shfl(w, 0, 64);
+        verdict = (w == 0 || w == kFailTag) ? 2 : 3;
+        break;
+      }
+      uint64_t c = l < stop && valid ? ck : 0;
+      for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+      if (stop < 64) {
+        const uint64_t ws = __shfl(iw, stop, 64);
+        if (!ws) {  // the stop is a failed tile
+          verdict = 2;
+          break;
+        }
+        prefix = (ws & ((1ull << 40) - 1)) + c + sum;
+        verdict = own == kNo ? 1 : 0;
+        break;
+      }
+      if (top < 63) {  // down to tile 0, which is not verified yet: wait for it
+        uint64_t w = 0;
+        if (l == 0) w = op_wait_final(a, 0);
+        w = __shfl(w, 0, 64);
+        verdict = (w == 0 || w == kFailTag) ? 2 : 3;
+        break;
+      }
+      sum += c;
+      need = __shfl(sk, 63, 64);
+      top -= 64;
+#ifdef TGPU_ONEPASS_STATS
+      if (l == 0) atomicAdd(&a.scal[8], 1ull);
+#endif
+    }
+    if (verdict != 3) break;
+#ifdef TGPU_ONEPASS_STATS
+    if (l == 0) atomicAdd(&a.scal[9], 1ull);
+#endif
+  }
+  if (l == 0) {
+    op.verdict = verdict == 1 ? kOpIncl : verdict == 0 ? 0 : kOpFail;
+    op.prefix = prefix;
+    op.start = own;
+  }
+}
+
+// Thread 0: tile j's final word (INCL, or FAIL when the fields cannot hold it)
+// and the arrays the index epilogue reads.
+__device__ __forceinline__ void op_publish_incl(const IndexArgs& a, uint64_t j, uint64_t s,
+                                                uint64_t e, uint64_t c, uint64_t prefix,
+                                                OnePassShared& op) {
+  const uint64_t w = op_incl(chunk_hi(a, j), e, prefix + c);
+  if (!w) {
+    op.verdict = kOpFail;
+    atomicExch(&a.scal[7], 1ull);
+    op_st(a.pf + j, kFailTag);
+    return;
+  }
+  a.s[j] = s;
+  a.e[j] = e;
+  a.cnt[j] = c;
+  a.base[j] = prefix;
+  op_st(a.ep + j, w);
+}
+
+template <bool kDecode, class PP>
+__device__ __forceinline__ void index_onepass_tile(const IndexArgs& a, const PP& P, uint8_t* lds,
+                                                   IndexTileShared& sm, uint8_t* rtile,
+                                                   OnePassShared& op) {
+  const uint64_t j = blockIdx.x;
+  const uint64_t lo = chunk_lo(a, j), hi = chunk_hi(a, j);
+  const uint32_t sh0 = (uint32_t)((uintptr_t)(a.in + lo) & 15);
+  const uint32_t ent = (j == 0 && !a.speculative) ? sh0 : kNoPos;
+  TileLane L;
+  uint32_t sh, first;
+  bool ok = tile_resolve(a, P, j, lds, ent, L, sh, first, sm.E, &sm.flag, &sm.first_lane, &sm.fs,
+                         sm.cmask);
+  bool good = ok && first != kNoPos;
+  for (int pass = 0; pass < 2; ++pass) {
+    if (threadIdx.x == 0) sm.csum = 0;
+    __syncthreads();
+    if (good) atomicAdd(&sm.csum, (unsigned long long)L.c);
+    if (threadIdx.x == kTileLanes - 1) op.e = lo - sh + L.e;
+    __syncthreads();
+    const uint64_t sj = lo - sh + first, cj = sm.csum;
+    uint64_t aw = 0;
+    if (good && pass == 0) aw = op_agg(lo, sj, op.e, cj);
+    if (threadIdx.x == 0) {
+      if (!good || (pass == 0 && !aw)) {
+        op.verdict = kOpFail;
+        atomicExch(&a.scal[7], 1ull);
+        op_st(a.pf + j, kFailTag);
+      } else if (pass == 0) {
+        op_st(a.pf + j, aw);
+      }
+    }
+#ifdef TGPU_ONEPASS_NOLOOK  // A/B timing only: no look-back (wrong record positions)
+    if (pass == 0 && aw && threadIdx.x == 0) {
+      op.verdict = kOpIncl;
+      op.prefix = 0;
+    }
+#else
+    if (pass == 0 && aw && threadIdx.x < 64) op_look_back(a, j, sj, op);
+#endif
+    if (threadIdx.x == 0 && good && (pass == 1 || aw)) {
+      if (pass == 1) op.verdict = kOpIncl;  // re-chained from the verified start
+      if (op.verdict == kOpIncl) {
+        op_publish_incl(a, j, sj, op.e, cj, op.prefix, op);
+      } else if (op.verdict == kOpFail) {
+        atomicExch(&a.scal[7], 1ull);
+        op_st(a.pf + j, kFailTag);
+#ifdef TGPU_ONEPASS_STATS
+        atomicAdd(&a.scal[11], 1ull);
+#endif
+      }
+    }
+    __syncthreads();
+    if (op.verdict != 0) break;
+#ifdef TGPU_ONEPASS_STATS
+    if (threadIdx.x == 0) atomicAdd(&a.scal[10], 1ull);
+#endif
+    if (op.start >= hi) {  // the true chain passes the whole tile: no record starts here
+      L.s = L.e = L.c = 0;
+      if (threadIdx.x == 0) {
+        op.verdict = kOpIncl;
+        op_publish_incl(a, j, op.start, op.start, 0, op.prefix, op);
+      }
+      __syncthreads();
+      break;
+    }
+    // repair: the chain from the verified start, inside this tile
+    ok = tile_resolve(a, P, j, lds, (uint32_t)(op.start - (lo - sh0)), L, sh, first, sm.E,
+                      &sm.flag, &sm.first_lane, &sm.fs, sm.cmask);
+    good = ok && first != kNoPos;
+  }
+  if (op.verdict != kOpIncl) return;
+#ifndef TGPU_ONEPASS_NOEMIT  // A/B timing only: no emission
+  emit_lanes<kDecode>(a, P, lds, sm, rtile, L, sh, lo, op.prefix);
+#endif
 }
 
 }  // namespace prog

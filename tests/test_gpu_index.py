@@ -233,3 +233,39 @@ def test_decode_stream_error_mid_stream(gpu, codec):
     assert st.as_tuple() == ost.as_tuple() and got == bad
     k = bad * schema.record_size
     assert np.array_equal(rec.cpu().numpy()[:k], orec[:k])
+
+
+@pytest.mark.parametrize("sname,proto", [("mixed", 2), ("mixed", 0), ("nested", 0)])
+def test_onepass_index(gpu, sname, proto, monkeypatch):
+    """The single-pass index (TGPU_INDEX_ONEPASS=1: look-back over packed tile
+    statuses, k_index.hip launch_index_onepass) gives the oracle's offsets and
+    records, whole and as speculative byte ranges; a malformed record makes it
+    fall back to the two-pass index, which reports the reference status."""
+    monkeypatch.setenv("TGPU_INDEX_ONEPASS", "1")
+    n = 300_000 if sname == "mixed" else 100_000
+    schema, wire, woffs = _stream(sname, proto, n, seed=3)
+    gs = _gs(schema)
+    w = _t(wire, gpu)
+    offs, got, first, last, st = _ser(proto).index_stream(gs, w)
+    assert (st.code, got, first, last) == (0, n, 0, len(wire))
+    assert np.array_equal(offs.cpu().numpy().astype(np.uint64), woffs)
+    rec, arena, st2, nd, cons = _ser(proto).deserialize_status(gs, w[: len(wire)], n)
+    ost, orec, oarena, ond, ocons = oracle.decode(schema, proto, wire, n)
+    assert st2.as_tuple() == ost.as_tuple() and (nd, cons) == (ond, ocons)
+    assert np.array_equal(rec.cpu().numpy(), orec)
+    L = len(wire)
+    b, e = L // 3 + 7, 2 * L // 3 + 5
+    offs, got, first, last, st = _ser(proto).index_stream(gs, w[:L], begin=b, end=e,
+                                                          speculative=True)
+    inside = woffs[(woffs >= b) & (woffs < e)]
+    assert st.code == 0 and first == inside[0] and got == inside.size
+    assert last == woffs[np.searchsorted(woffs, e)]
+    bad = n // 2
+    wb = bytearray(wire)
+    wb[int(woffs[bad])] = 0x1E if proto == 2 else 0x7F  # an unknown field type
+    wb = bytes(wb)
+    rec, arena, st3, nd, cons = _ser(proto).deserialize_status(gs, _t(wb, gpu)[:L], n)
+    ost, orec, _, ond, ocons = oracle.decode(schema, proto, wb, n)
+    assert st3.as_tuple() == ost.as_tuple() and (nd, cons) == (ond, ocons)
+    k = (ond + 1) * schema.size[0]
+    assert np.array_equal(rec.cpu().numpy()[:k], orec[:k])

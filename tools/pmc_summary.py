@@ -14,7 +14,9 @@ counters by the factor of the access width it issues:
   plan_binary_decode_kernel : reads 16 B/lane (LDS-DMA), writes 8 B/lane
   plan_binary_encode_kernel : reads 8 B/lane, writes 16 B/lane
 
-usage: pmc_summary.py PMC_ROOT RECORDS_PER_LAUNCH [OUT.json]
+usage: pmc_summary.py PMC_ROOT RECORDS_PER_LAUNCH [OUT.json]   (config 2's plan kernels)
+       pmc_summary.py PMC_ROOT --config C   (tools/pmc_config.sh: every kernel of config C
+                                             -> profiles/pmc_cC.json)
   PMC_ROOT holds fetch_calib/, write_calib/ (pmc_calib.py) and fetch_bench/,
   write_bench/ (bench.py) rocprofv3 output directories.
 """
@@ -46,7 +48,65 @@ def load(d, counter):
     return out
 
 
+def main_config(root, config):
+    """Every kernel of one bench config (tools/pmc_config.sh): all of them
+    read their input with 16-byte LDS-DMA / vector loads and store 16-byte
+    vectors (offsets: 8-byte stores, same calibration factors), so the 16-byte
+    factors apply. Records per launch and the decode / encode kernels'
+    algorithmic bytes come from the bench line of the FETCH pass."""
+    out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "profiles", "pmc_c%d.json" % config)
+    line = None
+    with open(os.path.join(root, "fetch_bench.log")) as fh:
+        for ln in fh:
+            if ln.startswith("{") and '"metric"' in ln:
+                line = json.loads(ln)
+    if line is None:
+        raise SystemExit("no bench line in fetch_bench.log")
+    n = line["config"]["records_per_gpu"]
+    wire = line["config"]["wire_bytes_per_record"]
+    rec = line["config"]["record_bytes"]
+    roof = line["roofline"]
+    algo = {roof["kernel"]: roof["algorithmic_bytes_per_launch"] / n}
+    if "encode" in roof:
+        algo[roof["encode"]["kernel"]] = roof["encode"]["algorithmic_bytes_per_launch"] / n
+    algo.setdefault("tgpu_jit_index_spec", wire)
+    algo.setdefault("index_tile_spec_kernel", wire)
+    fetch = load(os.path.join(root, "fetch_bench"), "FETCH_SIZE")
+    write = load(os.path.join(root, "write_bench"), "WRITE_SIZE")
+    cfetch = load(os.path.join(root, "fetch_calib"), "FETCH_SIZE")
+    cwrite = load(os.path.join(root, "write_calib"), "WRITE_SIZE")
+
+    def avg(v):
+        return sum(v) / len(v)
+
+    ff = CALIB_BYTES / (avg(cfetch["copy_kernel"]) * 1024)
+    wf = CALIB_BYTES / (avg(cwrite["copy_kernel"]) * 1024)
+    res = {"config": config, "records_per_launch": n, "wire_bytes_per_record": wire,
+           "record_bytes": rec, "calibration": {"bytes": CALIB_BYTES, "fetch_factor": round(ff, 4),
+                                                "write_factor": round(wf, 4)},
+           "bench_value": line["value"], "bench_unit": line["unit"]}
+    for k in sorted(set(fetch) & set(write)):
+        fb = avg(fetch[k]) * 1024 * ff
+        wb = avg(write[k]) * 1024 * wf
+        if fb + wb < 64 * n:  # bookkeeping kernels: skip
+            continue
+        d = {"fetch_bytes": int(fb), "write_bytes": int(wb), "raw_fetch_kib": avg(fetch[k]),
+             "raw_write_kib": avg(write[k]), "dispatches": [len(fetch[k]), len(write[k])],
+             "fetch_bytes_per_record": round(fb / n, 3), "write_bytes_per_record": round(wb / n, 3),
+             "hbm_bytes_per_record": round((fb + wb) / n, 3)}
+        if k in algo:
+            d["algorithmic_bytes_per_record"] = round(algo[k], 3)
+            d["traffic_over_algorithmic"] = round((fb + wb) / n / algo[k], 4)
+        res[k] = d
+    with open(out_path, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res, indent=1))
+
+
 def main():
+    if len(sys.argv) > 3 and sys.argv[2] == "--config":
+        return main_config(sys.argv[1], int(sys.argv[3]))
     root, n = sys.argv[1], int(sys.argv[2])
     out_path = sys.argv[3] if len(sys.argv) > 3 else os.path.join(
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_latest.json")
