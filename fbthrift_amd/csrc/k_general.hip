@@ -363,9 +363,12 @@ hipError_t launch_serial_decode(const DecodeArgs& a, int protocol, bool from_irr
 
 hipError_t launch_fixed_exceptions(const DecodeArgs& a, int protocol, uint64_t L,
                                    hipStream_t stream) {
-  const uint32_t g = grid_for(a.exc_cap < a.n ? a.exc_cap : a.n);
-  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(fixed_exception_kernel<P_>, dim3(g), dim3(256), 0,
-                                                stream, a, L));
+  // a small grid striding over the list: usually empty, and a launch of
+  // thousands of workgroups that only read the count cost 29 us
+  const uint64_t most = a.exc_cap < a.n ? a.exc_cap : a.n;
+  const uint32_t g = (uint32_t)std::min<uint64_t>((most + 255) / 256, 256);
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(fixed_exception_kernel<P_>, dim3(g ? g : 1),
+                                                dim3(256), 0, stream, a, L));
   hipLaunchKernelGGL(fixed_exception_resolve_kernel, dim3(1), dim3(1), 0, stream, a.res, a.exc_cap);
   return hipGetLastError();
 }

@@ -76,6 +76,15 @@ __device__ __forceinline__ unsigned long long decode_word(const FixedPlan* P,
   return v;
 }
 
+// The rare path of a word the plan cannot take (kept out of the wave-uniform
+// main loop: no ballot there).
+__device__ __attribute__((noinline)) void note_word_exception(uint64_t i, DevResult* res,
+                                                              uint64_t* exc, uint64_t cap) {
+  atomicMin(&res->first_irregular, (unsigned long long)i);
+  const unsigned long long k = atomicAdd(&res->n_irregular, 1ull);
+  if (k < cap) exc[k] = i;
+}
+
 // T records (= threads) per tile. kGlds: stage through LDS-DMA
 // (global_load_lds_dwordx4) instead of registers. kPair: 16-byte stores of
 // two consecutive words. kNT: non-temporal stores (output is never re-read).
@@ -89,11 +98,6 @@ __global__ __launch_bounds__(T) void plan_binary_decode_kernel(
   const uint64_t tile0 = (uint64_t)blockIdx.x * T;
   const uint32_t nrec = (uint32_t)min((uint64_t)T, n - tile0);
   FixedPlan* P = (FixedPlan*)(smem + wire_region(T, L));
-  // records of the tile a word of which the plan could not take (several
-  // threads may mark one record)
-  uint8_t* bad = smem + wire_region(T, L) + sizeof(FixedPlan);
-  bad[threadIdx.x] = 0;
-  bool any_bad = false;
 
   // stage the wire tile (16-byte phase of the stream preserved)
   const uint8_t* g = in + tile0 * L;
@@ -130,10 +134,9 @@ __global__ __launch_bounds__(T) void plan_binary_decode_kernel(
       const unsigned long long v = decode_word(P, w32, sh + r * L, j, ok);
       if (kNT) __builtin_nontemporal_store(v, o + q);
       else o[q] = v;
-      if (!ok) {
-        bad[r] = 1;
-        any_bad = true;
-      }
+      // a record one of whose words the plan cannot take joins the exception
+      // list (once per word that failed: duplicates read the same record again)
+      if (!ok) note_word_exception(tile0 + r, res, exc, exc_cap);
       r += sr;
       j += sj;
       if (j >= Q) {
@@ -158,14 +161,8 @@ __global__ __launch_bounds__(T) void plan_binary_decode_kernel(
       } else {
         o[q] = v0;
       }
-      if (!ok0) {
-        bad[r] = 1;
-        any_bad = true;
-      }
-      if (!ok1) {
-        bad[r1] = 1;
-        any_bad = true;
-      }
+      if (!ok0) note_word_exception(tile0 + r, res, exc, exc_cap);
+      if (!ok1) note_word_exception(tile0 + r1, res, exc, exc_cap);
       r += sr;
       j += sj;
       if (j >= Q) {
@@ -173,10 +170,6 @@ __global__ __launch_bounds__(T) void plan_binary_decode_kernel(
         ++r;
       }
     }
-  }
-  if (__syncthreads_or(any_bad)) {
-    const uint32_t k = threadIdx.x;
-    prog::note_exception(k < nrec && bad[k], tile0 + k, res, exc, exc_cap);
   }
 }
 
@@ -355,7 +348,7 @@ hipError_t launch_plan_binary_decode(const FixedPlan* p, const FixedPlan* d_p, c
   DecVariant use = v;
   if (((uintptr_t)out & 15) != 0) use.pair = 0;  // 16-byte stores need 16-byte records base
   const uint64_t blocks = (n + use.T - 1) / use.T;
-  const uint32_t lds = wire_region(use.T, p->wire_len) + (uint32_t)sizeof(FixedPlan) + use.T;
+  const uint32_t lds = wire_region(use.T, p->wire_len) + (uint32_t)sizeof(FixedPlan);
   auto* o = (unsigned long long*)out;
   switch (use.T) {
     case 128: return launch_dec_T<128>(use, lds, blocks, stream, d_p, in, n, o, res, exc, exc_cap);

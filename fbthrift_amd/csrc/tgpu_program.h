@@ -30,9 +30,10 @@ namespace prog {
 // A fixed-stride batch (record i at i * L): record i is one the fast kernel
 // could not take. It latches first_irregular and joins the exception list
 // (irr[0 .. cap), count in n_irregular) that fixed_exception_kernel reads at
-// the record's stride position. Called by every lane of a wave together (a
-// lane passes flag = false when it has nothing), with i increasing with the
-// lane: one atomic per wave, the lowest flagged lane's i is the minimum.
+// the record's stride position. Called by the active lanes of a wave together
+// (a lane passes flag = false when it has nothing), with i non-decreasing with
+// the lane: one atomic per wave, the lowest flagged lane's i is the minimum.
+// A record may be listed more than once (the reads are idempotent).
 __device__ __forceinline__ void note_exception(bool flag, uint64_t i, DevResult* res,
                                                uint64_t* irr, uint64_t cap) {
   const uint64_t m = __ballot(flag);
