@@ -118,10 +118,18 @@ __device__ __forceinline__ uint64_t bswap_n(uint64_t x, uint32_t width) {
 // LEB128 at p (VarintUtils-inl.h:94-134): up to 8 bytes from one window,
 // 9-10 byte i64 varints byte-wise. Returns false (irregular) on anything the
 // fast path does not take (past `end`, more than ceil(bits/7) bytes).
+// w: the 8 bytes at p (a caller's cached window), or read here.
+template <class Src>
+__device__ __forceinline__ bool read_varint_w(const Src& src, uint64_t w, uint32_t& p,
+                                              uint32_t end, uint32_t bits, uint64_t& v);
 template <class Src>
 __device__ __forceinline__ bool read_varint(const Src& src, uint32_t& p, uint32_t end,
                                             uint32_t bits, uint64_t& v) {
-  const uint64_t w = src.win8(p);
+  return read_varint_w(src, src.win8(p), p, end, bits, v);
+}
+template <class Src>
+__device__ __forceinline__ bool read_varint_w(const Src& src, uint64_t w, uint32_t& p,
+                                              uint32_t end, uint32_t bits, uint64_t& v) {
   const uint64_t stop = ~w & 0x8080808080808080ull;
   if (stop) {
     const uint32_t len = ((uint32_t)__builtin_ctzll(stop) >> 3) + 1;
@@ -278,26 +286,54 @@ __device__ __forceinline__ bool skip_unknown_tail(const VOp op, const bool compa
   return false;
 }
 
+// The last 8-byte window a record's walk read. With TGPU_WINCACHE an op whose
+// bytes lie inside it takes them from there (a Compact field header and its
+// varint share one window: about one dependent LDS read per field instead of
+// one per op). Measured slower (decode config 3 1.47 -> 1.51 ms, config 4
+// 2.50 -> 2.69, config 5 6.70 -> 6.88; tools/kbench_jit.py), so off: every op
+// reads its own window.
+struct Win {
+  uint64_t w = 0;
+  uint32_t wp = 0;
+  bool valid = false;
+  template <class Src>
+  __device__ __forceinline__ uint64_t at(const Src& src, uint32_t p, uint32_t need) {
+#ifdef TGPU_WINCACHE
+    const uint32_t d = p - wp;
+    if (valid && d + need <= 8) return w >> (8 * d);
+#endif
+    w = src.win8(p);
+    wp = p;
+    valid = true;
+    return w;
+  }
+};
+
 // One op of the program at p (bounded by end); false = irregular.
 template <bool kStore, class Src>
 __device__ __forceinline__ bool run_op(const VOp op, const bool compact, const Src& src,
-                                       const Ctx& c, uint32_t& p, uint32_t end, uint8_t* rec) {
+                                       const Ctx& c, uint32_t& p, uint32_t end, uint8_t* rec,
+                                       Win& W) {
   switch (op.kind) {
     case VOP_CONST: {
       if (p + op.hdr_len > end) return false;
-      const uint32_t lo = (uint32_t)src.win8(p);
+      const uint32_t lo = (uint32_t)W.at(src, p, op.hdr_len);
       const uint32_t mask = op.hdr_len >= 4 ? 0xffffffffu : ((1u << (8 * op.hdr_len)) - 1);
       if ((lo ^ op.hdr) & mask) {
+#ifdef TGPU_NO_TAILS  // a compiled strict program (tgpu_jit.cpp)
+        return false;
+#else
         if (op.elem_kind != kStopSkipsUnknown) return false;
         if (!skip_unknown_tail(op, compact, src, c, p, end)) return false;
         break;
+#endif
       }
       p += op.hdr_len;
       break;
     }
     case VOP_CBOOL: {
       if (p + op.hdr_len > end) return false;
-      const uint32_t lo = (uint32_t)src.win8(p);
+      const uint32_t lo = (uint32_t)W.at(src, p, op.hdr_len);
       const uint32_t mask = (op.hdr_len >= 4 ? 0xffffffffu : ((1u << (8 * op.hdr_len)) - 1)) & ~0xfu;
       const uint32_t ct = lo & 0xf;
       if (((lo ^ op.hdr) & mask) || (ct != 1 && ct != 2)) return false;
@@ -307,7 +343,7 @@ __device__ __forceinline__ bool run_op(const VOp op, const bool compact, const S
     }
     case VOP_FIXED: {
       if (p + op.width > end) return false;
-      const uint64_t v = bswap_n(src.win8(p), op.width);
+      const uint64_t v = bswap_n(W.at(src, p, op.width), op.width);
       if (op.is_bool && v > 1) return false;  // readBool throws: general path
       if (kStore) store_n(rec + op.member, v, op.width);
       p += op.width;
@@ -315,7 +351,8 @@ __device__ __forceinline__ bool run_op(const VOp op, const bool compact, const S
     }
     case VOP_VARINT: {
       uint64_t z;
-      if (!read_varint(src, p, end, op.bits, z)) return false;
+      if (!read_varint_w(src, W.at(src, p, op.bits == 32 ? 5 : 8), p, end, op.bits, z))
+        return false;
       if (kStore) store_n(rec + op.member, unzigzag(z, op.bits), op.width);
       break;
     }
@@ -323,11 +360,11 @@ __device__ __forceinline__ bool run_op(const VOp op, const bool compact, const S
       int64_t len;
       if (compact) {
         uint64_t z;
-        if (!read_varint(src, p, end, 32, z)) return false;
+        if (!read_varint_w(src, W.at(src, p, 5), p, end, 32, z)) return false;
         len = (int32_t)(uint32_t)z;
       } else {
         if (p + 4 > end) return false;
-        len = (int32_t)(uint32_t)bswap_n(src.win8(p), 4);
+        len = (int32_t)(uint32_t)bswap_n(W.at(src, p, 4), 4);
         p += 4;
       }
       if (len < 0 || (c.string_limit > 0 && len > c.string_limit) || len > (int64_t)(end - p))
@@ -345,7 +382,7 @@ __device__ __forceinline__ bool run_op(const VOp op, const bool compact, const S
       int64_t n;
       if (compact) {
         if (p + 1 > end) return false;
-        const uint32_t b = (uint32_t)(src.win8(p) & 0xff);
+        const uint32_t b = (uint32_t)(W.at(src, p, 1) & 0xff);
         const uint32_t ct = b & 0xf;
         const bool ok_ct = op.elem_ttype == TGPU_T_BOOL ? (ct == 1 || ct == 2) : ct == op.elem_ct;
         if (!ok_ct) return false;
@@ -358,7 +395,7 @@ __device__ __forceinline__ bool run_op(const VOp op, const bool compact, const S
         }
       } else {
         if (p + 5 > end) return false;
-        const uint64_t w = src.win8(p);
+        const uint64_t w = W.at(src, p, 5);
         if ((w & 0xff) != op.elem_ttype) return false;
         n = (int32_t)(uint32_t)bswap_n(w >> 8, 4);
         p += 5;
@@ -420,7 +457,8 @@ __device__ __forceinline__ bool run_program(const PP& P, const Src& src, const C
                                             uint32_t& pos, uint32_t end, uint8_t* rec) {
   const bool compact = P.protocol() == TGPU_PROTOCOL_COMPACT;
   uint32_t p = pos;
-  if (!all_ops(P, [&](const VOp op) { return run_op<kStore>(op, compact, src, c, p, end, rec); }))
+  Win W;
+  if (!all_ops(P, [&](const VOp op) { return run_op<kStore>(op, compact, src, c, p, end, rec, W); }))
     return false;
   pos = p;
   return true;
