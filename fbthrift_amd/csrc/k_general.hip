@@ -138,6 +138,7 @@ __global__ void fixed_probe_kernel(DecodeArgs a, uint64_t L) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const Reader r = decode_record<P>(a, 0, -1, 0);
   a.res->first_misfit = (r.ok() && r.pos == L) ? kNone : 0;
+  a.res->total_bytes = r.ok() ? r.pos : 0;  // record 0's length (the caller's second stride)
 }
 
 // Unindexed streams the fixed-layout path cannot take: one lane reads the

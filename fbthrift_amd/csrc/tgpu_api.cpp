@@ -823,7 +823,7 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
 // known (the record-0 probe), else read from the device result.
 int fixed_tail(tgpu_context* ctx, const tgpu_schema* schema, int protocol, const DecodeArgs& a,
                uint64_t L, const tgpu_limits* limits, hipStream_t s, hipError_t& e,
-               uint64_t first = ~0ull) {
+               uint64_t first = ~0ull, bool tolerant = false) {
   uint64_t irr = first;
   if (first == ~0ull) {
     if (e == hipSuccess)
@@ -846,7 +846,7 @@ int fixed_tail(tgpu_context* ctx, const tgpu_schema* schema, int protocol, const
   // record carries appended fields, which the tolerant programs take
   const int rc = launch_index(ctx, schema, protocol, a.in, a.in_len, irr * L, a.in_len, 0,
                               ctx->d_offs + irr, t.n, t.n, limits, s, e, &t, &fused,
-                              first == 0, true);
+                              first == 0 || tolerant, true);
   if (rc) {
     e = hipErrorOutOfMemory;
     return 0;
@@ -1304,12 +1304,43 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
       if (e == hipSuccess) e = hipStreamSynchronize(s);
       if (e == hipSuccess && ctx->h_res->first_misfit == 0) {
         a.offs = ctx->d_offs;
-        const int trc = fixed_tail(ctx, schema, protocol, a, fixed, limits, s, e, 0);
+        // record 0's length: a stream of records that all carry the same
+        // appended fields is fixed-stride too, at this length — the tolerant
+        // program decodes record i at i * L2, the exception list and the
+        // misfit rule work as at L, and a stream that is not takes the index
+        // from its first misfit
+        const uint64_t L2 = ctx->h_res->total_bytes;
+        const int32_t height = a.height ? a.height : a.max_depth;
+        const bool stride2 = L2 && L2 != fixed && L2 <= (1ull << 20) && n * L2 <= in_len &&
+                             has_prog(schema, protocol) && height >= 2 && a.max_depth >= 2;
+        int trc;
+        uint64_t len = fixed;
+        if (stride2) {
+          const int q = prog_protocol(schema, protocol);
+          DecodeArgs f = a;
+          f.fixed_len = len = L2;
+          e = launch_result_init(ctx->d_res, n, s);
+          if (e == hipSuccess)
+            e = launch_program_decode(
+                f, schema->d_prog_tol[q], a.rec_size, ctx->d_irr, &ctx->d_res->n_irregular, s,
+                jit_kernels(schema->prog_tol[q], schema->device, JIT_DECODE, n, 0, false));
+          if (e == hipSuccess) e = launch_fixed_exceptions(f, protocol, L2, s);
+          // (the tail after a misfit is indexed: its decode is not fixed-stride)
+          trc = fixed_tail(ctx, schema, protocol, a, L2, limits, s, e, ~0ull, true);
+        } else {
+          trc = fixed_tail(ctx, schema, protocol, a, fixed, limits, s, e, 0);
+        }
         ctx->last_op = 1;
         if (e != hipSuccess || trc < 0) {
           fill_status(st, TGPU_ERR_HIP, 0, 0);
           if (st) st->reserved = (int32_t)e;
           return TGPU_ERR_HIP;
+        }
+        if (trc == 0) {  // every record at its stride L2
+          fill_status(st, TGPU_OK, n, 0);
+          if (n_decoded) *n_decoded = n;
+          if (consumed) *consumed = n * len;
+          return TGPU_OK;
         }
         tgpu_status tmp;
         return tgpu_context_wait(ctx, stream, st ? st : &tmp, n_decoded, consumed);

@@ -161,3 +161,33 @@ def test_exception_then_length_change(gpu, sync):
     w = np.concatenate([w[: 89 * 5000], extra, w[89 * 5001:]])
     st, nd = run(gpu, w, n, sync)
     assert st.code == 0 and nd == n
+
+
+def test_every_record_extra_field_then_change(gpu):
+    """A stream at a second stride (every record + one appended field) whose
+    records change shape again at 600k (an appended string instead): the
+    tolerant program decodes at the second stride up to there, the stream is
+    indexed from the first record off it."""
+    _, wire = canonical(N)
+    w = with_extra_field(wire).reshape(N, 96).copy()
+    k = 600_000
+    tail = wire.reshape(N, 89)[k:]
+    extra = np.zeros((N - k, 89 + 3 + 4 + 5), np.uint8)
+    extra[:, :88] = tail[:, :88]
+    extra[:, 88:91] = (11, 0, 21)          # field 21: string
+    extra[:, 91:95] = (0, 0, 0, 5)         # length 5
+    extra[:, 95:100] = tail[:, 3:8]
+    extra[:, 100] = 0
+    s = np.concatenate([w[:k].reshape(-1), extra.reshape(-1)])
+    st, nd = run(gpu, s, N)
+    assert st.code == 0 and nd == N
+
+
+def test_second_stride_with_error(gpu):
+    """A bad record (an unknown field type) deep in a second-stride stream:
+    the reference status at that record."""
+    _, wire = canonical(200_000)
+    w = with_extra_field(wire).copy()
+    j = 150_001
+    w[96 * j + 88] = 0x7F
+    run(gpu, w, 200_000)
