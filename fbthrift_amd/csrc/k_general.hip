@@ -83,9 +83,12 @@ __global__ __launch_bounds__(256) void general_decode_tile_kernel(DecodeArgs a,
   __syncthreads();
   const uint64_t i = r0 + threadIdx.x;
   if (i >= a.n) return;
-  Reader r = staged ? decode_record<P>(a, i, -1, kIndexed, tile, a0, b1)
-                    : decode_record<P>(a, i, -1);
-  if (staged && !r.ok() && r.err != kErrDeep) r = decode_record<P>(a, i, -1);
+  // one decode_record call site (the copy, then HBM when the copy failed)
+  Reader r;
+  for (int from_lds = staged ? 1 : 0;; from_lds = 0) {
+    r = decode_record<P>(a, i, -1, kIndexed, from_lds ? tile : nullptr, a0, b1);
+    if (!from_lds || r.ok() || r.err == kErrDeep) break;
+  }
   if (!r.ok()) defer_or_fail(r, a.deep, &a.res->first_fail, i);
 }
 

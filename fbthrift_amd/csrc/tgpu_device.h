@@ -515,8 +515,28 @@ __device__ void skip(Reader& r, uint32_t type, int32_t depth) {
 }
 
 // ------------------------------------------------------------ struct read ---
+// Stores in the widest units the alignment allows: the general reader's slots
+// (records, arena elements, pairs) are 8-byte aligned with sizes that are
+// mostly multiples of 8, and byte stores to them were its main cost (the
+// nested leg's decode).
 __device__ __forceinline__ void zero_bytes(uint8_t* p, uint32_t n) {
-  for (uint32_t b = 0; b < n; ++b) p[b] = 0;
+  uint32_t b = 0;
+  if (((uintptr_t)p & 7) == 0)
+    for (; b + 8 <= n; b += 8) *(uint64_t*)(p + b) = 0;
+  for (; b < n; ++b) p[b] = 0;
+}
+// dst <- src for n bytes (src: a private buffer, 8-byte aligned).
+__device__ __forceinline__ void copy_bytes(uint8_t* dst, const uint8_t* src, uint32_t n) {
+  uint32_t b = 0;
+  const uintptr_t a = (uintptr_t)dst;
+  if ((a & 7) == 0) {
+    for (; b + 8 <= n; b += 8) *(uint64_t*)(dst + b) = *(const uint64_t*)(src + b);
+  } else if ((a & 3) == 0) {
+    for (; b + 4 <= n; b += 4) *(uint32_t*)(dst + b) = *(const uint32_t*)(src + b);
+  }
+  if (((a + b) & 1) == 0)
+    for (; b + 2 <= n; b += 2) *(uint16_t*)(dst + b) = *(const uint16_t*)(src + b);
+  for (; b < n; ++b) dst[b] = src[b];
 }
 
 // A container's element (list/set) or key/value (map) types, from a
@@ -580,8 +600,7 @@ __device__ __forceinline__ void read_elem(Reader& r, uint32_t t, uint8_t* dst) {
     Proto<P>::read_string(r, v, l);
     if (r.ok()) {
       const tgpu_span e{l ? v : 0, l, 0};
-      const uint8_t* b = (const uint8_t*)&e;
-      for (uint32_t k = 0; k < 16; ++k) dst[k] = b[k];
+      copy_bytes(dst, (const uint8_t*)&e, 16);
     }
     return;
   }
@@ -642,14 +661,14 @@ __device__ void read_list(Reader& r, const CType& c, uint8_t* m, Arena& A) {
         // read first: a truncated stream fails as the reader does, and an
         // element that was read always fits an arena of the documented size
         const uint64_t at = aoff + (uint64_t)i * es;
-        uint8_t tmp[16];
+        alignas(8) uint8_t tmp[16];
         read_elem<P>(r, c.elem, tmp);
         if (!r.ok()) break;
         if (at + es > arena_cap) {
           r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
           break;
         }
-        for (uint32_t b = 0; b < es; ++b) arena[at + b] = tmp[b];
+        copy_bytes(arena + at, tmp, es);
       }
       if (!r.ok()) {
         if (c.ttype == TGPU_T_SET) {
@@ -662,8 +681,7 @@ __device__ void read_list(Reader& r, const CType& c, uint8_t* m, Arena& A) {
           // non-trivial elements: reserve + emplace_back_default + read
           // (protocol_methods.h:374-386,458-461): the failing element is
           // in the list, empty (readString throws before assigning)
-          if (at_ok(aoff, i, es, arena_cap))
-            for (uint32_t b = 0; b < es; ++b) arena[aoff + (uint64_t)i * es + b] = 0;
+          if (at_ok(aoff, i, es, arena_cap)) zero_bytes(arena + aoff + (uint64_t)i * es, es);
           sp.length = (uint32_t)(i + 1);
           *(tgpu_span*)m = sp;
         } else {
@@ -671,7 +689,7 @@ __device__ void read_list(Reader& r, const CType& c, uint8_t* m, Arena& A) {
           for (; i < n; ++i) {
             const uint64_t at = aoff + (uint64_t)i * es;
             if (at + es > arena_cap) break;
-            for (uint32_t b = 0; b < es; ++b) arena[at + b] = 0;
+            zero_bytes(arena + at, es);
           }
         }
       }
@@ -716,7 +734,7 @@ __device__ void read_map(Reader& r, const CType& c, uint8_t* m, Arena& A) {
     const uint64_t aoff = (n > 0 && !discard) ? A.alloc(r.pos, (uint64_t)(uint32_t)n * ps) : 0;
     int32_t i = 0;
     for (; i < n; ++i) {
-      uint8_t pr[32];
+      alignas(8) uint8_t pr[32];
       read_elem<P>(r, c.elem, pr);
       if (!r.ok()) break;
       read_elem<P>(r, c.val, pr + ks);
@@ -727,7 +745,7 @@ __device__ void read_map(Reader& r, const CType& c, uint8_t* m, Arena& A) {
         r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
         break;
       }
-      for (uint32_t b = 0; b < ps; ++b) A.base[at + b] = pr[b];
+      copy_bytes(A.base + at, pr, ps);
     }
     if (i > 0 && !discard) {
       sp.offset = aoff;
@@ -784,9 +802,11 @@ __device__ __forceinline__ void child_done(const DevSchema& sc, ReadFrame& p, co
 // Opens the container value of type c at member / element slot m: simple
 // elements are read here (returns true: done), elements that are structs
 // or containers get a frame (returns false).
+// depth: frames open below this container's frame (its level for the
+// measuring reads' per-level slots).
 template <int P>
 __device__ bool open_container(Reader& r, const DevSchema& sc, const CType& c, uint8_t* m,
-                               Arena& A, ReadFrame* st, int& sp) {
+                               Arena& A, int depth, ReadFrame& f) {
   using Pr = Proto<P>;
   const bool is_map = c.ttype == TGPU_T_MAP;
   const uint32_t et = is_map ? c.val : c.elem;
@@ -822,7 +842,7 @@ __device__ bool open_container(Reader& r, const DevSchema& sc, const CType& c, u
     r.ascend();
     return true;
   }
-  if (sp == kMaxSchemaDepth) {
+  if (depth + 1 >= kMaxSchemaDepth) {
     r.fail(TGPU_ERR_UNSUPPORTED, r.pos);
     return true;
   }
@@ -831,7 +851,7 @@ __device__ bool open_container(Reader& r, const DevSchema& sc, const CType& c, u
   uint8_t* arr;
   uint32_t stride = es;
   if (A.discard()) {
-    arr = A.nest + (uint64_t)sp * A.nest_slot;  // one reused slot per level
+    arr = A.nest + (uint64_t)(depth + 1) * A.nest_slot;  // one reused slot per level
     stride = 0;
   } else {
     if (!A.base) {
@@ -846,7 +866,6 @@ __device__ bool open_container(Reader& r, const DevSchema& sc, const CType& c, u
     }
     arr = A.base + aoff;
   }
-  ReadFrame& f = st[sp++];
   f.kind = is_map ? RF_MAP : RF_LIST;
   f.is_set = c.ttype == TGPU_T_SET;
   f.etype = (uint8_t)et;
@@ -863,29 +882,40 @@ __device__ bool open_container(Reader& r, const DevSchema& sc, const CType& c, u
 }
 
 // Reads one record into rec (zeroed by the caller). A.bump: the record's
-// region start when A.regions.
+// region start when A.regions. The open frame `fr` lives in registers; the
+// frames below it are saved in `st` (sp of them) only while a child is open
+// (a per-iteration reload of the whole frame from scratch was the general
+// reader's main cost).
+__device__ __forceinline__ ReadFrame struct_frame(int32_t si, uint8_t* obj) {
+  ReadFrame f;
+  f.kind = RF_STRUCT;
+  f.is_set = 0;
+  f.etype = f.ktype = 0;
+  f.si = si;
+  f.obj = obj;
+  f.prev = 0;
+  f.nread = 0;
+  f.fidx = 0;
+  f.seen = 0;
+  f.ti = 0;
+  f.n = f.i = f.es = f.ks = 0;
+  f.span = nullptr;
+  return f;
+}
+
 template <int P>
 __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, Arena& A) {
   using Pr = Proto<P>;
-  ReadFrame st[kMaxSchemaDepth];
-  int sp = 0;
-  {
-    ReadFrame& f = st[sp++];
-    f.kind = RF_STRUCT;
-    f.si = 0;
-    f.obj = rec;
-    f.prev = 0;
-    f.nread = 0;
-    f.fidx = 0;
-    f.seen = 0;
-  }
-  while (sp > 0 && r.ok()) {
-    ReadFrame& fr = st[sp - 1];
+  ReadFrame st[kMaxSchemaDepth - 1];
+  int sp = 0;  // frames saved below fr
+  ReadFrame fr = struct_frame(0, rec);
+  while (r.ok()) {
     if (fr.kind != RF_STRUCT) {
       if (fr.i == fr.n) {  // readListEnd / readMapEnd
         r.ascend();
-        --sp;
-        if (sp > 0) child_done(sc, st[sp - 1], A);
+        if (sp == 0) return;
+        fr = st[--sp];
+        child_done(sc, fr, A);
         continue;
       }
       const uint32_t esz = fr.es ? fr.es : (fr.ks + slot_size(sc, fr.etype, fr.si));
@@ -900,17 +930,17 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, Arena&
         set_span_len(fr.span, fr.obj, A.base, fr.i + 1);  // emplace_back_default
       }
       if (fr.etype == TGPU_T_STRUCT) {
-        if (sp == kMaxSchemaDepth) return r.fail(TGPU_ERR_UNSUPPORTED, r.pos);
-        ReadFrame& f = st[sp++];
-        f.kind = RF_STRUCT;
-        f.si = fr.si;
-        f.obj = val;
-        f.prev = 0;
-        f.nread = 0;
-        f.fidx = 0;
-        f.seen = 0;
-      } else if (open_container<P>(r, sc, ctype_node(sc, fr.ti), val, A, st, sp)) {
-        if (r.ok()) child_done(sc, fr, A);
+        if (sp + 1 >= kMaxSchemaDepth) return r.fail(TGPU_ERR_UNSUPPORTED, r.pos);
+        st[sp++] = fr;
+        fr = struct_frame(fr.si, val);
+      } else {
+        ReadFrame nf;
+        if (open_container<P>(r, sc, ctype_node(sc, fr.ti), val, A, sp, nf)) {
+          if (r.ok()) child_done(sc, fr, A);
+        } else {
+          st[sp++] = fr;
+          fr = nf;
+        }
       }
       continue;
     }
@@ -930,19 +960,29 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, Arena&
             return r.fail(TGPU_ERR_MISSING_REQUIRED_FIELD, r.pos);
       }
       // STOP: struct done
-      --sp;
-      if (sp > 0) child_done(sc, st[sp - 1], A);
+      if (sp == 0) return;
+      fr = st[--sp];
+      child_done(sc, fr, A);
       continue;
     }
     // a union's one field must be followed by STOP (throwUnionMissingStop)
     if (un && fr.nread) return r.fail(TGPU_ERR_UNION_MISSING_STOP, r.pos);
     ++fr.nread;
     fr.prev = id;
+    // the expected field first (fields in declaration order: the generated
+    // reader's fast path), then a scan
     int32_t hit = -1;
-    for (uint32_t k = 0; k < sd.num_fields; ++k) {
-      if (sc.f[sd.first_field + k].id == id) {
-        hit = (int32_t)(sd.first_field + k);
-        break;
+    {
+      const uint32_t guess = fr.fidx ? fr.fidx + 1 - sd.first_field : 0;
+      if (guess < sd.num_fields && sc.f[sd.first_field + guess].id == id) {
+        hit = (int32_t)(sd.first_field + guess);
+      } else {
+        for (uint32_t k = 0; k < sd.num_fields; ++k) {
+          if (sc.f[sd.first_field + k].id == id) {
+            hit = (int32_t)(sd.first_field + k);
+            break;
+          }
+        }
       }
     }
     if (hit < 0 || sc.f[hit].ttype != wt) {
@@ -951,6 +991,7 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, Arena&
     }
     const tgpu_field_desc f = sc.f[hit];
     uint8_t* m = fr.obj + f.member_offset;
+    fr.fidx = (uint32_t)hit;
     if (un) {  // field_ref().emplace(): a fresh member becomes active
       zero_bytes(fr.obj, sd.size);
       fr.obj[f.isset_offset] = 1;
@@ -963,20 +1004,17 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, Arena&
       Pr::read_string(r, v, l);
       if (r.ok()) *(tgpu_span*)m = tgpu_span{l ? v : 0, l, 0};
     } else if (f.ttype == TGPU_T_STRUCT) {
-      if (sp == kMaxSchemaDepth) return r.fail(TGPU_ERR_UNSUPPORTED, r.pos);
-      fr.fidx = (uint32_t)hit;
-      ReadFrame& nf = st[sp++];
-      nf.kind = RF_STRUCT;
-      nf.si = f.struct_index;
-      nf.obj = m;
-      nf.prev = 0;
-      nf.nread = 0;
-      nf.fidx = 0;
-      nf.seen = 0;
+      if (sp + 1 >= kMaxSchemaDepth) return r.fail(TGPU_ERR_UNSUPPORTED, r.pos);
+      st[sp++] = fr;
+      fr = struct_frame(f.struct_index, m);
       continue;  // isset set when the nested STOP is reached
     } else {
-      fr.fidx = (uint32_t)hit;
-      if (!open_container<P>(r, sc, ctype_of(f), m, A, st, sp)) continue;
+      ReadFrame nf;
+      if (!open_container<P>(r, sc, ctype_of(f), m, A, sp, nf)) {
+        st[sp++] = fr;
+        fr = nf;
+        continue;
+      }
     }
     if (r.ok()) {
       fr.obj[f.isset_offset] = 1;
@@ -1047,22 +1085,15 @@ __device__ Reader decode_record(const DecodeArgs& a, uint64_t i, int lane,
     }
   }
   if (lane >= 0) attach_slab(r, a.deep, (uint32_t)lane);
-  if (!indexed) {
-    if (start > a.in_len) {
-      r.fail(TGPU_ERR_UNDERFLOW, start);
-      return r;
-    }
-    Arena A = record_arena<P>(a.sc, a.arena, a.arena_cap, start, nullptr);
-    read_record<P>(r, a.sc, rec, A);
-    return r;
-  }
-  if (start > a.in_len || (a.check_index && a.offs[i + 1] < start)) {
-    r.fail(TGPU_ERR_INDEX_MISMATCH, start);
+  // (one read_record call site: each inlined copy carries its own frames)
+  if (start > a.in_len || (indexed && a.check_index && a.offs[i + 1] < start)) {
+    r.fail(indexed ? TGPU_ERR_INDEX_MISMATCH : TGPU_ERR_UNDERFLOW, start);
     return r;
   }
   Arena A = record_arena<P>(a.sc, a.arena, a.arena_cap, start, nullptr);
   read_record<P>(r, a.sc, rec, A);
-  if (r.ok() && a.check_index && r.pos != a.offs[i + 1]) r.fail(TGPU_ERR_INDEX_MISMATCH, r.pos);
+  if (indexed && r.ok() && a.check_index && r.pos != a.offs[i + 1])
+    r.fail(TGPU_ERR_INDEX_MISMATCH, r.pos);
   return r;
 }
 
@@ -1138,8 +1169,12 @@ __device__ __forceinline__ void write_elem(Writer& w, uint32_t t, const uint8_t*
                                            const uint8_t* sbase) {
   if (t != TGPU_T_STRING) return write_scalar<P>(w, t, p);
   tgpu_span e;
-  uint8_t* b = (uint8_t*)&e;
-  for (uint32_t k = 0; k < 16; ++k) b[k] = p[k];
+  if (((uintptr_t)p & 7) == 0) {
+    e = *(const tgpu_span*)p;
+  } else {
+    uint8_t* b = (uint8_t*)&e;
+    for (uint32_t k = 0; k < 16; ++k) b[k] = p[k];
+  }
   if (e.length > 0x7fffffffu) return w.fail(TGPU_ERR_WRITE_SIZE_LIMIT, w.pos);  // checkBinarySize
   if (P == TGPU_PROTOCOL_BINARY) w.put_be(e.length, 4);
   else w.varint(e.length);
