@@ -378,14 +378,36 @@ __global__ __launch_bounds__(kTileLanes) void index_tile_spec_kernel(IndexArgs a
 __global__ __launch_bounds__(kTileLanes) void index_tile_emit_kernel(IndexArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[prog::kTileLds];
   __shared__ prog::IndexTileShared sm;
-  prog::index_emit_tile<false>(a, prog::DynProg{a.prog}, lds, sm, nullptr);
+  prog::index_emit_kernel_body(a, prog::DynProg{a.prog}, lds, sm);
+}
+
+// Stored starts (a.st16): tile j's current starts go to offs[base[j] ..], one
+// wave per tile, four tiles per workgroup; a tile whose starts are not
+// current (no stored list, or the repair re-chained or moved it) is listed
+// in bad[] (count scal[6]) for the emit kernel's re-walk.
+__global__ __launch_bounds__(256) void index_starts_copy_kernel(IndexArgs a) {
+  const uint64_t j = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63;
+  if (j >= a.n_chunks) return;
+  if (lane == 0) a.ep[j] = kNo;
+  if (j >= a.scal[1] || a.cnt[j] == 0) return;
+  if (!prog::starts_current(a, j)) {
+    if (lane == 0) a.bad[atomicAdd(&a.scal[6], 1ull)] = j;
+    return;
+  }
+  const uint64_t lo = chunk_lo(a, j);
+  const uint64_t gb = lo - ((uintptr_t)(a.in + lo) & 15);
+  const uint16_t* st = a.st16 + j * a.st_cap;
+  const uint64_t n = a.cnt[j], b = a.base[j];
+  for (uint64_t i = lane; i < n; i += 64)
+    if (b + i <= a.max_records) a.offs[b + i] = gb + st[i];
 }
 
 __global__ __launch_bounds__(kTileLanes) void index_tile_decode_kernel(IndexArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[prog::kTileLds];
   __shared__ __attribute__((aligned(16))) uint8_t rtile[prog::kRecTileBytes + 32];
   __shared__ prog::IndexTileShared sm;
-  prog::index_emit_tile<true>(a, prog::DynProg{a.prog}, lds, sm, rtile);
+  prog::index_emit_tile<true>(a, prog::DynProg{a.prog}, lds, sm, rtile, blockIdx.x);
 }
 
 // Single pass (tgpu_prog_kernels.h index_onepass_tile), interpreted program.
@@ -518,6 +540,7 @@ __global__ void index_fix_kernel(IndexArgs a) {
 __global__ __launch_bounds__(256) void index_prep_kernel(IndexArgs a) {
   const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   if (j < a.n_chunks) a.base[j] = j < a.scal[1] ? a.cnt[j] : 0;
+  if (j == 0) a.scal[6] = 0;  // tiles listed for the emit's re-walk (stored starts)
 }
 
 // Emit, program-only; a chain the program cannot finish is handed to
@@ -656,7 +679,8 @@ uint64_t index_chunk_bytes(uint64_t span, bool tiles) {
 
 hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const JitKernels* jit,
                                bool* fused) {
-  const bool decode = a.recs && a.prog && a.chunk == kTile;
+  // (st_decode: the caller decodes from the index; the finish keeps the tail rule)
+  const bool decode = a.recs && a.prog && a.chunk == kTile && !a.st_decode;
   if (fused) *fused = decode;
   const uint64_t C = a.n_chunks;
   const dim3 g((uint32_t)((C + 255) / 256)), b(256);
@@ -691,13 +715,22 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
   if (e != hipSuccess) return e;
   IndexArgs x = a;
   if (!decode) x.recs = nullptr;
+  // stored starts: copied by a light kernel; the emit tiles re-walk only the
+  // tiles it lists, a grid of at most ~6 resident workgroups per CU looping
+  const bool copy = !decode && a.st16 && a.prog && a.chunk == kTile;
+  if (!copy) x.st16 = nullptr;
+  const uint64_t emit_grid = copy ? std::min<uint64_t>(C, 2048) : C;
+  if (copy)
+    hipLaunchKernelGGL(index_starts_copy_kernel, dim3((uint32_t)((C + 3) / 4)), dim3(256), 0, stream,
+                       x);
   if (a.prog && a.chunk == kTile && jit) {
-    e = jit_launch_index(jit, decode ? 2 : 1, x, C, stream);
+    e = jit_launch_index(jit, decode ? 2 : 1, x, decode ? C : emit_grid, stream);
     if (e != hipSuccess) return e;
   } else if (decode) {
     hipLaunchKernelGGL(index_tile_decode_kernel, dim3((uint32_t)C), dim3(kTileLanes), 0, stream, x);
   } else if (a.prog && a.chunk == kTile)
-    hipLaunchKernelGGL(index_tile_emit_kernel, dim3((uint32_t)C), dim3(kTileLanes), 0, stream, x);
+    hipLaunchKernelGGL(index_tile_emit_kernel, dim3((uint32_t)emit_grid), dim3(kTileLanes), 0,
+                       stream, x);
   else
     hipLaunchKernelGGL(index_emit_kernel, g, b, 0, stream, a);
   TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_emit_cont_kernel<P_>, g, b, 0, stream, x));
@@ -705,7 +738,7 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
     TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_deep_emit_kernel<P_>,
                                                     dim3((a.deep.lanes + 63) / 64), dim3(64), 0,
                                                     stream, x));
-  return launch_index_finish(a, decode, stream);
+  return launch_index_finish(a, decode || (a.st_decode && a.recs), stream);
 }
 
 hipError_t launch_index_finish(const IndexArgs& a, bool decode, hipStream_t stream) {

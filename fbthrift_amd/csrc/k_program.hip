@@ -61,10 +61,12 @@ __global__ __launch_bounds__(256) void general_decode_list_kernel(DecodeArgs a,
 // at most 1.12 x mean + 512 B. (A/B on MI355X, tools/kbench_prog.py: config 3
 // 1.64 -> 1.45 ms going from the old fixed 1.3 x mean + 1 KiB to 5
 // workgroups/CU.) TGPU_PROG_DECODE="factor,pad" overrides the upper bound.
-uint32_t program_decode_wire_cap(const DecodeArgs& a, uint32_t rec_size) {
+// span_bytes: the wire bytes of the n records (0: a.in_len).
+uint32_t program_decode_wire_cap(const DecodeArgs& a, uint32_t rec_size, uint64_t span_bytes) {
   double factor = 1.12, pad = 512.0;
   if (const char* e = getenv("TGPU_PROG_DECODE")) sscanf(e, "%lf,%lf", &factor, &pad);
-  const double mean = (double)a.in_len / (double)(a.n ? a.n : 1) * kPT;
+  const double span = (double)(span_bytes ? span_bytes : a.in_len);
+  const double mean = span / (double)(a.n ? a.n : 1) * kPT;
   const double lo = 1.04 * mean + 256.0, hi = std::max(factor * mean + pad, lo);
   const uint32_t rt = (kPT * rec_size + 16 + 15) & ~15u;
   double cap = hi;
@@ -86,9 +88,9 @@ uint32_t program_decode_lds(uint32_t wire_cap, uint32_t rec_size) {
 
 hipError_t launch_program_decode(const DecodeArgs& a, const VProgram* d_prog, uint32_t rec_size,
                                  uint64_t* irregular, unsigned long long* n_irregular,
-                                 hipStream_t stream, const JitKernels* jit) {
+                                 hipStream_t stream, const JitKernels* jit, uint64_t span_bytes) {
   if (a.n == 0) return hipSuccess;
-  const uint32_t cap = program_decode_wire_cap(a, rec_size);
+  const uint32_t cap = program_decode_wire_cap(a, rec_size, span_bytes);
   const uint64_t tiles = (a.n + kPT - 1) / kPT;
   const uint32_t lds = program_decode_lds(cap, rec_size);
   if (jit) return jit_launch_decode(jit, a, tiles, cap, lds, irregular, n_irregular, stream);

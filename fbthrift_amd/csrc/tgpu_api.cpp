@@ -700,6 +700,33 @@ hipError_t launch_indexed_decode(tgpu_context* ctx, const tgpu_schema* schema, i
   return launch_general_decode(a, protocol, s);
 }
 
+// Fewest wire bytes a record of the program can take (every value at its
+// shortest: 1-byte varints, empty strings and lists).
+uint32_t prog_min_len(const VProgram& P) {
+  const bool compact = P.protocol != TGPU_PROTOCOL_BINARY;
+  uint32_t n = 0;
+  for (uint32_t k = 0; k < P.n_ops; ++k) {
+    const VOp& o = P.ops[k];
+    switch (o.kind) {
+      case VOP_CONST: case VOP_CBOOL: n += o.hdr_len; break;
+      case VOP_FIXED: n += o.width; break;
+      case VOP_VARINT: n += 1; break;
+      case VOP_STRING: n += compact ? 1 : 4; break;
+      case VOP_LIST: n += compact ? 1 : 5; break;
+      default: break;
+    }
+  }
+  return n;
+}
+
+// TGPU_INDEX_STARTS=0: the emit pass re-walks every tile instead of copying
+// the speculation pass's stored starts, and unindexed decodes take the fused
+// index + decode tiles (A/B).
+bool index_starts_enabled() {
+  const char* e = getenv("TGPU_INDEX_STARTS");
+  return !(e && e[0] == '0');
+}
+
 // Stream index into offs (max_records + 1 entries); see launch_index_stream.
 // Returns a TGPU_ERR_* for host-side failures; HIP launch errors go to `e`.
 // dec (optional): decode the records during the index when the tile path
@@ -752,7 +779,14 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   const uint64_t rs = (x.rec_size + 7) & ~7u;
   const uint64_t parts = scan_tiles_parts(C) + 1;
   const uint64_t lane_words = x.chunk == index_tile_bytes() ? C * index_tile_lanes() : 0;
-  const uint64_t need = 8 * ((9 + kSpecStarts) * C + parts + 17) + C * rs + 4 * lane_words;
+  // stored starts: a tile holds at most chunk / min_len + 1 record starts
+  const bool starts = lane_words && x.prog && index_starts_enabled();
+  x.st_cap = starts ? (uint32_t)std::min<uint64_t>(
+                          x.chunk / std::max<uint32_t>(prog_min_len(schema->prog[pq]), 1) + 2, 2048)
+                    : 0;
+  const uint64_t st_bytes = (2 * (uint64_t)x.st_cap * C + 15) & ~15ull;
+  const uint64_t need =
+      8 * ((9 + kSpecStarts) * C + parts + 17) + C * rs + 4 * lane_words + 16 + st_bytes;
   if (need > ctx->index_bytes) {
     if (ctx->d_index) (void)hipFree(ctx->d_index);
     ctx->d_index = nullptr;
@@ -775,6 +809,10 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   x.lanes = (uint32_t*)(x.scratch + C * rs);
   x.deep_chunks = (uint64_t*)(x.lanes + lane_words + (lane_words & 1));
   x.sst = x.deep_chunks + C;
+  x.st16 = starts ? (uint16_t*)(((uintptr_t)(x.sst + kSpecStarts * C) + 15) & ~(uintptr_t)15) : nullptr;
+  // decode: the indexed program decode after the index (balanced: 256 records
+  // per workgroup) instead of the emit tiles' per-lane chains
+  x.st_decode = starts && dec && x.recs ? 1 : 0;
   if (x.n_chunks == 0) {
     // nothing starts in [begin, end): the index is just the end position
     if (e == hipSuccess) e = launch_index_empty(x.res, offs, x.begin, fill_to, s);
@@ -807,6 +845,30 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
     if (e == hipSuccess && x.nirr) e = hipMemsetAsync(x.nirr, 0, sizeof(unsigned long long), s);
   }
   if (e == hipSuccess) e = launch_index_stream(x, s, jit, fused);
+  if (e == hipSuccess && x.st_decode && x.chunk == index_tile_bytes()) {
+    // the records the index found, [0, min(total, n_decode)): program decode,
+    // the rest to the general decoder's list (as the fused tiles leave them)
+    DecodeArgs t = *dec;
+    t.offs = offs;
+    t.n_dev = x.scal + 5;
+    t.fixed_len = 0;
+    if (may_sync) {
+      // the record count sizes the decode's LDS wire tile (its mean record);
+      // otherwise the caller's max_records bounds it and tiles too large for
+      // the cap read their records from HBM
+      unsigned long long total = 0;
+      e = hipMemcpyAsync(&total, x.scal + 5, sizeof(total), hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+      if (e != hipSuccess) return TGPU_OK;
+      t.n = std::min<uint64_t>(t.n, total);
+    }
+    e = launch_program_decode(
+        t, x.prog, t.rec_size, ctx->d_irr, &ctx->d_res->n_irregular, s,
+        tolerant ? jit_kernels(schema->prog_tol[pq], schema->device, JIT_DECODE, t.n, 0, false)
+                 : schema_jit(schema, protocol, JIT_DECODE, t.n, 0),
+        end - begin);
+    if (fused) *fused = true;
+  }
   return TGPU_OK;
 }
 

@@ -225,6 +225,9 @@ struct DecodeArgs {
   uint64_t* exc;
   uint64_t exc_cap;
   DeepArgs deep;
+  // records actually present (device word, e.g. the stream index's total):
+  // records [min(n, *n_dev), n) are left alone; nullptr: all n
+  const unsigned long long* n_dev;
 };
 
 // Schemaless skim of an indexed stream (k_skim.hip, tgpu_skim_batch).
@@ -310,6 +313,15 @@ struct IndexArgs {
   int32_t pad_;
   DeepArgs deep;        // records: fused decode deferrals; chunks: deep_chunks
   uint64_t* deep_chunks;  // emit chains stopped by kErrDeep (count: res->n_deep_chunks)
+  // LDS tiles: the speculation pass's record starts per tile (tile-relative,
+  // st_cap per tile; valid where pf[j] == kStartsValid), so the emit pass
+  // copies them instead of re-walking the tile; nullptr: off
+  uint16_t* st16;
+  uint32_t st_cap;
+  // the records are decoded after the index by the indexed program decode
+  // (launch_index) rather than in the emit tiles: emit writes starts only,
+  // the finish keeps the fused decode's tail rule
+  int32_t st_decode;
 };
 
 #ifndef __HIPCC_RTC__
@@ -370,7 +382,7 @@ hipError_t jit_launch_index(const JitKernels* J, int which, const IndexArgs& a, 
 hipError_t launch_program_decode(const DecodeArgs& a, const VProgram* d_prog,
                                  uint32_t rec_size, uint64_t* irregular,
                                  unsigned long long* n_irregular, hipStream_t stream,
-                                 const JitKernels* jit);
+                                 const JitKernels* jit, uint64_t span_bytes = 0);
 hipError_t launch_general_decode_list(const DecodeArgs& a, int protocol,
                                       const uint64_t* list,
                                       const unsigned long long* n_list,

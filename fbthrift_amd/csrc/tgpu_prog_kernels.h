@@ -79,7 +79,9 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
   uint8_t* wire = smem;
   uint8_t* rtile = smem + decode_wire_region(wire_cap);
   const uint64_t r0 = (uint64_t)blockIdx.x * kPT;
-  const uint32_t nrec = (uint32_t)min((uint64_t)kPT, a.n - r0);
+  const uint64_t n_all = a.n_dev ? min(a.n, (uint64_t)*a.n_dev) : a.n;
+  if (r0 >= n_all) return;  // (whole workgroup)
+  const uint32_t nrec = (uint32_t)min((uint64_t)kPT, n_all - r0);
   const uint64_t L = a.fixed_len;
   const uint64_t t0 = L ? r0 * L : a.offs[r0], t1 = L ? (r0 + nrec) * L : a.offs[r0 + nrec];
   const bool tile_ok = t1 >= t0 && t1 <= a.in_len && (t1 - t0) + 16 <= wire_cap;
@@ -729,6 +731,7 @@ constexpr uint64_t kNo = ~0ull;             // no start found / unset
 constexpr uint64_t kErr = ~0ull - 1;        // chain ended in a reader error
 constexpr uint64_t kPartial = ~0ull - 2;    // program stopped: general reader continues
 constexpr uint64_t kLanesValid = ~0ull - 3; // pf: the tile's per-lane results are current
+constexpr uint64_t kStartsValid = ~0ull - 4; // pf: ... and its record starts are in st16
 constexpr uint32_t kPosCap = 0x7fffff00u;
 constexpr uint32_t kTileLanes = 256;
 constexpr uint32_t kSub = 64;
@@ -766,10 +769,25 @@ struct TileSrc {
   }
 };
 
+constexpr uint32_t kLaneStarts = 8;  // record starts a lane keeps (u16 pairs in st[])
 struct TileLane {
   uint32_t s, e, c;  // first start, end, count (tile-relative); s == kNoPos: none
   bool stuck;
+  uint32_t st[kLaneStarts / 2];  // the chain's record starts, u16 each (first kLaneStarts)
 };
+
+// start k of the lane's chain := p (register selects: no dynamic indexing)
+__device__ __forceinline__ void put_start(TileLane& L, uint32_t k, uint32_t p) {
+  const uint32_t sh = (k & 1) * 16, m = 0xffffu << sh, x = (p & 0xffffu) << sh;
+#pragma unroll
+  for (uint32_t w = 0; w < kLaneStarts / 2; ++w) L.st[w] = (k >> 1) == w ? (L.st[w] & ~m) | x : L.st[w];
+}
+__device__ __forceinline__ uint32_t get_start(const TileLane& L, uint32_t k) {
+  uint32_t v = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < kLaneStarts / 2; ++w) v = (k >> 1) == w ? L.st[w] : v;
+  return (v >> ((k & 1) * 16)) & 0xffffu;
+}
 
 // Cheap rejection of a candidate start before running the program: the byte
 // after the first header's value must be the second header (first ops
@@ -795,6 +813,55 @@ __device__ __forceinline__ bool quick_reject(const PP& P, const TileSrc& src, ui
   return ((w >> (8 * len)) & 0xff) != (o2.hdr & 0xff);
 }
 
+// run_program<false> over the tile source, out of line: the rare records the
+// branch-free walk leaves undecided (see measure_lds)
+template <class PP>
+__device__ __attribute__((noinline)) bool tile_walk_slow(const PP P, const TileSrc src,
+                                                         const Ctx pc, uint32_t* pos,
+                                                         uint32_t end) {
+  uint32_t q = *pos;
+  const bool ok = run_program<false>(P, src, pc, q, end, nullptr);
+  *pos = q;
+  return ok;
+}
+
+// One record's measuring walk at q (tile-relative): branch-free over the
+// staged bytes, run_program for what that leaves undecided.
+template <class PP>
+__device__ __forceinline__ bool tile_walk(const PP& P, const TileSrc& src, const Ctx& pc,
+                                          uint32_t& q, uint32_t end) {
+#ifdef TGPU_BRANCHY_WALK  // A/B: the early-return program walk
+  return run_program<false>(P, src, pc, q, end, nullptr);
+#else
+  bool slow = src.lds_len < 12;
+  bool ok = false;
+  if (!slow) ok = measure_lds(P, src.w32, src.lds_len - 12, pc, q, end, slow);
+  if (slow) ok = tile_walk_slow(P, src, pc, &q, end);
+  return ok;
+#endif
+}
+
+// The tile's nvec 16-byte vectors HBM -> LDS by LDS DMA
+// (global_load_lds_dwordx4: no register round trip; lanes past the tile are
+// masked off, so nothing is written past nvec vectors). The caller's
+// __syncthreads waits for the loads.
+__device__ __forceinline__ void stage_tile(uint8_t* lds, const uint8_t* gb, uint32_t nvec) {
+#ifdef TGPU_SPEC_REGSTAGE  // A/B: staging through registers
+  for (uint32_t i = threadIdx.x; i < nvec; i += kTileLanes)
+    ((uint4*)lds)[i] = ((const uint4*)gb)[i];
+#else
+  const uint32_t wave = threadIdx.x >> 6;
+  for (uint32_t k = 0; k * kTileLanes < nvec; ++k) {
+    const uint32_t i = k * kTileLanes + threadIdx.x;
+    if (i < nvec)
+      __builtin_amdgcn_global_load_lds(
+          (const void*)((const uint4*)gb + i),
+          (__attribute__((address_space(3))) void*)(lds + (size_t)(k * kTileLanes + wave * 64) * 16),
+          16, 0, 0);
+  }
+#endif
+}
+
 // chain of canonical records from x while position < hi (tile-relative)
 template <class PP>
 __device__ __forceinline__ void tile_chain(const PP& P, const TileSrc& src, const Ctx& pc,
@@ -805,10 +872,11 @@ __device__ __forceinline__ void tile_chain(const PP& P, const TileSrc& src, cons
   uint32_t p = x;
   while (p < hi) {
     uint32_t q = p;
-    if (!run_program<false>(P, src, pc, q, end, nullptr)) {
+    if (!tile_walk(P, src, pc, q, end)) {
       L.stuck = true;
       break;
     }
+    put_start(L, L.c, p);
     ++L.c;
     p = q;
   }
@@ -833,8 +901,7 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
   const uint32_t avail = (uint32_t)(avail64 < kPosCap ? avail64 : kPosCap);
   const uint32_t staged = avail < kTile + kOver + 16 ? avail : kTile + kOver + 16;
   const uint32_t nvec = (staged + 15) >> 4;
-  for (uint32_t i = threadIdx.x; i < nvec; i += kTileLanes)
-    ((uint4*)lds)[i] = ((const uint4*)gb)[i];
+  stage_tile(lds, gb, nvec);
   __syncthreads();
   const TileSrc src{(const uint32_t*)lds, staged & ~3u, HbmSrc{gb, avail}};
   const Ctx pc{0, nullptr, 0, a.string_limit, a.container_limit};
@@ -987,14 +1054,24 @@ __device__ __forceinline__ void index_spec_tile(const IndexArgs& a, const PP& P,
   uint32_t sh, first;
   const bool ok = tile_resolve(a, P, j, lds, ent, L, sh, first, sm.E, &sm.flag, &sm.first_lane,
                                &sm.fs, sm.cmask);
-  if (threadIdx.x == 0) sm.csum = 0;
-  __syncthreads();
-  if (ok && first != kNoPos) atomicAdd(&sm.csum, (unsigned long long)L.c);
-  __syncthreads();
+  // (ok and first are the same in every lane)
+  const bool have = ok && first != kNoPos;
+  unsigned long long tile_n = 0;
+  const unsigned long long pre =
+      block_exscan256(have ? (unsigned long long)L.c : 0ull, sm.part, &tile_n);
   // per-lane starts/counts for the emit pass (valid while the tile keeps this
   // start: pf[j] == kLanesValid)
-  if (ok && first != kNoPos)
-    a.lanes[j * kTileLanes + threadIdx.x] = (L.s & 0xffffu) | ((uint32_t)L.c << 16);
+  if (have) a.lanes[j * kTileLanes + threadIdx.x] = (L.s & 0xffffu) | ((uint32_t)L.c << 16);
+  // the tile's record starts in order (pf[j] == kStartsValid): lane k's after
+  // those of lanes < k
+  bool stored = false;
+  if (a.st16 && have) {
+    stored = !__syncthreads_or(L.c > kLaneStarts) && tile_n <= a.st_cap;
+    if (stored) {
+      uint16_t* dst = a.st16 + j * a.st_cap + pre;
+      for (uint32_t i = 0; i < L.c; ++i) dst[i] = (uint16_t)get_start(L, i);
+    }
+  }
   if (threadIdx.x == kTileLanes - 1) {
     if (first == kNoPos) {
       a.s[j] = kNo;
@@ -1009,8 +1086,8 @@ __device__ __forceinline__ void index_spec_tile(const IndexArgs& a, const PP& P,
     } else {
       a.s[j] = lo - sh + first;
       a.e[j] = lo - sh + L.e;
-      a.cnt[j] = sm.csum;
-      a.pf[j] = kLanesValid;
+      a.cnt[j] = tile_n;
+      a.pf[j] = stored ? kStartsValid : kLanesValid;
     }
   }
 }
@@ -1035,10 +1112,20 @@ __device__ __forceinline__ void emit_lanes(const IndexArgs& a, const PP& P, cons
                                            IndexTileShared& sm, uint8_t* rtile, const TileLane& L,
                                            uint32_t sh, uint64_t lo, uint64_t b);
 
+// Tile j's stored starts are current: the speculation pass stored them and
+// the chain still begins where it did (the repair may move a tile's start
+// forward onto its speculated chain, take_over).
+__device__ __forceinline__ bool starts_current(const IndexArgs& a, uint64_t j) {
+  if (a.pf[j] != kStartsValid) return false;
+  const uint64_t lo = chunk_lo(a, j);
+  const uint64_t gb = lo - ((uintptr_t)(a.in + lo) & 15);
+  return gb + a.st16[j * a.st_cap] == a.s[j];
+}
+
 template <bool kDecode, class PP>
 __device__ __forceinline__ void index_emit_tile(const IndexArgs& a, const PP& P, uint8_t* lds,
-                                                IndexTileShared& sm, uint8_t* rtile) {
-  const uint64_t j = blockIdx.x;
+                                                IndexTileShared& sm, uint8_t* rtile,
+                                                uint64_t j) {
   if (threadIdx.x == 0) a.ep[j] = kNo;
   if (j >= a.scal[1] || a.cnt[j] == 0) return;
   const uint64_t lo = chunk_lo(a, j);
@@ -1048,7 +1135,7 @@ __device__ __forceinline__ void index_emit_tile(const IndexArgs& a, const PP& P,
   TileLane L;
   uint32_t sh, first;
   bool ok;
-  if (a.pf[j] == kLanesValid) {
+  if (a.pf[j] == kLanesValid || a.pf[j] == kStartsValid) {
     // the speculation pass's lane results still hold: stage the tile only
     const uint8_t* g = a.in + lo;
     sh = sh0;
@@ -1057,8 +1144,7 @@ __device__ __forceinline__ void index_emit_tile(const IndexArgs& a, const PP& P,
     const uint32_t avail = (uint32_t)(av < kPosCap ? av : kPosCap);
     const uint32_t staged = avail < kTile + kOver + 16 ? avail : kTile + kOver + 16;
     const uint32_t nvec = (staged + 15) >> 4;
-    for (uint32_t i = threadIdx.x; i < nvec; i += kTileLanes)
-      ((uint4*)lds)[i] = ((const uint4*)gb)[i];
+    stage_tile(lds, gb, nvec);
     const uint32_t v = a.lanes[j * kTileLanes + threadIdx.x];
     L.s = v & 0xffffu;
     L.c = v >> 16;
@@ -1078,6 +1164,24 @@ __device__ __forceinline__ void index_emit_tile(const IndexArgs& a, const PP& P,
     return;
   }
   emit_lanes<kDecode>(a, P, lds, sm, rtile, L, sh, lo, b);
+}
+
+// The emit kernel body: every tile (j = blockIdx.x), or, when the
+// speculation pass stored starts (a.st16: index_starts_copy_kernel copied the
+// current ones), the tiles it listed in bad[0 .. scal[6]), strided over the
+// grid.
+template <class PP>
+__device__ __forceinline__ void index_emit_kernel_body(const IndexArgs& a, const PP& P,
+                                                       uint8_t* lds, IndexTileShared& sm) {
+  if (!a.st16) {
+    index_emit_tile<false>(a, P, lds, sm, nullptr, blockIdx.x);
+    return;
+  }
+  const uint64_t m = a.scal[6];
+  for (uint64_t k = blockIdx.x; k < m; k += gridDim.x) {
+    index_emit_tile<false>(a, P, lds, sm, nullptr, a.bad[k]);
+    __syncthreads();  // the next tile's staging overwrites lds
+  }
 }
 
 // The emission body of a tile whose lanes hold verified chains (L) and whose
@@ -1109,7 +1213,7 @@ __device__ __forceinline__ void emit_lanes(const IndexArgs& a, const PP& P, cons
       const uint64_t idx = b + pre + i;
       if (idx <= a.max_records) a.offs[idx] = gb + p;
       uint32_t q = p;
-      run_program<false>(P, src, pc, q, avail, nullptr);
+      tile_walk(P, src, pc, q, avail);
       p = q;
     }
   } else {
@@ -1150,7 +1254,7 @@ __device__ __forceinline__ void emit_lanes(const IndexArgs& a, const PP& P, cons
           run_program<false>(P, src, pc, q, avail, nullptr);
         }
       } else {
-        run_program<false>(P, src, pc, q, avail, nullptr);
+        tile_walk(P, src, pc, q, avail);
       }
       p = q;
     }

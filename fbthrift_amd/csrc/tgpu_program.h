@@ -449,6 +449,146 @@ __device__ __forceinline__ bool run_op(const VOp op, const bool compact, const S
   return true;
 }
 
+// ---- branch-free measuring walk (stream index) ---------------------------------
+// run_program<false> decides each op with an early return; in the index's
+// speculation (every lane walking its slice's records, most of them
+// different lengths) each return is a divergent branch: the compiled config-5
+// speculation kernel ran ~1,500 SALU (exec-mask) instructions per wave. Here
+// every op is straight-line: the checks AND into `ok` and the walk carries on
+// over whatever bytes follow (reads clamped into the staged tile), so a wave
+// runs the record's ops once, in lockstep. Accepts exactly what
+// run_program<false> accepts with the same end position, for every record
+// whose reads stay inside the staged bytes (position <= lim); anything it
+// does not decide here sets `slow` (a read past lim, a 9-10 byte i64
+// varint, element loops, the tolerant programs' appended fields) and the
+// caller runs run_program on the record instead.
+template <class PP>
+__device__ __forceinline__ bool measure_lds(const PP& P, const uint32_t* w32, uint32_t lim,
+                                            const Ctx& c, uint32_t& pos, uint32_t end, bool& slow) {
+  const bool compact = P.protocol() != TGPU_PROTOCOL_BINARY;
+  const LdsSrc src{w32};
+  uint32_t p = pos;
+  bool ok = true, sl = false;
+  auto rd = [&](uint32_t q) {
+    sl |= ok && q > lim;
+    return src.win8(q > lim ? lim : q);
+  };
+  // LEB128 of a 32-bit value in w (read_varint_w's fast form): length, value
+  auto var32 = [&](uint64_t w, uint32_t& len) {
+    const uint64_t stop = ~w & 0x8080808080808080ull;
+    len = stop ? ((uint32_t)__builtin_ctzll(stop) >> 3) + 1 : 8;
+    ok &= stop != 0 && len <= 5;
+    uint64_t x = w & ((len >= 8 ? 0 : (1ull << (8 * len))) - 1) & 0x7f7f7f7f7f7f7f7full;
+    x = ((x & 0x7f007f007f007f00ull) >> 1) | (x & 0x007f007f007f007full);
+    x = ((x & 0x3fff00003fff0000ull) >> 2) | (x & 0x00003fff00003fffull);
+    x = ((x & 0x0fffffff00000000ull) >> 4) | (x & 0x000000000fffffffull);
+    return (uint32_t)x;
+  };
+  all_ops(P, [&](const VOp op) {
+    switch (op.kind) {
+      case VOP_CONST: {
+        const uint32_t lo = (uint32_t)rd(p);
+        const uint32_t mask = op.hdr_len >= 4 ? 0xffffffffu : ((1u << (8 * op.hdr_len)) - 1);
+        const bool hit = ((lo ^ op.hdr) & mask) == 0;
+#ifndef TGPU_NO_TAILS
+        if (op.elem_kind == kStopSkipsUnknown) sl |= ok && !hit;
+#endif
+        ok &= p + op.hdr_len <= end && hit;
+        p += op.hdr_len;
+        break;
+      }
+      case VOP_CBOOL: {
+        const uint32_t lo = (uint32_t)rd(p);
+        const uint32_t mask =
+            (op.hdr_len >= 4 ? 0xffffffffu : ((1u << (8 * op.hdr_len)) - 1)) & ~0xfu;
+        const uint32_t ct = lo & 0xf;
+        ok &= p + op.hdr_len <= end && ((lo ^ op.hdr) & mask) == 0 && (ct == 1 || ct == 2);
+        p += op.hdr_len;
+        break;
+      }
+      case VOP_FIXED: {
+        const uint64_t v = bswap_n(rd(p), op.width);
+        ok &= p + op.width <= end && !(op.is_bool && v > 1);
+        p += op.width;
+        break;
+      }
+      case VOP_VARINT: {
+        const uint64_t w = rd(p);
+        const uint64_t stop = ~w & 0x8080808080808080ull;
+        const uint32_t len = stop ? ((uint32_t)__builtin_ctzll(stop) >> 3) + 1 : 8;
+        if (op.bits == 32) {
+          ok &= stop != 0 && len <= 5;
+        } else {
+          sl |= ok && stop == 0;  // 9-10 byte i64 varint
+        }
+        ok &= p + len <= end;
+        p += len;
+        break;
+      }
+      case VOP_STRING: {
+        const uint64_t w = rd(p);
+        uint32_t hl, n;
+        if (compact) {
+          n = var32(w, hl);
+        } else {
+          hl = 4;
+          n = (uint32_t)bswap_n(w, 4);
+        }
+        ok &= p + hl <= end;
+        p += hl;
+        const int64_t len = (int32_t)n;
+        ok &= len >= 0 && !(c.string_limit > 0 && len > c.string_limit) &&
+              len <= (int64_t)end - (int64_t)p;
+        p += ok ? (uint32_t)len : 0u;
+        break;
+      }
+      case VOP_LIST: {
+        const uint64_t w = rd(p);
+        int64_t n;
+        if (compact) {
+          const uint32_t b = (uint32_t)(w & 0xff);
+          const uint32_t ct = b & 0xf;
+          ok &= p + 1 <= end &&
+                (op.elem_ttype == TGPU_T_BOOL ? (ct == 1 || ct == 2) : ct == op.elem_ct);
+          p += 1;
+          n = b >> 4;
+          if (n == 15) {  // count in a varint (uniform per op: rare, branch kept)
+            uint32_t vl;
+            const uint32_t z = var32(rd(p), vl);
+            ok &= p + vl <= end;
+            p += vl;
+            n = (int32_t)z;
+          }
+        } else {
+          ok &= p + 5 <= end && (w & 0xff) == op.elem_ttype;
+          n = (int32_t)(uint32_t)bswap_n(w >> 8, 4);
+          p += 5;
+        }
+        ok &= n >= 0 && !(c.container_limit && n > c.container_limit) &&
+              n <= (int64_t)end - (int64_t)p;
+        const bool fixed = op.elem_kind == VEL_FIXED || (compact && op.elem_kind == VEL_BOOL);
+        if (fixed) {
+          const uint64_t bytes = (uint64_t)(ok ? n : 0) * (op.elem_kind == VEL_BOOL ? 1u : op.width);
+          ok &= bytes <= (uint64_t)end - p;
+          p += ok ? (uint32_t)bytes : 0u;
+        } else {
+          sl |= ok && n > 0;  // element loops: run_program
+        }
+        break;
+      }
+      case VOP_ISSET:
+        break;
+      default:
+        sl |= ok;
+        break;
+    }
+    return true;
+  });
+  slow = sl;
+  if (ok && !sl) pos = p;
+  return ok;
+}
+
 // Runs the program from pos over at most [pos, end). On success pos is the
 // end of the record. kStore: write members / isset / spans into rec and list
 // elements into the arena; otherwise only measure and validate.

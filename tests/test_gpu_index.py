@@ -235,13 +235,21 @@ def test_decode_stream_error_mid_stream(gpu, codec):
     assert np.array_equal(rec.cpu().numpy()[:k], orec[:k])
 
 
+@pytest.mark.parametrize("variant", ["onepass", "fused"])
 @pytest.mark.parametrize("sname,proto", [("mixed", 2), ("mixed", 0), ("nested", 0)])
-def test_onepass_index(gpu, sname, proto, monkeypatch):
-    """The single-pass index (TGPU_INDEX_ONEPASS=1: look-back over packed tile
-    statuses, k_index.hip launch_index_onepass) gives the oracle's offsets and
-    records, whole and as speculative byte ranges; a malformed record makes it
-    fall back to the two-pass index, which reports the reference status."""
-    monkeypatch.setenv("TGPU_INDEX_ONEPASS", "1")
+def test_index_variants(gpu, sname, proto, variant, monkeypatch):
+    """The index forms that are off by default give the oracle's offsets and
+    records, whole and as speculative byte ranges, and a malformed record the
+    reference status: the single pass (TGPU_INDEX_ONEPASS=1: look-back over
+    packed tile statuses, k_index.hip launch_index_onepass; a malformed record
+    makes it fall back to the two-pass index) and the two-pass index whose
+    emit tiles re-walk their chains and decode the records as they go
+    (TGPU_INDEX_STARTS=0; by default the emit copies the speculation pass's
+    stored starts and the indexed program decode follows)."""
+    if variant == "onepass":
+        monkeypatch.setenv("TGPU_INDEX_ONEPASS", "1")
+    else:
+        monkeypatch.setenv("TGPU_INDEX_STARTS", "0")
     n = 300_000 if sname == "mixed" else 100_000
     schema, wire, woffs = _stream(sname, proto, n, seed=3)
     gs = _gs(schema)
