@@ -213,13 +213,28 @@ __global__ __launch_bounds__(256) void index_spec_kernel(IndexArgs a) {
   a.cnt[j] = 0;
 }
 
+// Kernels whose lanes run the general reader keep its frame stacks in
+// scratch (1.5-2.5 KB per lane). The runtime backs a dispatch's scratch for as
+// many waves as the grid can keep resident, and re-backs it when a call
+// finds it released: a one-lane-per-chunk grid over a 3.5 GB stream (850
+// workgroups) cost 0.3-0.5 ms per such kernel per call, where the work itself
+// (nothing to do for almost every chunk) takes microseconds. These run a
+// small grid (kScratchGrid workgroups) that strides over the chunks.
+#define SCRATCH_KERNEL(name, body)                                            \
+  template <int P>                                                            \
+  __global__ __launch_bounds__(256) void name(IndexArgs a) {                  \
+    const uint64_t stride = (uint64_t)gridDim.x * 256;                        \
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < a.n_chunks; \
+         j += stride)                                                         \
+      body<P>(a, j);                                                          \
+  }
+
 // Finishes partial chains with the general reader (program first per record).
 // A reader error rejects a speculated start (kNo: the repair pass decides);
 // from a verified start (chunk 0 of a non-speculative call) it is final (kErr).
 template <int P>
-__global__ __launch_bounds__(256) void index_cont_kernel(IndexArgs a) {
-  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= a.n_chunks || a.e[j] != kPartial) return;
+__device__ __forceinline__ void index_cont_one(const IndexArgs& a, uint64_t j) {
+  if (a.e[j] != kPartial) return;
   Chain c;
   const bool verified = j == 0 && !a.speculative;
   chain<P>(a, a.pf[j], chunk_hi(a, j), false, a.scratch + j * a.rec_size, c, nullptr, 0, kNo, -1,
@@ -238,6 +253,7 @@ __global__ __launch_bounds__(256) void index_cont_kernel(IndexArgs a) {
   a.cnt[j] += c.count;
   a.pf[j] = 0;
 }
+SCRATCH_KERNEL(index_cont_kernel, index_cont_one)
 
 // Speculation for schemas without a program: any record the general reader
 // accepts may open a chain.
@@ -282,9 +298,7 @@ __global__ __launch_bounds__(256) void index_spec_general_kernel(IndexArgs a) {
 // records; the chain's first kSpecStarts starts (sst) let the repair pass
 // take it over in O(1) when the true start is one of them.
 template <int P>
-__global__ __launch_bounds__(256) void index_spec_fallback_kernel(IndexArgs a) {
-  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= a.n_chunks) return;
+__device__ __forceinline__ void index_spec_fallback_one(const IndexArgs& a, uint64_t j) {
   uint64_t* starts = a.sst + j * kSpecStarts;
   starts[0] = kNo;
   if (a.s[j] != kNo || a.e[j] != kNo) return;
@@ -312,6 +326,7 @@ __global__ __launch_bounds__(256) void index_spec_fallback_kernel(IndexArgs a) {
   }
   starts[0] = kNo;
 }
+SCRATCH_KERNEL(index_spec_fallback_kernel, index_spec_fallback_one)
 
 // Parallel link repair, one lane per chunk whose speculated start s[j] is not
 // its predecessor's end T = e[j-1]. A false start inside the record straddling
@@ -327,9 +342,8 @@ __global__ __launch_bounds__(256) void index_spec_fallback_kernel(IndexArgs a) {
 // in order (a chunk whose T changes there is walked again), so this pass only
 // decides speed. A reader error leaves the chunk to index_fix_kernel.
 template <int P>
-__global__ __launch_bounds__(256) void index_merge_kernel(IndexArgs a) {
-  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j == 0 || j >= a.n_chunks) return;
+__device__ __forceinline__ void index_merge_one(const IndexArgs& a, uint64_t j) {
+  if (j == 0) return;
   const uint64_t T = a.e[j - 1];
   if (T == kNo || T == kErr || T == kPartial) return;
   const uint64_t s0 = a.s[j], e0 = a.e[j];
@@ -367,6 +381,7 @@ __global__ __launch_bounds__(256) void index_merge_kernel(IndexArgs a) {
   a.s[j] = T;
   a.pf[j] = 0;
 }
+SCRATCH_KERNEL(index_merge_kernel, index_merge_one)
 
 // ---- LDS tiles (schemas with a program; tgpu_prog_kernels.h) ---------------
 __global__ __launch_bounds__(kTileLanes) void index_tile_spec_kernel(IndexArgs a) {
@@ -584,11 +599,11 @@ __device__ __forceinline__ void emit_cont(const IndexArgs& a, uint64_t j, int la
 }
 
 template <int P>
-__global__ __launch_bounds__(256) void index_emit_cont_kernel(IndexArgs a) {
-  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (j >= a.n_chunks || a.ep[j] == kNo) return;
+__device__ __forceinline__ void index_emit_cont_one(const IndexArgs& a, uint64_t j) {
+  if (a.ep[j] == kNo) return;
   emit_cont<P>(a, j, -1);
 }
+SCRATCH_KERNEL(index_emit_cont_kernel, index_emit_cont_one)
 
 template <int P>
 __global__ __launch_bounds__(64) void index_deep_emit_kernel(IndexArgs a) {
@@ -677,13 +692,70 @@ uint64_t index_chunk_bytes(uint64_t span, bool tiles) {
   return c;
 }
 
+// TGPU_INDEX_TIMING=2: HIP events between the index's launches (stderr)
+struct PhaseTimer {
+  hipStream_t s;
+  bool on;
+  int n = 0;
+  hipEvent_t ev[32];
+  const char* name[32];
+  PhaseTimer(hipStream_t st) : s(st) {
+    const char* e = getenv("TGPU_INDEX_TIMING");
+    on = e && e[0] == '2';
+    mark("start");
+  }
+  void mark(const char* what) {
+    if (!on || n >= 32) return;
+    (void)hipEventCreate(&ev[n]);
+    (void)hipEventRecord(ev[n], s);
+    name[n++] = what;
+  }
+  ~PhaseTimer() {
+    if (!on) return;
+    (void)hipEventSynchronize(ev[n - 1]);
+    for (int k = 1; k < n; ++k) {
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, ev[k - 1], ev[k]);
+      fprintf(stderr, "  %-10s %.3f ms\n", name[k], ms);
+    }
+    for (int k = 0; k < n; ++k) (void)hipEventDestroy(ev[k]);
+  }
+};
+
+// What the general-reader helpers would find after the tile speculation:
+// scal[8] tiles the program left partial (index_cont), scal[9] tiles without
+// a start (index_spec_fallback), scal[10] broken links (index_merge).
+__global__ __launch_bounds__(256) void index_summary_kernel(IndexArgs a) {
+  const uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  bool partial = false, none = false, broken = false;
+  if (j < a.n_chunks) {
+    const uint64_t s0 = a.s[j], e0 = a.e[j];
+    partial = e0 == kPartial;
+    none = s0 == kNo && e0 == kNo;
+    if (j > 0 && e0 != kErr && e0 != kPartial) {
+      const uint64_t T = a.e[j - 1];
+      broken = T != kNo && T != kErr && T != kPartial && s0 != T;
+    }
+  }
+  const int np = __syncthreads_count(partial), nn = __syncthreads_count(none),
+            nb = __syncthreads_count(broken);
+  if (threadIdx.x == 0) {
+    if (np) atomicAdd(&a.scal[8], (unsigned long long)np);
+    if (nn) atomicAdd(&a.scal[9], (unsigned long long)nn);
+    if (nb) atomicAdd(&a.scal[10], (unsigned long long)nb);
+  }
+}
+
 hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const JitKernels* jit,
-                               bool* fused) {
+                               bool* fused, uint64_t* h_sync) {
+  PhaseTimer pt(stream);
   // (st_decode: the caller decodes from the index; the finish keeps the tail rule)
   const bool decode = a.recs && a.prog && a.chunk == kTile && !a.st_decode;
   if (fused) *fused = decode;
   const uint64_t C = a.n_chunks;
   const dim3 g((uint32_t)((C + 255) / 256)), b(256);
+  const dim3 sg((uint32_t)std::min<uint64_t>((C + 255) / 256, kScratchGrid));
+  bool need_cont = true, need_fallback = true, need_merge = true;
   if (a.prog && a.chunk == kTile) {
     if (jit) {
       const hipError_t e = jit_launch_index(jit, 0, a, C, stream);
@@ -691,25 +763,45 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
     } else {
       hipLaunchKernelGGL(index_tile_spec_kernel, dim3((uint32_t)C), dim3(kTileLanes), 0, stream, a);
     }
-    TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_cont_kernel<P_>, g, b, 0, stream, a));
+    pt.mark("spec");
+    if (h_sync) {
+      hipError_t e = hipMemsetAsync(a.scal + 8, 0, 3 * sizeof(unsigned long long), stream);
+      hipLaunchKernelGGL(index_summary_kernel, g, b, 0, stream, a);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(h_sync, a.scal + 8, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(stream);
+      if (e != hipSuccess) return e;
+      // the fallback and the repair act on what the continuation leaves
+      need_cont = h_sync[0] != 0;
+      need_fallback = need_cont || h_sync[1] != 0;
+      need_merge = need_fallback || h_sync[2] != 0;
+      pt.mark("summary");
+    }
+    if (need_cont)
+      TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_cont_kernel<P_>, sg, b, 0, stream, a));
+    pt.mark("cont");
   } else if (a.prog) {
     hipLaunchKernelGGL(index_spec_kernel, g, b, 0, stream, a);
-    TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_cont_kernel<P_>, g, b, 0, stream, a));
+    TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_cont_kernel<P_>, sg, b, 0, stream, a));
   } else {
     TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_spec_general_kernel<P_>, g, b, 0, stream, a));
   }
   // (a speculative range opens at its first program-confirmed start: a
   // general-reader start there has no predecessor chunk to verify it)
-  if (a.prog && !a.speculative)
-    TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_spec_fallback_kernel<P_>, g, b, 0, stream, a));
-  TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_merge_kernel<P_>, g, b, 0, stream, a));
+  if (a.prog && !a.speculative && need_fallback)
+    TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_spec_fallback_kernel<P_>, sg, b, 0, stream, a));
+  pt.mark("fallback");
+  if (need_merge)
+    TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_merge_kernel<P_>, sg, b, 0, stream, a));
   // sst is written by the general speculation and the fallback only
   const int sst_valid = !a.prog || !a.speculative;
+  pt.mark("merge");
   hipLaunchKernelGGL(index_flag_kernel, g, b, 0, stream, a, sst_valid);
   hipError_t e = launch_scan_tiles(a.base, C, a.part, a.scal, nullptr, stream);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(index_list_kernel, g, b, 0, stream, a);
   TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_fix_kernel<P_>, dim3(1), dim3(64), 0, stream, a));
+  pt.mark("fix");
   hipLaunchKernelGGL(index_prep_kernel, g, b, 0, stream, a);
   e = launch_scan_tiles(a.base, C, a.part, nullptr, nullptr, stream);
   if (e != hipSuccess) return e;
@@ -720,9 +812,11 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
   const bool copy = !decode && a.st16 && a.prog && a.chunk == kTile;
   if (!copy) x.st16 = nullptr;
   const uint64_t emit_grid = copy ? std::min<uint64_t>(C, 2048) : C;
+  pt.mark("prep");
   if (copy)
     hipLaunchKernelGGL(index_starts_copy_kernel, dim3((uint32_t)((C + 3) / 4)), dim3(256), 0, stream,
                        x);
+  pt.mark("copy");
   if (a.prog && a.chunk == kTile && jit) {
     e = jit_launch_index(jit, decode ? 2 : 1, x, decode ? C : emit_grid, stream);
     if (e != hipSuccess) return e;
@@ -733,12 +827,33 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
                        stream, x);
   else
     hipLaunchKernelGGL(index_emit_kernel, g, b, 0, stream, a);
-  TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_emit_cont_kernel<P_>, g, b, 0, stream, x));
-  if (a.deep.lanes)
-    TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_deep_emit_kernel<P_>,
-                                                    dim3((a.deep.lanes + 63) / 64), dim3(64), 0,
-                                                    stream, x));
-  return launch_index_finish(a, decode || (a.st_decode && a.recs), stream);
+  pt.mark("emit");
+  // the emit's continuation only has work where a re-walked tile stopped
+  // (copied tiles never do): with host reads, the finish goes first (it does
+  // not depend on it) and one read gives both the re-walk count and the total
+  const bool defer = copy && h_sync;
+  if (defer) {
+    e = launch_index_finish(a, decode || (a.st_decode && a.recs), stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(h_sync, a.scal + 6, sizeof(uint64_t),
+                                            hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(h_sync + 3, a.scal + 5, sizeof(uint64_t), hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return e;
+    pt.mark("finish");
+  }
+  if (!defer || h_sync[0]) {
+    TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_emit_cont_kernel<P_>, sg, b, 0, stream, x));
+    if (a.deep.lanes)
+      TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_deep_emit_kernel<P_>,
+                                                      dim3((a.deep.lanes + 63) / 64), dim3(64), 0,
+                                                      stream, x));
+    pt.mark("emit_cont");
+  }
+  if (defer) return hipGetLastError();
+  const hipError_t fe = launch_index_finish(a, decode || (a.st_decode && a.recs), stream);
+  pt.mark("cont+fin");
+  return fe;
 }
 
 hipError_t launch_index_finish(const IndexArgs& a, bool decode, hipStream_t stream) {

@@ -101,8 +101,12 @@ hipError_t launch_program_decode(const DecodeArgs& a, const VProgram* d_prog, ui
 
 hipError_t launch_general_decode_list(const DecodeArgs& a, int protocol, const uint64_t* list,
                                       const unsigned long long* n_list, hipStream_t stream) {
+  // (a grid-stride loop over the list: few workgroups keep the general
+  // reader's scratch backing small, k_index.hip SCRATCH_KERNEL; 4 x
+  // kScratchGrid still covers a list of every record at a quarter wave per CU)
   const uint64_t b = (a.n + 255) / 256;
-  const uint32_t g = (uint32_t)(b < 2048 ? (b ? b : 1) : 2048);
+  const uint64_t cap = 4ull * kScratchGrid;
+  const uint32_t g = (uint32_t)(b < cap ? (b ? b : 1) : cap);
   TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(general_decode_list_kernel<P_>, dim3(g), dim3(256), 0,
                        stream, a, list, n_list));
   return hipGetLastError();

@@ -49,6 +49,7 @@ struct tgpu_context {
   int device = 0;
   DevResult* d_res = nullptr;
   DevResult* h_res = nullptr;  // pinned
+  uint64_t* h_words = nullptr;  // pinned, 8 words: the stream index's mid-call reads
   uint64_t* d_offs = nullptr;
   unsigned long long* d_block_sums = nullptr;
   unsigned long long* d_scan_part = nullptr;  // partial sums of the tile scan
@@ -844,7 +845,33 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
     }
     if (e == hipSuccess && x.nirr) e = hipMemsetAsync(x.nirr, 0, sizeof(unsigned long long), s);
   }
-  if (e == hipSuccess) e = launch_index_stream(x, s, jit, fused);
+  // TGPU_INDEX_TIMING=1: HIP events around the index and the decode (stderr)
+  static const bool timing = getenv("TGPU_INDEX_TIMING") != nullptr;
+  hipEvent_t tev[3] = {};
+  if (timing)
+    for (auto& v : tev) (void)hipEventCreate(&v);
+  if (timing) (void)hipEventRecord(tev[0], s);
+  // blocking calls let the index read its tile summary and total mid-call
+  // (skipping the general-reader helper kernels when no tile needs them)
+  uint64_t* h_sync = may_sync ? ctx->h_words : nullptr;
+  if (h_sync) h_sync[3] = ~0ull;
+  if (e == hipSuccess) e = launch_index_stream(x, s, jit, fused, h_sync);
+  if (timing) (void)hipEventRecord(tev[1], s);
+  struct TimingReport {
+    hipEvent_t* ev;
+    bool on;
+    hipStream_t st;
+    ~TimingReport() {
+      if (!on) return;
+      (void)hipEventRecord(ev[2], st);
+      (void)hipEventSynchronize(ev[2]);
+      float a = 0, b = 0;
+      (void)hipEventElapsedTime(&a, ev[0], ev[1]);
+      (void)hipEventElapsedTime(&b, ev[1], ev[2]);
+      fprintf(stderr, "tgpu index %.3f ms, then %.3f ms\n", a, b);
+      for (int k = 0; k < 3; ++k) (void)hipEventDestroy(ev[k]);
+    }
+  } report{tev, timing, s};
   if (e == hipSuccess && x.st_decode && x.chunk == index_tile_bytes()) {
     // the records the index found, [0, min(total, n_decode)): program decode,
     // the rest to the general decoder's list (as the fused tiles leave them)
@@ -854,12 +881,16 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
     t.fixed_len = 0;
     if (may_sync) {
       // the record count sizes the decode's LDS wire tile (its mean record);
-      // otherwise the caller's max_records bounds it and tiles too large for
-      // the cap read their records from HBM
-      unsigned long long total = 0;
-      e = hipMemcpyAsync(&total, x.scal + 5, sizeof(total), hipMemcpyDeviceToHost, s);
-      if (e == hipSuccess) e = hipStreamSynchronize(s);
-      if (e != hipSuccess) return TGPU_OK;
+      // otherwise the caller's max_records bounds it (an overestimate makes
+      // the cap too small: those tiles' records take the general decoder)
+      // (into the context's pinned result slot: a pageable destination costs
+      // a staged copy; the slot is rewritten by every later result read)
+      if (h_sync[3] == ~0ull) {  // (the index did not read it)
+        e = hipMemcpyAsync(&h_sync[3], x.scal + 5, sizeof(uint64_t), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return TGPU_OK;
+      }
+      const uint64_t total = h_sync[3];
       t.n = std::min<uint64_t>(t.n, total);
     }
     e = launch_program_decode(
@@ -1128,7 +1159,8 @@ int tgpu_context_create(tgpu_context** out) {
   if (!c) return TGPU_ERR_HIP;
   (void)hipGetDevice(&c->device);
   if (hipMalloc(&c->d_res, sizeof(DevResult)) != hipSuccess ||
-      hipHostMalloc(&c->h_res, sizeof(DevResult), hipHostMallocDefault) != hipSuccess) {
+      hipHostMalloc(&c->h_res, sizeof(DevResult), hipHostMallocDefault) != hipSuccess ||
+      hipHostMalloc(&c->h_words, 8 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) {
     tgpu_context_destroy(c);
     return TGPU_ERR_HIP;
   }
@@ -1141,6 +1173,7 @@ void tgpu_context_destroy(tgpu_context* c) {
   if (c->host_pipe) host_pipe_destroy(c->host_pipe);
   if (c->d_res) (void)hipFree(c->d_res);
   if (c->h_res) (void)hipHostFree(c->h_res);
+  if (c->h_words) (void)hipHostFree(c->h_words);
   if (c->d_offs) (void)hipFree(c->d_offs);
   if (c->d_block_sums) (void)hipFree(c->d_block_sums);
   if (c->d_scan_part) (void)hipFree(c->d_scan_part);

@@ -324,6 +324,12 @@ struct IndexArgs {
   int32_t st_decode;
 };
 
+// Workgroups of the grid-stride kernels whose lanes run the general reader
+// for the few records / chunks the fast paths hand over (k_index.hip
+// SCRATCH_KERNEL): their per-lane scratch is backed per resident wave, so a
+// small grid keeps that backing small.
+constexpr uint32_t kScratchGrid = 64;
+
 #ifndef __HIPCC_RTC__
 // Launchers (defined in the .hip files; all asynchronous on `stream`).
 // `t` is the host copy (launch geometry), `d_t` the device copy the kernels read.
@@ -438,8 +444,12 @@ uint64_t index_tile_lanes();
 // Returns (in *fused) whether the records were decoded during the index
 // (a.recs set and the LDS-tile path taken); otherwise the caller decodes them
 // from the index.
+// h_sync (pinned, >= 4 words; nullptr: no host reads): the index may
+// synchronize to read its tile summary and skip the general-reader helper
+// kernels no tile needs; h_sync[3] then holds the record total (else it is
+// left alone).
 hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const JitKernels* jit,
-                               bool* fused);
+                               bool* fused, uint64_t* h_sync = nullptr);
 // After a fused index + decode over a stream range: re-diagnoses a record
 // the index accepted but the decode could not store (list arena overflow).
 hipError_t launch_stream_decode_finish(const DecodeArgs& a, int protocol, hipStream_t stream);

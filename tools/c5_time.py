@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--records", type=int, default=1 << 26)
     ap.add_argument("--variants", nargs="*", default=["1", "0"])
     ap.add_argument("--reps", type=int, default=8)
+    ap.add_argument("--sync-before", action="store_true",
+                    help="synchronize after the encode (decode starts on an idle GPU)")
     args = ap.parse_args()
     import torch
 
@@ -37,6 +39,8 @@ def main():
             torch.cuda.synchronize()
             e[0].record(s)
             wl.encode()
+            if args.sync_before:
+                torch.cuda.synchronize()
             e[1].record(s)
             t0 = time.perf_counter()
             wl.decode()
