@@ -776,6 +776,10 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
       need_fallback = need_cont || h_sync[1] != 0;
       need_merge = need_fallback || h_sync[2] != 0;
       pt.mark("summary");
+      if (pt.on)
+        fprintf(stderr, "  tiles %llu: partial %llu, no start %llu, broken links %llu\n",
+                (unsigned long long)C, (unsigned long long)h_sync[0],
+                (unsigned long long)h_sync[1], (unsigned long long)h_sync[2]);
     }
     if (need_cont)
       TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_cont_kernel<P_>, sg, b, 0, stream, a));
@@ -841,6 +845,7 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
     if (e != hipSuccess) return e;
     pt.mark("finish");
+    if (pt.on) fprintf(stderr, "  re-walked tiles %llu\n", (unsigned long long)h_sync[0]);
   }
   if (!defer || h_sync[0]) {
     TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_emit_cont_kernel<P_>, sg, b, 0, stream, x));

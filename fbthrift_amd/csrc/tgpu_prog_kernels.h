@@ -841,24 +841,29 @@ __device__ __forceinline__ bool tile_walk(const PP& P, const TileSrc& src, const
 #endif
 }
 
-// The tile's nvec 16-byte vectors HBM -> LDS by LDS DMA
-// (global_load_lds_dwordx4: no register round trip; lanes past the tile are
-// masked off, so nothing is written past nvec vectors). The caller's
-// __syncthreads waits for the loads.
+// The tile's nvec 16-byte vectors HBM -> LDS. Whole waves of vectors go by
+// LDS DMA (global_load_lds_dwordx4: no register round trip); the last
+// partial wave's vectors through registers. A DMA issued by a partially
+// masked wave corrupted the tile now and then (speculated chains broke at
+// random tiles, 200-600 of 217k per config-5 call, none under the profiler;
+// decode_tile's DMA covers whole waves too). The caller's __syncthreads
+// waits for the loads.
 __device__ __forceinline__ void stage_tile(uint8_t* lds, const uint8_t* gb, uint32_t nvec) {
 #ifdef TGPU_SPEC_REGSTAGE  // A/B: staging through registers
   for (uint32_t i = threadIdx.x; i < nvec; i += kTileLanes)
     ((uint4*)lds)[i] = ((const uint4*)gb)[i];
 #else
+  const uint32_t whole = nvec & ~63u;  // vectors in whole waves
   const uint32_t wave = threadIdx.x >> 6;
-  for (uint32_t k = 0; k * kTileLanes < nvec; ++k) {
-    const uint32_t i = k * kTileLanes + threadIdx.x;
-    if (i < nvec)
+  for (uint32_t k = 0; k * kTileLanes < whole; ++k) {
+    const uint32_t w0 = k * kTileLanes + wave * 64;  // this wave's first vector (uniform)
+    if (w0 < whole)
       __builtin_amdgcn_global_load_lds(
-          (const void*)((const uint4*)gb + i),
-          (__attribute__((address_space(3))) void*)(lds + (size_t)(k * kTileLanes + wave * 64) * 16),
-          16, 0, 0);
+          (const void*)((const uint4*)gb + w0 + (threadIdx.x & 63)),
+          (__attribute__((address_space(3))) void*)(lds + (size_t)w0 * 16), 16, 0, 0);
   }
+  const uint32_t i = whole + threadIdx.x;
+  if (i < nvec) ((uint4*)lds)[i] = ((const uint4*)gb)[i];
 #endif
 }
 
