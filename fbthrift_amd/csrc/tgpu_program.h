@@ -292,12 +292,26 @@ __device__ __forceinline__ bool skip_unknown_tail(const VOp op, const bool compa
 // one per op). Measured slower (decode config 3 1.47 -> 1.51 ms, config 4
 // 2.50 -> 2.69, config 5 6.70 -> 6.88; tools/kbench_jit.py), so off: every op
 // reads its own window.
+//
+// TGPU_CARRY: a CONST header's window also serves the op right after it when
+// that op's bytes (need) fit in the 8 - hdr_len left (decided by the op kinds
+// alone, so it folds away in the compiled programs). Measured: config 3
+// decode 1.468 vs 1.473 ms, config 4 2.68 vs 1.84 ms (slower), so off here;
+// the index's branch-free walk (measure_lds) keeps it.
 struct Win {
   uint64_t w = 0;
   uint32_t wp = 0;
   bool valid = false;
+  uint32_t carry = 0;  // hdr_len of the CONST just read (its window is w)
   template <class Src>
   __device__ __forceinline__ uint64_t at(const Src& src, uint32_t p, uint32_t need) {
+    const uint32_t h = carry;
+    carry = 0;
+#ifdef TGPU_CARRY
+    if (h && h + need <= 8) return w >> (8 * h);
+#else
+    (void)h;
+#endif
 #ifdef TGPU_WINCACHE
     const uint32_t d = p - wp;
     if (valid && d + need <= 8) return w >> (8 * d);
@@ -317,7 +331,7 @@ __device__ __forceinline__ bool run_op(const VOp op, const bool compact, const S
   switch (op.kind) {
     case VOP_CONST: {
       if (p + op.hdr_len > end) return false;
-      const uint32_t lo = (uint32_t)W.at(src, p, op.hdr_len);
+      const uint32_t lo = (uint32_t)W.at(src, p, 8);
       const uint32_t mask = op.hdr_len >= 4 ? 0xffffffffu : ((1u << (8 * op.hdr_len)) - 1);
       if ((lo ^ op.hdr) & mask) {
 #ifdef TGPU_NO_TAILS  // a compiled strict program (tgpu_jit.cpp)
@@ -329,6 +343,7 @@ __device__ __forceinline__ bool run_op(const VOp op, const bool compact, const S
 #endif
       }
       p += op.hdr_len;
+      W.carry = op.hdr_len;
       break;
     }
     case VOP_CBOOL: {
@@ -484,10 +499,24 @@ __device__ __forceinline__ bool measure_lds(const PP& P, const uint32_t* w32, ui
     x = ((x & 0x0fffffff00000000ull) >> 4) | (x & 0x000000000fffffffull);
     return (uint32_t)x;
   };
+  // A header's window also holds the value right after it: the op after a
+  // CONST of hdr_len h takes the window shifted by h when the bytes it may
+  // look at (need) fit in the 8 - h left, instead of a dependent LDS read.
+  // (Whether it does is decided by the op kinds alone, so in the compiled
+  // programs it folds away.) A Compact {header, varint} field is one read.
+  uint64_t cw = 0;
+  uint32_t carry = 0;  // hdr_len of the previous op when it was a CONST, else 0
+  auto rdv = [&](uint32_t need) {
+    const uint32_t h = carry;
+    carry = 0;
+    if (h && h + need <= 8) return cw >> (8 * h);
+    return rd(p);
+  };
   all_ops(P, [&](const VOp op) {
     switch (op.kind) {
       case VOP_CONST: {
-        const uint32_t lo = (uint32_t)rd(p);
+        const uint64_t w = rdv(8);
+        const uint32_t lo = (uint32_t)w;
         const uint32_t mask = op.hdr_len >= 4 ? 0xffffffffu : ((1u << (8 * op.hdr_len)) - 1);
         const bool hit = ((lo ^ op.hdr) & mask) == 0;
 #ifndef TGPU_NO_TAILS
@@ -495,10 +524,12 @@ __device__ __forceinline__ bool measure_lds(const PP& P, const uint32_t* w32, ui
 #endif
         ok &= p + op.hdr_len <= end && hit;
         p += op.hdr_len;
+        cw = w;
+        carry = op.hdr_len;
         break;
       }
       case VOP_CBOOL: {
-        const uint32_t lo = (uint32_t)rd(p);
+        const uint32_t lo = (uint32_t)rdv(8);
         const uint32_t mask =
             (op.hdr_len >= 4 ? 0xffffffffu : ((1u << (8 * op.hdr_len)) - 1)) & ~0xfu;
         const uint32_t ct = lo & 0xf;
@@ -507,13 +538,15 @@ __device__ __forceinline__ bool measure_lds(const PP& P, const uint32_t* w32, ui
         break;
       }
       case VOP_FIXED: {
-        const uint64_t v = bswap_n(rd(p), op.width);
+        const uint64_t v = bswap_n(rdv(op.width), op.width);
         ok &= p + op.width <= end && !(op.is_bool && v > 1);
         p += op.width;
         break;
       }
       case VOP_VARINT: {
-        const uint64_t w = rd(p);
+        // (an i32 varint's verdict needs its first 5 bytes: a longer one
+        // fails either way; an i64's needs the whole window)
+        const uint64_t w = rdv(op.bits == 32 ? 5 : 8);
         const uint64_t stop = ~w & 0x8080808080808080ull;
         const uint32_t len = stop ? ((uint32_t)__builtin_ctzll(stop) >> 3) + 1 : 8;
         if (op.bits == 32) {
@@ -526,7 +559,7 @@ __device__ __forceinline__ bool measure_lds(const PP& P, const uint32_t* w32, ui
         break;
       }
       case VOP_STRING: {
-        const uint64_t w = rd(p);
+        const uint64_t w = rdv(compact ? 5 : 4);
         uint32_t hl, n;
         if (compact) {
           n = var32(w, hl);
@@ -543,7 +576,7 @@ __device__ __forceinline__ bool measure_lds(const PP& P, const uint32_t* w32, ui
         break;
       }
       case VOP_LIST: {
-        const uint64_t w = rd(p);
+        const uint64_t w = rdv(compact ? 1 : 5);
         int64_t n;
         if (compact) {
           const uint32_t b = (uint32_t)(w & 0xff);
@@ -577,9 +610,10 @@ __device__ __forceinline__ bool measure_lds(const PP& P, const uint32_t* w32, ui
         break;
       }
       case VOP_ISSET:
-        break;
+        break;  // (no bytes: a carried window stays valid)
       default:
         sl |= ok;
+        carry = 0;
         break;
     }
     return true;
