@@ -756,8 +756,11 @@ __device__ __forceinline__ uint64_t chunk_hi(const IndexArgs& a, uint64_t j) {
 // (the HBM path is rare — records straddling the staged bytes — and kept out
 // of line: inlined at every window of an unrolled program it multiplies the
 // schema compiler's code size and compile time)
-__device__ __attribute__((noinline)) uint64_t hbm_win8(const HbmSrc g, uint32_t p) {
-  return g.win8(p);
+// (out-of-line helpers take plain scalars: a struct passed by value to a
+// call goes through scratch, stored by every lane of every tile)
+__device__ __attribute__((noinline)) uint64_t hbm_win8(const uint8_t* base, uint32_t avail,
+                                                       uint32_t p) {
+  return HbmSrc{base, avail}.win8(p);
 }
 struct TileSrc {
   const uint32_t* w32;
@@ -765,7 +768,7 @@ struct TileSrc {
   HbmSrc g;
   __device__ __forceinline__ uint64_t win8(uint32_t p) const {
     if (p + 12 <= lds_len) return LdsSrc{w32}.win8(p);
-    return hbm_win8(g, p);
+    return hbm_win8(g.base, g.avail, p);
   }
 };
 
@@ -815,14 +818,19 @@ __device__ __forceinline__ bool quick_reject(const PP& P, const TileSrc& src, ui
 
 // run_program<false> over the tile source, out of line: the rare records the
 // branch-free walk leaves undecided (see measure_lds)
+// (returns ok << 32 | the end: a position passed by address would live in
+// scratch, stored on every walk of the hot path)
 template <class PP>
-__device__ __attribute__((noinline)) bool tile_walk_slow(const PP P, const TileSrc src,
-                                                         const Ctx pc, uint32_t* pos,
-                                                         uint32_t end) {
-  uint32_t q = *pos;
+__device__ __attribute__((noinline)) uint64_t tile_walk_slow(const PP P, const uint32_t* w32,
+                                                             uint32_t lds_len, const uint8_t* gb,
+                                                             uint32_t avail, int32_t string_limit,
+                                                             int32_t container_limit, uint32_t pos,
+                                                             uint32_t end) {
+  const TileSrc src{w32, lds_len, HbmSrc{gb, avail}};
+  const Ctx pc{0, nullptr, 0, string_limit, container_limit};
+  uint32_t q = pos;
   const bool ok = run_program<false>(P, src, pc, q, end, nullptr);
-  *pos = q;
-  return ok;
+  return ((uint64_t)ok << 32) | q;
 }
 
 // One record's measuring walk at q (tile-relative): branch-free over the
@@ -836,7 +844,12 @@ __device__ __forceinline__ bool tile_walk(const PP& P, const TileSrc& src, const
   bool slow = src.lds_len < 12;
   bool ok = false;
   if (!slow) ok = measure_lds(P, src.w32, src.lds_len - 12, pc, q, end, slow);
-  if (slow) ok = tile_walk_slow(P, src, pc, &q, end);
+  if (slow) {
+    const uint64_t r = tile_walk_slow(P, src.w32, src.lds_len, src.g.base, src.g.avail,
+                                      pc.string_limit, pc.container_limit, q, end);
+    q = (uint32_t)r;
+    ok = (r >> 32) != 0;
+  }
   return ok;
 #endif
 }
@@ -1078,22 +1091,16 @@ __device__ __forceinline__ void index_spec_tile(const IndexArgs& a, const PP& P,
     }
   }
   if (threadIdx.x == kTileLanes - 1) {
-    if (first == kNoPos) {
-      a.s[j] = kNo;
-      a.e[j] = kNo;
-      a.cnt[j] = 0;
-    } else if (!ok) {
-      // the general reader walks the whole tile from its (speculated) start
-      a.s[j] = lo - sh + first;
-      a.e[j] = kPartial;
-      a.pf[j] = lo - sh + first;
-      a.cnt[j] = 0;
-    } else {
-      a.s[j] = lo - sh + first;
-      a.e[j] = lo - sh + L.e;
-      a.cnt[j] = tile_n;
-      a.pf[j] = stored ? kStartsValid : kLanesValid;
-    }
+    // (values selected, then one store each: branches storing to different
+    // fields made the compiler keep a table of the field pointers in
+    // scratch, written by every lane of every tile)
+    const bool none = first == kNoPos;
+    const uint64_t st = lo - sh + first;
+    a.s[j] = none ? kNo : st;
+    // !ok: the general reader walks the whole tile from its (speculated) start
+    a.e[j] = none ? kNo : (!ok ? kPartial : lo - sh + L.e);
+    a.cnt[j] = none || !ok ? 0 : tile_n;
+    if (!none) a.pf[j] = !ok ? st : (stored ? kStartsValid : kLanesValid);
   }
 }
 
