@@ -945,14 +945,20 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
     for (uint32_t g = threadIdx.x; g < ngroups; g += kTileLanes) {
       const uint32_t base = g << 3;
       uint64_t m = 0x8080808080808080ull;
-      const uint64_t w = src.win8(base);
+      // the group's 8 bytes (8-byte aligned: one LDS read) and the byte
+      // before them (one more), where staged; HBM windows past that
+      const bool in_lds = base + 8 <= src.lds_len;
+      const uint64_t w = in_lds ? *(const uint64_t*)(lds + base) : src.win8(base);
       if (h0 < 0x100) {
         const uint64_t x = w ^ (h0 * 0x0101010101010101ull);
         m = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
       }
       if (stop < 0x100) {
         // byte i of y = the byte before position base + i
-        const uint64_t y = (base ? src.win8(base - 1) : (w << 8)) ^ (stop * 0x0101010101010101ull);
+        const uint64_t prev = !base ? (w << 8)
+                              : in_lds ? (w << 8) | lds[base - 1]
+                                       : src.win8(base - 1);
+        const uint64_t y = prev ^ (stop * 0x0101010101010101ull);
         uint64_t z = (y - 0x0101010101010101ull) & ~y & 0x8080808080808080ull;
         if (!base) z |= 0x80ull;  // position 0: predecessor not staged
         // the range's first byte has no predecessor inside the range
@@ -979,11 +985,12 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
     // candidates that survive quick_reject are chained in order (divergent
     // but cheap); the chain runs outside the search so all lanes of the
     // wave run it together
+    // (the slice's 64 bits from the 8-byte aligned words around them)
     const uint32_t g0 = sub_lo >> 3, off = sub_lo & 7;
-    uint64_t lo8 = 0;
-#pragma unroll
-    for (uint32_t i = 0; i < 8; ++i) lo8 |= (uint64_t)cmask[g0 + i] << (8 * i);
-    uint64_t cm = (lo8 >> off) | (off ? ((uint64_t)cmask[g0 + 8] << (64 - off)) : 0);
+    const uint32_t d = g0 >> 3, bo = (g0 & 7) * 8 + off;  // bit offset in word d
+    const uint64_t* cw = (const uint64_t*)cmask;
+    const uint64_t c0 = cw[d], c1 = cw[d + 1];
+    uint64_t cm = bo ? (c0 >> bo) | (c1 << (64 - bo)) : c0;
     if (sub_hi - sub_lo < 64) cm &= (1ull << (sub_hi - sub_lo)) - 1;
     bool need = true;
     while (need) {
@@ -1052,7 +1059,7 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
 }
 
 struct IndexTileShared {
-  uint8_t cmask[kTile / 8 + 16];  // candidate bits of the tile (one per byte)
+  alignas(8) uint8_t cmask[kTile / 8 + 16];  // candidate bits of the tile (one per byte)
   uint32_t E[kTileLanes];
   int flag;
   uint32_t first_lane, fs;
