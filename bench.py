@@ -382,9 +382,12 @@ class FileShards(Mixed):
         import torch.distributed as dist
 
         super().__init__(n, rank, dev)
-        # the decode call is the fused index + decode (tgpu_decode_stream)
-        self.dec_kernel = ("tgpu_jit_index_decode" if self.dec_kernel.startswith("tgpu_jit")
-                           else "index_tile_decode_kernel")
+        # the decode call (tgpu_decode_stream): the index speculation, the
+        # copy of its stored record starts, the indexed program decode
+        self.dec_kernel = ("tgpu_jit_index_spec+index_starts_copy_kernel+tgpu_jit_decode"
+                           if self.dec_kernel.startswith("tgpu_jit")
+                           else "index_tile_spec_kernel+index_starts_copy_kernel+"
+                                "program_decode_kernel")
         self.rank, self.dev = rank, dev
         self.world = dist.get_world_size() if dist.is_initialized() else 1
         self.enc = self.wire  # this rank's part of the file (in file order)
@@ -925,6 +928,7 @@ def pmc_traffic(kernel, n, config=2):
     profiles/pmc_latest.json, written by tools/pmc_summary.py from separate
     --pmc passes, gfx950 FETCH_SIZE x2 correction applied), scaled to
     this launch's record count; None when no summary exists."""
+    # `kernel` may name the kernels of one call joined by '+': their sum
     for name in ("pmc_c%d.json" % config, "pmc_latest.json"):
         path = os.path.join(ROOT, "profiles", name)
         try:
@@ -932,7 +936,7 @@ def pmc_traffic(kernel, n, config=2):
                 d = json.load(f)
             if d.get("config", 2) != config:
                 continue
-            return int(d[kernel]["hbm_bytes_per_record"] * n)
+            return int(sum(d[k]["hbm_bytes_per_record"] for k in kernel.split("+")) * n)
         except (OSError, KeyError, ValueError):
             continue
     return None

@@ -89,7 +89,7 @@ def main_config(root, config):
     for k in sorted(set(fetch) & set(write)):
         fb = avg(fetch[k]) * 1024 * ff
         wb = avg(write[k]) * 1024 * wf
-        if fb + wb < 64 * n:  # bookkeeping kernels: skip
+        if fb + wb < 4 * n:  # bookkeeping kernels: skip
             continue
         d = {"fetch_bytes": int(fb), "write_bytes": int(wb), "raw_fetch_kib": avg(fetch[k]),
              "raw_write_kib": avg(write[k]), "dispatches": [len(fetch[k]), len(write[k])],
