@@ -968,6 +968,7 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
       cmask[g] = (uint8_t)((((m >> 7) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
     }
     for (uint32_t g = ngroups + threadIdx.x; g < ngroups + 9; g += kTileLanes) cmask[g] = 0;
+    if (threadIdx.x == 0) *first_lane = ~0u;  // (the first-start minimum below)
   }
   __syncthreads();
   L.s = kNoPos;
@@ -1011,20 +1012,24 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
       }
     }
   }
-  // the tile's first start: the first lane that found one
-  if (k == 0) *first_lane = kTileLanes;
+  // the tile's first start: the first lane that found one, and its start,
+  // in one packed minimum (lane << 16 | start: starts are below 64 Ki;
+  // *first_lane was reset before the candidate-mask barrier)
+  if (L.s != kNoPos) atomicMin(first_lane, (k << 16) | (L.s < 0xffffu ? L.s : 0xffffu));
   __syncthreads();
-  if (L.s != kNoPos) atomicMin(first_lane, k);
-  __syncthreads();
-  const uint32_t f = *first_lane;
-  if (f == kTileLanes) {
+  const uint32_t fv = *first_lane;
+  if (fv == ~0u) {
     first = kNoPos;
     return true;
   }
+  const uint32_t f = fv >> 16;
+  uint32_t fs = fv & 0xffffu;
+  if (fs == 0xffffu) {  // (a start 64 Ki or more into the tile: an entry past a long record)
+    if (k == f) *fs_p = L.s;
+    __syncthreads();
+    fs = *fs_p;
+  }
   // lanes before it: no record starts there
-  if (k == f) *fs_p = L.s;
-  __syncthreads();
-  const uint32_t fs = *fs_p;
   if (k < f) {
     L.s = L.e = fs;
     L.c = 0;
@@ -1051,11 +1056,8 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
     }
     if (!__syncthreads_or(changed)) break;
   }
-  *flag = 0;
-  __syncthreads();
-  if (L.stuck || L.e == kNoPos) *flag = 1;
-  __syncthreads();
-  return *flag == 0;
+  (void)flag;
+  return !__syncthreads_or(L.stuck || L.e == kNoPos);
 }
 
 struct IndexTileShared {
