@@ -999,7 +999,9 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
       while (cm) {
         const uint32_t c = sub_lo + (uint32_t)__builtin_ctzll(cm);
         cm &= cm - 1;
+#ifndef TGPU_NO_QUICK_REJECT  // A/B: the measuring walk alone rejects false candidates
         if (quick_reject(P, src, c)) continue;
+#endif
         cand = c;
         break;
       }
