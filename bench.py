@@ -183,6 +183,7 @@ def cpu_baseline(wl, seconds=8.0):
 class Workload:
     """One BASELINE config: resident inputs, one encode+decode step, checks."""
     total_wire_bytes = None  # whole-job bytes per direction (default: per rank x world)
+    parallelism = "dp%d (independent record shards, no collective)"
 
     def timed_step(self, ev):
         ev[0].record(self.stream)
@@ -373,14 +374,13 @@ class FileShards(Mixed):
     index, and re-encoding the decoded records reproduces the range's bytes.
     """
     config_id = 5
+    parallelism = ("dp%d (one file split by bytes: all_to_all_single of the byte ranges + "
+                   "all_gather of the range boundaries)")
     name = ("config 5: Compact protocol, {4 x i32, 2 x string[0..32]} file split by bytes "
             "across GPUs, encode + boundary discovery + decode")
     overlap = 1 << 20
 
     def __init__(self, n, rank, dev):
-        import torch
-        import torch.distributed as dist
-
         super().__init__(n, rank, dev)
         # the decode call (tgpu_decode_stream): the index speculation, the
         # copy of its stored record starts, the indexed program decode
@@ -388,16 +388,24 @@ class FileShards(Mixed):
                            if self.dec_kernel.startswith("tgpu_jit")
                            else "index_tile_spec_kernel+index_starts_copy_kernel+"
                                 "program_decode_kernel")
+        self.setup_file(rank, dev)
+
+    def setup_file(self, rank, dev):
+        """The file layout every rank agrees on: each rank's encode output is
+        the file's next `wire_bytes` bytes (ranks in order); rank k owns the
+        bytes [B_k, B_k+1) and holds need_range(k) after the redistribution."""
+        import torch
+
+        from fbthrift_amd import shard
+
         self.rank, self.dev = rank, dev
-        self.world = dist.get_world_size() if dist.is_initialized() else 1
+        self.world = self.world_size()
         self.enc = self.wire  # this rank's part of the file (in file order)
         self.enc_offs = self.offs
         sizes = self._gather([self.wire_bytes])
         self.file_off = sum(r[0] for r in sizes[:rank])
         self.file_len = sum(r[0] for r in sizes)
         self.total_wire_bytes = self.file_len
-        from fbthrift_amd import shard
-
         self.ranges = shard.byte_ranges(self.file_len, self.world)
         self.enc_ranges = []
         off = 0
@@ -411,6 +419,39 @@ class FileShards(Mixed):
         self.idx = torch.empty(self.n * 2 + 2, dtype=torch.int64, device=dev)
         self.back = torch.empty(self.n * 2 * self.record_bytes, dtype=torch.uint8, device=dev)
         self.n_local = 0
+
+    def index_range(self, local, begin, end, speculative):
+        """Record starts + records of the records that start in
+        [begin, end) of `local` (this rank's held bytes): one
+        tgpu_decode_stream call. Returns (n, first, last, status)."""
+        recs, _, _, n, first, last, st = self.S.decode_stream(
+            self.gs, local, begin=begin, end=end, speculative=speculative,
+            max_records=self.idx.numel() - 1, offsets=self.idx, records=self.back)
+        return n, first, last, st
+
+    def expected_records(self, base, n):
+        """The generator's records [base, base + n) in the record layout (for
+        verify)."""
+        import ctypes
+
+        import torch
+
+        import datagen
+
+        lib = ctypes.CDLL(os.path.join(ROOT, "tools", "build", "libtgpu_datagen.so"))
+        want = torch.empty(n * self.record_bytes, dtype=torch.uint8, device=self.dev)
+        side = torch.empty(n * 64, dtype=torch.uint8, device=self.dev)
+        if lib.tgpu_gen_mixed(ctypes.c_uint64(datagen.SEED), ctypes.c_uint64(base),
+                              ctypes.c_uint64(n), ctypes.c_void_p(want.data_ptr()),
+                              ctypes.c_void_p(side.data_ptr()),
+                              ctypes.c_void_p(self.stream.cuda_stream)):
+            raise RuntimeError("generator failed")
+        return want
+
+    def reencode(self, records, n, local):
+        """Re-encodes decoded records whose strings view `local`."""
+        again, _ = self.S.serialize(self.gs, records, n, string_base=local)
+        return again
 
     # ---- collectives ---------------------------------------------------------
     def _gather(self, vals):
@@ -448,11 +489,9 @@ class FileShards(Mixed):
         self.status = None
 
         def index_fn(begin, speculative):
-            # fused index + decode of the records that start in [begin, e)
-            # (tgpu_decode_stream); a re-run after the exchange replaces them
-            recs, _, _, n, first, last, st = self.S.decode_stream(
-                self.gs, local, begin=begin - lo, end=e - lo, speculative=speculative,
-                max_records=cap, offsets=self.idx, records=self.back)
+            # index + decode of the records that start in [begin, e); a re-run
+            # after the exchange replaces them
+            n, first, last, st = self.index_range(local, begin - lo, e - lo, speculative)
             self.status = st
             if n == 0:
                 return 0, shard.NONE, shard.NONE
@@ -468,11 +507,7 @@ class FileShards(Mixed):
                 self.status.as_tuple() if self.status is not None else None,))
 
     def verify(self):
-        import ctypes
-
         import torch
-
-        import datagen
 
         self.check_timed()
         counts = self._gather([self.n_local])
@@ -482,24 +517,17 @@ class FileShards(Mixed):
         n, rs = self.n_local, self.record_bytes
         if n == 0:
             return
-        lib = ctypes.CDLL(os.path.join(ROOT, "tools", "build", "libtgpu_datagen.so"))
-        want = torch.empty(n * rs, dtype=torch.uint8, device=self.dev)
-        side = torch.empty(n * 64, dtype=torch.uint8, device=self.dev)
-        if lib.tgpu_gen_mixed(ctypes.c_uint64(datagen.SEED), ctypes.c_uint64(self.base),
-                              ctypes.c_uint64(n), ctypes.c_void_p(want.data_ptr()),
-                              ctypes.c_void_p(side.data_ptr()),
-                              ctypes.c_void_p(self.stream.cuda_stream)):
-            raise RuntimeError("generator failed")
+        want = self.expected_records(self.base, n)
         a, b = want.view(n, rs), self.back[: n * rs].view(n, rs)
         for lo, hi in self.fixed_ranges:
             if not torch.equal(a[:, lo:hi], b[:, lo:hi]):
                 raise RuntimeError("decoded records differ from the generator's")
         lo = self.need[0]
         local = self.buf[: self.need[1] - lo]
-        again, offs2 = self.S.serialize(self.gs, self.back[: n * rs], n, string_base=local)
+        again = self.reencode(self.back[: n * rs], n, local)
         if not torch.equal(again, local[self.first - lo: self.last - lo]):
             raise RuntimeError("re-encoded records differ from the file's bytes")
-        del want, side, again, offs2
+        del want, again
 
     def algorithmic(self):
         # per rank, per step: encode as config 3; decode (index + records in
@@ -512,9 +540,89 @@ class FileShards(Mixed):
 WORKLOADS = {2: Flat8, 3: Mixed, 4: Nested, 5: FileShards}
 
 
-def main():
+class CudaRuntime:
+    """Where the ranks run: one process per MI355X, RCCL (torch's "nccl"
+    backend) for the barrier, the max-over-ranks timing and config 5's
+    exchange; HIP events on the launch stream."""
+    backend = "nccl"
+
+    def setup(self, local):
+        import torch
+
+        # ranks beyond the visible GPUs share them round-robin (only with
+        # --backend gloo: a one-GPU rehearsal of the multi-rank path)
+        local %= max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        return torch.device("cuda", local)
+
+    def init_group(self, dev):
+        import torch.distributed as dist
+
+        if self.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(self.backend)
+
+    def sync(self):
+        import torch
+
+        torch.cuda.synchronize()
+
+    def event(self):
+        import torch
+
+        return torch.cuda.Event(enable_timing=True)
+
+
+RUNTIME = CudaRuntime()
+
+
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """`--gpus N` without a launcher: start N ranks (one per GPU) with
+    torch.distributed.run on 127.0.0.1 as a CHILD process, re-running this
+    same script (sys.argv[0]) with the same arguments, and return its exit
+    code. Called before anything touches the GPU; the parent never does."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=%d" % n, "--master-addr=127.0.0.1",
+           "--master-port=%d" % _free_port(), os.path.abspath(sys.argv[0])] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def resolve_world(gpus):
+    """(world, rank, local_rank) from the launcher's environment, checked
+    against --gpus; (None, None, None) when this process must launch the
+    ranks itself."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if gpus is not None and gpus > 1:
+            return None, None, None
+        return 1, 0, 0
+    world = int(env_world)
+    if gpus is not None and gpus != world:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (gpus, world))
+    return world, int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); without a launcher (no WORLD_SIZE) N > 1 "
+                         "starts N ranks with torch.distributed.run")
+    ap.add_argument("--backend", default=None, choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1 (default nccl = RCCL over xGMI; "
+                         "gloo lets N ranks share one GPU to rehearse the multi-rank path)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2, choices=[1] + sorted(WORKLOADS))
@@ -536,21 +644,27 @@ def main():
     ap.add_argument("--transcode", action="store_true",
                     help="also time device transcoding of the workload's stream into the "
                          "other protocol (tgpu_transcode_batch)")
-    args = ap.parse_args()
+    ap.add_argument("--host-batch", action="store_true",
+                    help="also time the IOBuf batch API (deserializeBatch / serializeBatch "
+                         "into std:: objects, tests/cpp/host_batch_bench) for configs 3/4")
+    args = ap.parse_args(argv)
     if args.config == 1:
         print(json.dumps(config1()), flush=True)
-        return
+        return 0
+
+    world, rank, local = resolve_world(args.gpus)
+    if world is None:
+        return launch_ranks(args.gpus)
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    rt = RUNTIME
+    if args.backend:
+        rt.backend = args.backend
+    dev = rt.setup(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+        rt.init_group(dev)
 
     W = WORKLOADS[args.config]
     n = args.records or W.default_records
@@ -559,17 +673,17 @@ def main():
     for _ in range(args.warmup):
         wl.encode()
         wl.decode()
-    torch.cuda.synchronize()
+    rt.sync()
     wl.verify()
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    evs = [[rt.event() for _ in range(3)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    rt.sync()
     t0 = time.perf_counter()
     for k in range(args.steps):
         wl.timed_step(evs[k])
-    torch.cuda.synchronize()
+    rt.sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -593,10 +707,10 @@ def main():
         "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic: splitmix64(seed 0x1729) records per tests/golden/datagen.py, "
                 "generated on device",
-        "config": {"workload": wl.name, "records_per_gpu": n, "wire_bytes_per_gpu": wl.wire_bytes,
+        "config": {"workload": wl.name, "records_per_gpu": n, "records_total": n * world, "wire_bytes_per_gpu": wl.wire_bytes,
                    "record_bytes": wl.record_bytes,
                    "wire_bytes_per_record": round(wl.wire_bytes / n, 3),
-                   "parallelism": "dp%d (independent record shards, no collective)" % world},
+                   "parallelism": wl.parallelism % world},
         "roofline": {"bound": "hbm", "kernel": wl.dec_kernel,
                      "achieved": round(dec_alg / dec_avg / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(dec_alg / dec_avg / 1e9 / HBM_PEAK_GBS, 4),
@@ -626,10 +740,13 @@ def main():
         line["nested"] = nested(dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(wl)
+    if args.host_batch and rank == 0:
+        line["host_batch"] = host_batch(wl)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 # Config 4's shape with containers of structs and of containers (the nested
@@ -1036,6 +1153,11 @@ def skim(wl, dev, reps=10):
         "check": "64 sampled records vs the oracle"}
 
 
+def host_batch(wl):
+    """Placeholder until the IOBuf batch bench exists."""
+    return {"skipped": "not built"}
+
+
 def host_start(wl, dev):
     """Host-memory start/end rates (PCIe-inclusive), never
     `value`. Config 2 runs the library's host path (tgpu_encode_host /
@@ -1111,4 +1233,4 @@ def host_start(wl, dev):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
