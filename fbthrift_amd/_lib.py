@@ -79,6 +79,7 @@ EXPORTS = [
     "tgpu_decode_batch", "tgpu_index_stream", "tgpu_schema_compile", "tgpu_schema_compile_check",
     "tgpu_decode_host", "tgpu_encode_host", "tgpu_decode_stream", "tgpu_transcode_batch",
     "tgpu_schema_arena_scale", "tgpu_decode_host_ex", "tgpu_encode_host_ex", "tgpu_skim_batch",
+    "tgpu_index_stats",
 ]
 
 # tgpu_skim_field as a numpy record (16 bytes).
@@ -123,6 +124,8 @@ def lib():
     L.tgpu_context_wait.restype = I32
     L.tgpu_context_wait.argtypes = [P, P, ctypes.POINTER(Status), ctypes.POINTER(U64),
                                     ctypes.POINTER(U64)]
+    L.tgpu_index_stats.restype = I32
+    L.tgpu_index_stats.argtypes = [P, P, P]
     L.tgpu_encode_batch.restype = I32
     L.tgpu_encode_batch.argtypes = [P, P, I32, P, U64, P, P, P, U64, P, P,
                                     ctypes.POINTER(Status), ctypes.POINTER(U64)]

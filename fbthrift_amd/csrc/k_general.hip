@@ -345,7 +345,8 @@ hipError_t launch_general_decode(const DecodeArgs& a, int protocol, hipStream_t 
     // LDS tile for 256 records of the stream's mean size, with slack
     const uint64_t mean = (a.in_len + a.n - 1) / a.n;
     const uint64_t want = ((mean * 256 * 5 / 4 + 15) & ~15ull) + 32;
-    const uint32_t cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 4096), 64 * 1024);
+    // (cap + 16 bytes of dynamic LDS stay within 64 KiB per workgroup)
+    const uint32_t cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 4096), 64 * 1024 - 16);
     const uint64_t blocks = (a.n + 255) / 256;
     TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(general_decode_tile_kernel<P_>,
                                                   dim3((uint32_t)blocks), dim3(256), cap + 16,

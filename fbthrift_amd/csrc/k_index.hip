@@ -756,40 +756,42 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
   const dim3 g((uint32_t)((C + 255) / 256)), b(256);
   const dim3 sg((uint32_t)std::min<uint64_t>((C + 255) / 256, kScratchGrid));
   bool need_cont = true, need_fallback = true, need_merge = true;
-  if (a.prog && a.chunk == kTile) {
+  const bool tiles = a.prog && a.chunk == kTile;
+  if (tiles) {
     if (jit) {
       const hipError_t e = jit_launch_index(jit, 0, a, C, stream);
       if (e != hipSuccess) return e;
     } else {
       hipLaunchKernelGGL(index_tile_spec_kernel, dim3((uint32_t)C), dim3(kTileLanes), 0, stream, a);
     }
-    pt.mark("spec");
-    if (h_sync) {
-      hipError_t e = hipMemsetAsync(a.scal + 8, 0, 3 * sizeof(unsigned long long), stream);
-      hipLaunchKernelGGL(index_summary_kernel, g, b, 0, stream, a);
-      if (e == hipSuccess)
-        e = hipMemcpyAsync(h_sync, a.scal + 8, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream);
-      if (e == hipSuccess) e = hipStreamSynchronize(stream);
-      if (e != hipSuccess) return e;
-      // the fallback and the repair act on what the continuation leaves
-      need_cont = h_sync[0] != 0;
-      need_fallback = need_cont || h_sync[1] != 0;
-      need_merge = need_fallback || h_sync[2] != 0;
-      pt.mark("summary");
-      if (pt.on)
-        fprintf(stderr, "  tiles %llu: partial %llu, no start %llu, broken links %llu\n",
-                (unsigned long long)C, (unsigned long long)h_sync[0],
-                (unsigned long long)h_sync[1], (unsigned long long)h_sync[2]);
-    }
-    if (need_cont)
-      TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_cont_kernel<P_>, sg, b, 0, stream, a));
-    pt.mark("cont");
   } else if (a.prog) {
     hipLaunchKernelGGL(index_spec_kernel, g, b, 0, stream, a);
-    TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_cont_kernel<P_>, sg, b, 0, stream, a));
   } else {
     TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_spec_general_kernel<P_>, g, b, 0, stream, a));
   }
+  pt.mark("spec");
+  // what the speculation left to repair: read mid-call by blocking tile
+  // calls (to skip the helpers nothing needs), kept for tgpu_index_stats
+  hipError_t e = hipMemsetAsync(a.scal + 8, 0, 3 * sizeof(unsigned long long), stream);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(index_summary_kernel, g, b, 0, stream, a);
+  if (tiles && h_sync) {
+    e = hipMemcpyAsync(h_sync, a.scal + 8, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    if (e != hipSuccess) return e;
+    // the fallback and the repair act on what the continuation leaves
+    need_cont = h_sync[0] != 0;
+    need_fallback = need_cont || h_sync[1] != 0;
+    need_merge = need_fallback || h_sync[2] != 0;
+    pt.mark("summary");
+    if (pt.on)
+      fprintf(stderr, "  tiles %llu: partial %llu, no start %llu, broken links %llu\n",
+              (unsigned long long)C, (unsigned long long)h_sync[0],
+              (unsigned long long)h_sync[1], (unsigned long long)h_sync[2]);
+  }
+  if (a.prog && need_cont)
+    TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_cont_kernel<P_>, sg, b, 0, stream, a));
+  pt.mark("cont");
   // (a speculative range opens at its first program-confirmed start: a
   // general-reader start there has no predecessor chunk to verify it)
   if (a.prog && !a.speculative && need_fallback)
@@ -797,11 +799,13 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
   pt.mark("fallback");
   if (need_merge)
     TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_merge_kernel<P_>, sg, b, 0, stream, a));
-  // sst is written by the general speculation and the fallback only
-  const int sst_valid = !a.prog || !a.speculative;
+  // sst is written by the general speculation and the fallback only (and by
+  // the fallback only when it ran: a skipped one leaves an earlier call's
+  // starts in the reused workspace)
+  const int sst_valid = !a.prog || (!a.speculative && need_fallback);
   pt.mark("merge");
   hipLaunchKernelGGL(index_flag_kernel, g, b, 0, stream, a, sst_valid);
-  hipError_t e = launch_scan_tiles(a.base, C, a.part, a.scal, nullptr, stream);
+  e = launch_scan_tiles(a.base, C, a.part, a.scal, nullptr, stream);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(index_list_kernel, g, b, 0, stream, a);
   TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_fix_kernel<P_>, dim3(1), dim3(64), 0, stream, a));

@@ -78,8 +78,14 @@ __device__ __forceinline__ unsigned long long decode_word(const FixedPlan* P,
 
 // The rare path of a word the plan cannot take (kept out of the wave-uniform
 // main loop: no ballot there).
-__device__ __attribute__((noinline)) void note_word_exception(uint64_t i, DevResult* res,
+// seen: the tile's LDS bitmap of records already listed (a record with
+// several failing words is listed once: duplicates would make several
+// exception lanes decode the same record into the same slot).
+__device__ __attribute__((noinline)) void note_word_exception(uint64_t i, uint32_t r,
+                                                              uint32_t* seen, DevResult* res,
                                                               uint64_t* exc, uint64_t cap) {
+  const uint32_t bit = 1u << (r & 31);
+  if (atomicOr(&seen[r >> 5], bit) & bit) return;
   atomicMin(&res->first_irregular, (unsigned long long)i);
   const unsigned long long k = atomicAdd(&res->n_irregular, 1ull);
   if (k < cap) exc[k] = i;
@@ -121,6 +127,8 @@ __global__ __launch_bounds__(T) void plan_binary_decode_kernel(
   }
   for (uint32_t i = threadIdx.x; i < (uint32_t)(sizeof(FixedPlan) / 16); i += T)
     ((uint4*)P)[i] = ((const uint4*)pp)[i];
+  uint32_t* seen = (uint32_t*)(smem + wire_region(T, L) + sizeof(FixedPlan));
+  if (threadIdx.x < T / 32) seen[threadIdx.x] = 0;
   __syncthreads();
 
   const uint32_t* w32 = (const uint32_t*)smem;
@@ -135,8 +143,8 @@ __global__ __launch_bounds__(T) void plan_binary_decode_kernel(
       if (kNT) __builtin_nontemporal_store(v, o + q);
       else o[q] = v;
       // a record one of whose words the plan cannot take joins the exception
-      // list (once per word that failed: duplicates read the same record again)
-      if (!ok) note_word_exception(tile0 + r, res, exc, exc_cap);
+      // list (once)
+      if (!ok) note_word_exception(tile0 + r, r, seen, res, exc, exc_cap);
       r += sr;
       j += sj;
       if (j >= Q) {
@@ -161,8 +169,8 @@ __global__ __launch_bounds__(T) void plan_binary_decode_kernel(
       } else {
         o[q] = v0;
       }
-      if (!ok0) note_word_exception(tile0 + r, res, exc, exc_cap);
-      if (!ok1) note_word_exception(tile0 + r1, res, exc, exc_cap);
+      if (!ok0) note_word_exception(tile0 + r, r, seen, res, exc, exc_cap);
+      if (!ok1) note_word_exception(tile0 + r1, r1, seen, res, exc, exc_cap);
       r += sr;
       j += sj;
       if (j >= Q) {
@@ -348,7 +356,8 @@ hipError_t launch_plan_binary_decode(const FixedPlan* p, const FixedPlan* d_p, c
   DecVariant use = v;
   if (((uintptr_t)out & 15) != 0) use.pair = 0;  // 16-byte stores need 16-byte records base
   const uint64_t blocks = (n + use.T - 1) / use.T;
-  const uint32_t lds = wire_region(use.T, p->wire_len) + (uint32_t)sizeof(FixedPlan);
+  // + the tile's bitmap of listed exception records (one bit per record)
+  const uint32_t lds = wire_region(use.T, p->wire_len) + (uint32_t)sizeof(FixedPlan) + use.T / 8;
   auto* o = (unsigned long long*)out;
   switch (use.T) {
     case 128: return launch_dec_T<128>(use, lds, blocks, stream, d_p, in, n, o, res, exc, exc_cap);

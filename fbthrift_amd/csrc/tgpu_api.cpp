@@ -63,6 +63,9 @@ struct tgpu_context {
   // stream indexer workspace (per chunk)
   uint8_t* d_index = nullptr;
   uint64_t index_bytes = 0;
+  // the last two-pass index's counters (tgpu_index_stats): its scal words
+  unsigned long long* last_scal = nullptr;
+  uint64_t last_chunks = 0;
   int last_op = 0;        // 1 decode, 2 encode
   void* host_pipe = nullptr;  // tgpu_host.cpp: streams + chunk buffers of the host path
   // transcode: decoded records and list arena between the two passes
@@ -855,6 +858,8 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   // (skipping the general-reader helper kernels when no tile needs them)
   uint64_t* h_sync = may_sync ? ctx->h_words : nullptr;
   if (h_sync) h_sync[3] = ~0ull;
+  ctx->last_scal = x.scal;
+  ctx->last_chunks = x.n_chunks;
   if (e == hipSuccess) e = launch_index_stream(x, s, jit, fused, h_sync);
   if (timing) (void)hipEventRecord(tev[1], s);
   struct TimingReport {
@@ -1127,6 +1132,10 @@ int tgpu_schema_compile_check(const tgpu_struct_desc* structs, uint32_t n_struct
   if (!structs || n_structs == 0 || (!fields && n_fields) ||
       !valid_protocol(protocol))
     return TGPU_ERR_INVALID_ARGUMENT;
+  // containers nested in containers (a type table, tgpu_schema_create_ex)
+  // never have a program: the general kernels read them, nothing to compile
+  for (uint32_t k = 0; k < n_fields; ++k)
+    if (fields[k].type_index) return TGPU_ERR_UNSUPPORTED;
   SchemaFacts facts;
   const int rc = validate(structs, n_structs, fields, n_fields, nullptr, 0, facts);
   if (rc) return rc;
@@ -1209,6 +1218,22 @@ int tgpu_context_wait(tgpu_context* ctx, void* stream, tgpu_status* st, uint64_t
   if (n_done) *n_done = r.n_records;
   if (bytes) *bytes = r.total_bytes;
   return code;
+}
+
+int tgpu_index_stats(tgpu_context* ctx, void* stream, uint64_t* out) {
+  if (!ctx || !out || !ctx->last_scal) return TGPU_ERR_INVALID_ARGUMENT;
+  uint64_t sc[11] = {};
+  hipError_t e = hipMemcpyAsync(sc, ctx->last_scal, sizeof(sc), hipMemcpyDeviceToHost,
+                                (hipStream_t)stream);
+  if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+  if (e != hipSuccess) return TGPU_ERR_HIP;
+  out[TGPU_ISTAT_CHUNKS] = ctx->last_chunks;
+  out[TGPU_ISTAT_PARTIAL] = sc[8];
+  out[TGPU_ISTAT_NO_START] = sc[9];
+  out[TGPU_ISTAT_BROKEN] = sc[10];
+  out[TGPU_ISTAT_REPAIRED] = sc[0];
+  out[TGPU_ISTAT_REWALKED] = sc[6];
+  return TGPU_OK;
 }
 
 int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol,

@@ -113,6 +113,20 @@ class GpuSchema:
         canonical program or the compiler is unavailable (interpreted)."""
         return _lib.lib().tgpu_schema_compile(self.handle, protocol) == 0
 
+    INDEX_STATS = ("chunks", "partial", "no_start", "broken", "repaired", "rewalked")
+
+    def index_stats(self, stream=None):
+        """Repair counters of this context's last stream index
+        (tgpu_index_stats): a dict over INDEX_STATS."""
+        import numpy as np
+
+        out = np.zeros(len(self.INDEX_STATS), np.uint64)
+        rc = _lib.lib().tgpu_index_stats(self.handle, _stream(stream),
+                                         ctypes.c_void_p(out.ctypes.data))
+        if rc:
+            raise TgpuError("tgpu_index_stats: %d" % rc)
+        return dict(zip(self.INDEX_STATS, (int(v) for v in out)))
+
     def __del__(self):
         h = getattr(self, "handle", None)
         if h is not None and _lib._lib is not None:
@@ -318,6 +332,8 @@ class BatchSerializer:
         if max_records is None:
             # a record can be one byte (STOP), so end - begin bounds the count;
             # sizing records for that is up to 8 x S per byte: count first
+            # (an extra index pass: hot callers pass max_records, as
+            # bench.py's config 5 does)
             max_records = self._count_records(gschema, wire, begin, end, speculative, limits,
                                               stream)
         if offsets is None:
@@ -433,8 +449,18 @@ class BatchSerializer:
 
         end = wire.numel() if end is None else end
         if max_records is None:
-            max_records = self._count_records(gschema, wire, begin, end, speculative, limits,
-                                              stream)
+            # sized by a first index into a guessed buffer; when the guess
+            # holds every record that index is the result (no second pass)
+            span = max(end - begin, 0)
+            guess = min(span, max(1024, span // 16))
+            r = self.index_stream(gschema, wire, begin, end, speculative, max_records=guess,
+                                  limits=limits, stream=stream, check=False)
+            if r[1] <= guess and r[4].code != 21:  # TGPU_ERR_OUTPUT_OVERFLOW
+                if check:
+                    raise_for_status(r[4])
+                return r
+            max_records = r[1]
+            offsets = None
         if offsets is None:
             offsets = torch.empty(max_records + 1, dtype=torch.int64, device=wire.device)
         lim = None

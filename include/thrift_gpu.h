@@ -327,7 +327,9 @@ int tgpu_schema_compile(const tgpu_schema* schema, int protocol);
 /* Diagnostics: generates and compiles the kernels of the schema given by the
  * tables (as for tgpu_schema_create) for `arch` (e.g. "gfx950"; NULL =
  * gfx950) without loading them — needs no GPU. The compiler log goes to
- * log[0..log_capacity) (may be NULL). */
+ * log[0..log_capacity) (may be NULL). TGPU_ERR_UNSUPPORTED as for
+ * tgpu_schema_compile, including every schema whose fields reference a
+ * nested container type (type_index != 0: no program, general kernels). */
 int tgpu_schema_compile_check(const tgpu_struct_desc* structs, uint32_t n_structs,
                               const tgpu_field_desc* fields, uint32_t n_fields, int protocol,
                               const char* arch, char* log, uint64_t log_capacity);
@@ -341,6 +343,24 @@ int tgpu_context_reserve(tgpu_context* ctx, uint64_t n_records);
 /* Waits for `stream` and reports the last call's result on this context. */
 int tgpu_context_wait(tgpu_context* ctx, void* stream, tgpu_status* st,
                       uint64_t* n_done, uint64_t* bytes);
+/*
+ * Repair counters of the last stream index on this context (the parallel
+ * form of the file loop, Serializer.h:97-100; tgpu_index_stream,
+ * tgpu_decode_stream, unindexed tgpu_decode_batch). Waits for `stream`.
+ * out[TGPU_ISTAT_*]: chunks (LDS tiles or lane chunks) of the call; tiles the
+ * speculation left partial, without a start, with a broken link to their
+ * predecessor; links the ordered repair lane visited; tiles whose stored
+ * record starts were re-walked. A canonical stream needs no repair: every
+ * counter but the first is 0 (a diagnostic: speed, not correctness, depends
+ * on it). Returns TGPU_ERR_INVALID_ARGUMENT when the context has run no
+ * index.
+ */
+enum {
+  TGPU_ISTAT_CHUNKS = 0, TGPU_ISTAT_PARTIAL = 1, TGPU_ISTAT_NO_START = 2,
+  TGPU_ISTAT_BROKEN = 3, TGPU_ISTAT_REPAIRED = 4, TGPU_ISTAT_REWALKED = 5,
+  TGPU_ISTAT_COUNT = 6
+};
+int tgpu_index_stats(tgpu_context* ctx, void* stream, uint64_t* out);
 
 /* ---- batch encode ----------------------------------------------------- */
 /*
