@@ -113,20 +113,6 @@ class GpuSchema:
         canonical program or the compiler is unavailable (interpreted)."""
         return _lib.lib().tgpu_schema_compile(self.handle, protocol) == 0
 
-    INDEX_STATS = ("chunks", "partial", "no_start", "broken", "repaired", "rewalked")
-
-    def index_stats(self, stream=None):
-        """Repair counters of this context's last stream index
-        (tgpu_index_stats): a dict over INDEX_STATS."""
-        import numpy as np
-
-        out = np.zeros(len(self.INDEX_STATS), np.uint64)
-        rc = _lib.lib().tgpu_index_stats(self.handle, _stream(stream),
-                                         ctypes.c_void_p(out.ctypes.data))
-        if rc:
-            raise TgpuError("tgpu_index_stats: %d" % rc)
-        return dict(zip(self.INDEX_STATS, (int(v) for v in out)))
-
     def __del__(self):
         h = getattr(self, "handle", None)
         if h is not None and _lib._lib is not None:
@@ -168,6 +154,20 @@ class Context:
         _lib.lib().tgpu_context_wait(self.handle, _stream(stream), ctypes.byref(st),
                                      ctypes.byref(n), ctypes.byref(b))
         return st, n.value, b.value
+
+    INDEX_STATS = ("chunks", "partial", "no_start", "broken", "repaired", "rewalked")
+
+    def index_stats(self, stream=None):
+        """Repair counters of this context's last stream index
+        (tgpu_index_stats): a dict over INDEX_STATS."""
+        import numpy as np
+
+        out = np.zeros(len(self.INDEX_STATS), np.uint64)
+        rc = _lib.lib().tgpu_index_stats(self.handle, _stream(stream),
+                                         ctypes.c_void_p(out.ctypes.data))
+        if rc:
+            raise TgpuError("tgpu_index_stats: %d" % rc)
+        return dict(zip(self.INDEX_STATS, (int(v) for v in out)))
 
     def __del__(self):
         h = getattr(self, "handle", None)
