@@ -275,8 +275,10 @@ class VarLen(Workload):
         self.stream = torch.cuda.current_stream()
         lib = ctypes.CDLL(os.path.join(ROOT, "tools", "build", "libtgpu_datagen.so"))
         self.recs = torch.empty(n * rs, dtype=torch.uint8, device=dev)
-        self.side = torch.empty(n * 64, dtype=torch.uint8, device=dev)  # string / list slots
-        gen = lib.tgpu_gen_mixed if self.schema == "mixed" else lib.tgpu_gen_nested
+        self.side = torch.empty(n * 64, dtype=torch.uint8, device=dev)  # string / list payloads
+        # payload bytes (strings / list elements) packed back to back in record
+        # order (tools/datagen.hip: the columnar layout a caller hands over)
+        gen = lib.tgpu_gen_mixed_packed if self.schema == "mixed" else lib.tgpu_gen_nested_packed
         if gen(ctypes.c_uint64(datagen.SEED), ctypes.c_uint64(rank * n), ctypes.c_uint64(n),
                ctypes.c_void_p(self.recs.data_ptr()), ctypes.c_void_p(self.side.data_ptr()),
                ctypes.c_void_p(self.stream.cuda_stream)):

@@ -737,7 +737,7 @@ constexpr uint32_t kTileLanes = 256;
 constexpr uint32_t kSub = 64;
 constexpr uint32_t kTile = kTileLanes * kSub;
 #ifndef TGPU_KOVER
-#define TGPU_KOVER 4096
+#define TGPU_KOVER 512
 #endif
 constexpr uint32_t kOver = TGPU_KOVER;
 constexpr uint32_t kTileLds = kTile + kOver + 32;
@@ -880,6 +880,52 @@ __device__ __forceinline__ void stage_tile(uint8_t* lds, const uint8_t* gb, uint
 #endif
 }
 
+// Candidate starts of the tile, one bit per byte (cmask; tile-relative
+// positions, 8 per byte), computed cooperatively: thread t owns 8-byte groups
+// t, t + 256, ... (consecutive threads read consecutive LDS words: no bank
+// conflicts, where one slice per lane read words 16 apart — 32-way
+// conflicts). A candidate is a byte equal to the program's first header byte
+// (h0) preceded by its STOP byte: every record ends with STOP, so every record
+// start but the range's first is preceded by it (a necessary condition: it
+// only prunes; for the mixed schema, whose four int headers all equal h0, it
+// removes ~3 of 4). The caller's barrier publishes cmask.
+template <class PP>
+__device__ __forceinline__ void cand_mask(const PP& P, const TileSrc& src, const uint8_t* lds,
+                                          uint64_t j, uint32_t sh, uint32_t thi, uint8_t* cmask) {
+  const VOp o0 = P.op(0);
+  const uint32_t h0 = o0.kind == VOP_CONST ? (o0.hdr & 0xff) : 0x100;
+  const VOp ol = P.op(P.n_ops() - 1);
+  const uint32_t stop =
+      (ol.kind == VOP_CONST && ol.hdr_len) ? ((ol.hdr >> (8 * (ol.hdr_len - 1))) & 0xff) : 0x100;
+  const uint32_t ngroups = (thi + 7) >> 3;
+  for (uint32_t g = threadIdx.x; g < ngroups; g += kTileLanes) {
+    const uint32_t base = g << 3;
+    uint64_t m = 0x8080808080808080ull;
+    // the group's 8 bytes (8-byte aligned: one LDS read) and the byte
+    // before them (one more), where staged; HBM windows past that
+    const bool in_lds = base + 8 <= src.lds_len;
+    const uint64_t w = in_lds ? *(const uint64_t*)(lds + base) : src.win8(base);
+    if (h0 < 0x100) {
+      const uint64_t x = w ^ (h0 * 0x0101010101010101ull);
+      m = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
+    }
+    if (stop < 0x100) {
+      // byte i of y = the byte before position base + i
+      const uint64_t prev = !base ? (w << 8)
+                            : in_lds ? (w << 8) | lds[base - 1]
+                                     : src.win8(base - 1);
+      const uint64_t y = prev ^ (stop * 0x0101010101010101ull);
+      uint64_t z = (y - 0x0101010101010101ull) & ~y & 0x8080808080808080ull;
+      if (!base) z |= 0x80ull;  // position 0: predecessor not staged
+      // the range's first byte has no predecessor inside the range
+      if (j == 0 && sh >= base && sh < base + 8) z |= 0x80ull << (8 * (sh - base));
+      m &= z;
+    }
+    cmask[g] = (uint8_t)((((m >> 7) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
+  }
+  for (uint32_t g = ngroups + threadIdx.x; g < ngroups + 9; g += kTileLanes) cmask[g] = 0;
+}
+
 // chain of canonical records from x while position < hi (tile-relative)
 template <class PP>
 __device__ __forceinline__ void tile_chain(const PP& P, const TileSrc& src, const Ctx& pc,
@@ -927,49 +973,9 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
   const uint32_t k = threadIdx.x;
   const uint32_t sub_lo = sh + k * kSub;
   const uint32_t sub_hi = sub_lo + kSub < thi ? sub_lo + kSub : thi;
-  // candidate starts of the whole tile, one bit per byte, computed
-  // cooperatively: thread t owns 8-byte groups t, t + 256, ... (consecutive
-  // threads read consecutive LDS words: no bank conflicts, where one slice
-  // per lane read words 16 apart — 32-way conflicts). A candidate is a byte
-  // equal to the program's first header byte (h0) preceded by its STOP byte:
-  // every record ends with STOP, so every record start but the range's first
-  // is preceded by it (a necessary condition: it only prunes; for the mixed
-  // schema, whose four int headers all equal h0, it removes ~3 of 4).
-  {
-    const VOp o0 = P.op(0);
-    const uint32_t h0 = o0.kind == VOP_CONST ? (o0.hdr & 0xff) : 0x100;
-    const VOp ol = P.op(P.n_ops() - 1);
-    const uint32_t stop =
-        (ol.kind == VOP_CONST && ol.hdr_len) ? ((ol.hdr >> (8 * (ol.hdr_len - 1))) & 0xff) : 0x100;
-    const uint32_t ngroups = (thi + 7) >> 3;
-    for (uint32_t g = threadIdx.x; g < ngroups; g += kTileLanes) {
-      const uint32_t base = g << 3;
-      uint64_t m = 0x8080808080808080ull;
-      // the group's 8 bytes (8-byte aligned: one LDS read) and the byte
-      // before them (one more), where staged; HBM windows past that
-      const bool in_lds = base + 8 <= src.lds_len;
-      const uint64_t w = in_lds ? *(const uint64_t*)(lds + base) : src.win8(base);
-      if (h0 < 0x100) {
-        const uint64_t x = w ^ (h0 * 0x0101010101010101ull);
-        m = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
-      }
-      if (stop < 0x100) {
-        // byte i of y = the byte before position base + i
-        const uint64_t prev = !base ? (w << 8)
-                              : in_lds ? (w << 8) | lds[base - 1]
-                                       : src.win8(base - 1);
-        const uint64_t y = prev ^ (stop * 0x0101010101010101ull);
-        uint64_t z = (y - 0x0101010101010101ull) & ~y & 0x8080808080808080ull;
-        if (!base) z |= 0x80ull;  // position 0: predecessor not staged
-        // the range's first byte has no predecessor inside the range
-        if (j == 0 && sh >= base && sh < base + 8) z |= 0x80ull << (8 * (sh - base));
-        m &= z;
-      }
-      cmask[g] = (uint8_t)((((m >> 7) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
-    }
-    for (uint32_t g = ngroups + threadIdx.x; g < ngroups + 9; g += kTileLanes) cmask[g] = 0;
-    if (threadIdx.x == 0) *first_lane = ~0u;  // (the first-start minimum below)
-  }
+  // candidate starts of the whole tile (see cand_mask)
+  cand_mask(P, src, lds, j, sh, thi, cmask);
+  if (threadIdx.x == 0) *first_lane = ~0u;  // (the first-start minimum below)
   __syncthreads();
   L.s = kNoPos;
   L.e = kNoPos;
@@ -1062,14 +1068,186 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
   return !__syncthreads_or(L.stuck || L.e == kNoPos);
 }
 
+// The candidate-list speculation (spec_tile_cands): at most kCandCap
+// candidates per tile (more, and the tile takes the slice speculation).
+#ifndef TGPU_CAND_CAP
+#define TGPU_CAND_CAP 768
+#endif
+constexpr uint32_t kCandCap = TGPU_CAND_CAP;
+constexpr uint32_t kCandWords = kTile / 64 + 2;  // 64-position words of cmask
+struct CandLists {
+  uint16_t cand[kCandCap + 2];  // candidate positions in order (+ a sentinel)
+  uint16_t len[kCandCap];       // record length walked from each (0: not a record)
+  uint16_t wbase[kCandWords];   // index of the first candidate of each cmask word
+};
+
 struct IndexTileShared {
   alignas(8) uint8_t cmask[kTile / 8 + 16];  // candidate bits of the tile (one per byte)
-  uint32_t E[kTileLanes];
+  union {
+    uint32_t E[kTileLanes];  // slice speculation: the lanes' chain ends
+    CandLists cl;            // candidate-list speculation
+  };
   int flag;
   uint32_t first_lane, fs;
   unsigned long long csum;
   unsigned long long part[4];
 };
+
+// Tile speculation over the list of candidate starts (the common case; the
+// slice speculation of tile_resolve is the fallback for tiles with more than
+// kCandCap candidates). Every candidate is walked once, by its own lane
+// (record i of the list on lane i mod 256: balanced, where a lane owning a
+// 64-byte slice walked all its records in turn and the wave waited for the
+// lane with the most); the walk gives each candidate's record length. The
+// tile's first start is the first candidate that is a canonical record (as
+// in the slice speculation), and its chain follows the lengths: a record
+// whose end is the next candidate links to it, which wave 0 checks 64
+// candidates per step (one ballot), hopping over the rare false candidates
+// (a STOP byte followed by h0 inside a record) by the rank of the end in
+// the candidate bits. The chain's starts are stored (u16, st16) as it goes.
+// Writes the tile's (s, e, cnt, pf) like index_spec_tile; returns false,
+// with nothing written, when the tile has too many candidates.
+template <class PP>
+__device__ __forceinline__ bool spec_tile_cands(const IndexArgs& a, const PP& P, uint64_t j,
+                                                uint8_t* lds, uint32_t ent,
+                                                IndexTileShared& sm) {
+  const uint64_t lo = chunk_lo(a, j);
+  const uint64_t hi_abs = chunk_hi(a, j);
+  const uint8_t* g = a.in + lo;
+  const uint32_t sh = (uint32_t)((uintptr_t)g & 15);
+  const uint8_t* gb = g - sh;
+  const uint64_t avail64 = a.in_len - lo + sh;
+  const uint32_t avail = (uint32_t)(avail64 < kPosCap ? avail64 : kPosCap);
+  const uint32_t staged = avail < kTile + kOver + 16 ? avail : kTile + kOver + 16;
+  stage_tile(lds, gb, (staged + 15) >> 4);
+  __syncthreads();
+  const TileSrc src{(const uint32_t*)lds, staged & ~3u, HbmSrc{gb, avail}};
+  const Ctx pc{0, nullptr, 0, a.string_limit, a.container_limit};
+  const uint32_t thi = sh + (uint32_t)(hi_abs - lo);  // tile end (relative)
+  cand_mask(P, src, lds, j, sh, thi, sm.cmask);
+  if (threadIdx.x == 0) sm.first_lane = ~0u;
+  __syncthreads();
+  // candidates per cmask word (positions [64 w, 64 w + 64) inside [sh, thi)):
+  // thread t owns word t and, for the last thread, the words past 256
+  const uint64_t* cw = (const uint64_t*)sm.cmask;
+  const uint32_t t = threadIdx.x;
+  const uint32_t nw = (thi + 63) >> 6;
+  auto word = [&](uint32_t w) -> uint64_t {
+    if (w >= nw) return 0;
+    uint64_t m = cw[w];
+    const uint32_t b0 = w << 6;
+    if (sh > b0) m &= sh - b0 >= 64 ? 0 : ~0ull << (sh - b0);      // before the tile
+    if (thi < b0 + 64) m &= thi <= b0 ? 0 : (1ull << (thi - b0)) - 1;  // past its end
+    return m;
+  };
+  const uint64_t m0 = word(t);
+  uint64_t mx = 0;
+  if (t == kTileLanes - 1)
+    for (uint32_t w = kTileLanes; w < nw; ++w) mx |= (uint64_t)__builtin_popcountll(word(w)) << (8 * (w - kTileLanes));
+  const uint32_t c0 = (uint32_t)__builtin_popcountll(m0);
+  uint32_t cx = 0;
+  for (uint32_t k = 0; k < kCandWords - kTileLanes; ++k) cx += (uint32_t)((mx >> (8 * k)) & 0xff);
+  unsigned long long total;
+  const uint32_t pre = (uint32_t)block_exscan256(c0 + cx, sm.part, &total);
+  const uint32_t N = (uint32_t)total;
+  if (N > kCandCap || N > a.st_cap) return false;  // (uniform)
+  sm.cl.wbase[t] = (uint16_t)pre;
+  {
+    uint32_t k = pre;
+    for (uint64_t m = m0; m; m &= m - 1) sm.cl.cand[k++] = (uint16_t)((t << 6) + __builtin_ctzll(m));
+    for (uint32_t w = kTileLanes; w < nw && t == kTileLanes - 1; ++w) {
+      sm.cl.wbase[w] = (uint16_t)k;
+      for (uint64_t m = word(w); m; m &= m - 1)
+        sm.cl.cand[k++] = (uint16_t)((w << 6) + __builtin_ctzll(m));
+    }
+    if (t == 0) sm.cl.cand[N] = sm.cl.cand[N + 1] = 0xffffu;  // sentinel: no position
+  }
+  __syncthreads();
+  // one walk per candidate
+  for (uint32_t i = t; i < N; i += kTileLanes) {
+    const uint32_t c = sm.cl.cand[i];
+    uint32_t q = c;
+    const bool ok = tile_walk(P, src, pc, q, avail);
+    const uint32_t len = q - c;
+    sm.cl.len[i] = ok ? (uint16_t)(len < 0xffffu ? len : 0xffffu) : 0;
+    if (ok) atomicMin(&sm.first_lane, i);
+  }
+  __syncthreads();
+  if (t >= 64) return true;  // wave 0 follows the chain and writes the tile's result
+  const uint32_t lane = t;
+  // the chain's first candidate: the range's first byte (tile 0 of a
+  // non-speculative call), else the first canonical record
+  uint32_t f;
+  bool stuck = false;
+  if (ent != kNoPos) {
+    const uint64_t m = cw[ent >> 6];
+    const uint64_t bit = 1ull << (ent & 63);
+    f = (m & bit) ? sm.cl.wbase[ent >> 6] + (uint32_t)__builtin_popcountll(m & (bit - 1)) : kNoPos;
+    stuck = f == kNoPos || sm.cl.len[f] == 0;
+  } else {
+    f = sm.first_lane;
+    if (f == ~0u) f = kNoPos;
+  }
+  const uint32_t first = f == kNoPos ? (ent != kNoPos ? ent : kNoPos) : sm.cl.cand[f];
+  uint32_t count = 0, e = 0;
+  uint16_t* dst = a.st16 + j * a.st_cap;
+  uint32_t i = f;
+  while (!stuck && f != kNoPos) {
+    // candidates [i, i + 64): lane l's record links to candidate i + l + 1
+    const uint32_t x = i + lane;
+    const bool in = x < N;
+    const uint32_t c = in ? sm.cl.cand[x] : 0xffffu;
+    const uint32_t len = in ? sm.cl.len[x] : 0u;
+    const uint32_t next = sm.cl.cand[in ? x + 1 : N];
+    const uint32_t q = c + len;
+    const bool link = in && len != 0 && len != 0xffffu && q < thi && q == next;
+    const uint64_t brk = __ballot(!link);
+    const uint32_t b = brk ? (uint32_t)__builtin_ctzll(brk) : 64u;
+    // lanes [0, b) are records linked to their successor; lane b's record
+    // ends the run (its successor is not the next candidate)
+    if (lane < b) dst[count + lane] = (uint16_t)c;
+    if (b == 64) {
+      count += 64;
+      i += 64;
+      continue;
+    }
+    const uint32_t cb = __shfl(c, b, 64), lb = __shfl(len, b, 64);
+    if (i + b >= N || lb == 0) {  // the run ends in a record the program cannot take
+      stuck = true;
+      break;
+    }
+    if (lane == b) dst[count + b] = (uint16_t)cb;
+    count += b + 1;
+    uint32_t qb = cb + lb;
+    if (lb == 0xffffu) {  // a record of 64 KiB or more: measure it again
+      qb = cb;
+      tile_walk(P, src, pc, qb, avail);
+    }
+    if (qb >= thi) {  // the record straddling the tile's end: done
+      e = qb;
+      break;
+    }
+    // the next record starts at qb: a candidate (every canonical record
+    // start after a STOP is one), whose index is its rank in the bits
+    const uint64_t m = cw[qb >> 6];
+    const uint64_t bit = 1ull << (qb & 63);
+    if (!(m & bit)) {
+      stuck = true;
+      break;
+    }
+    i = sm.cl.wbase[qb >> 6] + (uint32_t)__builtin_popcountll(m & (bit - 1));
+  }
+  if (lane == 0) {
+    const bool none = first == kNoPos;
+    const uint64_t st = lo - sh + first;
+    a.s[j] = none ? kNo : st;
+    // stuck: the general reader walks the whole tile from its (speculated) start
+    a.e[j] = none ? kNo : (stuck ? kPartial : lo - sh + e);
+    a.cnt[j] = none || stuck ? 0 : count;
+    if (!none) a.pf[j] = stuck ? st : kStartsValid;
+  }
+  return true;
+}
 
 template <class PP>
 __device__ __forceinline__ void index_spec_tile(const IndexArgs& a, const PP& P, uint8_t* lds,
@@ -1079,6 +1257,12 @@ __device__ __forceinline__ void index_spec_tile(const IndexArgs& a, const PP& P,
   // tile 0 of a non-speculative call starts at begin exactly (relative 0 + sh)
   const uint32_t ent = (j == 0 && !a.speculative) ? (uint32_t)((uintptr_t)(a.in + lo) & 15)
                                                   : kNoPos;
+#ifndef TGPU_SLICE_SPEC  // A/B: the slice speculation for every tile
+  if (a.st16) {
+    if (spec_tile_cands(a, P, j, lds, ent, sm)) return;
+    __syncthreads();  // (the slice speculation restages the tile)
+  }
+#endif
   TileLane L;
   uint32_t sh, first;
   const bool ok = tile_resolve(a, P, j, lds, ent, L, sh, first, sm.E, &sm.flag, &sm.first_lane,
@@ -1158,7 +1342,7 @@ __device__ __forceinline__ void index_emit_tile(const IndexArgs& a, const PP& P,
   TileLane L;
   uint32_t sh, first;
   bool ok;
-  if (a.pf[j] == kLanesValid || a.pf[j] == kStartsValid) {
+  if (a.pf[j] == kLanesValid) {
     // the speculation pass's lane results still hold: stage the tile only
     const uint8_t* g = a.in + lo;
     sh = sh0;

@@ -16,7 +16,7 @@ from fbthrift_amd.schema import Schema  # noqa: E402
 LIB = os.path.join(ROOT, "tools", "build", "libtgpu_datagen.so")
 
 
-def _gen(kind, first, n):
+def _gen(kind, first, n, packed=False):
     import torch
 
     schema = Schema.from_table(datagen.SCHEMAS[kind])
@@ -24,7 +24,7 @@ def _gen(kind, first, n):
     recs = torch.zeros(n * rs, dtype=torch.uint8, device="cuda")
     side = torch.zeros(n * 64, dtype=torch.uint8, device="cuda")
     lib = ctypes.CDLL(LIB)
-    fn = lib.tgpu_gen_mixed if kind == "mixed" else lib.tgpu_gen_nested
+    fn = getattr(lib, "tgpu_gen_%s%s" % (kind, "_packed" if packed else ""))
     assert fn(ctypes.c_uint64(datagen.SEED), ctypes.c_uint64(first), ctypes.c_uint64(n),
               ctypes.c_void_p(recs.data_ptr()), ctypes.c_void_p(side.data_ptr()), None) == 0
     torch.cuda.synchronize()
@@ -32,9 +32,10 @@ def _gen(kind, first, n):
 
 
 @pytest.mark.gpu
-def test_mixed_generator_matches_spec(gpu):
+@pytest.mark.parametrize("packed", [False, True])
+def test_mixed_generator_matches_spec(gpu, packed):
     first, n = 123456, 3000
-    _, r, side = _gen("mixed", first, n)
+    _, r, side = _gen("mixed", first, n, packed)
     for t in range(n):
         exp = datagen.gen_mixed(first + t)
         assert [int(r["f%d" % (k + 1)][t]) for k in range(4)] == exp[:4]
@@ -46,9 +47,10 @@ def test_mixed_generator_matches_spec(gpu):
 
 
 @pytest.mark.gpu
-def test_nested_generator_matches_spec(gpu):
+@pytest.mark.parametrize("packed", [False, True])
+def test_nested_generator_matches_spec(gpu, packed):
     first, n = 98765, 3000
-    _, r, side = _gen("nested", first, n)
+    _, r, side = _gen("nested", first, n, packed)
     elems = side.view(np.int32)
     for t in range(n):
         i64, lst, inner = datagen.gen_nested(first + t)
@@ -57,3 +59,16 @@ def test_nested_generator_matches_spec(gpu):
         assert list(elems[sp["offset"] // 4: sp["offset"] // 4 + sp["length"]]) == lst
         assert [float(r["f3"][t]["f%d" % (k + 1)]) for k in range(3)] == inner
         assert list(r["f3"][t]["__isset"]) == [1] * 3 and list(r["__isset"][t]) == [1] * 3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["mixed", "nested"])
+def test_packed_payloads_are_contiguous(gpu, kind):
+    """The packed generators leave no gaps: payload k starts where k-1 ends."""
+    _, r, side = _gen(kind, 7, 5000, True)
+    spans = ([r["f5"], r["f6"]] if kind == "mixed" else [r["f2"]])
+    off = np.stack([s["offset"] for s in spans], 1).reshape(-1).astype(np.int64)
+    ln = np.stack([s["length"] for s in spans], 1).reshape(-1).astype(np.int64)
+    if kind == "nested":
+        ln = ln * 4
+    assert off[0] == 0 and np.array_equal(off[1:], np.cumsum(ln)[:-1])
