@@ -145,7 +145,15 @@ hipError_t launch_program_encode(const EncodeArgs& a, const VProgram* d_prog,
   const uint32_t rt = prog::enc_record_region(a.rec_size);
   hipError_t e;
   if (jit) {
-    e = jit_launch_encode(jit, false, a, tiles, rt, stream);
+    // the compiled write pass sizes its own records (tile sums suffice)
+    EncodeArgs x = a;
+    x.recompute = size_only ? 0u : 1u;
+    e = jit_launch_encode(jit, false, x, tiles, rt, stream);
+    if (e == hipSuccess)
+      e = launch_scan_tiles(a.block_sums, tiles, part, &a.res->total_bytes, a.offs + a.n, stream);
+    if (e != hipSuccess || size_only) return e;
+    return jit_launch_encode(jit, true, x, tiles,
+                             (x.out_cap ? x.out_cap : kOutCap) + 32 + elem_stage_bytes(), stream);
   } else {
     hipLaunchKernelGGL(program_size_kernel, dim3((uint32_t)tiles), dim3(kET), rt, stream, a,
                        d_prog);
@@ -155,9 +163,6 @@ hipError_t launch_program_encode(const EncodeArgs& a, const VProgram* d_prog,
     e = launch_scan_tiles(a.block_sums, tiles, part, &a.res->total_bytes, a.offs + a.n, stream);
   if (e != hipSuccess || size_only) return e;
   const uint32_t lds = rt + kOutCap + 32;
-  // the compiled write kernel reads records from HBM: output tile (+ the
-  // list element stage, prog::kElemStage)
-  if (jit) return jit_launch_encode(jit, true, a, tiles, kOutCap + 32 + elem_stage_bytes(), stream);
   hipLaunchKernelGGL(program_write_kernel, dim3((uint32_t)tiles), dim3(kET), lds, stream, a,
                      d_prog);
   return hipGetLastError();

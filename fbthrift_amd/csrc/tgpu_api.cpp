@@ -2,6 +2,7 @@
 // validation/upload, the canonical Binary template, context workspaces and
 // the stream-ordered launch sequences of encode/decode.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -43,7 +44,37 @@ struct tgpu_schema {
   // their register footprint; used where a stream is known to carry them
   VProgram prog_tol[3]{};
   VProgram* d_prog_tol[3] = {nullptr, nullptr, nullptr};
+  // the wire bytes per record (x16) of the last batch whose size this schema
+  // learned (blocking encode / size calls), by protocol id: sizes the
+  // compiled write pass's LDS output tile (enc_out_cap)
+  std::atomic<uint64_t> mean16[3] = {0, 0, 0};
 };
+
+namespace {
+int proto_slot(int protocol) { return protocol == TGPU_PROTOCOL_BINARY ? 0 : protocol == TGPU_PROTOCOL_COMPACT ? 1 : 2; }
+
+void learn_mean(const tgpu_schema* s, int protocol, uint64_t bytes, uint64_t n) {
+  if (n >= 256 && bytes) const_cast<tgpu_schema*>(s)->mean16[proto_slot(protocol)] = bytes * 16 / n;
+}
+
+// LDS output tile of the compiled write pass: 256 records of the schema's
+// mean size with 25 % slack (records past it go to HBM directly), between
+// 4 and 24 KiB (a smaller tile lets more workgroups share a CU: the write
+// pass waits on memory most of the time). 0 = the kernel's default (24 KiB)
+// until a size is known. TGPU_ENC_OUTCAP=<bytes> overrides (A/B).
+uint32_t enc_out_cap(const tgpu_schema* s, int protocol) {
+  static const uint32_t force = [] {
+    const char* v = getenv("TGPU_ENC_OUTCAP");
+    return v ? (uint32_t)strtoul(v, nullptr, 10) : 0u;
+  }();
+  if (force) return std::min<uint32_t>(std::max<uint32_t>(force, 4096), 24 * 1024) & ~15u;
+  const uint64_t m16 = s->mean16[proto_slot(protocol)];
+  if (!m16) return 0;
+  const uint64_t want = (m16 * 256 / 16) * 5 / 4 + 64;
+  const uint64_t cap = (want + 1023) & ~1023ull;
+  return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(cap, 4096), 24 * 1024);
+}
+}  // namespace
 
 struct tgpu_context {
   int device = 0;
@@ -1290,6 +1321,7 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
     a.offs = out_offsets ? out_offsets : ctx->d_offs;
     a.block_sums = ctx->d_block_sums;
     a.scan_part = ctx->d_scan_part;
+    a.out_cap = enc_out_cap(schema, protocol);
     if (e == hipSuccess && n) {
       if (has_prog(schema, protocol) && program_encode_fits(rs))
         e = launch_program_encode(a, schema->d_prog[prog_protocol(schema, protocol)], ctx->d_scan_part, false, s,
@@ -1310,6 +1342,7 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
     uint64_t bytes = 0;
     const int rc = tgpu_context_wait(ctx, stream, st ? st : &tmp, nullptr, &bytes);
     if (out_size) *out_size = bytes;
+    if (rc == TGPU_OK) learn_mean(schema, protocol, bytes, n);
     return rc;
   }
   return TGPU_OK;
@@ -1365,7 +1398,11 @@ int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   }
   if (st || total) {
     tgpu_status tmp;
-    return tgpu_context_wait(ctx, stream, st ? st : &tmp, nullptr, total);
+    uint64_t bytes = 0;
+    const int rc = tgpu_context_wait(ctx, stream, st ? st : &tmp, nullptr, &bytes);
+    if (total) *total = bytes;
+    if (rc == TGPU_OK) learn_mean(schema, protocol, bytes, n);
+    return rc;
   }
   return TGPU_OK;
 }

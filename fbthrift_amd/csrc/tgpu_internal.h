@@ -259,6 +259,8 @@ struct EncodeArgs {
   uint32_t rec_size;
   DevResult* res;
   uint64_t fixed_len;  // program write of a fixed-layout schema: record i at i * fixed_len
+  uint32_t recompute;  // compiled write pass sizes its records; the size pass writes tile sums only
+  uint32_t out_cap;    // write pass: LDS output tile bytes (0: prog::kOutCap)
 };
 
 // ---- stream indexer (k_index.hip) -------------------------------------------

@@ -199,6 +199,60 @@ __device__ __forceinline__ uint64_t zz_member(uint64_t raw, uint32_t width, uint
   return i64_to_zz(v);
 }
 
+// A record's members as the encoder reads them: PtrRec through a pointer
+// (HBM or the LDS record tile), RegRec from registers — the record loaded
+// once at the start of the write pass (8-byte loads), every member access a
+// constant register select in the compiled programs (their offsets fold).
+struct PtrRec {
+  const uint8_t* p;
+  __device__ __forceinline__ uint32_t u8(uint32_t off) const { return p[off]; }
+  __device__ __forceinline__ uint64_t member(uint32_t off, uint32_t width) const {
+    return load_member(p + off, width);
+  }
+  __device__ __forceinline__ tgpu_span span(uint32_t off) const {
+    return *(const tgpu_span*)(p + off);
+  }
+};
+template <uint32_t S>
+struct RegRec {
+  static constexpr uint32_t kW = (S + 7) / 8 * 2;
+  uint32_t w[kW];
+  __device__ __forceinline__ void load(const uint8_t* p) {
+    // records are at least 8-byte aligned when S % 8 == 0 (i64/double/span
+    // members); otherwise 4-byte loads
+    if constexpr (S % 8 == 0) {
+#pragma unroll
+      for (uint32_t i = 0; i < S / 8; ++i) {
+        const uint2 v = ((const uint2*)p)[i];
+        w[2 * i] = v.x;
+        w[2 * i + 1] = v.y;
+      }
+    } else {
+#pragma unroll
+      for (uint32_t i = 0; i < kW; ++i) w[i] = i * 4 < S ? ((const uint32_t*)p)[i] : 0u;
+    }
+  }
+  __device__ __forceinline__ uint32_t u8(uint32_t off) const {
+    return (w[off >> 2] >> (8 * (off & 3))) & 0xffu;
+  }
+  __device__ __forceinline__ uint64_t member(uint32_t off, uint32_t width) const {
+    // members at natural alignment
+    switch (width) {
+      case 8: return ((uint64_t)w[(off >> 2) + 1] << 32) | w[off >> 2];
+      case 4: return w[off >> 2];
+      case 2: return (w[off >> 2] >> (8 * (off & 3))) & 0xffffu;
+      default: return u8(off);
+    }
+  }
+  __device__ __forceinline__ tgpu_span span(uint32_t off) const {
+    tgpu_span sp;
+    sp.offset = ((uint64_t)w[(off >> 2) + 1] << 32) | w[off >> 2];
+    sp.length = w[(off >> 2) + 2];
+    sp.reserved = 0;
+    return sp;
+  }
+};
+
 // list elements of `width` bytes from HBM, kElemBatch loads in flight
 #ifndef TGPU_ELEM_BATCH
 #define TGPU_ELEM_BATCH 8
@@ -233,8 +287,8 @@ __device__ __forceinline__ void for_elems(const uint8_t* __restrict__ e, uint32_
 // emits it (emission would copy `length` bytes) and reports the record.
 constexpr uint64_t kNeverFits = 1ull << 44;
 
-template <class PP>
-__device__ __forceinline__ uint64_t program_size(const PP& P, const uint8_t* rec,
+template <class PP, class R>
+__device__ __forceinline__ uint64_t program_size(const PP& P, const R& rec,
                                                  const uint8_t* __restrict__ lbase, bool& ok) {
   const bool compact = P.protocol() == TGPU_PROTOCOL_COMPACT;
   uint64_t n = 0;
@@ -244,18 +298,18 @@ __device__ __forceinline__ uint64_t program_size(const PP& P, const uint8_t* rec
         n += op.hdr_len;
         break;
       case VOP_CBOOL:
-        if (rec[op.member] > 1) ok = false;
+        if (rec.u8(op.member) > 1) ok = false;
         n += op.hdr_len;
         break;
       case VOP_FIXED:
-        if (op.is_bool && rec[op.member] > 1) ok = false;
+        if (op.is_bool && rec.u8(op.member) > 1) ok = false;
         n += op.width;
         break;
       case VOP_VARINT:
-        n += varint_len(zz_member(load_member(rec + op.member, op.width), op.width, op.bits));
+        n += varint_len(zz_member(rec.member(op.member, op.width), op.width, op.bits));
         break;
       case VOP_STRING: {
-        const uint32_t len = ((const tgpu_span*)(rec + op.member))->length;
+        const uint32_t len = rec.span(op.member).length;
         if (len > 0x7fffffffu) {  // checkBinarySize: never emitted (see kNeverFits)
           ok = false;
           n += kNeverFits;
@@ -265,7 +319,7 @@ __device__ __forceinline__ uint64_t program_size(const PP& P, const uint8_t* rec
         break;
       }
       case VOP_LIST: {
-        const tgpu_span sp = *(const tgpu_span*)(rec + op.member);
+        const tgpu_span sp = rec.span(op.member);
         const uint32_t len = sp.length;
         if (len > 0x7fffffffu) {
           ok = false;
@@ -431,24 +485,39 @@ __device__ __forceinline__ void put_bytes(Sink& s, const uint8_t* __restrict__ s
 #ifndef TGPU_STR_PREFETCH
 #define TGPU_STR_PREFETCH 0
 #endif
-template <class PP, class Sink>
-__device__ __forceinline__ void program_emit(const PP& P, const uint8_t* rec,
-                                             const uint8_t* __restrict__ sbase,
-                                             const uint8_t* __restrict__ lbase, Sink& s) {
-  const bool compact = P.protocol() == TGPU_PROTOCOL_COMPACT;
-  constexpr uint32_t kPf = PP::kStatic ? TGPU_STR_PREFETCH : 0;
-  StrPrefetch pf[kPf > 0 ? kPf : 1];
-  uint32_t npf = 0, ipf = 0;
-  if constexpr (kPf > 0) {
+// The first batch (8 dwords) of every string op's payload, up to kN strings,
+// loaded ahead of the emission (the compiled write pass issues them before
+// its block scan, so their latency overlaps the scan).
+template <uint32_t kN>
+struct StrAhead {
+  StrPrefetch f[kN > 0 ? kN : 1];
+  uint32_t n = 0;
+};
+template <uint32_t kN, class PP, class R>
+__device__ __forceinline__ void str_ahead(const PP& P, const R& rec,
+                                          const uint8_t* __restrict__ sbase, StrAhead<kN>& ah) {
+  if constexpr (kN > 0) {
     all_ops(P, [&](const VOp op) {
-      if (op.kind == VOP_STRING && npf < kPf) {
-        const tgpu_span sp = *(const tgpu_span*)(rec + op.member);
-        str_prefetch(pf[npf], sbase + sp.offset, sp.length);
-        ++npf;
+      if (op.kind == VOP_STRING && ah.n < kN) {
+        const tgpu_span sp = rec.span(op.member);
+        str_prefetch(ah.f[ah.n], sbase + sp.offset, sp.length);
+        ++ah.n;
       }
       return true;
     });
   }
+}
+
+template <class PP, class Sink, class R, uint32_t kA = 0>
+__device__ __forceinline__ void program_emit(const PP& P, const R& rec,
+                                             const uint8_t* __restrict__ sbase,
+                                             const uint8_t* __restrict__ lbase, Sink& s,
+                                             const StrAhead<kA>* ahead = nullptr) {
+  const bool compact = P.protocol() == TGPU_PROTOCOL_COMPACT;
+  constexpr uint32_t kPf = PP::kStatic && kA == 0 ? TGPU_STR_PREFETCH : 0;
+  StrAhead<kPf> own;
+  str_ahead(P, rec, sbase, own);
+  uint32_t ipf = 0;
   all_ops(P, [&](const VOp op) {
     switch (op.kind) {
       case VOP_CONST:
@@ -456,25 +525,37 @@ __device__ __forceinline__ void program_emit(const PP& P, const uint8_t* rec,
         break;
       case VOP_CBOOL:
         // the bool's value rides in the header's type nibble (CT_BOOLEAN_TRUE/FALSE)
-        put8(s, op.hdr | (rec[op.member] ? 1u : 2u), op.hdr_len);
+        put8(s, op.hdr | (rec.u8(op.member) ? 1u : 2u), op.hdr_len);
         break;
       case VOP_FIXED:
-        put_be(s, load_member(rec + op.member, op.width), op.width);
+        put_be(s, rec.member(op.member, op.width), op.width);
         break;
       case VOP_VARINT:
-        put_varint(s, zz_member(load_member(rec + op.member, op.width), op.width, op.bits));
+        put_varint(s, zz_member(rec.member(op.member, op.width), op.width, op.bits));
         break;
       case VOP_STRING: {
-        const tgpu_span sp = *(const tgpu_span*)(rec + op.member);
+        const tgpu_span sp = rec.span(op.member);
         if (compact) put_varint(s, sp.length);
         else put_be(s, sp.length, 4);
-        const StrPrefetch* f = ipf < npf ? &pf[ipf] : nullptr;
-        ++ipf;
-        put_bytes(s, sbase + sp.offset, sp.length, f);
+        // (no pointer chosen at run time between a prefetched batch and
+        // none: that kept the batches in scratch)
+        const uint32_t k = ipf++;
+        if constexpr (kA > 0) {
+          if (k < kA) {
+            put_bytes(s, sbase + sp.offset, sp.length, &ahead->f[k < kA ? k : 0]);
+            break;
+          }
+        } else if constexpr (kPf > 0) {
+          if (k < kPf) {
+            put_bytes(s, sbase + sp.offset, sp.length, &own.f[k < kPf ? k : 0]);
+            break;
+          }
+        }
+        put_bytes(s, sbase + sp.offset, sp.length);
         break;
       }
       case VOP_LIST: {
-        const tgpu_span sp = *(const tgpu_span*)(rec + op.member);
+        const tgpu_span sp = rec.span(op.member);
         const uint32_t len = sp.length;
         if (compact) {
           if (len <= 14) {
@@ -520,7 +601,7 @@ __device__ TGPU_HBM_EMIT_ATTR void emit_to_hbm(const PP P, const uint8_t* rec,
                                                       const uint8_t* __restrict__ lbase,
                                                       uint8_t* dst) {
   ByteSink b(dst);
-  program_emit(P, rec, sbase, lbase, b);
+  program_emit(P, PtrRec{rec}, sbase, lbase, b);
 }
 
 // Records [r0, r0+nrec) of stride S into LDS; returns the 16-byte phase.
@@ -552,9 +633,10 @@ __device__ __forceinline__ void size_tile(const EncodeArgs& a, const PP& P, uint
   unsigned long long sz = 0;
   if (threadIdx.x < nrec) {
     bool ok = true;
-    sz = program_size(P, recs + sh + threadIdx.x * S, a.lbase, ok);
+    sz = program_size(P, PtrRec{recs + sh + threadIdx.x * S}, a.lbase, ok);
     if (!ok) atomicMin(&a.res->first_fail, (unsigned long long)(r0 + threadIdx.x));
-    a.offs[r0 + threadIdx.x] = sz;
+    // (a.recompute: the write pass sizes its records itself; tile sums only)
+    if (!a.recompute) a.offs[r0 + threadIdx.x] = sz;
   }
   unsigned long long total;
   (void)block_exscan256(sz, part, &total);
@@ -585,11 +667,24 @@ struct EncodeShared {
 #endif
 constexpr uint32_t kElemStage = TGPU_ELEM_STAGE;
 
-template <class PP>
+// Strings whose first 32 bytes the compiled write pass loads before its block
+// scan (A/B: TGPU_ENC_AHEAD=0 loads them during the emission)
+#ifndef TGPU_ENC_AHEAD
+#define TGPU_ENC_AHEAD 2
+#endif
+
+// SR (compiled programs: the record size as a constant): with a.recompute the
+// size pass left tile sums only, and this pass loads its record into
+// registers (RegRec), sizes it for the block scan and emits from the same
+// registers — the record is read once, and the string loads (issued right
+// after it, before the scan) overlap the scan's barriers, where the size
+// pass's per-record sizes cost a dependent HBM round trip first.
+template <class PP, uint32_t SR = 0>
 __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uint32_t S,
                                            uint8_t* smem, EncodeShared& sm) {
   const uint64_t r0 = (uint64_t)blockIdx.x * kET;
   const uint32_t nrec = (uint32_t)min((uint64_t)kET, a.n - r0);
+  const uint32_t ocap = a.out_cap ? a.out_cap : kOutCap;  // LDS output tile bytes
   // compiled programs read their record's members straight from HBM (the
   // unrolled loads issue together; no LDS record tile, so 6 instead of 4
   // workgroups fit a CU: config 3 encode -9 %, config 4 -21 %); the
@@ -607,6 +702,16 @@ __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uin
     rsh = stage_records(a.recs, r0, nrec, S, rtile);
   }
   const uint32_t r = threadIdx.x;
+  // (one emission path per kernel: two instantiations of the unrolled
+  // emitter left the compiler's unroller short, and the register record then
+  // went to scratch)
+  constexpr bool kReg = PP::kStatic && SR > 0;
+  constexpr uint32_t kAhead = kReg ? TGPU_ENC_AHEAD : 0;
+  RegRec<kReg ? SR : 8> R;
+  StrAhead<kAhead> ah;
+  if constexpr (kReg) {
+    if (r < nrec) R.load(a.recs + (r0 + r) * S);
+  }
   if (kElemStage > 0 && r == 0) {
     sm.elo = ~0ull;
     sm.ehi = 0;
@@ -620,6 +725,17 @@ __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uin
     rel = (unsigned long long)r * a.fixed_len;
     tile_base = r0 * a.fixed_len;
     if (a.offs && r == 0 && r0 + nrec == a.n) a.offs[a.n] = a.n * a.fixed_len;
+  } else if (kReg) {
+    // (a.recompute, set for every compiled write: the size pass wrote tile
+    // sums only)
+    tile_base = a.block_sums[blockIdx.x];
+    sz = 0;
+    if (r < nrec) {
+      bool ok = true;  // (the size pass reported validation failures)
+      sz = program_size(P, R, a.lbase, ok);
+      str_ahead(P, R, a.sbase, ah);
+    }
+    rel = block_exscan256(sz, sm.part, &tile_total);
   } else {
     sz = r < nrec ? a.offs[r0 + r] : 0;
     rel = block_exscan256(sz, sm.part, &tile_total);
@@ -656,7 +772,7 @@ __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uin
         const uintptr_t g0 = ((uintptr_t)a.lbase + elo) & ~(uintptr_t)15;
         const uint32_t nvec = (uint32_t)(((uintptr_t)a.lbase + ehi - g0 + 15) >> 4);
         if (nvec * 16 <= kElemStage) {
-          uint8_t* stage = smem + kOutCap + 32;
+          uint8_t* stage = smem + ocap + 32;
           for (uint32_t i = threadIdx.x; i < nvec; i += kET)
             ((uint4*)stage)[i] = ((const uint4*)g0)[i];
           // a flat (generic) address into the LDS aperture, computed in 64-bit
@@ -670,10 +786,10 @@ __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uin
   {  // zero the part of the output tile the records will OR into
     const uint4 z = {0u, 0u, 0u, 0u};
     const uint32_t nz =
-        (osh + (uint32_t)min(tile_total, (unsigned long long)kOutCap) + 4 + 15) >> 4;
+        (osh + (uint32_t)min(tile_total, (unsigned long long)ocap) + 4 + 15) >> 4;
     for (uint32_t i = threadIdx.x; i < nz; i += kET) ((uint4*)otile)[i] = z;
   }
-  if (r == 0) sm.lds_end = (unsigned int)min(tile_total, (unsigned long long)kOutCap);
+  if (r == 0) sm.lds_end = (unsigned int)min(tile_total, (unsigned long long)ocap);
   __syncthreads();  // record tile staged, output tile zeroed, lds_end initialised
   bool fits = false;
   if (r < nrec) {
@@ -681,9 +797,9 @@ __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uin
     if (a.offs) a.offs[r0 + r] = start;
     if (start + sz > a.cap) {
       atomicMin(&a.res->first_fail, (unsigned long long)(r0 + r));
-      atomicMin(&sm.lds_end, (unsigned int)min(rel, (unsigned long long)kOutCap));
+      atomicMin(&sm.lds_end, (unsigned int)min(rel, (unsigned long long)ocap));
     } else {
-      fits = rel + sz <= kOutCap;
+      fits = rel + sz <= ocap;
       if (!fits) atomicMin(&sm.lds_end, (unsigned int)rel);
     }
   }
@@ -692,12 +808,16 @@ __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uin
     const uint8_t* rec = rtile + rsh + r * S;
     if (a.fixed_len) {  // the validation the size pass does otherwise (validate_bool)
       bool ok = true;
-      (void)program_size(P, rec, a.lbase, ok);
+      if constexpr (kReg) (void)program_size(P, R, a.lbase, ok);
+      else (void)program_size(P, PtrRec{rec}, a.lbase, ok);
       if (!ok) atomicMin(&a.res->first_fail, (unsigned long long)(r0 + r));
     }
     if (fits && rel + sz <= sm.lds_end) {
       OrSink w((uint32_t*)otile, osh + (uint32_t)rel);
-      program_emit(P, rec, a.sbase, lbase, w);
+      if constexpr (kReg)
+        program_emit<PP, OrSink, RegRec<kReg ? SR : 8>, kAhead>(P, R, a.sbase, lbase, w, &ah);
+      else
+        program_emit(P, PtrRec{rec}, a.sbase, lbase, w);
     } else if (tile_base + rel + sz <= a.cap) {
       emit_to_hbm(P, rec, a.sbase, a.lbase, gtile + rel);
     }
@@ -1237,6 +1357,29 @@ __device__ __forceinline__ bool spec_tile_cands(const IndexArgs& a, const PP& P,
     }
     i = sm.cl.wbase[qb >> 6] + (uint32_t)__builtin_popcountll(m & (bit - 1));
   }
+#ifdef TGPU_SPEC_CHECK  // diagnostics: a tile left partial, its staged bytes against HBM
+  if (stuck) {
+    uint32_t bad = 0, first_bad = ~0u;
+    const uint32_t nw4 = (staged & ~3u) >> 2;
+    for (uint32_t d = lane; d < nw4; d += 64) {
+      const uint32_t x = ((const uint32_t*)lds)[d];
+      const uint32_t y = __builtin_nontemporal_load((const uint32_t*)gb + d);
+      if (x != y) {
+        ++bad;
+        first_bad = min(first_bad, d);
+      }
+    }
+    for (int o = 32; o; o >>= 1) {
+      bad += __shfl_xor(bad, o, 64);
+      first_bad = min(first_bad, (uint32_t)__shfl_xor(first_bad, o, 64));
+    }
+    if (lane == 0) {
+      atomicAdd(&a.scal[13], 1ull);             // stuck tiles
+      if (bad) atomicAdd(&a.scal[14], 1ull);    // ... whose LDS copy differs from HBM
+      atomicAdd(&a.scal[15], (unsigned long long)bad);
+    }
+  }
+#endif
   if (lane == 0) {
     const bool none = first == kNoPos;
     const uint64_t st = lo - sh + first;

@@ -64,12 +64,22 @@ struct DynProg {
 };
 
 // f(op) for every op in order; stops at the first op for which f returns false.
+// Compiled programs expand the ops as a fold over a constant index sequence:
+// every op is a constant and every call its own straight-line copy. (A
+// `#pragma unroll` loop was left rolled by the compiler for large bodies —
+// the write pass's emitter read the op table at run time.)
+template <class T, T... K>
+struct OpSeq {};
+template <class PP, class F, uint32_t... K>
+__device__ __forceinline__ bool all_ops_seq(const PP& P, F& f, OpSeq<uint32_t, K...>) {
+  bool go = true;
+  ((go = go && f(P.op(K))), ...);
+  return go;
+}
 template <class PP, class F>
 __device__ __forceinline__ bool all_ops(const PP& P, F&& f) {
   if constexpr (PP::kStatic) {
-#pragma unroll
-    for (uint32_t k = 0; k < PP::kN; ++k)
-      if (!f(P.op(k))) return false;
+    return all_ops_seq(P, f, __make_integer_seq<OpSeq, uint32_t, PP::kN>{});
   } else {
     const uint32_t n = P.n_ops();
     for (uint32_t k = 0; k < n; ++k)

@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--records", type=int, default=1 << 26)
     ap.add_argument("--variants", nargs="*", default=["1", "0"])
     ap.add_argument("--reps", type=int, default=8)
+    ap.add_argument("--stats", action="store_true",
+                    help="print each call's time and index repair counters (tgpu_index_stats)")
     ap.add_argument("--sync-before", action="store_true",
                     help="synchronize after the encode (decode starts on an idle GPU)")
     args = ap.parse_args()
@@ -51,6 +53,9 @@ def main():
                 wall.append((t1 - t0) * 1e3)
                 evt.append(e[1].elapsed_time(e[2]))
                 enc.append(e[0].elapsed_time(e[1]))
+            if args.stats:
+                print("  rep %d: decode events %.3f ms, index repairs %s" % (
+                    r, e[1].elapsed_time(e[2]), wl.S.context().index_stats()), flush=True)
         wl.check_timed()
         print("TGPU_INDEX_STARTS=%s decode wall %.3f ms  events %.3f ms  (encode events %.3f)"
               % (v, statistics.median(wall), statistics.median(evt), statistics.median(enc)))
