@@ -757,7 +757,7 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
   const dim3 sg((uint32_t)std::min<uint64_t>((C + 255) / 256, kScratchGrid));
   bool need_cont = true, need_fallback = true, need_merge = true;
   const bool tiles = a.prog && a.chunk == kTile;
-  if (pt.on) (void)hipMemsetAsync(a.scal + 13, 0, 3 * sizeof(unsigned long long), stream);
+  if (pt.on) (void)hipMemsetAsync(a.scal + 12, 0, 4 * sizeof(unsigned long long), stream);
   if (tiles) {
     if (jit) {
       const hipError_t e = jit_launch_index(jit, 0, a, C, stream);
@@ -772,11 +772,12 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
   }
   pt.mark("spec");
   if (pt.on && jit) {  // (TGPU_SPEC_CHECK builds: stuck tiles, of them with LDS != HBM, words)
-    uint64_t d[3] = {};
-    (void)hipMemcpyAsync(d, a.scal + 13, sizeof(d), hipMemcpyDeviceToHost, stream);
+    uint64_t d[4] = {};
+    (void)hipMemcpyAsync(d, a.scal + 12, sizeof(d), hipMemcpyDeviceToHost, stream);
     (void)hipStreamSynchronize(stream);
-    fprintf(stderr, "  spec check: stuck %llu, staged copy differs %llu, words %llu\n",
-            (unsigned long long)d[0], (unsigned long long)d[1], (unsigned long long)d[2]);
+    fprintf(stderr, "  spec check: threads whose staged words changed after the staging barrier %llu; stuck %llu, "
+            "staged copy differs at the end %llu, words %llu\n", (unsigned long long)d[0],
+            (unsigned long long)d[1], (unsigned long long)d[2], (unsigned long long)d[3]);
   }
   // what the speculation left to repair: read mid-call by blocking tile
   // calls (to skip the helpers nothing needs), kept for tgpu_index_stats

@@ -1241,6 +1241,19 @@ __device__ __forceinline__ bool spec_tile_cands(const IndexArgs& a, const PP& P,
   const uint32_t staged = avail < kTile + kOver + 16 ? avail : kTile + kOver + 16;
   stage_tile(lds, gb, (staged + 15) >> 4);
   __syncthreads();
+#ifdef TGPU_SPEC_EARLY  // diagnostics: the staged bytes right after the staging barrier
+  {
+    uint32_t bad = 0;
+    for (uint32_t d = threadIdx.x; d < ((staged & ~3u) >> 2); d += kTileLanes)
+      bad += ((const uint32_t*)lds)[d] != __builtin_nontemporal_load((const uint32_t*)gb + d);
+    if (bad) atomicAdd(&a.scal[12], (unsigned long long)bad);
+  }
+#endif
+#ifdef TGPU_SPEC_LATE  // diagnostics: does the staged tile change after the staging barrier?
+  uint32_t late0 = 0;
+  for (uint32_t d = threadIdx.x; d < ((staged & ~3u) >> 2); d += kTileLanes)
+    late0 ^= ((const volatile uint32_t*)lds)[d] * (d | 1);
+#endif
   const TileSrc src{(const uint32_t*)lds, staged & ~3u, HbmSrc{gb, avail}};
   const Ctx pc{0, nullptr, 0, a.string_limit, a.container_limit};
   const uint32_t thi = sh + (uint32_t)(hi_abs - lo);  // tile end (relative)
@@ -1293,14 +1306,29 @@ __device__ __forceinline__ bool spec_tile_cands(const IndexArgs& a, const PP& P,
     if (ok) atomicMin(&sm.first_lane, i);
   }
   __syncthreads();
+#ifdef TGPU_SPEC_LATE
+  {
+    uint32_t late1 = 0;
+    for (uint32_t d = threadIdx.x; d < ((staged & ~3u) >> 2); d += kTileLanes)
+      late1 ^= ((const volatile uint32_t*)lds)[d] * (d | 1);
+    if (late1 != late0) atomicAdd(&a.scal[12], 1ull);  // threads that saw their words change
+  }
+#endif
+#ifdef TGPU_SPEC_NOEXIT  // A/B: waves 1-3 wait for wave 0 at a final barrier
+  if (t >= 64) {
+    __syncthreads();
+    return true;
+  }
+#else
   if (t >= 64) return true;  // wave 0 follows the chain and writes the tile's result
+#endif
   const uint32_t lane = t;
   // the chain's first candidate: the range's first byte (tile 0 of a
   // non-speculative call), else the first canonical record
   uint32_t f;
   bool stuck = false;
   if (ent != kNoPos) {
-    const uint64_t m = cw[ent >> 6];
+    const uint64_t m = word(ent >> 6);  // (the counted bits: none before sh)
     const uint64_t bit = 1ull << (ent & 63);
     f = (m & bit) ? sm.cl.wbase[ent >> 6] + (uint32_t)__builtin_popcountll(m & (bit - 1)) : kNoPos;
     stuck = f == kNoPos || sm.cl.len[f] == 0;
@@ -1349,7 +1377,7 @@ __device__ __forceinline__ bool spec_tile_cands(const IndexArgs& a, const PP& P,
     }
     // the next record starts at qb: a candidate (every canonical record
     // start after a STOP is one), whose index is its rank in the bits
-    const uint64_t m = cw[qb >> 6];
+    const uint64_t m = word(qb >> 6);  // (the counted bits: none before sh)
     const uint64_t bit = 1ull << (qb & 63);
     if (!(m & bit)) {
       stuck = true;
@@ -1389,6 +1417,9 @@ __device__ __forceinline__ bool spec_tile_cands(const IndexArgs& a, const PP& P,
     a.cnt[j] = none || stuck ? 0 : count;
     if (!none) a.pf[j] = stuck ? st : kStartsValid;
   }
+#ifdef TGPU_SPEC_NOEXIT
+  __syncthreads();
+#endif
   return true;
 }
 

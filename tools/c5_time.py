@@ -54,8 +54,10 @@ def main():
                 evt.append(e[1].elapsed_time(e[2]))
                 enc.append(e[0].elapsed_time(e[1]))
             if args.stats:
-                print("  rep %d: decode events %.3f ms, index repairs %s" % (
-                    r, e[1].elapsed_time(e[2]), wl.S.context().index_stats()), flush=True)
+                w = wl.wire[: wl.wire_bytes // 4 * 4].view(torch.int32)
+                print("  rep %d: decode events %.3f ms, index repairs %s, wire sum %d" % (
+                    r, e[1].elapsed_time(e[2]), wl.S.context().index_stats(),
+                    int(w.sum(dtype=torch.int64))), flush=True)
         wl.check_timed()
         print("TGPU_INDEX_STARTS=%s decode wall %.3f ms  events %.3f ms  (encode events %.3f)"
               % (v, statistics.median(wall), statistics.median(evt), statistics.median(enc)))
