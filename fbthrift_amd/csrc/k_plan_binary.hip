@@ -121,6 +121,10 @@ __global__ __launch_bounds__(T) void plan_binary_decode_kernel(
             (__attribute__((address_space(3))) void*)(smem + (size_t)(k * T + wave * 64) * 16), 16,
             0, 0);
       }
+      // (lds_dma_settle, tgpu_program.h; TGPU_NO_DMA_SETTLE builds leave it out)
+#ifndef TGPU_NO_DMA_SETTLE
+      prog::lds_dma_settle(smem, threadIdx.x, T, (nvec + T - 1) / T);
+#endif
     } else {
       for (uint32_t i = threadIdx.x; i < nvec; i += T) ((uint4*)smem)[i] = src[i];
     }

@@ -1252,10 +1252,15 @@ int tgpu_context_wait(tgpu_context* ctx, void* stream, tgpu_status* st, uint64_t
 }
 
 int tgpu_index_stats(tgpu_context* ctx, void* stream, uint64_t* out) {
-  if (!ctx || !out || !ctx->last_scal) return TGPU_ERR_INVALID_ARGUMENT;
-  uint64_t sc[11] = {};
-  hipError_t e = hipMemcpyAsync(sc, ctx->last_scal, sizeof(sc), hipMemcpyDeviceToHost,
+  if (!ctx || !out) return TGPU_ERR_INVALID_ARGUMENT;
+  hipError_t e = hipMemcpyAsync(ctx->h_res, ctx->d_res, sizeof(DevResult), hipMemcpyDeviceToHost,
                                 (hipStream_t)stream);
+  if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+  if (e != hipSuccess) return TGPU_ERR_HIP;
+  out[TGPU_ISTAT_GENERAL] = ctx->h_res->n_irregular;
+  if (!ctx->last_scal) return TGPU_ERR_INVALID_ARGUMENT;
+  uint64_t sc[11] = {};
+  e = hipMemcpyAsync(sc, ctx->last_scal, sizeof(sc), hipMemcpyDeviceToHost, (hipStream_t)stream);
   if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
   if (e != hipSuccess) return TGPU_ERR_HIP;
   out[TGPU_ISTAT_CHUNKS] = ctx->last_chunks;

@@ -102,6 +102,9 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
           (__attribute__((address_space(3))) void*)(wire + (size_t)(k * kPT + wave * 64) * 16), 16,
           0, 0);
     }
+#ifndef TGPU_NO_DMA_SETTLE
+    lds_dma_settle(wire, threadIdx.x, kPT, (nvec + kPT - 1) / kPT);
+#endif
   }
   uint8_t* gout = a.recs + r0 * S;
   const uint32_t osh = (uint32_t)((uintptr_t)gout & 15);
@@ -997,6 +1000,12 @@ __device__ __forceinline__ void stage_tile(uint8_t* lds, const uint8_t* gb, uint
   }
   const uint32_t i = whole + threadIdx.x;
   if (i < nvec) ((uint4*)lds)[i] = ((const uint4*)gb)[i];
+#ifndef TGPU_NO_DMA_SETTLE  // A/B: (see lds_dma_settle)
+  {
+    const uint32_t w0 = wave * 64 + (threadIdx.x & 63);  // this lane's first DMA'd vector
+    lds_dma_settle(lds, w0, kTileLanes, w0 < whole ? (whole - 1 - w0) / kTileLanes + 1 : 0);
+  }
+#endif
 #endif
 }
 
@@ -1087,6 +1096,11 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
   const uint32_t nvec = (staged + 15) >> 4;
   stage_tile(lds, gb, nvec);
   __syncthreads();
+#ifdef TGPU_SPEC_LATE
+  uint32_t late0 = 0;
+  for (uint32_t d = threadIdx.x; d < ((staged & ~3u) >> 2); d += kTileLanes)
+    late0 ^= ((const volatile uint32_t*)lds)[d] * (d | 1);
+#endif
   const TileSrc src{(const uint32_t*)lds, staged & ~3u, HbmSrc{gb, avail}};
   const Ctx pc{0, nullptr, 0, a.string_limit, a.container_limit};
   const uint32_t thi = sh + (uint32_t)(hi_abs - lo);  // tile end (relative)
@@ -1185,6 +1199,14 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
     if (!__syncthreads_or(changed)) break;
   }
   (void)flag;
+#ifdef TGPU_SPEC_LATE
+  {
+    uint32_t late1 = 0;
+    for (uint32_t d = threadIdx.x; d < ((staged & ~3u) >> 2); d += kTileLanes)
+      late1 ^= ((const volatile uint32_t*)lds)[d] * (d | 1);
+    if (late1 != late0) atomicAdd(&a.scal[12], 1ull);
+  }
+#endif
   return !__syncthreads_or(L.stuck || L.e == kNoPos);
 }
 

@@ -52,6 +52,25 @@ __device__ __forceinline__ void note_exception(bool flag, uint64_t i, DevResult*
   }
 }
 
+// ---- LDS-DMA settle ------------------------------------------------------------
+// After a wave's global_load_lds writes, `s_waitcnt vmcnt(0)` + `s_barrier`
+// alone did not make them visible to the workgroup's other waves in the
+// stream index's tiles: measured (TGPU_SPEC_LATE), 900-4400 threads per
+// config-5 call saw their staged words change AFTER the staging barrier
+// (round 2's "broken chains", hidden by the repair passes), while a
+// standalone probe of the same staging never did (tools/glds_probe.hip).
+// Each lane reading back one word of every vector it DMA'd, after
+// vmcnt(0), made every such call clean (as did a 128-cycle pause, or
+// staging through registers, which costs 0.2 ms per call); the caller's
+// barrier then waits for these reads (lgkmcnt(0)). `first` = the lane's first
+// vector index, `step` = the vector stride between its DMAs, `n` = its DMAs.
+__device__ __forceinline__ void lds_dma_settle(const uint8_t* lds, uint32_t first, uint32_t step,
+                                               uint32_t n) {
+  __builtin_amdgcn_s_waitcnt(0);  // (vmcnt(0) expcnt(0) lgkmcnt(0))
+  for (uint32_t k = 0; k < n; ++k)
+    (void)((const volatile uint32_t*)lds)[(first + k * step) * 4];
+}
+
 // ---- program accessors --------------------------------------------------------
 struct DynProg {
   static constexpr bool kStatic = false;

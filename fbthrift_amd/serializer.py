@@ -155,7 +155,7 @@ class Context:
                                      ctypes.byref(n), ctypes.byref(b))
         return st, n.value, b.value
 
-    INDEX_STATS = ("chunks", "partial", "no_start", "broken", "repaired", "rewalked")
+    INDEX_STATS = ("chunks", "partial", "no_start", "broken", "repaired", "rewalked", "general")
 
     def index_stats(self, stream=None):
         """Repair counters of this context's last stream index
@@ -165,7 +165,7 @@ class Context:
         out = np.zeros(len(self.INDEX_STATS), np.uint64)
         rc = _lib.lib().tgpu_index_stats(self.handle, _stream(stream),
                                          ctypes.c_void_p(out.ctypes.data))
-        if rc:
+        if rc and rc != 23:  # (INVALID_ARGUMENT: no index yet; "general" is still filled)
             raise TgpuError("tgpu_index_stats: %d" % rc)
         return dict(zip(self.INDEX_STATS, (int(v) for v in out)))
 

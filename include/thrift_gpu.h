@@ -352,13 +352,15 @@ int tgpu_context_wait(tgpu_context* ctx, void* stream, tgpu_status* st,
  * predecessor; links the ordered repair lane visited; tiles whose stored
  * record starts were re-walked. A canonical stream needs no repair: every
  * counter but the first is 0 (a diagnostic: speed, not correctness, depends
- * on it). Returns TGPU_ERR_INVALID_ARGUMENT when the context has run no
- * index.
+ * on it). out[TGPU_ISTAT_GENERAL]: records of the context's last decode call
+ * (any kind) that left the compiled / fixed-layout fast path for the general
+ * reader (0 on a canonical stream). Returns TGPU_ERR_INVALID_ARGUMENT when
+ * the context has run no index (out[TGPU_ISTAT_GENERAL] is still filled).
  */
 enum {
   TGPU_ISTAT_CHUNKS = 0, TGPU_ISTAT_PARTIAL = 1, TGPU_ISTAT_NO_START = 2,
   TGPU_ISTAT_BROKEN = 3, TGPU_ISTAT_REPAIRED = 4, TGPU_ISTAT_REWALKED = 5,
-  TGPU_ISTAT_COUNT = 6
+  TGPU_ISTAT_GENERAL = 6, TGPU_ISTAT_COUNT = 7
 };
 int tgpu_index_stats(tgpu_context* ctx, void* stream, uint64_t* out);
 

@@ -8,7 +8,10 @@
 // a second barrier. Threads whose two hashes differ saw the tile change after
 // the staging barrier. mode 0: LDS-DMA; 1: register staging; 2: LDS-DMA, then
 // each wave reads back its own last DMA'd vector (ds_read + lgkmcnt(0))
-// before the barrier; 3: LDS-DMA, then s_sleep before the first hash.
+// before the barrier; 3: LDS-DMA, then s_sleep before the first hash; 4:
+// LDS-DMA with heavy LDS traffic (bank-conflicting ds_or) by every wave after
+// its DMAs are issued and again after the barrier, as in the stream index's
+// tiles; 5: mode 4's traffic with register staging.
 // Built into tools/build/libglds_probe.so; bench/diagnostic only.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -18,15 +21,16 @@ constexpr uint32_t kT = 256;
 constexpr uint32_t kMaxTile = 20 * 1024;
 
 __global__ __launch_bounds__(kT) void probe_kernel(const uint8_t* __restrict__ src, uint64_t len,
-                                                   uint32_t tile, int mode,
+                                                   uint32_t tile, uint32_t stride, int mode,
                                                    unsigned long long* out) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[kMaxTile + 32];
-  const uint64_t lo = (uint64_t)blockIdx.x * tile;
+  __shared__ uint32_t busy[2048];
+  const uint64_t lo = (uint64_t)blockIdx.x * stride;  // (stride < tile: tiles overlap)
   if (lo >= len) return;
   const uint32_t bytes = (uint32_t)min((uint64_t)tile, len - lo);
   const uint32_t nvec = (bytes + 15) >> 4;
   const uint4* g = (const uint4*)(src + lo);
-  const uint32_t whole = mode == 1 ? 0u : (nvec & ~63u);
+  const uint32_t whole = (mode == 1 || mode == 5) ? 0u : (nvec & ~63u);
   const uint32_t wave = threadIdx.x >> 6;
   uint32_t last = ~0u;
   for (uint32_t k = 0; k * kT < whole; ++k) {
@@ -39,6 +43,8 @@ __global__ __launch_bounds__(kT) void probe_kernel(const uint8_t* __restrict__ s
     }
   }
   for (uint32_t i = whole + threadIdx.x; i < nvec; i += kT) ((uint4*)lds)[i] = g[i];
+  if (mode >= 4)  // LDS traffic (32-way bank conflicts) while the DMAs are in flight
+    for (uint32_t r = 0; r < 64; ++r) atomicOr(&busy[((threadIdx.x * 32) + r) & 2047], r);
   if (mode == 2 && last != ~0u) {
     __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) lgkmcnt(0) (all counters)
     const uint32_t v = ((volatile uint32_t*)lds)[last * 4];
@@ -46,6 +52,8 @@ __global__ __launch_bounds__(kT) void probe_kernel(const uint8_t* __restrict__ s
   }
   __syncthreads();
   if (mode == 3) __builtin_amdgcn_s_sleep(10);
+  if (mode >= 4)
+    for (uint32_t r = 0; r < 64; ++r) atomicOr(&busy[((threadIdx.x * 32) + r * 7) & 2047], r);
   const uint32_t nw = bytes >> 2;
   uint32_t h0 = 0, h1 = 0, hg = 0;
   for (uint32_t d = threadIdx.x; d < nw; d += kT) h0 ^= ((volatile uint32_t*)lds)[d] * (d | 1);
@@ -61,16 +69,22 @@ __global__ __launch_bounds__(kT) void probe_kernel(const uint8_t* __restrict__ s
 }  // namespace
 
 // Runs the probe over [0, len) of src `reps` times; out[0..3) summed.
-extern "C" int glds_probe_run(const void* src, uint64_t len, uint32_t tile, int mode, int reps,
+// refresh != NULL: before every launch the buffer is rewritten from refresh
+// (a device copy: the probe then reads bytes another kernel just wrote, as the
+// stream index reads the encoder's output)
+extern "C" int glds_probe_run(const void* src, uint64_t len, uint32_t tile, uint32_t stride,
+                              int mode, int reps, const void* refresh,
                               unsigned long long* host_out) {
   if (tile > kMaxTile || tile % 16) return 1;
   unsigned long long* d = nullptr;
   if (hipMalloc(&d, 4 * sizeof(unsigned long long)) != hipSuccess) return 2;
   hipMemset(d, 0, 4 * sizeof(unsigned long long));
-  const uint64_t blocks = (len + tile - 1) / tile;
-  for (int r = 0; r < reps; ++r)
+  const uint64_t blocks = (len + stride - 1) / stride;
+  for (int r = 0; r < reps; ++r) {
+    if (refresh) (void)hipMemcpyAsync((void*)src, refresh, len, hipMemcpyDeviceToDevice, 0);
     hipLaunchKernelGGL(probe_kernel, dim3((uint32_t)blocks), dim3(kT), 0, 0, (const uint8_t*)src,
-                       len, tile, mode, d);
+                       len, tile, stride, mode, d);
+  }
   const hipError_t e = hipMemcpy(host_out, d, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
   hipFree(d);
   return e == hipSuccess ? 0 : 3;
