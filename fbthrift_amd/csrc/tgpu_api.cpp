@@ -258,8 +258,6 @@ int validate_struct(const Tables& T, uint32_t si, int depth, SchemaFacts& facts)
     // required fields are checked through a 64-bit per-struct mask
     if (fd.qualifier == TGPU_REQUIRED && k >= 64 && (sd.flags & TGPU_STRUCT_ENFORCE_REQUIRED))
       return TGPU_ERR_UNSUPPORTED;
-    // a terse struct's emptiness is its fields' (thrift::empty): not supported
-    if (fd.qualifier == TGPU_TERSE && fd.ttype == TGPU_T_STRUCT) return TGPU_ERR_UNSUPPORTED;
     if (fd.isset_offset >= sd.size) return TGPU_ERR_INVALID_ARGUMENT;
     uint32_t sz;
     if (is_scalar(fd.ttype)) {

@@ -1182,14 +1182,62 @@ __device__ __forceinline__ void write_elem(Writer& w, uint32_t t, const uint8_t*
 }
 
 // op::isEmpty of a terse member (Clear.h:98-127): scalars by identity with
-// the intrinsic default (all bits zero), strings/containers by length.
-__device__ __forceinline__ bool terse_empty(const tgpu_field_desc& f, const uint8_t* m) {
+// the intrinsic default (all bits zero), strings/containers by length,
+// structs by thrift::empty (below).
+__device__ __forceinline__ bool terse_leaf_empty(const tgpu_field_desc& f, const uint8_t* m) {
   if (is_scalar(f.ttype)) {
     uint32_t any = 0;
     for (uint32_t b = 0; b < scalar_size(f.ttype); ++b) any |= m[b];
     return any == 0;
   }
   return ((const tgpu_span*)m)->length == 0;
+}
+
+// thrift::empty of struct si at obj — the generated __fbthrift_is_empty
+// (module_types_cpp/declare_members.whisker:83-113): never empty with an
+// unqualified or required field; otherwise empty when no optional field is
+// set and every terse field is empty (terse structs recursively); a union
+// (union_declare_members.whisker:43-45) when no member is active. The walk
+// keeps one (struct, object, next field) per nesting level.
+__device__ bool struct_empty(const DevSchema& sc, uint32_t si, const uint8_t* obj) {
+  struct Lvl {
+    uint32_t si, k;
+    const uint8_t* obj;
+  } st[kMaxSchemaDepth];
+  int sp = 0;
+  st[0] = Lvl{si, 0, obj};
+  for (;;) {
+    Lvl& L = st[sp];
+    const tgpu_struct_desc sd = sc.s[L.si];
+    if (L.k >= sd.num_fields) {  // this level is empty
+      if (sp == 0) return true;
+      --sp;
+      continue;
+    }
+    const tgpu_field_desc f = sc.f[sd.first_field + L.k++];
+    if (sd.flags & TGPU_STRUCT_UNION) {
+      if (L.obj[f.isset_offset]) return false;
+      continue;
+    }
+    if (f.qualifier == TGPU_UNQUALIFIED || f.qualifier == TGPU_REQUIRED) return false;
+    if (f.qualifier == TGPU_OPTIONAL) {
+      if (L.obj[f.isset_offset]) return false;
+      continue;
+    }
+    const uint8_t* m = L.obj + f.member_offset;  // terse
+    if (f.ttype == TGPU_T_STRUCT) {
+      if (sp + 1 >= kMaxSchemaDepth) return false;  // (schemas nest at most that deep)
+      st[++sp] = Lvl{(uint32_t)f.struct_index, 0, m};
+      continue;
+    }
+    if (!terse_leaf_empty(f, m)) return false;
+  }
+}
+
+__device__ __forceinline__ bool terse_empty(const DevSchema& sc, const tgpu_field_desc& f,
+                                            const uint8_t* m) {
+  return f.ttype == TGPU_T_STRUCT ? struct_empty(sc, (uint32_t)f.struct_index, m)
+                                  : terse_leaf_empty(f, m);
 }
 
 // The record writer: the generated write (serialize_struct.whisker:40-67,
@@ -1346,7 +1394,7 @@ __device__ void write_record(Writer& w, const DevSchema& sc, const uint8_t* rec,
     const uint8_t* obj = fr.obj;
     if (f.qualifier == TGPU_OPTIONAL && !obj[f.isset_offset]) continue;
     const uint8_t* m = obj + f.member_offset;
-    if (f.qualifier == TGPU_TERSE && terse_empty(f, m)) continue;
+    if (f.qualifier == TGPU_TERSE && terse_empty(sc, f, m)) continue;
     if (P == TGPU_PROTOCOL_BINARY) {
       w.put(f.ttype);
       w.put_be((uint16_t)f.id, 2);

@@ -161,7 +161,7 @@ uint32_t scalar_size(uint8_t t) {
 // op::isEmpty (thrift/lib/cpp2/op/detail/Clear.h:98-127) of a terse member:
 // scalars compare identical (bitwise) to the intrinsic default, so -0.0 is
 // not empty; strings and containers are empty when they have no elements.
-bool terse_empty(const tgpu_field_desc& f, const uint8_t* m) {
+bool terse_leaf_empty(const tgpu_field_desc& f, const uint8_t* m) {
   if (is_scalar(f.ttype)) {
     for (uint32_t b = 0; b < scalar_size(f.ttype); ++b)
       if (m[b]) return false;
@@ -170,6 +170,37 @@ bool terse_empty(const tgpu_field_desc& f, const uint8_t* m) {
   uint32_t len;
   std::memcpy(&len, m + 8, 4);  // tgpu_span.length
   return len == 0;
+}
+
+// thrift::empty of a struct: the generated __fbthrift_is_empty
+// (compiler/generate/templates/cpp2/module_types_cpp/declare_members.whisker:
+// 83-113) — false with any unqualified (or required) field; else no optional
+// field set and every terse field empty (terse structs recursively). Unions:
+// no active member (union_declare_members.whisker:43-45).
+bool struct_empty(const Schema& sc, uint32_t si, const uint8_t* obj) {
+  const tgpu_struct_desc& sd = sc.s[si];
+  for (uint32_t k = 0; k < sd.num_fields; ++k) {
+    const tgpu_field_desc& f = sc.f[sd.first_field + k];
+    if (sd.flags & TGPU_STRUCT_UNION) {
+      if (obj[f.isset_offset]) return false;
+      continue;
+    }
+    if (f.qualifier == TGPU_UNQUALIFIED || f.qualifier == TGPU_REQUIRED) return false;
+    if (f.qualifier == TGPU_OPTIONAL) {
+      if (obj[f.isset_offset]) return false;
+      continue;
+    }
+    const uint8_t* m = obj + f.member_offset;
+    if (f.ttype == TGPU_T_STRUCT ? !struct_empty(sc, (uint32_t)f.struct_index, m)
+                                 : !terse_leaf_empty(f, m))
+      return false;
+  }
+  return true;
+}
+
+bool terse_empty(const Schema& sc, const tgpu_field_desc& f, const uint8_t* m) {
+  return f.ttype == TGPU_T_STRUCT ? struct_empty(sc, (uint32_t)f.struct_index, m)
+                                  : terse_leaf_empty(f, m);
 }
 
 // ================================================================ readers ===
@@ -1046,7 +1077,7 @@ struct BinaryWriter {
       const tgpu_field_desc& f = ec.sc->f[sd.first_field + k];
       if (f.qualifier == TGPU_OPTIONAL && !obj[f.isset_offset]) continue;
       const uint8_t* m = obj + f.member_offset;
-      if (f.qualifier == TGPU_TERSE && terse_empty(f, m)) continue;  // fields.whisker:84
+      if (f.qualifier == TGPU_TERSE && terse_empty(*ec.sc, f, m)) continue;  // fields.whisker:84
       s.put(f.ttype);  // writeFieldBegin: byte type + BE i16 id
       s.putBE((uint16_t)f.id, 2);
       if (is_scalar(f.ttype)) {
@@ -1154,7 +1185,7 @@ struct CompactWriterT {
       const tgpu_field_desc& f = ec.sc->f[sd.first_field + k];
       if (f.qualifier == TGPU_OPTIONAL && !obj[f.isset_offset]) continue;
       const uint8_t* m = obj + f.member_offset;
-      if (f.qualifier == TGPU_TERSE && terse_empty(f, m)) continue;  // fields.whisker:84
+      if (f.qualifier == TGPU_TERSE && terse_empty(*ec.sc, f, m)) continue;  // fields.whisker:84
       if (f.ttype == TGPU_T_BOOL) {  // bool value rides in the header
         const uint8_t b = load_bool_checked(m, s.pos);
         fieldHeader(b ? 1 : 2, f.id, last);

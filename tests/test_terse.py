@@ -97,3 +97,129 @@ def test_gpu_terse_matches_oracle(gpu, protocol):
     dst, drec, darena, dnd, dcons = oracle.decode(schema, protocol, owire, n)
     assert gst.as_tuple() == dst.as_tuple() and (gnd, gcons) == (dnd, dcons)
     assert np.array_equal(grec.cpu().numpy(), drec)
+
+
+# ---- terse struct fields ----------------------------------------------------
+# A terse struct member is written unless thrift::empty (the generated
+# __fbthrift_is_empty, compiler/generate/templates/cpp2/module_types_cpp/
+# declare_members.whisker:83-113): never empty with an unqualified field;
+# else empty when no optional field is set and every terse field is empty
+# (terse structs recursively); a union (union_declare_members.whisker:43-45)
+# when no member is active.
+# Root {1: terse Inner inner; 2: terse Plain plain; 3: terse U u; 4: i64 z}
+# Inner {1: terse i32 a; 2: optional string s; 3: terse Deep d}
+# Deep {1: terse list<i32> l}
+# Plain {1: i32 x}                 (unqualified: never empty)
+# U union {1: i32 p; 2: string q}
+STABLE = [
+    [[1, 12, 0, 2, 1], [2, 12, 0, 2, 3], [3, 12, 0, 2, 4], [4, 10, 0, 0, -1]],
+    [[1, 8, 0, 2, -1], [2, 11, 0, 1, -1], [3, 12, 0, 2, 2]],
+    [[1, 15, 8, 2, -1]],
+    [[1, 8, 0, 0, -1]],
+    {"union": True, "fields": [[1, 8, 0, 0, -1], [2, 11, 0, 0, -1]]},
+]
+
+
+def _srecords(schema, rows):
+    """rows: dict per record with keys a, s (None = unset), l (list), x, u
+    (None | ('p', int) | ('q', bytes)), z."""
+    r = np.zeros(len(rows), dtype=schema.dtype())
+    sarena, larena = bytearray(), bytearray()
+    for i, row in enumerate(rows):
+        inner = r["f1"][i]
+        inner["f1"] = row.get("a", 0)
+        if row.get("s") is not None:
+            s = row["s"]
+            inner["f2"]["offset"], inner["f2"]["length"] = len(sarena), len(s)
+            sarena += s
+            inner["__isset"][1] = 1
+        lst = row.get("l", [])
+        inner["f3"]["f1"]["offset"], inner["f3"]["f1"]["length"] = len(larena), len(lst)
+        larena += b"".join(struct.pack("<i", v) for v in lst)
+        r["f2"][i]["f1"] = row.get("x", 0)
+        u = row.get("u")
+        if u is not None:
+            if u[0] == "p":
+                r["f3"][i]["f1"] = u[1]
+                r["f3"][i]["__isset"][0] = 1
+            else:
+                r["f3"][i]["f2"]["offset"], r["f3"][i]["f2"]["length"] = len(sarena), len(u[1])
+                sarena += u[1]
+                r["f3"][i]["__isset"][1] = 1
+        r["f4"][i] = row.get("z", 0)
+    return (r.view(np.uint8), np.frombuffer(bytes(sarena) or b"\0", np.uint8).copy(),
+            np.frombuffer(bytes(larena) or b"\0\0\0\0", np.uint8).copy())
+
+
+def test_oracle_terse_struct_bytes():
+    schema = Schema.from_table(STABLE)
+    rows = [
+        dict(z=7),                       # inner, u empty; plain (unqualified x) written
+        dict(a=5, u=("p", 0)),           # inner written (a); u active (member 0 is 0)
+        dict(s=b""),                     # optional s set (even empty): inner written
+        dict(l=[3]),                     # deep terse list non-empty: inner, deep written
+    ]
+    rec, sa, la = _srecords(schema, rows)
+    st, wire, offs = oracle.encode(schema, 0, rec, len(rows), sa, la)
+    assert st.code == 0
+    plain = "0c0002 080001 00000000 00"
+    want = bytes.fromhex(
+        plain + " 0a0004 0000000000000007 00"
+        + "0c0001 080001 00000005 00 " + plain + " 0c0003 080001 00000000 00 0a0004 0000000000000000 00"
+        + "0c0001 0b0002 00000000 00 " + plain + " 0a0004 0000000000000000 00"
+        + "0c0001 0c0003 0f0001 08 00000001 00000003 00 00 " + plain
+        + " 0a0004 0000000000000000 00")
+    assert wire == want
+    st, wire, offs = oracle.encode(schema, 2, rec, len(rows), sa, la)
+    assert st.code == 0
+    cplain = "2c 15 00 00"  # delta 2, struct; {1: i32 0}; STOP
+    want_c = bytes.fromhex(
+        cplain + " 26 0e 00"                        # z = 7: delta 2 from 2
+        + "1c 15 0a 00 " + "1c 15 00 00" + " 1c 15 00 00 16 00 00"
+        + "1c 28 00 00 1c 15 00 00 26 00 00"   # plain follows field 1: delta 1
+        + "1c 3c 19 15 06 00 00 1c 15 00 00 26 00 00")
+    assert wire == want_c
+    # read back: absent terse structs stay at their defaults
+    for proto in (0, 2):
+        st, w, _ = oracle.encode(schema, proto, rec, len(rows), sa, la)
+        st, out, arena, nd, _ = oracle.decode(schema, proto, w, len(rows))
+        assert st.code == 0 and nd == len(rows)
+        r = out.view(schema.dtype())
+        assert r["f4"][0] == 7 and r["f1"]["f1"][1] == 5 and r["f3"]["__isset"][1][0] == 1
+        assert list(r["__isset"][0]) == [0, 1, 0, 1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("protocol", [0, 2])
+def test_gpu_terse_struct_matches_oracle(gpu, protocol):
+    import torch
+
+    from fbthrift_amd.serializer import BinarySerializer, CompactSerializer, GpuSchema
+
+    S = BinarySerializer if protocol == 0 else CompactSerializer
+    schema = Schema.from_table(STABLE)
+    rng = np.random.default_rng(11)
+    rows = []
+    for i in range(20_000):
+        e = rng.integers(0, 2, 6)
+        u = None if e[4] else (("p", int(rng.integers(-9, 9))) if e[5] else
+                               ("q", bytes(rng.integers(0, 256, int(rng.integers(0, 4)),
+                                                        dtype=np.uint8))))
+        rows.append(dict(a=0 if e[0] else int(rng.integers(-9, 9)),
+                         s=None if e[1] else b"xy"[: int(rng.integers(0, 3))],
+                         l=[] if e[2] else [int(v) for v in rng.integers(-9, 9, 2)],
+                         x=0 if e[3] else 4, u=u, z=int(rng.integers(0, 99))))
+    rec, sa, la = _srecords(schema, rows)
+    n = len(rows)
+    ost, owire, ooffs = oracle.encode(schema, protocol, rec, n, sa, la)
+    assert ost.code == 0
+    gs = GpuSchema(schema)
+    dev = gpu
+    wire, offs = S.serialize(gs, torch.from_numpy(rec).to(dev), n, torch.from_numpy(sa).to(dev),
+                             torch.from_numpy(la).to(dev))
+    assert bytes(wire.cpu().numpy()) == owire
+    w = torch.from_numpy(np.frombuffer(owire, np.uint8).copy()).to(dev)
+    grec, garena, gst, gnd, gcons = S.deserialize_status(gs, w, n)
+    dst, drec, darena, dnd, dcons = oracle.decode(schema, protocol, owire, n)
+    assert gst.as_tuple() == dst.as_tuple() and (gnd, gcons) == (dnd, dcons)
+    assert np.array_equal(grec.cpu().numpy(), drec)
