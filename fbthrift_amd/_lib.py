@@ -33,7 +33,7 @@ CODE = {v: k for k, v in CODES.items()}
 class FieldDesc(ctypes.Structure):
     _fields_ = [("id", ctypes.c_int16), ("ttype", ctypes.c_uint8),
                 ("elem_ttype", ctypes.c_uint8), ("qualifier", ctypes.c_uint8),
-                ("val_ttype", ctypes.c_uint8), ("reserved0", ctypes.c_uint8 * 2), ("member_offset", ctypes.c_uint32),
+                ("val_ttype", ctypes.c_uint8), ("key_index", ctypes.c_uint16), ("member_offset", ctypes.c_uint32),
                 ("isset_offset", ctypes.c_uint32), ("struct_index", ctypes.c_int32),
                 ("type_index", ctypes.c_uint32)]
 
@@ -42,7 +42,7 @@ class TypeDesc(ctypes.Structure):
     _fields_ = [("ttype", ctypes.c_uint8), ("elem_ttype", ctypes.c_uint8),
                 ("val_ttype", ctypes.c_uint8), ("reserved0", ctypes.c_uint8),
                 ("struct_index", ctypes.c_int32), ("type_index", ctypes.c_uint32),
-                ("reserved1", ctypes.c_uint32)]
+                ("key_index", ctypes.c_uint32)]
 
 
 class StructDesc(ctypes.Structure):

@@ -237,9 +237,20 @@ __global__ void stream_decode_finish_kernel(DecodeArgs a) {
 }
 
 // ------------------------------------------------------------------ encode --
+// lane >= 0: the deep-pass lane whose HBM frames the writer may use.
+__device__ __forceinline__ void attach_slab(Writer& w, const DeepArgs& d, int lane) {
+  if (lane < 0 || !d.slabs) return;
+  w.deep = d.slabs + (uint64_t)lane * slab_lane_bytes(d.slab_frames);
+  w.deep_cap = d.slab_frames;
+}
+
+// (out of line: inlined into the size kernel, the writer made this
+// compiler's inliner crash, ROCm 7.2 clang 22)
 template <int P>
-__device__ __forceinline__ Writer size_one(const EncodeArgs& a, uint64_t i) {
+__device__ __attribute__((noinline)) Writer size_one(const EncodeArgs& a, uint64_t i,
+                                                     int lane = -1) {
   Writer w{nullptr, 0, 0, 0, 0};
+  attach_slab(w, a.deep, lane);
   write_record<P>(w, a.sc, a.recs + i * a.rec_size, a.sbase, a.lbase);
   return w;
 }
@@ -271,18 +282,38 @@ __device__ __forceinline__ unsigned long long block_exscan(unsigned long long v)
   return pre + x - v;
 }
 
+// A record nested past the private frames is sized 0 here and deferred: the
+// deep size pass adds its size to its tile's sum before the scan.
 template <int P>
 __global__ __launch_bounds__(256) void encode_size_kernel(EncodeArgs a) {
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   unsigned long long sz = 0;
   if (i < a.n) {
     const Writer w = size_one<P>(a, i);
-    if (!w.ok()) atomicMin(&a.res->first_fail, (unsigned long long)i);
-    sz = w.pos;
+    if (w.err == kErrDeep) a.deep.list[atomicAdd(a.deep.count, 1ull)] = i;
+    else if (!w.ok()) atomicMin(&a.res->first_fail, (unsigned long long)i);
+    else sz = w.pos;
     a.offs[i] = sz;
   }
   const unsigned long long t = block_sum(sz);
   if (threadIdx.x == 0) a.block_sums[blockIdx.x] = t;
+}
+
+template <int P>
+__global__ __launch_bounds__(64) void deep_size_kernel(EncodeArgs a) {
+  const uint32_t lane = blockIdx.x * 64 + threadIdx.x;
+  if (lane >= a.deep.lanes) return;
+  const uint64_t m = *a.deep.count;
+  for (uint64_t k = lane; k < m; k += a.deep.lanes) {
+    const uint64_t i = a.deep.list[k];
+    const Writer w = size_one<P>(a, i, (int)lane);
+    if (!w.ok()) {
+      atomicMin(&a.res->first_fail, (unsigned long long)i);
+      continue;
+    }
+    a.offs[i] = w.pos;
+    atomicAdd(&a.block_sums[i / 256], (unsigned long long)w.pos);
+  }
 }
 
 template <int P>
@@ -296,8 +327,25 @@ __global__ __launch_bounds__(256) void encode_write_kernel(EncodeArgs a) {
     atomicMin(&a.res->first_fail, (unsigned long long)i);
     return;
   }
+  // (a deferred record stops at its private frames; the deep write pass
+  // writes it whole)
   Writer w{a.out, start, a.cap, 0, 0};
   write_record<P>(w, a.sc, a.recs + i * a.rec_size, a.sbase, a.lbase);
+}
+
+template <int P>
+__global__ __launch_bounds__(64) void deep_write_kernel(EncodeArgs a) {
+  const uint32_t lane = blockIdx.x * 64 + threadIdx.x;
+  if (lane >= a.deep.lanes) return;
+  const uint64_t m = *a.deep.count;
+  for (uint64_t k = lane; k < m; k += a.deep.lanes) {
+    const uint64_t i = a.deep.list[k];
+    const uint64_t start = a.offs[i];
+    if (a.res->first_fail <= i) continue;
+    Writer w{a.out, start, a.cap, 0, 0};
+    attach_slab(w, a.deep, (int)lane);
+    write_record<P>(w, a.sc, a.recs + i * a.rec_size, a.sbase, a.lbase);
+  }
 }
 
 // sizes -> exclusive offsets (block-local scan + scanned block sums)
@@ -314,7 +362,7 @@ __global__ void encode_finish_kernel(EncodeArgs a, uint64_t fixed_len) {
   DevResult* res = a.res;
   const uint64_t f = res->first_fail;
   if (f < a.n) {
-    const Writer w = size_one<P>(a, f);
+    const Writer w = size_one<P>(a, f, a.deep.slabs ? 0 : -1);
     const uint64_t start = fixed_len ? f * fixed_len : a.offs[f];
     res->code = w.ok() ? TGPU_ERR_OUTPUT_OVERFLOW : w.err;
     res->fail_offset = start + (w.ok() ? 0 : w.err_off);
@@ -417,15 +465,29 @@ hipError_t launch_tail_decode_finish(const DecodeArgs& a, int protocol, uint64_t
   return hipGetLastError();
 }
 
+// The deep passes of the general encode (a record nested past the private
+// frames): launched on every call, their lanes exit on an empty list.
+hipError_t launch_deep_size(const EncodeArgs& a, int protocol, hipStream_t stream) {
+  if (!a.deep.lanes) return hipSuccess;
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(deep_size_kernel<P_>, dim3((a.deep.lanes + 63) / 64),
+                                                dim3(64), 0, stream, a));
+  return hipGetLastError();
+}
+
 hipError_t launch_general_encode(const EncodeArgs& a, int protocol, uint64_t n_blocks,
                                  hipStream_t stream) {
   if (a.n == 0) return hipSuccess;
   const dim3 grid((uint32_t)n_blocks);
   TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_size_kernel<P_>, grid, dim3(256), 0, stream, a));
-  const hipError_t e = launch_scan_tiles(a.block_sums, n_blocks, a.scan_part, &a.res->total_bytes,
-                                         a.offs + a.n, stream);
+  hipError_t e = launch_deep_size(a, protocol, stream);
+  if (e != hipSuccess) return e;
+  e = launch_scan_tiles(a.block_sums, n_blocks, a.scan_part, &a.res->total_bytes, a.offs + a.n,
+                        stream);
   if (e != hipSuccess) return e;
   TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_write_kernel<P_>, grid, dim3(256), 0, stream, a));
+  if (a.deep.lanes)
+    TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(deep_write_kernel<P_>, dim3((a.deep.lanes + 63) / 64),
+                                                  dim3(64), 0, stream, a));
   return hipGetLastError();
 }
 
@@ -434,8 +496,10 @@ hipError_t launch_general_size(const EncodeArgs& a, int protocol, uint64_t n_blo
   if (a.n == 0) return hipSuccess;
   const dim3 grid((uint32_t)n_blocks);
   TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_size_kernel<P_>, grid, dim3(256), 0, stream, a));
-  const hipError_t e = launch_scan_tiles(a.block_sums, n_blocks, a.scan_part, &a.res->total_bytes,
-                                         a.offs + a.n, stream);
+  hipError_t e = launch_deep_size(a, protocol, stream);
+  if (e != hipSuccess) return e;
+  e = launch_scan_tiles(a.block_sums, n_blocks, a.scan_part, &a.res->total_bytes, a.offs + a.n,
+                        stream);
   if (e != hipSuccess) return e;
   return launch_size_offsets(a, n_blocks, stream);
 }

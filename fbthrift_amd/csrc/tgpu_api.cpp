@@ -150,16 +150,23 @@ uint32_t scalar_size(uint32_t t) {
   }
 }
 uint32_t align_up(uint32_t x, uint32_t a) { return (x + a - 1) / a * a; }
-// container element types: scalars, or strings (as tgpu_span)
-bool is_elem(uint32_t t) { return is_scalar(t) || t == TGPU_T_STRING; }
+
+bool is_container_t(uint32_t t) { return t == TGPU_T_LIST || t == TGPU_T_SET || t == TGPU_T_MAP; }
+bool is_complex_t(uint32_t t) { return t == TGPU_T_STRUCT || is_container_t(t); }
+bool is_boxed(const tgpu_field_desc& f) {
+  return f.qualifier == TGPU_BOXED || f.qualifier == TGPU_OPTIONAL_BOXED;
+}
 
 // Layout of struct si (memoized in `done`): declaration-order members at
-// natural alignment, then one isset byte per field (Isset.h:243-296).
+// natural alignment, then one isset byte per field (Isset.h:243-296). A boxed
+// struct member is a 16-byte span (the pointer), so recursion through it (or
+// through a container) needs no layout recursion; a struct holding itself
+// by value has no layout.
 int layout_struct(tgpu_struct_desc* s, uint32_t ns, tgpu_field_desc* f, uint32_t nf,
                   uint32_t si, std::vector<int>& state) {
   if (si >= ns) return TGPU_ERR_INVALID_ARGUMENT;
   if (state[si] == 2) return TGPU_OK;
-  if (state[si] == 1) return TGPU_ERR_UNSUPPORTED;  // recursive struct
+  if (state[si] == 1) return TGPU_ERR_UNSUPPORTED;  // a struct holding itself by value
   state[si] = 1;
   tgpu_struct_desc& sd = s[si];
   if ((uint64_t)sd.first_field + sd.num_fields > nf) return TGPU_ERR_INVALID_ARGUMENT;
@@ -169,8 +176,8 @@ int layout_struct(tgpu_struct_desc* s, uint32_t ns, tgpu_field_desc* f, uint32_t
     uint32_t sz, al;
     if (is_scalar(fd.ttype)) {
       sz = al = scalar_size(fd.ttype);
-    } else if (fd.ttype == TGPU_T_STRING || fd.ttype == TGPU_T_LIST || fd.ttype == TGPU_T_SET ||
-               fd.ttype == TGPU_T_MAP) {
+    } else if (fd.ttype == TGPU_T_STRING || is_container_t(fd.ttype) ||
+               (fd.ttype == TGPU_T_STRUCT && is_boxed(fd))) {
       sz = 16;
       al = 8;
     } else if (fd.ttype == TGPU_T_STRUCT) {
@@ -195,8 +202,8 @@ int layout_struct(tgpu_struct_desc* s, uint32_t ns, tgpu_field_desc* f, uint32_t
   return TGPU_OK;
 }
 
-// The schema tables a validation walks (fields' type_index / struct_index
-// into these).
+// The schema tables a validation walks (fields' type_index / struct_index /
+// key_index into these).
 struct Tables {
   const tgpu_struct_desc* s;
   uint32_t ns;
@@ -208,94 +215,190 @@ struct Tables {
 
 struct SchemaFacts {
   bool has_lists = false;
-  bool nested = false;  // a container holds structs or containers
+  bool nested = false;  // a container holds structs or containers, a complex key, a boxed field
 };
 
-int validate_struct(const Tables& T, uint32_t si, int depth, SchemaFacts& facts);
+// Terse struct members nest at most this deep (the device's emptiness walk,
+// tgpu_device.h struct_empty, keeps one level per terse struct member).
+constexpr int kMaxTerseDepth = 16;
 
-// A container (list/set/map) description c at nesting depth `depth` (each
-// struct or container of structs/containers takes one of the device's
-// kMaxSchemaDepth frames).
-int validate_container(const Tables& T, uint32_t ttype, uint32_t elem, uint32_t val,
-                       int32_t struct_index, uint32_t type_index, int depth, SchemaFacts& facts) {
-  facts.has_lists = true;
-  if (depth >= kMaxSchemaDepth) return TGPU_ERR_UNSUPPORTED;
-  const bool is_map = ttype == TGPU_T_MAP;
-  if (ttype != TGPU_T_LIST && ttype != TGPU_T_SET && !is_map) return TGPU_ERR_INVALID_ARGUMENT;
-  if (is_map && !is_elem(elem)) return TGPU_ERR_UNSUPPORTED;  // keys: scalars, strings
-  const uint32_t v = is_map ? val : elem;
-  if (is_elem(v)) return TGPU_OK;
-  facts.nested = true;
-  if (v == TGPU_T_STRUCT) {
-    if (struct_index < 0 || (uint32_t)struct_index >= T.ns) return TGPU_ERR_INVALID_ARGUMENT;
-    return validate_struct(T, (uint32_t)struct_index, depth + 1, facts);
-  }
-  if (v == TGPU_T_LIST || v == TGPU_T_SET || v == TGPU_T_MAP) {
-    if (type_index == 0 || type_index > T.nt) return TGPU_ERR_INVALID_ARGUMENT;
-    const tgpu_type_desc& n = T.t[type_index - 1];
-    if (n.ttype != v) return TGPU_ERR_INVALID_ARGUMENT;
-    return validate_container(T, n.ttype, n.elem_ttype, n.val_ttype, n.struct_index,
-                              n.type_index, depth + 1, facts);
-  }
-  return TGPU_ERR_UNSUPPORTED;
-}
+// Validation of a schema whose structs may be recursive (through containers
+// and boxed fields): every struct and type node reachable from the root is
+// checked once (visited sets), so recursion terminates; two shapes without a
+// finite form are rejected — a struct holding itself by value (no layout)
+// and a cycle of type nodes alone (list<list<...>> forever).
+struct Validator {
+  const Tables& T;
+  SchemaFacts& facts;
+  std::vector<uint8_t> sv, tv;  // visited structs / type nodes
+  std::vector<uint32_t> work;   // structs to check
 
-int validate_struct(const Tables& T, uint32_t si, int depth, SchemaFacts& facts) {
-  if (si >= T.ns || depth > kMaxSchemaDepth - 1) return TGPU_ERR_UNSUPPORTED;
-  const tgpu_struct_desc& sd = T.s[si];
-  if ((uint64_t)sd.first_field + sd.num_fields > T.nf || sd.size == 0 || sd.align == 0 ||
-      sd.size % sd.align)
-    return TGPU_ERR_INVALID_ARGUMENT;
-  if (sd.flags & ~(uint32_t)(TGPU_STRUCT_UNION | TGPU_STRUCT_ENFORCE_REQUIRED))
-    return TGPU_ERR_UNSUPPORTED;
-  for (uint32_t k = 0; k < sd.num_fields; ++k) {
-    const tgpu_field_desc& fd = T.f[sd.first_field + k];
-    if ((sd.flags & TGPU_STRUCT_UNION) && fd.qualifier != TGPU_UNQUALIFIED)
-      return TGPU_ERR_UNSUPPORTED;
-    for (uint32_t j = 0; j < k; ++j)
-      if (T.f[sd.first_field + j].id == fd.id) return TGPU_ERR_INVALID_ARGUMENT;
-    if (fd.qualifier > TGPU_REQUIRED) return TGPU_ERR_UNSUPPORTED;
-    // required fields are checked through a 64-bit per-struct mask
-    if (fd.qualifier == TGPU_REQUIRED && k >= 64 && (sd.flags & TGPU_STRUCT_ENFORCE_REQUIRED))
-      return TGPU_ERR_UNSUPPORTED;
-    if (fd.isset_offset >= sd.size) return TGPU_ERR_INVALID_ARGUMENT;
-    uint32_t sz;
-    if (is_scalar(fd.ttype)) {
-      sz = scalar_size(fd.ttype);
-    } else if (fd.ttype == TGPU_T_STRING) {
-      sz = 16;
-    } else if (fd.ttype == TGPU_T_LIST || fd.ttype == TGPU_T_SET || fd.ttype == TGPU_T_MAP) {
-      const int rc = validate_container(T, fd.ttype, fd.elem_ttype, fd.val_ttype, fd.struct_index,
-                                        fd.type_index, depth, facts);
-      if (rc) return rc;
-      sz = 16;
-    } else if (fd.ttype == TGPU_T_STRUCT) {
-      if (fd.struct_index < 0 || (uint32_t)fd.struct_index >= T.ns) return TGPU_ERR_INVALID_ARGUMENT;
-      const int rc = validate_struct(T, (uint32_t)fd.struct_index, depth + 1, facts);
-      if (rc) return rc;
-      sz = T.s[fd.struct_index].size;
-    } else {
-      return TGPU_ERR_UNSUPPORTED;
+  int node(uint32_t ti, uint32_t want_ttype) {  // ti: 1 + index
+    if (ti == 0 || ti > T.nt) return TGPU_ERR_INVALID_ARGUMENT;
+    const tgpu_type_desc& n = T.t[ti - 1];
+    if (n.ttype != want_ttype) return TGPU_ERR_INVALID_ARGUMENT;
+    if (tv[ti - 1]) return TGPU_OK;
+    tv[ti - 1] = 1;
+    if (n.ttype == TGPU_T_STRUCT) return value(TGPU_T_STRUCT, n.struct_index, 0);
+    return container(n.ttype, n.elem_ttype, n.val_ttype, n.struct_index, n.type_index, n.key_index);
+  }
+  // a container element / map value / map key of type t
+  int value(uint32_t t, int32_t si, uint32_t ti) {
+    if (t == TGPU_T_STRUCT) {
+      if (si < 0 || (uint32_t)si >= T.ns) return TGPU_ERR_INVALID_ARGUMENT;
+      if (!sv[si]) {
+        sv[si] = 1;
+        work.push_back((uint32_t)si);
+      }
+      return TGPU_OK;
     }
-    if ((uint64_t)fd.member_offset + sz > sd.size) return TGPU_ERR_INVALID_ARGUMENT;
-    // natural alignment: a nested struct's own, else min(size, 8)
-    const uint32_t al = fd.ttype == TGPU_T_STRUCT ? T.s[fd.struct_index].align : (sz >= 8 ? 8 : sz);
-    if (fd.member_offset % al) return TGPU_ERR_INVALID_ARGUMENT;
+    if (is_container_t(t)) return node(ti, t);
+    return (is_scalar(t) || t == TGPU_T_STRING) ? TGPU_OK : TGPU_ERR_UNSUPPORTED;
   }
-  return TGPU_OK;
-}
+  int container(uint32_t ttype, uint32_t elem, uint32_t val, int32_t si, uint32_t ti,
+                uint32_t ki) {
+    facts.has_lists = true;
+    const bool is_map = ttype == TGPU_T_MAP;
+    if (!is_container_t(ttype)) return TGPU_ERR_INVALID_ARGUMENT;
+    const uint32_t v = is_map ? val : elem;
+    if (is_complex_t(v)) facts.nested = true;
+    int rc = value(v, si, ti);
+    if (rc) return rc;
+    if (!is_map) return ki ? TGPU_ERR_INVALID_ARGUMENT : TGPU_OK;
+    if (!is_complex_t(elem)) {
+      if (ki) return TGPU_ERR_INVALID_ARGUMENT;
+      return value(elem, -1, 0);
+    }
+    facts.nested = true;
+    return node(ki, elem);  // a struct key: a T_STRUCT node
+  }
+  int struct_(uint32_t si) {
+    const tgpu_struct_desc& sd = T.s[si];
+    if ((uint64_t)sd.first_field + sd.num_fields > T.nf || sd.size == 0 || sd.align == 0 ||
+        sd.size % sd.align)
+      return TGPU_ERR_INVALID_ARGUMENT;
+    if (sd.flags & ~(uint32_t)(TGPU_STRUCT_UNION | TGPU_STRUCT_ENFORCE_REQUIRED))
+      return TGPU_ERR_UNSUPPORTED;
+    for (uint32_t k = 0; k < sd.num_fields; ++k) {
+      const tgpu_field_desc& fd = T.f[sd.first_field + k];
+      if ((sd.flags & TGPU_STRUCT_UNION) && fd.qualifier != TGPU_UNQUALIFIED)
+        return TGPU_ERR_UNSUPPORTED;
+      for (uint32_t j = 0; j < k; ++j)
+        if (T.f[sd.first_field + j].id == fd.id) return TGPU_ERR_INVALID_ARGUMENT;
+      if (fd.qualifier > TGPU_OPTIONAL_BOXED) return TGPU_ERR_UNSUPPORTED;
+      if (is_boxed(fd) && fd.ttype != TGPU_T_STRUCT) return TGPU_ERR_UNSUPPORTED;
+      if (fd.key_index && fd.ttype != TGPU_T_MAP) return TGPU_ERR_INVALID_ARGUMENT;
+      // required fields are checked through a 64-bit per-struct mask
+      if (fd.qualifier == TGPU_REQUIRED && k >= 64 && (sd.flags & TGPU_STRUCT_ENFORCE_REQUIRED))
+        return TGPU_ERR_UNSUPPORTED;
+      if (fd.isset_offset >= sd.size) return TGPU_ERR_INVALID_ARGUMENT;
+      uint32_t sz;
+      if (is_scalar(fd.ttype)) {
+        sz = scalar_size(fd.ttype);
+      } else if (fd.ttype == TGPU_T_STRING) {
+        sz = 16;
+      } else if (is_container_t(fd.ttype)) {
+        const int rc = container(fd.ttype, fd.elem_ttype, fd.val_ttype, fd.struct_index,
+                                 fd.type_index, fd.key_index);
+        if (rc) return rc;
+        sz = 16;
+      } else if (fd.ttype == TGPU_T_STRUCT) {
+        if (fd.struct_index < 0 || (uint32_t)fd.struct_index >= T.ns) return TGPU_ERR_INVALID_ARGUMENT;
+        const int rc = value(TGPU_T_STRUCT, fd.struct_index, 0);
+        if (rc) return rc;
+        if (is_boxed(fd)) facts.nested = facts.has_lists = true;  // objects in the arena
+        sz = is_boxed(fd) ? 16 : T.s[fd.struct_index].size;
+      } else {
+        return TGPU_ERR_UNSUPPORTED;
+      }
+      if ((uint64_t)fd.member_offset + sz > sd.size) return TGPU_ERR_INVALID_ARGUMENT;
+      // natural alignment: a nested struct's own, else min(size, 8)
+      const uint32_t al = (fd.ttype == TGPU_T_STRUCT && !is_boxed(fd))
+                              ? T.s[fd.struct_index].align : (sz >= 8 ? 8 : sz);
+      if (fd.member_offset % al) return TGPU_ERR_INVALID_ARGUMENT;
+    }
+    return TGPU_OK;
+  }
+  // struct si's by-value struct members never lead back to si; terse struct
+  // members nest at most kMaxTerseDepth deep
+  int by_value(uint32_t si, std::vector<uint8_t>& st, int terse_depth) {
+    if (st[si] == 1) return TGPU_ERR_UNSUPPORTED;
+    if (st[si] == 2 && terse_depth == 0) return TGPU_OK;
+    if (terse_depth > kMaxTerseDepth) return TGPU_ERR_UNSUPPORTED;
+    st[si] = 1;
+    const tgpu_struct_desc& sd = T.s[si];
+    for (uint32_t k = 0; k < sd.num_fields; ++k) {
+      const tgpu_field_desc& fd = T.f[sd.first_field + k];
+      if (fd.ttype != TGPU_T_STRUCT || is_boxed(fd)) continue;
+      const int rc = by_value((uint32_t)fd.struct_index, st,
+                              fd.qualifier == TGPU_TERSE ? terse_depth + 1 : 0);
+      if (rc) return rc;
+    }
+    st[si] = 2;
+    return TGPU_OK;
+  }
+  int run() {
+    sv.assign(T.ns, 0);
+    tv.assign(T.nt, 0);
+    // type-node chains (type_index / key_index edges between nodes) are
+    // finite: a colored DFS over the node graph finds any cycle
+    std::vector<uint8_t> color(T.nt, 0);
+    for (uint32_t k = 0; k < T.nt; ++k) {
+      if (color[k]) continue;
+      std::vector<std::pair<uint32_t, int>> stack{{k, 0}};
+      color[k] = 1;
+      while (!stack.empty()) {
+        auto& [x, e] = stack.back();
+        const tgpu_type_desc& n = T.t[x];
+        const uint32_t nx = e == 0 ? n.type_index : e == 1 ? n.key_index : 0;
+        if (e >= 2) {
+          color[x] = 2;
+          stack.pop_back();
+          continue;
+        }
+        ++e;
+        if (!nx || nx > T.nt) continue;
+        if (color[nx - 1] == 1) return TGPU_ERR_INVALID_ARGUMENT;
+        if (color[nx - 1] == 0) {
+          color[nx - 1] = 1;
+          stack.push_back({nx - 1, 0});
+        }
+      }
+    }
+    sv[0] = 1;
+    work.push_back(0);
+    while (!work.empty()) {
+      const uint32_t si = work.back();
+      work.pop_back();
+      const int rc = struct_(si);
+      if (rc) return rc;
+    }
+    std::vector<uint8_t> st(T.ns, 0);
+    for (uint32_t si = 0; si < T.ns; ++si)
+      if (sv[si]) {
+        const int rc = by_value(si, st, 0);
+        if (rc) return rc;
+      }
+    return TGPU_OK;
+  }
+};
 
 int validate(const tgpu_struct_desc* s, uint32_t ns, const tgpu_field_desc* f, uint32_t nf,
              const tgpu_type_desc* t, uint32_t nt, SchemaFacts& facts) {
-  return validate_struct(Tables{s, ns, f, nf, t, nt}, 0, 0, facts);
+  const Tables T{s, ns, f, nf, t, nt};
+  Validator v{T, facts, {}, {}, {}};
+  return v.run();
 }
 
 // ---- arena regions of nested schemas (thrift_gpu.h tgpu_schema_arena_scale)
 // Every arena byte of a record is charged to wire bytes of its own: an
 // element's slot (scalar, span, struct, packed pair) to the element's own
 // bytes (a struct element's own bytes can be one STOP), a container's
-// allocation padding (<= 7) to its header. The region scale is the largest
-// bytes-per-wire-byte ratio any element kind of the schema reaches.
+// allocation padding (<= 7) to its header, a boxed struct's object (+ its
+// padding) to its field header and STOP. The region scale is the largest
+// bytes-per-wire-byte ratio any element kind of the schema reaches; every
+// container description (fields and type nodes) and every boxed field is
+// looked at once, so recursive schemas are covered.
 uint32_t min_wire(uint32_t t, bool compact) {
   switch (t) {
     case TGPU_T_BOOL: case TGPU_T_BYTE: return 1;
@@ -312,39 +415,46 @@ uint32_t min_wire(uint32_t t, bool compact) {
 }
 uint32_t slot_bytes(const Tables& T, uint32_t t, int32_t si) {
   if (t == TGPU_T_STRUCT) return T.s[si].size;
-  if (t == TGPU_T_STRING || t == TGPU_T_LIST || t == TGPU_T_SET || t == TGPU_T_MAP) return 16;
+  if (t == TGPU_T_STRING || is_container_t(t)) return 16;
   return scalar_size(t);
 }
-// arena bytes charged to one element of type t (+ padding of its own allocation)
-uint32_t charged(const Tables& T, uint32_t t, int32_t si) {
-  const bool cont = t == TGPU_T_LIST || t == TGPU_T_SET || t == TGPU_T_MAP;
-  return slot_bytes(T, t, si) + (cont ? 7 : 0);
+// the struct of a key type node (T_STRUCT node), else -1
+int32_t key_struct(const Tables& T, uint32_t elem, uint32_t ki) {
+  return (elem == TGPU_T_STRUCT && ki) ? T.t[ki - 1].struct_index : -1;
 }
 void region_ratio(const Tables& T, uint32_t ttype, uint32_t elem, uint32_t val, int32_t si,
-                  uint32_t ti, bool compact, double& ratio, uint32_t& slot) {
+                  uint32_t ki, bool compact, double& ratio, uint32_t& slot) {
+  if (!is_container_t(ttype)) return;
   const bool is_map = ttype == TGPU_T_MAP;
   const uint32_t v = is_map ? val : elem;
-  const uint32_t kb = is_map ? slot_bytes(T, elem, -1) : 0;
+  const uint32_t kb = is_map ? slot_bytes(T, elem, key_struct(T, elem, ki)) : 0;
   const uint32_t kw = is_map ? min_wire(elem, compact) : 0;
-  ratio = std::max(ratio, (double)(kb + charged(T, v, si)) / (double)(kw + min_wire(v, compact)));
+  // a pair's bytes + the padding of the containers its key and value open
+  const uint32_t pad = (is_container_t(v) ? 7 : 0) + (is_map && is_container_t(elem) ? 7 : 0);
+  ratio = std::max(ratio, (double)(kb + slot_bytes(T, v, si) + pad) /
+                              (double)(kw + min_wire(v, compact)));
   ratio = std::max(ratio, 7.0 / (double)min_wire(ttype, compact));  // this container's padding
-  if (v == TGPU_T_STRUCT || v == TGPU_T_LIST || v == TGPU_T_SET || v == TGPU_T_MAP)
+  if (is_complex_t(v) || (is_map && is_complex_t(elem)))
     slot = std::max(slot, kb + slot_bytes(T, v, si));
-  if (v == TGPU_T_LIST || v == TGPU_T_SET || v == TGPU_T_MAP) {
-    const tgpu_type_desc& n = T.t[ti - 1];
-    region_ratio(T, n.ttype, n.elem_ttype, n.val_ttype, n.struct_index, n.type_index, compact,
-                 ratio, slot);
-  }
 }
 void region_scale(const tgpu_schema& sc, bool compact, uint32_t& scale, uint32_t& slot) {
   const Tables T{sc.structs.data(), (uint32_t)sc.structs.size(), sc.fields.data(),
                  (uint32_t)sc.fields.size(), sc.types.data(), (uint32_t)sc.types.size()};
   double ratio = 8.0;
   slot = 16;
-  for (const tgpu_field_desc& f : sc.fields)
-    if (f.ttype == TGPU_T_LIST || f.ttype == TGPU_T_SET || f.ttype == TGPU_T_MAP)
-      region_ratio(T, f.ttype, f.elem_ttype, f.val_ttype, f.struct_index, f.type_index, compact,
-                   ratio, slot);
+  for (const tgpu_field_desc& f : sc.fields) {
+    region_ratio(T, f.ttype, f.elem_ttype, f.val_ttype, f.struct_index, f.key_index, compact,
+                 ratio, slot);
+    if (f.ttype == TGPU_T_STRUCT && is_boxed(f)) {
+      // field header (Binary 3, Compact >= 1) + the struct's STOP
+      const uint32_t sz = T.s[f.struct_index].size;
+      ratio = std::max(ratio, (double)(sz + 7) / (compact ? 2.0 : 4.0));
+      slot = std::max(slot, sz);
+    }
+  }
+  for (const tgpu_type_desc& n : sc.types)
+    region_ratio(T, n.ttype, n.elem_ttype, n.val_ttype, n.struct_index, n.key_index, compact,
+                 ratio, slot);
   scale = ((uint32_t)std::ceil(ratio) + 7) & ~7u;
   slot = (slot + 15) & ~15u;
 }
@@ -636,10 +746,13 @@ int ensure_workspace(tgpu_context* ctx, uint64_t n) {
   return TGPU_OK;
 }
 
-// Skip frames for the deep pass: max_depth + 2 frames per lane (the skip's
-// depth check fires first), up to kMaxDeepFrames; as many lanes (<= 256) as
-// fit 64 MiB. Deferred records are rare (a value nested past 16 levels), so
-// the pass's width only bounds its time, never its result.
+// Frames for the deep pass: max_depth + 2 skip frames and as many record
+// frames per lane (the skip's depth check fires first; records nest through
+// containers, each a level of depth, or through boxed fields, past which
+// the slab's record frames are the limit: TGPU_ERR_UNSUPPORTED), up to
+// kMaxDeepFrames; as many lanes (<= 256) as fit 64 MiB. Deferred records are
+// rare (a value nested past the private frames), so the pass's width only
+// bounds its time, never its result.
 int ensure_deep(tgpu_context* ctx, int32_t max_depth) {
   const uint64_t want = std::min<uint64_t>(std::max<int64_t>((int64_t)max_depth + 2, 1),
                                            kMaxDeepFrames);
@@ -648,9 +761,9 @@ int ensure_deep(tgpu_context* ctx, int32_t max_depth) {
   ctx->d_slabs = nullptr;
   ctx->slab_frames = 0;
   ctx->slab_lanes = 0;
-  const uint64_t frame = 12;  // sizeof(dev::SkipFrame)
-  const uint64_t lanes = std::min<uint64_t>(256, std::max<uint64_t>(1, (64ull << 20) / (want * frame)));
-  if (hipMalloc(&ctx->d_slabs, lanes * want * frame) != hipSuccess) return TGPU_ERR_HIP;
+  const uint64_t lane_bytes = slab_lane_bytes(want);
+  const uint64_t lanes = std::min<uint64_t>(256, std::max<uint64_t>(1, (64ull << 20) / lane_bytes));
+  if (hipMalloc(&ctx->d_slabs, lanes * lane_bytes) != hipSuccess) return TGPU_ERR_HIP;
   ctx->slab_frames = want;
   ctx->slab_lanes = (uint32_t)lanes;
   return TGPU_OK;
@@ -704,10 +817,11 @@ DevSchema dev_schema(const tgpu_schema* s, int protocol) {
 }
 
 // Scratch bytes per record of a measuring read (stream index): the root
-// record, then one element slot per nesting level.
+// record, then one element slot every nesting level shares (the measuring
+// reader only writes objects, never reads them back).
 uint64_t measure_scratch(const tgpu_schema* s) {
   const uint64_t root = (s->structs[0].size + 15) & ~15ull;
-  return root + (s->nested ? (uint64_t)kMaxSchemaDepth * s->nest_slot : 0);
+  return root + (s->nested ? (uint64_t)s->nest_slot : 0);
 }
 
 // Indexed decode (a.offs = record starts): compiled-program fast path, then
@@ -1317,10 +1431,12 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   } else {
     const uint64_t nb = (n + 255) / 256;
     int rc = ensure_workspace(ctx, n);
+    if (!rc) rc = ensure_deep(ctx, 12000);
     if (rc) {
       fill_status(st, rc, 0, 0);
       return rc;
     }
+    a.deep = deep_args(ctx);
     a.offs = out_offsets ? out_offsets : ctx->d_offs;
     a.block_sums = ctx->d_block_sums;
     a.scan_part = ctx->d_scan_part;
@@ -1362,11 +1478,13 @@ int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   }
   const hipStream_t s = (hipStream_t)stream;
   int rc = ensure_workspace(ctx, n);
+  if (!rc) rc = ensure_deep(ctx, 12000);
   if (rc) {
     fill_status(st, rc, 0, 0);
     return rc;
   }
   EncodeArgs a{};
+  a.deep = deep_args(ctx);
   a.sc = dev_schema(schema, protocol);
   a.recs = (const uint8_t*)records;
   a.n = n;

@@ -409,6 +409,7 @@ struct SkipFrame {
   int32_t last_or_remaining;
   int32_t depth;  // depth of the values inside this frame
 };
+static_assert(sizeof(SkipFrame) == kSkipFrameBytes, "slab layout (tgpu_internal.h)");
 
 // Frames live in the lane's private array, or all of them in the reader's
 // HBM slab when it has one (deep-pass lanes). Running out of private frames
@@ -545,13 +546,14 @@ struct CType {
   uint32_t ttype, elem, val;
   int32_t si;   // struct of the elements / values (T_STRUCT)
   uint32_t ti;  // 1 + type node of container elements / values
+  uint32_t ki;  // map: 1 + type node of a struct / container key
 };
 __device__ __forceinline__ CType ctype_of(const tgpu_field_desc& f) {
-  return CType{f.ttype, f.elem_ttype, f.val_ttype, f.struct_index, f.type_index};
+  return CType{f.ttype, f.elem_ttype, f.val_ttype, f.struct_index, f.type_index, f.key_index};
 }
 __device__ __forceinline__ CType ctype_node(const DevSchema& sc, uint32_t ti) {
   const tgpu_type_desc t = sc.t[ti - 1];
-  return CType{t.ttype, t.elem_ttype, t.val_ttype, t.struct_index, t.type_index};
+  return CType{t.ttype, t.elem_ttype, t.val_ttype, t.struct_index, t.type_index, t.key_index};
 }
 __device__ __forceinline__ bool is_container(uint32_t t) {
   return t == TGPU_T_LIST || t == TGPU_T_SET || t == TGPU_T_MAP;
@@ -579,7 +581,7 @@ struct Arena {
   uint64_t scale;
   uint64_t bump;    // next free offset (record regions)
   bool regions;
-  uint8_t* nest;    // measure only: slots, nest_slot bytes per frame depth
+  uint8_t* nest;    // measure only: the element slot every level shares
   uint32_t nest_slot;
   __device__ __forceinline__ bool discard() const { return !base && cap == kDiscardArena; }
   __device__ __forceinline__ uint64_t alloc(uint64_t first_elem_pos, uint64_t bytes) {
@@ -759,26 +761,38 @@ __device__ void read_map(Reader& r, const CType& c, uint8_t* m, Arena& A) {
 // The record reader: the generated readNoXfer (deserialize_struct.whisker:
 // 19-160) as an explicit frame machine. Frames: a struct being read field by
 // field; a list/set whose elements are structs or containers; a map whose
-// values are. Their element semantics are the reference's:
+// keys or values are. Their element semantics are the reference's:
 //   list  reserve + emplace_back_default + read (protocol_methods.h:374-386,
 //         458-461): the list holds the elements read plus the failing one;
 //   set   an element is inserted once read (EncodeHelpers.h:248-259);
 //   map   a pair is inserted once key and value are read (:188-205).
+// A boxed struct field (cpp.ref / thrift.box) is read into a fresh object in
+// the arena and pointed to once its read completed (deserialize_field.
+// whisker:21-23,49-51).
 enum : uint8_t { RF_STRUCT = 1, RF_LIST = 2, RF_MAP = 3 };
+// kphase of a list/map frame: the element / pair at i is
+enum : uint8_t { KP_NEXT = 0, KP_KEY_OPEN = 1, KP_VALUE = 2, KP_VALUE_OPEN = 3 };
 struct ReadFrame {
   uint8_t kind;
   uint8_t is_set;
   uint8_t etype;   // list: element type; map: value type
   uint8_t ktype;   // map: key type
-  int32_t prev;    // struct: Compact delta base
+  uint8_t kphase;  // list/map: KP_*
+  uint8_t pad_[3];
   int32_t si;      // struct: its index; list/map: struct of the elements / values
   uint32_t ti;     // list/map: type node of container elements / values
-  uint32_t fidx;   // struct: field whose struct / container value is open
-  uint32_t nread;  // struct: fields read or skipped (a union takes one)
-  uint64_t seen;   // struct: fields (index < 64) read by this read (required check)
-  uint32_t n, i;   // list/map: elements, elements done
-  uint32_t es, ks; // list/map: element (pair) stride in the arena, key bytes
   uint8_t* obj;    // struct: the object; list/map: element array
+  // struct
+  int32_t prev;      // Compact delta base
+  uint32_t fidx;     // field whose struct / container value is open
+  uint32_t nread;    // fields read or skipped (a union takes one)
+  uint32_t pad2_;
+  uint64_t seen;     // fields (index < 64) read by this read (required check)
+  // list/map
+  uint32_t n, i;     // elements, elements done
+  uint32_t es, ks;   // element (pair) stride in the arena, key bytes
+  int32_t ksi;       // map: struct of struct keys
+  uint32_t kti;      // map: type node of container keys
   uint8_t* span;   // list/map: the member / element span being filled
 };
 
@@ -787,30 +801,39 @@ __device__ __forceinline__ void set_span_len(uint8_t* m, uint8_t* arr, uint8_t* 
   *(tgpu_span*)m = sp;
 }
 
+__device__ __forceinline__ bool boxed(const tgpu_field_desc& f) {
+  return f.qualifier == TGPU_BOXED || f.qualifier == TGPU_OPTIONAL_BOXED;
+}
+
+// A list frame holding a boxed struct field's object (is_set value).
+constexpr uint8_t kBoxedFrame = 2;
+
 // Child value of frame p is complete (and the reader ok).
 __device__ __forceinline__ void child_done(const DevSchema& sc, ReadFrame& p, const Arena& A) {
   if (p.kind == RF_STRUCT) {
-    p.obj[sc.f[p.fidx].isset_offset] = 1;  // __isset.set(idx, true)
+    const tgpu_field_desc f = sc.f[p.fidx];
+    p.obj[f.isset_offset] = 1;  // __isset.set(idx, true)
     const uint32_t k = p.fidx - sc.s[p.si].first_field;
     if (k < 64) p.seen |= 1ull << k;
+  } else if (p.kphase == KP_KEY_OPEN) {
+    p.kphase = KP_VALUE;
   } else {
     ++p.i;
+    p.kphase = KP_NEXT;
     if (p.kind == RF_MAP || p.is_set) set_span_len(p.span, p.obj, A.base, p.i);
   }
 }
 
 // Opens the container value of type c at member / element slot m: simple
-// elements are read here (returns true: done), elements that are structs
-// or containers get a frame (returns false).
-// depth: frames open below this container's frame (its level for the
-// measuring reads' per-level slots).
+// elements are read here (returns true: done), elements, keys or values that
+// are structs or containers get a frame (returns false).
 template <int P>
 __device__ bool open_container(Reader& r, const DevSchema& sc, const CType& c, uint8_t* m,
-                               Arena& A, int depth, ReadFrame& f) {
+                               Arena& A, ReadFrame& f) {
   using Pr = Proto<P>;
   const bool is_map = c.ttype == TGPU_T_MAP;
   const uint32_t et = is_map ? c.val : c.elem;
-  if (!is_complex(et)) {
+  if (!is_complex(et) && !(is_map && is_complex(c.elem))) {
     if (is_map) read_map<P>(r, c, m, A);
     else read_list<P>(r, c, m, A);
     return true;
@@ -842,16 +865,18 @@ __device__ bool open_container(Reader& r, const DevSchema& sc, const CType& c, u
     r.ascend();
     return true;
   }
-  if (depth + 1 >= kMaxSchemaDepth) {
-    r.fail(TGPU_ERR_UNSUPPORTED, r.pos);
-    return true;
+  int32_t ksi = -1;
+  uint32_t kti = 0;
+  if (is_map && is_complex(c.elem)) {
+    if (c.elem == TGPU_T_STRUCT) ksi = sc.t[c.ki - 1].struct_index;
+    else kti = c.ki;
   }
-  const uint32_t ks = is_map ? elem_size(c.elem) : 0;
+  const uint32_t ks = is_map ? slot_size(sc, c.elem, ksi) : 0;
   const uint32_t es = ks + slot_size(sc, et, c.si);
   uint8_t* arr;
   uint32_t stride = es;
   if (A.discard()) {
-    arr = A.nest + (uint64_t)(depth + 1) * A.nest_slot;  // one reused slot per level
+    arr = A.nest;  // one slot every level reuses (the measuring reads only write)
     stride = 0;
   } else {
     if (!A.base) {
@@ -870,15 +895,45 @@ __device__ bool open_container(Reader& r, const DevSchema& sc, const CType& c, u
   f.is_set = c.ttype == TGPU_T_SET;
   f.etype = (uint8_t)et;
   f.ktype = (uint8_t)c.elem;
+  f.kphase = KP_NEXT;
   f.si = c.si;
   f.ti = c.ti;
   f.n = (uint32_t)n;
   f.i = 0;
   f.es = stride;
   f.ks = ks;
+  f.ksi = ksi;
+  f.kti = kti;
   f.obj = arr;
   f.span = m;
   return false;
+}
+
+__device__ __forceinline__ ReadFrame struct_frame(int32_t si, uint8_t* obj) {
+  ReadFrame f;
+  f.kind = RF_STRUCT;
+  f.is_set = 0;
+  f.etype = f.ktype = f.kphase = 0;
+  f.si = si;
+  f.ti = 0;
+  f.obj = obj;
+  f.prev = 0;
+  f.nread = 0;
+  f.fidx = 0;
+  f.pad2_ = 0;
+  f.seen = 0;
+  f.n = f.i = f.es = f.ks = f.kti = 0;
+  f.ksi = -1;
+  f.span = nullptr;
+  return f;
+}
+
+// The frames a reader keeps: kPrivFrames in the lane's private array, or (a
+// deep-pass lane, r.deep set) all of them in its HBM slab after its skip
+// frames. Running out of private frames is kErrDeep (the record is redone by
+// the deep pass), out of slab frames TGPU_ERR_UNSUPPORTED.
+__device__ __forceinline__ ReadFrame* slab_read_frames(const Reader& r) {
+  return (ReadFrame*)(r.deep + slab_skip_bytes(r.deep_cap));
 }
 
 // Reads one record into rec (zeroed by the caller). A.bump: the record's
@@ -886,56 +941,73 @@ __device__ bool open_container(Reader& r, const DevSchema& sc, const CType& c, u
 // frames below it are saved in `st` (sp of them) only while a child is open
 // (a per-iteration reload of the whole frame from scratch was the general
 // reader's main cost).
-__device__ __forceinline__ ReadFrame struct_frame(int32_t si, uint8_t* obj) {
-  ReadFrame f;
-  f.kind = RF_STRUCT;
-  f.is_set = 0;
-  f.etype = f.ktype = 0;
-  f.si = si;
-  f.obj = obj;
-  f.prev = 0;
-  f.nread = 0;
-  f.fidx = 0;
-  f.seen = 0;
-  f.ti = 0;
-  f.n = f.i = f.es = f.ks = 0;
-  f.span = nullptr;
-  return f;
-}
-
 template <int P>
 __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, Arena& A) {
   using Pr = Proto<P>;
-  ReadFrame st[kMaxSchemaDepth - 1];
-  int sp = 0;  // frames saved below fr
+  ReadFrame priv[kPrivFrames];
+  ReadFrame* const st = r.deep ? slab_read_frames(r) : priv;
+  const uint32_t cap = r.deep ? (uint32_t)r.deep_cap : (uint32_t)kPrivFrames;
+  const int32_t full = r.deep ? TGPU_ERR_UNSUPPORTED : kErrDeep;
+  uint32_t sp = 0;  // frames saved below fr
   ReadFrame fr = struct_frame(0, rec);
   while (r.ok()) {
     if (fr.kind != RF_STRUCT) {
-      if (fr.i == fr.n) {  // readListEnd / readMapEnd
-        r.ascend();
-        if (sp == 0) return;
-        fr = st[--sp];
+      uint8_t* val;
+      if (fr.kphase == KP_NEXT) {
+        if (fr.i == fr.n) {  // readListEnd / readMapEnd
+          if (fr.is_set != kBoxedFrame) r.ascend();
+          if (sp == 0) return;
+          fr = st[--sp];
+          child_done(sc, fr, A);
+          continue;
+        }
+        const uint32_t esz = fr.es ? fr.es : (fr.ks + slot_size(sc, fr.etype, fr.si));
+        uint8_t* el = fr.obj + (uint64_t)fr.i * fr.es;
+        zero_bytes(el, esz);  // a default-constructed element / pair
+        val = el;
+        if (fr.kind == RF_MAP) {
+          if (!is_complex(fr.ktype)) {
+            read_elem<P>(r, fr.ktype, el);
+            if (!r.ok()) break;
+          } else {  // a struct / container key: its own frame, the value after it
+            if (sp >= cap) return r.fail(full, r.pos);
+            fr.kphase = KP_KEY_OPEN;
+            if (fr.ktype == TGPU_T_STRUCT) {
+              st[sp++] = fr;
+              fr = struct_frame(fr.ksi, el);
+            } else {
+              ReadFrame nf;
+              if (open_container<P>(r, sc, ctype_node(sc, fr.kti), el, A, nf)) {
+                if (r.ok()) child_done(sc, fr, A);
+              } else {
+                st[sp++] = fr;
+                fr = nf;
+              }
+            }
+            continue;
+          }
+          val = el + fr.ks;
+        } else if (!fr.is_set) {
+          set_span_len(fr.span, fr.obj, A.base, fr.i + 1);  // emplace_back_default
+        }
+      } else {  // KP_VALUE: the key of pair i is read
+        val = fr.obj + (uint64_t)fr.i * fr.es + fr.ks;
+      }
+      if (!is_complex(fr.etype)) {  // (a map with a struct / container key)
+        read_elem<P>(r, fr.etype, val);
+        if (!r.ok()) break;
+        fr.kphase = KP_VALUE_OPEN;
         child_done(sc, fr, A);
         continue;
       }
-      const uint32_t esz = fr.es ? fr.es : (fr.ks + slot_size(sc, fr.etype, fr.si));
-      uint8_t* el = fr.obj + (uint64_t)fr.i * fr.es;
-      zero_bytes(el, esz);  // a default-constructed element / pair
-      uint8_t* val = el;
-      if (fr.kind == RF_MAP) {
-        read_elem<P>(r, fr.ktype, el);
-        if (!r.ok()) break;
-        val = el + fr.ks;
-      } else if (!fr.is_set) {
-        set_span_len(fr.span, fr.obj, A.base, fr.i + 1);  // emplace_back_default
-      }
+      if (sp >= cap) return r.fail(full, r.pos);
+      fr.kphase = KP_VALUE_OPEN;
       if (fr.etype == TGPU_T_STRUCT) {
-        if (sp + 1 >= kMaxSchemaDepth) return r.fail(TGPU_ERR_UNSUPPORTED, r.pos);
         st[sp++] = fr;
         fr = struct_frame(fr.si, val);
       } else {
         ReadFrame nf;
-        if (open_container<P>(r, sc, ctype_node(sc, fr.ti), val, A, sp, nf)) {
+        if (open_container<P>(r, sc, ctype_node(sc, fr.ti), val, A, nf)) {
           if (r.ok()) child_done(sc, fr, A);
         } else {
           st[sp++] = fr;
@@ -1004,13 +1076,45 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, Arena&
       Pr::read_string(r, v, l);
       if (r.ok()) *(tgpu_span*)m = tgpu_span{l ? v : 0, l, 0};
     } else if (f.ttype == TGPU_T_STRUCT) {
-      if (sp + 1 >= kMaxSchemaDepth) return r.fail(TGPU_ERR_UNSUPPORTED, r.pos);
+      if (sp >= cap) return r.fail(full, r.pos);
       st[sp++] = fr;
+      if (boxed(f)) {
+        // make_mutable_smart_ptr: a fresh object in the arena, read as the
+        // one element of a frame that points the member to it once read (a
+        // set's insert-after-read; no list header, so no height)
+        const uint32_t size = sc.s[f.struct_index].size;
+        uint8_t* obj;
+        if (A.discard()) {
+          obj = A.nest;
+        } else {
+          if (!A.base) return r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
+          const uint64_t aoff = A.alloc(r.pos, size);
+          if (aoff + size > A.cap) return r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
+          obj = A.base + aoff;
+        }
+        fr.kind = RF_LIST;
+        fr.is_set = kBoxedFrame;
+        fr.etype = TGPU_T_STRUCT;
+        fr.ktype = 0;
+        fr.kphase = KP_NEXT;
+        fr.si = f.struct_index;
+        fr.ti = 0;
+        fr.obj = obj;
+        fr.n = 1;
+        fr.i = 0;
+        fr.es = A.discard() ? 0 : size;
+        fr.ks = 0;
+        fr.ksi = -1;
+        fr.kti = 0;
+        fr.span = m;
+        continue;
+      }
       fr = struct_frame(f.struct_index, m);
       continue;  // isset set when the nested STOP is reached
     } else {
+      if (sp >= cap) return r.fail(full, r.pos);
       ReadFrame nf;
-      if (!open_container<P>(r, sc, ctype_of(f), m, A, sp, nf)) {
+      if (!open_container<P>(r, sc, ctype_of(f), m, A, nf)) {
         st[sp++] = fr;
         fr = nf;
         continue;
@@ -1045,7 +1149,7 @@ __device__ __forceinline__ Arena record_arena(const DevSchema& sc, uint8_t* base
 // Lane `lane`'s HBM skip frames (DeepArgs), attached to a reader.
 __device__ __forceinline__ void attach_slab(Reader& r, const DeepArgs& d, uint32_t lane) {
   if (!d.slabs) return;
-  r.deep = d.slabs + (uint64_t)lane * d.slab_frames * sizeof(SkipFrame);
+  r.deep = d.slabs + (uint64_t)lane * slab_lane_bytes(d.slab_frames);
   r.deep_cap = d.slab_frames;
 }
 
@@ -1103,6 +1207,10 @@ struct Writer {
   uint64_t pos, cap;
   int32_t err;
   uint64_t err_off;
+  // record frames past the private kPrivFrames (nullptr: kErrDeep instead):
+  // a deep-pass lane's HBM slab (the reader's layout)
+  uint8_t* deep = nullptr;
+  uint64_t deep_cap = 0;
   __device__ __forceinline__ bool ok() const { return err == 0; }
   __device__ __forceinline__ void fail(int32_t code, uint64_t off) {
     if (!err) {
@@ -1195,15 +1303,17 @@ __device__ __forceinline__ bool terse_leaf_empty(const tgpu_field_desc& f, const
 
 // thrift::empty of struct si at obj — the generated __fbthrift_is_empty
 // (module_types_cpp/declare_members.whisker:83-113): never empty with an
-// unqualified or required field; otherwise empty when no optional field is
-// set and every terse field is empty (terse structs recursively); a union
-// (union_declare_members.whisker:43-45) when no member is active. The walk
-// keeps one (struct, object, next field) per nesting level.
+// unqualified, required or boxed-unqualified field; otherwise empty when no
+// optional field is set and every terse field is empty (terse structs
+// recursively); a union (union_declare_members.whisker:43-45) when no member
+// is active. The walk keeps one (struct, object, next field) per terse
+// struct level (schemas nest those at most kMaxTerseDepth deep).
+constexpr int kMaxTerseDepth = 16;
 __device__ bool struct_empty(const DevSchema& sc, uint32_t si, const uint8_t* obj) {
   struct Lvl {
     uint32_t si, k;
     const uint8_t* obj;
-  } st[kMaxSchemaDepth];
+  } st[kMaxTerseDepth + 1];
   int sp = 0;
   st[0] = Lvl{si, 0, obj};
   for (;;) {
@@ -1219,14 +1329,16 @@ __device__ bool struct_empty(const DevSchema& sc, uint32_t si, const uint8_t* ob
       if (L.obj[f.isset_offset]) return false;
       continue;
     }
-    if (f.qualifier == TGPU_UNQUALIFIED || f.qualifier == TGPU_REQUIRED) return false;
-    if (f.qualifier == TGPU_OPTIONAL) {
+    if (f.qualifier == TGPU_UNQUALIFIED || f.qualifier == TGPU_REQUIRED ||
+        f.qualifier == TGPU_BOXED)
+      return false;
+    if (f.qualifier == TGPU_OPTIONAL || f.qualifier == TGPU_OPTIONAL_BOXED) {
       if (L.obj[f.isset_offset]) return false;
       continue;
     }
     const uint8_t* m = L.obj + f.member_offset;  // terse
     if (f.ttype == TGPU_T_STRUCT) {
-      if (sp + 1 >= kMaxSchemaDepth) return false;  // (schemas nest at most that deep)
+      if (sp >= kMaxTerseDepth) return false;  // (validated: never reached)
       st[++sp] = Lvl{(uint32_t)f.struct_index, 0, m};
       continue;
     }
@@ -1242,20 +1354,22 @@ __device__ __forceinline__ bool terse_empty(const DevSchema& sc, const tgpu_fiel
 
 // The record writer: the generated write (serialize_struct.whisker:40-67,
 // serialize_field.whisker:17-71) as an explicit frame machine — a struct's
-// fields in declaration order, and lists/sets/maps whose elements or values
-// are structs or containers element by element.
+// fields in declaration order, and lists/sets/maps whose elements, keys or
+// values are structs or containers element by element.
 enum : uint8_t { WF_STRUCT = 1, WF_LIST = 2, WF_MAP = 3 };
 struct WriteFrame {
   uint8_t kind;
-  uint8_t etype;  // list: element type; map: value type
-  uint8_t ktype;  // map: key type
-  uint8_t pad;
-  uint32_t si;    // struct: its index; list/map: struct of the elements / values
-  uint32_t ti;    // list/map: type node of container elements / values
-  uint32_t k;     // struct: next field index; list/map: next element
-  int32_t last;   // struct: Compact lastFieldId_
-  uint32_t end;   // struct: one past the last field to write; list/map: elements
+  uint8_t etype;   // list: element type; map: value type
+  uint8_t ktype;   // map: key type
+  uint8_t kphase;  // list/map: 0 = element k next, 1 = its value next (key written)
+  uint32_t si;     // struct: its index; list/map: struct of the elements / values
+  uint32_t ti;     // list/map: type node of container elements / values
+  uint32_t k;      // struct: next field index; list/map: next element
+  int32_t last;    // struct: Compact lastFieldId_
+  uint32_t end;    // struct: one past the last field to write; list/map: elements
   uint32_t es, ks;
+  int32_t ksi;     // map: struct of struct keys
+  uint32_t kti;    // map: type node of container keys
   const uint8_t* obj;
 };
 
@@ -1312,12 +1426,12 @@ __device__ __forceinline__ void container_header(Writer& w, const CType& c, uint
 }
 
 // Writes the container value of type c held in span member m: simple
-// elements here (returns true), structs / containers as elements get a
-// frame (returns false).
+// elements here (returns true), a container whose elements, keys or values
+// are structs / containers gets a frame (returns false).
 template <int P>
 __device__ bool write_container(Writer& w, const DevSchema& sc, const CType& c,
                                 const uint8_t* m, const uint8_t* sbase, const uint8_t* lbase,
-                                WriteFrame* st, int& sp) {
+                                WriteFrame* st, uint32_t& sp, uint32_t cap, int32_t full) {
   const tgpu_span sp_ = *(const tgpu_span*)m;
   // checked_container_size: > INT32_MAX -> SIZE_LIMIT
   if (sp_.length > 0x7fffffffu) {
@@ -1327,9 +1441,9 @@ __device__ bool write_container(Writer& w, const DevSchema& sc, const CType& c,
   container_header<P>(w, c, sp_.length);
   const bool is_map = c.ttype == TGPU_T_MAP;
   const uint32_t et = is_map ? c.val : c.elem;
-  const uint32_t ks = is_map ? elem_size(c.elem) : 0;
   const uint8_t* e = lbase + sp_.offset;
-  if (!is_complex(et)) {
+  if (!is_complex(et) && !(is_map && is_complex(c.elem))) {
+    const uint32_t ks = is_map ? elem_size(c.elem) : 0;
     const uint32_t ps = ks + elem_size(et);
     for (uint32_t i = 0; i < sp_.length && w.ok(); ++i) {
       if (is_map) write_elem<P>(w, c.elem, e + (uint64_t)i * ps, sbase);
@@ -1338,9 +1452,15 @@ __device__ bool write_container(Writer& w, const DevSchema& sc, const CType& c,
     return true;
   }
   if (sp_.length == 0) return true;
-  if (sp == kMaxSchemaDepth) {
-    w.fail(TGPU_ERR_UNSUPPORTED, w.pos);
+  if (sp >= cap) {
+    w.fail(full, w.pos);
     return true;
+  }
+  int32_t ksi = -1;
+  uint32_t kti = 0;
+  if (is_map && is_complex(c.elem)) {
+    if (c.elem == TGPU_T_STRUCT) ksi = sc.t[c.ki - 1].struct_index;
+    else kti = c.ki;
   }
   WriteFrame& f = st[sp++];
   f = WriteFrame{};
@@ -1351,37 +1471,66 @@ __device__ bool write_container(Writer& w, const DevSchema& sc, const CType& c,
   f.ti = c.ti;
   f.k = 0;
   f.end = sp_.length;
-  f.ks = ks;
-  f.es = ks + slot_size(sc, et, c.si);
+  f.ks = is_map ? slot_size(sc, c.elem, ksi) : 0;
+  f.es = f.ks + slot_size(sc, et, c.si);
+  f.ksi = ksi;
+  f.kti = kti;
   f.obj = e;
   return false;
+}
+
+// A struct / container value of type t at p (struct si, node ti): a frame
+// (or, for a container of simple elements, written here).
+template <int P>
+__device__ __forceinline__ void write_complex(Writer& w, const DevSchema& sc, uint32_t t,
+                                              int32_t si, uint32_t ti, const uint8_t* p,
+                                              const uint8_t* sbase, const uint8_t* lbase,
+                                              WriteFrame* st, uint32_t& sp, uint32_t cap,
+                                              int32_t full) {
+  if (t == TGPU_T_STRUCT) {
+    if (sp >= cap) return w.fail(full, w.pos);
+    st[sp++] = write_frame(sc, (uint32_t)si, p);
+  } else {
+    write_container<P>(w, sc, ctype_node(sc, ti), p, sbase, lbase, st, sp, cap, full);
+  }
 }
 
 template <int P>
 __device__ void write_record(Writer& w, const DevSchema& sc, const uint8_t* rec,
                              const uint8_t* sbase, const uint8_t* lbase) {
-  WriteFrame st[kMaxSchemaDepth];
-  int sp = 0;
+  WriteFrame priv[kPrivFrames];
+  WriteFrame* const st = w.deep ? (WriteFrame*)(w.deep + slab_skip_bytes(w.deep_cap)) : priv;
+  const uint32_t cap = w.deep ? (uint32_t)w.deep_cap : (uint32_t)kPrivFrames;
+  const int32_t full = w.deep ? TGPU_ERR_UNSUPPORTED : kErrDeep;
+  uint32_t sp = 0;
   st[sp++] = write_frame(sc, 0, rec);
   while (sp > 0 && w.ok()) {
     WriteFrame& fr = st[sp - 1];
     if (fr.kind != WF_STRUCT) {
-      if (fr.k >= fr.end) {  // lists and maps have no end marker on the wire
-        --sp;
-        continue;
+      if (fr.kphase == 0) {
+        if (fr.k >= fr.end) {  // lists and maps have no end marker on the wire
+          --sp;
+          continue;
+        }
+        fr.kphase = 1;
+        if (fr.kind == WF_MAP) {
+          const uint8_t* key = fr.obj + (uint64_t)fr.k * fr.es;
+          if (!is_complex(fr.ktype)) {
+            write_elem<P>(w, fr.ktype, key, sbase);
+            if (!w.ok()) break;
+          } else {  // the key's frame first; its value when the frame is done
+            const uint32_t before = sp;
+            write_complex<P>(w, sc, fr.ktype, fr.ksi, fr.kti, key, sbase, lbase, st, sp, cap,
+                             full);
+            if (sp != before) continue;
+          }
+        }
       }
-      const uint8_t* el = fr.obj + (uint64_t)fr.k++ * fr.es;
-      if (fr.kind == WF_MAP) {
-        write_elem<P>(w, fr.ktype, el, sbase);
-        if (!w.ok()) break;
-        el += fr.ks;
-      }
-      if (fr.etype == TGPU_T_STRUCT) {
-        if (sp == kMaxSchemaDepth) return w.fail(TGPU_ERR_UNSUPPORTED, w.pos);
-        st[sp++] = write_frame(sc, fr.si, el);
-      } else {
-        write_container<P>(w, sc, ctype_node(sc, fr.ti), el, sbase, lbase, st, sp);
-      }
+      const uint8_t* el = fr.obj + (uint64_t)fr.k++ * fr.es + fr.ks;
+      fr.kphase = 0;
+      if (!is_complex(fr.etype)) write_elem<P>(w, fr.etype, el, sbase);
+      else write_complex<P>(w, sc, fr.etype, (int32_t)fr.si, fr.ti, el, sbase, lbase, st, sp, cap,
+                            full);
       continue;
     }
     const tgpu_struct_desc sd = sc.s[fr.si];
@@ -1392,7 +1541,9 @@ __device__ void write_record(Writer& w, const DevSchema& sc, const uint8_t* rec,
     }
     const tgpu_field_desc f = sc.f[sd.first_field + fr.k++];
     const uint8_t* obj = fr.obj;
-    if (f.qualifier == TGPU_OPTIONAL && !obj[f.isset_offset]) continue;
+    if ((f.qualifier == TGPU_OPTIONAL || f.qualifier == TGPU_OPTIONAL_BOXED) &&
+        !obj[f.isset_offset])
+      continue;
     const uint8_t* m = obj + f.member_offset;
     if (f.qualifier == TGPU_TERSE && terse_empty(sc, f, m)) continue;
     if (P == TGPU_PROTOCOL_BINARY) {
@@ -1420,10 +1571,19 @@ __device__ void write_record(Writer& w, const DevSchema& sc, const uint8_t* rec,
       else w.varint(sp_.length);
       w.bytes(sbase + sp_.offset, sp_.length);
     } else if (f.ttype == TGPU_T_STRUCT) {
-      if (sp == kMaxSchemaDepth) return w.fail(TGPU_ERR_UNSUPPORTED, w.pos);
-      st[sp++] = write_frame(sc, (uint32_t)f.struct_index, m);
+      const uint8_t* p = m;
+      if (boxed(f)) {
+        const tgpu_span b = *(const tgpu_span*)m;
+        if (b.length == 0) {  // a null pointer: an empty struct (serialize_field.whisker:44-49)
+          w.put(0);
+          continue;
+        }
+        p = lbase + b.offset;
+      }
+      if (sp >= cap) return w.fail(full, w.pos);
+      st[sp++] = write_frame(sc, (uint32_t)f.struct_index, p);
     } else {
-      write_container<P>(w, sc, ctype_of(f), m, sbase, lbase, st, sp);
+      write_container<P>(w, sc, ctype_of(f), m, sbase, lbase, st, sp, cap, full);
     }
   }
 }

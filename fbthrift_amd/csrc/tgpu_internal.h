@@ -50,8 +50,23 @@ constexpr int kBlock = 256;
 constexpr uint32_t kMaxFixedWire = 192;
 constexpr uint32_t kMaxFixedRecord = 160;
 constexpr int kMaxTemplateItems = 96;
-// Nesting supported by the general device reader/writer.
-constexpr int kMaxSchemaDepth = 8;
+// Record frames (struct / container levels) the general reader and writer
+// keep per lane privately. A record nested deeper is not an error: the lane
+// reports kErrDeep and the record is redone by a deep pass whose lanes keep
+// their frames in HBM (DeepArgs), so records nest as deep as the data does
+// (recursive schemas) up to the slab's frames.
+constexpr int kPrivFrames = 8;
+// HBM slab of one deep-pass lane: slab_frames skip frames (12 bytes each,
+// rounded up to 16 bytes in all), then slab_frames record frames of at most
+// kRecordFrameBytes (dev::ReadFrame / dev::WriteFrame).
+constexpr uint64_t kSkipFrameBytes = 12;
+constexpr uint64_t kRecordFrameBytes = 80;
+constexpr uint64_t slab_skip_bytes(uint64_t frames) {
+  return (frames * kSkipFrameBytes + 15) & ~15ull;
+}
+constexpr uint64_t slab_lane_bytes(uint64_t frames) {
+  return slab_skip_bytes(frames) + frames * kRecordFrameBytes;
+}
 // Skip frames a lane keeps privately. A value nested deeper is not an error:
 // the lane reports kErrDeep and its record (or index chunk) is redone by a
 // deep pass whose lanes keep max_depth frames in HBM (DeepArgs), so the skip
@@ -65,7 +80,7 @@ constexpr uint64_t kMaxDeepFrames = 1ull << 22;
 struct DeepArgs {
   uint64_t* list;               // deferred records (or index chunks)
   unsigned long long* count;    // entries in list
-  uint8_t* slabs;               // lanes x slab_frames skip frames (dev::SkipFrame)
+  uint8_t* slabs;               // lanes x slab_lane_bytes(slab_frames)
   uint64_t slab_frames;
   uint32_t lanes;
   uint32_t pad;
@@ -261,6 +276,9 @@ struct EncodeArgs {
   uint64_t fixed_len;  // program write of a fixed-layout schema: record i at i * fixed_len
   uint32_t recompute;  // compiled write pass sizes its records; the size pass writes tile sums only
   uint32_t out_cap;    // write pass: LDS output tile bytes (0: prog::kOutCap)
+  // general encode: records nested past the private frames (kErrDeep) are
+  // sized and written again by deep-pass lanes with HBM frames
+  DeepArgs deep;
 };
 
 // ---- stream indexer (k_index.hip) -------------------------------------------

@@ -23,17 +23,23 @@ SPAN = np.dtype([("offset", "<u8"), ("length", "<u4"), ("reserved", "<u4")])
 OPTIONAL = 1
 TERSE = 2  # @thrift.TerseWrite: written only when not empty (op::isEmpty)
 REQUIRED = 3  # `required`: always written; enforced on read with Struct(enforce_required)
+# cpp.ref / @thrift.Box struct fields: the member is a pointer (a span into the
+# list arena / list_base; length 1 = present). BOXED is always written (a
+# null one as an empty struct), OPTIONAL_BOXED when its isset byte is set.
+BOXED = 4
+OPTIONAL_BOXED = 5
 
 
 class Type:
-    """A container type held by a container (a list/set element or a map
-    value that is itself a list, set or map): tgpu_type_desc. `struct` is
-    the struct of T_STRUCT elements / values, `inner` the Type of container
-    elements / values."""
+    """A container type held by a container (a list/set element, a map value
+    or a map key that is itself a list, set or map): tgpu_type_desc. `struct`
+    is the struct of T_STRUCT elements / values, `inner` the Type of
+    container elements / values, `key` the Type of a map's struct or
+    container key (a struct key: Type(T_STRUCT, 0, struct=S))."""
 
-    def __init__(self, ttype, elem_ttype, val_ttype=0, struct=None, inner=None):
+    def __init__(self, ttype, elem_ttype=0, val_ttype=0, struct=None, inner=None, key=None):
         self.ttype, self.elem_ttype, self.val_ttype = int(ttype), int(elem_ttype), int(val_ttype)
-        self.struct, self.inner = struct, inner
+        self.struct, self.inner, self.key = struct, inner, key
 
 
 class Field:
@@ -43,12 +49,14 @@ class Field:
     elements / values."""
 
     def __init__(self, id, ttype, elem_ttype=0, optional=False, struct=None, name=None,
-                 qualifier=None, val_ttype=0, inner=None):
+                 qualifier=None, val_ttype=0, inner=None, key=None):
         self.id, self.ttype, self.elem_ttype = int(id), int(ttype), int(elem_ttype)
         self.val_ttype = int(val_ttype)  # T_MAP: value type (elem_ttype = key type)
         self.qualifier = int(qualifier) if qualifier is not None else (OPTIONAL if optional else 0)
         self.optional, self.struct = self.qualifier == OPTIONAL, struct
         self.inner = inner
+        self.key = key  # T_MAP with a struct / container key: its Type
+        self.boxed = self.qualifier in (BOXED, OPTIONAL_BOXED)
         self.name = name or "f%d" % self.id
 
 
@@ -77,15 +85,24 @@ class Schema:
 
         self.types, tindex = [], {}
 
+        def visit_type(t):
+            if id(t) in tindex:
+                return
+            tindex[id(t)] = len(self.types)
+            self.types.append(t)
+            if t.ttype == T_STRUCT:
+                visit(t.struct)
+            else:
+                visit_container(t)
+
         def visit_container(t):
             es = element_struct(t)
             if es is not None:
                 visit(es)
+            if getattr(t, "key", None) is not None:
+                visit_type(t.key)
             if t.inner is not None:
-                if id(t.inner) not in tindex:
-                    tindex[id(t.inner)] = len(self.types)
-                    self.types.append(t.inner)
-                visit_container(t.inner)
+                visit_type(t.inner)
 
         def visit(s):
             if id(s) in index:
@@ -117,7 +134,7 @@ class Schema:
             for k, f in enumerate(s.fields):
                 if f.ttype in SCALAR:
                     sz = al = SCALAR[f.ttype]
-                elif f.ttype in (T_STRING, T_LIST, T_SET, T_MAP):
+                elif f.ttype in (T_STRING, T_LIST, T_SET, T_MAP) or f.boxed:
                     sz, al = 16, 8
                 elif f.ttype == T_STRUCT:
                     sub = self._index[id(f.struct)]
@@ -161,6 +178,7 @@ class Schema:
                 fd.isset_offset = self.isset[(si, k)]
                 fd.struct_index = self._struct_ref(f)
                 fd.type_index = self._type_ref(f)
+                fd.key_index = self._key_ref(f)
                 j += 1
         return structs, len(self.structs), fields, nf
 
@@ -172,24 +190,32 @@ class Schema:
     def _type_ref(self, t):
         return 1 + self._tindex[id(t.inner)] if getattr(t, "inner", None) is not None else 0
 
+    def _key_ref(self, t):
+        return 1 + self._tindex[id(t.key)] if getattr(t, "key", None) is not None else 0
+
     def type_descriptors(self):
         """The nested container types (tgpu_type_desc[]) for
         tgpu_schema_create_ex: (array, count)."""
         types = (_lib.TypeDesc * max(len(self.types), 1))()
         for k, t in enumerate(self.types):
             types[k].ttype, types[k].elem_ttype, types[k].val_ttype = t.ttype, t.elem_ttype, t.val_ttype
-            types[k].struct_index = self._struct_ref(t)
+            types[k].struct_index = (self._index[id(t.struct)] if t.ttype == T_STRUCT
+                                     else self._struct_ref(t))
             types[k].type_index = self._type_ref(t)
+            types[k].key_index = self._key_ref(t)
         return types, len(self.types)
 
     @property
     def nested(self):
-        """Some container holds structs or containers (arena record regions)."""
+        """Some container holds structs or containers (as elements, values
+        or keys), or a field is boxed (arena record regions)."""
+        cx = (T_STRUCT, T_LIST, T_SET, T_MAP)
+
         def complex_(t):
             v = t.val_ttype if t.ttype == T_MAP else t.elem_ttype
-            return v in (T_STRUCT, T_LIST, T_SET, T_MAP)
-        return any(complex_(f) for s in self.structs for f in s.fields
-                   if f.ttype in (T_LIST, T_SET, T_MAP))
+            return v in cx or (t.ttype == T_MAP and t.elem_ttype in cx)
+        return any((f.ttype in (T_LIST, T_SET, T_MAP) and complex_(f)) or f.boxed
+                   for s in self.structs for f in s.fields)
 
     # -- numpy view of the record layout -------------------------------------
     def dtype(self, si=0):
@@ -199,7 +225,7 @@ class Schema:
             names.append(f.name)
             if f.ttype in SCALAR:
                 formats.append(NP_SCALAR[f.ttype])
-            elif f.ttype in (T_STRING, T_LIST, T_SET, T_MAP):
+            elif f.ttype in (T_STRING, T_LIST, T_SET, T_MAP) or f.boxed:
                 formats.append(SPAN)
             else:
                 formats.append(self.dtype(self._index[id(f.struct)]))
@@ -219,9 +245,12 @@ class Schema:
         """Builds a Schema from the tests/golden manifest form: a list of
         structs, each a list of [id, ttype, elem_ttype, qualifier, struct_index]
         (+ val_ttype for a map, + the nested container type of the elements /
-        values as [ttype, elem_ttype, val_ttype, struct_index, nested]); a
-        union is {"union": true, "fields": [...]}. struct_index names the
-        struct of a T_STRUCT field or of T_STRUCT elements / values."""
+        values as [ttype, elem_ttype, val_ttype, struct_index, nested, key],
+        + a map's struct / container key type in that form, a struct key as
+        [T_STRUCT, 0, 0, struct_index]); a union is {"union": true,
+        "fields": [...]}. struct_index names the struct of a T_STRUCT field
+        or of T_STRUCT elements / values. Structs may refer to each other
+        recursively (through containers or BOXED / OPTIONAL_BOXED fields)."""
         structs = [Struct("S%d" % i, [], union=isinstance(e, dict) and e.get("union"),
                           enforce_required=isinstance(e, dict) and e.get("enforce_required"))
                    for i, e in enumerate(table)]
@@ -231,7 +260,8 @@ class Schema:
                 return None
             tt, et, vt, sub = spec[:4]
             return Type(tt, et, vt, struct=structs[sub] if sub is not None and sub >= 0 else None,
-                        inner=typ(spec[4] if len(spec) > 4 else None))
+                        inner=typ(spec[4] if len(spec) > 4 else None),
+                        key=typ(spec[5] if len(spec) > 5 else None))
 
         for si, e in enumerate(table):
             for row in (e["fields"] if isinstance(e, dict) else e):
@@ -240,7 +270,8 @@ class Schema:
                     Field(fid, tt, et, qualifier=q,
                           struct=structs[sub] if sub is not None and sub >= 0 else None,
                           val_ttype=row[5] if len(row) > 5 else 0,
-                          inner=typ(row[6] if len(row) > 6 else None)))
+                          inner=typ(row[6] if len(row) > 6 else None),
+                          key=typ(row[7] if len(row) > 7 else None)))
         return cls(structs[0])
 
 

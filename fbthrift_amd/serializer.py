@@ -101,7 +101,8 @@ class GpuSchema:
             raise TgpuError("tgpu_schema_create: %s" % _lib.CODES.get(rc, rc))
         self.handle = h
         self.record_size = _lib.lib().tgpu_schema_record_size(h)
-        self.has_lists = any(f.ttype in (_lib.T_LIST, _lib.T_SET, _lib.T_MAP)
+        # containers and boxed struct fields keep their contents in the arena
+        self.has_lists = any(f.ttype in (_lib.T_LIST, _lib.T_SET, _lib.T_MAP) or f.boxed
                              for s in schema.structs for f in s.fields)
 
     def fixed_wire_size(self, protocol):

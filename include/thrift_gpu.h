@@ -110,6 +110,19 @@ enum tgpu_qualifier {
      did not see the field fails with TGPU_ERR_MISSING_REQUIRED_FIELD
      (deserialize_struct.whisker:116-124). Its isset byte records the read. */
   TGPU_REQUIRED = 3,
+  /* A boxed struct field: cpp.ref / @cpp.Ref (std::unique_ptr<T>) or
+     @thrift.Box (thrift::box<T>), the form recursive structs take
+     (struct Node { 2: optional Node next (cpp.ref) }). The member is a
+     tgpu_span pointing at the struct's object in the list arena (decode)
+     or relative to list_base (encode): length 1 = present, 0 = null.
+     Read: a fresh object is read and assigned once its read completed
+     (deserialize_field.whisker:21-23,49-51: make_mutable_smart_ptr, read,
+     move). Write (serialize_field.whisker:32-50): TGPU_BOXED is always
+     written, a null one as an empty struct (writeStructBegin,
+     writeFieldStop, writeStructEnd); TGPU_OPTIONAL_BOXED only when its
+     isset byte is set (a null one then also as an empty struct). */
+  TGPU_BOXED = 4,
+  TGPU_OPTIONAL_BOXED = 5,
 };
 
 /*
@@ -118,8 +131,8 @@ enum tgpu_qualifier {
  *   ttype        T_BOOL..T_FLOAT scalar, T_STRING (binary/string), T_STRUCT,
  *                T_LIST or T_SET, T_MAP.
  *   elem_ttype   element type for T_LIST/T_SET, key type for T_MAP, else 0.
- *                A list/set element may be a scalar, a string, a struct or
- *                itself a list/set/map; a map key is a scalar or a string.
+ *                A list/set element, a map key and a map value may each be
+ *                a scalar, a string, a struct or itself a list/set/map.
  *   val_ttype    value type for T_MAP (any type, like a list element), else 0.
  * A string inside a container is a tgpu_span (like a string field); the
  * list arena then needs tgpu_schema_arena_scale bytes per input byte.
@@ -129,6 +142,15 @@ enum tgpu_qualifier {
  *   type_index   1 + index into the schema's type table (tgpu_type_desc,
  *                tgpu_schema_create_ex) of the container that is this
  *                list/set's element or this map's value type; 0 otherwise.
+ *   key_index    T_MAP whose key is a struct or a container: 1 + index into
+ *                the type table of the key's type (a node of ttype T_STRUCT
+ *                naming the struct, or the key container's node); else 0.
+ * Structs may be recursive through containers (struct Tree
+ * { 1: list<Tree> kids }) and through boxed fields; a struct cannot hold
+ * itself by value. Records nest as deep as the data does: the device reader
+ * and writer keep a few frames per lane and redo deeper records in a pass
+ * whose lanes keep their frames in HBM (tgpu_limits.max_depth bounds the
+ * containers, as the reference's descend/ascend does).
  * Containers hold their elements in the list arena: scalars in native
  * layout, strings and containers as tgpu_span, structs in the struct layout;
  * a map holds packed {key, value} pairs. This is the shape of the
@@ -142,7 +164,7 @@ typedef struct tgpu_field_desc {
   uint8_t elem_ttype;
   uint8_t qualifier;
   uint8_t val_ttype;
-  uint8_t reserved0[2];
+  uint16_t key_index;
   uint32_t member_offset;
   uint32_t isset_offset;
   int32_t struct_index;
@@ -152,17 +174,19 @@ typedef struct tgpu_field_desc {
 /*
  * A container type nested inside a container (list<list<i32>>,
  * map<string, list<Struct>>, ...): the same description a container field
- * carries (elem_ttype / val_ttype / struct_index / type_index as in
- * tgpu_field_desc), for a list/set element or a map value.
+ * carries (elem_ttype / val_ttype / struct_index / type_index / key_index as
+ * in tgpu_field_desc), for a list/set element, a map value or a map key.
+ * A map key that is a struct is a node of ttype T_STRUCT whose struct_index
+ * names the struct (referenced only through key_index).
  */
 typedef struct tgpu_type_desc {
-  uint8_t ttype;      /* T_LIST, T_SET or T_MAP */
+  uint8_t ttype;      /* T_LIST, T_SET or T_MAP (T_STRUCT: a struct key) */
   uint8_t elem_ttype;
   uint8_t val_ttype;
   uint8_t reserved0;
   int32_t struct_index;
   uint32_t type_index;
-  uint32_t reserved1;
+  uint32_t key_index;
 } tgpu_type_desc; /* 16 bytes */
 
 /* Struct flags. */

@@ -266,8 +266,9 @@ struct FieldSpec {
   bool optional = false;
   int32_t struct_index = -1;
   uint8_t val_ttype = 0;   /* map value */
-  uint8_t qualifier = 0;   /* TGPU_TERSE etc.; `optional` wins when set */
+  uint8_t qualifier = 0;   /* TGPU_TERSE, TGPU_BOXED etc.; `optional` wins when set */
   uint32_t type_index = 0; /* 1 + nested container type (tgpu_type_desc) */
+  uint16_t key_index = 0;  /* map: 1 + type node of a struct / container key */
 };
 
 /* Owns a tgpu_schema. Structs are given as lists of FieldSpec (struct 0 =
@@ -301,6 +302,7 @@ class GpuSchema {
         fd.qualifier = f.optional ? TGPU_OPTIONAL : f.qualifier;
         fd.struct_index = f.struct_index;
         fd.type_index = f.type_index;
+        fd.key_index = f.key_index;
         fields_.push_back(fd);
       }
     }

@@ -34,7 +34,7 @@ struct HostStruct;
 
 /* How one value (a field's, an element's, a key's) lives on the host. */
 struct HostType {
-  enum Kind : uint8_t { Scalar, String, Struct, Container };
+  enum Kind : uint8_t { Scalar, String, Struct, Container, Boxed };
   using Fill = void (*)(void* ctx, void* elem_or_key, void* val);
   using Visit = void (*)(void* ctx, const void* elem_or_key, const void* val);
   Kind kind = Scalar;
@@ -51,6 +51,11 @@ struct HostType {
   void (*add)(void* c, void* ctx, Fill fill) = nullptr;
   /* Every element in container order (encode). */
   void (*each)(const void* c, void* ctx, Visit fn) = nullptr;
+  /* Boxed (a cpp.ref / thrift.box member, e.g. std::unique_ptr<T>; `st` is
+     T's binding): a fresh default-constructed T the member now owns, and
+     the object the member points to (nullptr: null). */
+  void* (*make)(void* member) = nullptr;
+  const void* (*get)(const void* member) = nullptr;
 };
 
 /* One schema field of a struct, in the schema's declaration order. */
@@ -78,6 +83,21 @@ inline HostType structType(const HostStruct* st) {
   HostType t;
   t.kind = HostType::Struct;
   t.st = st;
+  return t;
+}
+/* std::unique_ptr<T> (or another owning pointer with reset / get) for a
+   boxed struct field. */
+template <class Ptr>
+HostType boxType(const HostStruct* st) {
+  HostType t;
+  t.kind = HostType::Boxed;
+  t.st = st;
+  t.make = [](void* m) -> void* {
+    auto* p = static_cast<Ptr*>(m);
+    p->reset(new typename Ptr::element_type());
+    return p->get();
+  };
+  t.get = [](const void* m) -> const void* { return static_cast<const Ptr*>(m)->get(); };
   return t;
 }
 /* std::vector<E> for list<...>. */
@@ -162,13 +182,22 @@ struct CType {
   uint32_t ttype, elem, val;
   int32_t si;
   uint32_t ti;
+  uint32_t ki;  /* map: 1 + type node of a struct / container key */
 };
 inline CType ctypeOf(const tgpu_field_desc& f) {
-  return CType{f.ttype, f.elem_ttype, f.val_ttype, f.struct_index, f.type_index};
+  return CType{f.ttype, f.elem_ttype, f.val_ttype, f.struct_index, f.type_index, f.key_index};
 }
 inline CType ctypeNode(const SchemaTables& sc, uint32_t ti) {
   const tgpu_type_desc& t = sc.t[ti - 1];
-  return CType{t.ttype, t.elem_ttype, t.val_ttype, t.struct_index, t.type_index};
+  return CType{t.ttype, t.elem_ttype, t.val_ttype, t.struct_index, t.type_index, t.key_index};
+}
+/* A map key's struct (a T_STRUCT key node), and its container node. */
+inline int32_t keyStruct(const SchemaTables& sc, const CType& c) {
+  return (c.elem == TGPU_T_STRUCT && c.ki) ? sc.t[c.ki - 1].struct_index : -1;
+}
+inline uint32_t keyNode(const CType& c) { return c.elem == TGPU_T_STRUCT ? 0 : c.ki; }
+inline bool isBoxed(const tgpu_field_desc& f) {
+  return f.qualifier == TGPU_BOXED || f.qualifier == TGPU_OPTIONAL_BOXED;
 }
 inline tgpu_span loadSpan(const uint8_t* p) {
   tgpu_span s;
@@ -221,7 +250,7 @@ inline void readContainer(const SchemaTables& sc, const CType& c, const uint8_t*
   ht.clear(host);
   const bool is_map = c.ttype == TGPU_T_MAP;
   const uint32_t v = is_map ? c.val : c.elem;
-  const uint32_t ks = is_map ? slotBytes(sc, c.elem, -1) : 0;
+  const uint32_t ks = is_map ? slotBytes(sc, c.elem, keyStruct(sc, c)) : 0;
   const uint32_t es = ks + slotBytes(sc, v, c.si);
   for (uint32_t i = 0; i < s.length; ++i) {
     ElemCtx ctx{&sc, &c, &src, &ht, src.arena + s.offset + (uint64_t)i * es, ks};
@@ -229,7 +258,8 @@ inline void readContainer(const SchemaTables& sc, const CType& c, const uint8_t*
       const ElemCtx& x = *static_cast<const ElemCtx*>(p);
       const bool m = x.c->ttype == TGPU_T_MAP;
       if (m) {
-        readValue(*x.sc, x.c->elem, -1, 0, x.e, *x.src, *x.ht->elem, ek);
+        readValue(*x.sc, x.c->elem, keyStruct(*x.sc, *x.c), keyNode(*x.c), x.e, *x.src,
+                  *x.ht->elem, ek);
         readValue(*x.sc, x.c->val, x.c->si, x.c->ti, x.e + x.ks, *x.src, *x.ht->val, hv);
       } else {
         readValue(*x.sc, x.c->elem, x.c->si, x.c->ti, x.e, *x.src, *x.ht->elem, ek);
@@ -250,8 +280,16 @@ inline void readStruct(const SchemaTables& sc, uint32_t si, const uint8_t* dev,
     if (!set) continue;  // absent on the wire: the member keeps its value
     const uint8_t* m = dev + f.member_offset;
     void* h = host + hf.offset;
-    if (isContainer(f.ttype)) readContainer(sc, ctypeOf(f), m, src, *hf.type, h);
-    else readValue(sc, f.ttype, f.struct_index, 0, m, src, *hf.type, h);
+    if (isBoxed(f)) {  // the object the device member points to, in the arena
+      const tgpu_span b = loadSpan(m);
+      if (b.length)
+        readStruct(sc, (uint32_t)f.struct_index, src.arena + b.offset, src, *hf.type->st,
+                   (uint8_t*)hf.type->make(h));
+    } else if (isContainer(f.ttype)) {
+      readContainer(sc, ctypeOf(f), m, src, *hf.type, h);
+    } else {
+      readValue(sc, f.ttype, f.struct_index, 0, m, src, *hf.type, h);
+    }
   }
 }
 
@@ -293,7 +331,7 @@ inline void writeContainer(const SchemaTables& sc, const CType& c, const void* h
   ht.each(host, &n, [](void* p, const void*, const void*) { ++*static_cast<uint64_t*>(p); });
   const bool is_map = c.ttype == TGPU_T_MAP;
   const uint32_t v = is_map ? c.val : c.elem;
-  const uint32_t ks = is_map ? slotBytes(sc, c.elem, -1) : 0;
+  const uint32_t ks = is_map ? slotBytes(sc, c.elem, keyStruct(sc, c)) : 0;
   const uint32_t es = ks + slotBytes(sc, v, c.si);
   const uint64_t arr = n ? out.alloc(n * es) : 0;
   storeSpan(buf->data() + off, arr, n);
@@ -302,7 +340,8 @@ inline void writeContainer(const SchemaTables& sc, const CType& c, const void* h
     WriteCtx& x = *static_cast<WriteCtx*>(p);
     const uint64_t at = x.arr + x.i++ * x.es;
     if (x.c->ttype == TGPU_T_MAP) {
-      writeValue(*x.sc, x.c->elem, -1, 0, ek, *x.ht->elem, *x.out, &x.out->lists, at);
+      writeValue(*x.sc, x.c->elem, keyStruct(*x.sc, *x.c), keyNode(*x.c), ek, *x.ht->elem,
+                 *x.out, &x.out->lists, at);
       writeValue(*x.sc, x.c->val, x.c->si, x.c->ti, hv, *x.ht->val, *x.out, &x.out->lists,
                  at + x.ks);
     } else {
@@ -339,7 +378,15 @@ inline void writeStruct(const SchemaTables& sc, uint32_t si, const uint8_t* host
     const uint8_t set = hf.isset >= 0 ? host[hf.isset] : 1;
     (*buf)[dev_off + f.isset_offset] = set;
     const void* h = host + hf.offset;
-    if (isContainer(f.ttype))
+    if (isBoxed(f)) {  // the pointee into the list base; null stays {0, 0}
+      const void* obj = hf.type->get(h);
+      if (obj) {
+        const uint64_t o = out.alloc(sc.s[f.struct_index].size);
+        storeSpan(buf->data() + dev_off + f.member_offset, o, 1);
+        writeStruct(sc, (uint32_t)f.struct_index, (const uint8_t*)obj, *hf.type->st, out, o,
+                    &out.lists);
+      }
+    } else if (isContainer(f.ttype))
       writeContainer(sc, ctypeOf(f), h, *hf.type, out, buf, dev_off + f.member_offset);
     else
       writeValue(sc, f.ttype, f.struct_index, 0, h, *hf.type, out, buf,

@@ -128,13 +128,23 @@ struct CT {
   uint8_t ttype, elem, val;
   int32_t si;   // struct of T_STRUCT elements / values
   uint32_t ti;  // 1 + nested type of container elements / values
+  uint32_t ki;  // map: 1 + type node of a struct / container key
 };
 CT ct_of(const tgpu_field_desc& f) {
-  return CT{f.ttype, f.elem_ttype, f.val_ttype, f.struct_index, f.type_index};
+  return CT{f.ttype, f.elem_ttype, f.val_ttype, f.struct_index, f.type_index, f.key_index};
 }
 CT ct_node(const Schema& sc, uint32_t ti) {
   const tgpu_type_desc& t = sc.t[ti - 1];
-  return CT{t.ttype, t.elem_ttype, t.val_ttype, t.struct_index, t.type_index};
+  return CT{t.ttype, t.elem_ttype, t.val_ttype, t.struct_index, t.type_index, t.key_index};
+}
+// A map key's struct (a T_STRUCT key node) and container node.
+int32_t key_si(const Schema& sc, const CT& c) {
+  return c.elem == TGPU_T_STRUCT ? sc.t[c.ki - 1].struct_index : -1;
+}
+uint32_t key_ti(const CT& c) { return c.elem == TGPU_T_STRUCT ? 0 : c.ki; }
+// cpp.ref / thrift.box struct fields (thrift_gpu.h TGPU_BOXED)
+bool is_boxed(const tgpu_field_desc& f) {
+  return f.qualifier == TGPU_BOXED || f.qualifier == TGPU_OPTIONAL_BOXED;
 }
 bool is_container_t(uint8_t t) {
   return t == TGPU_T_LIST || t == TGPU_T_SET || t == TGPU_T_MAP;
@@ -185,8 +195,10 @@ bool struct_empty(const Schema& sc, uint32_t si, const uint8_t* obj) {
       if (obj[f.isset_offset]) return false;
       continue;
     }
-    if (f.qualifier == TGPU_UNQUALIFIED || f.qualifier == TGPU_REQUIRED) return false;
-    if (f.qualifier == TGPU_OPTIONAL) {
+    if (f.qualifier == TGPU_UNQUALIFIED || f.qualifier == TGPU_REQUIRED ||
+        f.qualifier == TGPU_BOXED)
+      return false;
+    if (f.qualifier == TGPU_OPTIONAL || f.qualifier == TGPU_OPTIONAL_BOXED) {
       if (obj[f.isset_offset]) return false;
       continue;
     }
@@ -636,25 +648,35 @@ uint32_t min_wire(uint8_t t, bool compact) {
 }
 bool nested_schema(const Schema& sc) {
   auto nested = [](uint8_t t, uint8_t e, uint8_t v) {
-    return is_container_t(t) && is_complex_t(t == TGPU_T_MAP ? v : e);
+    return is_container_t(t) && (is_complex_t(t == TGPU_T_MAP ? v : e) ||
+                                 (t == TGPU_T_MAP && is_complex_t(e)));
   };
   for (uint32_t k = 0; k < sc.nf; ++k)
-    if (nested(sc.f[k].ttype, sc.f[k].elem_ttype, sc.f[k].val_ttype)) return true;
+    if (nested(sc.f[k].ttype, sc.f[k].elem_ttype, sc.f[k].val_ttype) || is_boxed(sc.f[k]))
+      return true;
   return false;
 }
+// Every container description (fields and type nodes) and every boxed field
+// once: recursive schemas are covered without recursion.
 void ratio_of(const Schema& sc, const CT& c, bool compact, double& ratio) {
+  if (!is_container_t(c.ttype)) return;
   const bool is_map = c.ttype == TGPU_T_MAP;
   const uint8_t v = is_map ? c.val : c.elem;
-  const double kb = is_map ? elem_size(c.elem) : 0, kw = is_map ? min_wire(c.elem, compact) : 0;
-  const double vb = slot_size(sc, v, c.si) + (is_container_t(v) ? 7 : 0);
-  ratio = std::max(ratio, (kb + vb) / (kw + min_wire(v, compact)));
+  const double kb = is_map ? slot_size(sc, c.elem, key_si(sc, c)) : 0;
+  const double kw = is_map ? min_wire(c.elem, compact) : 0;
+  const double pad = (is_container_t(v) ? 7 : 0) + (is_map && is_container_t(c.elem) ? 7 : 0);
+  const double vb = slot_size(sc, v, c.si);
+  ratio = std::max(ratio, (kb + vb + pad) / (kw + min_wire(v, compact)));
   ratio = std::max(ratio, 7.0 / min_wire(c.ttype, compact));
-  if (is_container_t(v)) ratio_of(sc, ct_node(sc, c.ti), compact, ratio);
 }
 uint32_t region_scale(const Schema& sc, bool compact) {
   double ratio = 8.0;
-  for (uint32_t k = 0; k < sc.nf; ++k)
-    if (is_container_t(sc.f[k].ttype)) ratio_of(sc, ct_of(sc.f[k]), compact, ratio);
+  for (uint32_t k = 0; k < sc.nf; ++k) {
+    ratio_of(sc, ct_of(sc.f[k]), compact, ratio);
+    if (sc.f[k].ttype == TGPU_T_STRUCT && is_boxed(sc.f[k]))  // field header + STOP
+      ratio = std::max(ratio, (sc.s[sc.f[k].struct_index].size + 7.0) / (compact ? 2.0 : 4.0));
+  }
+  for (uint32_t k = 0; k < sc.nt; ++k) ratio_of(sc, ct_node(sc, k + 1), compact, ratio);
   return ((uint32_t)std::ceil(ratio) + 7) & ~7u;
 }
 
@@ -784,9 +806,12 @@ void readMap(R& r, const CT& f, uint8_t* member, DecodeCtx& dc) {
   r.readMapBegin(kv[0], kv[1], n);
   if (n > 0 && (kv[0] != f.elem || kv[1] != f.val)) {
     r.skip_n((uint32_t)n, kv, 2, 0);
-  } else if (is_complex_t(f.val)) {
+  } else if (is_complex_t(f.val) || is_complex_t(f.elem)) {
+    // structs / containers as keys or values: the key's and the value's
+    // reads, then the pair is inserted
     if (!r.c.canAdvance((uint64_t)(uint32_t)n * 2)) fail(TGPU_ERR_TRUNCATED, r.c.pos);
-    const uint32_t ks = elem_size(f.elem), ps = ks + slot_size(*dc.sc, f.val, f.si);
+    const int32_t ksi = key_si(*dc.sc, f);
+    const uint32_t ks = slot_size(*dc.sc, f.elem, ksi), ps = ks + slot_size(*dc.sc, f.val, f.si);
     if (n > 0) {
       if (!dc.arena) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
       const uint64_t bytes = (uint64_t)(uint32_t)n * ps;
@@ -795,7 +820,7 @@ void readMap(R& r, const CT& f, uint8_t* member, DecodeCtx& dc) {
       for (int32_t i = 0; i < n; ++i) {
         uint8_t* pr = dc.arena + aoff + (uint64_t)i * ps;
         std::memset(pr, 0, ps);
-        readElem(r, f.elem, pr);
+        readValue(r, f.elem, ksi, key_ti(f), pr, dc);
         readValue(r, f.val, f.si, f.ti, pr + ks, dc);
         put_span(member, aoff, (uint32_t)(i + 1));
       }
@@ -881,6 +906,16 @@ void readStruct(R& r, uint32_t si, uint8_t* obj, DecodeCtx& dc) {
       r.readString(sp.offset, sp.length);
       if (sp.length == 0) sp.offset = 0;
       std::memcpy(m, &sp, sizeof(sp));
+    } else if (f->ttype == TGPU_T_STRUCT && is_boxed(*f)) {
+      // cpp.ref / thrift.box: make_mutable_smart_ptr, read, then the member
+      // points to the fresh object (deserialize_field.whisker:21-23,49-51)
+      const uint32_t size = dc.sc->s[f->struct_index].size;
+      if (!dc.arena) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
+      const uint64_t aoff = dc.alloc(r.c.pos, size);
+      if (aoff + size > dc.arena_cap) fail(TGPU_ERR_OUTPUT_OVERFLOW, r.c.pos);
+      std::memset(dc.arena + aoff, 0, size);
+      readStruct(r, (uint32_t)f->struct_index, dc.arena + aoff, dc);
+      put_span(m, aoff, 1);
     } else if (f->ttype == TGPU_T_STRUCT) {
       readStruct(r, (uint32_t)f->struct_index, m, dc);  // merges into member
     } else if (is_container_t(f->ttype)) {
@@ -985,6 +1020,12 @@ struct EncodeCtx {
   const uint8_t* lbase;
 };
 
+tgpu_span ld_span(const uint8_t* p) {
+  tgpu_span v;
+  std::memcpy(&v, p, sizeof(v));
+  return v;
+}
+
 // A union writes its active member only (serialize_union.whisker:52-66,
 // switch (getType())): the first member whose isset byte is set, or none.
 void union_range(const EncodeCtx& ec, const tgpu_struct_desc& sd, const uint8_t* obj,
@@ -998,6 +1039,16 @@ void union_range(const EncodeCtx& ec, const tgpu_struct_desc& sd, const uint8_t*
       return;
     }
   }
+}
+
+// The object a struct member holds: the member itself, or for a boxed member
+// the object its pointer (span into list_base) names; nullptr for a null
+// pointer, which serialize_field.whisker:44-49 writes as an empty struct
+// (writeStructBegin, writeFieldStop, writeStructEnd).
+const uint8_t* boxed_object(const EncodeCtx& ec, const tgpu_field_desc& f, const uint8_t* m) {
+  if (!is_boxed(f)) return m;
+  const tgpu_span sp = ld_span(m);
+  return sp.length ? ec.lbase + sp.offset : nullptr;
 }
 
 uint8_t load_bool_checked(const uint8_t* p, uint64_t off) {
@@ -1053,10 +1104,12 @@ struct BinaryWriter {
     header(c, sp.length);
     const bool is_map = c.ttype == TGPU_T_MAP;
     const uint8_t v = is_map ? c.val : c.elem;
-    const uint32_t ks = is_map ? elem_size(c.elem) : 0, ps = ks + slot_size(*ec.sc, v, c.si);
+    const int32_t ksi = is_map ? key_si(*ec.sc, c) : -1;
+    const uint32_t ks = is_map ? slot_size(*ec.sc, c.elem, ksi) : 0;
+    const uint32_t ps = ks + slot_size(*ec.sc, v, c.si);
     const uint8_t* e = ec.lbase + sp.offset;
     for (uint32_t i = 0; i < sp.length; ++i) {
-      if (is_map) elem(ec, c.elem, e + (uint64_t)i * ps);
+      if (is_map) value(ec, c.elem, ksi, key_ti(c), e + (uint64_t)i * ps);
       value(ec, v, c.si, c.ti, e + (uint64_t)i * ps + ks);
     }
   }
@@ -1075,7 +1128,9 @@ struct BinaryWriter {
     union_range(ec, sd, obj, k0, k1);
     for (uint32_t k = k0; k < k1; ++k) {
       const tgpu_field_desc& f = ec.sc->f[sd.first_field + k];
-      if (f.qualifier == TGPU_OPTIONAL && !obj[f.isset_offset]) continue;
+      if ((f.qualifier == TGPU_OPTIONAL || f.qualifier == TGPU_OPTIONAL_BOXED) &&
+          !obj[f.isset_offset])
+        continue;
       const uint8_t* m = obj + f.member_offset;
       if (f.qualifier == TGPU_TERSE && terse_empty(*ec.sc, f, m)) continue;  // fields.whisker:84
       s.put(f.ttype);  // writeFieldBegin: byte type + BE i16 id
@@ -1088,7 +1143,9 @@ struct BinaryWriter {
         s.putBE(sp.length, 4);
         s.putBytes(ec.sbase + sp.offset, sp.length);
       } else if (f.ttype == TGPU_T_STRUCT) {
-        structure(ec, (uint32_t)f.struct_index, m);
+        const uint8_t* o = boxed_object(ec, f, m);
+        if (o) structure(ec, (uint32_t)f.struct_index, o);
+        else s.put(TGPU_T_STOP);  // a null ref: an empty struct
       } else {  // list / set / map
         container(ec, ct_of(f), m);
       }
@@ -1160,10 +1217,12 @@ struct CompactWriterT {
     header(c, sp.length);
     const bool is_map = c.ttype == TGPU_T_MAP;
     const uint8_t v = is_map ? c.val : c.elem;
-    const uint32_t ks = is_map ? elem_size(c.elem) : 0, ps = ks + slot_size(*ec.sc, v, c.si);
+    const int32_t ksi = is_map ? key_si(*ec.sc, c) : -1;
+    const uint32_t ks = is_map ? slot_size(*ec.sc, c.elem, ksi) : 0;
+    const uint32_t ps = ks + slot_size(*ec.sc, v, c.si);
     const uint8_t* e = ec.lbase + sp.offset;
     for (uint32_t i = 0; i < sp.length; ++i) {
-      if (is_map) elem(ec, c.elem, e + (uint64_t)i * ps);
+      if (is_map) value(ec, c.elem, ksi, key_ti(c), e + (uint64_t)i * ps);
       value(ec, v, c.si, c.ti, e + (uint64_t)i * ps + ks);
     }
   }
@@ -1183,7 +1242,9 @@ struct CompactWriterT {
     union_range(ec, sd, obj, k0, k1);
     for (uint32_t k = k0; k < k1; ++k) {
       const tgpu_field_desc& f = ec.sc->f[sd.first_field + k];
-      if (f.qualifier == TGPU_OPTIONAL && !obj[f.isset_offset]) continue;
+      if ((f.qualifier == TGPU_OPTIONAL || f.qualifier == TGPU_OPTIONAL_BOXED) &&
+          !obj[f.isset_offset])
+        continue;
       const uint8_t* m = obj + f.member_offset;
       if (f.qualifier == TGPU_TERSE && terse_empty(*ec.sc, f, m)) continue;  // fields.whisker:84
       if (f.ttype == TGPU_T_BOOL) {  // bool value rides in the header
@@ -1200,7 +1261,9 @@ struct CompactWriterT {
         s.varint(sp.length);  // writeVarint(out_, (int32_t)size)
         s.putBytes(ec.sbase + sp.offset, sp.length);
       } else if (f.ttype == TGPU_T_STRUCT) {
-        structure(ec, (uint32_t)f.struct_index, m);
+        const uint8_t* o = boxed_object(ec, f, m);
+        if (o) structure(ec, (uint32_t)f.struct_index, o);
+        else s.put(0);  // a null ref: an empty struct (writeFieldStop only)
       } else {  // list / set / map
         container(ec, ct_of(f), m);
       }
@@ -1362,7 +1425,8 @@ uint32_t oracle_arena_scale(const tgpu_struct_desc* structs, uint32_t n_structs,
   Schema sc{structs, n_structs, fields, n_fields, types, n_types};
   const bool bin = protocol == TGPU_PROTOCOL_BINARY;
   bool lists = false;
-  for (uint32_t k = 0; k < n_fields; ++k) lists |= is_container_t(fields[k].ttype);
+  for (uint32_t k = 0; k < n_fields; ++k)
+    lists |= is_container_t(fields[k].ttype) || is_boxed(fields[k]);  // boxed objects: the arena
   if (!lists) return 0;
   if (nested_schema(sc)) return region_scale(sc, !bin);
   return has_string_elems(sc) ? (bin ? 4 : 16) : (bin ? 1 : 8);

@@ -14,11 +14,15 @@ from datagen import (SEED, T_BOOL, T_BYTE, T_DOUBLE, T_FLOAT, T_I16, T_I32, T_I6
                      T_MAP, T_SET, T_STRING, T_STRUCT, bits_to_double, finite_bits, s32, s64,
                      splitmix64_at)
 
-# Field rows: [id, ttype, elem_ttype, qualifier, struct_index, val_ttype, inner]
-# where inner = [ttype, elem_ttype, val_ttype, struct_index, inner] describes
-# container elements / map values that are themselves containers.
+# Field rows: [id, ttype, elem_ttype, qualifier, struct_index, val_ttype, inner,
+# key] where inner = [ttype, elem_ttype, val_ttype, struct_index, inner, key]
+# describes container elements / map values that are themselves containers
+# and key a map's struct key ([T_STRUCT, 0, 0, struct_index]) or container
+# key (an inner form). Qualifier 4 / 5: a boxed (cpp.ref / thrift.box)
+# struct field, unqualified / optional.
 ITEM = [[1, T_I32, 0, 0, -1], [2, T_STRING, 0, 0, -1], [3, T_LIST, T_I16, 0, -1],
         [4, T_DOUBLE, 0, 1, -1]]
+POINT = [[1, T_I32, 0, 0, -1], [2, T_I32, 0, 0, -1], [3, T_STRING, 0, 1, -1]]
 NESTED_SCHEMAS = {
     # struct 1 = Item {1: i32, 2: string, 3: list<i16>, 4: optional double}
     "structlist": [
@@ -34,6 +38,28 @@ NESTED_SCHEMAS = {
          [5, T_SET, T_LIST, 0, -1, 0, [T_LIST, T_LIST, 0, -1, [T_LIST, T_I64, 0, -1]]],
          [6, T_I32, 0, 0, -1]],
         ITEM,
+    ],
+    # struct 1 = Point {1: i32 x, 2: i32 y, 3: optional string label}
+    "keyed": [
+        [[1, T_MAP, T_STRUCT, 0, -1, T_STRING, None, [T_STRUCT, 0, 0, 1]],
+         [2, T_MAP, T_LIST, 0, -1, T_I64, None, [T_LIST, T_I32, 0, -1]],
+         [3, T_MAP, T_SET, 0, 1, T_STRUCT, None, [T_SET, T_STRING, 0, -1]],
+         [4, T_LIST, T_MAP, 0, -1, 0,
+          [T_MAP, T_STRUCT, T_LIST, -1, [T_LIST, T_I16, 0, -1], [T_STRUCT, 0, 0, 1]]],
+         [5, T_I32, 0, 0, -1]],
+        POINT,
+    ],
+    # Tree {1: i32 v, 2: list<Tree> kids, 3: string tag}: recursive through a
+    # list, up to 12 levels (past the device's private frames)
+    "tree": [
+        [[1, T_I32, 0, 0, -1], [2, T_LIST, T_STRUCT, 0, 0], [3, T_STRING, 0, 0, -1]],
+    ],
+    # Node {1: i64 v, 2: optional Node next (thrift.box), 3: Leaf leaf
+    # (cpp.ref)}, Leaf {1: i32 a, 2: optional string b}: a linked list of
+    # 0..60 boxed nodes
+    "chain": [
+        [[1, T_I64, 0, 0, -1], [2, T_STRUCT, 0, 5, 0], [3, T_STRUCT, 0, 4, 1]],
+        [[1, T_I32, 0, 0, -1], [2, T_STRING, 0, 1, -1]],
     ],
 }
 
@@ -94,16 +120,66 @@ def gen_deepcont(i):
     return [grid, index, maps, mm, cube, s32(r.u())]
 
 
-NESTED_GENERATORS = {"structlist": gen_structlist, "deepcont": gen_deepcont}
+def point(r):
+    return [s32(r.u()) % 1000, s32(r.u()) % 1000, _str(r, 6) if r.below(2) else None]
+
+
+def gen_keyed(i):
+    r = _R(i, 0x4E)
+    by_point = [[point(r), _str(r, 8)] for _ in range(r.below(5))]
+    by_path = [[[s32(r.u()) for _ in range(r.below(4))], s64(r.u())] for _ in range(r.below(4))]
+    by_tags = [[[_str(r, 4) for _ in range(r.below(3))], point(r)] for _ in range(r.below(3))]
+    grids = [[[point(r), [(r.u() & 0xFFFF) - 0x8000 for _ in range(r.below(4))]]
+              for _ in range(r.below(3))] for _ in range(r.below(3))]
+    return [by_point, by_path, by_tags, grids, s32(r.u())]
+
+
+def _tree(r, depth):
+    # a spine `depth` levels deep, with a few shallow side branches
+    kids = []
+    if depth > 0:
+        kids = [_tree(r, depth - 1)] + [_tree(r, min(1, depth - 1)) for _ in range(r.below(2))]
+        if r.below(3) == 0:
+            kids.reverse()
+    return [s32(r.u()), kids, _str(r, 5)]
+
+
+def gen_tree(i):
+    r = _R(i, 0x7E)
+    return _tree(r, r.below(13) if i % 5 else 12)
+
+
+def gen_chain(i):
+    r = _R(i, 0xC4)
+    n = r.below(61) if i % 4 == 0 else r.below(10)
+    node = None
+    for k in range(n + 1):
+        leaf = [s32(r.u()), _str(r, 6) if r.below(2) else None]
+        node = [s64(r.u()), node, leaf]
+    return node
+
+
+NESTED_GENERATORS = {"structlist": gen_structlist, "deepcont": gen_deepcont,
+                     "keyed": gen_keyed, "tree": gen_tree, "chain": gen_chain}
 
 
 # ---- type specs ------------------------------------------------------------
-# A spec is (ttype, sub): sub = struct index for T_STRUCT; for containers
-# (ttype, elem_spec, val_spec) with val_spec None for list/set.
+# A spec is (ttype, sub): sub = struct index for T_STRUCT (a boxed field:
+# (T_STRUCT, sub, True)); for containers (ttype, elem_spec, val_spec) with
+# val_spec None for list/set and elem_spec the key's spec for a map.
 def _inner_spec(inner):
     tt, et, vt, sub = inner[:4]
     nxt = inner[4] if len(inner) > 4 else None
-    return container_spec(tt, et, vt, sub, nxt)
+    key = inner[5] if len(inner) > 5 else None
+    return container_spec(tt, et, vt, sub, nxt, key)
+
+
+def _key_spec(et, key):
+    if key is None:
+        return (et, None)
+    if key[0] == T_STRUCT:
+        return (T_STRUCT, key[3])
+    return _inner_spec(key)
 
 
 def _elem_spec(t, sub, inner):
@@ -114,19 +190,20 @@ def _elem_spec(t, sub, inner):
     return (t, None)
 
 
-def container_spec(tt, et, vt, sub, inner):
+def container_spec(tt, et, vt, sub, inner, key=None):
     if tt == T_MAP:
-        return (tt, (et, None), _elem_spec(vt, sub, inner))
+        return (tt, _key_spec(et, key), _elem_spec(vt, sub, inner))
     return (tt, _elem_spec(et, sub, inner), None)
 
 
 def field_spec(row):
     fid, tt, et, q, sub = row[:5]
     if tt == T_STRUCT:
-        return (T_STRUCT, sub)
+        return (T_STRUCT, sub, True) if q in (4, 5) else (T_STRUCT, sub)
     if tt in (T_LIST, T_SET, T_MAP):
         return container_spec(tt, et, row[5] if len(row) > 5 else 0, sub,
-                              row[6] if len(row) > 6 else None)
+                              row[6] if len(row) > 6 else None,
+                              row[7] if len(row) > 7 else None)
     return (tt, None)
 
 

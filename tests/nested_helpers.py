@@ -84,6 +84,9 @@ def materialize(lay, rec, off, wire, arena, spec=(T_STRUCT, 0)):
     if t == T_STRING:
         o, n = _span(rec, off)
         return bytes(wire[o:o + n]).hex()
+    if t == T_STRUCT and len(spec) > 2 and spec[2]:  # boxed: a pointer into the arena
+        o, n = _span(rec, off)
+        return materialize(lay, arena, o, wire, arena, (T_STRUCT, spec[1])) if n else None
     if t == T_STRUCT:
         out = []
         for k, row in enumerate(lay.table[spec[1]]):
@@ -129,6 +132,10 @@ def pack(case):
             b = bytes.fromhex(v)
             struct.pack_into("<QII", buf, off, len(strings), len(b), 0)
             strings.extend(b)
+        elif t == T_STRUCT and len(spec) > 2 and spec[2]:  # boxed
+            o = alloc(lay.size[spec[1]])
+            struct.pack_into("<QII", buf, off, o, 1, 0)
+            put(lists, o, (T_STRUCT, spec[1]), v)
         elif t == T_STRUCT:
             for k, row in enumerate(lay.table[spec[1]]):
                 if v[k] is None:

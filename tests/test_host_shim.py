@@ -37,3 +37,16 @@ def test_host_objects_runs(gpu):
     r = subprocess.run([BIN2], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert "host objects ok" in r.stdout
+
+
+BIN3 = os.path.join(CPP, "build", "test_host_recursive")
+
+
+@pytest.mark.gpu
+def test_host_recursive_runs(gpu):
+    """Boxed (std::unique_ptr) recursive members and struct map keys through
+    serializeBatch / deserializeBatch (tests/cpp/test_host_recursive.cpp)."""
+    subprocess.run(["make", "-s", "-C", CPP], check=True)
+    r = subprocess.run([BIN3], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "host recursive ok" in r.stdout

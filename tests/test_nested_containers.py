@@ -23,7 +23,7 @@ CASES = nh.case_names()
 
 
 def test_golden_cases_exist():
-    assert len(CASES) == 4
+    assert len(CASES) == 10
 
 
 @pytest.mark.parametrize("name", CASES)
