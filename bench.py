@@ -1155,9 +1155,29 @@ def skim(wl, dev, reps=10):
         "check": "64 sampled records vs the oracle"}
 
 
-def host_batch(wl):
-    """Placeholder until the IOBuf batch bench exists."""
-    return {"skipped": "not built"}
+def host_batch(wl, records=1 << 22):
+    """The drop-in caller's rate, never `value`:
+    serializeBatch of codegen'd C++ objects (std::string / std::vector
+    members) into an IOBufQueue and deserializeBatch of the IOBuf back into
+    objects, through the C++ host mirror (include/thrift_gpu/
+    GpuBatchSerializer.h: host materialization on up to 16 threads, the
+    device pass pipelined over PCIe); beside it one core of a reader / writer
+    in the generated code's shape. Configs 3 and 4 (tools/host_batch_bench,
+    a child process)."""
+    import json
+    import subprocess
+
+    cfg = getattr(wl, "config_id", None)
+    if cfg not in (3, 4):
+        return {"skipped": "configs 3 and 4 only"}
+    exe = os.path.join(ROOT, "tools", "build", "host_batch_bench")
+    if not os.path.exists(exe):
+        raise RuntimeError("tools/build/host_batch_bench is not built (__graft_entry__.build())")
+    r = subprocess.run([exe, str(cfg), str(records), "3"], capture_output=True, text=True,
+                       timeout=600)
+    if r.returncode:
+        raise RuntimeError("host_batch_bench failed: %s" % r.stderr[-2000:])
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
 def host_start(wl, dev):

@@ -79,8 +79,11 @@ EXPORTS = [
     "tgpu_decode_batch", "tgpu_index_stream", "tgpu_schema_compile", "tgpu_schema_compile_check",
     "tgpu_decode_host", "tgpu_encode_host", "tgpu_decode_stream", "tgpu_transcode_batch",
     "tgpu_schema_arena_scale", "tgpu_decode_host_ex", "tgpu_encode_host_ex", "tgpu_skim_batch",
-    "tgpu_index_stats",
+    "tgpu_index_stats", "tgpu_decode_host_chunks", "tgpu_encode_host_chunks",
 ]
+
+# callbacks of the chunk-pipelined host calls
+CHUNK_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64)
 
 # tgpu_skim_field as a numpy record (16 bytes).
 SKIM_FIELDS = [("id", "<i2"), ("ttype", "u1"), ("flags", "u1"), ("length", "<u4"),
@@ -168,6 +171,11 @@ def lib():
     L.tgpu_encode_host_ex.restype = I32
     L.tgpu_encode_host_ex.argtypes = [P, P, I32, P, U64, P, U64, P, U64, P, U64, P,
                                       ctypes.POINTER(Status), ctypes.POINTER(U64)]
+    L.tgpu_decode_host_chunks.restype = I32
+    L.tgpu_decode_host_chunks.argtypes = [P, P, I32, P, U64, U64, P, P, U64,
+                                          ctypes.POINTER(Limits), U64, CHUNK_FN, P,
+                                          ctypes.POINTER(Status), ctypes.POINTER(U64),
+                                          ctypes.POINTER(U64)]
     L.tgpu_encoded_size_host.restype = I32
     L.tgpu_encoded_size_host.argtypes = [P, P, I32, P, U64, P, U64, P, ctypes.POINTER(Status),
                                          ctypes.POINTER(U64)]

@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cstring>
 #include <new>
+#include <vector>
 
 #include "tgpu_internal.h"
 
@@ -426,6 +427,338 @@ int tgpu_encode_host_ex(tgpu_context* ctx, const tgpu_schema* schema, int protoc
   if (st) *st = cs;
   if (out_size) *out_size = size;
   return code;
+}
+
+// ---- any schema, chunk-pipelined (tgpu_decode_host_chunks /
+// tgpu_encode_host_chunks) ---------------------------------------------------
+namespace {
+constexpr uint64_t kDefaultChunkBytes = 64ull << 20;
+constexpr uint64_t kDefaultChunkRecords = 1ull << 20;
+
+struct Events {
+  std::vector<hipEvent_t> ev;
+  explicit Events(size_t n) : ev(n, nullptr) {
+    for (auto& e : ev) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  }
+  ~Events() {
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+  }
+};
+
+struct Range {
+  uint64_t r0, r1;
+  hipEvent_t done;
+};
+}  // namespace
+
+int tgpu_decode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                            const void* h_in, uint64_t in_len, uint64_t n, void* h_records,
+                            void* h_arena, uint64_t arena_capacity, const tgpu_limits* limits,
+                            uint64_t chunk_bytes, tgpu_chunk_fn on_chunk, void* user,
+                            tgpu_status* st, uint64_t* n_decoded, uint64_t* consumed) {
+  if (n_decoded) *n_decoded = 0;
+  if (consumed) *consumed = 0;
+  if (!ctx || !schema || (n && (!h_in || !h_records)) || (arena_capacity && !h_arena)) {
+    set_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+    return TGPU_ERR_INVALID_ARGUMENT;
+  }
+  const uint64_t C = chunk_bytes ? chunk_bytes : kDefaultChunkBytes;
+  const uint32_t S = tgpu_schema_record_size(schema);
+  const uint64_t scale = tgpu_schema_arena_scale(schema, protocol);
+  auto resident_all = [&]() {
+    tgpu_status cs{};
+    uint64_t nd = 0, cons = 0;
+    const int code = tgpu_decode_host_ex(ctx, schema, protocol, h_in, in_len, n, h_records,
+                                         h_arena, arena_capacity, limits, &cs, &nd, &cons);
+    if (on_chunk && cs.exc_class != TGPU_EXC_RUNTIME) {  // (runtime errors decode nothing)
+      const uint64_t back = std::min<uint64_t>(n, nd + (code ? 1 : 0));
+      if (back) on_chunk(user, 0, back);
+    }
+    if (st) *st = cs;
+    if (n_decoded) *n_decoded = nd;
+    if (consumed) *consumed = cons;
+    return code;
+  };
+  // small batches (or no arena where one is needed): the resident pass
+  if (n == 0 || in_len <= 2 * C || (scale && arena_capacity < scale * in_len)) return resident_all();
+  void* vp = context_host_pipe(ctx);
+  if (!vp) {
+    set_status(st, TGPU_ERR_HIP, 0, 0);
+    return TGPU_ERR_HIP;
+  }
+  auto* p = (HostPipe*)vp;
+  PinGuard pin_in(h_in, in_len), pin_rec(h_records, n * S), pin_ar(h_arena, arena_capacity);
+  DevBuf din, drec, dar, doffs;
+  if (!din.alloc(in_len) || !drec.alloc(n * S) || (arena_capacity && !dar.alloc(arena_capacity)) ||
+      !doffs.alloc((n + 1) * 8)) {
+    set_status(st, TGPU_ERR_HIP, 0, 0);
+    return TGPU_ERR_HIP;
+  }
+  const uint64_t P = (in_len + C - 1) / C;
+  Events evin(P), evdec(P), evout(P);
+  const hipStream_t sin = p->s[0], sdec = p->s[1], sout = p->s[2];
+  for (uint64_t k = 0; k < P; ++k) {
+    const uint64_t b = k * C, e = std::min(in_len, b + C);
+    if (hipMemcpyAsync(din.p + b, (const uint8_t*)h_in + b, e - b, hipMemcpyHostToDevice, sin) !=
+            hipSuccess ||
+        hipEventRecord(evin.ev[k], sin) != hipSuccess) {
+      (void)hipStreamSynchronize(sin);
+      set_status(st, TGPU_ERR_HIP, 0, 0);
+      return TGPU_ERR_HIP;
+    }
+  }
+  std::vector<Range> pending;
+  uint64_t announced = 0;
+  auto announce = [&](bool all) {
+    size_t k = 0;
+    for (; k < pending.size(); ++k) {
+      if (!all && hipEventQuery(pending[k].done) != hipSuccess) break;
+      if (all) (void)hipEventSynchronize(pending[k].done);
+      if (on_chunk) on_chunk(user, pending[k].r0, pending[k].r1);
+      announced = pending[k].r1;
+    }
+    pending.erase(pending.begin(), pending.begin() + k);
+  };
+  uint64_t B = 0, r0 = 0, k = 0;
+  bool clean = true;
+  while (r0 < n && B < in_len) {
+    const uint64_t end = std::min(in_len, (k + 1) * C);
+    if (end <= B) {
+      ++k;
+      continue;
+    }
+    const uint64_t ap = std::min(k + 1, P - 1);  // the next piece must be resident too
+    const uint64_t avail = std::min(in_len, (ap + 1) * C);
+    tgpu_status cs{};
+    uint64_t nk = 0, first = 0, last = 0;
+    if (hipStreamWaitEvent(sdec, evin.ev[ap], 0) != hipSuccess) return TGPU_ERR_HIP;
+    const int rc = tgpu_decode_stream(p->c[1], schema, protocol, din.p, avail, B, end, 0,
+                                      (uint64_t*)doffs.p + r0, n - r0, drec.p + r0 * S,
+                                      arena_capacity ? dar.p : nullptr, arena_capacity, limits,
+                                      sdec, &cs, &nk, &first, &last);
+    if (rc != TGPU_OK || first != B || last < B || (nk == 0 && end < in_len)) {
+      clean = false;  // a record the range cannot end cleanly on: the resident pass
+      break;
+    }
+    if (nk) {
+      if (hipEventRecord(evdec.ev[k], sdec) != hipSuccess ||
+          hipStreamWaitEvent(sout, evdec.ev[k], 0) != hipSuccess ||
+          hipMemcpyAsync((uint8_t*)h_records + r0 * S, drec.p + r0 * S, nk * S,
+                         hipMemcpyDeviceToHost, sout) != hipSuccess ||
+          (scale && hipMemcpyAsync((uint8_t*)h_arena + scale * B, dar.p + scale * B,
+                                   std::min(arena_capacity, scale * last) - scale * B,
+                                   hipMemcpyDeviceToHost, sout) != hipSuccess) ||
+          hipEventRecord(evout.ev[k], sout) != hipSuccess) {
+        clean = false;
+        break;
+      }
+      pending.push_back(Range{r0, r0 + nk, evout.ev[k]});
+    }
+    announce(false);
+    B = last;
+    r0 += nk;
+    ++k;
+  }
+  (void)hipStreamSynchronize(sin);
+  (void)hipStreamSynchronize(sdec);
+  announce(true);
+  if (clean && r0 == n) {
+    set_status(st, TGPU_OK, n, 0);
+    if (n_decoded) *n_decoded = n;
+    if (consumed) *consumed = B;
+    return TGPU_OK;
+  }
+  // a range that did not end cleanly (or the stream ended before n records):
+  // the whole batch resident on the device, exact status; the records from
+  // the first one not yet handed over come back
+  tgpu_status cs{};
+  uint64_t nd = 0, cons = 0;
+  int code = tgpu_decode_batch(p->c[1], schema, protocol, din.p, in_len, nullptr, n, drec.p,
+                               arena_capacity ? dar.p : nullptr, arena_capacity, limits, sdec,
+                               &cs, &nd, &cons);
+  if (code != TGPU_ERR_HIP) {
+    const uint64_t back = std::min<uint64_t>(n, nd + (code ? 1 : 0));
+    uint64_t a0 = 0;  // arena bytes of the records from `announced` on
+    if (announced && hipMemcpy(&a0, (const uint64_t*)doffs.p + announced, 8,
+                               hipMemcpyDeviceToHost) != hipSuccess)
+      code = TGPU_ERR_HIP;
+    a0 = std::min(arena_capacity, scale * a0);
+    if (code != TGPU_ERR_HIP && back > announced &&
+        (hipMemcpy((uint8_t*)h_records + announced * S, drec.p + announced * S,
+                   (back - announced) * S, hipMemcpyDeviceToHost) != hipSuccess ||
+         (scale && hipMemcpy((uint8_t*)h_arena + a0, dar.p + a0, arena_capacity - a0,
+                             hipMemcpyDeviceToHost) != hipSuccess)))
+      code = TGPU_ERR_HIP;
+    if (code != TGPU_ERR_HIP && on_chunk && back > announced && cs.exc_class != TGPU_EXC_RUNTIME)
+      on_chunk(user, announced, back);
+  }
+  if (code == TGPU_ERR_HIP) {
+    set_status(st, TGPU_ERR_HIP, 0, 0);
+    return TGPU_ERR_HIP;
+  }
+  if (st) *st = cs;
+  if (n_decoded) *n_decoded = nd;
+  if (consumed) *consumed = cons;
+  return code;
+}
+
+int tgpu_encode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                            uint64_t n, uint64_t chunk_records, tgpu_fill_fn fill,
+                            tgpu_reserve_fn reserve, void* user, tgpu_status* st,
+                            uint64_t* out_size) {
+  if (out_size) *out_size = 0;
+  if (!ctx || !schema || !fill || !reserve) {
+    set_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+    return TGPU_ERR_INVALID_ARGUMENT;
+  }
+  if (n == 0) {
+    set_status(st, TGPU_OK, 0, 0);
+    return TGPU_OK;
+  }
+  void* vp = context_host_pipe(ctx);
+  if (!vp) {
+    set_status(st, TGPU_ERR_HIP, 0, 0);
+    return TGPU_ERR_HIP;
+  }
+  auto* p = (HostPipe*)vp;
+  const uint64_t K = chunk_records ? chunk_records : kDefaultChunkRecords;
+  const uint64_t nch = (n + K - 1) / K;
+  const uint32_t S = tgpu_schema_record_size(schema);
+  const hipStream_t sin = p->s[0], senc = p->s[1], sout = p->s[2];
+  // two slots: chunk k's device form and output in slot k % 2
+  struct Slot {
+    DevBuf rec, str, lst, out;
+    uint64_t rec_cap = 0, str_cap = 0, lst_cap = 0, out_cap = 0;
+    hipEvent_t in_done = nullptr, out_done = nullptr;
+    uint64_t m = 0;
+  } slot[2];
+  for (auto& sl : slot) {
+    (void)hipEventCreateWithFlags(&sl.in_done, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&sl.out_done, hipEventDisableTiming);
+  }
+  struct EvFree {
+    Slot* s;
+    ~EvFree() {
+      for (int i = 0; i < 2; ++i) {
+        (void)hipEventDestroy(s[i].in_done);
+        (void)hipEventDestroy(s[i].out_done);
+      }
+    }
+  } evfree{slot};
+  auto grow = [](DevBuf& b, uint64_t& cap, uint64_t want) {
+    if (want <= cap) return true;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    cap = 0;
+    if (!b.alloc(want)) return false;
+    cap = want;
+    return true;
+  };
+  // upload chunk c's form into its slot (after the slot's previous output left)
+  auto upload = [&](uint64_t c) -> int {
+    Slot& sl = slot[c % 2];
+    const uint64_t r0 = c * K, m = std::min(K, n - r0);
+    tgpu_host_form f{};
+    if (fill(user, r0, r0 + m, &f) != 0 || !f.records) return TGPU_ERR_INVALID_ARGUMENT;
+    if (!grow(sl.rec, sl.rec_cap, m * S) || !grow(sl.str, sl.str_cap, f.strings_len + 16) ||
+        !grow(sl.lst, sl.lst_cap, f.lists_len + 16))
+      return TGPU_ERR_HIP;
+    if (hipStreamWaitEvent(sin, sl.out_done, 0) != hipSuccess ||
+        hipMemcpyAsync(sl.rec.p, f.records, m * S, hipMemcpyHostToDevice, sin) != hipSuccess ||
+        (f.strings_len && hipMemcpyAsync(sl.str.p, f.strings, f.strings_len,
+                                         hipMemcpyHostToDevice, sin) != hipSuccess) ||
+        (f.lists_len && hipMemcpyAsync(sl.lst.p, f.lists, f.lists_len, hipMemcpyHostToDevice,
+                                       sin) != hipSuccess) ||
+        hipEventRecord(sl.in_done, sin) != hipSuccess)
+      return TGPU_ERR_HIP;
+    sl.m = m;
+    return TGPU_OK;
+  };
+  // encode chunk c (async); the output buffer grows to the chunk's size on
+  // an overflow, found by the blocking size pass
+  auto encode = [&](uint64_t c) -> int {
+    Slot& sl = slot[c % 2];
+    if (!sl.out_cap && !grow(sl.out, sl.out_cap, std::max<uint64_t>(16ull << 20, sl.m * 64)))
+      return TGPU_ERR_HIP;
+    if (hipStreamWaitEvent(senc, sl.in_done, 0) != hipSuccess ||
+        hipStreamWaitEvent(senc, sl.out_done, 0) != hipSuccess)
+      return TGPU_ERR_HIP;
+    return tgpu_encode_batch(p->c[c % 2], schema, protocol, sl.rec.p, sl.m, sl.str.p, sl.lst.p,
+                             sl.out.p, sl.out_cap, nullptr, senc, nullptr, nullptr);
+  };
+  uint64_t total = 0;
+  int rc = upload(0);
+  if (rc == TGPU_OK) rc = encode(0);
+  for (uint64_t c = 0; c < nch && rc == TGPU_OK; ++c) {
+    Slot& sl = slot[c % 2];
+    if (c + 1 < nch) rc = upload(c + 1);  // the host builds chunk c+1 while c encodes
+    if (rc) break;
+    tgpu_status cs{};
+    uint64_t done = 0, bytes = 0;
+    int code = tgpu_context_wait(p->c[c % 2], senc, &cs, &done, &bytes);
+    if (code == TGPU_ERR_OUTPUT_OVERFLOW) {
+      // the slot's output was too small for this chunk: size it exactly
+      uint64_t need = 0;
+      tgpu_status ss{};
+      DevBuf offs;
+      if (!offs.alloc((sl.m + 1) * 8)) {
+        rc = TGPU_ERR_HIP;
+        break;
+      }
+      code = tgpu_encoded_size(p->c[c % 2], schema, protocol, sl.rec.p, sl.m, sl.lst.p,
+                               (uint64_t*)offs.p, senc, &ss, &need);
+      if (code == TGPU_OK) {
+        if (!grow(sl.out, sl.out_cap, need + 16)) {
+          rc = TGPU_ERR_HIP;
+          break;
+        }
+        code = tgpu_encode_batch(p->c[c % 2], schema, protocol, sl.rec.p, sl.m, sl.str.p,
+                                 sl.lst.p, sl.out.p, sl.out_cap, nullptr, senc, &cs, &bytes);
+      } else {
+        cs = ss;
+        bytes = 0;
+      }
+    }
+    if (code == TGPU_ERR_HIP) {
+      rc = TGPU_ERR_HIP;
+      break;
+    }
+    // the chunk's wire (or, on an error, the records before it) goes out
+    if (bytes) {
+      void* dst = reserve(user, bytes);
+      if (!dst || hipMemcpyAsync(dst, sl.out.p, bytes, hipMemcpyDeviceToHost, sout) != hipSuccess ||
+          hipEventRecord(sl.out_done, sout) != hipSuccess) {
+        rc = dst ? TGPU_ERR_HIP : TGPU_ERR_OUTPUT_OVERFLOW;
+        if (!dst) set_status(st, TGPU_ERR_OUTPUT_OVERFLOW, c * K, total);
+        break;
+      }
+      total += bytes;
+    }
+    if (code != TGPU_OK) {
+      (void)hipStreamSynchronize(sout);
+      if (st) {
+        *st = cs;
+        st->record = c * K + cs.record;
+        st->byte_offset = total - bytes + cs.byte_offset;
+      }
+      if (out_size) *out_size = total;
+      (void)hipStreamSynchronize(sin);
+      return code;
+    }
+    if (c + 1 < nch) rc = encode(c + 1);
+  }
+  (void)hipStreamSynchronize(sin);
+  (void)hipStreamSynchronize(senc);
+  (void)hipStreamSynchronize(sout);
+  if (rc) {
+    if (rc != TGPU_ERR_OUTPUT_OVERFLOW) set_status(st, rc, 0, 0);
+    if (out_size) *out_size = total;
+    return rc;
+  }
+  set_status(st, TGPU_OK, n, 0);
+  if (out_size) *out_size = total;
+  return TGPU_OK;
 }
 
 int tgpu_encoded_size_host(tgpu_context* ctx, const tgpu_schema* schema, int protocol,

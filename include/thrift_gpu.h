@@ -507,6 +507,54 @@ int tgpu_encode_host_ex(tgpu_context* ctx, const tgpu_schema* schema, int protoc
                         void* host_out, uint64_t out_capacity, uint64_t* host_out_offsets,
                         tgpu_status* st, uint64_t* out_size);
 
+/*
+ * Host-memory batches of any schema, chunk-pipelined. Decode: the stream
+ * goes to the device in chunk_bytes pieces on a copy stream while the
+ * records beginning in each piece are indexed and decoded (the piece after
+ * it must be resident: a record may continue there) and the previous
+ * piece's records and list-arena slice come back on a third stream; every
+ * finished range of records [r0, r1) is announced through on_chunk (may be
+ * NULL) while later chunks are still moving, so a caller can materialize
+ * them meanwhile (host_records / host_arena as for tgpu_decode_host_ex; the
+ * arena slice of a range is arena_scale x its wire bytes). Any chunk that
+ * does not finish cleanly (a malformed record, more records than
+ * n_records, a record longer than a piece) sends the whole batch through
+ * the resident pass, so results and status are exactly
+ * tgpu_decode_host_ex's; on_chunk then reports [r0, n_decoded + 1).
+ * chunk_bytes 0 = 64 MiB. Blocking.
+ */
+typedef void (*tgpu_chunk_fn)(void* user, uint64_t r0, uint64_t r1);
+int tgpu_decode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                            const void* host_in, uint64_t in_len, uint64_t n_records,
+                            void* host_records, void* host_arena, uint64_t arena_capacity,
+                            const tgpu_limits* limits, uint64_t chunk_bytes,
+                            tgpu_chunk_fn on_chunk, void* user, tgpu_status* st,
+                            uint64_t* n_decoded, uint64_t* consumed);
+/*
+ * Encode: the caller's fill(user, r0, r1, &form) provides the device form of
+ * records [r0, r1) (records, and the string / list bases their spans are
+ * relative to: each chunk its own) just before the chunk is needed, so the
+ * caller builds chunk k+1 on the host while the device encodes chunk k;
+ * reserve(user, bytes) returns where a chunk's `bytes` wire bytes go (an
+ * IOBufQueue::preallocate), written in record order. The buffers fill gives
+ * must stay valid until the next-but-one fill call. chunk_records 0 = 1 Mi.
+ * Status as tgpu_encode_batch (records relative to the batch; the wire of
+ * the records before a failing one has been handed to reserve). Blocking.
+ */
+typedef struct tgpu_host_form {
+  const void* records;
+  const void* strings;
+  uint64_t strings_len;
+  const void* lists;
+  uint64_t lists_len;
+} tgpu_host_form;
+typedef int (*tgpu_fill_fn)(void* user, uint64_t r0, uint64_t r1, tgpu_host_form* form);
+typedef void* (*tgpu_reserve_fn)(void* user, uint64_t bytes);
+int tgpu_encode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                            uint64_t n_records, uint64_t chunk_records, tgpu_fill_fn fill,
+                            tgpu_reserve_fn reserve, void* user, tgpu_status* st,
+                            uint64_t* out_size);
+
 /* Exact wire size of host-memory records (tgpu_encoded_size over host
  * buffers; host_out_offsets, n+1 entries, may be NULL): what an encode into
  * an IOBufQueue preallocates. Blocking. */

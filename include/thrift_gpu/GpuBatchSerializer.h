@@ -33,6 +33,9 @@
 #include <string>
 #include <utility>
 #include <vector>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 
 #include <memory>
 
@@ -447,50 +450,149 @@ class GpuBatchSerializer {
    * with COPY semantics, Protocol.h:406-454) through `binding`. out[0..n)
    * are default-constructed T. Returns bytes consumed; throws like the
    * reference on the first failing record, the records before it set (the
-   * failing one partially, as the reference leaves it). */
+   * failing one partially, as the reference leaves it).
+   * The device pass is chunk-pipelined (tgpu_decode_host_chunks): while
+   * later chunks cross PCIe and decode, a host thread materializes the
+   * records of the finished ones (materialize_threads() threads each). */
   template <class T>
   uint64_t deserializeBatch(const IOBuf* buf, T* out, uint64_t n, const HostStruct& binding) {
-    const std::vector<uint8_t> in = coalesced(buf);
+    std::vector<uint8_t> joined;
+    const uint8_t* in = nullptr;
+    uint64_t len = 0;
+    if (buf && !buf->isChained()) {
+      in = buf->data();
+      len = buf->length();
+    } else {
+      joined = coalesced(buf);
+      in = joined.data();
+      len = joined.size();
+    }
     const uint32_t S = schema_.recordSize();
-    std::vector<uint8_t> recs(n * S + 16);
-    const uint64_t acap = in.size() * tgpu_schema_arena_scale(schema_.get(), Protocol::kId);
-    std::vector<uint8_t> arena(acap + 16);
+    std::unique_ptr<uint8_t[]> recs(new uint8_t[n * S + 16]);
+    const uint64_t acap = len * tgpu_schema_arena_scale(schema_.get(), Protocol::kId);
+    std::unique_ptr<uint8_t[]> arena(new uint8_t[acap + 16]);
+    // finished record ranges, materialized in order by one host thread
+    struct Feed {
+      std::mutex mu;
+      std::condition_variable cv;
+      std::vector<std::pair<uint64_t, uint64_t>> ranges;
+      bool closed = false;
+    } feed;
+    const SchemaTables tables = schema_.tables();
+    std::thread worker([&] {
+      size_t next = 0;
+      for (;;) {
+        std::pair<uint64_t, uint64_t> r;
+        {
+          std::unique_lock<std::mutex> lk(feed.mu);
+          feed.cv.wait(lk, [&] { return feed.closed || next < feed.ranges.size(); });
+          if (next == feed.ranges.size()) return;
+          r = feed.ranges[next++];
+        }
+        materialize(tables, recs.get() + r.first * S, r.second - r.first, S, in, arena.get(),
+                    binding, out + r.first, sizeof(T));
+      }
+    });
+    auto on_chunk = [](void* u, uint64_t r0, uint64_t r1) {
+      Feed& f = *static_cast<Feed*>(u);
+      {
+        std::lock_guard<std::mutex> lk(f.mu);
+        f.ranges.emplace_back(r0, r1);
+      }
+      f.cv.notify_one();
+    };
     tgpu_status st{};
     uint64_t done = 0, consumed = 0;
-    tgpu_decode_host_ex(ctx_, schema_.get(), Protocol::kId, in.data(), in.size(), n, recs.data(),
-                        acap ? arena.data() : nullptr, acap, &limits_, &st, &done, &consumed);
-    const uint64_t m = st.code == TGPU_OK ? n : (st.exc_class == TGPU_EXC_RUNTIME ? 0 : done + 1);
-    materialize(schema_.tables(), recs.data(), std::min(m, n), S, in.data(), arena.data(),
-                binding, out, sizeof(T));
+    tgpu_decode_host_chunks(ctx_, schema_.get(), Protocol::kId, in, len, n, recs.get(),
+                            acap ? arena.get() : nullptr, acap, &limits_, 0, on_chunk, &feed, &st,
+                            &done, &consumed);
+    {
+      std::lock_guard<std::mutex> lk(feed.mu);
+      feed.closed = true;
+    }
+    feed.cv.notify_one();
+    worker.join();
     if (st.code != TGPU_OK) rethrow(st);
     return consumed;
   }
 
   /* serialize of codegen'd objects appended to an IOBufQueue: N x
-   * Serializer::serialize(obj, &queue) (Serializer.h:136-148). The exact
-   * size is computed first (tgpu_encoded_size_host), one preallocate() of
-   * it is filled by the device encoder. Returns the bytes appended. */
+   * Serializer::serialize(obj, &queue) (Serializer.h:136-148). Chunk-
+   * pipelined (tgpu_encode_host_chunks): the host builds chunk k+1's device
+   * form (materialize_threads() threads) while the device encodes chunk k,
+   * and each chunk's wire lands in a preallocate() of its exact size.
+   * Returns the bytes appended. */
   template <class T>
   uint64_t serializeBatch(const T* in, uint64_t n, const HostStruct& binding, IOBufQueue* out) {
-    const uint32_t S = schema_.recordSize();
-    detail::DeviceForm form = dematerialize(schema_.tables(), S, in, n, sizeof(T), binding);
-    form.strings.resize(form.strings.size() + 16);
-    form.lists.resize(form.lists.size() + 16);
+    constexpr uint64_t kChunk = 1ull << 20;  // records per chunk
+    const uint64_t nch = (n + kChunk - 1) / kChunk;
+    // a host thread builds the chunks' device forms ahead (3 slots: the one
+    // being uploaded, the one the library keeps until the next-but-one fill,
+    // the next one being built)
+    struct Ctx {
+      const T* in;
+      const HostStruct* binding;
+      SchemaTables tables;
+      uint32_t S;
+      uint64_t n, nch;
+      detail::DeviceForm form[3];
+      uint64_t built = 0, taken = 0;  // chunks built / handed to the library
+      std::mutex mu;
+      std::condition_variable cv;
+      bool stop = false;
+      IOBufQueue* out;
+    } c{in, &binding, schema_.tables(), schema_.recordSize(), n, nch, {}, 0, 0, {}, {}, false, out};
+    std::thread producer([&c] {
+      for (uint64_t k = 0; k < c.nch; ++k) {
+        {
+          std::unique_lock<std::mutex> lk(c.mu);
+          // slot k % 3 is free once the library took chunk k - 1 (it keeps
+          // at most chunks k - 2, k - 1)
+          c.cv.wait(lk, [&] { return c.stop || c.taken + 2 > k; });
+          if (c.stop) return;
+        }
+        const uint64_t r0 = k * kChunk, r1 = std::min(c.n, r0 + kChunk);
+        c.form[k % 3] = dematerialize(c.tables, c.S, c.in + r0, r1 - r0, sizeof(T), *c.binding);
+        {
+          std::lock_guard<std::mutex> lk(c.mu);
+          c.built = k + 1;
+        }
+        c.cv.notify_all();
+      }
+    });
+    auto fill = [](void* u, uint64_t r0, uint64_t, tgpu_host_form* f) -> int {
+      Ctx& x = *static_cast<Ctx*>(u);
+      const uint64_t k = r0 / kChunk;
+      std::unique_lock<std::mutex> lk(x.mu);
+      x.cv.wait(lk, [&] { return x.built > k; });
+      x.taken = k + 1;
+      lk.unlock();
+      x.cv.notify_all();
+      detail::DeviceForm& d = x.form[k % 3];
+      f->records = d.records.data();
+      f->strings = d.strings.data();
+      f->strings_len = d.strings.size();
+      f->lists = d.lists.data();
+      f->lists_len = d.lists.size();
+      return 0;
+    };
+    auto reserve = [](void* u, uint64_t bytes) -> void* {
+      IOBufQueue& q = *static_cast<Ctx*>(u)->out;
+      auto space = q.preallocate(bytes, bytes);
+      q.postallocate(bytes);  // filled before serializeBatch returns
+      return space.first;
+    };
     tgpu_status st{};
-    uint64_t total = 0;
-    tgpu_encoded_size_host(ctx_, schema_.get(), Protocol::kId, form.records.data(), n,
-                           form.lists.data(), form.lists.size(), nullptr, &st, &total);
-    if (st.code != TGPU_OK) rethrow(st);
-    auto space = out->preallocate(total ? total : 1, total ? total : 1);
     uint64_t size = 0;
-    tgpu_encode_host_ex(ctx_, schema_.get(), Protocol::kId, form.records.data(), n,
-                        form.strings.data(), form.strings.size(), form.lists.data(),
-                        form.lists.size(), space.first, space.second, nullptr, &st, &size);
-    if (st.code != TGPU_OK) {
-      out->postallocate(0);
-      rethrow(st);
+    tgpu_encode_host_chunks(ctx_, schema_.get(), Protocol::kId, n, kChunk, fill, reserve, &c,
+                            &st, &size);
+    {
+      std::lock_guard<std::mutex> lk(c.mu);
+      c.stop = true;
     }
-    out->postallocate(size);
+    c.cv.notify_all();
+    producer.join();
+    if (st.code != TGPU_OK) rethrow(st);
     return size;
   }
 

@@ -19,10 +19,13 @@
 #ifndef THRIFT_GPU_HOST_BINDING_H_
 #define THRIFT_GPU_HOST_BINDING_H_
 
+#include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -394,28 +397,150 @@ inline void writeStruct(const SchemaTables& sc, uint32_t si, const uint8_t* host
   }
 }
 
+// ---- spans of one thread's part moved to the merged buffers -------------------
+/* Adds sd to every string span and ld to every list / boxed span of a value
+   (the thread's records, and its part of the merged list buffer `lists`
+   whose contents it reaches through spans already moved by ld). */
+void rebaseStruct(const SchemaTables& sc, uint32_t si, uint8_t* obj, uint8_t* lists,
+                  uint64_t sd, uint64_t ld);
+void rebaseContainer(const SchemaTables& sc, const CType& c, uint8_t* p, uint8_t* lists,
+                     uint64_t sd, uint64_t ld);
+inline void rebaseSpan(uint8_t* p, uint64_t d) {
+  tgpu_span s = loadSpan(p);
+  if (s.length) {
+    s.offset += d;
+    std::memcpy(p, &s, sizeof(s));
+  }
+}
+inline void rebaseValue(const SchemaTables& sc, uint32_t t, int32_t si, uint32_t ti, uint8_t* p,
+                        uint8_t* lists, uint64_t sd, uint64_t ld) {
+  if (t == TGPU_T_STRING) rebaseSpan(p, sd);
+  else if (t == TGPU_T_STRUCT) rebaseStruct(sc, (uint32_t)si, p, lists, sd, ld);
+  else if (isContainer(t)) rebaseContainer(sc, ctypeNode(sc, ti), p, lists, sd, ld);
+}
+inline bool hasSpans(uint32_t t) {
+  return t == TGPU_T_STRING || t == TGPU_T_STRUCT || isContainer(t);
+}
+inline void rebaseContainer(const SchemaTables& sc, const CType& c, uint8_t* p, uint8_t* lists,
+                            uint64_t sd, uint64_t ld) {
+  rebaseSpan(p, ld);
+  const tgpu_span s = loadSpan(p);
+  const bool is_map = c.ttype == TGPU_T_MAP;
+  const uint32_t v = is_map ? c.val : c.elem;
+  if (!hasSpans(v) && !(is_map && hasSpans(c.elem))) return;
+  const int32_t ksi = is_map ? keyStruct(sc, c) : -1;
+  const uint32_t ks = is_map ? slotBytes(sc, c.elem, ksi) : 0;
+  const uint32_t es = ks + slotBytes(sc, v, c.si);
+  for (uint32_t i = 0; i < s.length; ++i) {
+    uint8_t* e = lists + s.offset + (uint64_t)i * es;
+    if (is_map) rebaseValue(sc, c.elem, ksi, keyNode(c), e, lists, sd, ld);
+    rebaseValue(sc, v, c.si, c.ti, e + ks, lists, sd, ld);
+  }
+}
+inline void rebaseStruct(const SchemaTables& sc, uint32_t si, uint8_t* obj, uint8_t* lists,
+                         uint64_t sd, uint64_t ld) {
+  const tgpu_struct_desc& d = sc.s[si];
+  for (uint32_t k = 0; k < d.num_fields; ++k) {
+    const tgpu_field_desc& f = sc.f[d.first_field + k];
+    uint8_t* m = obj + f.member_offset;
+    if (isBoxed(f)) {
+      rebaseSpan(m, ld);
+      const tgpu_span b = loadSpan(m);
+      if (b.length) rebaseStruct(sc, (uint32_t)f.struct_index, lists + b.offset, lists, sd, ld);
+    } else if (isContainer(f.ttype)) {
+      rebaseContainer(sc, ctypeOf(f), m, lists, sd, ld);
+    } else {
+      rebaseValue(sc, f.ttype, f.struct_index, 0, m, lists, sd, ld);
+    }
+  }
+}
+
+}  // namespace detail
+
+/* Host threads the batch materialization uses: TGPU_HOST_THREADS, else the
+   hardware's, at most 16 (the GPU boxes' CPU share per GPU). */
+inline unsigned materialize_threads() {
+  static const unsigned t = [] {
+    const char* e = std::getenv("TGPU_HOST_THREADS");
+    const unsigned v = e ? (unsigned)std::atoi(e) : std::thread::hardware_concurrency();
+    return std::max(1u, std::min(v ? v : 1u, 16u));
+  }();
+  return t;
+}
+
+namespace detail {
+/* fn(t, begin, end) over contiguous parts of [0, n) on up to T threads. */
+template <class F>
+void parallel_parts(uint64_t n, unsigned T, F&& fn) {
+  if (T <= 1 || n < 4096) {
+    fn(0u, (uint64_t)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  const uint64_t per = (n + T - 1) / T;
+  for (unsigned t = 0; t < T; ++t) {
+    const uint64_t b = std::min<uint64_t>(n, t * per), e = std::min<uint64_t>(n, b + per);
+    if (b < e) th.emplace_back([&fn, t, b, e] { fn(t, b, e); });
+  }
+  for (auto& x : th) x.join();
+}
 }  // namespace detail
 
 /* Decoded device-form records (host copies) -> host objects T (stride
-   sizeof(T), default-constructed by the caller). */
+   sizeof(T), default-constructed by the caller); records are independent,
+   so contiguous parts go to materialize_threads() threads. */
 inline void materialize(const SchemaTables& sc, const uint8_t* records, uint64_t n,
                         uint32_t record_size, const uint8_t* strings, const uint8_t* arena,
                         const HostStruct& hs, void* objects, size_t stride) {
   const detail::Sources src{strings, arena};
-  for (uint64_t i = 0; i < n; ++i)
-    detail::readStruct(sc, 0, records + i * record_size, src, hs,
-                       (uint8_t*)objects + i * stride);
+  detail::parallel_parts(n, materialize_threads(), [&](unsigned, uint64_t b, uint64_t e) {
+    for (uint64_t i = b; i < e; ++i)
+      detail::readStruct(sc, 0, records + i * record_size, src, hs,
+                         (uint8_t*)objects + i * stride);
+  });
 }
 
-/* Host objects T -> the encode input (records + string base + list base). */
+/* Host objects T -> the encode input (records + string base + list base).
+   Each thread writes its part's records in place and its strings / lists
+   into buffers of its own; the parts' buffers are then concatenated and
+   their spans moved by the part's base. */
 inline detail::DeviceForm dematerialize(const SchemaTables& sc, uint32_t record_size,
                                         const void* objects, uint64_t n, size_t stride,
                                         const HostStruct& hs) {
   detail::DeviceForm out;
   out.records.assign(n * record_size, 0);
-  for (uint64_t i = 0; i < n; ++i)
-    detail::writeStruct(sc, 0, (const uint8_t*)objects + i * stride, hs, out, i * record_size,
-                        &out.records);
+  const unsigned T = (n < 4096) ? 1u : materialize_threads();
+  std::vector<detail::DeviceForm> part(T);
+  std::vector<std::pair<uint64_t, uint64_t>> range(T, {0, 0});
+  detail::parallel_parts(n, T, [&](unsigned t, uint64_t b, uint64_t e) {
+    range[t] = {b, e};
+    detail::DeviceForm& f = T == 1 ? out : part[t];
+    for (uint64_t i = b; i < e; ++i)
+      detail::writeStruct(sc, 0, (const uint8_t*)objects + i * stride, hs, f, i * record_size,
+                          &out.records);
+  });
+  if (T == 1) return out;
+  std::vector<uint64_t> sbase(T), lbase(T);
+  uint64_t S = 0, L = 0;
+  for (unsigned t = 0; t < T; ++t) {
+    sbase[t] = S;
+    lbase[t] = L;
+    S += part[t].strings.size();
+    L = (L + part[t].lists.size() + 7) & ~7ull;
+  }
+  out.strings.resize(S);
+  out.lists.resize(L);
+  // each part's thread copies its buffers into place and moves its spans
+  // (the part boundaries are the same as in the write above)
+  detail::parallel_parts(n, T, [&](unsigned t, uint64_t b, uint64_t e) {
+    if (!part[t].strings.empty())
+      std::memcpy(out.strings.data() + sbase[t], part[t].strings.data(), part[t].strings.size());
+    if (!part[t].lists.empty())
+      std::memcpy(out.lists.data() + lbase[t], part[t].lists.data(), part[t].lists.size());
+    for (uint64_t i = b; i < e; ++i)
+      detail::rebaseStruct(sc, 0, out.records.data() + i * record_size, out.lists.data(),
+                           sbase[t], lbase[t]);
+  });
   return out;
 }
 
