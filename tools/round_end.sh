@@ -12,7 +12,7 @@ cat "$OUT/bench_default.json"
 (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_default" -o run -- python3 "$OLDPWD/bench.py" --steps 5 --warmup 1 --no-copy-ceiling --no-cpu-baseline) > "$OUT/prof_default.log" 2>&1 || { echo "prof failed $?"; tail -20 "$OUT/prof_default.log"; exit 4; }
 timeout -k 10 300 python bench.py --config 1 > "$OUT/bench_c1.json" 2> "$OUT/bench_c1.err" || { echo "bench c1 failed $?"; exit 5; }
 for c in ${CONFIGS:-3 4 5}; do
-  EXTRA="--transcode"; [ $c != 5 ] && EXTRA="$EXTRA --host-start"
+  EXTRA="--transcode"; [ $c != 5 ] && EXTRA="$EXTRA --host-start --host-batch"
   timeout -k 10 600 python bench.py --config $c --steps 10 --warmup 2 --no-copy-ceiling $EXTRA > "$OUT/bench_c$c.json" 2> "$OUT/bench_c$c.err" || { echo "bench c$c failed $?"; tail -20 "$OUT/bench_c$c.err"; exit 5; }
   tail -c 300 "$OUT/bench_c$c.json"
 done
