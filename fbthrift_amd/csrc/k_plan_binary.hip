@@ -186,12 +186,7 @@ __global__ __launch_bounds__(T) void plan_binary_decode_kernel(
 }
 
 
-// kPlain: no zero pass and no LDS atomics on the common dwords — every byte
-// of a record belongs to exactly one item (headers, values, STOPs), so a
-// dword is written whole by the item holding its byte 0 (its own bytes, zeros
-// after them); after a barrier, an item that starts inside a dword another
-// item holds ORs its first bytes into it.
-template <uint32_t T, bool kNT, bool kPlain = false>
+template <uint32_t T, bool kNT>
 __global__ __launch_bounds__(T) void plan_binary_encode_kernel(
     const FixedPlan* __restrict__ pp, const unsigned long long* __restrict__ recs, uint64_t n,
     uint32_t value_words, uint8_t* __restrict__ out, uint64_t* __restrict__ offsets,
@@ -222,22 +217,19 @@ __global__ __launch_bounds__(T) void plan_binary_encode_kernel(
   // 2. zero the wire tile, plan -> LDS
   uint8_t* gout = out + tile0 * L;
   const uint32_t osh = (uint32_t)((uintptr_t)gout & 15);
-  if (!kPlain) {
+  {
     const uint4 z = {0u, 0u, 0u, 0u};
     for (uint32_t i = threadIdx.x; i < (wreg >> 4); i += T) ((uint4*)smem)[i] = z;
-  } else if (threadIdx.x == 0 && (osh & 3)) {
-    ((uint32_t*)smem)[osh >> 2] = 0;  // the tile's first dword: its byte 0 is no item's
   }
   for (uint32_t i = threadIdx.x; i < (uint32_t)(sizeof(FixedPlan) / 16); i += T)
     ((uint4*)P)[i] = ((const uint4*)pp)[i];
   __syncthreads();
 
-  // 3. OR each owned item's wire bytes into the tile (kPlain: two phases)
+  // 3. OR each owned item's wire bytes into the tile
   uint32_t* w32 = (uint32_t*)smem;
   bool bad_bool = false;
   uint32_t bad_rec = 0;
-  for (int phase = 0; phase < (kPlain ? 2 : 1); ++phase) {
-    if (phase) __syncthreads();
+  {
     uint32_t r = threadIdx.x / Q, j = threadIdx.x - r * Q;
     const uint32_t sr = T / Q, sj = T - sr * Q;
 #pragma unroll
@@ -275,19 +267,10 @@ __global__ __launch_bounds__(T) void plan_binary_encode_kernel(
           const unsigned long long Hlo = Flo << (8 * s);
           const unsigned long long Hhi = (Fhi << (8 * s)) | (s ? (Flo >> (64 - 8 * s)) : 0);
           const uint32_t nb = s + h + it.width;
-          if (!kPlain) {
-            atomicOr(&w32[d], (uint32_t)Hlo);
-            if (nb > 4) atomicOr(&w32[d + 1], (uint32_t)(Hlo >> 32));
-            if (nb > 8) atomicOr(&w32[d + 2], (uint32_t)Hhi);
-            if (nb > 12) atomicOr(&w32[d + 3], (uint32_t)(Hhi >> 32));
-          } else if (phase == 0) {  // the dwords whose byte 0 is this item's
-            if (!s) w32[d] = (uint32_t)Hlo;
-            if (nb > 4) w32[d + 1] = (uint32_t)(Hlo >> 32);
-            if (nb > 8) w32[d + 2] = (uint32_t)Hhi;
-            if (nb > 12) w32[d + 3] = (uint32_t)(Hhi >> 32);
-          } else if (s) {  // this item's head, inside the previous item's dword
-            atomicOr(&w32[d], (uint32_t)Hlo);
-          }
+          atomicOr(&w32[d], (uint32_t)Hlo);
+          if (nb > 4) atomicOr(&w32[d + 1], (uint32_t)(Hlo >> 32));
+          if (nb > 8) atomicOr(&w32[d + 2], (uint32_t)Hhi);
+          if (nb > 12) atomicOr(&w32[d + 3], (uint32_t)(Hhi >> 32));
         }
       }
       r += sr;
@@ -328,7 +311,7 @@ __global__ __launch_bounds__(T) void plan_binary_encode_kernel(
 // TGPU_PLAN_DECODE="T,glds,pair,nt" / TGPU_PLAN_ENCODE="T,nt" override them for
 // tuning runs (tools/kbench.py).
 struct DecVariant { uint32_t T; int glds, pair, nt; };
-struct EncVariant { uint32_t T; int nt; int plain; };
+struct EncVariant { uint32_t T; int nt; };
 
 DecVariant dec_variant() {
   // tuned on MI355X (profiles/r01_kbench_sweep.log): 512-record tiles, LDS-DMA
@@ -342,12 +325,11 @@ DecVariant dec_variant() {
   return v;
 }
 EncVariant enc_variant() {
-  EncVariant v{512, 1, 0};  // tuned: 512-record tiles, non-temporal loads/stores
+  EncVariant v{512, 1};  // tuned: 512-record tiles, non-temporal loads/stores
   if (const char* s = getenv("TGPU_PLAN_ENCODE")) {
     unsigned t = 256;
-    int nt = 0, plain = 0;
-    const int k = sscanf(s, "%u,%d,%d", &t, &nt, &plain);
-    if (k >= 2) v = EncVariant{t, nt, k == 3 ? plain : 0};
+    int nt = 0;
+    if (sscanf(s, "%u,%d", &t, &nt) == 2) v = EncVariant{t, nt};
   }
   return v;
 }
@@ -399,14 +381,14 @@ hipError_t launch_plan_binary_encode(const FixedPlan* p, const FixedPlan* d_p,
   const uint64_t blocks = (n + v.T - 1) / v.T;
   const uint32_t lds = wire_region(v.T, p->wire_len) + (uint32_t)sizeof(FixedPlan);
   const auto* r = (const unsigned long long*)recs;
-#define TGPU_ENC(TT, N, PL)                                                                    \
-  if (v.T == TT && v.nt == N && v.plain == PL) {                                               \
-    hipLaunchKernelGGL((plan_binary_encode_kernel<TT, N, PL>), dim3((uint32_t)blocks), dim3(TT), \
-                       lds, stream, d_p, r, n, value_words, out, offsets, res);                \
+#define TGPU_ENC(TT, N)                                                                        \
+  if (v.T == TT && v.nt == N) {                                                                \
+    hipLaunchKernelGGL((plan_binary_encode_kernel<TT, N>), dim3((uint32_t)blocks), dim3(TT), lds, \
+                       stream, d_p, r, n, value_words, out, offsets, res);                     \
     return hipGetLastError();                                                                  \
   }
-  TGPU_ENC(128, 0, 0) TGPU_ENC(128, 1, 0) TGPU_ENC(256, 0, 0) TGPU_ENC(256, 1, 0)
-  TGPU_ENC(512, 0, 0) TGPU_ENC(512, 1, 0) TGPU_ENC(256, 1, 1) TGPU_ENC(512, 1, 1)
+  TGPU_ENC(128, 0) TGPU_ENC(128, 1) TGPU_ENC(256, 0) TGPU_ENC(256, 1) TGPU_ENC(512, 0)
+  TGPU_ENC(512, 1)
 #undef TGPU_ENC
   return hipErrorInvalidValue;
 }
