@@ -44,12 +44,17 @@ __device__ __forceinline__ Reader decode_one(const DecodeArgs& a, uint64_t i, in
   return decode_record<P>(a, i, lane);
 }
 
-// Indexed streams: one lane per record, records independent.
+// Indexed streams: one lane per record, records independent. scap: dynamic
+// LDS bytes for the schema tables (stage_schema).
 template <int P>
-__global__ __launch_bounds__(256) void general_decode_kernel(DecodeArgs a) {
+__global__ __launch_bounds__(256) void general_decode_kernel(DecodeArgs a, uint32_t scap) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sch[];
+  DecodeArgs b = a;
+  b.sc = stage_schema(a.sc, sch, scap);
+  __syncthreads();
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-    const Reader r = decode_one<P>(a, i, -1);
+    const Reader r = decode_one<P>(b, i, -1);
     if (!r.ok()) defer_or_fail(r, a.deep, &a.res->first_fail, i);
   }
 }
@@ -62,8 +67,11 @@ __global__ __launch_bounds__(256) void general_decode_kernel(DecodeArgs a) {
 // HBM, so every status is the stream's own; a tile too large reads from HBM.
 template <int P>
 __global__ __launch_bounds__(256) void general_decode_tile_kernel(DecodeArgs a,
-                                                                  uint32_t tile_cap) {
+                                                                  uint32_t tile_cap,
+                                                                  uint32_t scap) {
   extern __shared__ __attribute__((aligned(16))) uint8_t tile[];
+  DecodeArgs b = a;  // the schema tables after the wire tile
+  b.sc = stage_schema(a.sc, (uint32_t*)(tile + tile_cap + 16), scap);
   const uint64_t r0 = (uint64_t)blockIdx.x * 256;
   const uint64_t r1 = min(r0 + 256, a.n);
   const uint64_t b0 = a.offs[r0], b1 = a.offs[r1];
@@ -86,7 +94,7 @@ __global__ __launch_bounds__(256) void general_decode_tile_kernel(DecodeArgs a,
   // one decode_record call site (the copy, then HBM when the copy failed)
   Reader r;
   for (int from_lds = staged ? 1 : 0;; from_lds = 0) {
-    r = decode_record<P>(a, i, -1, kIndexed, from_lds ? tile : nullptr, a0, b1);
+    r = decode_record<P>(b, i, -1, kIndexed, from_lds ? tile : nullptr, a0, b1);
     if (!from_lds || r.ok() || r.err == kErrDeep) break;
   }
   if (!r.ok()) defer_or_fail(r, a.deep, &a.res->first_fail, i);
@@ -244,14 +252,16 @@ __device__ __forceinline__ void attach_slab(Writer& w, const DeepArgs& d, int la
   w.deep_cap = d.slab_frames;
 }
 
-// (out of line: inlined into the size kernel, the writer made this
-// compiler's inliner crash, ROCm 7.2 clang 22)
+// Size of record i; lane >= 0: a deep-pass lane (HBM frames).
 template <int P>
-__device__ __attribute__((noinline)) Writer size_one(const EncodeArgs& a, uint64_t i,
-                                                     int lane = -1) {
+__device__ __forceinline__ Writer size_one(const EncodeArgs& a, uint64_t i, int lane = -1) {
   Writer w{nullptr, 0, 0, 0, 0};
-  attach_slab(w, a.deep, lane);
-  write_record<P>(w, a.sc, a.recs + i * a.rec_size, a.sbase, a.lbase);
+  if (lane >= 0 && a.deep.slabs) {
+    attach_slab(w, a.deep, lane);
+    write_record<P, true>(w, a.sc, a.recs + i * a.rec_size, a.sbase, a.lbase);
+  } else {
+    write_record<P>(w, a.sc, a.recs + i * a.rec_size, a.sbase, a.lbase);
+  }
   return w;
 }
 
@@ -285,11 +295,15 @@ __device__ __forceinline__ unsigned long long block_exscan(unsigned long long v)
 // A record nested past the private frames is sized 0 here and deferred: the
 // deep size pass adds its size to its tile's sum before the scan.
 template <int P>
-__global__ __launch_bounds__(256) void encode_size_kernel(EncodeArgs a) {
+__global__ __launch_bounds__(256) void encode_size_kernel(EncodeArgs a, uint32_t scap) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sch[];
+  EncodeArgs b = a;
+  b.sc = stage_schema(a.sc, sch, scap);
+  __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   unsigned long long sz = 0;
   if (i < a.n) {
-    const Writer w = size_one<P>(a, i);
+    const Writer w = size_one<P>(b, i);
     if (w.err == kErrDeep) a.deep.list[atomicAdd(a.deep.count, 1ull)] = i;
     else if (!w.ok()) atomicMin(&a.res->first_fail, (unsigned long long)i);
     else sz = w.pos;
@@ -317,7 +331,10 @@ __global__ __launch_bounds__(64) void deep_size_kernel(EncodeArgs a) {
 }
 
 template <int P>
-__global__ __launch_bounds__(256) void encode_write_kernel(EncodeArgs a) {
+__global__ __launch_bounds__(256) void encode_write_kernel(EncodeArgs a, uint32_t scap) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t sch[];
+  const DevSchema sc = stage_schema(a.sc, sch, scap);
+  __syncthreads();
   const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
   const unsigned long long sz = i < a.n ? a.offs[i] : 0;
   const unsigned long long start = a.block_sums[blockIdx.x] + block_exscan(sz);
@@ -330,7 +347,7 @@ __global__ __launch_bounds__(256) void encode_write_kernel(EncodeArgs a) {
   // (a deferred record stops at its private frames; the deep write pass
   // writes it whole)
   Writer w{a.out, start, a.cap, 0, 0};
-  write_record<P>(w, a.sc, a.recs + i * a.rec_size, a.sbase, a.lbase);
+  write_record<P>(w, sc, a.recs + i * a.rec_size, a.sbase, a.lbase);
 }
 
 template <int P>
@@ -344,7 +361,7 @@ __global__ __launch_bounds__(64) void deep_write_kernel(EncodeArgs a) {
     if (a.res->first_fail <= i) continue;
     Writer w{a.out, start, a.cap, 0, 0};
     attach_slab(w, a.deep, (int)lane);
-    write_record<P>(w, a.sc, a.recs + i * a.rec_size, a.sbase, a.lbase);
+    write_record<P, true>(w, a.sc, a.recs + i * a.rec_size, a.sbase, a.lbase);
   }
 }
 
@@ -375,6 +392,15 @@ __global__ void encode_finish_kernel(EncodeArgs a, uint64_t fixed_len) {
   }
 }
 
+// Dynamic LDS for the schema tables of a general kernel (0: they stay in
+// global memory, when larger than 16 KiB).
+uint32_t schema_stage_bytes(const DevSchema& sc) {
+  const uint32_t b = sc.ns * (uint32_t)sizeof(tgpu_struct_desc) +
+                     sc.nf * (uint32_t)sizeof(tgpu_field_desc) +
+                     sc.nt * (uint32_t)sizeof(tgpu_type_desc);
+  return b <= 16 * 1024 ? (b + 15) & ~15u : 0;
+}
+
 uint32_t grid_for(uint64_t n) {
   const uint64_t b = (n + 255) / 256;
   return (uint32_t)(b < 4096 ? (b ? b : 1) : 4096);
@@ -394,16 +420,20 @@ hipError_t launch_general_decode(const DecodeArgs& a, int protocol, hipStream_t 
     const uint64_t mean = (a.in_len + a.n - 1) / a.n;
     const uint64_t want = ((mean * 256 * 5 / 4 + 15) & ~15ull) + 32;
     // (cap + 16 bytes of dynamic LDS stay within 64 KiB per workgroup)
-    const uint32_t cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 4096), 64 * 1024 - 16);
+    // (cap + 16 + the schema tables stay within 64 KiB per workgroup)
+    const uint32_t sb = schema_stage_bytes(a.sc);
+    const uint32_t cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 4096),
+                                                      64 * 1024 - 16 - sb) & ~15u;
     const uint64_t blocks = (a.n + 255) / 256;
     TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(general_decode_tile_kernel<P_>,
-                                                  dim3((uint32_t)blocks), dim3(256), cap + 16,
-                                                  stream, a, cap));
+                                                  dim3((uint32_t)blocks), dim3(256), cap + 16 + sb,
+                                                  stream, a, cap, sb));
     return hipGetLastError();
   }
   const uint32_t g = grid_for(a.n);
-  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(general_decode_kernel<P_>, dim3(g), dim3(256), 0, stream,
-                       a));
+  const uint32_t sb = schema_stage_bytes(a.sc);
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(general_decode_kernel<P_>, dim3(g), dim3(256), sb,
+                                                stream, a, sb));
   return hipGetLastError();
 }
 
@@ -478,13 +508,16 @@ hipError_t launch_general_encode(const EncodeArgs& a, int protocol, uint64_t n_b
                                  hipStream_t stream) {
   if (a.n == 0) return hipSuccess;
   const dim3 grid((uint32_t)n_blocks);
-  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_size_kernel<P_>, grid, dim3(256), 0, stream, a));
+  const uint32_t sb = schema_stage_bytes(a.sc);
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_size_kernel<P_>, grid, dim3(256), sb, stream, a,
+                                                sb));
   hipError_t e = launch_deep_size(a, protocol, stream);
   if (e != hipSuccess) return e;
   e = launch_scan_tiles(a.block_sums, n_blocks, a.scan_part, &a.res->total_bytes, a.offs + a.n,
                         stream);
   if (e != hipSuccess) return e;
-  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_write_kernel<P_>, grid, dim3(256), 0, stream, a));
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_write_kernel<P_>, grid, dim3(256), sb, stream, a,
+                                                sb));
   if (a.deep.lanes)
     TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(deep_write_kernel<P_>, dim3((a.deep.lanes + 63) / 64),
                                                   dim3(64), 0, stream, a));
@@ -495,7 +528,9 @@ hipError_t launch_general_size(const EncodeArgs& a, int protocol, uint64_t n_blo
                                hipStream_t stream) {
   if (a.n == 0) return hipSuccess;
   const dim3 grid((uint32_t)n_blocks);
-  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_size_kernel<P_>, grid, dim3(256), 0, stream, a));
+  const uint32_t sb = schema_stage_bytes(a.sc);
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_size_kernel<P_>, grid, dim3(256), sb, stream, a,
+                                                sb));
   hipError_t e = launch_deep_size(a, protocol, stream);
   if (e != hipSuccess) return e;
   e = launch_scan_tiles(a.block_sums, n_blocks, a.scan_part, &a.res->total_bytes, a.offs + a.n,

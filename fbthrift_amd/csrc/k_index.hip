@@ -90,7 +90,7 @@ __device__ __forceinline__ int one_record(const IndexArgs& a, uint64_t p, uint64
   // slots after it (the index's scratch stride holds both)
   const uint32_t root = (a.sc.s[0].size + 15) & ~15u;
   dev::Arena A = dev::record_arena<P>(a.sc, nullptr, kDiscardArena, p, scratch + root);
-  dev::read_record<P>(r, a.sc, scratch, A);
+  dev::read_record_any<P>(r, a.sc, scratch, A);
   if (!r.ok()) {
     out.code = r.err;
     out.err_off = r.err_off;

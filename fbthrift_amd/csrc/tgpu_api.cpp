@@ -813,7 +813,8 @@ DevSchema dev_schema(const tgpu_schema* s, int protocol) {
   const uint32_t scale =
       s->nested ? s->region_scale[protocol == TGPU_PROTOCOL_BINARY ? 0 : 1] : 0u;
   return DevSchema{s->d_structs, s->d_fields, s->d_types, (uint32_t)s->structs.size(),
-                   (uint32_t)s->fields.size(), s->str_elems ? 1u : 0u, scale, s->nest_slot, 0u};
+                   (uint32_t)s->fields.size(), s->str_elems ? 1u : 0u, scale, s->nest_slot,
+                   (uint32_t)s->types.size()};
 }
 
 // Scratch bytes per record of a measuring read (stream index): the root

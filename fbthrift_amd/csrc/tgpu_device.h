@@ -941,13 +941,15 @@ __device__ __forceinline__ ReadFrame* slab_read_frames(const Reader& r) {
 // frames below it are saved in `st` (sp of them) only while a child is open
 // (a per-iteration reload of the whole frame from scratch was the general
 // reader's main cost).
-template <int P>
+// kDeep: the reader has an HBM slab (r.deep): every frame there (a
+// compile-time choice, so the bulk kernels keep theirs in scratch).
+template <int P, bool kDeep = false>
 __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, Arena& A) {
   using Pr = Proto<P>;
-  ReadFrame priv[kPrivFrames];
-  ReadFrame* const st = r.deep ? slab_read_frames(r) : priv;
-  const uint32_t cap = r.deep ? (uint32_t)r.deep_cap : (uint32_t)kPrivFrames;
-  const int32_t full = r.deep ? TGPU_ERR_UNSUPPORTED : kErrDeep;
+  ReadFrame priv[kDeep ? 1 : kPrivFrames];
+  ReadFrame* const st = kDeep ? slab_read_frames(r) : priv;
+  const uint32_t cap = kDeep ? (uint32_t)r.deep_cap : (uint32_t)kPrivFrames;
+  const int32_t full = kDeep ? TGPU_ERR_UNSUPPORTED : kErrDeep;
   uint32_t sp = 0;  // frames saved below fr
   ReadFrame fr = struct_frame(0, rec);
   while (r.ok()) {
@@ -1128,6 +1130,42 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, Arena&
   }
 }
 
+// The schema tables in LDS: the general reader and writer look a struct /
+// field / type descriptor up on every field, element and header — dependent
+// loads on each lane's critical path, cheaper from LDS than from the caches.
+// Copies by the whole workgroup (the caller barriers before use); returns sc
+// itself when the tables do not fit `cap` bytes.
+__device__ __forceinline__ uint32_t schema_lds_bytes(const DevSchema& sc) {
+  return sc.ns * (uint32_t)sizeof(tgpu_struct_desc) + sc.nf * (uint32_t)sizeof(tgpu_field_desc) +
+         sc.nt * (uint32_t)sizeof(tgpu_type_desc);
+}
+__device__ __forceinline__ DevSchema stage_schema(const DevSchema& sc, uint32_t* lds, uint32_t cap) {
+  const uint32_t bs = sc.ns * (uint32_t)sizeof(tgpu_struct_desc);
+  const uint32_t bf = sc.nf * (uint32_t)sizeof(tgpu_field_desc);
+  const uint32_t bt = sc.nt * (uint32_t)sizeof(tgpu_type_desc);
+  if (bs + bf + bt > cap) return sc;
+  const uint32_t* src[3] = {(const uint32_t*)sc.s, (const uint32_t*)sc.f, (const uint32_t*)sc.t};
+  const uint32_t words[3] = {bs / 4, bf / 4, bt / 4};
+  uint32_t at = 0;
+  for (int k = 0; k < 3; ++k) {
+    for (uint32_t w = threadIdx.x; w < words[k]; w += blockDim.x) lds[at + w] = src[k][w];
+    at += words[k];
+  }
+  DevSchema d = sc;
+  d.s = (const tgpu_struct_desc*)lds;
+  d.f = (const tgpu_field_desc*)(lds + bs / 4);
+  d.t = (const tgpu_type_desc*)(lds + (bs + bf) / 4);
+  return d;
+}
+
+// read_record with the reader's frames: its slab when it has one.
+template <int P>
+__device__ __forceinline__ void read_record_any(Reader& r, const DevSchema& sc, uint8_t* rec,
+                                                Arena& A) {
+  if (r.deep) read_record<P, true>(r, sc, rec, A);
+  else read_record<P, false>(r, sc, rec, A);
+}
+
 // The arena of one record read: the position rule, or the record's region
 // (scale x its start) for nested schemas; `nest` = per-level element slots
 // when measuring only.
@@ -1195,7 +1233,8 @@ __device__ Reader decode_record(const DecodeArgs& a, uint64_t i, int lane,
     return r;
   }
   Arena A = record_arena<P>(a.sc, a.arena, a.arena_cap, start, nullptr);
-  read_record<P>(r, a.sc, rec, A);
+  if (lane >= 0 && r.deep) read_record<P, true>(r, a.sc, rec, A);
+  else read_record<P, false>(r, a.sc, rec, A);
   if (indexed && r.ok() && a.check_index && r.pos != a.offs[i + 1])
     r.fail(TGPU_ERR_INDEX_MISMATCH, r.pos);
   return r;
@@ -1495,13 +1534,16 @@ __device__ __forceinline__ void write_complex(Writer& w, const DevSchema& sc, ui
   }
 }
 
-template <int P>
+// kDeep: a deep-pass lane (w.deep set): every frame in its HBM slab; else
+// the lane's kPrivFrames private frames (a compile-time choice, so the bulk
+// kernels keep their frames in scratch / registers).
+template <int P, bool kDeep = false>
 __device__ void write_record(Writer& w, const DevSchema& sc, const uint8_t* rec,
                              const uint8_t* sbase, const uint8_t* lbase) {
-  WriteFrame priv[kPrivFrames];
-  WriteFrame* const st = w.deep ? (WriteFrame*)(w.deep + slab_skip_bytes(w.deep_cap)) : priv;
-  const uint32_t cap = w.deep ? (uint32_t)w.deep_cap : (uint32_t)kPrivFrames;
-  const int32_t full = w.deep ? TGPU_ERR_UNSUPPORTED : kErrDeep;
+  WriteFrame priv[kDeep ? 1 : kPrivFrames];
+  WriteFrame* const st = kDeep ? (WriteFrame*)(w.deep + slab_skip_bytes(w.deep_cap)) : priv;
+  const uint32_t cap = kDeep ? (uint32_t)w.deep_cap : (uint32_t)kPrivFrames;
+  const int32_t full = kDeep ? TGPU_ERR_UNSUPPORTED : kErrDeep;
   uint32_t sp = 0;
   st[sp++] = write_frame(sc, 0, rec);
   while (sp > 0 && w.ok()) {

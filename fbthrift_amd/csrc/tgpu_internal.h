@@ -218,7 +218,7 @@ struct DevSchema {
   uint32_t str_elems;   // some list/set/map holds strings: arena scale 4 / 16
   uint32_t bump_scale;  // nested schema: record regions of this scale (0: position rule)
   uint32_t nest_slot;   // nested schema, measuring reads: element slot bytes per level
-  uint32_t pad_;
+  uint32_t nt;          // type-table nodes
 };
 
 struct DecodeArgs {
