@@ -1468,7 +1468,7 @@ __device__ __forceinline__ void container_header(Writer& w, const CType& c, uint
 // elements here (returns true), a container whose elements, keys or values
 // are structs / containers gets a frame (returns false).
 template <int P>
-__device__ bool write_container(Writer& w, const DevSchema& sc, const CType& c,
+__device__ __forceinline__ bool write_container(Writer& w, const DevSchema& sc, const CType& c,
                                 const uint8_t* m, const uint8_t* sbase, const uint8_t* lbase,
                                 WriteFrame* st, uint32_t& sp, uint32_t cap, int32_t full) {
   const tgpu_span sp_ = *(const tgpu_span*)m;
@@ -1538,7 +1538,7 @@ __device__ __forceinline__ void write_complex(Writer& w, const DevSchema& sc, ui
 // the lane's kPrivFrames private frames (a compile-time choice, so the bulk
 // kernels keep their frames in scratch / registers).
 template <int P, bool kDeep = false>
-__device__ void write_record(Writer& w, const DevSchema& sc, const uint8_t* rec,
+__device__ __forceinline__ void write_record(Writer& w, const DevSchema& sc, const uint8_t* rec,
                              const uint8_t* sbase, const uint8_t* lbase) {
   WriteFrame priv[kDeep ? 1 : kPrivFrames];
   WriteFrame* const st = kDeep ? (WriteFrame*)(w.deep + slab_skip_bytes(w.deep_cap)) : priv;
