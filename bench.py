@@ -763,18 +763,13 @@ NESTED_TABLE = [
 ]
 
 
-def nested(dev, n=1 << 24, reps=5, seed=0x1729):
-    """Nested containers on the device (the general reader / writer's frame
-    machines, per-record arena regions): n records generated on the device
-    (torch, seeded), encoded from a list base holding the Item arrays, the
-    grid's row spans and the rows' i32 arrays, then decoded from the indexed
-    stream. Timed with HIP events around each call (best of `reps`); checked
-    by re-encoding the decoded records (their spans now index the decode's
-    arena) to the same bytes. Rates are wire GiB/s; the rooflines price the
-    algorithmic bytes (wire + records + element arrays) against HBM."""
+def nested_batch(dev, n, seed=0x1729):
+    """n records of NESTED_TABLE generated on the device (torch, seeded):
+    (schema, records, list base, items, grid rows, i32 elements). The list
+    base holds the Item arrays, the grid's row spans and the rows' i32
+    arrays."""
     import torch
 
-    from fbthrift_amd import serializer as SZ
     from fbthrift_amd.schema import Schema
 
     schema = Schema.from_table(NESTED_TABLE)
@@ -829,7 +824,24 @@ def nested(dev, n=1 << 24, reps=5, seed=0x1729):
     sp[:, mo(r0, 2) // 8 + 1] = ng
     for k in range(3):
         rv[:, io(r0, k)] = 1
-    del it, outer, sp, rv
+    return schema, recs, lbase, items, rows, int(rl.sum().item())
+
+
+def nested(dev, n=1 << 24, reps=5, seed=0x1729):
+    """Nested containers on the device (the general reader / writer's frame
+    machines, per-record arena regions): n records generated on the device
+    (torch, seeded), encoded from a list base holding the Item arrays, the
+    grid's row spans and the rows' i32 arrays, then decoded from the indexed
+    stream. Timed with HIP events around each call (best of `reps`); checked
+    by re-encoding the decoded records (their spans now index the decode's
+    arena) to the same bytes. Rates are wire GiB/s; the rooflines price the
+    algorithmic bytes (wire + records + element arrays) against HBM."""
+    import torch
+
+    from fbthrift_amd import serializer as SZ
+
+    schema, recs, lbase, items, rows, nints = nested_batch(dev, n, seed)
+    S, IS = schema.size[0], schema.size[1]
     gs = SZ.GpuSchema(schema)
     Ser = SZ.BinarySerializer
     Ser.context().reserve(n)
@@ -863,7 +875,7 @@ def nested(dev, n=1 << 24, reps=5, seed=0x1729):
     w2, _ = Ser.serialize(gs, back, n, list_base=arena, out=again, offsets=None)
     if w2.numel() != wire_bytes or not torch.equal(w2, wire[:wire_bytes]):
         raise RuntimeError("nested re-encode differs")
-    elem = items * IS + rows * 16 + int(rl.sum().item()) * 4
+    elem = items * IS + rows * 16 + nints * 4
     alg = wire_bytes + n * S + elem  # either direction: wire + records + element arrays
     gib = wire_bytes / 2**30
     return {"records": n, "wire_bytes": wire_bytes, "record_bytes": S,
@@ -878,8 +890,9 @@ def nested(dev, n=1 << 24, reps=5, seed=0x1729):
                          "encode_achieved_GBps": round(alg / enc_ms / 1e6, 1),
                          "encode_frac": round(alg / enc_ms / 1e6 / HBM_PEAK_GBS, 4),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s"},
-            "kernels": "general_decode_kernel / encode_size_kernel + encode_write_kernel "
-                       "(no program: containers of structs and of containers)"}
+            "kernels": "decode: tgpu_jit_ndecode (the nested program, one loop per "
+                       "container level) + the general decoder for records it leaves; "
+                       "encode: encode_size_kernel + encode_write_kernel (general writer)"}
 
 
 def irregular(wl, dev, reps=3):

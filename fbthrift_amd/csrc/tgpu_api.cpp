@@ -44,6 +44,12 @@ struct tgpu_schema {
   // their register footprint; used where a stream is known to carry them
   VProgram prog_tol[3]{};
   VProgram* d_prog_tol[3] = {nullptr, nullptr, nullptr};
+  // nested schemas (lists / sets of structs or of scalar lists): the
+  // canonical form with VOP_SEQ loops, compiled only (JIT_NESTED); nprog_depth
+  // = the deepest container nesting (the height it needs)
+  bool has_nprog[3] = {false, false, false};
+  VProgram nprog[3]{};
+  uint32_t nprog_depth[3] = {0, 0, 0};
   // the wire bytes per record (x16) of the last batch whose size this schema
   // learned (blocking encode / size calls), by protocol id: sizes the
   // compiled write pass's LDS output tile (enc_out_cap)
@@ -537,7 +543,14 @@ VOp make_op(uint8_t kind) {
 // header bytes the generated writer emits (BinaryProtocol-inl.h:53-59,
 // CompactProtocol-inl.h:133-160 incl. long-form ids, bools in the header) and
 // each value's encoding.
-bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, VProgram& P) {
+bool emit_seq(const tgpu_schema& sc, uint32_t et, int32_t esi, uint32_t eti, uint32_t member,
+              uint32_t isset, int proto, VProgram& P, uint32_t depth, uint32_t* max_depth);
+
+// nested (build_nested_program): lists / sets of structs or of scalar lists
+// become VOP_SEQ loops whose bodies address the element slot (base 0);
+// `depth` tracks the container nesting for the height check.
+bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, VProgram& P,
+                  bool nested = false, uint32_t depth = 0, uint32_t* max_depth = nullptr) {
   const tgpu_struct_desc& sd = sc.structs[si];
   if (sd.flags & TGPU_STRUCT_UNION) return false;
   int32_t prev = 0;
@@ -595,6 +608,11 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
     } else if (f.ttype == TGPU_T_STRING) {
       v.kind = VOP_STRING;
       if (!push_op(P, v)) return false;
+    } else if (nested && (f.ttype == TGPU_T_LIST || f.ttype == TGPU_T_SET) &&
+               !is_scalar(f.elem_ttype)) {
+      if (!emit_seq(sc, f.elem_ttype, f.struct_index, f.type_index, member, isset, proto, P,
+                    depth + 1, max_depth))
+        return false;
     } else if (f.ttype == TGPU_T_LIST || f.ttype == TGPU_T_SET) {
       v.kind = VOP_LIST;
       const uint32_t e = f.elem_ttype;
@@ -610,9 +628,11 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
         v.bits = e == TGPU_T_I64 ? 64 : 32;
       }
       P.has_list = 1;
+      if (max_depth) *max_depth = std::max(*max_depth, depth + 1);
       if (!push_op(P, v)) return false;
     } else if (f.ttype == TGPU_T_STRUCT) {
-      if (!emit_program(sc, (uint32_t)f.struct_index, member, proto, P)) return false;
+      if (!emit_program(sc, (uint32_t)f.struct_index, member, proto, P, nested, depth, max_depth))
+        return false;
       VOp stop = make_op(VOP_CONST);
       stop.hdr_len = 1;
       VOp is = make_op(VOP_ISSET);
@@ -623,6 +643,67 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
     }
   }
   return true;
+}
+
+// A list / set (member / isset of the enclosing object) of elements `et`:
+// VOP_SEQ, the element's body (a struct's fields + STOP, or one scalar list
+// at the element slot), VOP_SEQ_END.
+bool emit_seq(const tgpu_schema& sc, uint32_t et, int32_t esi, uint32_t eti, uint32_t member,
+              uint32_t isset, int proto, VProgram& P, uint32_t depth, uint32_t* max_depth) {
+  VOp q = make_op(VOP_SEQ);
+  q.member = (uint16_t)member;
+  q.isset = (uint16_t)isset;
+  q.elem_ttype = (uint8_t)et;
+  q.elem_ct = (uint8_t)compact_ctype(et);
+  const uint32_t at = P.n_ops;
+  if (et == TGPU_T_STRUCT) {
+    if (esi < 0 || (uint32_t)esi >= sc.structs.size()) return false;
+    q.hdr = sc.structs[esi].size;
+    if (!push_op(P, q) || !emit_program(sc, (uint32_t)esi, 0, proto, P, true, depth, max_depth))
+      return false;
+    VOp stop = make_op(VOP_CONST);
+    stop.hdr_len = 1;
+    if (!push_op(P, stop)) return false;
+  } else if (et == TGPU_T_LIST || et == TGPU_T_SET) {
+    if (eti == 0 || eti > sc.types.size()) return false;
+    const tgpu_type_desc& t = sc.types[eti - 1];
+    const uint32_t e = t.elem_ttype;
+    if (t.ttype != et || !is_scalar(e)) return false;  // deeper / string elements: general
+    q.hdr = (uint32_t)sizeof(tgpu_span);
+    VOp v = make_op(VOP_LIST);
+    v.member = 0;
+    v.width = (uint8_t)scalar_size(e);
+    v.elem_ttype = (uint8_t)e;
+    v.elem_ct = (uint8_t)compact_ctype(e);
+    v.elem_kind = e == TGPU_T_BOOL ? VEL_BOOL : VEL_FIXED;
+    if (proto == TGPU_PROTOCOL_COMPACT && (e == TGPU_T_I16 || e == TGPU_T_I32 || e == TGPU_T_I64)) {
+      v.elem_kind = VEL_VARINT;
+      v.bits = e == TGPU_T_I64 ? 64 : 32;
+    }
+    if (!push_op(P, q) || !push_op(P, v)) return false;
+    if (max_depth) *max_depth = std::max(*max_depth, depth + 1);
+  } else {
+    return false;  // maps, strings: the general kernels
+  }
+  if (max_depth) *max_depth = std::max(*max_depth, depth);
+  if (!push_op(P, make_op(VOP_SEQ_END))) return false;
+  P.ops[at].hdr_len = (uint8_t)P.n_ops;  // one past the matching VOP_SEQ_END
+  P.has_list = 1;
+  return true;
+}
+
+// The nested program of a schema whose containers hold structs or scalar
+// lists (every field unqualified / required, no maps, no strings inside
+// containers): compiled by JIT_NESTED only.
+bool build_nested_program(const tgpu_schema& sc, int proto, VProgram& P, uint32_t& depth) {
+  P = VProgram{};
+  P.protocol = (uint32_t)proto;
+  P.rec_size = sc.structs[0].size;
+  depth = 0;
+  if (!emit_program(sc, 0, 0, proto, P, true, 0, &depth)) return false;
+  VOp stop = make_op(VOP_CONST);
+  stop.hdr_len = 1;
+  return push_op(P, stop);
 }
 
 bool build_program(const tgpu_schema& sc, int proto, VProgram& P, bool tolerant = false) {
@@ -830,8 +911,50 @@ uint64_t measure_scratch(const tgpu_schema* s) {
 // when the schema has no program or the limits forbid its fast path (a list
 // depth of 1 must be allowed: the program never skips, so max_depth is not
 // reached otherwise).
+// The nested program's compiled decode (JIT_NESTED) of an indexed batch,
+// then the general decoder over the records it left; false: no such kernel
+// (no nested program, a height below its nesting, TGPU_NESTED=0, not
+// compiled), the caller runs the general decoder.
+// TGPU_NESTED_SRC=hbm: the unstaged variant (A/B).
+bool launch_nested_decode(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                          const DecodeArgs& a, hipStream_t s, hipError_t& e) {
+  const char* v = getenv("TGPU_NESTED");
+  const bool off = v && v[0] == '0';
+  v = getenv("TGPU_NESTED_SRC");
+  const bool hbm = v && !strcmp(v, "hbm");
+  const int q = prog_protocol(schema, protocol);
+  if (off || q < 0 || !schema->has_nprog[q] || a.n == 0) return false;
+  const int32_t height = a.height ? a.height : a.max_depth;
+  const int32_t need = (int32_t)schema->nprog_depth[q] + 1;
+  if (height < need || a.max_depth < need) return false;
+  const JitKernels* J = jit_kernels(schema->nprog[q], schema->device, JIT_NESTED, a.n, 0, false);
+  if (!J) return false;
+  constexpr uint32_t kPT = 256;  // records per tile (prog::kPT)
+  const uint64_t tiles = (a.n + kPT - 1) / kPT;
+  // the wire tile: 1.15 x the mean tile + 1 KiB, within 64 KiB of LDS with
+  // the record tile (a larger tile's records take the general decoder)
+  const uint32_t rt = (kPT * a.rec_size + 16 + 15) & ~15u;
+  const double mean = (double)a.in_len / (double)a.n * kPT;
+  double cap = 1.15 * mean + 1024.0;
+  const double room = 65536.0 - rt - 4096.0 - 32.0;
+  if (cap > room) cap = room;
+  if (cap < 4096.0) cap = 4096.0;
+  const uint32_t wire_cap = (uint32_t)cap & ~15u;
+  // (prog::decode_wire_region: whole 4 KiB staging rounds)
+  const uint32_t lds = hbm ? 0 : (wire_cap + 32 + 4095) / 4096 * 4096 + rt;
+  e = jit_launch_decode(J, a, tiles, wire_cap, lds, ctx->d_irr, &ctx->d_res->n_irregular, s,
+                        hbm ? 1 : 0);
+  if (e == hipSuccess)
+    e = launch_general_decode_list(a, protocol, ctx->d_irr, &ctx->d_res->n_irregular, s);
+  return true;
+}
+
 hipError_t launch_indexed_decode(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
                                  const DecodeArgs& a, hipStream_t s) {
+  {
+    hipError_t e = hipSuccess;
+    if (launch_nested_decode(ctx, schema, protocol, a, s, e)) return e;
+  }
   const int32_t height = a.height ? a.height : a.max_depth;
   if (has_prog(schema, protocol) && height >= 2 && a.max_depth >= 2) {
     const int q = prog_protocol(schema, protocol);
@@ -1206,6 +1329,8 @@ int tgpu_schema_create_ex(const tgpu_struct_desc* structs, uint32_t n_structs,
     return TGPU_ERR_HIP;
   }
   for (int proto : {TGPU_PROTOCOL_BINARY, TGPU_PROTOCOL_COMPACT}) {
+    if (s->nested)
+      s->has_nprog[proto] = build_nested_program(*s, proto, s->nprog[proto], s->nprog_depth[proto]);
     if (!build_program(*s, proto, s->prog[proto])) continue;
     build_program(*s, proto, s->prog_tol[proto], true);
     if (hipMalloc(&s->d_prog[proto], sizeof(VProgram)) != hipSuccess ||
@@ -1264,35 +1389,53 @@ uint32_t tgpu_schema_record_size(const tgpu_schema* s) { return s ? s->structs[0
 int tgpu_schema_compile(const tgpu_schema* s, int protocol) {
   if (!s || !valid_protocol(protocol))
     return TGPU_ERR_INVALID_ARGUMENT;
+  const int q = prog_protocol(s, protocol);
+  if (q >= 0 && s->has_nprog[q])
+    return jit_kernels(s->nprog[q], s->device, JIT_NESTED, 0, 0, true) ? TGPU_OK
+                                                                       : TGPU_ERR_UNSUPPORTED;
   if (!has_prog(s, protocol)) return TGPU_ERR_UNSUPPORTED;
   for (int group : {JIT_DECODE, JIT_ENCODE, JIT_INDEX})
-    if (!jit_kernels(s->prog[prog_protocol(s, protocol)], s->device, group, 0, 0, true)) return TGPU_ERR_UNSUPPORTED;
+    if (!jit_kernels(s->prog[q], s->device, group, 0, 0, true)) return TGPU_ERR_UNSUPPORTED;
   return TGPU_OK;
+}
+
+int tgpu_schema_compile_check_ex(const tgpu_struct_desc* structs, uint32_t n_structs,
+                                 const tgpu_field_desc* fields, uint32_t n_fields,
+                                 const tgpu_type_desc* types, uint32_t n_types, int protocol,
+                                 const char* arch, char* log, uint64_t log_capacity) {
+  if (!structs || n_structs == 0 || (!fields && n_fields) || (!types && n_types) ||
+      !valid_protocol(protocol))
+    return TGPU_ERR_INVALID_ARGUMENT;
+  SchemaFacts facts;
+  const int rc = validate(structs, n_structs, fields, n_fields, types, n_types, facts);
+  if (rc) return rc;
+  tgpu_schema h;  // host tables only: nothing is uploaded
+  h.structs.assign(structs, structs + n_structs);
+  h.fields.assign(fields, fields + n_fields);
+  if (n_types) h.types.assign(types, types + n_types);
+  h.nested = facts.nested;
+  for (uint32_t k = 0; k < n_fields; ++k)
+    h.has_double |= fields[k].ttype == TGPU_T_DOUBLE || fields[k].elem_ttype == TGPU_T_DOUBLE ||
+                    fields[k].val_ttype == TGPU_T_DOUBLE;
+  for (uint32_t k = 0; k < n_types; ++k)
+    h.has_double |= types[k].elem_ttype == TGPU_T_DOUBLE || types[k].val_ttype == TGPU_T_DOUBLE;
+  const int q = prog_protocol(&h, protocol);
+  VProgram P{};
+  uint32_t depth = 0;
+  // nested schemas: the nested program (JIT_NESTED); others: the canonical
+  // record program's three groups
+  if (q < 0 || !(h.nested ? build_nested_program(h, q, P, depth) : build_program(h, q, P)))
+    return TGPU_ERR_UNSUPPORTED;
+  return jit_compile_check(P, arch, log, log_capacity);
 }
 
 int tgpu_schema_compile_check(const tgpu_struct_desc* structs, uint32_t n_structs,
                               const tgpu_field_desc* fields, uint32_t n_fields, int protocol,
                               const char* arch, char* log, uint64_t log_capacity) {
-  if (!structs || n_structs == 0 || (!fields && n_fields) ||
-      !valid_protocol(protocol))
-    return TGPU_ERR_INVALID_ARGUMENT;
-  // containers nested in containers (a type table, tgpu_schema_create_ex)
-  // never have a program: the general kernels read them, nothing to compile
-  for (uint32_t k = 0; k < n_fields; ++k)
-    if (fields[k].type_index) return TGPU_ERR_UNSUPPORTED;
-  SchemaFacts facts;
-  const int rc = validate(structs, n_structs, fields, n_fields, nullptr, 0, facts);
-  if (rc) return rc;
-  tgpu_schema h;  // host tables only: nothing is uploaded
-  h.structs.assign(structs, structs + n_structs);
-  h.fields.assign(fields, fields + n_fields);
-  for (uint32_t k = 0; k < n_fields; ++k)
-    h.has_double |= fields[k].ttype == TGPU_T_DOUBLE || fields[k].elem_ttype == TGPU_T_DOUBLE ||
-                    fields[k].val_ttype == TGPU_T_DOUBLE;
-  const int q = prog_protocol(&h, protocol);
-  VProgram P{};
-  if (q < 0 || !build_program(h, q, P)) return TGPU_ERR_UNSUPPORTED;
-  return jit_compile_check(P, arch, log, log_capacity);
+  for (uint32_t k = 0; fields && k < n_fields; ++k)
+    if (fields[k].type_index) return TGPU_ERR_UNSUPPORTED;  // (needs the type table: _ex)
+  return tgpu_schema_compile_check_ex(structs, n_structs, fields, n_fields, nullptr, 0, protocol,
+                                      arch, log, log_capacity);
 }
 
 uint32_t tgpu_schema_arena_scale(const tgpu_schema* s, int protocol) {

@@ -160,6 +160,13 @@ enum VOpKind : uint8_t {
   VOP_LIST = 5,    // list header + scalar elements -> arena, tgpu_span
   VOP_CBOOL = 6,   // Compact bool field: value carried in the header byte
   VOP_ISSET = 7,   // set an isset byte (after a nested struct's STOP)
+  // nested programs only (build_nested_program): a list / set whose elements
+  // are structs or scalar lists. Header + count, the element array from the
+  // record's arena region, then the body ops (up to index hdr_len, the
+  // matching VOP_SEQ_END) once per element with members relative to the
+  // element slot of hdr bytes; elem_ttype / elem_ct: the wire element type.
+  VOP_SEQ = 8,
+  VOP_SEQ_END = 9,
 };
 enum VElemKind : uint8_t {
   VEL_FIXED = 1,   // big-endian fixed width (Binary ints, doubles/floats, bytes)
@@ -391,13 +398,15 @@ hipError_t launch_general_decode(const DecodeArgs& a, int protocol,
 // Kernels generated and compiled for one program (nullptr: not compiled —
 // policy or failure; the interpreting kernels run instead).
 struct JitKernels;
-enum JitGroup { JIT_DECODE = 0, JIT_ENCODE = 1, JIT_INDEX = 2 };
+// JIT_NESTED: the indexed decode of a nested program (VOP_SEQ), generated as
+// straight-line code with one loop per container level.
+enum JitGroup { JIT_DECODE = 0, JIT_ENCODE = 1, JIT_INDEX = 2, JIT_NESTED = 3 };
 const JitKernels* jit_kernels(const VProgram& prog, int device, int group, uint64_t records,
                               uint64_t bytes, bool force);
 int jit_compile_check(const VProgram& P, const char* arch, char* log, uint64_t log_cap);
 hipError_t jit_launch_decode(const JitKernels* J, const DecodeArgs& a, uint64_t grid,
                              uint32_t cap, uint32_t lds, uint64_t* irr, unsigned long long* nirr,
-                             hipStream_t s);
+                             hipStream_t s, int which = 0);
 hipError_t jit_launch_encode(const JitKernels* J, bool write, const EncodeArgs& a, uint64_t grid,
                              uint32_t lds, hipStream_t s);
 // which: 0 speculation, 1 emit, 2 emit + fused decode

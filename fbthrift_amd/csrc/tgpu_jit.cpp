@@ -72,11 +72,49 @@ std::string cache_key(const VProgram& P, int device, int group) {
   return k;
 }
 
-const char* const kEntry[3][5] = {
+const char* const kEntry[4][5] = {
     {"tgpu_jit_decode", nullptr, nullptr, nullptr, nullptr},
     {"tgpu_jit_size", "tgpu_jit_write", nullptr, nullptr, nullptr},
     {"tgpu_jit_index_spec", "tgpu_jit_index_emit", "tgpu_jit_index_decode",
-     "tgpu_jit_index_onepass", "tgpu_jit_index_onepass_decode"}};
+     "tgpu_jit_index_onepass", "tgpu_jit_index_onepass_decode"},
+    {"tgpu_jit_ndecode", "tgpu_jit_ndecode_hbm", nullptr, nullptr, nullptr}};
+
+// The record function of a nested program: ops [k, stop) at object base `b`
+// (a variable name), each VOP_SEQ a counted loop over its element slots with
+// the body at the slot. Leaf ops are run_op / nlist calls on the constant op.
+void gen_ops(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t stop,
+             const std::string& b, int indent) {
+  const std::string in(indent, ' ');
+  while (k < stop) {
+    const VOp& v = P.ops[k];
+    if (v.kind == VOP_SEQ) {
+      const std::string n = "n" + std::to_string(k), a = "a" + std::to_string(k),
+                        i = "i" + std::to_string(k), e = "e" + std::to_string(k);
+      o << in << "{\n"
+        << in << "  uint32_t " << n << ";\n"
+        << in << "  uint8_t* " << a << ";\n"
+        << in << "  if (!seq_open(kOps[" << k << "], kCompact, src, c, p, end, " << b << ", bump, "
+        << n << ", " << a << ")) return false;\n"
+        << in << "  for (uint32_t " << i << " = 0; " << i << " < " << n << "; ++" << i << ") {\n"
+        << in << "    uint8_t* " << e << " = " << a << " + (uint64_t)" << i << " * " << v.hdr
+        << "u;\n";
+      if (v.elem_ttype == TGPU_T_STRUCT) o << in << "    zero_slot<" << v.hdr << "u>(" << e << ");\n";
+      gen_ops(o, P, k + 1, v.hdr_len - 1, e, indent + 4);
+      o << in << "  }\n"
+        << in << "  seq_close(kOps[" << k << "], " << b << ");\n"
+        << in << "}\n";
+      k = v.hdr_len;  // past the VOP_SEQ_END
+      continue;
+    }
+    if (v.kind == VOP_LIST)
+      o << in << "if (!nlist(kOps[" << k << "], kCompact, src, c, p, end, " << b
+        << ", bump)) return false;\n";
+    else if (v.kind != VOP_SEQ_END)
+      o << in << "if (!run_op<true>(kOps[" << k << "], kCompact, src, c, p, end, " << b
+        << ", W)) return false;\n";
+    ++k;
+  }
+}
 
 // The generated translation unit: the program as constants + one entry point
 // per kernel body.
@@ -123,6 +161,40 @@ std::string gen_source(const VProgram& P, int group) {
     << ";\n"
        "}  // namespace\n"
        "using namespace tgpu;\n";
+  if (group == JIT_NESTED) {
+    o << "#include \"tgpu_nested.h\"\n"
+         "namespace {\n"
+         "using namespace tgpu;\n"
+         "using namespace tgpu::prog;\n"
+         "constexpr bool kCompact = "
+      << (P.protocol == TGPU_PROTOCOL_BINARY ? "false" : "true")
+      << ";\n"
+         "template <class Src>\n"
+         "__device__ __forceinline__ bool nrec(const Src& src, const Ctx& c, uint32_t& p, "
+         "const uint32_t end, uint8_t* rec, uint64_t& bump) {\n"
+         "  Win W;\n";
+    gen_ops(o, P, 0, P.n_ops, "rec", 2);
+    o << "  return true;\n"
+         "}\n"
+         "struct NR {\n"
+         "  template <class Src>\n"
+         "  __device__ __forceinline__ bool operator()(const Src& src, const Ctx& c, uint32_t& p, "
+         "uint32_t end, uint8_t* rec, uint64_t& bump) const {\n"
+         "    return nrec(src, c, p, end, rec, bump);\n"
+         "  }\n"
+         "};\n"
+         "}  // namespace\n"
+         "extern \"C\" __global__ __launch_bounds__(256) void tgpu_jit_ndecode(DecodeArgs a, "
+         "uint32_t wire_cap, uint64_t* __restrict__ irr, unsigned long long* __restrict__ nirr) {\n"
+         "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+         "  nested_decode_tile(a, NR{}, kS, wire_cap, irr, nirr, smem);\n"
+         "}\n"
+         "extern \"C\" __global__ __launch_bounds__(256) void tgpu_jit_ndecode_hbm(DecodeArgs a, "
+         "uint32_t wire_cap, uint64_t* __restrict__ irr, unsigned long long* __restrict__ nirr) {\n"
+         "  nested_decode_hbm(a, NR{}, kS, irr, nirr);\n"
+         "}\n";
+    return o.str();
+  }
   if (group == JIT_DECODE)
     o << "extern \"C\" __global__ __launch_bounds__(256) void tgpu_jit_decode(DecodeArgs a, "
          "uint32_t wire_cap, uint64_t* __restrict__ irr, unsigned long long* __restrict__ nirr) "
@@ -278,10 +350,10 @@ const JitKernels* jit_kernels(const VProgram& P, int device, int group, uint64_t
 
 hipError_t jit_launch_decode(const JitKernels* J, const DecodeArgs& a, uint64_t grid,
                              uint32_t cap, uint32_t lds, uint64_t* irr, unsigned long long* nirr,
-                             hipStream_t s) {
+                             hipStream_t s, int which) {
   DecodeArgs x = a;
   void* p[] = {&x, &cap, &irr, &nirr};
-  return launch(J->f[0], grid, lds, s, p);
+  return launch(J->f[which], grid, lds, s, p);
 }
 
 hipError_t jit_launch_encode(const JitKernels* J, bool write, const EncodeArgs& a, uint64_t grid,
@@ -303,7 +375,10 @@ hipError_t jit_launch_index(const JitKernels* J, int which, const IndexArgs& a, 
 int jit_compile_check(const VProgram& P, const char* arch, char* log, uint64_t log_cap) {
   std::string l;
   bool ok = true;
-  for (int group = 0; group < 3 && ok; ++group) {
+  bool nested = false;
+  for (uint32_t k = 0; k < P.n_ops; ++k) nested |= P.ops[k].kind == VOP_SEQ;
+  for (int group = nested ? JIT_NESTED : 0; group < (nested ? JIT_NESTED + 1 : JIT_NESTED) && ok;
+       ++group) {
     std::vector<char> code;
     ok = compile_code(P, group, arch ? arch : "gfx950", code, l);
   }

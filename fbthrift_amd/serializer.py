@@ -123,12 +123,16 @@ class GpuSchema:
 
 def compile_check(schema, protocol, arch="gfx950"):
     """Generates and compiles `schema`'s kernels for `arch` without a GPU
-    (tgpu_schema_compile_check). Returns (code, compiler log)."""
+    (tgpu_schema_compile_check_ex: the record program's decode / encode /
+    index kernels, or a nested schema's nested decode). Returns (code,
+    compiler log)."""
     structs, ns, fields, nf = schema.descriptors()
+    types, nt = schema.type_descriptors()
     log = ctypes.create_string_buffer(1 << 16)
-    rc = _lib.lib().tgpu_schema_compile_check(ctypes.addressof(structs), ns,
-                                              ctypes.addressof(fields), nf, protocol,
-                                              arch.encode(), log, len(log))
+    rc = _lib.lib().tgpu_schema_compile_check_ex(ctypes.addressof(structs), ns,
+                                                 ctypes.addressof(fields), nf,
+                                                 ctypes.addressof(types), nt, protocol,
+                                                 arch.encode(), log, len(log))
     return rc, log.value.decode(errors="replace")
 
 

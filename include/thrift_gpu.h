@@ -352,11 +352,19 @@ int tgpu_schema_compile(const tgpu_schema* schema, int protocol);
  * tables (as for tgpu_schema_create) for `arch` (e.g. "gfx950"; NULL =
  * gfx950) without loading them — needs no GPU. The compiler log goes to
  * log[0..log_capacity) (may be NULL). TGPU_ERR_UNSUPPORTED as for
- * tgpu_schema_compile, including every schema whose fields reference a
- * nested container type (type_index != 0: no program, general kernels). */
+ * tgpu_schema_compile. Nested container types need the _ex form (here a
+ * field with type_index != 0 has no program). */
 int tgpu_schema_compile_check(const tgpu_struct_desc* structs, uint32_t n_structs,
                               const tgpu_field_desc* fields, uint32_t n_fields, int protocol,
                               const char* arch, char* log, uint64_t log_capacity);
+/* The same with a container type table (tgpu_schema_create_ex). Schemas whose
+ * lists / sets hold structs or scalar lists (and no maps or strings inside
+ * containers, every field unqualified or required) compile their nested
+ * record program: one decode kernel with a loop per container level. */
+int tgpu_schema_compile_check_ex(const tgpu_struct_desc* structs, uint32_t n_structs,
+                                 const tgpu_field_desc* fields, uint32_t n_fields,
+                                 const tgpu_type_desc* types, uint32_t n_types, int protocol,
+                                 const char* arch, char* log, uint64_t log_capacity);
 
 /* ---- context ---------------------------------------------------------- */
 int tgpu_context_create(tgpu_context** out);

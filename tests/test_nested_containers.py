@@ -105,10 +105,19 @@ def _gpu_decode(c, wire, n, offsets, gpu, limits=None):
     return st, rec.cpu().numpy(), arena.cpu().numpy(), nd, cons
 
 
+@pytest.fixture(params=["general", "compiled"])
+def jit(request, monkeypatch):
+    """general: the AOT kernels; compiled: TGPU_JIT=1, so the schemas with a
+    nested record program (lists / sets of structs or scalar lists) decode
+    through it (tgpu_nested.h) and the rest through the general reader."""
+    monkeypatch.setenv("TGPU_JIT", "1" if request.param == "compiled" else "0")
+    return request.param
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", CASES)
 @pytest.mark.parametrize("indexed", [False, True])
-def test_gpu_decode_golden(gpu, name, indexed):
+def test_gpu_decode_golden(gpu, name, indexed, jit):
     c = nh.NestedCase(name)
     offs = c.offsets if indexed else None
     st, rec, arena, nd, cons = _gpu_decode(c, c.wire, c.n, offs, gpu)
@@ -148,7 +157,7 @@ def test_gpu_arena_scale_matches(gpu, name):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", CASES)
-def test_gpu_truncation_parity(gpu, name):
+def test_gpu_truncation_parity(gpu, name, jit):
     """Every cut of a record: the oracle's status and the same partial record
     (failing list element present, set element / map pair absent)."""
     c = nh.NestedCase(name)
@@ -180,7 +189,7 @@ def test_gpu_transcode_golden(gpu, name):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["structlist_compact", "deepcont_binary"])
-def test_gpu_container_limit_nested(gpu, name):
+def test_gpu_container_limit_nested(gpu, name, jit):
     """container_limit applies to every nested container (checkContainerSize
     on each readListBegin / readMapBegin)."""
     c = nh.NestedCase(name)
