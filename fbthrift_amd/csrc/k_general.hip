@@ -505,10 +505,18 @@ hipError_t launch_deep_size(const EncodeArgs& a, int protocol, hipStream_t strea
 }
 
 hipError_t launch_general_encode(const EncodeArgs& a, int protocol, uint64_t n_blocks,
-                                 hipStream_t stream) {
+                                 hipStream_t stream, const JitKernels* nj) {
   if (a.n == 0) return hipSuccess;
   const dim3 grid((uint32_t)n_blocks);
   const uint32_t sb = schema_stage_bytes(a.sc);
+  if (nj) {  // the nested program's passes (no record is deferred: bounded depth)
+    hipError_t e = jit_launch_encode(nj, false, a, n_blocks, 0, stream, 2);
+    if (e == hipSuccess)
+      e = launch_scan_tiles(a.block_sums, n_blocks, a.scan_part, &a.res->total_bytes,
+                            a.offs + a.n, stream);
+    if (e == hipSuccess) e = jit_launch_encode(nj, true, a, n_blocks, 0, stream, 2);
+    return e;
+  }
   TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_size_kernel<P_>, grid, dim3(256), sb, stream, a,
                                                 sb));
   hipError_t e = launch_deep_size(a, protocol, stream);
@@ -525,13 +533,18 @@ hipError_t launch_general_encode(const EncodeArgs& a, int protocol, uint64_t n_b
 }
 
 hipError_t launch_general_size(const EncodeArgs& a, int protocol, uint64_t n_blocks,
-                               hipStream_t stream) {
+                               hipStream_t stream, const JitKernels* nj) {
   if (a.n == 0) return hipSuccess;
   const dim3 grid((uint32_t)n_blocks);
   const uint32_t sb = schema_stage_bytes(a.sc);
-  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_size_kernel<P_>, grid, dim3(256), sb, stream, a,
-                                                sb));
-  hipError_t e = launch_deep_size(a, protocol, stream);
+  hipError_t e;
+  if (nj) {
+    e = jit_launch_encode(nj, false, a, n_blocks, 0, stream, 2);
+  } else {
+    TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_size_kernel<P_>, grid, dim3(256), sb, stream,
+                                                  a, sb));
+    e = launch_deep_size(a, protocol, stream);
+  }
   if (e != hipSuccess) return e;
   e = launch_scan_tiles(a.block_sums, n_blocks, a.scan_part, &a.res->total_bytes, a.offs + a.n,
                         stream);

@@ -911,6 +911,20 @@ uint64_t measure_scratch(const tgpu_schema* s) {
 // when the schema has no program or the limits forbid its fast path (a list
 // depth of 1 must be allowed: the program never skips, so max_depth is not
 // reached otherwise).
+// The nested program's compiled kernels for a call of n records (nullptr:
+// none — no nested program, a height below its nesting (decode),
+// TGPU_NESTED=0, not compiled).
+const JitKernels* nested_jit(const tgpu_schema* schema, int protocol, uint64_t n, int32_t height,
+                             int32_t max_depth) {
+  const char* v = getenv("TGPU_NESTED");
+  if (v && v[0] == '0') return nullptr;
+  const int q = prog_protocol(schema, protocol);
+  if (q < 0 || !schema->has_nprog[q] || n == 0) return nullptr;
+  const int32_t need = (int32_t)schema->nprog_depth[q] + 1;
+  if (height < need || max_depth < need) return nullptr;
+  return jit_kernels(schema->nprog[q], schema->device, JIT_NESTED, n, 0, false);
+}
+
 // The nested program's compiled decode (JIT_NESTED) of an indexed batch,
 // then the general decoder over the records it left; false: no such kernel
 // (no nested program, a height below its nesting, TGPU_NESTED=0, not
@@ -918,16 +932,10 @@ uint64_t measure_scratch(const tgpu_schema* s) {
 // TGPU_NESTED_SRC=hbm: the unstaged variant (A/B).
 bool launch_nested_decode(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
                           const DecodeArgs& a, hipStream_t s, hipError_t& e) {
-  const char* v = getenv("TGPU_NESTED");
-  const bool off = v && v[0] == '0';
-  v = getenv("TGPU_NESTED_SRC");
+  const char* v = getenv("TGPU_NESTED_SRC");
   const bool hbm = v && !strcmp(v, "hbm");
-  const int q = prog_protocol(schema, protocol);
-  if (off || q < 0 || !schema->has_nprog[q] || a.n == 0) return false;
-  const int32_t height = a.height ? a.height : a.max_depth;
-  const int32_t need = (int32_t)schema->nprog_depth[q] + 1;
-  if (height < need || a.max_depth < need) return false;
-  const JitKernels* J = jit_kernels(schema->nprog[q], schema->device, JIT_NESTED, a.n, 0, false);
+  const JitKernels* J =
+      nested_jit(schema, protocol, a.n, a.height ? a.height : a.max_depth, a.max_depth);
   if (!J) return false;
   constexpr uint32_t kPT = 256;  // records per tile (prog::kPT)
   const uint64_t tiles = (a.n + kPT - 1) / kPT;
@@ -1589,8 +1597,9 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
       if (has_prog(schema, protocol) && program_encode_fits(rs))
         e = launch_program_encode(a, schema->d_prog[prog_protocol(schema, protocol)], ctx->d_scan_part, false, s,
                                   schema_jit(schema, protocol, JIT_ENCODE, n, 0));
-      else
-        e = launch_general_encode(a, protocol, nb, s);
+      else  // (the writer has no depth limit: height / max_depth do not apply)
+        e = launch_general_encode(a, protocol, nb, s,
+                                  nested_jit(schema, protocol, n, INT32_MAX, INT32_MAX));
     }
   }
   if (e == hipSuccess && n) e = launch_encode_finish(a, protocol, fixed, s);
@@ -1651,7 +1660,8 @@ int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol
                                 schema_jit(schema, protocol, JIT_ENCODE, n, 0));
       if (e == hipSuccess) e = launch_size_offsets(a, (n + 255) / 256, s);
     } else {
-      e = launch_general_size(a, protocol, (n + 255) / 256, s);
+      e = launch_general_size(a, protocol, (n + 255) / 256, s,
+                              nested_jit(schema, protocol, n, INT32_MAX, INT32_MAX));
     }
   }
   if (e == hipSuccess && n) e = launch_encode_finish(a, protocol, 0, s);

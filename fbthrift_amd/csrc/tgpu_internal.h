@@ -407,8 +407,9 @@ int jit_compile_check(const VProgram& P, const char* arch, char* log, uint64_t l
 hipError_t jit_launch_decode(const JitKernels* J, const DecodeArgs& a, uint64_t grid,
                              uint32_t cap, uint32_t lds, uint64_t* irr, unsigned long long* nirr,
                              hipStream_t s, int which = 0);
+// first: the group's first encode entry (JIT_NESTED: 2, its size / write)
 hipError_t jit_launch_encode(const JitKernels* J, bool write, const EncodeArgs& a, uint64_t grid,
-                             uint32_t lds, hipStream_t s);
+                             uint32_t lds, hipStream_t s, int first = 0);
 // which: 0 speculation, 1 emit, 2 emit + fused decode
 hipError_t jit_launch_index(const JitKernels* J, int which, const IndexArgs& a, uint64_t grid,
                             hipStream_t s);
@@ -434,10 +435,14 @@ hipError_t launch_serial_decode(const DecodeArgs& a, int protocol,
                                 hipStream_t stream);
 hipError_t launch_decode_finish(const DecodeArgs& a, int protocol,
                                 uint64_t fixed_len, hipStream_t stream);
+// nj: a nested program's compiled kernels (JIT_NESTED) for the size / write
+// passes instead of the general writer's (nullptr: the general writer).
 hipError_t launch_general_encode(const EncodeArgs& a, int protocol,
-                                 uint64_t n_blocks, hipStream_t stream);
+                                 uint64_t n_blocks, hipStream_t stream,
+                                 const JitKernels* nj = nullptr);
 hipError_t launch_general_size(const EncodeArgs& a, int protocol,
-                               uint64_t n_blocks, hipStream_t stream);
+                               uint64_t n_blocks, hipStream_t stream,
+                               const JitKernels* nj = nullptr);
 hipError_t launch_encode_finish(const EncodeArgs& a, int protocol,
                                 uint64_t fixed_len, hipStream_t stream);
 hipError_t launch_result_init(DevResult* res, uint64_t n, hipStream_t stream);

@@ -77,7 +77,38 @@ const char* const kEntry[4][5] = {
     {"tgpu_jit_size", "tgpu_jit_write", nullptr, nullptr, nullptr},
     {"tgpu_jit_index_spec", "tgpu_jit_index_emit", "tgpu_jit_index_decode",
      "tgpu_jit_index_onepass", "tgpu_jit_index_onepass_decode"},
-    {"tgpu_jit_ndecode", "tgpu_jit_ndecode_hbm", nullptr, nullptr, nullptr}};
+    {"tgpu_jit_ndecode", "tgpu_jit_ndecode_hbm", "tgpu_jit_nsize", "tgpu_jit_nwrite", nullptr}};
+
+// The record writer of a nested program: ops [k, stop) of the object at `b`;
+// each VOP_SEQ writes its header and loops over the element slots of its
+// span in the list base.
+void gen_enc_ops(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t stop,
+                 const std::string& b, int indent) {
+  const std::string in(indent, ' ');
+  while (k < stop) {
+    const VOp& v = P.ops[k];
+    if (v.kind == VOP_SEQ) {
+      const std::string sp = "s" + std::to_string(k), a = "a" + std::to_string(k),
+                        i = "i" + std::to_string(k), e = "e" + std::to_string(k);
+      o << in << "{\n"
+        << in << "  const tgpu_span " << sp << " = seq_span(kOps[" << k << "], " << b << ");\n"
+        << in << "  if (!put_list_header(o, kOps[" << k << "], kCompact, " << sp
+        << ".length)) return false;\n"
+        << in << "  const uint8_t* " << a << " = lbase + " << sp << ".offset;\n"
+        << in << "  for (uint32_t " << i << " = 0; " << i << " < " << sp << ".length; ++" << i
+        << ") {\n"
+        << in << "    const uint8_t* " << e << " = " << a << " + (uint64_t)" << i << " * " << v.hdr
+        << "u;\n";
+      gen_enc_ops(o, P, k + 1, v.hdr_len - 1, e, indent + 4);
+      o << in << "  }\n" << in << "}\n";
+      k = v.hdr_len;
+      continue;
+    }
+    if (v.kind != VOP_SEQ_END && v.kind != VOP_ISSET)
+      o << in << "if (!enc_op(kOps[" << k << "], kCompact, " << b << ", sbase, lbase, o)) return false;\n";
+    ++k;
+  }
+}
 
 // The record function of a nested program: ops [k, stop) at object base `b`
 // (a variable name), each VOP_SEQ a counted loop over its element slots with
@@ -192,6 +223,29 @@ std::string gen_source(const VProgram& P, int group) {
          "extern \"C\" __global__ __launch_bounds__(256) void tgpu_jit_ndecode_hbm(DecodeArgs a, "
          "uint32_t wire_cap, uint64_t* __restrict__ irr, unsigned long long* __restrict__ nirr) {\n"
          "  nested_decode_hbm(a, NR{}, kS, irr, nirr);\n"
+         "}\n"
+         "namespace {\n"
+         "template <class O>\n"
+         "__device__ __forceinline__ bool nenc(const uint8_t* rec, const uint8_t* sbase, "
+         "const uint8_t* lbase, O& o) {\n";
+    gen_enc_ops(o, P, 0, P.n_ops, "rec", 2);
+    o << "  return true;\n"
+         "}\n"
+         "struct NE {\n"
+         "  template <class O>\n"
+         "  __device__ __forceinline__ bool operator()(const uint8_t* rec, const uint8_t* sbase, "
+         "const uint8_t* lbase, O& o) const {\n"
+         "    return nenc(rec, sbase, lbase, o);\n"
+         "  }\n"
+         "};\n"
+         "}  // namespace\n"
+         "extern \"C\" __global__ __launch_bounds__(256) void tgpu_jit_nsize(EncodeArgs a) {\n"
+         "  __shared__ unsigned long long part[4];\n"
+         "  nested_size_tile(a, NE{}, part);\n"
+         "}\n"
+         "extern \"C\" __global__ __launch_bounds__(256) void tgpu_jit_nwrite(EncodeArgs a) {\n"
+         "  __shared__ unsigned long long part[4];\n"
+         "  nested_write_tile(a, NE{}, part);\n"
          "}\n";
     return o.str();
   }
@@ -357,10 +411,10 @@ hipError_t jit_launch_decode(const JitKernels* J, const DecodeArgs& a, uint64_t 
 }
 
 hipError_t jit_launch_encode(const JitKernels* J, bool write, const EncodeArgs& a, uint64_t grid,
-                             uint32_t lds, hipStream_t s) {
+                             uint32_t lds, hipStream_t s, int first) {
   EncodeArgs x = a;
   void* p[] = {&x};
-  return launch(J->f[write ? 1 : 0], grid, lds, s, p);
+  return launch(J->f[first + (write ? 1 : 0)], grid, lds, s, p);
 }
 
 hipError_t jit_launch_index(const JitKernels* J, int which, const IndexArgs& a, uint64_t grid,

@@ -247,5 +247,239 @@ __device__ __forceinline__ void nested_decode_hbm(const DecodeArgs& a, const R& 
   if (!ok) irr[atomicAdd(nirr, 1ull)] = i;
 }
 
+// ================================================================ encode ======
+// The generated record writer runs twice: over Count (the size pass: bytes
+// only) and over Out (the write pass). Either way the bytes are the general
+// writer's (tgpu_device.h write_record: the generated write of every field in
+// declaration order, serialize_struct.whisker:40-67), for records of the
+// canonical kind these schemas have (every field unqualified / required): a
+// value the writer rejects (a bool byte > 1, a length > INT32_MAX) fails the
+// record, and the finish kernel diagnoses it with the general writer.
+struct Count {
+  static constexpr bool kCount = true;
+  uint64_t n = 0;
+  __device__ __forceinline__ void put(uint64_t, uint32_t k) { n += k; }
+  __device__ __forceinline__ void bytes(const uint8_t*, uint32_t k) { n += k; }
+};
+
+// Bytes into HBM from an 8-byte accumulator: whole aligned words with one
+// 8-byte store, the record's first and last partial words byte by byte (the
+// neighbouring records own the rest of those words).
+struct Out {
+  static constexpr bool kCount = false;
+  uint8_t* w;      // current aligned word
+  uint64_t acc;    // its pending bytes (little-endian)
+  uint32_t nb;     // bytes in acc (incl. the skipped head of the first word)
+  uint32_t lo;     // first byte of the current word this record owns
+  __device__ __forceinline__ Out(uint8_t* out, uint64_t start) {
+    const uintptr_t at = (uintptr_t)out + start;
+    w = (uint8_t*)(at & ~(uintptr_t)7);
+    nb = lo = (uint32_t)(at & 7);
+    acc = 0;
+  }
+  __device__ __forceinline__ void emit(uint64_t x) {
+    if (lo == 0) {
+      *(uint64_t*)w = x;
+    } else {
+      for (uint32_t b = lo; b < 8; ++b) w[b] = (uint8_t)(x >> (8 * b));
+      lo = 0;
+    }
+    w += 8;
+  }
+  // the low k bytes of v (1 <= k <= 8), first byte lowest
+  __device__ __forceinline__ void put(uint64_t v, uint32_t k) {
+    if (k < 8) v &= (1ull << (8 * k)) - 1;
+    acc |= v << (8 * nb);
+    const uint32_t t = nb + k;
+    if (t >= 8) {
+      emit(acc);
+      acc = nb ? v >> (8 * (8 - nb)) : 0;
+      nb = t - 8;
+    } else {
+      nb = t;
+    }
+  }
+  // k bytes from src (a string payload): 8 at a time from aligned loads (never
+  // past the 8-byte words that hold src's bytes)
+  __device__ __forceinline__ void bytes(const uint8_t* src, uint32_t k) {
+    while (k) {
+      const uint32_t m = k < 8 ? k : 8;
+      const uintptr_t a = (uintptr_t)src;
+      const uint64_t* q = (const uint64_t*)(a & ~(uintptr_t)7);
+      const uint32_t sh = (uint32_t)(a & 7);
+      uint64_t x = q[0] >> (8 * sh);
+      if (sh && sh + m > 8) x |= q[1] << (8 * (8 - sh));
+      put(x, m);
+      src += m;
+      k -= m;
+    }
+  }
+  __device__ __forceinline__ void flush() {
+    for (uint32_t b = lo; b < nb; ++b) w[b] = (uint8_t)(acc >> (8 * b));
+  }
+};
+
+__device__ __forceinline__ uint32_t lebn(uint64_t v) {  // LEB128 bytes of v
+  const uint32_t bits = 64 - (uint32_t)__builtin_clzll(v | 1);
+  return (bits + 6) / 7;
+}
+
+template <class O>
+__device__ __forceinline__ void nput_varint(O& o, uint64_t v) {
+  if constexpr (O::kCount) {
+    o.n += lebn(v);
+  } else {
+    uint64_t x = 0;
+    uint32_t n = 0;
+    while (v >= 0x80 && n < 8) {
+      x |= ((v & 0x7f) | 0x80) << (8 * n);
+      v >>= 7;
+      ++n;
+    }
+    if (n < 8) {
+      o.put(x | (v << (8 * n)), n + 1);
+      return;
+    }
+    o.put(x, 8);  // (a 9-10 byte i64 varint)
+    x = 0;
+    n = 0;
+    while (v >= 0x80) {
+      x |= ((v & 0x7f) | 0x80) << (8 * n);
+      v >>= 7;
+      ++n;
+    }
+    o.put(x | (v << (8 * n)), n + 1);
+  }
+}
+
+// writeListBegin / writeSetBegin (BinaryProtocol-inl.h:69-96,
+// CompactProtocol-inl.h:182-246) of n elements of op.elem_ttype
+template <class O>
+__device__ __forceinline__ bool put_list_header(O& o, const VOp op, const bool compact,
+                                                uint32_t n) {
+  if (n > 0x7fffffffu) return false;  // checked_container_size: WRITE_SIZE_LIMIT
+  if (!compact) {
+    o.put(op.elem_ttype, 1);
+    o.put(__builtin_bswap32(n), 4);
+  } else if (n <= 14) {
+    o.put((n << 4) | op.elem_ct, 1);
+  } else {
+    o.put(0xf0 | op.elem_ct, 1);
+    nput_varint(o, n);
+  }
+  return true;
+}
+
+// A fixed-width scalar of w bytes at p as the writer emits it
+// (write_scalar): big-endian, a bool validated (0/1; Compact 1 / 2).
+template <class O>
+__device__ __forceinline__ bool put_fixed(O& o, const bool compact, const uint8_t* p, uint32_t w,
+                                          bool is_bool) {
+  const uint64_t raw = load_member(p, w);
+  if (is_bool) {
+    if (raw > 1) return false;  // validate_bool: INVALID_BOOL_WRITE
+    o.put(compact ? (raw ? 1 : 2) : raw, 1);
+    return true;
+  }
+  o.put(__builtin_bswap64(raw) >> (64 - 8 * w), w);
+  return true;
+}
+
+// One non-container op of the program (the ops run_op decodes).
+template <class O>
+__device__ __forceinline__ bool enc_op(const VOp op, const bool compact, const uint8_t* base,
+                                       const uint8_t* sbase, const uint8_t* lbase, O& o) {
+  switch (op.kind) {
+    case VOP_CONST:
+      o.put(op.hdr, op.hdr_len);
+      return true;
+    case VOP_CBOOL: {
+      const uint32_t b = base[op.member];
+      if (b > 1) return false;
+      o.put(op.hdr | (b ? 1u : 2u), op.hdr_len);
+      return true;
+    }
+    case VOP_FIXED:
+      return put_fixed(o, compact, base + op.member, op.width, op.is_bool);
+    case VOP_VARINT:
+      nput_varint(o, zz_member(load_member(base + op.member, op.width), op.width, op.bits));
+      return true;
+    case VOP_STRING: {
+      const tgpu_span sp = *(const tgpu_span*)(base + op.member);
+      if (sp.length > 0x7fffffffu) return false;  // checkBinarySize
+      if (compact) nput_varint(o, sp.length);
+      else o.put(__builtin_bswap32(sp.length), 4);
+      o.bytes(sbase + sp.offset, sp.length);
+      return true;
+    }
+    case VOP_LIST: {
+      const tgpu_span sp = *(const tgpu_span*)(base + op.member);
+      if (!put_list_header(o, op, compact, sp.length)) return false;
+      const uint8_t* e = lbase + sp.offset;
+      const uint32_t es = op.width;
+      if constexpr (O::kCount) {
+        if (op.elem_kind != VEL_VARINT && op.elem_kind != VEL_BOOL) {
+          o.n += (uint64_t)sp.length * es;
+          return true;
+        }
+      }
+      for (uint32_t i = 0; i < sp.length; ++i) {
+        const uint8_t* p = e + (uint64_t)i * es;
+        if (op.elem_kind == VEL_VARINT) {
+          nput_varint(o, zz_member(load_member(p, es), es, op.bits));
+        } else if (!put_fixed(o, compact, p, es, op.elem_kind == VEL_BOOL)) {
+          return false;
+        }
+      }
+      return true;
+    }
+    default:
+      return true;  // VOP_ISSET, VOP_SEQ_END: no bytes
+  }
+}
+
+// VOP_SEQ: the header; the caller loops over the elements of the span
+__device__ __forceinline__ tgpu_span seq_span(const VOp op, const uint8_t* base) {
+  return *(const tgpu_span*)(base + op.member);
+}
+
+// Size pass: per-record sizes into a.offs, tile sums into a.block_sums (the
+// general encode's layout, k_general.hip encode_size_kernel).
+template <class E>
+__device__ __forceinline__ void nested_size_tile(const EncodeArgs& a, const E& enc,
+                                                 unsigned long long* part) {
+  const uint64_t i = (uint64_t)blockIdx.x * kET + threadIdx.x;
+  unsigned long long sz = 0;
+  if (i < a.n) {
+    Count o;
+    if (enc(a.recs + i * a.rec_size, a.sbase, a.lbase, o)) sz = o.n;
+    else atomicMin(&a.res->first_fail, (unsigned long long)i);
+    a.offs[i] = sz;
+  }
+  unsigned long long total;
+  (void)block_exscan256(sz, part, &total);
+  if (threadIdx.x == 0) a.block_sums[blockIdx.x] = total;
+}
+
+// Write pass: record starts from the scanned tile sums (encode_write_kernel),
+// each lane writing its record straight to the stream.
+template <class E>
+__device__ __forceinline__ void nested_write_tile(const EncodeArgs& a, const E& enc,
+                                                  unsigned long long* part) {
+  const uint64_t i = (uint64_t)blockIdx.x * kET + threadIdx.x;
+  const unsigned long long sz = i < a.n ? a.offs[i] : 0;
+  unsigned long long total;
+  const unsigned long long start = a.block_sums[blockIdx.x] + block_exscan256(sz, part, &total);
+  if (i >= a.n) return;
+  a.offs[i] = start;
+  if (start + sz > a.cap) {
+    atomicMin(&a.res->first_fail, (unsigned long long)i);
+    return;
+  }
+  if (sz == 0) return;  // (a record the size pass failed: the finish kernel reports it)
+  Out o(a.out, start);
+  if (enc(a.recs + i * a.rec_size, a.sbase, a.lbase, o)) o.flush();
+}
+
 }  // namespace prog
 }  // namespace tgpu

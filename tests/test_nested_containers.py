@@ -131,7 +131,7 @@ def test_gpu_decode_golden(gpu, name, indexed, jit):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", CASES)
-def test_gpu_encode_golden(gpu, name):
+def test_gpu_encode_golden(gpu, name, jit):
     c = nh.NestedCase(name)
     rec, sb, lb = nh.pack(c)
     from fbthrift_amd.serializer import GpuSchema
@@ -173,7 +173,7 @@ def test_gpu_truncation_parity(gpu, name, jit):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", CASES)
-def test_gpu_transcode_golden(gpu, name):
+def test_gpu_transcode_golden(gpu, name, jit):
     """Binary <-> Compact of nested records == the reference's stream of the
     same values in the other protocol."""
     src = nh.NestedCase(name)

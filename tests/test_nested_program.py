@@ -44,12 +44,15 @@ def test_nested_program_scope():
     assert rc == 0, log
 
 
-def _encode(gpu, protocol, n, seed):
+def _encode(gpu, protocol, n, seed, monkeypatch=None, nested=False, batch=None):
     import torch
 
     from fbthrift_amd import serializer as SZ
 
-    schema, recs, lbase, *_ = bench.nested_batch(gpu, n, seed)
+    if monkeypatch is not None:
+        monkeypatch.setenv("TGPU_JIT", "1")
+        monkeypatch.setenv("TGPU_NESTED", "1" if nested else "0")
+    schema, recs, lbase, *_ = batch or bench.nested_batch(gpu, n, seed)
     gs = SZ.GpuSchema(schema)
     Ser = {0: SZ.BinarySerializer, 2: SZ.CompactSerializer}[protocol]
     wire, offs = Ser.serialize(gs, recs, n, list_base=lbase)
@@ -114,3 +117,57 @@ def test_nested_program_irregular_records(gpu, protocol, monkeypatch):
     assert st.as_tuple() == gst.as_tuple() and (nd, cons) == (gnd, gcons)
     assert np.array_equal(rec, grec)
     assert np.array_equal(arena, garena)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("protocol", [0, 2])
+def test_nested_program_encode_parity(gpu, protocol, monkeypatch):
+    """The nested program's size / write passes: the general writer's bytes
+    and offsets, and the oracle's encode of the same records."""
+    import torch
+
+    n = 40 * 1024
+    batch = bench.nested_batch(gpu, n, 0xe0c + protocol)
+    schema, gs, Ser, wire, offs = _encode(gpu, protocol, n, 0, monkeypatch, True, batch)
+    _, _, _, gwire, goffs = _encode(gpu, protocol, n, 0, monkeypatch, False, batch)
+    assert torch.equal(wire, gwire) and torch.equal(offs, goffs)
+    monkeypatch.setenv("TGPU_NESTED", "1")
+    sz, total = Ser.encoded_size(gs, batch[1], n, list_base=batch[2])
+    assert total == wire.numel()
+    assert torch.equal(sz.to(offs.dtype)[: n + 1], offs[: n + 1])
+    rec = batch[1].cpu().numpy()
+    lb = batch[2].cpu().numpy()
+    ost, owire, ooffs = oracle.encode(schema, protocol, rec, n, np.zeros(1, np.uint8), lb)
+    assert ost.code == 0 and owire == wire.cpu().numpy().tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("protocol", [0, 2])
+def test_nested_program_encode_size_limit(gpu, protocol, monkeypatch):
+    """A list length above INT32_MAX (checked_container_size): the same
+    WRITE_SIZE_LIMIT status, record and offset as the general writer."""
+    from fbthrift_amd import serializer as SZ
+
+    n = 1000
+    schema, recs, lbase, *_ = bench.nested_batch(gpu, n, 0x51)
+    m = schema.member[(0, 1)]
+    recs.view(-1, schema.size[0])[613, m + 8: m + 12] = torch_u8([0, 0, 0, 0x80], gpu)
+    gs = SZ.GpuSchema(schema)
+    Ser = {0: SZ.BinarySerializer, 2: SZ.CompactSerializer}[protocol]
+    import torch
+
+    buf = torch.empty(1 << 20, dtype=torch.uint8, device=gpu)
+    out = []
+    for nested in ("1", "0"):
+        monkeypatch.setenv("TGPU_JIT", "1")
+        monkeypatch.setenv("TGPU_NESTED", nested)
+        with pytest.raises(SZ.TProtocolException) as ei:
+            Ser.serialize(gs, recs, n, list_base=lbase, out=buf, offsets=None)
+        out.append(str(ei.value))
+    assert out[0] == out[1] and "WRITE_SIZE_LIMIT" in out[0] and "613" in out[0], out
+
+
+def torch_u8(v, dev):
+    import torch
+
+    return torch.tensor(v, dtype=torch.uint8, device=dev)
