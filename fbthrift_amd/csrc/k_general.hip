@@ -514,7 +514,9 @@ hipError_t launch_general_encode(const EncodeArgs& a, int protocol, uint64_t n_b
     if (e == hipSuccess)
       e = launch_scan_tiles(a.block_sums, n_blocks, a.scan_part, &a.res->total_bytes,
                             a.offs + a.n, stream);
-    if (e == hipSuccess) e = jit_launch_encode(nj, true, a, n_blocks, 0, stream, 2);
+    // (a.out_cap: the write pass's LDS output tile, 0 = none)
+    if (e == hipSuccess)
+      e = jit_launch_encode(nj, true, a, n_blocks, a.out_cap ? a.out_cap + 16 : 0, stream, 2);
     return e;
   }
   TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_size_kernel<P_>, grid, dim3(256), sb, stream, a,

@@ -68,6 +68,20 @@ void learn_mean(const tgpu_schema* s, int protocol, uint64_t bytes, uint64_t n) 
 // 4 and 24 KiB (a smaller tile lets more workgroups share a CU: the write
 // pass waits on memory most of the time). 0 = the kernel's default (24 KiB)
 // until a size is known. TGPU_ENC_OUTCAP=<bytes> overrides (A/B).
+// The nested write pass's LDS output tile: 256 records of the learned mean
+// size + 15 % + 1 KiB (48 KiB until a size is known), 4..60 KiB.
+// TGPU_NESTED_OUTCAP=<bytes> overrides (0: no staging, A/B).
+uint32_t nested_out_cap(const tgpu_schema* s, int protocol) {
+  if (const char* v = getenv("TGPU_NESTED_OUTCAP")) {
+    const uint32_t f = (uint32_t)strtoul(v, nullptr, 10);
+    return f ? std::min<uint32_t>(std::max<uint32_t>(f, 4096), 60 * 1024) & ~15u : 0u;
+  }
+  const uint64_t m16 = s->mean16[proto_slot(protocol)];
+  if (!m16) return 48 * 1024;
+  const uint64_t want = (m16 * 256 / 16) * 115 / 100 + 1024;
+  return (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, 4096), 60 * 1024) & ~15u;
+}
+
 uint32_t enc_out_cap(const tgpu_schema* s, int protocol) {
   static const uint32_t force = [] {
     const char* v = getenv("TGPU_ENC_OUTCAP");
@@ -1597,9 +1611,11 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
       if (has_prog(schema, protocol) && program_encode_fits(rs))
         e = launch_program_encode(a, schema->d_prog[prog_protocol(schema, protocol)], ctx->d_scan_part, false, s,
                                   schema_jit(schema, protocol, JIT_ENCODE, n, 0));
-      else  // (the writer has no depth limit: height / max_depth do not apply)
-        e = launch_general_encode(a, protocol, nb, s,
-                                  nested_jit(schema, protocol, n, INT32_MAX, INT32_MAX));
+      else {  // (the writer has no depth limit: height / max_depth do not apply)
+        const JitKernels* nj = nested_jit(schema, protocol, n, INT32_MAX, INT32_MAX);
+        if (nj) a.out_cap = nested_out_cap(schema, protocol);
+        e = launch_general_encode(a, protocol, nb, s, nj);
+      }
     }
   }
   if (e == hipSuccess && n) e = launch_encode_finish(a, protocol, fixed, s);

@@ -245,7 +245,8 @@ std::string gen_source(const VProgram& P, int group) {
          "}\n"
          "extern \"C\" __global__ __launch_bounds__(256) void tgpu_jit_nwrite(EncodeArgs a) {\n"
          "  __shared__ unsigned long long part[4];\n"
-         "  nested_write_tile(a, NE{}, part);\n"
+         "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+         "  nested_write_tile(a, NE{}, part, smem, a.out_cap);\n"
          "}\n";
     return o.str();
   }

@@ -265,13 +265,14 @@ struct Count {
 // Bytes into HBM from an 8-byte accumulator: whole aligned words with one
 // 8-byte store, the record's first and last partial words byte by byte (the
 // neighbouring records own the rest of those words).
-struct Out {
+template <bool kLds>
+struct OutT {
   static constexpr bool kCount = false;
   uint8_t* w;      // current aligned word
   uint64_t acc;    // its pending bytes (little-endian)
   uint32_t nb;     // bytes in acc (incl. the skipped head of the first word)
   uint32_t lo;     // first byte of the current word this record owns
-  __device__ __forceinline__ Out(uint8_t* out, uint64_t start) {
+  __device__ __forceinline__ OutT(uint8_t* out, uint64_t start) {
     const uintptr_t at = (uintptr_t)out + start;
     w = (uint8_t*)(at & ~(uintptr_t)7);
     nb = lo = (uint32_t)(at & 7);
@@ -280,6 +281,9 @@ struct Out {
   __device__ __forceinline__ void emit(uint64_t x) {
     if (lo == 0) {
       *(uint64_t*)w = x;
+    } else if constexpr (kLds) {  // a zero-filled LDS tile: OR in the bytes this record owns
+      atomicOr((unsigned long long*)w, (unsigned long long)(x & (~0ull << (8 * lo))));
+      lo = 0;
     } else {
       for (uint32_t b = lo; b < 8; ++b) w[b] = (uint8_t)(x >> (8 * b));
       lo = 0;
@@ -315,9 +319,16 @@ struct Out {
     }
   }
   __device__ __forceinline__ void flush() {
-    for (uint32_t b = lo; b < nb; ++b) w[b] = (uint8_t)(acc >> (8 * b));
+    if (nb <= lo) return;
+    if constexpr (kLds) {
+      const uint64_t m = (nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1)) & (~0ull << (8 * lo));
+      atomicOr((unsigned long long*)w, (unsigned long long)(acc & m));
+    } else {
+      for (uint32_t b = lo; b < nb; ++b) w[b] = (uint8_t)(acc >> (8 * b));
+    }
   }
 };
+using Out = OutT<false>;
 
 __device__ __forceinline__ uint32_t lebn(uint64_t v) {  // LEB128 bytes of v
   const uint32_t bits = 64 - (uint32_t)__builtin_clzll(v | 1);
@@ -461,24 +472,55 @@ __device__ __forceinline__ void nested_size_tile(const EncodeArgs& a, const E& e
   if (threadIdx.x == 0) a.block_sums[blockIdx.x] = total;
 }
 
-// Write pass: record starts from the scanned tile sums (encode_write_kernel),
-// each lane writing its record straight to the stream.
+// Write pass: record starts from the scanned tile sums (encode_write_kernel).
+// The tile's output (cap bytes of dynamic LDS, zero-filled) is built in LDS
+// — whole words stored, each record's two edge words OR-ed in — and leaves
+// with 16-byte stores, byte stores only in the two vectors shared with the
+// neighbouring tiles; a tile larger than cap writes its records straight to
+// the stream.
 template <class E>
 __device__ __forceinline__ void nested_write_tile(const EncodeArgs& a, const E& enc,
-                                                  unsigned long long* part) {
+                                                  unsigned long long* part, uint8_t* tile,
+                                                  uint32_t cap) {
   const uint64_t i = (uint64_t)blockIdx.x * kET + threadIdx.x;
   const unsigned long long sz = i < a.n ? a.offs[i] : 0;
   unsigned long long total;
-  const unsigned long long start = a.block_sums[blockIdx.x] + block_exscan256(sz, part, &total);
-  if (i >= a.n) return;
-  a.offs[i] = start;
-  if (start + sz > a.cap) {
-    atomicMin(&a.res->first_fail, (unsigned long long)i);
-    return;
+  const unsigned long long t0 = a.block_sums[blockIdx.x];
+  const unsigned long long start = t0 + block_exscan256(sz, part, &total);
+  const uint32_t sh = (uint32_t)(((uintptr_t)a.out + t0) & 15);
+  const bool staged = cap && total + sh + 16 <= cap && t0 + total <= a.cap;
+  if (staged) {
+    const uint4 z = {0u, 0u, 0u, 0u};
+    const uint32_t nz = (uint32_t)((sh + total + 15) >> 4);
+    for (uint32_t k = threadIdx.x; k < nz; k += kET) ((uint4*)tile)[k] = z;
   }
-  if (sz == 0) return;  // (a record the size pass failed: the finish kernel reports it)
-  Out o(a.out, start);
-  if (enc(a.recs + i * a.rec_size, a.sbase, a.lbase, o)) o.flush();
+  __syncthreads();
+  if (i < a.n) {
+    a.offs[i] = start;
+    if (start + sz > a.cap) {
+      atomicMin(&a.res->first_fail, (unsigned long long)i);
+    } else if (sz) {  // (sz 0: a record the size pass failed; the finish kernel reports it)
+      if (staged) {
+        OutT<true> o(tile + sh - (uintptr_t)0, start - t0);
+        if (enc(a.recs + i * a.rec_size, a.sbase, a.lbase, o)) o.flush();
+      } else {
+        Out o(a.out, start);
+        if (enc(a.recs + i * a.rec_size, a.sbase, a.lbase, o)) o.flush();
+      }
+    }
+  }
+  if (!staged) return;  // (uniform per workgroup)
+  __syncthreads();
+  uint8_t* base = a.out + t0 - sh;  // 16-byte aligned
+  const uint32_t end = sh + (uint32_t)total;
+  for (uint32_t k = threadIdx.x; k < ((end + 15) >> 4); k += kET) {
+    const uint32_t lo = k << 4, hi = lo + 16;
+    if (lo >= sh && hi <= end) {
+      ((uint4*)base)[k] = ((const uint4*)tile)[k];
+    } else {
+      for (uint32_t b = (lo < sh ? sh : lo); b < (hi < end ? hi : end); ++b) base[b] = tile[b];
+    }
+  }
 }
 
 }  // namespace prog

@@ -121,10 +121,16 @@ def test_nested_program_irregular_records(gpu, protocol, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("protocol", [0, 2])
-def test_nested_program_encode_parity(gpu, protocol, monkeypatch):
+@pytest.mark.parametrize("outcap", ["default", "4096"])
+def test_nested_program_encode_parity(gpu, protocol, outcap, monkeypatch):
     """The nested program's size / write passes: the general writer's bytes
-    and offsets, and the oracle's encode of the same records."""
+    and offsets, and the oracle's encode of the same records. outcap 4096:
+    the LDS output tile too small for any tile, every record written
+    straight to the stream."""
     import torch
+
+    if outcap != "default":
+        monkeypatch.setenv("TGPU_NESTED_OUTCAP", outcap)
 
     n = 40 * 1024
     batch = bench.nested_batch(gpu, n, 0xe0c + protocol)
