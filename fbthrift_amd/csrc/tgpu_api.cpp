@@ -953,12 +953,16 @@ bool launch_nested_decode(tgpu_context* ctx, const tgpu_schema* schema, int prot
   if (!J) return false;
   constexpr uint32_t kPT = 256;  // records per tile (prog::kPT)
   const uint64_t tiles = (a.n + kPT - 1) / kPT;
-  // the wire tile: 1.15 x the mean tile + 1 KiB, within 64 KiB of LDS with
-  // the record tile (a larger tile's records take the general decoder)
+  // the wire tile: 1.15 x the mean tile + 1 KiB, within 80 KiB of LDS with
+  // the record tile (half a CU's 160 KiB: two workgroups per CU; a larger
+  // tile's records take the general decoder). TGPU_NESTED_LDS=<bytes>
+  // overrides the 80 KiB (A/B).
   const uint32_t rt = (kPT * a.rec_size + 16 + 15) & ~15u;
   const double mean = (double)a.in_len / (double)a.n * kPT;
   double cap = 1.15 * mean + 1024.0;
-  const double room = 65536.0 - rt - 4096.0 - 32.0;
+  const char* lv = getenv("TGPU_NESTED_LDS");
+  const double lds_max = lv ? std::min(atof(lv), 163840.0) : 81920.0;
+  const double room = lds_max - rt - 4096.0 - 32.0;
   if (cap > room) cap = room;
   if (cap < 4096.0) cap = 4096.0;
   const uint32_t wire_cap = (uint32_t)cap & ~15u;
