@@ -557,8 +557,9 @@ VOp make_op(uint8_t kind) {
 // header bytes the generated writer emits (BinaryProtocol-inl.h:53-59,
 // CompactProtocol-inl.h:133-160 incl. long-form ids, bools in the header) and
 // each value's encoding.
-bool emit_seq(const tgpu_schema& sc, uint32_t et, int32_t esi, uint32_t eti, uint32_t member,
-              uint32_t isset, int proto, VProgram& P, uint32_t depth, uint32_t* max_depth);
+bool emit_container(const tgpu_schema& sc, uint32_t ttype, uint32_t et, uint32_t vt, int32_t esi,
+                    uint32_t eti, uint32_t ki, uint32_t member, uint32_t isset, int proto,
+                    VProgram& P, uint32_t depth, uint32_t* max_depth);
 
 // nested (build_nested_program): lists / sets of structs or of scalar lists
 // become VOP_SEQ loops whose bodies address the element slot (base 0);
@@ -622,10 +623,11 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
     } else if (f.ttype == TGPU_T_STRING) {
       v.kind = VOP_STRING;
       if (!push_op(P, v)) return false;
-    } else if (nested && (f.ttype == TGPU_T_LIST || f.ttype == TGPU_T_SET) &&
-               !is_scalar(f.elem_ttype)) {
-      if (!emit_seq(sc, f.elem_ttype, f.struct_index, f.type_index, member, isset, proto, P,
-                    depth + 1, max_depth))
+    } else if (nested && (f.ttype == TGPU_T_MAP || ((f.ttype == TGPU_T_LIST ||
+                                                     f.ttype == TGPU_T_SET) &&
+                                                    !is_scalar(f.elem_ttype)))) {
+      if (!emit_container(sc, f.ttype, f.elem_ttype, f.val_ttype, f.struct_index, f.type_index,
+                          f.key_index, member, isset, proto, P, depth, max_depth))
         return false;
     } else if (f.ttype == TGPU_T_LIST || f.ttype == TGPU_T_SET) {
       v.kind = VOP_LIST;
@@ -659,49 +661,118 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
   return true;
 }
 
-// A list / set (member / isset of the enclosing object) of elements `et`:
-// VOP_SEQ, the element's body (a struct's fields + STOP, or one scalar list
-// at the element slot), VOP_SEQ_END.
-bool emit_seq(const tgpu_schema& sc, uint32_t et, int32_t esi, uint32_t eti, uint32_t member,
-              uint32_t isset, int proto, VProgram& P, uint32_t depth, uint32_t* max_depth) {
-  VOp q = make_op(VOP_SEQ);
-  q.member = (uint16_t)member;
-  q.isset = (uint16_t)isset;
-  q.elem_ttype = (uint8_t)et;
-  q.elem_ct = (uint8_t)compact_ctype(et);
-  const uint32_t at = P.n_ops;
-  if (et == TGPU_T_STRUCT) {
-    if (esi < 0 || (uint32_t)esi >= sc.structs.size()) return false;
-    q.hdr = sc.structs[esi].size;
-    if (!push_op(P, q) || !emit_program(sc, (uint32_t)esi, 0, proto, P, true, depth, max_depth))
-      return false;
+// A leaf value op at member: a scalar (no bools: their Compact container
+// form differs) or a string view.
+bool emit_leaf(uint32_t t, uint32_t member, int proto, VProgram& P) {
+  VOp v = make_op(VOP_FIXED);
+  v.member = (uint16_t)member;
+  if (t == TGPU_T_STRING) {
+    v.kind = VOP_STRING;
+  } else if (is_scalar(t) && t != TGPU_T_BOOL) {
+    v.width = (uint8_t)scalar_size(t);
+    if (proto == TGPU_PROTOCOL_COMPACT && (t == TGPU_T_I16 || t == TGPU_T_I32 || t == TGPU_T_I64)) {
+      v.kind = VOP_VARINT;
+      v.bits = t == TGPU_T_I64 ? 64 : 32;
+    }
+  } else {
+    return false;
+  }
+  return push_op(P, v);
+}
+
+// One value of type t (struct si / type node ti) in a container slot at
+// member: a struct's fields + STOP, a container, or a leaf.
+bool emit_value(const tgpu_schema& sc, uint32_t t, int32_t si, uint32_t ti, uint32_t member,
+                int proto, VProgram& P, uint32_t depth, uint32_t* max_depth) {
+  if (t == TGPU_T_STRUCT) {
+    if (si < 0 || (uint32_t)si >= sc.structs.size()) return false;
+    if (!emit_program(sc, (uint32_t)si, member, proto, P, true, depth, max_depth)) return false;
     VOp stop = make_op(VOP_CONST);
     stop.hdr_len = 1;
-    if (!push_op(P, stop)) return false;
-  } else if (et == TGPU_T_LIST || et == TGPU_T_SET) {
-    if (eti == 0 || eti > sc.types.size()) return false;
-    const tgpu_type_desc& t = sc.types[eti - 1];
-    const uint32_t e = t.elem_ttype;
-    if (t.ttype != et || !is_scalar(e)) return false;  // deeper / string elements: general
-    q.hdr = (uint32_t)sizeof(tgpu_span);
-    VOp v = make_op(VOP_LIST);
-    v.member = 0;
-    v.width = (uint8_t)scalar_size(e);
-    v.elem_ttype = (uint8_t)e;
-    v.elem_ct = (uint8_t)compact_ctype(e);
-    v.elem_kind = e == TGPU_T_BOOL ? VEL_BOOL : VEL_FIXED;
-    if (proto == TGPU_PROTOCOL_COMPACT && (e == TGPU_T_I16 || e == TGPU_T_I32 || e == TGPU_T_I64)) {
-      v.elem_kind = VEL_VARINT;
-      v.bits = e == TGPU_T_I64 ? 64 : 32;
-    }
-    if (!push_op(P, q) || !push_op(P, v)) return false;
-    if (max_depth) *max_depth = std::max(*max_depth, depth + 1);
-  } else {
-    return false;  // maps, strings: the general kernels
+    return push_op(P, stop);
   }
-  if (max_depth) *max_depth = std::max(*max_depth, depth);
-  if (!push_op(P, make_op(VOP_SEQ_END))) return false;
-  P.ops[at].hdr_len = (uint8_t)P.n_ops;  // one past the matching VOP_SEQ_END
+  if (t == TGPU_T_LIST || t == TGPU_T_SET || t == TGPU_T_MAP) {
+    if (ti == 0 || ti > sc.types.size()) return false;
+    const tgpu_type_desc& n = sc.types[ti - 1];
+    if (n.ttype != t) return false;
+    return emit_container(sc, t, n.elem_ttype, n.val_ttype, n.struct_index, n.type_index,
+                          n.key_index, member, 0xffff, proto, P, depth, max_depth);
+  }
+  return emit_leaf(t, member, proto, P);
+}
+
+// Bytes of a container slot holding a value of type t.
+uint32_t slot_bytes(const tgpu_schema& sc, uint32_t t, int32_t si) {
+  if (t == TGPU_T_STRUCT) return si >= 0 && (uint32_t)si < sc.structs.size() ? sc.structs[si].size : 0;
+  if (t == TGPU_T_STRING || t == TGPU_T_LIST || t == TGPU_T_SET || t == TGPU_T_MAP)
+    return (uint32_t)sizeof(tgpu_span);
+  return scalar_size(t);
+}
+
+// A container value (list / set / map) whose span is at member (isset:
+// 0xffff inside containers). Lists of scalars / strings are one VOP_LIST;
+// lists of structs / containers a VOP_SEQ loop; maps a VOP_MSEQ loop with
+// the key (a non-bool scalar or a string) and the value in the body.
+bool emit_container(const tgpu_schema& sc, uint32_t ttype, uint32_t et, uint32_t vt, int32_t esi,
+                    uint32_t eti, uint32_t ki, uint32_t member, uint32_t isset, int proto,
+                    VProgram& P, uint32_t depth, uint32_t* max_depth) {
+  if (member > 0xfffe) return false;
+  const uint32_t d = depth + 1;  // this container's level
+  if (max_depth) *max_depth = std::max(*max_depth, d);
+  if (ttype == TGPU_T_LIST || ttype == TGPU_T_SET) {
+    if (is_scalar(et) || et == TGPU_T_STRING) {  // elements read in place
+      VOp v = make_op(VOP_LIST);
+      v.member = (uint16_t)member;
+      v.isset = (uint16_t)isset;
+      v.elem_ttype = (uint8_t)et;
+      v.elem_ct = (uint8_t)compact_ctype(et);
+      if (et == TGPU_T_STRING) {
+        v.width = (uint8_t)sizeof(tgpu_span);
+        v.elem_kind = VEL_STRING;
+      } else {
+        v.width = (uint8_t)scalar_size(et);
+        v.elem_kind = et == TGPU_T_BOOL ? VEL_BOOL : VEL_FIXED;
+        if (proto == TGPU_PROTOCOL_COMPACT &&
+            (et == TGPU_T_I16 || et == TGPU_T_I32 || et == TGPU_T_I64)) {
+          v.elem_kind = VEL_VARINT;
+          v.bits = et == TGPU_T_I64 ? 64 : 32;
+        }
+      }
+      P.has_list = 1;
+      return push_op(P, v);
+    }
+    VOp q = make_op(VOP_SEQ);
+    q.member = (uint16_t)member;
+    q.isset = (uint16_t)isset;
+    q.elem_ttype = (uint8_t)et;
+    q.elem_ct = (uint8_t)compact_ctype(et);
+    q.hdr = slot_bytes(sc, et, esi);
+    const uint32_t at = P.n_ops;
+    if (!q.hdr || !push_op(P, q) || !emit_value(sc, et, esi, eti, 0, proto, P, d, max_depth) ||
+        !push_op(P, make_op(VOP_SEQ_END)))
+      return false;
+    P.ops[at].hdr_len = (uint8_t)P.n_ops;  // one past the matching VOP_SEQ_END
+    P.has_list = 1;
+    return true;
+  }
+  if (ttype != TGPU_T_MAP || ki != 0) return false;  // struct / container keys: general
+  if (!(et == TGPU_T_STRING || (is_scalar(et) && et != TGPU_T_BOOL)) || vt == TGPU_T_BOOL)
+    return false;
+  VOp q = make_op(VOP_MSEQ);
+  q.member = (uint16_t)member;
+  q.isset = (uint16_t)isset;
+  q.width = (uint8_t)et;            // key ttype
+  q.bits = (uint8_t)slot_bytes(sc, et, -1);  // key slot bytes
+  q.elem_ttype = (uint8_t)vt;       // value ttype
+  q.elem_ct = (uint8_t)((compact_ctype(et) << 4) | compact_ctype(vt));
+  const uint32_t vs = slot_bytes(sc, vt, esi);
+  q.hdr = q.bits + vs;
+  const uint32_t at = P.n_ops;
+  if (!vs || !push_op(P, q) || !emit_leaf(et, 0, proto, P) ||
+      !emit_value(sc, vt, esi, eti, q.bits, proto, P, d, max_depth) ||
+      !push_op(P, make_op(VOP_SEQ_END)))
+    return false;
+  P.ops[at].hdr_len = (uint8_t)P.n_ops;
   P.has_list = 1;
   return true;
 }

@@ -167,11 +167,17 @@ enum VOpKind : uint8_t {
   // element slot of hdr bytes; elem_ttype / elem_ct: the wire element type.
   VOP_SEQ = 8,
   VOP_SEQ_END = 9,
+  // a map whose pairs are {key (width: its ttype, bits: its slot bytes),
+  // value (elem_ttype)}: header (elem_ct = Compact key/value ctypes), hdr-byte
+  // pairs from the region, the body (key op at 0, the value's ops at bits)
+  // once per pair, ended by VOP_SEQ_END like VOP_SEQ
+  VOP_MSEQ = 10,
 };
 enum VElemKind : uint8_t {
   VEL_FIXED = 1,   // big-endian fixed width (Binary ints, doubles/floats, bytes)
   VEL_VARINT = 2,  // zigzag varint (Compact i16/i32/i64)
   VEL_BOOL = 3,    // Binary: byte must be 0/1; Compact: value = (byte == 1)
+  VEL_STRING = 4,  // nested programs: a string -> tgpu_span element (a view into the stream)
 };
 struct VOp {
   uint8_t kind;

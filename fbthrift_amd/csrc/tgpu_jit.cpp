@@ -87,13 +87,13 @@ void gen_enc_ops(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t 
   const std::string in(indent, ' ');
   while (k < stop) {
     const VOp& v = P.ops[k];
-    if (v.kind == VOP_SEQ) {
+    if (v.kind == VOP_SEQ || v.kind == VOP_MSEQ) {
       const std::string sp = "s" + std::to_string(k), a = "a" + std::to_string(k),
                         i = "i" + std::to_string(k), e = "e" + std::to_string(k);
       o << in << "{\n"
         << in << "  const tgpu_span " << sp << " = seq_span(kOps[" << k << "], " << b << ");\n"
-        << in << "  if (!put_list_header(o, kOps[" << k << "], kCompact, " << sp
-        << ".length)) return false;\n"
+        << in << "  if (!" << (v.kind == VOP_SEQ ? "put_list_header" : "put_map_header") << "(o, kOps["
+        << k << "], kCompact, " << sp << ".length)) return false;\n"
         << in << "  const uint8_t* " << a << " = lbase + " << sp << ".offset;\n"
         << in << "  for (uint32_t " << i << " = 0; " << i << " < " << sp << ".length; ++" << i
         << ") {\n"
@@ -118,17 +118,20 @@ void gen_ops(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t stop
   const std::string in(indent, ' ');
   while (k < stop) {
     const VOp& v = P.ops[k];
-    if (v.kind == VOP_SEQ) {
+    if (v.kind == VOP_SEQ || v.kind == VOP_MSEQ) {
       const std::string n = "n" + std::to_string(k), a = "a" + std::to_string(k),
                         i = "i" + std::to_string(k), e = "e" + std::to_string(k);
       o << in << "{\n"
         << in << "  uint32_t " << n << ";\n"
         << in << "  uint8_t* " << a << ";\n"
-        << in << "  if (!seq_open(kOps[" << k << "], kCompact, src, c, p, end, " << b << ", bump, "
-        << n << ", " << a << ")) return false;\n"
+        << in << "  if (!" << (v.kind == VOP_SEQ ? "seq_open" : "mseq_open") << "(kOps[" << k
+        << "], kCompact, src, c, p, end, " << b << ", bump, " << n << ", " << a
+        << ")) return false;\n"
         << in << "  for (uint32_t " << i << " = 0; " << i << " < " << n << "; ++" << i << ") {\n"
         << in << "    uint8_t* " << e << " = " << a << " + (uint64_t)" << i << " * " << v.hdr
         << "u;\n";
+      // (a struct element / value is default-constructed first; every other
+      // slot is written whole)
       if (v.elem_ttype == TGPU_T_STRUCT) o << in << "    zero_slot<" << v.hdr << "u>(" << e << ");\n";
       gen_ops(o, P, k + 1, v.hdr_len - 1, e, indent + 4);
       o << in << "  }\n"
@@ -431,7 +434,8 @@ int jit_compile_check(const VProgram& P, const char* arch, char* log, uint64_t l
   std::string l;
   bool ok = true;
   bool nested = false;
-  for (uint32_t k = 0; k < P.n_ops; ++k) nested |= P.ops[k].kind == VOP_SEQ;
+  for (uint32_t k = 0; k < P.n_ops; ++k)
+    nested |= P.ops[k].kind == VOP_SEQ || P.ops[k].kind == VOP_MSEQ || P.ops[k].kind == VOP_SEQ_END;
   for (int group = nested ? JIT_NESTED : 0; group < (nested ? JIT_NESTED + 1 : JIT_NESTED) && ok;
        ++group) {
     std::vector<char> code;

@@ -88,6 +88,49 @@ __device__ __forceinline__ void seq_close(const VOp op, uint8_t* base) {
   if (op.isset != 0xffff) base[op.isset] = 1;
 }
 
+// VOP_MSEQ: a map header (Binary: key type, value type, BE i32; Compact:
+// varint size, then the key/value ctype byte when size > 0;
+// BinaryProtocol-inl.h:506-524, CompactProtocol-inl.h:662-690), the
+// truncation check of two bytes a pair, the pairs from the region.
+template <class Src>
+__device__ __forceinline__ bool mseq_open(const VOp op, const bool compact, const Src& src,
+                                          const Ctx& c, uint32_t& p, const uint32_t end,
+                                          uint8_t* base, uint64_t& bump, uint32_t& n_out,
+                                          uint8_t*& arr) {
+  int64_t n;
+  if (compact) {
+    uint64_t z;
+    if (!read_varint(src, p, end, 32, z)) return false;
+    n = (int32_t)(uint32_t)z;
+    if (n > 0) {
+      if (p + 1 > end || (src.win8(p) & 0xff) != op.elem_ct) return false;
+      ++p;
+    }
+  } else {
+    if (p + 6 > end) return false;
+    const uint64_t w = src.win8(p);
+    if ((w & 0xff) != op.width || ((w >> 8) & 0xff) != op.elem_ttype) return false;
+    n = (int32_t)(uint32_t)bswap_n(w >> 16, 4);
+    p += 6;
+  }
+  if (n < 0 || (c.container_limit && n > c.container_limit) || 2 * n > (int64_t)(end - p))
+    return false;
+  tgpu_span* sp = (tgpu_span*)(base + op.member);
+  n_out = (uint32_t)n;
+  arr = nullptr;
+  if (n == 0) {
+    *sp = tgpu_span{0, 0, 0};
+    return true;
+  }
+  const uint64_t bytes = (uint64_t)n * op.hdr;
+  if (!c.arena) return false;
+  const uint64_t aoff = region_alloc(bump, bytes);
+  if (aoff + bytes > c.arena_cap) return false;
+  arr = c.arena + aoff;
+  *sp = tgpu_span{aoff, (uint32_t)n, 0};
+  return true;
+}
+
 // A default-constructed struct element (the general reader zeroes the slot
 // before reading into it); ES is a compile-time constant.
 template <uint32_t ES>
@@ -122,6 +165,23 @@ __device__ __forceinline__ bool nlist(const VOp op, const bool compact, const Sr
   uint8_t* dst = c.arena + aoff;
   for (int64_t i = 0; i < n; ++i) {
     uint64_t v;
+    if (op.elem_kind == VEL_STRING) {  // read_elem: a view into the stream
+      int64_t len;
+      if (compact) {
+        uint64_t z;
+        if (!read_varint(src, p, end, 32, z)) return false;
+        len = (int32_t)(uint32_t)z;
+      } else {
+        if (p + 4 > end) return false;
+        len = (int32_t)(uint32_t)bswap_n(src.win8(p), 4);
+        p += 4;
+      }
+      if (len < 0 || (c.string_limit > 0 && len > c.string_limit) || len > (int64_t)(end - p))
+        return false;
+      *(tgpu_span*)(dst + (uint64_t)i * es) = tgpu_span{len ? c.gbase + p : 0, (uint32_t)len, 0};
+      p += (uint32_t)len;
+      continue;
+    }
     if (op.elem_kind == VEL_VARINT) {
       uint64_t z;
       if (!read_varint(src, p, end, op.bits, z)) return false;
@@ -381,6 +441,22 @@ __device__ __forceinline__ bool put_list_header(O& o, const VOp op, const bool c
   return true;
 }
 
+// writeMapBegin (BinaryProtocol-inl.h:83-96, CompactProtocol-inl.h:219-246)
+template <class O>
+__device__ __forceinline__ bool put_map_header(O& o, const VOp op, const bool compact, uint32_t n) {
+  if (n > 0x7fffffffu) return false;
+  if (!compact) {
+    o.put(op.width | ((uint32_t)op.elem_ttype << 8), 2);
+    o.put(__builtin_bswap32(n), 4);
+  } else if (n == 0) {
+    o.put(0, 1);
+  } else {
+    nput_varint(o, n);
+    o.put(op.elem_ct, 1);
+  }
+  return true;
+}
+
 // A fixed-width scalar of w bytes at p as the writer emits it
 // (write_scalar): big-endian, a bool validated (0/1; Compact 1 / 2).
 template <class O>
@@ -429,14 +505,20 @@ __device__ __forceinline__ bool enc_op(const VOp op, const bool compact, const u
       const uint8_t* e = lbase + sp.offset;
       const uint32_t es = op.width;
       if constexpr (O::kCount) {
-        if (op.elem_kind != VEL_VARINT && op.elem_kind != VEL_BOOL) {
+        if (op.elem_kind == VEL_FIXED) {
           o.n += (uint64_t)sp.length * es;
           return true;
         }
       }
       for (uint32_t i = 0; i < sp.length; ++i) {
         const uint8_t* p = e + (uint64_t)i * es;
-        if (op.elem_kind == VEL_VARINT) {
+        if (op.elem_kind == VEL_STRING) {
+          const tgpu_span st = *(const tgpu_span*)p;
+          if (st.length > 0x7fffffffu) return false;  // checkBinarySize
+          if (compact) nput_varint(o, st.length);
+          else o.put(__builtin_bswap32(st.length), 4);
+          o.bytes(sbase + st.offset, st.length);
+        } else if (op.elem_kind == VEL_VARINT) {
           nput_varint(o, zz_member(load_member(p, es), es, op.bits));
         } else if (!put_fixed(o, compact, p, es, op.elem_kind == VEL_BOOL)) {
           return false;

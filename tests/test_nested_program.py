@@ -6,9 +6,9 @@ arena bytes exactly (same record regions, same allocation order), and leave
 every record off the canonical form to the general decoder.
 
 CPU: the nested programs of the bench schema (tests/../bench.py NESTED_TABLE:
-{i64, list<Item>, list<list<i32>>}) compile for gfx950 in both protocols;
-schemas it does not cover (maps, strings inside containers, optional fields)
-have none. GPU: 40 Ki records of that schema against the oracle's decode of
+{i64, list<Item>, list<list<i32>>}) and of maps / string elements compile for
+gfx950 in both protocols; schemas it does not cover (struct keys, bools
+inside maps, optional fields) have none. GPU: 40 Ki records of that schema against the oracle's decode of
 the same stream, and the nested kernel against the general decoder
 (TGPU_NESTED=0) bit for bit, incl. records and arena bytes; the golden nested
 cases under TGPU_JIT=1 are in test_nested_containers.py."""
@@ -20,7 +20,7 @@ from fbthrift_amd.schema import Schema
 from fbthrift_amd.serializer import compile_check
 from oracle import oracle
 
-T_I32, T_STRING, T_LIST, T_STRUCT, T_MAP = 8, 11, 15, 12, 13
+T_BOOL, T_I32, T_STRING, T_LIST, T_STRUCT, T_MAP = 2, 8, 11, 15, 12, 13
 
 
 @pytest.mark.parametrize("protocol", [0, 2])
@@ -30,10 +30,22 @@ def test_nested_program_compiles(protocol):
 
 
 def test_nested_program_scope():
-    # map<i32, Item>: no nested program (general reader)
-    with_map = [[[1, T_MAP, T_I32, 0, 1, T_STRUCT]], [[1, T_I32, 0, 0, -1]]]
-    rc, _ = compile_check(Schema.from_table(with_map), 0)
+    # map<Item, i32> (a struct key): no nested program (general reader)
+    skey = [[[1, T_MAP, T_STRUCT, 0, -1, T_I32, None, [T_STRUCT, 0, 0, 1]]],
+            [[1, T_I32, 0, 0, -1]]]
+    rc, _ = compile_check(Schema.from_table(skey), 0)
     assert rc == 22
+    # list<map<i32, bool>>: none either (bools inside maps)
+    mbool = [[[1, T_LIST, T_MAP, 0, -1, 0, [T_MAP, T_I32, T_BOOL, -1]]]]
+    rc, _ = compile_check(Schema.from_table(mbool), 2)
+    assert rc == 22
+    # map<i32, Item>, map<string, list<string>>, list<map<i32, string>>: one each
+    for t in ([[[1, T_MAP, T_I32, 0, 1, T_STRUCT]], [[1, T_I32, 0, 0, -1]]],
+              [[[1, T_MAP, T_STRING, 0, -1, T_LIST, [T_LIST, T_STRING, 0, -1]]]],
+              [[[1, T_LIST, T_MAP, 0, -1, 0, [T_MAP, T_I32, T_STRING, -1]]]]):
+        for protocol in (0, 2):
+            rc, log = compile_check(Schema.from_table(t), protocol)
+            assert rc == 0, log
     # list<Item> with an optional member in Item: none either
     opt = [[[1, T_LIST, T_STRUCT, 0, 1]], [[1, T_I32, 0, 1, -1]]]
     rc, _ = compile_check(Schema.from_table(opt), 0)
@@ -177,3 +189,70 @@ def torch_u8(v, dev):
     import torch
 
     return torch.tensor(v, dtype=torch.uint8, device=dev)
+
+
+# ---- maps, sets and string elements: the golden nested schemas with every
+# field unqualified (Item's optional double made unqualified), values from
+# the same generators, the oracle's stream as the reference ------------------
+def _unqualified_case(name, protocol, n):
+    import copy
+    import types
+
+    import nested_helpers as nh
+    import nestgen
+
+    table = copy.deepcopy(nh.manifest()["nested_schemas"][name])
+    for row in table[1]:
+        row[3] = 0
+    schema = Schema.from_table(table)
+    gen = nestgen.NESTED_GENERATORS[name]
+    values = [nestgen.to_json((T_STRUCT, 0), gen(i), table) for i in range(n)]
+    c = types.SimpleNamespace(n=n, values=values, schema=schema, protocol=protocol,
+                              layout=nh.Layout(schema, table))
+    return c, nh.pack(c)
+
+
+@pytest.mark.parametrize("name", ["structlist", "deepcont"])
+def test_unqualified_nested_schemas_compile(name):
+    c, _ = _unqualified_case(name, 0, 1)
+    for protocol in (0, 2):
+        rc, log = compile_check(c.schema, protocol)
+        assert rc == 0, log
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["structlist", "deepcont"])
+@pytest.mark.parametrize("protocol", [0, 2])
+def test_nested_program_maps_strings(gpu, name, protocol, monkeypatch):
+    """list / set / map of structs, map<string, list<string>>,
+    list<map<i32, string>>, map<i32, map<i32, Item>>, set<list<list<i64>>>,
+    strings and list<i16> inside Items: the nested program's encode gives the
+    oracle's bytes, its decode (indexed and unindexed) the oracle's records
+    and arena."""
+    import torch
+
+    from fbthrift_amd import serializer as SZ
+
+    monkeypatch.setenv("TGPU_JIT", "1")
+    monkeypatch.setenv("TGPU_NESTED", "1")
+    n = 3000
+    c, (rec, sb, lb) = _unqualified_case(name, protocol, n)
+    ost, owire, ooffs = oracle.encode(c.schema, protocol, rec, n, sb, lb)
+    assert ost.code == 0
+    gs = SZ.GpuSchema(c.schema)
+    assert gs.compile(protocol)
+    Ser = {0: SZ.BinarySerializer, 2: SZ.CompactSerializer}[protocol]
+    t = lambda a: torch.from_numpy(np.array(a, copy=True)).to(gpu)
+    wire, offs = Ser.serialize(gs, t(rec), n, t(sb), t(lb))
+    assert wire.cpu().numpy().tobytes() == owire
+    assert np.array_equal(offs.cpu().numpy().astype(np.uint64), ooffs)
+    S = c.layout.size[0]
+    w = np.frombuffer(owire, np.uint8)
+    for indexed in (True, False):
+        o = offs if indexed else None
+        grec, garena, st, nd, cons = Ser.deserialize_status(gs, t(w), n, o)
+        dst, drec, darena, dnd, dcons = oracle.decode(c.schema, protocol, owire, n,
+                                                      offsets=ooffs if indexed else None)
+        assert st.code == 0 and nd == n and cons == len(owire), st.as_tuple()
+        assert np.array_equal(grec.cpu().numpy()[: n * S], drec[: n * S])
+        assert np.array_equal(garena.cpu().numpy()[: darena.size], darena)
