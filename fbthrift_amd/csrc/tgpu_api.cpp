@@ -569,11 +569,36 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
   const tgpu_struct_desc& sd = sc.structs[si];
   if (sd.flags & TGPU_STRUCT_UNION) return false;
   int32_t prev = 0;
+  const uint32_t sbegin = P.n_ops;
+  if (nested && !push_op(P, make_op(VOP_SBEGIN))) return false;
   for (uint32_t k = 0; k < sd.num_fields; ++k) {
     const tgpu_field_desc& f = sc.fields[sd.first_field + k];
-    if (f.qualifier != TGPU_UNQUALIFIED && f.qualifier != TGPU_REQUIRED) return false;
+    const bool opt = nested && f.qualifier == TGPU_OPTIONAL;
+    if (f.qualifier != TGPU_UNQUALIFIED && f.qualifier != TGPU_REQUIRED && !opt) return false;
     const uint32_t member = base + f.member_offset, isset = base + f.isset_offset;
     if (member > 0xfffe || isset > 0xfffe) return false;
+    const uint32_t fhdr = P.n_ops;
+    if (nested) {
+      // the field header, computed at run time (VOP_FHDR)
+      VOp h = make_op(VOP_FHDR);
+      h.member = (uint16_t)f.id;
+      h.hdr = f.ttype | ((uint32_t)((uint16_t)f.id >> 8) << 8) |
+              ((uint32_t)((uint16_t)f.id & 0xff) << 16);
+      h.hdr_len = 3;
+      h.elem_ct = (uint8_t)(f.ttype == TGPU_T_BOOL ? 0 : compact_ctype(f.ttype));
+      h.is_bool = f.ttype == TGPU_T_BOOL;
+      h.width = opt ? 1 : 0;
+      h.isset = (uint16_t)isset;
+      if (!push_op(P, h)) return false;
+      if (proto != TGPU_PROTOCOL_BINARY && f.ttype == TGPU_T_BOOL) {
+        VOp cb = make_op(VOP_CBOOL);  // (its member / isset: the header carries the value)
+        cb.member = (uint16_t)member;
+        cb.isset = (uint16_t)isset;
+        if (!push_op(P, cb)) return false;
+        P.ops[fhdr].bits = 1;
+        continue;
+      }
+    }
     VOp hdr = make_op(VOP_CONST);
     if (proto == TGPU_PROTOCOL_BINARY) {
       hdr.hdr_len = 3;
@@ -606,7 +631,7 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
         continue;
       }
     }
-    if (!push_op(P, hdr)) return false;
+    if (!nested && !push_op(P, hdr)) return false;
     VOp v = make_op(VOP_FIXED);
     v.member = (uint16_t)member;
     v.isset = (uint16_t)isset;
@@ -653,10 +678,19 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
       stop.hdr_len = 1;
       VOp is = make_op(VOP_ISSET);
       is.isset = (uint16_t)isset;
-      if (!push_op(P, stop) || !push_op(P, is)) return false;
+      if ((!nested && !push_op(P, stop)) || !push_op(P, is)) return false;
     } else {
       return false;
     }
+    if (nested) {
+      const uint32_t nv = P.n_ops - fhdr - 1;  // the field's value ops
+      if (nv > 255) return false;
+      P.ops[fhdr].bits = (uint8_t)nv;
+    }
+  }
+  if (nested) {
+    if (!push_op(P, make_op(VOP_SEND))) return false;
+    P.ops[sbegin].hdr_len = (uint8_t)P.n_ops;  // one past its VOP_SEND
   }
   return true;
 }
@@ -686,10 +720,7 @@ bool emit_value(const tgpu_schema& sc, uint32_t t, int32_t si, uint32_t ti, uint
                 int proto, VProgram& P, uint32_t depth, uint32_t* max_depth) {
   if (t == TGPU_T_STRUCT) {
     if (si < 0 || (uint32_t)si >= sc.structs.size()) return false;
-    if (!emit_program(sc, (uint32_t)si, member, proto, P, true, depth, max_depth)) return false;
-    VOp stop = make_op(VOP_CONST);
-    stop.hdr_len = 1;
-    return push_op(P, stop);
+    return emit_program(sc, (uint32_t)si, member, proto, P, true, depth, max_depth);
   }
   if (t == TGPU_T_LIST || t == TGPU_T_SET || t == TGPU_T_MAP) {
     if (ti == 0 || ti > sc.types.size()) return false;
@@ -785,10 +816,7 @@ bool build_nested_program(const tgpu_schema& sc, int proto, VProgram& P, uint32_
   P.protocol = (uint32_t)proto;
   P.rec_size = sc.structs[0].size;
   depth = 0;
-  if (!emit_program(sc, 0, 0, proto, P, true, 0, &depth)) return false;
-  VOp stop = make_op(VOP_CONST);
-  stop.hdr_len = 1;
-  return push_op(P, stop);
+  return emit_program(sc, 0, 0, proto, P, true, 0, &depth);
 }
 
 bool build_program(const tgpu_schema& sc, int proto, VProgram& P, bool tolerant = false) {
@@ -1426,9 +1454,12 @@ int tgpu_schema_create_ex(const tgpu_struct_desc* structs, uint32_t n_structs,
     return TGPU_ERR_HIP;
   }
   for (int proto : {TGPU_PROTOCOL_BINARY, TGPU_PROTOCOL_COMPACT}) {
-    if (s->nested)
+    const bool flat = build_program(*s, proto, s->prog[proto]);
+    // the nested program: schemas with containers of structs / containers,
+    // and schemas with no canonical record program (optional fields)
+    if (s->nested || !flat)
       s->has_nprog[proto] = build_nested_program(*s, proto, s->nprog[proto], s->nprog_depth[proto]);
-    if (!build_program(*s, proto, s->prog[proto])) continue;
+    if (!flat) continue;
     build_program(*s, proto, s->prog_tol[proto], true);
     if (hipMalloc(&s->d_prog[proto], sizeof(VProgram)) != hipSuccess ||
         hipMemcpy(s->d_prog[proto], &s->prog[proto], sizeof(VProgram), hipMemcpyHostToDevice) !=
@@ -1521,8 +1552,9 @@ int tgpu_schema_compile_check_ex(const tgpu_struct_desc* structs, uint32_t n_str
   uint32_t depth = 0;
   // nested schemas: the nested program (JIT_NESTED); others: the canonical
   // record program's three groups
-  if (q < 0 || !(h.nested ? build_nested_program(h, q, P, depth) : build_program(h, q, P)))
-    return TGPU_ERR_UNSUPPORTED;
+  if (q < 0) return TGPU_ERR_UNSUPPORTED;
+  if (h.nested || !build_program(h, q, P))
+    if (!build_nested_program(h, q, P, depth)) return TGPU_ERR_UNSUPPORTED;
   return jit_compile_check(P, arch, log, log_capacity);
 }
 

@@ -172,6 +172,15 @@ enum VOpKind : uint8_t {
   // pairs from the region, the body (key op at 0, the value's ops at bits)
   // once per pair, ended by VOP_SEQ_END like VOP_SEQ
   VOP_MSEQ = 10,
+  // nested programs: a field header (member: the field id; hdr: its Binary
+  // header; elem_ct: its Compact ctype; is_bool: a bool field; width 1: an
+  // optional field, present when its header is next; isset: its isset
+  // byte; bits: the value ops that follow). Compact headers are deltas from
+  // the struct's last field (VOP_SBEGIN's scope), so they are computed, not
+  // constant, once fields may be absent.
+  VOP_FHDR = 11,
+  VOP_SBEGIN = 12,  // a struct's fields begin (hdr_len: one past its VOP_SEND)
+  VOP_SEND = 13,    // its STOP
 };
 enum VElemKind : uint8_t {
   VEL_FIXED = 1,   // big-endian fixed width (Binary ints, doubles/floats, bytes)

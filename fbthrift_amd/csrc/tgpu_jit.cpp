@@ -79,73 +79,123 @@ const char* const kEntry[4][5] = {
      "tgpu_jit_index_onepass", "tgpu_jit_index_onepass_decode"},
     {"tgpu_jit_ndecode", "tgpu_jit_ndecode_hbm", "tgpu_jit_nsize", "tgpu_jit_nwrite", nullptr}};
 
-// The record writer of a nested program: ops [k, stop) of the object at `b`;
-// each VOP_SEQ writes its header and loops over the element slots of its
-// span in the list base.
-void gen_enc_ops(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t stop,
-                 const std::string& b, int indent) {
-  const std::string in(indent, ' ');
+// The record function of a nested program (decode when !enc, the writer
+// when enc): ops [k, stop) of the object at `b` (a variable name). Each
+// VOP_SBEGIN opens a struct's scope with its Compact delta base `l<k>` (the
+// last field id read / written), VOP_FHDR is a field header — read or
+// written from the base, in a branch on presence for an optional field
+// (its value ops, the next `bits` ops, inside) — VOP_SEND the struct's STOP;
+// each VOP_SEQ / VOP_MSEQ a counted loop over its element slots. Leaf ops
+// are the program's op helpers on the constant op.
+void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t stop,
+              const std::string& b, int indent, bool enc, std::string last) {
+  const bool compact = P.protocol != TGPU_PROTOCOL_BINARY;
   while (k < stop) {
+    const std::string in(indent, ' ');
     const VOp& v = P.ops[k];
-    if (v.kind == VOP_SEQ || v.kind == VOP_MSEQ) {
-      const std::string sp = "s" + std::to_string(k), a = "a" + std::to_string(k),
-                        i = "i" + std::to_string(k), e = "e" + std::to_string(k);
-      o << in << "{\n"
-        << in << "  const tgpu_span " << sp << " = seq_span(kOps[" << k << "], " << b << ");\n"
-        << in << "  if (!" << (v.kind == VOP_SEQ ? "put_list_header" : "put_map_header") << "(o, kOps["
-        << k << "], kCompact, " << sp << ".length)) return false;\n"
-        << in << "  const uint8_t* " << a << " = lbase + " << sp << ".offset;\n"
-        << in << "  for (uint32_t " << i << " = 0; " << i << " < " << sp << ".length; ++" << i
-        << ") {\n"
-        << in << "    const uint8_t* " << e << " = " << a << " + (uint64_t)" << i << " * " << v.hdr
-        << "u;\n";
-      gen_enc_ops(o, P, k + 1, v.hdr_len - 1, e, indent + 4);
-      o << in << "  }\n" << in << "}\n";
+    const std::string K = std::to_string(k), op = "kOps[" + K + "]";
+    if (v.kind == VOP_SBEGIN) {
+      // the struct's fields up to its VOP_SEND (hdr_len: one past it)
+      o << in << "{\n" << in << "  int32_t l" << K << " = 0;\n";
+      if (compact) o << in << "  (void)l" << K << ";\n";
+      gen_code(o, P, k + 1, v.hdr_len - 1, b, indent + 2, enc, "l" + K);
+      if (enc) o << in << "  o.put(0, 1);\n";  // writeFieldStop
+      else o << in << "  if (!struct_stop(src, p, end)) return false;\n";
+      o << in << "}\n";
       k = v.hdr_len;
       continue;
     }
-    if (v.kind != VOP_SEQ_END && v.kind != VOP_ISSET)
-      o << in << "if (!enc_op(kOps[" << k << "], kCompact, " << b << ", sbase, lbase, o)) return false;\n";
-    ++k;
-  }
-}
-
-// The record function of a nested program: ops [k, stop) at object base `b`
-// (a variable name), each VOP_SEQ a counted loop over its element slots with
-// the body at the slot. Leaf ops are run_op / nlist calls on the constant op.
-void gen_ops(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t stop,
-             const std::string& b, int indent) {
-  const std::string in(indent, ' ');
-  while (k < stop) {
-    const VOp& v = P.ops[k];
+    if (v.kind == VOP_FHDR) {
+      const uint32_t vend = k + 1 + v.bits;  // the field's value ops
+      const bool opt = v.width != 0;
+      const int32_t id = (int16_t)v.member;
+      const bool cbool = compact && v.is_bool;  // the value rides in the header
+      std::string hdr;
+      if (enc) {
+        if (cbool) {
+          const VOp& cv = P.ops[k + 1];
+          hdr = "put_cbool_field(o, " + std::to_string(id) + ", " + last + ", " + b + "[" +
+                std::to_string(cv.member) + "])";
+        } else if (compact) {
+          hdr = "(put_cfield(o, " + std::to_string(id) + ", " + std::to_string(v.elem_ct) + "u, " +
+                last + "), true)";
+        } else {
+          hdr = "(o.put(" + std::to_string(v.hdr) + "u, 3), true)";
+        }
+        if (opt) o << in << "if (" << b << "[" << v.isset << "]) {\n";
+        else o << in << "{\n";
+        o << in << "  if (!" << hdr << ") return false;\n";
+        if (!cbool) gen_code(o, P, k + 1, vend, b, indent + 2, enc, last);
+        o << in << "}\n";
+      } else {
+        if (cbool) {
+          const VOp& cv = P.ops[k + 1];
+          hdr = "cbool_field(src, p, end, " + std::to_string(id) + ", " + last + ", " + b + " + " +
+                std::to_string(cv.member) + "u, " + b + " + " + std::to_string(cv.isset) + "u)";
+        } else if (compact) {
+          hdr = "cfield(src, p, end, " + std::to_string(id) + ", " + std::to_string(v.elem_ct) + "u, " +
+                last + ")";
+        } else {
+          hdr = "bfield(src, p, end, " + std::to_string(v.hdr) + "u)";
+        }
+        if (opt) {
+          o << in << "if (" << hdr << ") {\n";
+        } else {
+          o << in << "if (!" << hdr << ") return false;\n" << in << "{\n";
+        }
+        if (!cbool) gen_code(o, P, k + 1, vend, b, indent + 2, enc, last);
+        o << in << "}\n";
+      }
+      k = vend;
+      continue;
+    }
     if (v.kind == VOP_SEQ || v.kind == VOP_MSEQ) {
-      const std::string n = "n" + std::to_string(k), a = "a" + std::to_string(k),
-                        i = "i" + std::to_string(k), e = "e" + std::to_string(k);
-      o << in << "{\n"
-        << in << "  uint32_t " << n << ";\n"
-        << in << "  uint8_t* " << a << ";\n"
-        << in << "  if (!" << (v.kind == VOP_SEQ ? "seq_open" : "mseq_open") << "(kOps[" << k
-        << "], kCompact, src, c, p, end, " << b << ", bump, " << n << ", " << a
-        << ")) return false;\n"
-        << in << "  for (uint32_t " << i << " = 0; " << i << " < " << n << "; ++" << i << ") {\n"
-        << in << "    uint8_t* " << e << " = " << a << " + (uint64_t)" << i << " * " << v.hdr
-        << "u;\n";
-      // (a struct element / value is default-constructed first; every other
-      // slot is written whole)
-      if (v.elem_ttype == TGPU_T_STRUCT) o << in << "    zero_slot<" << v.hdr << "u>(" << e << ");\n";
-      gen_ops(o, P, k + 1, v.hdr_len - 1, e, indent + 4);
-      o << in << "  }\n"
-        << in << "  seq_close(kOps[" << k << "], " << b << ");\n"
-        << in << "}\n";
+      const std::string n = "n" + K, a = "a" + K, i = "i" + K, e = "e" + K;
+      const bool seq = v.kind == VOP_SEQ;
+      o << in << "{\n";
+      if (enc) {
+        o << in << "  const tgpu_span s" << K << " = seq_span(" << op << ", " << b << ");\n"
+          << in << "  if (!" << (seq ? "put_list_header" : "put_map_header") << "(o, " << op
+          << ", kCompact, s" << K << ".length)) return false;\n"
+          << in << "  const uint32_t " << n << " = s" << K << ".length;\n"
+          << in << "  const uint8_t* " << a << " = lbase + s" << K << ".offset;\n"
+          << in << "  for (uint32_t " << i << " = 0; " << i << " < " << n << "; ++" << i << ") {\n"
+          << in << "    const uint8_t* " << e << " = " << a << " + (uint64_t)" << i << " * " << v.hdr
+          << "u;\n";
+      } else {
+        o << in << "  uint32_t " << n << ";\n"
+          << in << "  uint8_t* " << a << ";\n"
+          << in << "  if (!" << (seq ? "seq_open" : "mseq_open") << "(" << op
+          << ", kCompact, src, c, p, end, " << b << ", bump, " << n << ", " << a
+          << ")) return false;\n"
+          << in << "  for (uint32_t " << i << " = 0; " << i << " < " << n << "; ++" << i << ") {\n"
+          << in << "    uint8_t* " << e << " = " << a << " + (uint64_t)" << i << " * " << v.hdr
+          << "u;\n";
+        // (a struct element / value is default-constructed first; every
+        // other slot is written whole)
+        if (v.elem_ttype == TGPU_T_STRUCT)
+          o << in << "    zero_slot<" << v.hdr << "u>(" << e << ");\n";
+      }
+      gen_code(o, P, k + 1, v.hdr_len - 1, e, indent + 4, enc, last);
+      o << in << "  }\n";
+      if (!enc) o << in << "  seq_close(" << op << ", " << b << ");\n";
+      o << in << "}\n";
       k = v.hdr_len;  // past the VOP_SEQ_END
       continue;
     }
-    if (v.kind == VOP_LIST)
-      o << in << "if (!nlist(kOps[" << k << "], kCompact, src, c, p, end, " << b
-        << ", bump)) return false;\n";
-    else if (v.kind != VOP_SEQ_END)
-      o << in << "if (!run_op<true>(kOps[" << k << "], kCompact, src, c, p, end, " << b
+    if (v.kind == VOP_SEQ_END || v.kind == VOP_SEND) {
+      ++k;
+      continue;
+    }
+    if (enc) {
+      if (v.kind != VOP_ISSET)
+        o << in << "if (!enc_op(" << op << ", kCompact, " << b << ", sbase, lbase, o)) return false;\n";
+    } else if (v.kind == VOP_LIST) {
+      o << in << "if (!nlist(" << op << ", kCompact, src, c, p, end, " << b << ", bump)) return false;\n";
+    } else {
+      o << in << "if (!run_op<true>(" << op << ", kCompact, src, c, p, end, " << b
         << ", W)) return false;\n";
+    }
     ++k;
   }
 }
@@ -207,7 +257,7 @@ std::string gen_source(const VProgram& P, int group) {
          "__device__ __forceinline__ bool nrec(const Src& src, const Ctx& c, uint32_t& p, "
          "const uint32_t end, uint8_t* rec, uint64_t& bump) {\n"
          "  Win W;\n";
-    gen_ops(o, P, 0, P.n_ops, "rec", 2);
+    gen_code(o, P, 0, P.n_ops, "rec", 2, false, "");
     o << "  return true;\n"
          "}\n"
          "struct NR {\n"
@@ -221,17 +271,17 @@ std::string gen_source(const VProgram& P, int group) {
          "extern \"C\" __global__ __launch_bounds__(256) void tgpu_jit_ndecode(DecodeArgs a, "
          "uint32_t wire_cap, uint64_t* __restrict__ irr, unsigned long long* __restrict__ nirr) {\n"
          "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
-         "  nested_decode_tile(a, NR{}, kS, wire_cap, irr, nirr, smem);\n"
+         "  nested_decode_tile(a, NR{}, kS, kCompact, wire_cap, irr, nirr, smem);\n"
          "}\n"
          "extern \"C\" __global__ __launch_bounds__(256) void tgpu_jit_ndecode_hbm(DecodeArgs a, "
          "uint32_t wire_cap, uint64_t* __restrict__ irr, unsigned long long* __restrict__ nirr) {\n"
-         "  nested_decode_hbm(a, NR{}, kS, irr, nirr);\n"
+         "  nested_decode_hbm(a, NR{}, kS, kCompact, irr, nirr);\n"
          "}\n"
          "namespace {\n"
          "template <class O>\n"
          "__device__ __forceinline__ bool nenc(const uint8_t* rec, const uint8_t* sbase, "
          "const uint8_t* lbase, O& o) {\n";
-    gen_enc_ops(o, P, 0, P.n_ops, "rec", 2);
+    gen_code(o, P, 0, P.n_ops, "rec", 2, true, "");
     o << "  return true;\n"
          "}\n"
          "struct NE {\n"
@@ -435,7 +485,7 @@ int jit_compile_check(const VProgram& P, const char* arch, char* log, uint64_t l
   bool ok = true;
   bool nested = false;
   for (uint32_t k = 0; k < P.n_ops; ++k)
-    nested |= P.ops[k].kind == VOP_SEQ || P.ops[k].kind == VOP_MSEQ || P.ops[k].kind == VOP_SEQ_END;
+    nested |= P.ops[k].kind >= VOP_SEQ;
   for (int group = nested ? JIT_NESTED : 0; group < (nested ? JIT_NESTED + 1 : JIT_NESTED) && ok;
        ++group) {
     std::vector<char> code;

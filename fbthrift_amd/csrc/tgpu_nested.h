@@ -59,6 +59,74 @@ __device__ __forceinline__ bool seq_header(const VOp op, const bool compact, con
   return n >= 0 && !(c.container_limit && n > c.container_limit) && n <= (int64_t)(end - p);
 }
 
+// ---- field headers of the nested programs -----------------------------------
+// Binary: type byte + BE i16 id (BinaryProtocol-inl.h:53-59).
+template <class Src>
+__device__ __forceinline__ bool bfield(const Src& src, uint32_t& p, const uint32_t end,
+                                       uint32_t hdr) {
+  if (p + 3 > end || (src.win8(p) & 0xffffff) != hdr) return false;
+  p += 3;
+  return true;
+}
+
+// Compact (CompactProtocol-inl.h:133-160): the header the writer emits for
+// field `id` after field `last`: one byte (delta << 4 | ctype) when
+// 0 < delta <= 15, else ctype + zigzag varint id. ct 0: a bool field, the
+// byte's ctype 1 / 2 is its value (*val). On a match the header is
+// consumed and last = id.
+__device__ __forceinline__ void chdr_bytes(int32_t id, uint32_t ct, int32_t last, uint64_t& hb,
+                                           uint32_t& len) {
+  const int32_t d = id - last;
+  if (d > 0 && d <= 15) {
+    hb = ((uint32_t)d << 4) | ct;
+    len = 1;
+    return;
+  }
+  uint32_t zz = ((uint32_t)id << 1) ^ (uint32_t)(id >> 31);
+  hb = ct;
+  len = 1;
+  do {
+    hb |= (uint64_t)((zz & 0x7f) | (zz > 0x7f ? 0x80 : 0)) << (8 * len++);
+    zz >>= 7;
+  } while (zz);
+}
+template <class Src>
+__device__ __forceinline__ bool cfield(const Src& src, uint32_t& p, const uint32_t end, int32_t id,
+                                       uint32_t ct, int32_t& last) {
+  uint64_t hb;
+  uint32_t len;
+  chdr_bytes(id, ct, last, hb, len);
+  const uint64_t m = (1ull << (8 * len)) - 1;
+  if (p + len > end || (src.win8(p) & m) != hb) return false;
+  p += len;
+  last = id;
+  return true;
+}
+template <class Src>
+__device__ __forceinline__ bool cbool_field(const Src& src, uint32_t& p, const uint32_t end,
+                                            int32_t id, int32_t& last, uint8_t* member,
+                                            uint8_t* isset) {
+  uint64_t hb;
+  uint32_t len;
+  chdr_bytes(id, 0, last, hb, len);
+  const uint64_t m = (1ull << (8 * len)) - 1;
+  if (p + len > end) return false;
+  const uint64_t w = src.win8(p) & m;
+  const uint32_t ct = (uint32_t)(w & 0xf);
+  if ((w & ~0xfull) != hb || (ct != 1 && ct != 2)) return false;
+  *member = ct == 1 ? 1 : 0;
+  *isset = 1;
+  p += len;
+  last = id;
+  return true;
+}
+template <class Src>
+__device__ __forceinline__ bool struct_stop(const Src& src, uint32_t& p, const uint32_t end) {
+  if (p + 1 > end || (src.win8(p) & 0xff) != 0) return false;
+  ++p;
+  return true;
+}
+
 // VOP_SEQ: the container's element array (n x op.hdr bytes) from the region
 // and its span at base + member; the caller loops over the elements.
 template <class Src>
@@ -76,7 +144,7 @@ __device__ __forceinline__ bool seq_open(const VOp op, const bool compact, const
     return true;
   }
   const uint64_t bytes = (uint64_t)n * op.hdr;
-  if (!c.arena) return false;
+  if (!c.arena || c.pos_scale) return false;
   const uint64_t aoff = region_alloc(bump, bytes);
   if (aoff + bytes > c.arena_cap) return false;
   arr = c.arena + aoff;
@@ -123,7 +191,7 @@ __device__ __forceinline__ bool mseq_open(const VOp op, const bool compact, cons
     return true;
   }
   const uint64_t bytes = (uint64_t)n * op.hdr;
-  if (!c.arena) return false;
+  if (!c.arena || c.pos_scale) return false;
   const uint64_t aoff = region_alloc(bump, bytes);
   if (aoff + bytes > c.arena_cap) return false;
   arr = c.arena + aoff;
@@ -159,7 +227,8 @@ __device__ __forceinline__ bool nlist(const VOp op, const bool compact, const Sr
   uint64_t aoff = 0;
   if (n) {
     if (!c.arena) return false;
-    aoff = region_alloc(bump, (uint64_t)n * es);
+    // the record's region, or the position rule (schemas without regions)
+    aoff = c.pos_scale ? c.pos_scale * (c.gbase + p) : region_alloc(bump, (uint64_t)n * es);
     if (aoff + (uint64_t)n * es > c.arena_cap) return false;
   }
   uint8_t* dst = c.arena + aoff;
@@ -209,8 +278,15 @@ __device__ __forceinline__ bool nlist(const VOp op, const bool compact, const Sr
 //   bool R(const LdsSrc&, const Ctx&, uint32_t& p, uint32_t end, uint8_t* rec,
 //          uint64_t& bump)
 // with its region start in `bump`. Element arrays go straight to the arena.
+// tgpu_schema_arena_scale of a schema without record regions (0: regions)
+__device__ __forceinline__ uint64_t pos_scale(const DevSchema& sc, bool compact) {
+  if (sc.bump_scale) return 0;
+  return sc.str_elems ? (compact ? 16 : 4) : (compact ? 8 : 1);
+}
+
 template <class R>
 __device__ __forceinline__ void nested_decode_tile(const DecodeArgs& a, const R& run, uint32_t S,
+                                                   bool compact,
                                                    uint32_t wire_cap, uint64_t* __restrict__ irr,
                                                    unsigned long long* __restrict__ nirr,
                                                    uint8_t* smem) {
@@ -254,7 +330,8 @@ __device__ __forceinline__ void nested_decode_tile(const DecodeArgs& a, const R&
       const uint64_t s = a.offs[r0 + r], e = a.offs[r0 + r + 1];
       ok = s >= t0 && e >= s && e <= t1;
       if (ok) {
-        const Ctx c{t0 - sh, a.arena, a.arena_cap, a.string_limit, a.container_limit, nullptr};
+        const Ctx c{t0 - sh, a.arena, a.arena_cap, a.string_limit, a.container_limit, nullptr,
+                    pos_scale(a.sc, compact)};
         const LdsSrc src{(const uint32_t*)wire};
         uint32_t p = (uint32_t)(s - t0) + sh;
         const uint32_t pe = (uint32_t)(e - t0) + sh;
@@ -283,6 +360,7 @@ __device__ __forceinline__ void nested_decode_tile(const DecodeArgs& a, const R&
 // record in place — no LDS, so occupancy is set by registers alone.
 template <class R>
 __device__ __forceinline__ void nested_decode_hbm(const DecodeArgs& a, const R& run, uint32_t S,
+                                                  bool compact,
                                                   uint64_t* __restrict__ irr,
                                                   unsigned long long* __restrict__ nirr) {
   const uint64_t i = (uint64_t)blockIdx.x * kPT + threadIdx.x;
@@ -297,7 +375,8 @@ __device__ __forceinline__ void nested_decode_hbm(const DecodeArgs& a, const R& 
   const uint64_t s = a.offs[i], e = a.offs[i + 1];
   bool ok = e >= s && e <= a.in_len && e - s < (1ull << 31);
   if (ok) {
-    const Ctx c{s, a.arena, a.arena_cap, a.string_limit, a.container_limit, nullptr};
+    const Ctx c{s, a.arena, a.arena_cap, a.string_limit, a.container_limit, nullptr,
+                pos_scale(a.sc, compact)};
     const HbmSrc src{a.in + s, (uint32_t)min(a.in_len - s, (uint64_t)0xffffffffu)};
     uint32_t p = 0;
     const uint32_t pe = (uint32_t)(e - s);
@@ -529,6 +608,23 @@ __device__ __forceinline__ bool enc_op(const VOp op, const bool compact, const u
     default:
       return true;  // VOP_ISSET, VOP_SEQ_END: no bytes
   }
+}
+
+// Field headers on encode: Compact delta / long form from the struct's last
+// field; a bool's value in the header (validate_bool).
+template <class O>
+__device__ __forceinline__ void put_cfield(O& o, int32_t id, uint32_t ct, int32_t& last) {
+  uint64_t hb;
+  uint32_t len;
+  chdr_bytes(id, ct, last, hb, len);
+  o.put(hb, len);
+  last = id;
+}
+template <class O>
+__device__ __forceinline__ bool put_cbool_field(O& o, int32_t id, int32_t& last, uint32_t v) {
+  if (v > 1) return false;
+  put_cfield(o, id, v ? 1u : 2u, last);
+  return true;
 }
 
 // VOP_SEQ: the header; the caller loops over the elements of the span

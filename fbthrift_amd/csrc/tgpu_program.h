@@ -220,6 +220,9 @@ struct Ctx {
   // wire tile (an element's arena slot is its own wire bytes, scale 1) and
   // the tile is copied to the arena with coalesced stores afterwards
   uint8_t* lds_wire;
+  // nested programs of schemas without record regions: the position rule's
+  // scale (an element array at scale x its first element's stream offset)
+  uint64_t pos_scale = 0;
 };
 
 // At the root STOP (kStopSkipsUnknown) a field header instead of STOP: up to

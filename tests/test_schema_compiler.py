@@ -1,7 +1,8 @@
 """The schema compiler (tgpu_jit.cpp) on a GPU-less host: the kernels it
 generates for a schema compile for gfx950 with hipRTC (all three kernel
-groups: decode, encode, index); schemas without a canonical record program
-(optional fields) are refused — they run on the general reader. GPU parity of
+groups: decode, encode, index); schemas without one (optional fields,
+containers of structs) compile a nested record program instead; unions and
+the like are refused — they run on the general reader. GPU parity of
 the compiled kernels is in test_gpu_parity.py (TGPU_JIT=1 runs). Compiles
 cost seconds each, so the CPU suite covers the three BASELINE config schemas
 in their benchmarked protocol plus the bool/long-form-id heavy 'scalars'."""
@@ -21,6 +22,13 @@ def test_schema_kernels_compile(name, protocol):
     assert rc == 0, log
 
 
-def test_optional_fields_have_no_program():
-    rc, _ = compile_check(Schema.from_table(M["sparse"]), 2)
-    assert rc == 22  # TGPU_ERR_UNSUPPORTED: no canonical program, general reader path
+def test_optional_fields_compile_nested_program():
+    # optional fields: no canonical record program, but a nested record
+    # program (field headers checked at run time, tgpu_nested.h)
+    rc, log = compile_check(Schema.from_table(M["sparse"]), 2)
+    assert rc == 0, log
+
+
+def test_unions_have_no_program():
+    rc, _ = compile_check(Schema.from_table(M["unions"]), 2)
+    assert rc == 22  # TGPU_ERR_UNSUPPORTED: the general reader path
