@@ -49,6 +49,7 @@ struct tgpu_schema {
   // = the deepest container nesting (the height it needs)
   bool has_nprog[3] = {false, false, false};
   VProgram nprog[3]{};
+  VProgram* d_nprog[3] = {nullptr, nullptr, nullptr};  // (the index's AOT repair kernels read it)
   uint32_t nprog_depth[3] = {0, 0, 0};
   // the wire bytes per record (x16) of the last batch whose size this schema
   // learned (blocking encode / size calls), by protocol id: sizes the
@@ -1104,15 +1105,40 @@ uint32_t prog_min_len(const VProgram& P) {
   for (uint32_t k = 0; k < P.n_ops; ++k) {
     const VOp& o = P.ops[k];
     switch (o.kind) {
-      case VOP_CONST: case VOP_CBOOL: n += o.hdr_len; break;
+      case VOP_CONST: n += o.hdr_len; break;
+      case VOP_CBOOL: n += compact && o.hdr_len == 0 ? 0 : o.hdr_len; break;
       case VOP_FIXED: n += o.width; break;
       case VOP_VARINT: n += 1; break;
       case VOP_STRING: n += compact ? 1 : 4; break;
       case VOP_LIST: n += compact ? 1 : 5; break;
+      // nested programs: a header of each present field (an optional one
+      // may be absent: its value ops skipped), containers empty, STOPs
+      case VOP_FHDR:
+        if (o.width) k += o.bits;
+        else n += compact ? 1 : 3;
+        break;
+      case VOP_SEQ: case VOP_MSEQ:
+        n += compact ? 1 : (o.kind == VOP_SEQ ? 5 : 6);
+        k = o.hdr_len - 1u;
+        break;
+      case VOP_SEND: n += 1; break;
       default: break;
     }
   }
   return n;
+}
+
+// The nested program's index kernels (JIT_NINDEX) for an unindexed stream
+// of `bytes` (nullptr: none — the general reader measures the records).
+const JitKernels* nested_index_jit(const tgpu_schema* schema, int protocol, uint64_t bytes,
+                                   int32_t height, int32_t max_depth) {
+  const char* v = getenv("TGPU_NESTED");
+  if (v && v[0] == '0') return nullptr;
+  const int q = prog_protocol(schema, protocol);
+  if (q < 0 || !schema->has_nprog[q] || !schema->d_nprog[q] || !bytes) return nullptr;
+  const int32_t need = (int32_t)schema->nprog_depth[q] + 1;
+  if (height < need || max_depth < need) return nullptr;
+  return jit_kernels(schema->nprog[q], schema->device, JIT_NINDEX, 0, bytes, false);
 }
 
 // TGPU_INDEX_STARTS=0: the emit pass re-walks every tile instead of copying
@@ -1154,6 +1180,15 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   const int pq = prog_protocol(schema, protocol);
   x.prog = has_prog(schema, protocol) && height >= 2 && x.max_depth >= 2
                ? (tolerant ? schema->d_prog_tol[pq] : schema->d_prog[pq]) : nullptr;
+  // no record program: the nested program's measuring walk when compiled
+  // (index only — the nested decode runs after it, never a fused decode)
+  const JitKernels* njit =
+      x.prog ? nullptr : nested_index_jit(schema, protocol, end > begin ? end - begin : 0, height,
+                                          x.max_depth);
+  if (njit) {
+    x.prog = schema->d_nprog[pq];
+    dec = nullptr;
+  }
   x.chunk = index_chunk_bytes(end > begin ? end - begin : 0, x.prog != nullptr);
   x.window = (uint32_t)std::min<uint64_t>(x.chunk, 1024);
   x.n_chunks = end > begin ? (end - begin + x.chunk - 1) / x.chunk : 0;
@@ -1177,8 +1212,9 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   const uint64_t lane_words = x.chunk == index_tile_bytes() ? C * index_tile_lanes() : 0;
   // stored starts: a tile holds at most chunk / min_len + 1 record starts
   const bool starts = lane_words && x.prog && index_starts_enabled();
-  x.st_cap = starts ? (uint32_t)std::min<uint64_t>(
-                          x.chunk / std::max<uint32_t>(prog_min_len(schema->prog[pq]), 1) + 2, 2048)
+  const uint32_t min_len = prog_min_len(njit ? schema->nprog[pq] : schema->prog[pq]);
+  x.st_cap = starts ? (uint32_t)std::min<uint64_t>(x.chunk / std::max<uint32_t>(min_len, 1) + 2,
+                                                   2048)
                     : 0;
   const uint64_t st_bytes = (2 * (uint64_t)x.st_cap * C + 15) & ~15ull;
   const uint64_t need =
@@ -1215,11 +1251,13 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
     return TGPU_OK;
   }
   const JitKernels* jit =
-      !x.prog ? nullptr
+      njit ? njit
+      : !x.prog ? nullptr
       : tolerant ? jit_kernels(schema->prog_tol[pq], schema->device, JIT_INDEX, 0, end - begin,
                                false)
                  : schema_jit(schema, protocol, JIT_INDEX, 0, end - begin);
-  if (e == hipSuccess && may_sync && x.prog && x.chunk == index_tile_bytes() && onepass_enabled()) {
+  if (e == hipSuccess && may_sync && x.prog && !njit && x.chunk == index_tile_bytes() &&
+      onepass_enabled()) {
     // single pass with look-back; a range it cannot finish alone (a record
     // off the program, a record longer than a tile, ...) goes to the two-pass
     // index below, which redoes it whole
@@ -1459,6 +1497,13 @@ int tgpu_schema_create_ex(const tgpu_struct_desc* structs, uint32_t n_structs,
     // and schemas with no canonical record program (optional fields)
     if (s->nested || !flat)
       s->has_nprog[proto] = build_nested_program(*s, proto, s->nprog[proto], s->nprog_depth[proto]);
+    if (s->has_nprog[proto] &&
+        (hipMalloc(&s->d_nprog[proto], sizeof(VProgram)) != hipSuccess ||
+         hipMemcpy(s->d_nprog[proto], &s->nprog[proto], sizeof(VProgram), hipMemcpyHostToDevice) !=
+             hipSuccess)) {
+      tgpu_schema_destroy(s);
+      return TGPU_ERR_HIP;
+    }
     if (!flat) continue;
     build_program(*s, proto, s->prog_tol[proto], true);
     if (hipMalloc(&s->d_prog[proto], sizeof(VProgram)) != hipSuccess ||
@@ -1508,6 +1553,8 @@ void tgpu_schema_destroy(tgpu_schema* s) {
   for (VProgram* p : s->d_prog)
     if (p) (void)hipFree(p);
   for (VProgram* p : s->d_prog_tol)
+    if (p) (void)hipFree(p);
+  for (VProgram* p : s->d_nprog)
     if (p) (void)hipFree(p);
   delete s;
 }

@@ -415,7 +415,9 @@ hipError_t launch_general_decode(const DecodeArgs& a, int protocol,
 struct JitKernels;
 // JIT_NESTED: the indexed decode of a nested program (VOP_SEQ), generated as
 // straight-line code with one loop per container level.
-enum JitGroup { JIT_DECODE = 0, JIT_ENCODE = 1, JIT_INDEX = 2, JIT_NESTED = 3 };
+// JIT_NINDEX: the stream index's speculation / emit kernels over a nested
+// program's measuring walk.
+enum JitGroup { JIT_DECODE = 0, JIT_ENCODE = 1, JIT_INDEX = 2, JIT_NESTED = 3, JIT_NINDEX = 4 };
 const JitKernels* jit_kernels(const VProgram& prog, int device, int group, uint64_t records,
                               uint64_t bytes, bool force);
 int jit_compile_check(const VProgram& P, const char* arch, char* log, uint64_t log_cap);

@@ -72,12 +72,13 @@ std::string cache_key(const VProgram& P, int device, int group) {
   return k;
 }
 
-const char* const kEntry[4][5] = {
+const char* const kEntry[5][5] = {
     {"tgpu_jit_decode", nullptr, nullptr, nullptr, nullptr},
     {"tgpu_jit_size", "tgpu_jit_write", nullptr, nullptr, nullptr},
     {"tgpu_jit_index_spec", "tgpu_jit_index_emit", "tgpu_jit_index_decode",
      "tgpu_jit_index_onepass", "tgpu_jit_index_onepass_decode"},
-    {"tgpu_jit_ndecode", "tgpu_jit_ndecode_hbm", "tgpu_jit_nsize", "tgpu_jit_nwrite", nullptr}};
+    {"tgpu_jit_ndecode", "tgpu_jit_ndecode_hbm", "tgpu_jit_nsize", "tgpu_jit_nwrite", nullptr},
+    {"tgpu_jit_nindex_spec", "tgpu_jit_nindex_emit", nullptr, nullptr, nullptr}};
 
 // The record function of a nested program (decode when !enc, the writer
 // when enc): ops [k, stop) of the object at `b` (a variable name). Each
@@ -87,9 +88,11 @@ const char* const kEntry[4][5] = {
 // (its value ops, the next `bits` ops, inside) — VOP_SEND the struct's STOP;
 // each VOP_SEQ / VOP_MSEQ a counted loop over its element slots. Leaf ops
 // are the program's op helpers on the constant op.
+// meas: the measuring walk of the stream index (decode form, nothing stored).
 void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t stop,
-              const std::string& b, int indent, bool enc, std::string last) {
+              const std::string& b, int indent, bool enc, std::string last, bool meas = false) {
   const bool compact = P.protocol != TGPU_PROTOCOL_BINARY;
+  const std::string ks = meas ? "<false>" : "";
   while (k < stop) {
     const std::string in(indent, ' ');
     const VOp& v = P.ops[k];
@@ -98,7 +101,7 @@ void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t sto
       // the struct's fields up to its VOP_SEND (hdr_len: one past it)
       o << in << "{\n" << in << "  int32_t l" << K << " = 0;\n";
       if (compact) o << in << "  (void)l" << K << ";\n";
-      gen_code(o, P, k + 1, v.hdr_len - 1, b, indent + 2, enc, "l" + K);
+      gen_code(o, P, k + 1, v.hdr_len - 1, b, indent + 2, enc, "l" + K, meas);
       if (enc) o << in << "  o.put(0, 1);\n";  // writeFieldStop
       else o << in << "  if (!struct_stop(src, p, end)) return false;\n";
       o << in << "}\n";
@@ -125,12 +128,12 @@ void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t sto
         if (opt) o << in << "if (" << b << "[" << v.isset << "]) {\n";
         else o << in << "{\n";
         o << in << "  if (!" << hdr << ") return false;\n";
-        if (!cbool) gen_code(o, P, k + 1, vend, b, indent + 2, enc, last);
+        if (!cbool) gen_code(o, P, k + 1, vend, b, indent + 2, enc, last, meas);
         o << in << "}\n";
       } else {
         if (cbool) {
           const VOp& cv = P.ops[k + 1];
-          hdr = "cbool_field(src, p, end, " + std::to_string(id) + ", " + last + ", " + b + " + " +
+          hdr = "cbool_field" + ks + "(src, p, end, " + std::to_string(id) + ", " + last + ", " + b + " + " +
                 std::to_string(cv.member) + "u, " + b + " + " + std::to_string(cv.isset) + "u)";
         } else if (compact) {
           hdr = "cfield(src, p, end, " + std::to_string(id) + ", " + std::to_string(v.elem_ct) + "u, " +
@@ -143,7 +146,7 @@ void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t sto
         } else {
           o << in << "if (!" << hdr << ") return false;\n" << in << "{\n";
         }
-        if (!cbool) gen_code(o, P, k + 1, vend, b, indent + 2, enc, last);
+        if (!cbool) gen_code(o, P, k + 1, vend, b, indent + 2, enc, last, meas);
         o << in << "}\n";
       }
       k = vend;
@@ -165,7 +168,7 @@ void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t sto
       } else {
         o << in << "  uint32_t " << n << ";\n"
           << in << "  uint8_t* " << a << ";\n"
-          << in << "  if (!" << (seq ? "seq_open" : "mseq_open") << "(" << op
+          << in << "  if (!" << (seq ? "seq_open" : "mseq_open") << ks << "(" << op
           << ", kCompact, src, c, p, end, " << b << ", bump, " << n << ", " << a
           << ")) return false;\n"
           << in << "  for (uint32_t " << i << " = 0; " << i << " < " << n << "; ++" << i << ") {\n"
@@ -173,12 +176,12 @@ void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t sto
           << "u;\n";
         // (a struct element / value is default-constructed first; every
         // other slot is written whole)
-        if (v.elem_ttype == TGPU_T_STRUCT)
+        if (v.elem_ttype == TGPU_T_STRUCT && !meas)
           o << in << "    zero_slot<" << v.hdr << "u>(" << e << ");\n";
       }
-      gen_code(o, P, k + 1, v.hdr_len - 1, e, indent + 4, enc, last);
+      gen_code(o, P, k + 1, v.hdr_len - 1, e, indent + 4, enc, last, meas);
       o << in << "  }\n";
-      if (!enc) o << in << "  seq_close(" << op << ", " << b << ");\n";
+      if (!enc && !meas) o << in << "  seq_close(" << op << ", " << b << ");\n";
       o << in << "}\n";
       k = v.hdr_len;  // past the VOP_SEQ_END
       continue;
@@ -191,10 +194,11 @@ void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t sto
       if (v.kind != VOP_ISSET)
         o << in << "if (!enc_op(" << op << ", kCompact, " << b << ", sbase, lbase, o)) return false;\n";
     } else if (v.kind == VOP_LIST) {
-      o << in << "if (!nlist(" << op << ", kCompact, src, c, p, end, " << b << ", bump)) return false;\n";
-    } else {
-      o << in << "if (!run_op<true>(" << op << ", kCompact, src, c, p, end, " << b
-        << ", W)) return false;\n";
+      o << in << "if (!nlist" << ks << "(" << op << ", kCompact, src, c, p, end, " << b
+        << ", bump)) return false;\n";
+    } else if (v.kind != VOP_ISSET || !meas) {
+      o << in << "if (!run_op<" << (meas ? "false" : "true") << ">(" << op
+        << ", kCompact, src, c, p, end, " << b << ", W)) return false;\n";
     }
     ++k;
   }
@@ -245,6 +249,86 @@ std::string gen_source(const VProgram& P, int group) {
     << ";\n"
        "}  // namespace\n"
        "using namespace tgpu;\n";
+  if (group == JIT_NINDEX) {
+    // the stream index over a nested program: its measuring walk (the decode
+    // form with nothing stored) behind a program accessor whose ops are only
+    // what the index's candidate filter reads (the first header byte, STOP)
+    VOp h0{};
+    h0.kind = VOP_ISSET;  // (not a constant: no first-byte filter)
+    if (P.n_ops > 2 && P.ops[0].kind == VOP_SBEGIN && P.ops[1].kind == VOP_FHDR &&
+        !P.ops[1].width && !(P.protocol != TGPU_PROTOCOL_BINARY && P.ops[1].is_bool)) {
+      h0.kind = VOP_CONST;
+      h0.hdr_len = 1;
+      const int32_t id = (int16_t)P.ops[1].member;
+      h0.hdr = P.protocol == TGPU_PROTOCOL_BINARY ? (P.ops[1].hdr & 0xff)
+               : (id > 0 && id <= 15) ? (((uint32_t)id << 4) | P.ops[1].elem_ct)
+                                      : P.ops[1].elem_ct;
+    }
+    o << "#include \"tgpu_nested.h\"\n"
+         "namespace {\n"
+         "using namespace tgpu;\n"
+         "using namespace tgpu::prog;\n"
+         "constexpr bool kCompact = "
+      << (P.protocol == TGPU_PROTOCOL_BINARY ? "false" : "true")
+      << ";\n"
+         "template <class Src>\n"
+         "__device__ __forceinline__ bool nmeas(const Src& src, const Ctx& c, uint32_t& p, "
+         "const uint32_t end) {\n"
+         "  Win W;\n"
+         "  uint8_t* rec = nullptr;\n"
+         "  uint64_t bump = 0;\n"
+         "  (void)rec;\n"
+         "  (void)bump;\n";
+    gen_code(o, P, 0, P.n_ops, "rec", 2, false, "", true);
+    o << "  return true;\n"
+         "}\n"
+         "__device__ constexpr tgpu::VOp kH0 = {"
+      << (unsigned)h0.kind << ", " << (unsigned)h0.hdr_len << ", 0, 0, " << h0.hdr
+      << "u, 0, 65535, 0, 0, 0, 0};\n"
+         "__device__ constexpr tgpu::VOp kStop = {1, 1, 0, 0, 0u, 0, 65535, 0, 0, 0, 0};\n"
+         "struct NP {\n"
+         "  static constexpr bool kStatic = true;\n"
+         "  static constexpr uint32_t kN = 2;\n"
+         "  __device__ static constexpr uint32_t n_ops() { return kN; }\n"
+         "  __device__ static constexpr uint32_t protocol() { return "
+      << P.protocol
+      << "; }\n"
+         "  __device__ static constexpr bool has_lists() { return true; }\n"
+         "  __device__ constexpr tgpu::VOp op(uint32_t k) const { return k == 0 ? kH0 : kStop; }\n"
+         "};\n"
+         "// the measuring walks the index kernels take (found by ADL on NP)\n"
+         "__device__ __forceinline__ bool measure_lds(const NP&, const uint32_t* w32, uint32_t lim, "
+         "const Ctx& c, uint32_t& pos, uint32_t end, bool& slow) {\n"
+         "  bool sl = false;\n"
+         "  const ClampSrc src{w32, lim, &sl};\n"
+         "  uint32_t p = pos;\n"
+         "  const bool ok = nmeas(src, c, p, end);\n"
+         "  slow = sl;\n"
+         "  if (ok && !sl) pos = p;\n"
+         "  return ok;\n"
+         "}\n"
+         "template <bool kStore, class Src>\n"
+         "__device__ __forceinline__ bool run_program(const NP&, const Src& src, const Ctx& c, "
+         "uint32_t& pos, uint32_t end, uint8_t*) {\n"
+         "  if (kStore) return false;  // (never a fused decode: the nested decode follows)\n"
+         "  uint32_t p = pos;\n"
+         "  if (!nmeas(src, c, p, end)) return false;\n"
+         "  pos = p;\n"
+         "  return true;\n"
+         "}\n"
+         "}  // namespace\n"
+         "extern \"C\" __global__ __launch_bounds__(256) void tgpu_jit_nindex_spec(IndexArgs a) {\n"
+         "  __shared__ __attribute__((aligned(16))) uint8_t lds[prog::kTileLds];\n"
+         "  __shared__ prog::IndexTileShared sm;\n"
+         "  prog::index_spec_tile(a, NP{}, lds, sm);\n"
+         "}\n"
+         "extern \"C\" __global__ __launch_bounds__(256) void tgpu_jit_nindex_emit(IndexArgs a) {\n"
+         "  __shared__ __attribute__((aligned(16))) uint8_t lds[prog::kTileLds];\n"
+         "  __shared__ prog::IndexTileShared sm;\n"
+         "  prog::index_emit_kernel_body(a, NP{}, lds, sm);\n"
+         "}\n";
+    return o.str();
+  }
   if (group == JIT_NESTED) {
     o << "#include \"tgpu_nested.h\"\n"
          "namespace {\n"
@@ -486,7 +570,7 @@ int jit_compile_check(const VProgram& P, const char* arch, char* log, uint64_t l
   bool nested = false;
   for (uint32_t k = 0; k < P.n_ops; ++k)
     nested |= P.ops[k].kind >= VOP_SEQ;
-  for (int group = nested ? JIT_NESTED : 0; group < (nested ? JIT_NESTED + 1 : JIT_NESTED) && ok;
+  for (int group = nested ? JIT_NESTED : 0; group < (nested ? JIT_NINDEX + 1 : JIT_NESTED) && ok;
        ++group) {
     std::vector<char> code;
     ok = compile_code(P, group, arch ? arch : "gfx950", code, l);

@@ -102,7 +102,7 @@ __device__ __forceinline__ bool cfield(const Src& src, uint32_t& p, const uint32
   last = id;
   return true;
 }
-template <class Src>
+template <bool kStore = true, class Src>
 __device__ __forceinline__ bool cbool_field(const Src& src, uint32_t& p, const uint32_t end,
                                             int32_t id, int32_t& last, uint8_t* member,
                                             uint8_t* isset) {
@@ -114,8 +114,10 @@ __device__ __forceinline__ bool cbool_field(const Src& src, uint32_t& p, const u
   const uint64_t w = src.win8(p) & m;
   const uint32_t ct = (uint32_t)(w & 0xf);
   if ((w & ~0xfull) != hb || (ct != 1 && ct != 2)) return false;
-  *member = ct == 1 ? 1 : 0;
-  *isset = 1;
+  if (kStore) {
+    *member = ct == 1 ? 1 : 0;
+    *isset = 1;
+  }
   p += len;
   last = id;
   return true;
@@ -129,16 +131,18 @@ __device__ __forceinline__ bool struct_stop(const Src& src, uint32_t& p, const u
 
 // VOP_SEQ: the container's element array (n x op.hdr bytes) from the region
 // and its span at base + member; the caller loops over the elements.
-template <class Src>
+// kStore false: measuring only (the stream index), nothing allocated or written
+template <bool kStore = true, class Src>
 __device__ __forceinline__ bool seq_open(const VOp op, const bool compact, const Src& src,
                                          const Ctx& c, uint32_t& p, const uint32_t end,
                                          uint8_t* base, uint64_t& bump, uint32_t& n_out,
                                          uint8_t*& arr) {
   int64_t n;
   if (!seq_header(op, compact, src, c, p, end, n)) return false;
-  tgpu_span* sp = (tgpu_span*)(base + op.member);
   n_out = (uint32_t)n;
   arr = nullptr;
+  if (!kStore) return true;
+  tgpu_span* sp = (tgpu_span*)(base + op.member);
   if (n == 0) {
     *sp = tgpu_span{0, 0, 0};
     return true;
@@ -160,7 +164,7 @@ __device__ __forceinline__ void seq_close(const VOp op, uint8_t* base) {
 // varint size, then the key/value ctype byte when size > 0;
 // BinaryProtocol-inl.h:506-524, CompactProtocol-inl.h:662-690), the
 // truncation check of two bytes a pair, the pairs from the region.
-template <class Src>
+template <bool kStore = true, class Src>
 __device__ __forceinline__ bool mseq_open(const VOp op, const bool compact, const Src& src,
                                           const Ctx& c, uint32_t& p, const uint32_t end,
                                           uint8_t* base, uint64_t& bump, uint32_t& n_out,
@@ -183,9 +187,10 @@ __device__ __forceinline__ bool mseq_open(const VOp op, const bool compact, cons
   }
   if (n < 0 || (c.container_limit && n > c.container_limit) || 2 * n > (int64_t)(end - p))
     return false;
-  tgpu_span* sp = (tgpu_span*)(base + op.member);
   n_out = (uint32_t)n;
   arr = nullptr;
+  if (!kStore) return true;
+  tgpu_span* sp = (tgpu_span*)(base + op.member);
   if (n == 0) {
     *sp = tgpu_span{0, 0, 0};
     return true;
@@ -217,7 +222,7 @@ __device__ __forceinline__ void zero_slot(uint8_t* el) {
 
 // VOP_LIST of a nested program: scalar elements into the region (read_list,
 // tgpu_device.h: allocated only when n > 0), span at base + member.
-template <class Src>
+template <bool kStore = true, class Src>
 __device__ __forceinline__ bool nlist(const VOp op, const bool compact, const Src& src,
                                       const Ctx& c, uint32_t& p, const uint32_t end,
                                       uint8_t* base, uint64_t& bump) {
@@ -225,7 +230,12 @@ __device__ __forceinline__ bool nlist(const VOp op, const bool compact, const Sr
   if (!seq_header(op, compact, src, c, p, end, n)) return false;
   const uint32_t es = op.width;
   uint64_t aoff = 0;
-  if (n) {
+  if (!kStore && op.elem_kind == VEL_FIXED) {  // measuring: fixed-width elements skipped
+    if ((uint64_t)n * es > end - p) return false;
+    p += (uint32_t)n * es;
+    return true;
+  }
+  if (kStore && n) {
     if (!c.arena) return false;
     // the record's region, or the position rule (schemas without regions)
     aoff = c.pos_scale ? c.pos_scale * (c.gbase + p) : region_alloc(bump, (uint64_t)n * es);
@@ -247,7 +257,8 @@ __device__ __forceinline__ bool nlist(const VOp op, const bool compact, const Sr
       }
       if (len < 0 || (c.string_limit > 0 && len > c.string_limit) || len > (int64_t)(end - p))
         return false;
-      *(tgpu_span*)(dst + (uint64_t)i * es) = tgpu_span{len ? c.gbase + p : 0, (uint32_t)len, 0};
+      if (kStore)
+        *(tgpu_span*)(dst + (uint64_t)i * es) = tgpu_span{len ? c.gbase + p : 0, (uint32_t)len, 0};
       p += (uint32_t)len;
       continue;
     }
@@ -265,12 +276,29 @@ __device__ __forceinline__ bool nlist(const VOp op, const bool compact, const Sr
       }
       p += wb;
     }
-    store_n(dst + (uint64_t)i * es, v, es);
+    if (kStore) store_n(dst + (uint64_t)i * es, v, es);
   }
-  *(tgpu_span*)(base + op.member) = tgpu_span{n ? aoff : 0, (uint32_t)n, 0};
-  if (op.isset != 0xffff) base[op.isset] = 1;
+  if (kStore) {
+    *(tgpu_span*)(base + op.member) = tgpu_span{n ? aoff : 0, (uint32_t)n, 0};
+    if (op.isset != 0xffff) base[op.isset] = 1;
+  }
   return true;
 }
+
+// The stream index's view of the LDS tile for a measuring walk
+// (measure_lds): reads past lim are clamped and mark the walk undecided.
+struct ClampSrc {
+  const uint32_t* w32;
+  uint32_t lim;
+  bool* slow;
+  __device__ __forceinline__ uint64_t win8(uint32_t p) const {
+    if (p > lim) {
+      *slow = true;
+      p = lim;
+    }
+    return LdsSrc{w32}.win8(p);
+  }
+};
 
 // One 256-record tile of an indexed stream: decode_tile's staging (wire bytes
 // HBM -> LDS by LDS DMA, records built in an LDS record tile that leaves with
