@@ -1048,6 +1048,8 @@ bool launch_nested_decode(tgpu_context* ctx, const tgpu_schema* schema, int prot
                           const DecodeArgs& a, hipStream_t s, hipError_t& e) {
   const char* v = getenv("TGPU_NESTED_SRC");
   const bool hbm = v && !strcmp(v, "hbm");
+  v = getenv("TGPU_NESTED_RTILE");  // A/B: 0 = records straight to HBM, no LDS record tile
+  const bool rtile = !(v && v[0] == '0');
   const JitKernels* J =
       nested_jit(schema, protocol, a.n, a.height ? a.height : a.max_depth, a.max_depth);
   if (!J) return false;
@@ -1057,7 +1059,7 @@ bool launch_nested_decode(tgpu_context* ctx, const tgpu_schema* schema, int prot
   // the record tile (half a CU's 160 KiB: two workgroups per CU; a larger
   // tile's records take the general decoder). TGPU_NESTED_LDS=<bytes>
   // overrides the 80 KiB (A/B).
-  const uint32_t rt = (kPT * a.rec_size + 16 + 15) & ~15u;
+  const uint32_t rt = rtile ? (kPT * a.rec_size + 16 + 15) & ~15u : 0u;
   const double mean = (double)a.in_len / (double)a.n * kPT;
   double cap = 1.15 * mean + 1024.0;
   const char* lv = getenv("TGPU_NESTED_LDS");
@@ -1068,8 +1070,10 @@ bool launch_nested_decode(tgpu_context* ctx, const tgpu_schema* schema, int prot
   const uint32_t wire_cap = (uint32_t)cap & ~15u;
   // (prog::decode_wire_region: whole 4 KiB staging rounds)
   const uint32_t lds = hbm ? 0 : (wire_cap + 32 + 4095) / 4096 * 4096 + rt;
-  e = jit_launch_decode(J, a, tiles, wire_cap, lds, ctx->d_irr, &ctx->d_res->n_irregular, s,
-                        hbm ? 1 : 0);
+  // (entry 1: the variant without the LDS record tile, or with wire_cap 0
+  // the unstaged one)
+  e = jit_launch_decode(J, a, tiles, hbm ? 0 : wire_cap, lds, ctx->d_irr,
+                        &ctx->d_res->n_irregular, s, hbm || !rtile ? 1 : 0);
   if (e == hipSuccess)
     e = launch_general_decode_list(a, protocol, ctx->d_irr, &ctx->d_res->n_irregular, s);
   return true;

@@ -359,7 +359,9 @@ std::string gen_source(const VProgram& P, int group) {
          "}\n"
          "extern \"C\" __global__ __launch_bounds__(256) void tgpu_jit_ndecode_hbm(DecodeArgs a, "
          "uint32_t wire_cap, uint64_t* __restrict__ irr, unsigned long long* __restrict__ nirr) {\n"
-         "  nested_decode_hbm(a, NR{}, kS, kCompact, irr, nirr);\n"
+         "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+         "  if (wire_cap) nested_decode_tile<false>(a, NR{}, kS, kCompact, wire_cap, irr, nirr, smem);\n"
+         "  else nested_decode_hbm(a, NR{}, kS, kCompact, irr, nirr);\n"
          "}\n"
          "namespace {\n"
          "template <class O>\n"

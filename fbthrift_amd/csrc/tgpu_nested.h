@@ -312,7 +312,9 @@ __device__ __forceinline__ uint64_t pos_scale(const DevSchema& sc, bool compact)
   return sc.str_elems ? (compact ? 16 : 4) : (compact ? 8 : 1);
 }
 
-template <class R>
+// kRTile false (A/B, TGPU_NESTED_RTILE=0): no LDS record tile — each lane
+// zeroes and fills its record in HBM, the workgroup's LDS is the wire tile.
+template <bool kRTile = true, class R>
 __device__ __forceinline__ void nested_decode_tile(const DecodeArgs& a, const R& run, uint32_t S,
                                                    bool compact,
                                                    uint32_t wire_cap, uint64_t* __restrict__ irr,
@@ -344,7 +346,7 @@ __device__ __forceinline__ void nested_decode_tile(const DecodeArgs& a, const R&
   }
   uint8_t* gout = a.recs + r0 * S;
   const uint32_t osh = (uint32_t)((uintptr_t)gout & 15);
-  {
+  if (kRTile) {
     const uint4 z = {0u, 0u, 0u, 0u};
     const uint32_t nz = (kPT * S + osh + 15) >> 4;
     for (uint32_t i = threadIdx.x; i < nz; i += kPT) ((uint4*)rtile)[i] = z;
@@ -352,7 +354,14 @@ __device__ __forceinline__ void nested_decode_tile(const DecodeArgs& a, const R&
   __syncthreads();
   const uint32_t r = threadIdx.x;
   if (r < nrec) {
-    uint8_t* rec = rtile + osh + r * S;
+    uint8_t* rec = kRTile ? rtile + osh + r * S : gout + (uint64_t)r * S;
+    if (!kRTile) {
+      if ((S & 7) == 0 && ((uintptr_t)rec & 7) == 0) {
+        for (uint32_t b = 0; b < S; b += 8) *(uint64_t*)(rec + b) = 0;
+      } else {
+        for (uint32_t b = 0; b < S; ++b) rec[b] = 0;
+      }
+    }
     bool ok = tile_ok;
     if (ok) {
       const uint64_t s = a.offs[r0 + r], e = a.offs[r0 + r + 1];
@@ -369,6 +378,7 @@ __device__ __forceinline__ void nested_decode_tile(const DecodeArgs& a, const R&
     }
     if (!ok) irr[atomicAdd(nirr, 1ull)] = r0 + r;  // the general decoder's list
   }
+  if (!kRTile) return;
   __syncthreads();
   const uint32_t end = osh + nrec * S;
   const uint32_t nvec = (end + 15) >> 4;
