@@ -568,13 +568,18 @@ bool emit_container(const tgpu_schema& sc, uint32_t ttype, uint32_t et, uint32_t
 bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, VProgram& P,
                   bool nested = false, uint32_t depth = 0, uint32_t* max_depth = nullptr) {
   const tgpu_struct_desc& sd = sc.structs[si];
-  if (sd.flags & TGPU_STRUCT_UNION) return false;
+  const bool un = (sd.flags & TGPU_STRUCT_UNION) != 0;
+  if (un && !nested) return false;
   int32_t prev = 0;
   const uint32_t sbegin = P.n_ops;
-  if (nested && !push_op(P, make_op(VOP_SBEGIN))) return false;
+  if (nested) {
+    VOp sb = make_op(VOP_SBEGIN);
+    sb.width = un ? 1 : 0;  // a union: at most one member, the first present / set
+    if (!push_op(P, sb)) return false;
+  }
   for (uint32_t k = 0; k < sd.num_fields; ++k) {
     const tgpu_field_desc& f = sc.fields[sd.first_field + k];
-    const bool opt = nested && f.qualifier == TGPU_OPTIONAL;
+    const bool opt = nested && (f.qualifier == TGPU_OPTIONAL || un);
     if (f.qualifier != TGPU_UNQUALIFIED && f.qualifier != TGPU_REQUIRED && !opt) return false;
     const uint32_t member = base + f.member_offset, isset = base + f.isset_offset;
     if (member > 0xfffe || isset > 0xfffe) return false;

@@ -179,7 +179,8 @@ enum VOpKind : uint8_t {
   // the struct's last field (VOP_SBEGIN's scope), so they are computed, not
   // constant, once fields may be absent.
   VOP_FHDR = 11,
-  VOP_SBEGIN = 12,  // a struct's fields begin (hdr_len: one past its VOP_SEND)
+  VOP_SBEGIN = 12,  // a struct's fields begin (hdr_len: one past its VOP_SEND;
+                    // width 1: a union — one member at most, its FHDRs optional)
   VOP_SEND = 13,    // its STOP
 };
 enum VElemKind : uint8_t {

@@ -89,8 +89,13 @@ const char* const kEntry[5][5] = {
 // each VOP_SEQ / VOP_MSEQ a counted loop over its element slots. Leaf ops
 // are the program's op helpers on the constant op.
 // meas: the measuring walk of the stream index (decode form, nothing stored).
+// uvar: inside a union's scope, the flag of a member taken (union_declare:
+// the first present member on read — a second one fails the STOP check and
+// goes to the general reader, which reports UNION_MISSING_STOP — and the
+// first set one on write, serialize_union.whisker:52-66).
 void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t stop,
-              const std::string& b, int indent, bool enc, std::string last, bool meas = false) {
+              const std::string& b, int indent, bool enc, std::string last, bool meas = false,
+              const std::string& uvar = "") {
   const bool compact = P.protocol != TGPU_PROTOCOL_BINARY;
   const std::string ks = meas ? "<false>" : "";
   while (k < stop) {
@@ -101,7 +106,9 @@ void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t sto
       // the struct's fields up to its VOP_SEND (hdr_len: one past it)
       o << in << "{\n" << in << "  int32_t l" << K << " = 0;\n";
       if (compact) o << in << "  (void)l" << K << ";\n";
-      gen_code(o, P, k + 1, v.hdr_len - 1, b, indent + 2, enc, "l" + K, meas);
+      if (v.width) o << in << "  bool u" << K << " = false;\n";
+      gen_code(o, P, k + 1, v.hdr_len - 1, b, indent + 2, enc, "l" + K, meas,
+               v.width ? "u" + K : std::string());
       if (enc) o << in << "  o.put(0, 1);\n";  // writeFieldStop
       else o << in << "  if (!struct_stop(src, p, end)) return false;\n";
       o << in << "}\n";
@@ -125,7 +132,10 @@ void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t sto
         } else {
           hdr = "(o.put(" + std::to_string(v.hdr) + "u, 3), true)";
         }
-        if (opt) o << in << "if (" << b << "[" << v.isset << "]) {\n";
+        if (!uvar.empty())
+          o << in << "if (!" << uvar << " && " << b << "[" << v.isset << "]) {\n"
+            << in << "  " << uvar << " = true;\n";
+        else if (opt) o << in << "if (" << b << "[" << v.isset << "]) {\n";
         else o << in << "{\n";
         o << in << "  if (!" << hdr << ") return false;\n";
         if (!cbool) gen_code(o, P, k + 1, vend, b, indent + 2, enc, last, meas);
@@ -141,7 +151,9 @@ void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t sto
         } else {
           hdr = "bfield(src, p, end, " + std::to_string(v.hdr) + "u)";
         }
-        if (opt) {
+        if (!uvar.empty()) {
+          o << in << "if (!" << uvar << " && " << hdr << ") {\n" << in << "  " << uvar << " = true;\n";
+        } else if (opt) {
           o << in << "if (" << hdr << ") {\n";
         } else {
           o << in << "if (!" << hdr << ") return false;\n" << in << "{\n";

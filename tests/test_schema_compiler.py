@@ -1,8 +1,8 @@
 """The schema compiler (tgpu_jit.cpp) on a GPU-less host: the kernels it
 generates for a schema compile for gfx950 with hipRTC (all three kernel
 groups: decode, encode, index); schemas without one (optional fields,
-containers of structs) compile a nested record program instead; unions and
-the like are refused — they run on the general reader. GPU parity of
+containers of structs, unions) compile a nested record program instead;
+bools inside maps and the like are refused — they run on the general reader. GPU parity of
 the compiled kernels is in test_gpu_parity.py (TGPU_JIT=1 runs). Compiles
 cost seconds each, so the CPU suite covers the three BASELINE config schemas
 in their benchmarked protocol plus the bool/long-form-id heavy 'scalars'."""
@@ -29,6 +29,11 @@ def test_optional_fields_compile_nested_program():
     assert rc == 0, log
 
 
-def test_unions_have_no_program():
-    rc, _ = compile_check(Schema.from_table(M["unions"]), 2)
+def test_unions_compile_nested_program():
+    rc, log = compile_check(Schema.from_table(M["unions"]), 2)
+    assert rc == 0, log
+
+
+def test_bool_map_keys_have_no_program():
+    rc, _ = compile_check(Schema.from_table(M["maps"]), 2)
     assert rc == 22  # TGPU_ERR_UNSUPPORTED: the general reader path
