@@ -702,6 +702,8 @@ def main(argv=None):
     dec_avg = sum(dec_ms) / len(dec_ms) / 1e3
     enc_avg = sum(enc_ms) / len(enc_ms) / 1e3
     dec_alg, enc_alg = wl.algorithmic()
+    traffic, traffic_src = pmc_traffic(wl.dec_kernel, n, args.config)
+    enc_traffic, _ = pmc_traffic(wl.enc_kernel, n, args.config)
     line = {
         "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup,
@@ -716,7 +718,8 @@ def main(argv=None):
         "roofline": {"bound": "hbm", "kernel": wl.dec_kernel,
                      "achieved": round(dec_alg / dec_avg / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(dec_alg / dec_avg / 1e9 / HBM_PEAK_GBS, 4),
-                     "traffic": pmc_traffic(wl.dec_kernel, n, args.config),
+                     "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": dec_alg,
                      "avg_launch_ms": round(dec_avg * 1e3, 4),
                      "timing": "HIP events on the launch stream around the whole decode call "
@@ -726,6 +729,7 @@ def main(argv=None):
                                 "achieved": round(enc_alg / enc_avg / 1e9, 1),
                                 "frac": round(enc_alg / enc_avg / 1e9 / HBM_PEAK_GBS, 4),
                                 "algorithmic_bytes_per_launch": enc_alg,
+                                "traffic": enc_traffic,
                                 "avg_launch_ms": round(enc_avg * 1e3, 4)}},
     }
     if args.host_start and rank == 0:
@@ -885,6 +889,9 @@ def nested(dev, n=1 << 24, reps=5, seed=0x1729):
             "decode_GiBps": round(gib / dec_ms * 1e3, 1),
             "encode_plus_decode_GiBps": round(2 * gib / (enc_ms + dec_ms) * 1e3, 1),
             "roofline": {"bound": "hbm", "algorithmic_bytes_per_call": alg,
+                         "decode_traffic": pmc_traffic("tgpu_jit_ndecode", n, 4, True)[0],
+                         "encode_traffic": pmc_traffic("tgpu_jit_nsize+tgpu_jit_nwrite", n, 4,
+                                                       True)[0],
                          "decode_achieved_GBps": round(alg / dec_ms / 1e6, 1),
                          "decode_frac": round(alg / dec_ms / 1e6 / HBM_PEAK_GBS, 4),
                          "encode_achieved_GBps": round(alg / enc_ms / 1e6, 1),
@@ -892,7 +899,8 @@ def nested(dev, n=1 << 24, reps=5, seed=0x1729):
                          "peak": HBM_PEAK_GBS, "unit": "GB/s"},
             "kernels": "decode: tgpu_jit_ndecode (the nested program, one loop per "
                        "container level) + the general decoder for records it leaves; "
-                       "encode: encode_size_kernel + encode_write_kernel (general writer)"}
+                       "encode: tgpu_jit_nsize -> scan_tiles_* -> tgpu_jit_nwrite (the "
+                       "nested program's size and write passes)"}
 
 
 def irregular(wl, dev, reps=3):
@@ -1054,24 +1062,49 @@ def copy_ceiling(dev, nbytes=4 << 30):
     return {"GBps": round(2 * nbytes / t / 1e9, 1), "how": how}
 
 
-def pmc_traffic(kernel, n, config=2):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
-    summary (profiles/pmc_c<config>.json or, for config 2's plan kernels,
-    profiles/pmc_latest.json, written by tools/pmc_summary.py from separate
-    --pmc passes, gfx950 FETCH_SIZE x2 correction applied), scaled to
-    this launch's record count; None when no summary exists."""
-    # `kernel` may name the kernels of one call joined by '+': their sum
-    for name in ("pmc_c%d.json" % config, "pmc_latest.json"):
-        path = os.path.join(ROOT, "profiles", name)
+def pmc_summary(config, nested=False, root=None):
+    """The committed rocprofv3 PMC summary for this tree's kernels:
+    profiles/r<NN>/pmc/pmc_c<config>.json (pmc_nested.json for the nested
+    leg), newest round first, written by tools/pmc_summary.py from separate
+    FETCH_SIZE / WRITE_SIZE passes (gfx950 FETCH x2 correction calibrated on a
+    1 GiB copy). Only a summary stamped with the current kernel-source hash
+    (tools/srchash.py) counts: counters of other kernels are refused.
+    Returns (summary or None, note)."""
+    import glob
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from srchash import source_hash
+
+    root = root or ROOT
+    want = source_hash(root)
+    name = "pmc_nested.json" if nested else "pmc_c%d.json" % config
+    stale = []
+    for path in sorted(glob.glob(os.path.join(root, "profiles", "r[0-9]*", "pmc", name)),
+                       reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
-            if d.get("config", 2) != config:
-                continue
-            return int(sum(d[k]["hbm_bytes_per_record"] for k in kernel.split("+")) * n)
-        except (OSError, KeyError, ValueError):
+        except (OSError, ValueError):
             continue
-    return None
+        rel = os.path.relpath(path, root)
+        if d.get("source_hash") == want:
+            return d, rel
+        stale.append("%s (sources %s)" % (rel, d.get("source_hash")))
+    return None, ("no PMC summary of kernel sources %s; stale: %s"
+                  % (want, ", ".join(stale) or "none"))
+
+
+def pmc_traffic(kernel, n, config=2, nested=False, root=None):
+    """HBM bytes per launch of `kernel` (the kernels of one call joined by
+    '+': their sum) from pmc_summary(), scaled to this launch's record count;
+    (None, why) when no summary of the current kernels has it."""
+    d, note = pmc_summary(config, nested, root)
+    if d is None:
+        return None, note
+    try:
+        return int(sum(d[k]["hbm_bytes_per_record"] for k in kernel.split("+")) * n), note
+    except KeyError as e:
+        return None, "%s: no counters for %s" % (note, e)
 
 
 def transcode(wl, dev, reps=5):

@@ -15,8 +15,9 @@ counters by the factor of the access width it issues:
   plan_binary_encode_kernel : reads 8 B/lane, writes 16 B/lane
 
 usage: pmc_summary.py PMC_ROOT RECORDS_PER_LAUNCH [OUT.json]   (config 2's plan kernels)
-       pmc_summary.py PMC_ROOT --config C   (tools/pmc_config.sh: every kernel of config C
-                                             -> profiles/pmc_cC.json)
+       pmc_summary.py PMC_ROOT --config C [--nested] [--out OUT.json]
+                     (tools/profile_round.sh: every kernel of config C, or of its nested leg,
+                      -> OUT.json, default profiles/pmc_cC.json)
   PMC_ROOT holds fetch_calib/, write_calib/ (pmc_calib.py) and fetch_bench/,
   write_bench/ (bench.py) rocprofv3 output directories.
 """
@@ -48,14 +49,22 @@ def load(d, counter):
     return out
 
 
-def main_config(root, config):
-    """Every kernel of one bench config (tools/pmc_config.sh): all of them
+def main_config(root, config, out_path=None, nested=False):
+    """Every kernel of one bench config (tools/profile_round.sh): all of them
     read their input with 16-byte LDS-DMA / vector loads and store 16-byte
     vectors (offsets: 8-byte stores, same calibration factors), so the 16-byte
     factors apply. Records per launch and the decode / encode kernels'
-    algorithmic bytes come from the bench line of the FETCH pass."""
-    out_path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                            "profiles", "pmc_c%d.json" % config)
+    algorithmic bytes come from the bench line of the FETCH pass; with
+    `nested` from its nested leg (bench.py --nested: the nested programs'
+    records and algorithmic bytes per call). The summary is stamped with the
+    kernel-source hash (tools/srchash.py) and GIT_COMMIT, so bench.py can refuse
+    it once the kernels change."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    from srchash import source_hash
+
+    if out_path is None:
+        out_path = os.path.join(os.path.dirname(here), "profiles", "pmc_c%d.json" % config)
     line = None
     with open(os.path.join(root, "fetch_bench.log")) as fh:
         for ln in fh:
@@ -63,15 +72,30 @@ def main_config(root, config):
                 line = json.loads(ln)
     if line is None:
         raise SystemExit("no bench line in fetch_bench.log")
-    n = line["config"]["records_per_gpu"]
-    wire = line["config"]["wire_bytes_per_record"]
-    rec = line["config"]["record_bytes"]
-    roof = line["roofline"]
-    algo = {roof["kernel"]: roof["algorithmic_bytes_per_launch"] / n}
-    if "encode" in roof:
-        algo[roof["encode"]["kernel"]] = roof["encode"]["algorithmic_bytes_per_launch"] / n
-    algo.setdefault("tgpu_jit_index_spec", wire)
-    algo.setdefault("index_tile_spec_kernel", wire)
+    if nested:
+        nl = line["nested"]
+        n = nl["records"]
+        wire, rec = nl["wire_bytes"] / n, nl["record_bytes"]
+        a = nl["roofline"]["algorithmic_bytes_per_call"] / n
+        algo = {"tgpu_jit_ndecode": a, "tgpu_jit_nwrite": a}
+        calls = {"decode_call": ("tgpu_jit_ndecode", a),
+                 "encode_call": ("tgpu_jit_nsize+tgpu_jit_nwrite", a)}
+    else:
+        n = line["config"]["records_per_gpu"]
+        wire = line["config"]["wire_bytes_per_record"]
+        rec = line["config"]["record_bytes"]
+        roof = line["roofline"]
+        algo = {}
+        # a call's kernels joined by '+': the call's bytes go to its main kernel
+        algo[roof["kernel"].split("+")[-1]] = roof["algorithmic_bytes_per_launch"] / n
+        if "encode" in roof:
+            algo[roof["encode"]["kernel"].split("+")[-1]] = \
+                roof["encode"]["algorithmic_bytes_per_launch"] / n
+        algo.setdefault("tgpu_jit_index_spec", wire)
+        calls = {"decode_call": (roof["kernel"], roof["algorithmic_bytes_per_launch"] / n)}
+        if "encode" in roof:
+            calls["encode_call"] = (roof["encode"]["kernel"],
+                                    roof["encode"]["algorithmic_bytes_per_launch"] / n)
     fetch = load(os.path.join(root, "fetch_bench"), "FETCH_SIZE")
     write = load(os.path.join(root, "write_bench"), "WRITE_SIZE")
     cfetch = load(os.path.join(root, "fetch_calib"), "FETCH_SIZE")
@@ -82,15 +106,20 @@ def main_config(root, config):
 
     ff = CALIB_BYTES / (avg(cfetch["copy_kernel"]) * 1024)
     wf = CALIB_BYTES / (avg(cwrite["copy_kernel"]) * 1024)
-    res = {"config": config, "records_per_launch": n, "wire_bytes_per_record": wire,
-           "record_bytes": rec, "calibration": {"bytes": CALIB_BYTES, "fetch_factor": round(ff, 4),
-                                                "write_factor": round(wf, 4)},
+    res = {"config": config, "nested": nested, "records_per_launch": n,
+           "wire_bytes_per_record": round(wire, 3), "record_bytes": rec,
+           "source_hash": source_hash(os.path.dirname(here)),
+           "commit": os.environ.get("GIT_COMMIT"),
+           "calibration": {"bytes": CALIB_BYTES, "fetch_factor": round(ff, 4),
+                           "write_factor": round(wf, 4)},
            "bench_value": line["value"], "bench_unit": line["unit"]}
     for k in sorted(set(fetch) & set(write)):
         fb = avg(fetch[k]) * 1024 * ff
         wb = avg(write[k]) * 1024 * wf
-        if fb + wb < 4 * n:  # bookkeeping kernels: skip
+        if fb + wb < 4 * n and k not in algo:  # bookkeeping kernels: skip
             continue
+        if k.startswith(("gen_", "elementwise", "vectorized", "unrolled", "copy")):
+            continue  # data generation / torch checks, not the codec
         d = {"fetch_bytes": int(fb), "write_bytes": int(wb), "raw_fetch_kib": avg(fetch[k]),
              "raw_write_kib": avg(write[k]), "dispatches": [len(fetch[k]), len(write[k])],
              "fetch_bytes_per_record": round(fb / n, 3), "write_bytes_per_record": round(wb / n, 3),
@@ -99,6 +128,12 @@ def main_config(root, config):
             d["algorithmic_bytes_per_record"] = round(algo[k], 3)
             d["traffic_over_algorithmic"] = round((fb + wb) / n / algo[k], 4)
         res[k] = d
+    for c, (ks, a) in calls.items():  # a call's kernels together vs the call's bytes
+        if all(k in res for k in ks.split("+")):
+            b = sum(res[k]["hbm_bytes_per_record"] for k in ks.split("+"))
+            res[c] = {"kernels": ks, "hbm_bytes_per_record": round(b, 3),
+                      "algorithmic_bytes_per_record": round(a, 3),
+                      "traffic_over_algorithmic": round(b / a, 4)}
     with open(out_path, "w") as fh:
         json.dump(res, fh, indent=1)
     print(json.dumps(res, indent=1))
@@ -106,7 +141,8 @@ def main_config(root, config):
 
 def main():
     if len(sys.argv) > 3 and sys.argv[2] == "--config":
-        return main_config(sys.argv[1], int(sys.argv[3]))
+        out = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else None
+        return main_config(sys.argv[1], int(sys.argv[3]), out, "--nested" in sys.argv)
     root, n = sys.argv[1], int(sys.argv[2])
     out_path = sys.argv[3] if len(sys.argv) > 3 else os.path.join(
         os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_latest.json")
