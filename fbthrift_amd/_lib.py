@@ -73,7 +73,7 @@ assert ctypes.sizeof(Status) == 32
 EXPORTS = [
     "tgpu_abi_version", "tgpu_code_name", "tgpu_code_classify", "tgpu_layout_compute",
     "tgpu_schema_create", "tgpu_schema_create_ex", "tgpu_schema_destroy",
-    "tgpu_encoded_size_host", "tgpu_schema_record_size",
+    "tgpu_encoded_size_host", "tgpu_host_alloc", "tgpu_host_free", "tgpu_encode_host_chunks_ex", "tgpu_schema_record_size",
     "tgpu_schema_fixed_wire_size", "tgpu_context_create", "tgpu_context_destroy",
     "tgpu_context_reserve", "tgpu_context_wait", "tgpu_encode_batch", "tgpu_encoded_size",
     "tgpu_decode_batch", "tgpu_index_stream", "tgpu_schema_compile", "tgpu_schema_compile_check",

@@ -1054,7 +1054,7 @@ bool launch_nested_decode(tgpu_context* ctx, const tgpu_schema* schema, int prot
   const char* v = getenv("TGPU_NESTED_SRC");
   const bool hbm = v && !strcmp(v, "hbm");
   v = getenv("TGPU_NESTED_RTILE");  // A/B: 0 = records straight to HBM, no LDS record tile
-  const bool rtile = !(v && v[0] == '0');
+  bool rtile = !(v && v[0] == '0');
   const JitKernels* J =
       nested_jit(schema, protocol, a.n, a.height ? a.height : a.max_depth, a.max_depth);
   if (!J) return false;
@@ -1064,11 +1064,15 @@ bool launch_nested_decode(tgpu_context* ctx, const tgpu_schema* schema, int prot
   // the record tile (half a CU's 160 KiB: two workgroups per CU; a larger
   // tile's records take the general decoder). TGPU_NESTED_LDS=<bytes>
   // overrides the 80 KiB (A/B).
-  const uint32_t rt = rtile ? (kPT * a.rec_size + 16 + 15) & ~15u : 0u;
+  uint32_t rt = rtile ? (kPT * a.rec_size + 16 + 15) & ~15u : 0u;
   const double mean = (double)a.in_len / (double)a.n * kPT;
   double cap = 1.15 * mean + 1024.0;
   const char* lv = getenv("TGPU_NESTED_LDS");
   const double lds_max = lv ? std::min(atof(lv), 163840.0) : 81920.0;
+  // a record tile that leaves no room for the smallest wire region (root
+  // records of ~300 B and more) is dropped: records go straight to HBM
+  // (entry 1), the wire tile keeps the LDS
+  if (rt && rt + 4096.0 + 4096.0 + 32.0 > lds_max) rtile = false, rt = 0;
   const double room = lds_max - rt - 4096.0 - 32.0;
   if (cap > room) cap = room;
   if (cap < 4096.0) cap = 4096.0;

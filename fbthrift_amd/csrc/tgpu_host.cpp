@@ -29,6 +29,32 @@ namespace {
 constexpr int kSlots = 3;
 constexpr uint64_t kDefaultChunk = 1ull << 22;  // records per chunk
 
+// A device buffer kept by the pipe across calls, grown on demand (the
+// chunk pipelines' workspaces: hipMalloc / hipFree of hundreds of MiB per
+// call cost more than the copies they serve). Calls are blocking, so a
+// buffer is idle whenever a call starts and may be replaced then.
+struct GrowBuf {
+  uint8_t* p = nullptr;
+  uint64_t cap = 0;
+  bool reserve(uint64_t n) {
+    n = std::max<uint64_t>(n, 16);
+    if (n <= cap) return true;
+    release();
+    if (hipMalloc(&p, n) != hipSuccess) {
+      (void)hipGetLastError();
+      p = nullptr;
+      return false;
+    }
+    cap = n;
+    return true;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
 struct HostPipe {
   int device = 0;
   hipStream_t s[kSlots] = {};
@@ -36,6 +62,10 @@ struct HostPipe {
   uint8_t* d_in[kSlots] = {};
   uint8_t* d_out[kSlots] = {};
   uint64_t in_cap = 0, out_cap = 0;
+  // tgpu_decode_host_chunks: the stream, records, arena, offsets
+  GrowBuf din, drec, dar, doffs;
+  // tgpu_encode_host_chunks: two slots of records, strings, lists, wire
+  GrowBuf erec[2], estr[2], elst[2], eout[2];
 };
 
 void pipe_free_buffers(HostPipe* p) {
@@ -117,6 +147,9 @@ void host_pipe_destroy(void* vp) {
     if (p->s[k]) (void)hipStreamDestroy(p->s[k]);
   }
   pipe_free_buffers(p);
+  for (GrowBuf* b : {&p->din, &p->drec, &p->dar, &p->doffs}) b->release();
+  for (int k = 0; k < 2; ++k)
+    for (GrowBuf* b : {&p->erec[k], &p->estr[k], &p->elst[k], &p->eout[k]}) b->release();
   delete p;
 }
 
@@ -489,9 +522,9 @@ int tgpu_decode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int pr
   }
   auto* p = (HostPipe*)vp;
   PinGuard pin_in(h_in, in_len), pin_rec(h_records, n * S), pin_ar(h_arena, arena_capacity);
-  DevBuf din, drec, dar, doffs;
-  if (!din.alloc(in_len) || !drec.alloc(n * S) || (arena_capacity && !dar.alloc(arena_capacity)) ||
-      !doffs.alloc((n + 1) * 8)) {
+  GrowBuf &din = p->din, &drec = p->drec, &dar = p->dar, &doffs = p->doffs;
+  if (!din.reserve(in_len) || !drec.reserve(n * S) ||
+      (arena_capacity && !dar.reserve(arena_capacity)) || !doffs.reserve((n + 1) * 8)) {
     set_status(st, TGPU_ERR_HIP, 0, 0);
     return TGPU_ERR_HIP;
   }
@@ -532,7 +565,10 @@ int tgpu_decode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int pr
     const uint64_t avail = std::min(in_len, (ap + 1) * C);
     tgpu_status cs{};
     uint64_t nk = 0, first = 0, last = 0;
-    if (hipStreamWaitEvent(sdec, evin.ev[ap], 0) != hipSuccess) return TGPU_ERR_HIP;
+    if (hipStreamWaitEvent(sdec, evin.ev[ap], 0) != hipSuccess) {
+      clean = false;  // (the resident pass below reports the HIP failure)
+      break;
+    }
     const int rc = tgpu_decode_stream(p->c[1], schema, protocol, din.p, avail, B, end, 0,
                                       (uint64_t*)doffs.p + r0, n - r0, drec.p + r0 * S,
                                       arena_capacity ? dar.p : nullptr, arena_capacity, limits,
@@ -579,11 +615,10 @@ int tgpu_decode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int pr
                                &cs, &nd, &cons);
   if (code != TGPU_ERR_HIP) {
     const uint64_t back = std::min<uint64_t>(n, nd + (code ? 1 : 0));
-    uint64_t a0 = 0;  // arena bytes of the records from `announced` on
-    if (announced && hipMemcpy(&a0, (const uint64_t*)doffs.p + announced, 8,
-                               hipMemcpyDeviceToHost) != hipSuccess)
-      code = TGPU_ERR_HIP;
-    a0 = std::min(arena_capacity, scale * a0);
+    // arena bytes of the records from `announced` on: they start at the
+    // wire position of record `announced`, which is B (every announced
+    // range ended cleanly at the next one's start)
+    const uint64_t a0 = std::min(arena_capacity, scale * B);
     if (code != TGPU_ERR_HIP && back > announced &&
         (hipMemcpy((uint8_t*)h_records + announced * S, drec.p + announced * S,
                    (back - announced) * S, hipMemcpyDeviceToHost) != hipSuccess ||
@@ -607,6 +642,14 @@ int tgpu_encode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int pr
                             uint64_t n, uint64_t chunk_records, tgpu_fill_fn fill,
                             tgpu_reserve_fn reserve, void* user, tgpu_status* st,
                             uint64_t* out_size) {
+  return tgpu_encode_host_chunks_ex(ctx, schema, protocol, n, chunk_records, fill, reserve,
+                                    nullptr, user, st, out_size);
+}
+
+int tgpu_encode_host_chunks_ex(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                               uint64_t n, uint64_t chunk_records, tgpu_fill_fn fill,
+                               tgpu_reserve_fn reserve, tgpu_landed_fn landed, void* user,
+                               tgpu_status* st, uint64_t* out_size) {
   if (out_size) *out_size = 0;
   if (!ctx || !schema || !fill || !reserve) {
     set_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
@@ -627,12 +670,13 @@ int tgpu_encode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int pr
   const uint32_t S = tgpu_schema_record_size(schema);
   const hipStream_t sin = p->s[0], senc = p->s[1], sout = p->s[2];
   // two slots: chunk k's device form and output in slot k % 2
+  // (device buffers: the pipe's, kept across calls)
   struct Slot {
-    DevBuf rec, str, lst, out;
-    uint64_t rec_cap = 0, str_cap = 0, lst_cap = 0, out_cap = 0;
+    GrowBuf *rec, *str, *lst, *out;
     hipEvent_t in_done = nullptr, out_done = nullptr;
     uint64_t m = 0;
-  } slot[2];
+  } slot[2] = {{&p->erec[0], &p->estr[0], &p->elst[0], &p->eout[0]},
+               {&p->erec[1], &p->estr[1], &p->elst[1], &p->eout[1]}};
   for (auto& sl : slot) {
     (void)hipEventCreateWithFlags(&sl.in_done, hipEventDisableTiming);
     (void)hipEventCreateWithFlags(&sl.out_done, hipEventDisableTiming);
@@ -646,29 +690,20 @@ int tgpu_encode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int pr
       }
     }
   } evfree{slot};
-  auto grow = [](DevBuf& b, uint64_t& cap, uint64_t want) {
-    if (want <= cap) return true;
-    if (b.p) (void)hipFree(b.p);
-    b.p = nullptr;
-    cap = 0;
-    if (!b.alloc(want)) return false;
-    cap = want;
-    return true;
-  };
   // upload chunk c's form into its slot (after the slot's previous output left)
   auto upload = [&](uint64_t c) -> int {
     Slot& sl = slot[c % 2];
     const uint64_t r0 = c * K, m = std::min(K, n - r0);
     tgpu_host_form f{};
     if (fill(user, r0, r0 + m, &f) != 0 || !f.records) return TGPU_ERR_INVALID_ARGUMENT;
-    if (!grow(sl.rec, sl.rec_cap, m * S) || !grow(sl.str, sl.str_cap, f.strings_len + 16) ||
-        !grow(sl.lst, sl.lst_cap, f.lists_len + 16))
+    // (the slot's previous chunk has been encoded: its inputs are free)
+    if (!sl.rec->reserve(m * S) || !sl.str->reserve(f.strings_len + 16) ||
+        !sl.lst->reserve(f.lists_len + 16))
       return TGPU_ERR_HIP;
-    if (hipStreamWaitEvent(sin, sl.out_done, 0) != hipSuccess ||
-        hipMemcpyAsync(sl.rec.p, f.records, m * S, hipMemcpyHostToDevice, sin) != hipSuccess ||
-        (f.strings_len && hipMemcpyAsync(sl.str.p, f.strings, f.strings_len,
+    if (hipMemcpyAsync(sl.rec->p, f.records, m * S, hipMemcpyHostToDevice, sin) != hipSuccess ||
+        (f.strings_len && hipMemcpyAsync(sl.str->p, f.strings, f.strings_len,
                                          hipMemcpyHostToDevice, sin) != hipSuccess) ||
-        (f.lists_len && hipMemcpyAsync(sl.lst.p, f.lists, f.lists_len, hipMemcpyHostToDevice,
+        (f.lists_len && hipMemcpyAsync(sl.lst->p, f.lists, f.lists_len, hipMemcpyHostToDevice,
                                        sin) != hipSuccess) ||
         hipEventRecord(sl.in_done, sin) != hipSuccess)
       return TGPU_ERR_HIP;
@@ -679,13 +714,35 @@ int tgpu_encode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int pr
   // an overflow, found by the blocking size pass
   auto encode = [&](uint64_t c) -> int {
     Slot& sl = slot[c % 2];
-    if (!sl.out_cap && !grow(sl.out, sl.out_cap, std::max<uint64_t>(16ull << 20, sl.m * 64)))
+    const uint64_t want = std::max<uint64_t>(16ull << 20, sl.m * 64);
+    // (growing the wire buffer waits for its previous chunk's copy out)
+    if (want > sl.out->cap &&
+        (hipEventSynchronize(sl.out_done) != hipSuccess || !sl.out->reserve(want)))
       return TGPU_ERR_HIP;
     if (hipStreamWaitEvent(senc, sl.in_done, 0) != hipSuccess ||
         hipStreamWaitEvent(senc, sl.out_done, 0) != hipSuccess)
       return TGPU_ERR_HIP;
-    return tgpu_encode_batch(p->c[c % 2], schema, protocol, sl.rec.p, sl.m, sl.str.p, sl.lst.p,
-                             sl.out.p, sl.out_cap, nullptr, senc, nullptr, nullptr);
+    return tgpu_encode_batch(p->c[c % 2], schema, protocol, sl.rec->p, sl.m, sl.str->p, sl.lst->p,
+                             sl.out->p, sl.out->cap, nullptr, senc, nullptr, nullptr);
+  };
+  // chunks whose wire is on its way to the caller's memory, in order; the
+  // slot's out_done event is re-recorded two chunks later, so at most the
+  // previous chunk is still pending when a chunk's copy is issued
+  struct Landing {
+    uint64_t r0, r1;
+    void* dst;
+    uint64_t bytes;
+    hipEvent_t done;
+  };
+  std::vector<Landing> landing;
+  auto land = [&](bool all, uint64_t keep) {
+    size_t k = 0;
+    for (; k < landing.size() && landing.size() - k > keep; ++k) {
+      Landing& l = landing[k];
+      if (all || hipEventQuery(l.done) != hipSuccess) (void)hipEventSynchronize(l.done);
+      if (landed) landed(user, l.r0, l.r1, l.dst, l.bytes);
+    }
+    landing.erase(landing.begin(), landing.begin() + k);
   };
   uint64_t total = 0;
   int rc = upload(0);
@@ -706,15 +763,15 @@ int tgpu_encode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int pr
         rc = TGPU_ERR_HIP;
         break;
       }
-      code = tgpu_encoded_size(p->c[c % 2], schema, protocol, sl.rec.p, sl.m, sl.lst.p,
+      code = tgpu_encoded_size(p->c[c % 2], schema, protocol, sl.rec->p, sl.m, sl.lst->p,
                                (uint64_t*)offs.p, senc, &ss, &need);
       if (code == TGPU_OK) {
-        if (!grow(sl.out, sl.out_cap, need + 16)) {
+        if (hipEventSynchronize(sl.out_done) != hipSuccess || !sl.out->reserve(need + 16)) {
           rc = TGPU_ERR_HIP;
           break;
         }
-        code = tgpu_encode_batch(p->c[c % 2], schema, protocol, sl.rec.p, sl.m, sl.str.p,
-                                 sl.lst.p, sl.out.p, sl.out_cap, nullptr, senc, &cs, &bytes);
+        code = tgpu_encode_batch(p->c[c % 2], schema, protocol, sl.rec->p, sl.m, sl.str->p,
+                                 sl.lst->p, sl.out->p, sl.out->cap, nullptr, senc, &cs, &bytes);
       } else {
         cs = ss;
         bytes = 0;
@@ -726,17 +783,21 @@ int tgpu_encode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int pr
     }
     // the chunk's wire (or, on an error, the records before it) goes out
     if (bytes) {
+      land(false, 1);  // (the slot's event is re-recorded below)
       void* dst = reserve(user, bytes);
-      if (!dst || hipMemcpyAsync(dst, sl.out.p, bytes, hipMemcpyDeviceToHost, sout) != hipSuccess ||
+      if (!dst || hipMemcpyAsync(dst, sl.out->p, bytes, hipMemcpyDeviceToHost, sout) != hipSuccess ||
           hipEventRecord(sl.out_done, sout) != hipSuccess) {
         rc = dst ? TGPU_ERR_HIP : TGPU_ERR_OUTPUT_OVERFLOW;
         if (!dst) set_status(st, TGPU_ERR_OUTPUT_OVERFLOW, c * K, total);
         break;
       }
+      landing.push_back(Landing{c * K, c * K + (code == TGPU_OK ? sl.m : cs.record), dst, bytes,
+                                sl.out_done});
       total += bytes;
     }
     if (code != TGPU_OK) {
       (void)hipStreamSynchronize(sout);
+      land(true, 0);
       if (st) {
         *st = cs;
         st->record = c * K + cs.record;
@@ -751,6 +812,7 @@ int tgpu_encode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int pr
   (void)hipStreamSynchronize(sin);
   (void)hipStreamSynchronize(senc);
   (void)hipStreamSynchronize(sout);
+  land(true, 0);
   if (rc) {
     if (rc != TGPU_ERR_OUTPUT_OVERFLOW) set_status(st, rc, 0, 0);
     if (out_size) *out_size = total;
@@ -759,6 +821,21 @@ int tgpu_encode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int pr
   set_status(st, TGPU_OK, n, 0);
   if (out_size) *out_size = total;
   return TGPU_OK;
+}
+
+int tgpu_host_alloc(uint64_t bytes, void** out) {
+  if (!out) return TGPU_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  if (hipHostMalloc(out, std::max<uint64_t>(bytes, 16), hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    *out = nullptr;
+    return TGPU_ERR_HIP;
+  }
+  return TGPU_OK;
+}
+
+void tgpu_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
 }
 
 int tgpu_encoded_size_host(tgpu_context* ctx, const tgpu_schema* schema, int protocol,

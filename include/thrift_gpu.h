@@ -562,6 +562,23 @@ int tgpu_encode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int pr
                             uint64_t n_records, uint64_t chunk_records, tgpu_fill_fn fill,
                             tgpu_reserve_fn reserve, void* user, tgpu_status* st,
                             uint64_t* out_size);
+/* The same, and landed(user, r0, r1, dst, bytes) once the wire of records
+ * [r0, r1) has arrived at the `dst` reserve returned (in chunk order, on the
+ * calling thread, before the call returns; every chunk whose wire reserve
+ * took lands, also when a later one fails). A caller that reserves pinned
+ * staging moves each chunk on from there while later chunks still encode. */
+typedef void (*tgpu_landed_fn)(void* user, uint64_t r0, uint64_t r1, void* dst, uint64_t bytes);
+int tgpu_encode_host_chunks_ex(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                               uint64_t n_records, uint64_t chunk_records, tgpu_fill_fn fill,
+                               tgpu_reserve_fn reserve, tgpu_landed_fn landed, void* user,
+                               tgpu_status* st, uint64_t* out_size);
+
+/* Pinned (page-locked) host memory: staging for the host-memory entry
+ * points' records, arenas and device forms that the PCIe copies read and
+ * write without the runtime's bounce buffers or a per-call hipHostRegister
+ * (the C++ batch API keeps its staging in it across calls). */
+int tgpu_host_alloc(uint64_t bytes, void** out);
+void tgpu_host_free(void* p);
 
 /* Exact wire size of host-memory records (tgpu_encoded_size over host
  * buffers; host_out_offsets, n+1 entries, may be NULL): what an encode into

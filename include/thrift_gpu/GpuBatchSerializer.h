@@ -27,8 +27,12 @@
 #define THRIFT_GPU_GPU_BATCH_SERIALIZER_H_
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
+#include <exception>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -124,13 +128,16 @@ using IOBufQueue = folly::IOBufQueue;
 class IOBuf {
  public:
   static std::unique_ptr<IOBuf> copyBuffer(const void* p, size_t n) {
-    std::unique_ptr<IOBuf> b(new IOBuf());
-    b->bytes_.assign((const uint8_t*)p, (const uint8_t*)p + n);
+    std::unique_ptr<IOBuf> b = create(n);
+    if (n) std::memcpy(b->buf_.get(), p, n);
+    b->length_ = n;
     return b;
   }
+  /* An empty buffer of `capacity` bytes (not initialized, like folly's). */
   static std::unique_ptr<IOBuf> create(size_t capacity) {
     std::unique_ptr<IOBuf> b(new IOBuf());
-    b->bytes_.reserve(capacity);
+    b->buf_.reset(new uint8_t[capacity ? capacity : 1]);
+    b->capacity_ = capacity;
     return b;
   }
   ~IOBuf() {
@@ -146,10 +153,12 @@ class IOBuf {
       }
     }
   }
-  const uint8_t* data() const { return bytes_.data(); }
-  uint8_t* writableData() { return bytes_.data(); }
-  size_t length() const { return bytes_.size(); }
-  size_t capacity() const { return bytes_.capacity(); }
+  const uint8_t* data() const { return buf_.get(); }
+  uint8_t* writableData() { return buf_.get(); }
+  size_t length() const { return length_; }
+  size_t capacity() const { return capacity_; }
+  /* Grows / shrinks the data length within the capacity. */
+  void setLength(size_t n) { length_ = n < capacity_ ? n : capacity_; }
   IOBuf* next() { return next_; }
   const IOBuf* next() const { return next_; }
   bool isChained() const { return next_ != this; }
@@ -172,11 +181,11 @@ class IOBuf {
     } while (b != this);
     return n;
   }
-  std::vector<uint8_t>& bytes() { return bytes_; }
 
  private:
   IOBuf() : next_(this), prev_(this) {}
-  std::vector<uint8_t> bytes_;
+  std::unique_ptr<uint8_t[]> buf_;
+  size_t length_ = 0, capacity_ = 0;
   IOBuf* next_;
   IOBuf* prev_;
 };
@@ -185,14 +194,12 @@ class IOBufQueue {
  public:
   /* Writable space of at least `min` bytes at the end of the queue. */
   std::pair<void*, size_t> preallocate(size_t min, size_t newAllocationSize) {
-    std::unique_ptr<IOBuf> b = IOBuf::create(std::max(min, newAllocationSize));
-    b->bytes().resize(b->capacity());
-    pending_ = std::move(b);
-    return {pending_->writableData(), pending_->length()};
+    pending_ = IOBuf::create(std::max(min, newAllocationSize));
+    return {pending_->writableData(), pending_->capacity()};
   }
   /* Commits n bytes of the last preallocate(). */
   void postallocate(size_t n) {
-    pending_->bytes().resize(n);
+    pending_->setLength(n);
     if (!head_) head_ = std::move(pending_);
     else head_->prependChain(std::move(pending_));
   }
@@ -450,151 +457,191 @@ class GpuBatchSerializer {
    * with COPY semantics, Protocol.h:406-454) through `binding`. out[0..n)
    * are default-constructed T. Returns bytes consumed; throws like the
    * reference on the first failing record, the records before it set (the
-   * failing one partially, as the reference leaves it).
-   * The device pass is chunk-pipelined (tgpu_decode_host_chunks): while
-   * later chunks cross PCIe and decode, a host thread materializes the
-   * records of the finished ones (materialize_threads() threads each). */
+   * failing one partially, as the reference leaves it); an exception a
+   * binding hook throws reaches the caller too.
+   * The device pass is chunk-pipelined (tgpu_decode_host_chunks) into this
+   * serializer's pinned staging; every finished range of records is cut into
+   * blocks that the host pool's materialize_threads() workers turn into
+   * objects while later chunks cross PCIe and decode. */
   template <class T>
   uint64_t deserializeBatch(const IOBuf* buf, T* out, uint64_t n, const HostStruct& binding) {
-    std::vector<uint8_t> joined;
     const uint8_t* in = nullptr;
     uint64_t len = 0;
     if (buf && !buf->isChained()) {
       in = buf->data();
       len = buf->length();
-    } else {
-      joined = coalesced(buf);
-      in = joined.data();
-      len = joined.size();
+    } else if (buf) {  // a chain: its bytes in order, into pinned staging
+      len = buf->computeChainDataLength();
+      uint8_t* dst = in_.get(len + 16);
+      const IOBuf* b = buf;
+      uint64_t at = 0;
+      do {
+        std::memcpy(dst + at, b->data(), b->length());
+        at += b->length();
+        b = b->next();
+      } while (b != buf);
+      in = dst;
     }
     const uint32_t S = schema_.recordSize();
-    std::unique_ptr<uint8_t[]> recs(new uint8_t[n * S + 16]);
+    uint8_t* recs = recs_.get(n * S + 16);
     const uint64_t acap = len * tgpu_schema_arena_scale(schema_.get(), Protocol::kId);
-    std::unique_ptr<uint8_t[]> arena(new uint8_t[acap + 16]);
-    // finished record ranges, materialized in order by one host thread
+    uint8_t* arena = acap ? arena_.get(acap + 16) : nullptr;
     struct Feed {
-      std::mutex mu;
-      std::condition_variable cv;
-      std::vector<std::pair<uint64_t, uint64_t>> ranges;
-      bool closed = false;
-    } feed;
-    const SchemaTables tables = schema_.tables();
-    std::thread worker([&] {
-      size_t next = 0;
-      for (;;) {
-        std::pair<uint64_t, uint64_t> r;
-        {
-          std::unique_lock<std::mutex> lk(feed.mu);
-          feed.cv.wait(lk, [&] { return feed.closed || next < feed.ranges.size(); });
-          if (next == feed.ranges.size()) return;
-          r = feed.ranges[next++];
-        }
-        materialize(tables, recs.get() + r.first * S, r.second - r.first, S, in, arena.get(),
-                    binding, out + r.first, sizeof(T));
-      }
-    });
+      HostPool::Group g;
+      SchemaTables tables;
+      const uint8_t *recs, *in, *arena;
+      uint32_t S;
+      const HostStruct* binding;
+      T* out;
+    } feed{{}, schema_.tables(), recs, in, arena, S, &binding, out};
     auto on_chunk = [](void* u, uint64_t r0, uint64_t r1) {
       Feed& f = *static_cast<Feed*>(u);
-      {
-        std::lock_guard<std::mutex> lk(f.mu);
-        f.ranges.emplace_back(r0, r1);
-      }
-      f.cv.notify_one();
+      materializeAsync(f.g, f.tables, f.recs, r0, r1, f.S, f.in, f.arena, *f.binding, f.out,
+                       sizeof(T));
     };
     tgpu_status st{};
     uint64_t done = 0, consumed = 0;
-    tgpu_decode_host_chunks(ctx_, schema_.get(), Protocol::kId, in, len, n, recs.get(),
-                            acap ? arena.get() : nullptr, acap, &limits_, 0, on_chunk, &feed, &st,
-                            &done, &consumed);
-    {
-      std::lock_guard<std::mutex> lk(feed.mu);
-      feed.closed = true;
-    }
-    feed.cv.notify_one();
-    worker.join();
+    tgpu_decode_host_chunks(ctx_, schema_.get(), Protocol::kId, in, len, n, recs, arena, acap,
+                            &limits_, decodeChunkBytes(len), on_chunk, &feed, &st, &done,
+                            &consumed);
+    feed.g.wait();  // every announced record materialized (or a hook's exception)
     if (st.code != TGPU_OK) rethrow(st);
     return consumed;
   }
 
   /* serialize of codegen'd objects appended to an IOBufQueue: N x
    * Serializer::serialize(obj, &queue) (Serializer.h:136-148). Chunk-
-   * pipelined (tgpu_encode_host_chunks): the host builds chunk k+1's device
-   * form (materialize_threads() threads) while the device encodes chunk k,
-   * and each chunk's wire lands in a preallocate() of its exact size.
-   * Returns the bytes appended. */
+   * pipelined (tgpu_encode_host_chunks): while the device encodes chunk k,
+   * a producer builds chunk k+1's device form in this serializer's pinned
+   * slots (parts of the chunk sized, then written at their bases, on the host
+   * pool's threads), and each chunk's wire lands in a preallocate() of its
+   * exact size. Returns the bytes appended. */
   template <class T>
   uint64_t serializeBatch(const T* in, uint64_t n, const HostStruct& binding, IOBufQueue* out) {
-    constexpr uint64_t kChunk = 1ull << 20;  // records per chunk
-    const uint64_t nch = (n + kChunk - 1) / kChunk;
-    // a host thread builds the chunks' device forms ahead (3 slots: the one
-    // being uploaded, the one the library keeps until the next-but-one fill,
-    // the next one being built)
+    const uint64_t K = chunk_records_ ? chunk_records_ : (1ull << 20);  // records per chunk
+    const uint64_t nch = (n + K - 1) / K;
+    // three slots: chunk k is built into slot k % 3 once the library took
+    // chunk k - 1 (fill(k - 1)): it then holds chunks k - 1 and k - 2 only
+    // (the buffers of a fill stay in use until the next-but-one fill)
     struct Ctx {
       const T* in;
       const HostStruct* binding;
       SchemaTables tables;
       uint32_t S;
-      uint64_t n, nch;
-      detail::DeviceForm form[3];
+      uint64_t n, nch, K;
+      FormSlot* slot;
       uint64_t built = 0, taken = 0;  // chunks built / handed to the library
       std::mutex mu;
       std::condition_variable cv;
-      bool stop = false;
+      bool stop = false, failed = false;
+      std::exception_ptr err;
       IOBufQueue* out;
-    } c{in, &binding, schema_.tables(), schema_.recordSize(), n, nch, {}, 0, 0, {}, {}, false, out};
+      // the wire: each chunk's D2H lands in pinned staging (slot k % 3),
+      // then the pool copies it into the queue's preallocated space
+      WireStage* stage;
+      uint64_t reserved = 0;
+      std::vector<uint8_t*> dst;  // queue space of chunk k
+      double t_build = 0, t_fill = 0, t_reserve = 0;  // TGPU_HOST_TIMING (seconds)
+    } c{in, &binding, schema_.tables(), schema_.recordSize(), n, nch, K, slots_,
+        0, 0, {}, {}, false, false, nullptr, out, wire_, 0, {}};
+    using Clk = std::chrono::steady_clock;
+    auto secs = [](Clk::time_point t) {
+      return std::chrono::duration<double>(Clk::now() - t).count();
+    };
+    const auto t_call = Clk::now();
     std::thread producer([&c] {
-      for (uint64_t k = 0; k < c.nch; ++k) {
-        {
-          std::unique_lock<std::mutex> lk(c.mu);
-          // slot k % 3 is free once the library took chunk k - 1 (it keeps
-          // at most chunks k - 2, k - 1)
-          c.cv.wait(lk, [&] { return c.stop || c.taken + 2 > k; });
-          if (c.stop) return;
+      try {
+        for (uint64_t k = 0; k < c.nch; ++k) {
+          {
+            std::unique_lock<std::mutex> lk(c.mu);
+            c.cv.wait(lk, [&] { return c.stop || c.taken >= k; });
+            if (c.stop) return;
+          }
+          const uint64_t r0 = k * c.K, r1 = std::min(c.n, r0 + c.K);
+          const auto t0 = Clk::now();
+          c.slot[k % 3].build(c.tables, c.S, c.in, r0, r1, sizeof(T), *c.binding);
+          c.t_build += std::chrono::duration<double>(Clk::now() - t0).count();
+          {
+            std::lock_guard<std::mutex> lk(c.mu);
+            c.built = k + 1;
+          }
+          c.cv.notify_all();
         }
-        const uint64_t r0 = k * kChunk, r1 = std::min(c.n, r0 + kChunk);
-        c.form[k % 3] = dematerialize(c.tables, c.S, c.in + r0, r1 - r0, sizeof(T), *c.binding);
-        {
-          std::lock_guard<std::mutex> lk(c.mu);
-          c.built = k + 1;
-        }
+      } catch (...) {
+        std::lock_guard<std::mutex> lk(c.mu);
+        c.err = std::current_exception();
+        c.failed = true;
         c.cv.notify_all();
       }
     });
     auto fill = [](void* u, uint64_t r0, uint64_t, tgpu_host_form* f) -> int {
       Ctx& x = *static_cast<Ctx*>(u);
-      const uint64_t k = r0 / kChunk;
+      const uint64_t k = r0 / x.K;
+      const auto t0 = std::chrono::steady_clock::now();
       std::unique_lock<std::mutex> lk(x.mu);
-      x.cv.wait(lk, [&] { return x.built > k; });
+      x.cv.wait(lk, [&] { return x.built > k || x.failed; });
+      x.t_fill += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (x.built <= k) return -1;
       x.taken = k + 1;
       lk.unlock();
       x.cv.notify_all();
-      detail::DeviceForm& d = x.form[k % 3];
-      f->records = d.records.data();
-      f->strings = d.strings.data();
-      f->strings_len = d.strings.size();
-      f->lists = d.lists.data();
-      f->lists_len = d.lists.size();
+      const FormSlot& d = x.slot[k % 3];
+      f->records = d.rec.data();
+      f->strings = d.str.data();
+      f->strings_len = d.slen;
+      f->lists = d.lst.data();
+      f->lists_len = d.llen;
       return 0;
     };
     auto reserve = [](void* u, uint64_t bytes) -> void* {
-      IOBufQueue& q = *static_cast<Ctx*>(u)->out;
-      auto space = q.preallocate(bytes, bytes);
-      q.postallocate(bytes);  // filled before serializeBatch returns
-      return space.first;
+      Ctx& x = *static_cast<Ctx*>(u);
+      const auto t0 = std::chrono::steady_clock::now();
+      auto space = x.out->preallocate(bytes, bytes);
+      x.out->postallocate(bytes);  // filled before serializeBatch returns
+      x.dst.push_back(static_cast<uint8_t*>(space.first));
+      WireStage& w = x.stage[x.reserved++ % 3];
+      w.copies.wait();  // its previous chunk has left the staging
+      uint8_t* p = w.buf.get(bytes + 16);
+      x.t_reserve += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      return p;
+    };
+    auto landed = [](void* u, uint64_t r0, uint64_t, void* src, uint64_t bytes) {
+      Ctx& x = *static_cast<Ctx*>(u);
+      const uint64_t k = r0 / x.K;
+      uint8_t* d = x.dst[k];
+      const uint8_t* sp = static_cast<const uint8_t*>(src);
+      constexpr uint64_t kPiece = 4ull << 20;  // (first touch of the queue's pages too)
+      for (uint64_t a = 0; a < bytes; a += kPiece) {
+        const uint64_t m = std::min(kPiece, bytes - a);
+        x.stage[k % 3].copies.run([=] { std::memcpy(d + a, sp + a, m); });
+      }
     };
     tgpu_status st{};
     uint64_t size = 0;
-    tgpu_encode_host_chunks(ctx_, schema_.get(), Protocol::kId, n, kChunk, fill, reserve, &c,
-                            &st, &size);
+    tgpu_encode_host_chunks_ex(ctx_, schema_.get(), Protocol::kId, n, K, fill, reserve, landed,
+                               &c, &st, &size);
     {
       std::lock_guard<std::mutex> lk(c.mu);
       c.stop = true;
     }
     c.cv.notify_all();
     producer.join();
+    for (int k = 0; k < 3; ++k) wire_[k].copies.wait();
+    if (std::getenv("TGPU_HOST_TIMING"))
+      std::fprintf(stderr,
+                   "serializeBatch: %.3f ms total, build %.3f ms (producer), fill wait %.3f ms, "
+                   "reserve %.3f ms, %llu chunks\n",
+                   secs(t_call) * 1e3, c.t_build * 1e3, c.t_fill * 1e3, c.t_reserve * 1e3,
+                   (unsigned long long)nch);
+    if (c.err) std::rethrow_exception(c.err);
     if (st.code != TGPU_OK) rethrow(st);
     return size;
   }
+
+  /* Records per serializeBatch chunk (0 = 1 Mi) and wire bytes per
+   * deserializeBatch piece (0 = 1/16 of the batch, 4-64 MiB). */
+  void setChunkRecords(uint64_t k) { chunk_records_ = k; }
+  void setChunkBytes(uint64_t b) { chunk_bytes_ = b; }
 
   /* Re-encodes n records of `in` (this serializer's protocol) into protocol
    * To (tgpu_transcode_batch): serialize<To>(deserialize<From>(record)) per
@@ -659,10 +706,96 @@ class GpuBatchSerializer {
   }
 
  private:
+  uint64_t decodeChunkBytes(uint64_t len) const {
+    if (chunk_bytes_) return chunk_bytes_;
+    return std::min<uint64_t>(64ull << 20, std::max<uint64_t>(4ull << 20, len / 16));
+  }
+  /* Pinned host staging kept across calls (grown with 25 % slack). */
+  class Pinned {
+   public:
+    Pinned() = default;
+    Pinned(const Pinned&) = delete;
+    ~Pinned() { tgpu_host_free(p_); }
+    uint8_t* get(uint64_t n) {
+      if (n > cap_) {
+        tgpu_host_free(p_);
+        p_ = nullptr;
+        cap_ = 0;
+        const uint64_t want = n + n / 4;
+        void* q = nullptr;
+        check(tgpu_host_alloc(want, &q), "tgpu_host_alloc");
+        p_ = static_cast<uint8_t*>(q);
+        cap_ = want;
+      }
+      return p_;
+    }
+    uint8_t* data() const { return p_; }
+
+   private:
+    uint8_t* p_ = nullptr;
+    uint64_t cap_ = 0;
+  };
+  /* One chunk's device form in pinned memory: records, string base, list
+     base. build(): the chunk's records cut into parts, each part's string /
+     list bytes sized (formBytes), then every part written at its base
+     (formWrite) — both passes in parallel on the host pool. */
+  struct FormSlot {
+    Pinned rec, str, lst;
+    uint64_t slen = 0, llen = 0;
+    void build(const SchemaTables& sc, uint32_t S, const void* objects, uint64_t r0, uint64_t r1,
+               size_t stride, const HostStruct& hs) {
+      const uint64_t m = r1 - r0;
+      const uint64_t P = std::max<uint64_t>(
+          1, std::min<uint64_t>(4ull * materialize_threads(), m / 2048));
+      auto bound = [&](uint64_t t) { return r0 + m * t / P; };
+      std::vector<std::pair<uint64_t, uint64_t>> sz(P);
+      {
+        HostPool::Group g;
+        for (uint64_t t = 0; t < P; ++t)
+          g.run([&, t] { sz[t] = formBytes(sc, objects, bound(t), bound(t + 1), stride, hs); });
+        g.wait();
+      }
+      std::vector<detail::Sink> at(P);
+      uint64_t SB = 0, LB = 0;
+      for (uint64_t t = 0; t < P; ++t) {
+        at[t].spos = SB;
+        at[t].lpos = LB;
+        SB += sz[t].first;
+        LB = (LB + sz[t].second + 7) & ~7ull;
+      }
+      uint8_t* rp = rec.get(m * S + 16);
+      uint8_t* sp = str.get(SB + 16);
+      uint8_t* lp = lst.get(LB + 16);
+      slen = SB;
+      llen = LB;
+      HostPool::Group g;
+      for (uint64_t t = 0; t < P; ++t)
+        g.run([&, t] {
+          detail::Sink k = at[t];
+          k.strings = sp;
+          k.lists = lp;
+          formWrite(sc, S, objects, bound(t), bound(t + 1), stride, hs,
+                    rp + (bound(t) - r0) * S, k);
+        });
+      g.wait();
+    }
+  };
+
   const GpuSchema& schema_;
   void* stream_;
   tgpu_context* ctx_ = nullptr;
   tgpu_limits limits_{0, 0, 12000, 0};
+  /* Pinned landing place of one chunk's wire and the host copies that move
+     it into the queue. */
+  struct WireStage {
+    Pinned buf;
+    HostPool::Group copies;
+  };
+
+  uint64_t chunk_records_ = 0, chunk_bytes_ = 0;
+  Pinned in_, recs_, arena_;
+  FormSlot slots_[3];
+  WireStage wire_[3];
 };
 
 using BinaryBatchSerializer = GpuBatchSerializer<BinaryProtocol>;

@@ -20,12 +20,18 @@
 #define THRIFT_GPU_HOST_BINDING_H_
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <exception>
+#include <functional>
+#include <mutex>
 #include <new>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -59,6 +65,16 @@ struct HostType {
      the object the member points to (nullptr: null). */
   void* (*make)(void* member) = nullptr;
   const void* (*get)(const void* member) = nullptr;
+  /* Container: element count (encode sizes the element array with it). */
+  uint64_t (*count)(const void* c) = nullptr;
+  /* Contiguous containers of arithmetic elements (std::vector<int32_t>, ...):
+     the whole element array at once — `assign` replaces the contents with n
+     elements (decode: the reader's resize + readArithmeticVector,
+     protocol_methods.h:413-441, BinaryProtocol.cpp:49-72), `data` returns
+     them (encode: writeArithmeticVector, BinaryProtocol.cpp:95-117). The
+     device element slots of a scalar list are the elements themselves. */
+  void (*assign)(void* c, const void* data, uint64_t n) = nullptr;
+  const void* (*data)(const void* c) = nullptr;
 };
 
 /* One schema field of a struct, in the schema's declaration order. */
@@ -106,6 +122,7 @@ HostType boxType(const HostStruct* st) {
 /* std::vector<E> for list<...>. */
 template <class V>
 HostType listType(const HostType* elem) {
+  using E = typename V::value_type;
   HostType t;
   t.kind = HostType::Container;
   t.elem = elem;
@@ -116,6 +133,16 @@ HostType listType(const HostType* elem) {
   t.each = [](const void* c, void* ctx, HostType::Visit fn) {
     for (const auto& e : *static_cast<const V*>(c)) fn(ctx, &e, nullptr);
   };
+  t.count = [](const void* c) -> uint64_t { return static_cast<const V*>(c)->size(); };
+  if constexpr (std::is_arithmetic_v<E> && !std::is_same_v<E, bool> &&
+                std::is_same_v<V, std::vector<E>>) {
+    if (elem && elem->kind == HostType::Scalar && elem->size == sizeof(E)) {
+      t.assign = [](void* c, const void* d, uint64_t n) {
+        static_cast<V*>(c)->assign(static_cast<const E*>(d), static_cast<const E*>(d) + n);
+      };
+      t.data = [](const void* c) -> const void* { return static_cast<const V*>(c)->data(); };
+    }
+  }
   return t;
 }
 /* std::set<E> (or any insert-able set) for set<...>. */
@@ -133,6 +160,7 @@ HostType setType(const HostType* elem) {
   t.each = [](const void* c, void* ctx, HostType::Visit fn) {
     for (const auto& e : *static_cast<const C*>(c)) fn(ctx, &e, nullptr);
   };
+  t.count = [](const void* c) -> uint64_t { return static_cast<const C*>(c)->size(); };
   return t;
 }
 /* std::map<K, V> for map<...>: the first of equal keys wins (emplace). */
@@ -152,6 +180,7 @@ HostType mapType(const HostType* key, const HostType* val) {
   t.each = [](const void* c, void* ctx, HostType::Visit fn) {
     for (const auto& kv : *static_cast<const C*>(c)) fn(ctx, &kv.first, &kv.second);
   };
+  t.count = [](const void* c) -> uint64_t { return static_cast<const C*>(c)->size(); };
   return t;
 }
 
@@ -250,6 +279,10 @@ struct ElemCtx {
 inline void readContainer(const SchemaTables& sc, const CType& c, const uint8_t* dev,
                           const Sources& src, const HostType& ht, void* host) {
   const tgpu_span s = loadSpan(dev);
+  if (ht.assign && c.ttype == TGPU_T_LIST) {  // the element array, whole
+    ht.assign(host, src.arena + s.offset, s.length);
+    return;
+  }
   ht.clear(host);
   const bool is_map = c.ttype == TGPU_T_MAP;
   const uint32_t v = is_map ? c.val : c.elem;
@@ -297,160 +330,134 @@ inline void readStruct(const SchemaTables& sc, uint32_t si, const uint8_t* dev,
 }
 
 // ---- host objects -> device form (encode input) ------------------------------
-/* The encode-side buffers: records, then the string base and list base the
-   records' spans are relative to (list arrays 8-byte aligned). */
-struct DeviceForm {
-  std::vector<uint8_t> records, strings, lists;
+/* Where one part of a chunk's device form goes: string bytes at
+   strings + spos.., list arrays (8-byte aligned) at lists + lpos... Positions
+   are relative to the chunk's string / list base, and a part starts at its
+   own base, so every span it stores is final. Count mode (the sizing pass
+   that places the parts) only advances the positions. */
+struct Sink {
+  uint8_t* strings = nullptr;
+  uint8_t* lists = nullptr;
+  uint64_t spos = 0, lpos = 0;
   uint64_t alloc(uint64_t bytes) {
-    const uint64_t o = (lists.size() + 7) & ~7ull;
-    lists.resize(o + bytes);
+    const uint64_t o = (lpos + 7) & ~7ull;
+    lpos = o + bytes;
     return o;
   }
 };
 
-void writeStruct(const SchemaTables&, uint32_t si, const uint8_t* host, const HostStruct&,
-                 DeviceForm&, uint64_t dev_off, std::vector<uint8_t>* buf);
+template <bool Count>
+void writeStruct(const SchemaTables&, uint32_t si, const uint8_t* host, const HostStruct&, Sink&,
+                 uint8_t* dev);
+template <bool Count>
+void writeValue(const SchemaTables& sc, uint32_t t, int32_t si, uint32_t ti, const void* host,
+                const HostType& ht, Sink& out, uint8_t* dev);
 
-/* Writes the value at host into buf[off..] (buf: records or lists; resized
-   by nested allocations, so addressed by offset). */
-inline void writeValue(const SchemaTables& sc, uint32_t t, int32_t si, uint32_t ti,
-                       const void* host, const HostType& ht, DeviceForm& out,
-                       std::vector<uint8_t>* buf, uint64_t off);
-
+template <bool Count>
 struct WriteCtx {
   const SchemaTables* sc;
   const CType* c;
   const HostType* ht;
-  DeviceForm* out;
-  uint64_t arr;  /* element array offset in out->lists */
+  Sink* out;
+  uint64_t arr; /* element array position in the list base */
   uint32_t es, ks;
   uint64_t i;
 };
 
-inline void writeContainer(const SchemaTables& sc, const CType& c, const void* host,
-                           const HostType& ht, DeviceForm& out, std::vector<uint8_t>* buf,
-                           uint64_t off) {
+inline bool hasSpans(uint32_t t) {
+  return t == TGPU_T_STRING || t == TGPU_T_STRUCT || isContainer(t);
+}
+
+/* A container's span at dev and its element array in the list base. */
+template <bool Count>
+void writeContainer(const SchemaTables& sc, const CType& c, const void* host, const HostType& ht,
+                    Sink& out, uint8_t* dev) {
   uint64_t n = 0;
-  ht.each(host, &n, [](void* p, const void*, const void*) { ++*static_cast<uint64_t*>(p); });
+  if (ht.count) n = ht.count(host);
+  else ht.each(host, &n, [](void* p, const void*, const void*) { ++*static_cast<uint64_t*>(p); });
   const bool is_map = c.ttype == TGPU_T_MAP;
   const uint32_t v = is_map ? c.val : c.elem;
   const uint32_t ks = is_map ? slotBytes(sc, c.elem, keyStruct(sc, c)) : 0;
   const uint32_t es = ks + slotBytes(sc, v, c.si);
   const uint64_t arr = n ? out.alloc(n * es) : 0;
-  storeSpan(buf->data() + off, arr, n);
-  WriteCtx ctx{&sc, &c, &ht, &out, arr, es, ks, 0};
+  if (!Count) storeSpan(dev, arr, n);
+  if (!n) return;
+  if (ht.data && c.ttype == TGPU_T_LIST) {  // arithmetic elements: one copy
+    if (!Count) std::memcpy(out.lists + arr, ht.data(host), n * es);
+    return;
+  }
+  // scalar elements place nothing else (count mode is done)
+  if (Count && !hasSpans(v) && !(is_map && hasSpans(c.elem))) return;
+  // struct slots: fields the binding skips read as zero (unset)
+  if (!Count && (v == TGPU_T_STRUCT || (is_map && c.elem == TGPU_T_STRUCT)))
+    std::memset(out.lists + arr, 0, n * es);
+  WriteCtx<Count> ctx{&sc, &c, &ht, &out, arr, es, ks, 0};
   ht.each(host, &ctx, [](void* p, const void* ek, const void* hv) {
-    WriteCtx& x = *static_cast<WriteCtx*>(p);
+    WriteCtx<Count>& x = *static_cast<WriteCtx<Count>*>(p);
     const uint64_t at = x.arr + x.i++ * x.es;
+    uint8_t* e = Count ? nullptr : x.out->lists + at;
     if (x.c->ttype == TGPU_T_MAP) {
-      writeValue(*x.sc, x.c->elem, keyStruct(*x.sc, *x.c), keyNode(*x.c), ek, *x.ht->elem,
-                 *x.out, &x.out->lists, at);
-      writeValue(*x.sc, x.c->val, x.c->si, x.c->ti, hv, *x.ht->val, *x.out, &x.out->lists,
-                 at + x.ks);
+      writeValue<Count>(*x.sc, x.c->elem, keyStruct(*x.sc, *x.c), keyNode(*x.c), ek, *x.ht->elem,
+                        *x.out, e);
+      writeValue<Count>(*x.sc, x.c->val, x.c->si, x.c->ti, hv, *x.ht->val, *x.out,
+                        Count ? nullptr : e + x.ks);
     } else {
-      writeValue(*x.sc, x.c->elem, x.c->si, x.c->ti, ek, *x.ht->elem, *x.out, &x.out->lists,
-                 at);
+      writeValue<Count>(*x.sc, x.c->elem, x.c->si, x.c->ti, ek, *x.ht->elem, *x.out, e);
     }
   });
 }
 
-inline void writeValue(const SchemaTables& sc, uint32_t t, int32_t si, uint32_t ti,
-                       const void* host, const HostType& ht, DeviceForm& out,
-                       std::vector<uint8_t>* buf, uint64_t off) {
+/* The value at host into its device slot dev (nullptr in count mode). */
+template <bool Count>
+void writeValue(const SchemaTables& sc, uint32_t t, int32_t si, uint32_t ti, const void* host,
+                const HostType& ht, Sink& out, uint8_t* dev) {
   if (t == TGPU_T_STRING) {
     const std::string& s = *static_cast<const std::string*>(host);
-    storeSpan(buf->data() + off, out.strings.size(), s.size());
-    out.strings.insert(out.strings.end(), s.begin(), s.end());
+    if (!Count) {
+      storeSpan(dev, out.spos, s.size());
+      std::memcpy(out.strings + out.spos, s.data(), s.size());
+    }
+    out.spos += s.size();
   } else if (t == TGPU_T_STRUCT) {
-    writeStruct(sc, (uint32_t)si, (const uint8_t*)host, *ht.st, out, off, buf);
+    writeStruct<Count>(sc, (uint32_t)si, (const uint8_t*)host, *ht.st, out, dev);
   } else if (isContainer(t)) {
-    writeContainer(sc, ctypeNode(sc, ti), host, ht, out, buf, off);
-  } else {
-    std::memcpy(buf->data() + off, host, scalarBytes(t));
+    writeContainer<Count>(sc, ctypeNode(sc, ti), host, ht, out, dev);
+  } else if (!Count) {
+    std::memcpy(dev, host, scalarBytes(t));
   }
 }
 
-inline void writeStruct(const SchemaTables& sc, uint32_t si, const uint8_t* host,
-                        const HostStruct& hs, DeviceForm& out, uint64_t dev_off,
-                        std::vector<uint8_t>* buf) {
+/* A struct's members and isset bytes into its zero-filled slot dev. */
+template <bool Count>
+void writeStruct(const SchemaTables& sc, uint32_t si, const uint8_t* host, const HostStruct& hs,
+                 Sink& out, uint8_t* dev) {
   const tgpu_struct_desc& sd = sc.s[si];
   for (uint32_t k = 0; k < sd.num_fields && k < hs.fields.size(); ++k) {
     const tgpu_field_desc& f = sc.f[sd.first_field + k];
     const HostField& hf = hs.fields[k];
     if (!hf.type) continue;
     const uint8_t set = hf.isset >= 0 ? host[hf.isset] : 1;
-    (*buf)[dev_off + f.isset_offset] = set;
+    if (!Count) dev[f.isset_offset] = set;
     const void* h = host + hf.offset;
+    uint8_t* m = Count ? nullptr : dev + f.member_offset;
     if (isBoxed(f)) {  // the pointee into the list base; null stays {0, 0}
       const void* obj = hf.type->get(h);
       if (obj) {
-        const uint64_t o = out.alloc(sc.s[f.struct_index].size);
-        storeSpan(buf->data() + dev_off + f.member_offset, o, 1);
-        writeStruct(sc, (uint32_t)f.struct_index, (const uint8_t*)obj, *hf.type->st, out, o,
-                    &out.lists);
+        const uint32_t bs = sc.s[f.struct_index].size;
+        const uint64_t o = out.alloc(bs);
+        uint8_t* slot = nullptr;
+        if (!Count) {
+          storeSpan(m, o, 1);
+          slot = out.lists + o;
+          std::memset(slot, 0, bs);
+        }
+        writeStruct<Count>(sc, (uint32_t)f.struct_index, (const uint8_t*)obj, *hf.type->st, out,
+                           slot);
       }
-    } else if (isContainer(f.ttype))
-      writeContainer(sc, ctypeOf(f), h, *hf.type, out, buf, dev_off + f.member_offset);
-    else
-      writeValue(sc, f.ttype, f.struct_index, 0, h, *hf.type, out, buf,
-                 dev_off + f.member_offset);
-  }
-}
-
-// ---- spans of one thread's part moved to the merged buffers -------------------
-/* Adds sd to every string span and ld to every list / boxed span of a value
-   (the thread's records, and its part of the merged list buffer `lists`
-   whose contents it reaches through spans already moved by ld). */
-void rebaseStruct(const SchemaTables& sc, uint32_t si, uint8_t* obj, uint8_t* lists,
-                  uint64_t sd, uint64_t ld);
-void rebaseContainer(const SchemaTables& sc, const CType& c, uint8_t* p, uint8_t* lists,
-                     uint64_t sd, uint64_t ld);
-inline void rebaseSpan(uint8_t* p, uint64_t d) {
-  tgpu_span s = loadSpan(p);
-  if (s.length) {
-    s.offset += d;
-    std::memcpy(p, &s, sizeof(s));
-  }
-}
-inline void rebaseValue(const SchemaTables& sc, uint32_t t, int32_t si, uint32_t ti, uint8_t* p,
-                        uint8_t* lists, uint64_t sd, uint64_t ld) {
-  if (t == TGPU_T_STRING) rebaseSpan(p, sd);
-  else if (t == TGPU_T_STRUCT) rebaseStruct(sc, (uint32_t)si, p, lists, sd, ld);
-  else if (isContainer(t)) rebaseContainer(sc, ctypeNode(sc, ti), p, lists, sd, ld);
-}
-inline bool hasSpans(uint32_t t) {
-  return t == TGPU_T_STRING || t == TGPU_T_STRUCT || isContainer(t);
-}
-inline void rebaseContainer(const SchemaTables& sc, const CType& c, uint8_t* p, uint8_t* lists,
-                            uint64_t sd, uint64_t ld) {
-  rebaseSpan(p, ld);
-  const tgpu_span s = loadSpan(p);
-  const bool is_map = c.ttype == TGPU_T_MAP;
-  const uint32_t v = is_map ? c.val : c.elem;
-  if (!hasSpans(v) && !(is_map && hasSpans(c.elem))) return;
-  const int32_t ksi = is_map ? keyStruct(sc, c) : -1;
-  const uint32_t ks = is_map ? slotBytes(sc, c.elem, ksi) : 0;
-  const uint32_t es = ks + slotBytes(sc, v, c.si);
-  for (uint32_t i = 0; i < s.length; ++i) {
-    uint8_t* e = lists + s.offset + (uint64_t)i * es;
-    if (is_map) rebaseValue(sc, c.elem, ksi, keyNode(c), e, lists, sd, ld);
-    rebaseValue(sc, v, c.si, c.ti, e + ks, lists, sd, ld);
-  }
-}
-inline void rebaseStruct(const SchemaTables& sc, uint32_t si, uint8_t* obj, uint8_t* lists,
-                         uint64_t sd, uint64_t ld) {
-  const tgpu_struct_desc& d = sc.s[si];
-  for (uint32_t k = 0; k < d.num_fields; ++k) {
-    const tgpu_field_desc& f = sc.f[d.first_field + k];
-    uint8_t* m = obj + f.member_offset;
-    if (isBoxed(f)) {
-      rebaseSpan(m, ld);
-      const tgpu_span b = loadSpan(m);
-      if (b.length) rebaseStruct(sc, (uint32_t)f.struct_index, lists + b.offset, lists, sd, ld);
     } else if (isContainer(f.ttype)) {
-      rebaseContainer(sc, ctypeOf(f), m, lists, sd, ld);
+      writeContainer<Count>(sc, ctypeOf(f), h, *hf.type, out, m);
     } else {
-      rebaseValue(sc, f.ttype, f.struct_index, 0, m, lists, sd, ld);
+      writeValue<Count>(sc, f.ttype, f.struct_index, 0, h, *hf.type, out, m);
     }
   }
 }
@@ -468,79 +475,210 @@ inline unsigned materialize_threads() {
   return t;
 }
 
-namespace detail {
-/* fn(t, begin, end) over contiguous parts of [0, n) on up to T threads. */
-template <class F>
-void parallel_parts(uint64_t n, unsigned T, F&& fn) {
-  if (T <= 1 || n < 4096) {
-    fn(0u, (uint64_t)0, n);
-    return;
+/* A process-wide pool of materialize_threads() workers for the batch
+   materialization. Tasks belong to a Group; Group::wait() runs queued tasks
+   on the waiting thread as well until the group's last one is done, then
+   rethrows the first exception one of them threw (the reference's reader
+   throws into the caller, so a binding hook's exception must too). */
+class HostPool {
+ public:
+  class Group {
+   public:
+    Group() = default;
+    Group(const Group&) = delete;
+    ~Group() { instance().wait(*this, false); }
+    void run(std::function<void()> fn) { instance().submit(this, std::move(fn)); }
+    void wait() { instance().wait(*this, true); }
+
+   private:
+    friend class HostPool;
+    uint64_t pending = 0;  // guarded by the pool's mutex
+    std::exception_ptr err;
+  };
+  static HostPool& instance() {
+    static HostPool p(materialize_threads());
+    return p;
   }
-  std::vector<std::thread> th;
-  const uint64_t per = (n + T - 1) / T;
-  for (unsigned t = 0; t < T; ++t) {
-    const uint64_t b = std::min<uint64_t>(n, t * per), e = std::min<uint64_t>(n, b + per);
-    if (b < e) th.emplace_back([&fn, t, b, e] { fn(t, b, e); });
+  ~HostPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
   }
-  for (auto& x : th) x.join();
-}
-}  // namespace detail
+
+ private:
+  struct Task {
+    Group* g;
+    std::function<void()> fn;
+  };
+  explicit HostPool(unsigned n) {
+    for (unsigned i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
+  }
+  void submit(Group* g, std::function<void()> fn) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      ++g->pending;
+      q_.push_back(Task{g, std::move(fn)});
+    }
+    cv_.notify_one();
+  }
+  void execute(Task& t) {
+    std::exception_ptr e;
+    try {
+      t.fn();
+    } catch (...) {
+      e = std::current_exception();
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    if (e && !t.g->err) t.g->err = e;
+    if (--t.g->pending == 0) done_.notify_all();
+  }
+  void loop() {
+    for (;;) {
+      Task t;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        t = std::move(q_.front());
+        q_.pop_front();
+      }
+      execute(t);
+    }
+  }
+  void wait(Group& g, bool rethrow) {
+    std::unique_lock<std::mutex> lk(mu_);
+    while (g.pending) {
+      if (!q_.empty()) {  // help: run a queued task here
+        Task t = std::move(q_.front());
+        q_.pop_front();
+        lk.unlock();
+        execute(t);
+        lk.lock();
+        continue;
+      }
+      done_.wait(lk);
+    }
+    if (rethrow && g.err) {
+      std::exception_ptr e = g.err;
+      g.err = nullptr;
+      std::rethrow_exception(e);
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  std::deque<Task> q_;
+  std::vector<std::thread> workers_;
+  bool stop_ = false;
+};
+
+/* Records per materialization task: small enough that every worker has
+   work as soon as a chunk lands, large enough to keep the queue cheap. */
+constexpr uint64_t kMaterializeBlock = 8192;
 
 /* Decoded device-form records (host copies) -> host objects T (stride
-   sizeof(T), default-constructed by the caller); records are independent,
-   so contiguous parts go to materialize_threads() threads. */
+   sizeof(T), default-constructed by the caller), records [b, e) of the
+   batch, on the calling thread. */
+inline void materializeRange(const SchemaTables& sc, const uint8_t* records, uint64_t b,
+                             uint64_t e, uint32_t record_size, const uint8_t* strings,
+                             const uint8_t* arena, const HostStruct& hs, void* objects,
+                             size_t stride) {
+  const detail::Sources src{strings, arena};
+  for (uint64_t i = b; i < e; ++i)
+    detail::readStruct(sc, 0, records + i * record_size, src, hs, (uint8_t*)objects + i * stride);
+}
+
+/* The same for records [b, e), queued on the pool in blocks of
+   kMaterializeBlock records (records are independent). */
+inline void materializeAsync(HostPool::Group& g, const SchemaTables& sc, const uint8_t* records,
+                             uint64_t b, uint64_t e, uint32_t record_size, const uint8_t* strings,
+                             const uint8_t* arena, const HostStruct& hs, void* objects,
+                             size_t stride) {
+  for (uint64_t x = b; x < e; x += kMaterializeBlock) {
+    const uint64_t y = std::min(e, x + kMaterializeBlock);
+    g.run([=, &sc, &hs] {
+      materializeRange(sc, records, x, y, record_size, strings, arena, hs, objects, stride);
+    });
+  }
+}
+
+/* All n records, in parallel; returns when they are materialized. */
 inline void materialize(const SchemaTables& sc, const uint8_t* records, uint64_t n,
                         uint32_t record_size, const uint8_t* strings, const uint8_t* arena,
                         const HostStruct& hs, void* objects, size_t stride) {
-  const detail::Sources src{strings, arena};
-  detail::parallel_parts(n, materialize_threads(), [&](unsigned, uint64_t b, uint64_t e) {
-    for (uint64_t i = b; i < e; ++i)
-      detail::readStruct(sc, 0, records + i * record_size, src, hs,
-                         (uint8_t*)objects + i * stride);
-  });
+  HostPool::Group g;
+  materializeAsync(g, sc, records, 0, n, record_size, strings, arena, hs, objects, stride);
+  g.wait();
 }
 
-/* Host objects T -> the encode input (records + string base + list base).
-   Each thread writes its part's records in place and its strings / lists
-   into buffers of its own; the parts' buffers are then concatenated and
-   their spans moved by the part's base. */
-inline detail::DeviceForm dematerialize(const SchemaTables& sc, uint32_t record_size,
-                                        const void* objects, uint64_t n, size_t stride,
-                                        const HostStruct& hs) {
-  detail::DeviceForm out;
-  out.records.assign(n * record_size, 0);
-  const unsigned T = (n < 4096) ? 1u : materialize_threads();
-  std::vector<detail::DeviceForm> part(T);
-  std::vector<std::pair<uint64_t, uint64_t>> range(T, {0, 0});
-  detail::parallel_parts(n, T, [&](unsigned t, uint64_t b, uint64_t e) {
-    range[t] = {b, e};
-    detail::DeviceForm& f = T == 1 ? out : part[t];
-    for (uint64_t i = b; i < e; ++i)
-      detail::writeStruct(sc, 0, (const uint8_t*)objects + i * stride, hs, f, i * record_size,
-                          &out.records);
-  });
-  if (T == 1) return out;
-  std::vector<uint64_t> sbase(T), lbase(T);
-  uint64_t S = 0, L = 0;
-  for (unsigned t = 0; t < T; ++t) {
-    sbase[t] = S;
-    lbase[t] = L;
-    S += part[t].strings.size();
-    L = (L + part[t].lists.size() + 7) & ~7ull;
+/* String and list bytes of host objects [b, e) in the device form (the
+   sizing pass: strings packed, list arrays 8-byte aligned, from a base of
+   0 — the same bytes from any 8-aligned base). */
+inline std::pair<uint64_t, uint64_t> formBytes(const SchemaTables& sc, const void* objects,
+                                               uint64_t b, uint64_t e, size_t stride,
+                                               const HostStruct& hs) {
+  detail::Sink k;
+  for (uint64_t i = b; i < e; ++i)
+    detail::writeStruct<true>(sc, 0, (const uint8_t*)objects + i * stride, hs, k, nullptr);
+  return {k.spos, k.lpos};
+}
+
+/* Host objects [b, e) -> their device form: records at records[(i - b) * S]
+   (zero-filled here first), strings and list arrays through `sink`, whose
+   positions start at the part's base in the chunk's string / list base (from
+   formBytes; lpos 8-aligned). */
+inline void formWrite(const SchemaTables& sc, uint32_t record_size, const void* objects,
+                      uint64_t b, uint64_t e, size_t stride, const HostStruct& hs,
+                      uint8_t* records, detail::Sink sink) {
+  std::memset(records, 0, (e - b) * record_size);
+  for (uint64_t i = b; i < e; ++i)
+    detail::writeStruct<false>(sc, 0, (const uint8_t*)objects + i * stride, hs, sink,
+                               records + (i - b) * record_size);
+}
+
+/* The encode input of n host objects as owned buffers (records + string base
+   + list base), built in parallel parts (each part sized, then written at its
+   base). */
+struct DeviceForm {
+  std::vector<uint8_t> records, strings, lists;
+};
+inline DeviceForm dematerialize(const SchemaTables& sc, uint32_t record_size,
+                                const void* objects, uint64_t n, size_t stride,
+                                const HostStruct& hs) {
+  const uint64_t P = std::max<uint64_t>(1, std::min<uint64_t>(materialize_threads() * 4,
+                                                              n / 1024));
+  std::vector<std::pair<uint64_t, uint64_t>> sz(P);
+  auto part = [&](uint64_t t) { return std::make_pair(n * t / P, n * (t + 1) / P); };
+  {
+    HostPool::Group g;
+    for (uint64_t t = 0; t < P; ++t)
+      g.run([&, t] { sz[t] = formBytes(sc, objects, part(t).first, part(t).second, stride, hs); });
+    g.wait();
   }
+  std::vector<detail::Sink> at(P);
+  uint64_t S = 0, L = 0;
+  for (uint64_t t = 0; t < P; ++t) {
+    at[t].spos = S;
+    at[t].lpos = L;
+    S += sz[t].first;
+    L = (L + sz[t].second + 7) & ~7ull;
+  }
+  DeviceForm out;
+  out.records.resize(n * record_size);
   out.strings.resize(S);
   out.lists.resize(L);
-  // each part's thread copies its buffers into place and moves its spans
-  // (the part boundaries are the same as in the write above)
-  detail::parallel_parts(n, T, [&](unsigned t, uint64_t b, uint64_t e) {
-    if (!part[t].strings.empty())
-      std::memcpy(out.strings.data() + sbase[t], part[t].strings.data(), part[t].strings.size());
-    if (!part[t].lists.empty())
-      std::memcpy(out.lists.data() + lbase[t], part[t].lists.data(), part[t].lists.size());
-    for (uint64_t i = b; i < e; ++i)
-      detail::rebaseStruct(sc, 0, out.records.data() + i * record_size, out.lists.data(),
-                           sbase[t], lbase[t]);
-  });
+  HostPool::Group g;
+  for (uint64_t t = 0; t < P; ++t)
+    g.run([&, t] {
+      detail::Sink k = at[t];
+      k.strings = out.strings.data();
+      k.lists = out.lists.data();
+      formWrite(sc, record_size, objects, part(t).first, part(t).second, stride, hs,
+                out.records.data() + part(t).first * record_size, k);
+    });
+  g.wait();
   return out;
 }
 

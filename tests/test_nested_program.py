@@ -276,3 +276,48 @@ def test_nested_program_compiles_on_device(gpu, name):
 
     gs = GpuSchema(Schema.from_table(helpers.manifest()["schemas"][name]))
     assert gs.compile(0) and gs.compile(2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("protocol", [0, 2])
+def test_nested_program_large_root_record(gpu, protocol, monkeypatch):
+    """A flat schema of 44 optional string fields (a 720-byte root record:
+    44 spans + 44 isset bytes) has a nested program but no canonical one; at
+    64 Ki records (the compile threshold) its decode must not ask for a record
+    tile beyond the LDS: the record tile is dropped and records go straight to
+    HBM. Same records as the oracle, indexed and unindexed."""
+    import torch
+
+    import helpers
+    from fbthrift_amd import serializer as SZ
+
+    monkeypatch.setenv("TGPU_JIT", "1")
+    monkeypatch.setenv("TGPU_NESTED", "1")
+    nf, n = 44, 1 << 16
+    schema = Schema.from_table([[[k, T_STRING, 0, 1, -1] for k in range(1, nf + 1)]])
+    assert schema.size[0] >= 700
+    rng = np.random.default_rng(0x1a7e + protocol)
+    vals = {}
+    for k in range(nf):
+        present = rng.random(n) < 0.5
+        lens = np.where(present, rng.integers(0, 5, n), 0)
+        vals["%d.set" % k] = present.astype(np.uint8)
+        vals["%d.len" % k] = lens
+        vals["%d.data" % k] = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    rec, sarena, _ = helpers.pack(schema, vals, n)
+    rec = rec.view(np.uint8).reshape(-1)
+    ost, owire, ooffs = oracle.encode(schema, protocol, rec, n, sarena)
+    assert ost.code == 0
+    gs = SZ.GpuSchema(schema)
+    Ser = {0: SZ.BinarySerializer, 2: SZ.CompactSerializer}[protocol]
+    t = lambda a: torch.from_numpy(np.array(a, copy=True)).to(gpu)
+    wire, offs = Ser.serialize(gs, t(rec), n, t(sarena))
+    assert wire.cpu().numpy().tobytes() == owire
+    w = np.frombuffer(owire, np.uint8)
+    S = schema.size[0]
+    for indexed in (True, False):
+        grec, _, st, nd, cons = Ser.deserialize_status(gs, t(w), n, offs if indexed else None)
+        dst, drec, _, dnd, _ = oracle.decode(schema, protocol, owire, n,
+                                             offsets=ooffs if indexed else None)
+        assert st.code == 0 and nd == n and cons == len(owire), st.as_tuple()
+        assert np.array_equal(grec.cpu().numpy()[: n * S], drec[: n * S])

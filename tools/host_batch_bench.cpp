@@ -20,8 +20,10 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #define THRIFT_GPU_NO_ABORT 1
@@ -122,18 +124,43 @@ static Nested gen_nested(std::mt19937_64& r) {
 }
 
 // ---- the generated code's shape, one core -----------------------------------
+// An appender in the shape of folly's QueueAppender: a capacity check per
+// write, uninitialized storage grown geometrically.
 struct Out {
-  std::vector<uint8_t> b;
-  void u8(uint8_t v) { b.push_back(v); }
+  std::unique_ptr<uint8_t[]> buf;
+  size_t cap = 0, len = 0;
+  void reserve(size_t n) {
+    if (n <= cap) return;
+    std::unique_ptr<uint8_t[]> nb(new uint8_t[n]);
+    if (len) std::memcpy(nb.get(), buf.get(), len);
+    buf = std::move(nb);
+    cap = n;
+  }
+  uint8_t* room(size_t k) {
+    if (len + k > cap) reserve(std::max(2 * cap, len + k + (64 << 10)));
+    uint8_t* q = buf.get() + len;
+    len += k;
+    return q;
+  }
+  void u8(uint8_t v) { *room(1) = v; }
   void be(uint64_t v, int n) {
-    for (int k = n - 1; k >= 0; --k) b.push_back((uint8_t)(v >> (8 * k)));
+    uint8_t* q = room(n);
+    for (int k = 0; k < n; ++k) q[k] = (uint8_t)(v >> (8 * (n - 1 - k)));
   }
   void varint(uint64_t v) {
+    uint8_t* q = room(10);
+    int k = 0;
     while (v >= 0x80) {
-      b.push_back((uint8_t)(v | 0x80));
+      q[k++] = (uint8_t)(v | 0x80);
       v >>= 7;
     }
-    b.push_back((uint8_t)v);
+    q[k++] = (uint8_t)v;
+    len -= 10 - k;
+  }
+  void bytes(const std::string& s) { std::memcpy(room(s.size()), s.data(), s.size()); }
+  const uint8_t* data() const { return buf.get(); }
+  bool same(const std::vector<uint8_t>& b) const {
+    return len == b.size() && std::memcmp(buf.get(), b.data(), len) == 0;
   }
 };
 struct In {
@@ -175,7 +202,7 @@ static void write_mixed(Out& o, const Mixed& m) {  // Compact, fields 1..6 in or
   for (const std::string* s : {&m.e, &m.f}) {
     o.u8(0x18);
     o.varint(s->size());
-    o.b.insert(o.b.end(), s->begin(), s->end());
+    o.bytes(*s);
   }
   o.u8(0);
 }
@@ -256,21 +283,104 @@ static int run(int config, const GpuSchema& schema, const HostStruct& binding, u
       std::fprintf(stderr, "mismatch at record %llu\n", (unsigned long long)i);
       return 1;
     }
+  // the host side alone: materialize() of device-form records decoded once
+  // (the resident pass) into fresh objects, and the device pass alone
+  // (deserializeHostEx into pinned records / arena, nothing materialized)
+  double mat_ms = 1e30, dev_ms = 1e30;
+  {
+    const uint32_t S = schema.recordSize();
+    const uint64_t acap = bytes.size() * tgpu_schema_arena_scale(schema.get(), Ser::protocolType());
+    void *recs = nullptr, *ar = nullptr;
+    check(tgpu_host_alloc(n * S + 16, &recs), "tgpu_host_alloc");
+    check(tgpu_host_alloc(acap + 16, &ar), "tgpu_host_alloc");
+    for (int rep = 0; rep < reps; ++rep) {
+      auto t0 = Clock::now();
+      ser.deserializeHostEx(buf->data(), bytes.size(), n, recs, acap ? ar : nullptr, acap);
+      dev_ms = std::min(dev_ms, ms_since(t0));
+    }
+    for (int rep = 0; rep < reps; ++rep) {
+      back.assign(n, T{});
+      auto t0 = Clock::now();
+      materialize(schema.tables(), (const uint8_t*)recs, n, S, buf->data(), (const uint8_t*)ar,
+                  binding, back.data(), sizeof(T));
+      mat_ms = std::min(mat_ms, ms_since(t0));
+    }
+    tgpu_host_free(recs);
+    tgpu_host_free(ar);
+  }
   // the generated code's shape, one core (and its bytes must match)
   Out o;
-  o.b.reserve(wire);
+  o.reserve(wire);
   auto t0 = Clock::now();
   for (const T& x : src) write(o, x);
   const double cw = ms_since(t0);
-  if (o.b != bytes) {
+  if (!o.same(bytes)) {
     std::fprintf(stderr, "CPU writer bytes differ\n");
     return 1;
   }
   std::vector<T> cb(n);
+  std::vector<uint64_t> ends(n);
   t0 = Clock::now();
-  In in{o.b.data(), o.b.data() + o.b.size()};
-  for (uint64_t i = 0; i < n; ++i) read(in, cb[i]);
-  const double cr = ms_since(t0);
+  In in{o.data(), o.data() + o.len};
+  for (uint64_t i = 0; i < n; ++i) {
+    read(in, cb[i]);
+    ends[i] = (uint64_t)(in.p - o.data());
+  }
+  const double cr = ms_since(t0) ;
+  // the same reader / writer on materialize_threads() host threads, each on
+  // a contiguous record range: the writer's parts concatenated into one
+  // buffer (the copy timed too); the reader given every part's first record
+  // start (an index the reference's file loop does not have — its best case)
+  const unsigned TT = materialize_threads();
+  auto part = [&](unsigned t) { return std::make_pair(n * t / TT, n * (t + 1) / TT); };
+  double cwT = 1e30, crT = 1e30;
+  for (int rep = 0; rep < reps; ++rep) {
+    std::vector<Out> parts(TT);
+    std::unique_ptr<uint8_t[]> joined;
+    std::vector<uint64_t> base(TT + 1, 0);
+    auto t1 = Clock::now();
+    {
+      std::vector<std::thread> th;
+      for (unsigned t = 0; t < TT; ++t)
+        th.emplace_back([&, t] {
+          auto [b, e] = part(t);
+          parts[t].reserve((e - b) * (wire / n + 16));
+          for (uint64_t i = b; i < e; ++i) write(parts[t], src[i]);
+        });
+      for (auto& x : th) x.join();
+      for (unsigned t = 0; t < TT; ++t) base[t + 1] = base[t] + parts[t].len;
+      joined.reset(new uint8_t[base[TT]]);
+      th.clear();
+      for (unsigned t = 0; t < TT; ++t)
+        th.emplace_back([&, t] {
+          std::memcpy(joined.get() + base[t], parts[t].data(), parts[t].len);
+        });
+      for (auto& x : th) x.join();
+    }
+    cwT = std::min(cwT, ms_since(t1));
+    if (base[TT] != bytes.size() || std::memcmp(joined.get(), bytes.data(), bytes.size()) != 0) {
+      std::fprintf(stderr, "threaded CPU writer bytes differ\n");
+      return 1;
+    }
+    std::vector<T> cbT(n);
+    t1 = Clock::now();
+    {
+      std::vector<std::thread> th;
+      for (unsigned t = 0; t < TT; ++t)
+        th.emplace_back([&, t] {
+          auto [b, e] = part(t);
+          In pin{o.data() + (b ? ends[b - 1] : 0), o.data() + (e ? ends[e - 1] : 0)};
+          for (uint64_t i = b; i < e; ++i) read(pin, cbT[i]);
+        });
+      for (auto& x : th) x.join();
+    }
+    crT = std::min(crT, ms_since(t1));
+    for (uint64_t i = 0; i < n; i += 997)
+      if (!(cbT[i] == src[i])) {
+        std::fprintf(stderr, "threaded CPU reader mismatch at %llu\n", (unsigned long long)i);
+        return 1;
+      }
+  }
   const double gib = (double)wire / (1ull << 30);
   std::printf(
       "{\"config\": %d, \"records\": %llu, \"wire_bytes\": %llu, \"reps\": %d, "
@@ -278,10 +388,16 @@ static int run(int config, const GpuSchema& schema, const HostStruct& binding, u
       "\"serializeBatch_GiBps\": %.3f, \"deserializeBatch_GiBps\": %.3f, "
       "\"serializeBatch_ns_per_record\": %.2f, \"deserializeBatch_ns_per_record\": %.2f, "
       "\"cpu_generated_shape_1core\": {\"write_ms\": %.3f, \"read_ms\": %.3f, "
-      "\"write_GiBps\": %.3f, \"read_GiBps\": %.3f}, \"materialize_threads\": %u}\n",
+      "\"write_GiBps\": %.3f, \"read_GiBps\": %.3f}, "
+      "\"cpu_generated_shape_threads\": {\"threads\": %u, \"write_ms\": %.3f, "
+      "\"read_ms\": %.3f, \"write_GiBps\": %.3f, \"read_GiBps\": %.3f, "
+      "\"note\": \"reader given each thread's first record start\"}, "
+      "\"materialize_only_ms\": %.3f, \"device_pass_resident_ms\": %.3f, "
+      "\"materialize_threads\": %u}\n",
       config, (unsigned long long)n, (unsigned long long)wire, reps, ser_ms, de_ms,
       gib / (ser_ms / 1e3), gib / (de_ms / 1e3), ser_ms * 1e6 / n, de_ms * 1e6 / n, cw, cr,
-      gib / (cw / 1e3), gib / (cr / 1e3), materialize_threads());
+      gib / (cw / 1e3), gib / (cr / 1e3), TT, cwT, crT, gib / (cwT / 1e3), gib / (crT / 1e3),
+      mat_ms, dev_ms, materialize_threads());
   return 0;
 }
 
