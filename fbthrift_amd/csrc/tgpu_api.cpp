@@ -579,7 +579,10 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
   }
   for (uint32_t k = 0; k < sd.num_fields; ++k) {
     const tgpu_field_desc& f = sc.fields[sd.first_field + k];
-    const bool opt = nested && (f.qualifier == TGPU_OPTIONAL || un);
+    // a terse field reads like an optional one and is written unless empty
+    // (terse structs' emptiness rules stay with the general writer)
+    const bool terse = nested && f.qualifier == TGPU_TERSE && f.ttype != TGPU_T_STRUCT;
+    const bool opt = nested && (f.qualifier == TGPU_OPTIONAL || un || terse);
     if (f.qualifier != TGPU_UNQUALIFIED && f.qualifier != TGPU_REQUIRED && !opt) return false;
     const uint32_t member = base + f.member_offset, isset = base + f.isset_offset;
     if (member > 0xfffe || isset > 0xfffe) return false;
@@ -594,6 +597,7 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
       h.elem_ct = (uint8_t)(f.ttype == TGPU_T_BOOL ? 0 : compact_ctype(f.ttype));
       h.is_bool = f.ttype == TGPU_T_BOOL;
       h.width = opt ? 1 : 0;
+      h.elem_kind = terse ? 1 : 0;  // written when not empty (op::isEmpty), not by isset
       h.isset = (uint16_t)isset;
       if (!push_op(P, h)) return false;
       if (proto != TGPU_PROTOCOL_BINARY && f.ttype == TGPU_T_BOOL) {

@@ -175,7 +175,8 @@ enum VOpKind : uint8_t {
   // nested programs: a field header (member: the field id; hdr: its Binary
   // header; elem_ct: its Compact ctype; is_bool: a bool field; width 1: an
   // optional field, present when its header is next; isset: its isset
-  // byte; bits: the value ops that follow). Compact headers are deltas from
+  // byte; bits: the value ops that follow; elem_kind 1: a terse field, read
+  // like an optional one, written unless empty). Compact headers are deltas from
   // the struct's last field (VOP_SBEGIN's scope), so they are computed, not
   // constant, once fields may be absent.
   VOP_FHDR = 11,

@@ -132,11 +132,19 @@ void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t sto
         } else {
           hdr = "(o.put(" + std::to_string(v.hdr) + "u, 3), true)";
         }
-        if (!uvar.empty())
+        if (!uvar.empty()) {
           o << in << "if (!" << uvar << " && " << b << "[" << v.isset << "]) {\n"
             << in << "  " << uvar << " = true;\n";
-        else if (opt) o << in << "if (" << b << "[" << v.isset << "]) {\n";
-        else o << in << "{\n";
+        } else if (opt && v.elem_kind) {  // terse: written unless empty
+          const VOp& val = P.ops[k + 1];
+          const uint32_t w = (val.kind == VOP_FIXED || val.kind == VOP_VARINT) ? val.width
+                             : val.kind == VOP_CBOOL ? 1u : 0u;  // 0: a span (string, container)
+          o << in << "if (!terse_leaf_empty(" << b << " + " << val.member << "u, " << w << "u)) {\n";
+        } else if (opt) {
+          o << in << "if (" << b << "[" << v.isset << "]) {\n";
+        } else {
+          o << in << "{\n";
+        }
         o << in << "  if (!" << hdr << ") return false;\n";
         if (!cbool) gen_code(o, P, k + 1, vend, b, indent + 2, enc, last, meas);
         o << in << "}\n";

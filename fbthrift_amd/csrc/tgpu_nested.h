@@ -665,6 +665,15 @@ __device__ __forceinline__ bool put_cbool_field(O& o, int32_t id, int32_t& last,
   return true;
 }
 
+// op::isEmpty of a terse member (Clear.h:98-127): a scalar of w bytes all
+// zero bits (-0.0 is not empty), a string / container (w 0) of length 0.
+__device__ __forceinline__ bool terse_leaf_empty(const uint8_t* m, uint32_t w) {
+  if (!w) return ((const tgpu_span*)m)->length == 0;
+  uint32_t any = 0;
+  for (uint32_t b = 0; b < w; ++b) any |= m[b];
+  return any == 0;
+}
+
 // VOP_SEQ: the header; the caller loops over the elements of the span
 __device__ __forceinline__ tgpu_span seq_span(const VOp op, const uint8_t* base) {
   return *(const tgpu_span*)(base + op.member);

@@ -65,13 +65,19 @@ def test_oracle_terse_bytes():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("protocol", [0, 2])
-def test_gpu_terse_matches_oracle(gpu, protocol):
+@pytest.mark.parametrize("jit", ["0", "1"])
+def test_gpu_terse_matches_oracle(gpu, protocol, jit, monkeypatch):
+    """jit 1: the nested record program (terse fields read like optional
+    ones, written unless empty; tgpu_nested.h); 0: the general kernels."""
     import torch
 
     from fbthrift_amd.serializer import BinarySerializer, CompactSerializer, GpuSchema
 
+    monkeypatch.setenv("TGPU_JIT", jit)
     S = BinarySerializer if protocol == 0 else CompactSerializer
     schema = Schema.from_table(TABLE)
+    if jit == "1":
+        assert GpuSchema(schema).compile(protocol)
     rng = np.random.default_rng(7)
     rows = []
     for i in range(20_000):

@@ -113,10 +113,11 @@ def main_config(root, config, out_path=None, nested=False):
            "calibration": {"bytes": CALIB_BYTES, "fetch_factor": round(ff, 4),
                            "write_factor": round(wf, 4)},
            "bench_value": line["value"], "bench_unit": line["unit"]}
+    keep = {k for ks, _ in calls.values() for k in ks.split("+")}
     for k in sorted(set(fetch) & set(write)):
         fb = avg(fetch[k]) * 1024 * ff
         wb = avg(write[k]) * 1024 * wf
-        if fb + wb < 4 * n and k not in algo:  # bookkeeping kernels: skip
+        if fb + wb < 4 * n and k not in algo and k not in keep:  # bookkeeping kernels: skip
             continue
         if k.startswith(("gen_", "elementwise", "vectorized", "unrolled", "copy")):
             continue  # data generation / torch checks, not the codec
