@@ -562,6 +562,21 @@ bool emit_container(const tgpu_schema& sc, uint32_t ttype, uint32_t et, uint32_t
                     uint32_t eti, uint32_t ki, uint32_t member, uint32_t isset, int proto,
                     VProgram& P, uint32_t depth, uint32_t* max_depth);
 
+// The structs whose ops are being emitted (nested programs): a struct that
+// contains itself (a recursive schema, through a container or a boxed field)
+// has no finite straight-line program; it stays with the general kernels.
+thread_local std::vector<uint32_t> t_open_structs;
+struct OpenStruct {
+  bool ok;
+  explicit OpenStruct(uint32_t si) {
+    ok = std::find(t_open_structs.begin(), t_open_structs.end(), si) == t_open_structs.end();
+    if (ok) t_open_structs.push_back(si);
+  }
+  ~OpenStruct() {
+    if (ok) t_open_structs.pop_back();
+  }
+};
+
 // nested (build_nested_program): lists / sets of structs or of scalar lists
 // become VOP_SEQ loops whose bodies address the element slot (base 0);
 // `depth` tracks the container nesting for the height check.
@@ -570,6 +585,8 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
   const tgpu_struct_desc& sd = sc.structs[si];
   const bool un = (sd.flags & TGPU_STRUCT_UNION) != 0;
   if (un && !nested) return false;
+  const OpenStruct open(si);
+  if (nested && !open.ok) return false;  // recursive: the general kernels
   int32_t prev = 0;
   const uint32_t sbegin = P.n_ops;
   if (nested) {
@@ -582,8 +599,14 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
     // a terse field reads like an optional one and is written unless empty
     // (terse structs' emptiness rules stay with the general writer)
     const bool terse = nested && f.qualifier == TGPU_TERSE && f.ttype != TGPU_T_STRUCT;
-    const bool opt = nested && (f.qualifier == TGPU_OPTIONAL || un || terse);
-    if (f.qualifier != TGPU_UNQUALIFIED && f.qualifier != TGPU_REQUIRED && !opt) return false;
+    // a boxed struct field: the object in the record's region (VOP_BOX);
+    // optional boxed ones read / written like optional fields
+    const bool box = nested && f.ttype == TGPU_T_STRUCT &&
+                     (f.qualifier == TGPU_BOXED || f.qualifier == TGPU_OPTIONAL_BOXED);
+    const bool opt = nested && (f.qualifier == TGPU_OPTIONAL || un || terse ||
+                                (box && f.qualifier == TGPU_OPTIONAL_BOXED));
+    if (f.qualifier != TGPU_UNQUALIFIED && f.qualifier != TGPU_REQUIRED && !opt && !box)
+      return false;
     const uint32_t member = base + f.member_offset, isset = base + f.isset_offset;
     if (member > 0xfffe || isset > 0xfffe) return false;
     const uint32_t fhdr = P.n_ops;
@@ -681,6 +704,19 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
       P.has_list = 1;
       if (max_depth) *max_depth = std::max(*max_depth, depth + 1);
       if (!push_op(P, v)) return false;
+    } else if (box) {
+      VOp bx = make_op(VOP_BOX);
+      bx.member = (uint16_t)member;
+      bx.hdr = sc.structs[f.struct_index].size;
+      const uint32_t at = P.n_ops;
+      if (!push_op(P, bx) ||
+          !emit_program(sc, (uint32_t)f.struct_index, 0, proto, P, true, depth, max_depth) ||
+          !push_op(P, make_op(VOP_BOX_END)))
+        return false;
+      P.ops[at].hdr_len = (uint8_t)P.n_ops;  // one past the VOP_BOX_END
+      VOp is = make_op(VOP_ISSET);
+      is.isset = (uint16_t)isset;
+      if (!push_op(P, is)) return false;
     } else if (f.ttype == TGPU_T_STRUCT) {
       if (!emit_program(sc, (uint32_t)f.struct_index, member, proto, P, nested, depth, max_depth))
         return false;
@@ -705,15 +741,17 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
   return true;
 }
 
-// A leaf value op at member: a scalar (no bools: their Compact container
-// form differs) or a string view.
+// A leaf value op at member: a scalar or a string view. A bool here is a
+// container's (a map key / value): one byte, Binary 0 / 1, Compact 1 / 2
+// (CompactProtocol-inl.h:692-701: byte == 1 is true).
 bool emit_leaf(uint32_t t, uint32_t member, int proto, VProgram& P) {
   VOp v = make_op(VOP_FIXED);
   v.member = (uint16_t)member;
   if (t == TGPU_T_STRING) {
     v.kind = VOP_STRING;
-  } else if (is_scalar(t) && t != TGPU_T_BOOL) {
+  } else if (is_scalar(t)) {
     v.width = (uint8_t)scalar_size(t);
+    v.is_bool = t == TGPU_T_BOOL;
     if (proto == TGPU_PROTOCOL_COMPACT && (t == TGPU_T_I16 || t == TGPU_T_I32 || t == TGPU_T_I64)) {
       v.kind = VOP_VARINT;
       v.bits = t == TGPU_T_I64 ? 64 : 32;
@@ -796,20 +834,40 @@ bool emit_container(const tgpu_schema& sc, uint32_t ttype, uint32_t et, uint32_t
     P.has_list = 1;
     return true;
   }
-  if (ttype != TGPU_T_MAP || ki != 0) return false;  // struct / container keys: general
-  if (!(et == TGPU_T_STRING || (is_scalar(et) && et != TGPU_T_BOOL)) || vt == TGPU_T_BOOL)
+  if (ttype != TGPU_T_MAP) return false;
+  // the key: a scalar or string leaf, or (key_index) a struct / container
+  // key, whose node names its struct or is the key container's node
+  int32_t ksi = -1;
+  uint32_t kti = 0;
+  if (ki) {
+    if (ki > sc.types.size()) return false;
+    const tgpu_type_desc& kn = sc.types[ki - 1];
+    if (et == TGPU_T_STRUCT) {
+      if (kn.ttype != TGPU_T_STRUCT) return false;
+      ksi = kn.struct_index;
+    } else if (et == TGPU_T_LIST || et == TGPU_T_SET || et == TGPU_T_MAP) {
+      kti = ki;
+    } else {
+      return false;
+    }
+  } else if (!(et == TGPU_T_STRING || is_scalar(et))) {
     return false;
+  }
+  const uint32_t ks = slot_bytes(sc, et, ksi);
+  if (!ks || ks > 255) return false;
   VOp q = make_op(VOP_MSEQ);
   q.member = (uint16_t)member;
   q.isset = (uint16_t)isset;
   q.width = (uint8_t)et;            // key ttype
-  q.bits = (uint8_t)slot_bytes(sc, et, -1);  // key slot bytes
+  q.bits = (uint8_t)ks;             // key slot bytes
   q.elem_ttype = (uint8_t)vt;       // value ttype
   q.elem_ct = (uint8_t)((compact_ctype(et) << 4) | compact_ctype(vt));
   const uint32_t vs = slot_bytes(sc, vt, esi);
   q.hdr = q.bits + vs;
   const uint32_t at = P.n_ops;
-  if (!vs || !push_op(P, q) || !emit_leaf(et, 0, proto, P) ||
+  if (!vs || !push_op(P, q) ||
+      !(ki ? emit_value(sc, et, ksi, kti, 0, proto, P, d, max_depth)
+           : emit_leaf(et, 0, proto, P)) ||
       !emit_value(sc, vt, esi, eti, q.bits, proto, P, d, max_depth) ||
       !push_op(P, make_op(VOP_SEQ_END)))
     return false;
@@ -826,6 +884,7 @@ bool build_nested_program(const tgpu_schema& sc, int proto, VProgram& P, uint32_
   P.protocol = (uint32_t)proto;
   P.rec_size = sc.structs[0].size;
   depth = 0;
+  t_open_structs.clear();
   return emit_program(sc, 0, 0, proto, P, true, 0, &depth);
 }
 

@@ -183,6 +183,11 @@ enum VOpKind : uint8_t {
   VOP_SBEGIN = 12,  // a struct's fields begin (hdr_len: one past its VOP_SEND;
                     // width 1: a union — one member at most, its FHDRs optional)
   VOP_SEND = 13,    // its STOP
+  // a boxed struct field (cpp.ref / thrift.box): the object (hdr bytes) from
+  // the record's region, read / written by the body ops (members relative to
+  // it) up to its VOP_BOX_END (hdr_len: one past it); member: the field's span
+  VOP_BOX = 14,
+  VOP_BOX_END = 15,
 };
 enum VElemKind : uint8_t {
   VEL_FIXED = 1,   // big-endian fixed width (Binary ints, doubles/floats, bytes)
@@ -201,7 +206,8 @@ struct VOp {
   uint8_t elem_kind;  // LIST
   uint8_t elem_ttype; // LIST: TType of the elements (wire element type)
   uint8_t elem_ct;    // LIST: Compact element ctype
-  uint8_t is_bool;    // FIXED: Binary bool (byte must be 0/1)
+  uint8_t is_bool;    // FIXED: a bool (Binary: byte must be 0/1; Compact, a
+                      // container element / key / value: byte == 1)
 };
 // CONST op flag (elem_kind): the root record's STOP, before which fields with
 // ids above the schema's (member = the root's largest id; hdr bits 8..23 =

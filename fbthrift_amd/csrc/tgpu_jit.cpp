@@ -196,7 +196,8 @@ void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t sto
           << "u;\n";
         // (a struct element / value is default-constructed first; every
         // other slot is written whole)
-        if (v.elem_ttype == TGPU_T_STRUCT && !meas)
+        if ((v.elem_ttype == TGPU_T_STRUCT || (v.kind == VOP_MSEQ && v.width == TGPU_T_STRUCT)) &&
+            !meas)
           o << in << "    zero_slot<" << v.hdr << "u>(" << e << ");\n";
       }
       gen_code(o, P, k + 1, v.hdr_len - 1, e, indent + 4, enc, last, meas);
@@ -206,7 +207,38 @@ void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t sto
       k = v.hdr_len;  // past the VOP_SEQ_END
       continue;
     }
-    if (v.kind == VOP_SEQ_END || v.kind == VOP_SEND) {
+    if (v.kind == VOP_BOX) {
+      // a boxed struct field: its object from the record's region, zeroed
+      // (make_mutable_smart_ptr), read, then the member points to it
+      // (deserialize_field.whisker:21-23,49-51); written from its object, or
+      // as an empty struct when null (serialize_field.whisker:44-49)
+      const std::string x = "x" + K, s = "s" + K;
+      o << in << "{\n";
+      if (enc) {
+        o << in << "  const tgpu_span " << s << " = *(const tgpu_span*)(" << b << " + " << v.member
+          << "u);\n"
+          << in << "  if (" << s << ".length == 0) {\n"
+          << in << "    o.put(0, 1);\n"
+          << in << "  } else {\n"
+          << in << "    const uint8_t* " << x << " = lbase + " << s << ".offset;\n";
+        gen_code(o, P, k + 1, v.hdr_len - 1, x, indent + 4, enc, last, meas);
+        o << in << "  }\n";
+      } else if (meas) {
+        gen_code(o, P, k + 1, v.hdr_len - 1, b, indent + 2, enc, last, meas);
+      } else {
+        o << in << "  uint64_t a" << K << ";\n"
+          << in << "  uint8_t* " << x << ";\n"
+          << in << "  if (!box_open<" << v.hdr << "u>(c, bump, a" << K << ", " << x
+          << ")) return false;\n";
+        gen_code(o, P, k + 1, v.hdr_len - 1, x, indent + 2, enc, last, meas);
+        o << in << "  *(tgpu_span*)(" << b << " + " << v.member << "u) = tgpu_span{a" << K
+          << ", 1u, 0u};\n";
+      }
+      o << in << "}\n";
+      k = v.hdr_len;  // past the VOP_BOX_END
+      continue;
+    }
+    if (v.kind == VOP_SEQ_END || v.kind == VOP_SEND || v.kind == VOP_BOX_END) {
       ++k;
       continue;
     }

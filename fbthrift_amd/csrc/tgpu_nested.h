@@ -220,6 +220,20 @@ __device__ __forceinline__ void zero_slot(uint8_t* el) {
   }
 }
 
+// VOP_BOX: a boxed struct field's object (SZ bytes) from the record's region
+// (Arena::alloc at the struct's start, as the general reader allocates it),
+// default-constructed; the caller reads it, then points the member to it.
+template <uint32_t SZ>
+__device__ __forceinline__ bool box_open(const Ctx& c, uint64_t& bump, uint64_t& aoff,
+                                         uint8_t*& obj) {
+  if (!c.arena || c.pos_scale) return false;
+  aoff = region_alloc(bump, SZ);
+  if (aoff + SZ > c.arena_cap) return false;
+  obj = c.arena + aoff;
+  zero_slot<SZ>(obj);
+  return true;
+}
+
 // VOP_LIST of a nested program: scalar elements into the region (read_list,
 // tgpu_device.h: allocated only when n > 0), span at base + member.
 template <bool kStore = true, class Src>

@@ -390,8 +390,11 @@ __device__ __forceinline__ bool run_op(const VOp op, const bool compact, const S
     }
     case VOP_FIXED: {
       if (p + op.width > end) return false;
-      const uint64_t v = bswap_n(W.at(src, p, op.width), op.width);
-      if (op.is_bool && v > 1) return false;  // readBool throws: general path
+      uint64_t v = bswap_n(W.at(src, p, op.width), op.width);
+      // a bool: Binary readBool throws on a byte >= 2 (general path); a
+      // Compact container bool is byte == 1 (nested programs' map keys / values)
+      if (op.is_bool && !compact && v > 1) return false;
+      if (op.is_bool && compact) v = v == 1;
       if (kStore) store_n(rec + op.member, v, op.width);
       p += op.width;
       break;
@@ -571,7 +574,7 @@ __device__ __forceinline__ bool measure_lds(const PP& P, const uint32_t* w32, ui
       }
       case VOP_FIXED: {
         const uint64_t v = bswap_n(rdv(op.width), op.width);
-        ok &= p + op.width <= end && !(op.is_bool && v > 1);
+        ok &= p + op.width <= end && !(op.is_bool && !compact && v > 1);
         p += op.width;
         break;
       }

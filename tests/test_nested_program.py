@@ -7,8 +7,7 @@ every record off the canonical form to the general decoder.
 
 CPU: the nested programs of the bench schema (tests/../bench.py NESTED_TABLE:
 {i64, list<Item>, list<list<i32>>}) and of maps / string elements compile for
-gfx950 in both protocols; schemas it does not cover (struct keys, bools
-inside maps, optional fields) have none. GPU: 40 Ki records of that schema against the oracle's decode of
+gfx950 in both protocols; recursive schemas have none. GPU: 40 Ki records of that schema against the oracle's decode of
 the same stream, and the nested kernel against the general decoder
 (TGPU_NESTED=0) bit for bit, incl. records and arena bytes; the golden nested
 cases under TGPU_JIT=1 are in test_nested_containers.py."""
@@ -30,14 +29,18 @@ def test_nested_program_compiles(protocol):
 
 
 def test_nested_program_scope():
-    # map<Item, i32> (a struct key): no nested program (general reader)
+    # map<Item, i32> (a struct key) and list<map<i32, bool>> (bools inside
+    # maps): one each since round 4 (tests/test_nested_shapes.py)
     skey = [[[1, T_MAP, T_STRUCT, 0, -1, T_I32, None, [T_STRUCT, 0, 0, 1]]],
             [[1, T_I32, 0, 0, -1]]]
-    rc, _ = compile_check(Schema.from_table(skey), 0)
-    assert rc == 22
-    # list<map<i32, bool>>: none either (bools inside maps)
+    rc, log = compile_check(Schema.from_table(skey), 0)
+    assert rc == 0, log
     mbool = [[[1, T_LIST, T_MAP, 0, -1, 0, [T_MAP, T_I32, T_BOOL, -1]]]]
-    rc, _ = compile_check(Schema.from_table(mbool), 2)
+    rc, log = compile_check(Schema.from_table(mbool), 2)
+    assert rc == 0, log
+    # struct Tree {1: list<Tree> kids} (recursive): none (general reader)
+    tree = [[[1, T_LIST, T_STRUCT, 0, 0]]]
+    rc, _ = compile_check(Schema.from_table(tree), 0)
     assert rc == 22
     # map<i32, Item>, map<string, list<string>>, list<map<i32, string>>: one each
     for t in ([[[1, T_MAP, T_I32, 0, 1, T_STRUCT]], [[1, T_I32, 0, 0, -1]]],

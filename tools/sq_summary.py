@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-kernel averages of the SQ counters collected by tools/pmc_sq.sh.
+"""Per-kernel averages of the SQ counters collected by tools/profile_round.sh.
 usage: sq_summary.py DIR   (DIR/p*/**/*counter_collection*.csv)"""
 import csv
 import glob
