@@ -909,9 +909,10 @@ def irregular(wl, dev, reps=3):
     fields 1 and 2 swapped, (ii) every record carrying an extra unknown i32
     field (a newer writer's schema; 96 bytes per record). Blocking decodes
     (tgpu_decode_batch: plan kernel, then the parallel index + decode of the
-    tail), timed with HIP events around the call, each checked against the
-    records; reported beside the indexed program decode of the canonical
-    stream (offsets given) and the plan decode."""
+    tail) and stream-ordered ones (no host status: the strided tail decode,
+    then the finish kernel), timed with HIP events around the call, each
+    checked against the records; reported beside the indexed program decode
+    of the canonical stream (offsets given) and the plan decode."""
     import torch
 
     n, L = wl.n, wl.L
@@ -930,7 +931,7 @@ def irregular(wl, dev, reps=3):
     every = ex.view(-1)
     res = {"records": n}
 
-    def timed(name, wire, offsets=None, bytes_=None):
+    def timed(name, wire, offsets=None, sync=True):
         print("irregular %s: start" % name, file=sys.stderr, flush=True)
         best = None
         for _ in range(reps + 1):
@@ -939,11 +940,18 @@ def irregular(wl, dev, reps=3):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             t0 = time.perf_counter()
             e0.record()
-            _, _, consumed = wl.S.deserialize(wl.gs, wire, n, offsets=offsets, records=wl.back)
+            if sync:
+                _, _, consumed = wl.S.deserialize(wl.gs, wire, n, offsets=offsets, records=wl.back)
+            else:  # stream-ordered: no host status inside the call
+                wl.S.deserialize(wl.gs, wire, n, offsets=offsets, records=wl.back, sync=False)
             e1.record()
             torch.cuda.synchronize()
             wall = time.perf_counter() - t0
             ms = e0.elapsed_time(e1)
+            if not sync:
+                st, _, consumed = wl.S.context().wait()
+                if st.code:
+                    raise RuntimeError("irregular decode %s: %s" % (name, st.as_tuple()))
             if consumed != wire.numel() or not torch.equal(wl.back, wl.recs):
                 raise RuntimeError("irregular decode %s differs" % name)
             if best is None or ms < best[0]:
@@ -956,8 +964,12 @@ def irregular(wl, dev, reps=3):
     timed("indexed_program_decode_canonical", canon, offs)
     timed("first_record_reordered", first)
     timed("every_record_extra_field", every)
+    timed("async_plan_decode_canonical", canon, sync=False)
+    timed("async_first_record_reordered", first, sync=False)
+    timed("async_every_record_extra_field", every, sync=False)
     base = res["indexed_program_decode_canonical"]["ms"]
-    for k in ("first_record_reordered", "every_record_extra_field"):
+    for k in ("first_record_reordered", "every_record_extra_field",
+              "async_first_record_reordered", "async_every_record_extra_field"):
         res[k]["x_indexed_program_decode"] = round(res[k]["ms"] / base, 2)
     del first, ex, every, offs
     return res

@@ -36,6 +36,10 @@ __global__ void result_init_kernel(DevResult* res, uint64_t n) {
   res->n_deep = 0;
   res->n_deep_chunks = 0;
   res->first_misfit = kNone;
+  res->tail_first = kNone;
+  res->tail_pos = 0;
+  res->tail_stride = 0;
+  res->tail_min = kNone;
 }
 
 // Parses record i (record buffer zeroed first); lane: deep-pass lane or -1.
@@ -141,29 +145,66 @@ __global__ void fixed_exception_resolve_kernel(DevResult* res, uint64_t cap) {
   res->first_misfit = kNone;
 }
 
-// Record 0 of a fixed-stride batch read at 0: first_misfit = 0 unless it is
-// exactly L bytes (the plan kernel's work is wasted on a stream whose stride
-// is not L, e.g. every record carrying a field the schema does not know).
+// Stream-ordered form of the resolve step: then, when record m =
+// first_irregular is off the stride (or the list overflowed), record m's
+// length L2 by the general reader at m * L. A stream whose records all carry
+// the same appended fields from m on continues at stride L2 — the strided tail
+// decode takes it in parallel; no usable L2 (m fails, or L2 > max_stride, the
+// tail decode's tile) leaves the walk from m to the finish kernel.
 template <int P>
-__global__ void fixed_probe_kernel(DecodeArgs a, uint64_t L) {
+__global__ void fixed_tail_setup_kernel(DecodeArgs a, uint64_t cap, uint64_t L,
+                                        uint64_t max_stride) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const Reader r = decode_record<P>(a, 0, -1, 0);
-  a.res->first_misfit = (r.ok() && r.pos == L) ? kNone : 0;
-  a.res->total_bytes = r.ok() ? r.pos : 0;  // record 0's length (the caller's second stride)
+  DevResult* res = a.res;
+  if (res->n_irregular <= cap) res->first_irregular = res->first_misfit;
+  res->n_irregular = 0;
+  res->first_misfit = kNone;
+  const uint64_t m = res->first_irregular;
+  if (m >= a.n || !max_stride) return;
+  const uint64_t p0 = m * L;
+  const Reader r = decode_record<P>(a, m, -1, p0);
+  if (!r.ok() || r.pos <= p0 || r.pos - p0 > max_stride) return;
+  res->tail_first = m;
+  res->tail_pos = p0;
+  res->tail_min = kNone;
+  res->tail_stride = r.pos - p0;
 }
 
-// Unindexed streams the fixed-layout path cannot take: one lane reads the
-// records back to back exactly like repeated deserialize<T>(Cursor&)
-// (Serializer.h:97-100) and records each start offset. Serial by nature;
-// used from the first non-canonical record of a fixed-layout batch and for
-// unindexed variable-length streams.
+// Stream-ordered fixed-layout calls, last step (one workgroup): the strided
+// tail decode's exception records read by the general reader at their stride
+// positions (one not exactly L2 long, or failing, is a misfit; an overflowed
+// list leaves tail_min), then one lane walks record boundaries from the first
+// record off the strides — the reference's sequential deserialize<T>(Cursor&)
+// loop (Serializer.h:97-100) — writing offs. Without a strided tail the walk
+// starts at first_irregular.
 template <int P>
-__global__ void serial_decode_kernel(DecodeArgs a, int from_irregular, uint64_t fixed_len) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const uint64_t first = from_irregular ? a.res->first_irregular : 0;
+__global__ __launch_bounds__(256) void fixed_stream_finish_kernel(DecodeArgs a, uint64_t cap,
+                                                                  uint64_t L) {
+  __shared__ unsigned long long from_s;
+  DevResult* res = a.res;
+  const uint64_t L2 = res->tail_stride, m = res->tail_first, p0 = res->tail_pos;
+  if (threadIdx.x == 0) from_s = L2 ? kNone : res->first_irregular;
+  __syncthreads();
+  if (L2) {
+    const unsigned long long cnt = res->n_irregular;
+    if (cnt > cap) {
+      if (threadIdx.x == 0) from_s = res->tail_min;
+    } else {
+      for (uint64_t k = threadIdx.x; k < cnt; k += blockDim.x) {
+        const uint64_t i = a.exc[k];
+        if (i >= a.n) continue;
+        const uint64_t at = p0 + (i - m) * L2;
+        const Reader r = decode_record<P>(a, i, -1, at);
+        if (!r.ok() || r.pos != at + L2) atomicMin(&from_s, (unsigned long long)i);
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const uint64_t first = from_s;
   if (first >= a.n) return;
   uint64_t* offs = const_cast<uint64_t*>(a.offs);
-  uint64_t pos = first * fixed_len;
+  uint64_t pos = L2 ? p0 + (first - m) * L2 : first * L;
   for (uint64_t i = first; i < a.n; ++i) {
     offs[i] = pos;
     const Reader r = decode_one<P>(a, i);
@@ -174,6 +215,17 @@ __global__ void serial_decode_kernel(DecodeArgs a, int from_irregular, uint64_t 
     pos = r.pos;
   }
   offs[a.n] = pos;
+}
+
+// Record 0 of a fixed-stride batch read at 0: first_misfit = 0 unless it is
+// exactly L bytes (the plan kernel's work is wasted on a stream whose stride
+// is not L, e.g. every record carrying a field the schema does not know).
+template <int P>
+__global__ void fixed_probe_kernel(DecodeArgs a, uint64_t L) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const Reader r = decode_record<P>(a, 0, -1, 0);
+  a.res->first_misfit = (r.ok() && r.pos == L) ? kNone : 0;
+  a.res->total_bytes = r.ok() ? r.pos : 0;  // record 0's length (the caller's second stride)
 }
 
 template <int P>
@@ -437,13 +489,6 @@ hipError_t launch_general_decode(const DecodeArgs& a, int protocol, hipStream_t 
   return hipGetLastError();
 }
 
-hipError_t launch_serial_decode(const DecodeArgs& a, int protocol, bool from_irregular,
-                                uint64_t fixed_len, hipStream_t stream) {
-  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(serial_decode_kernel<P_>, dim3(1), dim3(64), 0, stream, a,
-                       (int)from_irregular, fixed_len));
-  return hipGetLastError();
-}
-
 hipError_t launch_fixed_exceptions(const DecodeArgs& a, int protocol, uint64_t L,
                                    hipStream_t stream) {
   // a small grid striding over the list: usually empty, and a launch of
@@ -453,6 +498,24 @@ hipError_t launch_fixed_exceptions(const DecodeArgs& a, int protocol, uint64_t L
   TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(fixed_exception_kernel<P_>, dim3(g ? g : 1),
                                                 dim3(256), 0, stream, a, L));
   hipLaunchKernelGGL(fixed_exception_resolve_kernel, dim3(1), dim3(1), 0, stream, a.res, a.exc_cap);
+  return hipGetLastError();
+}
+
+hipError_t launch_fixed_exceptions_stream(const DecodeArgs& a, int protocol, uint64_t L,
+                                          uint64_t max_stride, hipStream_t stream) {
+  const uint64_t most = a.exc_cap < a.n ? a.exc_cap : a.n;
+  const uint32_t g = (uint32_t)std::min<uint64_t>((most + 255) / 256, 256);
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(fixed_exception_kernel<P_>, dim3(g ? g : 1),
+                                                dim3(256), 0, stream, a, L));
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(fixed_tail_setup_kernel<P_>, dim3(1), dim3(64), 0,
+                                                stream, a, a.exc_cap, L, max_stride));
+  return hipGetLastError();
+}
+
+hipError_t launch_fixed_stream_finish(const DecodeArgs& a, int protocol, uint64_t L,
+                                      hipStream_t stream) {
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(fixed_stream_finish_kernel<P_>, dim3(1), dim3(256),
+                                                0, stream, a, a.exc_cap, L));
   return hipGetLastError();
 }
 

@@ -86,7 +86,12 @@ __device__ __attribute__((noinline)) void note_word_exception(uint64_t i, uint32
                                                               uint64_t* exc, uint64_t cap) {
   const uint32_t bit = 1u << (r & 31);
   if (atomicOr(&seen[r >> 5], bit) & bit) return;
-  atomicMin(&res->first_irregular, (unsigned long long)i);
+  // a stream off the stride from early on fails every record: skip the
+  // atomics a lower first record or an overflowed list make moot (the
+  // relaxed loads may be stale, which only costs an atomic)
+  if (i < __hip_atomic_load(&res->first_irregular, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicMin(&res->first_irregular, (unsigned long long)i);
+  if (__hip_atomic_load(&res->n_irregular, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > cap) return;
   const unsigned long long k = atomicAdd(&res->n_irregular, 1ull);
   if (k < cap) exc[k] = i;
 }
@@ -306,6 +311,119 @@ __global__ __launch_bounds__(T) void plan_binary_encode_kernel(
   }
 }
 
+// Encode, gather form: the record tile goes HBM -> LDS by LDS DMA; each lane
+// then produces whole 16-byte vectors of the tile's wire from it — the
+// template items (header bytes + big-endian value) overlapping the vector,
+// the first found from a per-wire-byte item table — and stores them straight
+// to HBM with non-temporal 16-byte stores: no wire tile, no zero pass, no LDS
+// atomics, one barrier (the decode's structure, run backwards).
+__host__ __device__ __forceinline__ uint32_t rec_region(uint32_t T, uint32_t S) {
+  return (T * S + 32 + 16 * T - 1) / (16 * T) * (16 * T);
+}
+__host__ __device__ __forceinline__ uint32_t gather_lds(uint32_t T, uint32_t S, uint32_t L) {
+  return rec_region(T, S) + kMaxTemplateItems * (uint32_t)sizeof(TemplateItem) + ((L + 15) & ~15u);
+}
+
+template <uint32_t T>
+__global__ __launch_bounds__(T) void plan_binary_encode_gather_kernel(
+    const FixedTemplate* __restrict__ tp, const uint8_t* __restrict__ recs, uint64_t n,
+    uint8_t* __restrict__ out, uint64_t* __restrict__ offsets, DevResult* __restrict__ res) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t L = tp->wire_len, S = tp->record_size, NI = tp->n_items;
+  const uint64_t tile0 = (uint64_t)blockIdx.x * T;
+  const uint32_t nrec = (uint32_t)min((uint64_t)T, n - tile0);
+  TemplateItem* items = (TemplateItem*)(smem + rec_region(T, S));
+  uint8_t* item_at = (uint8_t*)(items + kMaxTemplateItems);
+
+  // 1. record tile HBM -> LDS (16-byte phase of the records preserved)
+  const uint8_t* g = recs + tile0 * S;
+  const uint32_t sh = (uint32_t)((uintptr_t)g & 15);
+  {
+    const uint4* src = (const uint4*)(g - sh);
+    const uint32_t nvec = (nrec * S + sh + 15) >> 4;
+    const uint32_t wave = threadIdx.x >> 6;
+    for (uint32_t k = 0; k * T < nvec; ++k) {
+      const uint32_t i = k * T + threadIdx.x;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(src + (i < nvec ? i : nvec - 1)),
+          (__attribute__((address_space(3))) void*)(smem + (size_t)(k * T + wave * 64) * 16), 16,
+          0, 0);
+    }
+#ifndef TGPU_NO_DMA_SETTLE
+    prog::lds_dma_settle(smem, threadIdx.x, T, (nvec + T - 1) / T);
+#endif
+  }
+  // 2. the items (wire order) and the item each wire byte belongs to
+  for (uint32_t i = threadIdx.x; i < NI * (uint32_t)sizeof(TemplateItem) / 4; i += T)
+    ((uint32_t*)items)[i] = ((const uint32_t*)tp->items)[i];
+  for (uint32_t w = threadIdx.x; w < L; w += T) {
+    uint32_t k = 0;
+    while (k + 1 < NI && tp->items[k + 1].wire_off <= w) ++k;
+    item_at[w] = (uint8_t)k;
+  }
+  if (offsets) {
+    for (uint32_t i = threadIdx.x; i < nrec; i += T) offsets[tile0 + i] = (tile0 + i) * L;
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) offsets[n] = n * L;
+  }
+  __syncthreads();
+
+  // 3. the tile's wire, one 16-byte vector per lane step
+  const uint32_t M = 0xffffffffu / L + 1;  // p / L == umulhi(p, M) for p < 2^17
+  uint8_t* gout = out + tile0 * L;
+  const uint32_t osh = (uint32_t)((uintptr_t)gout & 15);
+  uint8_t* base = gout - osh;
+  const uint32_t end = osh + nrec * L;
+  const uint32_t nout = (end + 15) >> 4;
+  uint32_t bad = ~0u;
+  for (uint32_t v = threadIdx.x; v < nout; v += T) {
+    const int32_t p0 = (int32_t)(v * 16) - (int32_t)osh;  // tile-relative first byte
+    const uint32_t ps = p0 < 0 ? 0u : (uint32_t)p0;
+    uint32_t r = __umulhi(ps, M);
+    uint32_t k = item_at[ps - r * L];
+    unsigned __int128 win = 0;
+    int32_t pos = (int32_t)(r * L + items[k].wire_off);
+    while (pos < p0 + 16 && r < nrec) {
+      const TemplateItem it = items[k];
+      const uint8_t* m = smem + sh + r * S + it.member_off;
+      unsigned long long vbe = 0;  // big-endian value bytes, first byte lowest
+      switch (it.width) {
+        case 8: {
+          const uint2 x = *(const uint2*)m;
+          vbe = ((unsigned long long)bswap32(x.x) << 32) | bswap32(x.y);
+          break;
+        }
+        case 4: vbe = bswap32(*(const uint32_t*)m); break;
+        case 2: vbe = bswap32(*(const uint16_t*)m) >> 16; break;
+        case 1:
+          vbe = *m;
+          if (it.is_bool && vbe > 1 && r < bad) bad = r;  // validate_bool
+          break;
+        default: break;
+      }
+      const unsigned __int128 F =
+          (unsigned __int128)it.hdr | ((unsigned __int128)vbe << (8 * it.hdr_len));
+      const int32_t d = pos - p0;  // -11 .. 15
+      win |= d >= 0 ? F << (8 * d) : F >> (-8 * d);
+      if (++k == NI) {
+        k = 0;
+        ++r;
+      }
+      pos = (int32_t)(r * L + items[k].wire_off);
+    }
+    const uint32_t lo = v << 4;
+    if (lo >= osh && lo + 16 <= end) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 q = {(uint32_t)win, (uint32_t)(win >> 32), (uint32_t)(win >> 64),
+                       (uint32_t)(win >> 96)};
+      __builtin_nontemporal_store(q, (u32x4*)base + v);
+    } else {
+      for (uint32_t b = (lo < osh ? osh : lo); b < (lo + 16 < end ? lo + 16 : end); ++b)
+        base[b] = (uint8_t)(win >> (8 * (b - lo)));
+    }
+  }
+  if (bad != ~0u) atomicMin(&res->first_fail, (unsigned long long)(tile0 + bad));
+}
+
 // ---- variant selection -----------------------------------------------------
 // Defaults are the tuned configuration ("fixed-layout kernels");
 // TGPU_PLAN_DECODE="T,glds,pair,nt" / TGPU_PLAN_ENCODE="T,nt" override them for
@@ -391,6 +509,30 @@ hipError_t launch_plan_binary_encode(const FixedPlan* p, const FixedPlan* d_p,
   TGPU_ENC(512, 1)
 #undef TGPU_ENC
   return hipErrorInvalidValue;
+}
+
+// TGPU_PLAN_ENCODE_GATHER=<T> (256 | 512; A/B) selects the gather encoder.
+uint32_t plan_encode_gather_tile() {
+  const char* s = getenv("TGPU_PLAN_ENCODE_GATHER");
+  if (!s || !*s || s[0] == '0') return 0;
+  return atoi(s) == 512 ? 512u : 256u;
+}
+
+hipError_t launch_plan_binary_encode_gather(const FixedTemplate* t, const FixedTemplate* d_t,
+                                            const uint8_t* recs, uint64_t n, uint8_t* out,
+                                            uint64_t* offsets, DevResult* res, uint32_t T,
+                                            hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  if (t->record_size % 8 || t->n_items == 0 || ((uintptr_t)recs & 7)) return hipErrorInvalidValue;
+  const uint64_t blocks = (n + T - 1) / T;
+  const uint32_t lds = gather_lds(T, t->record_size, t->wire_len);
+  if (T == 512)
+    hipLaunchKernelGGL(plan_binary_encode_gather_kernel<512>, dim3((uint32_t)blocks), dim3(512),
+                       lds, stream, d_t, recs, n, out, offsets, res);
+  else
+    hipLaunchKernelGGL(plan_binary_encode_gather_kernel<256>, dim3((uint32_t)blocks), dim3(256),
+                       lds, stream, d_t, recs, n, out, offsets, res);
+  return hipGetLastError();
 }
 
 }  // namespace tgpu

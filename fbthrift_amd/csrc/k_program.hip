@@ -99,6 +99,36 @@ hipError_t launch_program_decode(const DecodeArgs& a, const VProgram* d_prog, ui
   return hipGetLastError();
 }
 
+// The strided tail decode's tile: the largest wire tile the program decode
+// takes (40 KiB) beside its record tile; records up to max_stride bytes.
+uint32_t stream_tail_wire_cap(uint32_t rec_size) {
+  const uint32_t rt = (kPT * rec_size + 16 + 15) & ~15u;
+  if (rt + 8192 > 163840) return 0;
+  const uint32_t room = (163840 - rt) / 4096 * 4096 - 32;
+  return std::min<uint32_t>(room, 40960) & ~15u;
+}
+
+uint64_t stream_tail_max_stride(uint32_t rec_size) {
+  const uint32_t cap = stream_tail_wire_cap(rec_size);
+  return cap > 16 ? (cap - 16) / kPT : 0;
+}
+
+hipError_t launch_stream_tail_decode(const DecodeArgs& a, uint32_t rec_size, uint64_t* irr,
+                                     unsigned long long* nirr, hipStream_t stream,
+                                     const JitKernels* J, int device) {
+  const uint32_t cap = stream_tail_wire_cap(rec_size);
+  if (!cap || !jit_has(J, 1)) return hipSuccess;
+  const uint32_t lds = program_decode_lds(cap, rec_size);
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      cus <= 0)
+    cus = 256;
+  // persistent: the workgroups one pass of the CUs holds (they loop over the
+  // tail's tiles; with no tail every one returns at once)
+  const uint64_t grid = (uint64_t)cus * std::max<uint32_t>(1, 163840 / lds);
+  return jit_launch_decode(J, a, grid, cap, lds, irr, nirr, stream, 1);
+}
+
 hipError_t launch_general_decode_list(const DecodeArgs& a, int protocol, const uint64_t* list,
                                       const unsigned long long* n_list, hipStream_t stream) {
   // (a grid-stride loop over the list: few workgroups keep the general

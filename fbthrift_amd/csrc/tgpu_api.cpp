@@ -1063,6 +1063,23 @@ const JitKernels* schema_jit(const tgpu_schema* s, int protocol, int group, uint
   return jit_kernels(s->prog[prog_protocol(s, protocol)], s->device, group, records, bytes, false);
 }
 
+// Stream-ordered fixed-layout calls: the tolerant program's compiled decode
+// group, whose strided tail decode re-reads the records from a misfit on
+// (nullptr: a batch under the probe's size, no program, a height the program
+// cannot read at, or the compile policy — the finish kernel's lane walks).
+// TGPU_STREAM_TAIL=1 turns it on (A/B, until measured on the GPU).
+const JitKernels* stream_tail_jit(const tgpu_schema* s, int protocol, const DecodeArgs& a) {
+  const char* v = getenv("TGPU_STREAM_TAIL");
+  if (!v || v[0] != '1') return nullptr;
+  const int32_t height = a.height ? a.height : a.max_depth;
+  if (a.n < kFixedProbeMin || !has_prog(s, protocol) || height < 2 || a.max_depth < 2 ||
+      !stream_tail_max_stride(a.rec_size))
+    return nullptr;
+  const JitKernels* J =
+      jit_kernels(s->prog_tol[prog_protocol(s, protocol)], s->device, JIT_DECODE, a.n, 0, false);
+  return jit_has(J, 1) ? J : nullptr;
+}
+
 // Fixed-layout Binary schemas: the compiled program kernels instead of the
 // word-gather plan kernels (TGPU_FIXED_PATH=jit; A/B).
 const JitKernels* fixed_jit(const tgpu_schema* s, int protocol, int group, uint64_t n) {
@@ -1676,9 +1693,15 @@ int tgpu_schema_compile_check_ex(const tgpu_struct_desc* structs, uint32_t n_str
   // nested schemas: the nested program (JIT_NESTED); others: the canonical
   // record program's three groups
   if (q < 0) return TGPU_ERR_UNSUPPORTED;
-  if (h.nested || !build_program(h, q, P))
+  if (h.nested || !build_program(h, q, P)) {
     if (!build_nested_program(h, q, P, depth)) return TGPU_ERR_UNSUPPORTED;
-  return jit_compile_check(P, arch, log, log_capacity);
+    return jit_compile_check(P, arch, log, log_capacity);
+  }
+  const int rc2 = jit_compile_check(P, arch, log, log_capacity);
+  // the tolerant variant's decode group (with the strided tail decode)
+  VProgram T{};
+  if (rc2 || !build_program(h, q, T, true)) return rc2;
+  return jit_compile_check(T, arch, log, log_capacity, JIT_DECODE);
 }
 
 int tgpu_schema_compile_check(const tgpu_struct_desc* structs, uint32_t n_structs,
@@ -1818,9 +1841,13 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
       f.fixed_len = fixed;
       f.offs = out_offsets;
       e = launch_program_write_fixed(f, schema->d_prog[prog_protocol(schema, protocol)], s, fj);
-    } else if (e == hipSuccess && schema->has_plan && ((uintptr_t)records & 7) == 0)
-      e = launch_plan_binary_encode(&schema->plan, schema->d_plan, a.recs, n, a.out, out_offsets,
-                                    ctx->d_res, s);
+    } else if (e == hipSuccess && schema->has_plan && ((uintptr_t)records & 7) == 0) {
+      const uint32_t gt = plan_encode_gather_tile();
+      e = gt ? launch_plan_binary_encode_gather(&schema->tmpl, schema->d_tmpl, a.recs, n, a.out,
+                                                out_offsets, ctx->d_res, gt, s)
+             : launch_plan_binary_encode(&schema->plan, schema->d_plan, a.recs, n, a.out,
+                                         out_offsets, ctx->d_res, s);
+    }
     else if (e == hipSuccess)
       e = launch_fixed_binary_encode(&schema->tmpl, schema->d_tmpl, a.recs, n, a.out,
                                      out_offsets, ctx->d_res, s);
@@ -2039,9 +2066,17 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
                                      a.exc, a.exc_cap, s);
     a.offs = ctx->d_offs;
     a.check_index = 0;
+    // stream-ordered calls re-read the records from a misfit on without the
+    // host: at the misfit's own length by the tolerant program (persistent,
+    // returns at once when every record was at its stride), then one lane
+    // from the first record off that stride too
+    const JitKernels* tj = blocking ? nullptr : stream_tail_jit(schema, protocol, a);
     // exceptions read at their stride; first_irregular becomes the first
     // record not at its stride position
-    if (e == hipSuccess) e = launch_fixed_exceptions(a, protocol, fixed, s);
+    if (e == hipSuccess)
+      e = blocking ? launch_fixed_exceptions(a, protocol, fixed, s)
+                   : launch_fixed_exceptions_stream(
+                         a, protocol, fixed, tj ? stream_tail_max_stride(a.rec_size) : 0, s);
     if (blocking) {
       // blocking call: look at the plan kernel's verdict, and index + decode
       // the tail after a non-canonical record in parallel
@@ -2063,7 +2098,10 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
         return tgpu_context_wait(ctx, stream, st ? st : &tmp, n_decoded, consumed);
       }
     }
-    if (e == hipSuccess) e = launch_serial_decode(a, protocol, true, fixed, s);
+    if (e == hipSuccess && tj)
+      e = launch_stream_tail_decode(a, a.rec_size, a.exc, &ctx->d_res->n_irregular, s, tj,
+                                    schema->device);
+    if (e == hipSuccess) e = launch_fixed_stream_finish(a, protocol, fixed, s);
   } else if (n) {
     if (offsets) {
       a.offs = offsets;

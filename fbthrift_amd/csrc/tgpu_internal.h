@@ -238,6 +238,10 @@ struct DevResult {
   unsigned long long n_deep;           // records deferred to the deep pass
   unsigned long long n_deep_chunks;    // index chunks deferred to the deep emit pass
   unsigned long long first_misfit;     // fixed path: first exception not L bytes long
+  // Stream-ordered fixed path, from the first misfit m on (tail_stride 0: none):
+  // record i >= m at tail_pos + (i - m) * tail_stride (record m's length);
+  // tail_min: the first record the strided tail decode did not take.
+  unsigned long long tail_first, tail_pos, tail_stride, tail_min;
 };
 
 struct DevSchema {
@@ -405,6 +409,24 @@ hipError_t launch_plan_binary_decode(const FixedPlan* p, const FixedPlan* d_p,
 // complete (else it stands), n_irregular = 0. Stream-ordered, no host sync.
 hipError_t launch_fixed_exceptions(const DecodeArgs& a, int protocol, uint64_t L,
                                    hipStream_t stream);
+// Stream-ordered fixed-layout calls (no host status, no host round trip):
+// launch_fixed_exceptions with the resolve step followed, when a record m is
+// off the stride, by record m's length L2 read by the general reader
+// (res->tail_*; tail_stride stays 0 when L2 > max_stride or record m fails).
+// The strided tail decode (tgpu_jit_decode_tail) then takes records m.. at
+// stride L2; launch_fixed_stream_finish reads its exceptions at their stride
+// positions and one lane walks from the first record off either stride.
+hipError_t launch_fixed_exceptions_stream(const DecodeArgs& a, int protocol, uint64_t L,
+                                          uint64_t max_stride, hipStream_t stream);
+hipError_t launch_fixed_stream_finish(const DecodeArgs& a, int protocol, uint64_t L,
+                                      hipStream_t stream);
+// The strided tail decode (J: the tolerant program's JIT_DECODE group),
+// persistent, one launch; max_stride: the longest record its tile takes.
+uint64_t stream_tail_max_stride(uint32_t rec_size);
+struct JitKernels;
+hipError_t launch_stream_tail_decode(const DecodeArgs& a, uint32_t rec_size, uint64_t* irr,
+                                     unsigned long long* nirr, hipStream_t stream,
+                                     const JitKernels* J, int device);
 // Blocking fixed-layout calls: reads record 0 at offset 0 with the general
 // reader; res->first_misfit = 0 when it is not L bytes long (or fails).
 hipError_t launch_fixed_probe(const DecodeArgs& a, int protocol, uint64_t L, hipStream_t stream);
@@ -412,6 +434,14 @@ hipError_t launch_plan_binary_encode(const FixedPlan* p, const FixedPlan* d_p,
                                      const uint8_t* recs, uint64_t n, uint8_t* out,
                                      uint64_t* offsets, DevResult* res,
                                      hipStream_t stream);
+// Gather form of the fixed-layout encode (A/B: TGPU_PLAN_ENCODE_GATHER=<T>;
+// 0 = the plan encode): the record tile by LDS DMA, 16-byte wire vectors
+// built per lane from the template items and stored straight to HBM.
+uint32_t plan_encode_gather_tile();
+hipError_t launch_plan_binary_encode_gather(const FixedTemplate* t, const FixedTemplate* d_t,
+                                            const uint8_t* recs, uint64_t n, uint8_t* out,
+                                            uint64_t* offsets, DevResult* res, uint32_t T,
+                                            hipStream_t stream);
 hipError_t launch_general_decode(const DecodeArgs& a, int protocol,
                                  hipStream_t stream);
 // Compiled-program fast path over an indexed stream (a.offs): canonical records
@@ -428,7 +458,12 @@ struct JitKernels;
 enum JitGroup { JIT_DECODE = 0, JIT_ENCODE = 1, JIT_INDEX = 2, JIT_NESTED = 3, JIT_NINDEX = 4 };
 const JitKernels* jit_kernels(const VProgram& prog, int device, int group, uint64_t records,
                               uint64_t bytes, bool force);
-int jit_compile_check(const VProgram& P, const char* arch, char* log, uint64_t log_cap);
+// only_group >= 0: that group alone
+int jit_compile_check(const VProgram& P, const char* arch, char* log, uint64_t log_cap,
+                      int only_group = -1);
+// entry `which` of a compiled group exists (JIT_DECODE entry 1, the strided
+// tail decode: tolerant programs only)
+bool jit_has(const JitKernels* J, int which);
 hipError_t jit_launch_decode(const JitKernels* J, const DecodeArgs& a, uint64_t grid,
                              uint32_t cap, uint32_t lds, uint64_t* irr, unsigned long long* nirr,
                              hipStream_t s, int which = 0);
@@ -455,9 +490,6 @@ hipError_t launch_deep_decode(const DecodeArgs& a, int protocol, hipStream_t str
 // and decoded (a: the tail, indices relative to rec_base).
 hipError_t launch_tail_decode_finish(const DecodeArgs& a, int protocol, uint64_t rec_base,
                                      hipStream_t stream);
-hipError_t launch_serial_decode(const DecodeArgs& a, int protocol,
-                                bool from_irregular, uint64_t fixed_len,
-                                hipStream_t stream);
 hipError_t launch_decode_finish(const DecodeArgs& a, int protocol,
                                 uint64_t fixed_len, hipStream_t stream);
 // nj: a nested program's compiled kernels (JIT_NESTED) for the size / write

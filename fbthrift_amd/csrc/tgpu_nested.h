@@ -234,6 +234,13 @@ __device__ __forceinline__ bool box_open(const Ctx& c, uint64_t& bump, uint64_t&
   return true;
 }
 
+// A struct slot built in registers (ES % 8 == 0) to its arena place.
+template <uint32_t ES>
+__device__ __forceinline__ void copy_slot(uint8_t* dst, const uint8_t* src) {
+#pragma unroll
+  for (uint32_t b = 0; b < ES; b += 8) *(uint64_t*)(dst + b) = *(const uint64_t*)(src + b);
+}
+
 // VOP_LIST of a nested program: scalar elements into the region (read_list,
 // tgpu_device.h: allocated only when n > 0), span at base + member.
 template <bool kStore = true, class Src>
@@ -256,6 +263,28 @@ __device__ __forceinline__ bool nlist(const VOp op, const bool compact, const Sr
     if (aoff + (uint64_t)n * es > c.arena_cap) return false;
   }
   uint8_t* dst = c.arena + aoff;
+#ifdef TGPU_NLIST_PAIR  // A/B (TGPU_JIT_DEFINES): two elements per window
+  if (kStore && !compact && op.elem_kind == VEL_FIXED && es == 4 && !c.pos_scale) {
+    // Binary 4-byte elements two at a time: one window, one 8-byte store
+    // (region arrays are 8-byte aligned)
+    if ((uint64_t)n * 4 > end - p) return false;
+    int64_t i = 0;
+    for (; i + 1 < n; i += 2) {
+      const uint64_t w = src.win8(p);
+      const uint64_t v = (uint64_t)__builtin_bswap32((uint32_t)w) |
+                         ((uint64_t)__builtin_bswap32((uint32_t)(w >> 32)) << 32);
+      *(uint64_t*)(dst + (uint64_t)i * 4) = v;
+      p += 8;
+    }
+    if (i < n) {
+      *(uint32_t*)(dst + (uint64_t)i * 4) = __builtin_bswap32((uint32_t)src.win8(p));
+      p += 4;
+    }
+    *(tgpu_span*)(base + op.member) = tgpu_span{n ? aoff : 0, (uint32_t)n, 0};
+    if (op.isset != 0xffff) base[op.isset] = 1;
+    return true;
+  }
+#endif
   for (int64_t i = 0; i < n; ++i) {
     uint64_t v;
     if (op.elem_kind == VEL_STRING) {  // read_elem: a view into the stream

@@ -71,19 +71,28 @@ __device__ __forceinline__ unsigned long long block_exscan256(unsigned long long
 __host__ __device__ __forceinline__ uint32_t decode_wire_region(uint32_t wire_cap) {
   return (wire_cap + 32 + 16 * kPT - 1) / (16 * kPT) * (16 * kPT);  // whole staging rounds
 }
-template <class PP>
+// kTail: the stream-ordered fixed-layout tail (DevResult tail_*): records
+// r0.. of the tile at pos + (i - first) * stride; their offsets are written,
+// a record not taken is listed (wave-aggregated atomics: a wrong stride
+// fails every record) and moves tail_min instead of first_irregular.
+struct TailStride {
+  uint64_t first, pos, stride, r0;
+};
+template <class PP, bool kTail = false>
 __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, uint32_t S,
                                             uint32_t wire_cap, uint64_t* __restrict__ irr,
                                             unsigned long long* __restrict__ nirr,
-                                            uint8_t* smem) {
+                                            uint8_t* smem, const TailStride& ts = {}) {
   uint8_t* wire = smem;
   uint8_t* rtile = smem + decode_wire_region(wire_cap);
-  const uint64_t r0 = (uint64_t)blockIdx.x * kPT;
-  const uint64_t n_all = a.n_dev ? min(a.n, (uint64_t)*a.n_dev) : a.n;
+  const uint64_t r0 = kTail ? ts.r0 : (uint64_t)blockIdx.x * kPT;
+  const uint64_t n_all = !kTail && a.n_dev ? min(a.n, (uint64_t)*a.n_dev) : a.n;
   if (r0 >= n_all) return;  // (whole workgroup)
   const uint32_t nrec = (uint32_t)min((uint64_t)kPT, n_all - r0);
-  const uint64_t L = a.fixed_len;
-  const uint64_t t0 = L ? r0 * L : a.offs[r0], t1 = L ? (r0 + nrec) * L : a.offs[r0 + nrec];
+  const uint64_t L = kTail ? ts.stride : a.fixed_len;
+  const uint64_t b0 = kTail ? ts.pos - ts.first * L : 0;  // record i at b0 + i * L
+  const uint64_t t0 = L ? b0 + r0 * L : a.offs[r0];
+  const uint64_t t1 = L ? b0 + (r0 + nrec) * L : a.offs[r0 + nrec];
   const bool tile_ok = t1 >= t0 && t1 <= a.in_len && (t1 - t0) + 16 <= wire_cap;
   uint32_t sh = 0;
   if (tile_ok) {
@@ -125,6 +134,7 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
                            a.arena && t1 <= a.arena_cap &&
                            (((uintptr_t)a.arena - (uintptr_t)a.in) & 15) == 0;
   const uint32_t r = threadIdx.x;
+  bool failed = false;
   if (r < nrec) {
     uint8_t* rec = rtile + osh + r * S;
     bool ok = tile_ok;
@@ -140,12 +150,33 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
         ok = run_program<true>(P, src, c, p, pe, rec) && p == pe;
       }
     }
-    if (!ok) {
+    if constexpr (kTail) {
+      failed = !ok;
+      if (a.offs) {
+        uint64_t* offs = const_cast<uint64_t*>(a.offs);
+        offs[r0 + r] = t0 + r * L;
+        if (r0 + r + 1 == a.n) offs[a.n] = t1;
+      }
+    } else if (!ok) {
       // general decoder list; a fixed-stride batch's exception list (irr ==
       // a.exc, read again at the stride position by fixed_exception_kernel)
       const unsigned long long k = atomicAdd(nirr, 1ull);
       if (!L || k < a.exc_cap) irr[k] = r0 + r;
       if (L) atomicMin(&a.res->first_irregular, (unsigned long long)(r0 + r));
+    }
+  }
+  if constexpr (kTail) {
+    const uint64_t bad = __ballot(failed);
+    if (bad) {
+      const uint32_t lane = threadIdx.x & 63, lead = (uint32_t)__builtin_ctzll(bad);
+      unsigned long long k0 = 0;
+      if (lane == lead) {
+        k0 = atomicAdd(nirr, (unsigned long long)__builtin_popcountll(bad));
+        atomicMin(&a.res->tail_min, (unsigned long long)(r0 + r));
+      }
+      k0 = __shfl(k0, (int)lead, 64);
+      const unsigned long long k = k0 + __builtin_popcountll(bad & ((1ull << lane) - 1));
+      if (failed && k < a.exc_cap) irr[k] = r0 + r;
     }
   }
   __syncthreads();

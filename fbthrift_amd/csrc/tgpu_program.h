@@ -67,8 +67,12 @@ __device__ __forceinline__ void note_exception(bool flag, uint64_t i, DevResult*
 __device__ __forceinline__ void lds_dma_settle(const uint8_t* lds, uint32_t first, uint32_t step,
                                                uint32_t n) {
   __builtin_amdgcn_s_waitcnt(0);  // (vmcnt(0) expcnt(0) lgkmcnt(0))
+#ifdef TGPU_SETTLE_ONE  // A/B: one read-back per lane (its last DMA'd vector)
+  if (n) (void)((const volatile uint32_t*)lds)[(first + (n - 1) * step) * 4];
+#else
   for (uint32_t k = 0; k < n; ++k)
     (void)((const volatile uint32_t*)lds)[(first + k * step) * 4];
+#endif
 }
 
 // ---- program accessors --------------------------------------------------------

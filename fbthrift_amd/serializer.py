@@ -124,8 +124,9 @@ class GpuSchema:
 def compile_check(schema, protocol, arch="gfx950"):
     """Generates and compiles `schema`'s kernels for `arch` without a GPU
     (tgpu_schema_compile_check_ex: the record program's decode / encode /
-    index kernels, or a nested schema's nested decode). Returns (code,
-    compiler log)."""
+    index kernels, or a nested schema's nested decode). arch "": the program
+    and kernel sources are generated only (whether the schema has a program,
+    without the seconds of compiling). Returns (code, compiler log)."""
     structs, ns, fields, nf = schema.descriptors()
     types, nt = schema.type_descriptors()
     log = ctypes.create_string_buffer(1 << 16)

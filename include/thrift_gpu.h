@@ -353,7 +353,9 @@ int tgpu_schema_compile(const tgpu_schema* schema, int protocol);
  * gfx950) without loading them — needs no GPU. The compiler log goes to
  * log[0..log_capacity) (may be NULL). TGPU_ERR_UNSUPPORTED as for
  * tgpu_schema_compile. Nested container types need the _ex form (here a
- * field with type_index != 0 has no program). */
+ * field with type_index != 0 has no program). arch "" (empty): the program is
+ * built and the kernel sources generated, nothing compiled (whether a schema
+ * has a program, in milliseconds instead of seconds). */
 int tgpu_schema_compile_check(const tgpu_struct_desc* structs, uint32_t n_structs,
                               const tgpu_field_desc* fields, uint32_t n_fields, int protocol,
                               const char* arch, char* log, uint64_t log_capacity);

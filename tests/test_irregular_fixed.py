@@ -6,8 +6,11 @@ and lists the ones it cannot take; the general reader reads those at their
 stride position (k_general.hip fixed_exception_kernel). From the first one
 that is not exactly the stride long (or fails) the stream is indexed and
 decoded in parallel (tgpu_api.cpp fixed_tail); a stream whose record 0 is
-already off the stride is indexed directly. Records, offsets and status are
-compared with the oracle at 1M records."""
+already off the stride is indexed directly. Stream-ordered calls (no host
+status) re-read from the first misfit at its own length with the tolerant
+program (tgpu_jit_decode_tail) and walk from the first record off that
+stride (k_general.hip fixed_stream_finish_kernel). Records, offsets and status
+are compared with the oracle at 1M records."""
 import numpy as np
 import pytest
 
@@ -70,20 +73,26 @@ def run(gpu, wire, n, sync=True):
     return st, nd
 
 
-def test_first_record_irregular(gpu):
+@pytest.mark.parametrize("sync", [True, False])
+def test_first_record_irregular(gpu, sync):
     recs, wire = canonical(N)
     w = np.concatenate([reordered(wire[:89]), wire[89:]])
-    st, nd = run(gpu, w, N)
+    st, nd = run(gpu, w, N, sync)
     assert st.code == 0 and nd == N
 
 
-def test_every_record_has_an_unknown_field(gpu):
-    _, wire = canonical(N)
-    st, nd = run(gpu, with_extra_field(wire), N)
+@pytest.mark.parametrize("sync,tail", [(True, "1"), (False, "1"), (False, "0")])
+def test_every_record_has_an_unknown_field(gpu, sync, tail, monkeypatch):
+    """Stream-ordered: the strided tail decode takes every record at 96 bytes
+    (TGPU_STREAM_TAIL=0: the finish kernel's lane walks them all)."""
+    monkeypatch.setenv("TGPU_STREAM_TAIL", tail)
+    _, wire = canonical(N if tail == "1" else 1 << 16)
+    st, nd = run(gpu, with_extra_field(wire), wire.size // 89, sync)
     assert st.code == 0 and nd == N
 
 
-def test_irregular_in_the_middle_then_error(gpu):
+@pytest.mark.parametrize("sync", [True, False])
+def test_irregular_in_the_middle_then_error(gpu, sync):
     _, wire = canonical(N)
     k = 700_001
     w = wire.copy()
@@ -93,14 +102,15 @@ def test_irregular_in_the_middle_then_error(gpu):
     # sent as T_STRING with a huge length is a reader error (truncated)
     j = 900_000
     w[89 * j + 33] = 11  # field 4's header type byte: T_STRING, length from the value bytes
-    run(gpu, w, N)
+    run(gpu, w, N, sync)
 
 
-def test_tail_shorter_than_n(gpu):
+@pytest.mark.parametrize("sync", [True, False])
+def test_tail_shorter_than_n(gpu, sync):
     """The stream ends before n records: UNDERFLOW at the first missing one."""
     _, wire = canonical(4096)
     w = np.concatenate([reordered(wire[:89]), wire[89:]])
-    st, nd = run(gpu, w, 5000)
+    st, nd = run(gpu, w, 5000, sync)
     assert st.code == 1 and nd == 4096
 
 
@@ -139,14 +149,15 @@ def test_every_record_reordered(gpu):
     assert st.code == 0 and nd == N
 
 
-def test_exception_list_overflow(gpu):
+@pytest.mark.parametrize("sync", [True, False])
+def test_exception_list_overflow(gpu, sync):
     """More exceptions than the list holds: the stream is indexed from the
-    first one."""
+    first one (stream-ordered: re-read at record 0's length, 89)."""
     n = N + 4096
     _, wire = canonical(n)
     w = wire.reshape(n, 89).copy()
     w[:, 0:11], w[:, 11:22] = wire.reshape(n, 89)[:, 11:22], wire.reshape(n, 89)[:, 0:11]
-    st, nd = run(gpu, w.reshape(-1), n)
+    st, nd = run(gpu, w.reshape(-1), n, sync)
     assert st.code == 0 and nd == n
 
 
@@ -163,7 +174,8 @@ def test_exception_then_length_change(gpu, sync):
     assert st.code == 0 and nd == n
 
 
-def test_every_record_extra_field_then_change(gpu):
+@pytest.mark.parametrize("sync", [True, False])
+def test_every_record_extra_field_then_change(gpu, sync):
     """A stream at a second stride (every record + one appended field) whose
     records change shape again at 600k (an appended string instead): the
     tolerant program decodes at the second stride up to there, the stream is
@@ -179,15 +191,16 @@ def test_every_record_extra_field_then_change(gpu):
     extra[:, 95:100] = tail[:, 3:8]
     extra[:, 100] = 0
     s = np.concatenate([w[:k].reshape(-1), extra.reshape(-1)])
-    st, nd = run(gpu, s, N)
+    st, nd = run(gpu, s, N, sync)
     assert st.code == 0 and nd == N
 
 
-def test_second_stride_with_error(gpu):
+@pytest.mark.parametrize("sync", [True, False])
+def test_second_stride_with_error(gpu, sync):
     """A bad record (an unknown field type) deep in a second-stride stream:
     the reference status at that record."""
     _, wire = canonical(200_000)
     w = with_extra_field(wire).copy()
     j = 150_001
     w[96 * j + 88] = 0x7F
-    run(gpu, w, 200_000)
+    run(gpu, w, 200_000, sync)

@@ -29,38 +29,40 @@ def test_nested_program_compiles(protocol):
 
 
 def test_nested_program_scope():
+    """Which shapes get a nested program (generated only: compiling is
+    test_nested_program_compiles' and the GPU tests' job)."""
     # map<Item, i32> (a struct key) and list<map<i32, bool>> (bools inside
     # maps): one each since round 4 (tests/test_nested_shapes.py)
     skey = [[[1, T_MAP, T_STRUCT, 0, -1, T_I32, None, [T_STRUCT, 0, 0, 1]]],
             [[1, T_I32, 0, 0, -1]]]
-    rc, log = compile_check(Schema.from_table(skey), 0)
+    rc, log = compile_check(Schema.from_table(skey), 0, arch="")
     assert rc == 0, log
     mbool = [[[1, T_LIST, T_MAP, 0, -1, 0, [T_MAP, T_I32, T_BOOL, -1]]]]
-    rc, log = compile_check(Schema.from_table(mbool), 2)
+    rc, log = compile_check(Schema.from_table(mbool), 2, arch="")
     assert rc == 0, log
     # struct Tree {1: list<Tree> kids} (recursive): none (general reader)
     tree = [[[1, T_LIST, T_STRUCT, 0, 0]]]
-    rc, _ = compile_check(Schema.from_table(tree), 0)
+    rc, _ = compile_check(Schema.from_table(tree), 0, arch="")
     assert rc == 22
     # map<i32, Item>, map<string, list<string>>, list<map<i32, string>>: one each
     for t in ([[[1, T_MAP, T_I32, 0, 1, T_STRUCT]], [[1, T_I32, 0, 0, -1]]],
               [[[1, T_MAP, T_STRING, 0, -1, T_LIST, [T_LIST, T_STRING, 0, -1]]]],
               [[[1, T_LIST, T_MAP, 0, -1, 0, [T_MAP, T_I32, T_STRING, -1]]]]):
         for protocol in (0, 2):
-            rc, log = compile_check(Schema.from_table(t), protocol)
+            rc, log = compile_check(Schema.from_table(t), protocol, arch="")
             assert rc == 0, log
     # list<Item> with a union Item: one (at most one member a record)
     un = [[[1, T_LIST, T_STRUCT, 0, 1]],
           {"union": True, "fields": [[1, T_I32, 0, 0, -1], [2, T_STRING, 0, 0, -1]]}]
-    rc, log = compile_check(Schema.from_table(un), 0)
+    rc, log = compile_check(Schema.from_table(un), 0, arch="")
     assert rc == 0, log
     # list<Item> with an optional member in Item: one (headers checked at run time)
     opt = [[[1, T_LIST, T_STRUCT, 0, 1]], [[1, T_I32, 0, 1, -1], [2, T_I32, 0, 0, -1]]]
-    rc, log = compile_check(Schema.from_table(opt), 2)
+    rc, log = compile_check(Schema.from_table(opt), 2, arch="")
     assert rc == 0, log
     # list<Item>: one
     ok = [[[1, T_LIST, T_STRUCT, 0, 1]], [[1, T_I32, 0, 0, -1], [2, T_STRING, 0, 0, -1]]]
-    rc, log = compile_check(Schema.from_table(ok), 2)
+    rc, log = compile_check(Schema.from_table(ok), 2, arch="")
     assert rc == 0, log
 
 
@@ -223,8 +225,8 @@ def _unqualified_case(name, protocol, n):
 @pytest.mark.parametrize("name", ["structlist", "deepcont"])
 def test_unqualified_nested_schemas_compile(name):
     c, _ = _unqualified_case(name, 0, 1)
-    for protocol in (0, 2):
-        rc, log = compile_check(c.schema, protocol)
+    for protocol in (0, 2):  # compiled in one protocol, generated in the other
+        rc, log = compile_check(c.schema, protocol, arch="gfx950" if protocol == 0 else "")
         assert rc == 0, log
 
 

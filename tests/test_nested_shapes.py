@@ -72,13 +72,17 @@ class Case:
 
 @pytest.mark.parametrize("protocol", [0, 2])
 def test_programs_exist(protocol):
-    rc, log = compile_check(Schema.from_table(TABLE), protocol)
+    """TABLE compiles (Binary; Compact generated only), keyed has a program,
+    the recursive schemas none."""
+    rc, log = compile_check(Schema.from_table(TABLE), protocol, arch="gfx950" if protocol == 0 else "")
     assert rc == 0, log
     for name in ("keyed",):
-        rc, log = compile_check(Schema.from_table(nh.manifest()["nested_schemas"][name]), protocol)
+        rc, log = compile_check(Schema.from_table(nh.manifest()["nested_schemas"][name]), protocol,
+                                arch="")
         assert rc == 0, log
     for name in ("tree", "chain"):  # recursive: none
-        rc, _ = compile_check(Schema.from_table(nh.manifest()["nested_schemas"][name]), protocol)
+        rc, _ = compile_check(Schema.from_table(nh.manifest()["nested_schemas"][name]), protocol,
+                              arch="")
         assert rc == 22
 
 

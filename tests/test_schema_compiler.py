@@ -1,8 +1,9 @@
 """The schema compiler (tgpu_jit.cpp) on a GPU-less host: the kernels it
 generates for a schema compile for gfx950 with hipRTC (all three kernel
 groups: decode, encode, index); schemas without one (optional fields,
-containers of structs, unions) compile a nested record program instead;
-bools inside maps and the like are refused — they run on the general reader. GPU parity of
+containers of structs, unions, bools inside maps) compile a nested record
+program instead; recursive schemas are refused — they run on the general
+reader. GPU parity of
 the compiled kernels is in test_gpu_parity.py (TGPU_JIT=1 runs). Compiles
 cost seconds each, so the CPU suite covers the three BASELINE config schemas
 in their benchmarked protocol plus the bool/long-form-id heavy 'scalars'."""
@@ -34,6 +35,10 @@ def test_unions_compile_nested_program():
     assert rc == 0, log
 
 
-def test_bool_map_keys_have_no_program():
-    rc, _ = compile_check(Schema.from_table(M["maps"]), 2)
-    assert rc == 22  # TGPU_ERR_UNSUPPORTED: the general reader path
+@pytest.mark.parametrize("protocol", [0, 2])
+def test_bool_map_keys_compile(protocol):
+    """Bools inside maps are nested-program leaves since round 4 (Compact's
+    container bool byte 1 / 2, Binary's 0 / 1, CompactProtocol-inl.h:692-701)."""
+    rc, log = compile_check(Schema.from_table(M["maps"]), protocol,
+                            arch="gfx950" if protocol == 2 else "")
+    assert rc == 0, log
