@@ -76,24 +76,43 @@ __device__ __forceinline__ unsigned long long decode_word(const FixedPlan* P,
   return v;
 }
 
-// The rare path of a word the plan cannot take (kept out of the wave-uniform
-// main loop: no ballot there).
-// seen: the tile's LDS bitmap of records already listed (a record with
-// several failing words is listed once: duplicates would make several
-// exception lanes decode the same record into the same slot).
-__device__ __attribute__((noinline)) void note_word_exception(uint64_t i, uint32_t r,
-                                                              uint32_t* seen, DevResult* res,
-                                                              uint64_t* exc, uint64_t cap) {
-  const uint32_t bit = 1u << (r & 31);
-  if (atomicOr(&seen[r >> 5], bit) & bit) return;
-  // a stream off the stride from early on fails every record: skip the
-  // atomics a lower first record or an overflowed list make moot (the
-  // relaxed loads may be stale, which only costs an atomic)
-  if (i < __hip_atomic_load(&res->first_irregular, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-    atomicMin(&res->first_irregular, (unsigned long long)i);
-  if (__hip_atomic_load(&res->n_irregular, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > cap) return;
-  const unsigned long long k = atomicAdd(&res->n_irregular, 1ull);
-  if (k < cap) exc[k] = i;
+// The exception records of a tile: a record with a word the plan cannot take
+// is marked in the tile's LDS bitmap `seen` (once, however many of its words
+// fail) and the tile lists them at its end — one atomicMin / atomicAdd per
+// tile, so a stream off the stride from early on (every record fails) costs
+// two global atomics per tile, not one per word (the same-address atomics of
+// every lane of every wave were 28 ms on 64 Mi records, 15x the decode).
+template <uint32_t T>
+__device__ __forceinline__ void list_tile_exceptions(uint64_t tile0, const uint32_t* seen,
+                                                     DevResult* res, uint64_t* exc, uint64_t cap) {
+  static_assert(T / 32 <= 64, "one bitmap word per lane of wave 0");
+  const uint32_t lane = threadIdx.x;
+  const uint32_t w = lane < T / 32 ? seen[lane] : 0u;
+  const uint64_t nz = __ballot(w != 0);
+  if (!nz) return;
+  const uint32_t c = (uint32_t)__builtin_popcount(w);
+  uint32_t pre = c;  // inclusive prefix of the counts over the lanes
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t x = __shfl_up(pre, o, 64);
+    if (lane >= o) pre += x;
+  }
+  const uint32_t total = __shfl(pre, 63, 64);
+  const uint32_t fl = (uint32_t)__builtin_ctzll(nz);
+  unsigned long long k0 = ~0ull;
+  if (lane == fl) {
+    const uint64_t i = tile0 + 32 * lane + (uint32_t)__builtin_ctz(w);
+    if (i < __hip_atomic_load(&res->first_irregular, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMin(&res->first_irregular, (unsigned long long)i);
+    // (an overflowed list is left alone; the relaxed load may be stale, which
+    // only costs the atomic)
+    if (__hip_atomic_load(&res->n_irregular, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= cap)
+      k0 = atomicAdd(&res->n_irregular, (unsigned long long)total);
+  }
+  k0 = __shfl(k0, (int)fl, 64);
+  if (k0 == ~0ull) return;
+  unsigned long long k = k0 + (pre - c);
+  for (uint32_t m = w; m; m &= m - 1, ++k)
+    if (k < cap) exc[k] = tile0 + 32 * lane + (uint32_t)__builtin_ctz(m);
 }
 
 // T records (= threads) per tile. kGlds: stage through LDS-DMA
@@ -138,7 +157,19 @@ __global__ __launch_bounds__(T) void plan_binary_decode_kernel(
     ((uint4*)P)[i] = ((const uint4*)pp)[i];
   uint32_t* seen = (uint32_t*)(smem + wire_region(T, L) + sizeof(FixedPlan));
   if (threadIdx.x < T / 32) seen[threadIdx.x] = 0;
+  // an overflowed exception list below this tile: every record from
+  // first_irregular on is re-read by the tail (index, or the stream-ordered
+  // strided decode), so the tile's work is moot (read with the staging in
+  // flight; both values only move one way; seen[T / 32]: the tile's verdict)
+  if (threadIdx.x == 0) {
+    const unsigned long long irr0 =
+        __hip_atomic_load(&res->first_irregular, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long nirr0 =
+        __hip_atomic_load(&res->n_irregular, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    seen[T / 32] = nirr0 > exc_cap && irr0 < tile0;
+  }
   __syncthreads();
+  if (seen[T / 32]) return;
 
   const uint32_t* w32 = (const uint32_t*)smem;
   const uint32_t total = nrec * Q;
@@ -153,7 +184,7 @@ __global__ __launch_bounds__(T) void plan_binary_decode_kernel(
       else o[q] = v;
       // a record one of whose words the plan cannot take joins the exception
       // list (once)
-      if (!ok) note_word_exception(tile0 + r, r, seen, res, exc, exc_cap);
+      if (!ok) atomicOr(&seen[r >> 5], 1u << (r & 31));
       r += sr;
       j += sj;
       if (j >= Q) {
@@ -178,8 +209,8 @@ __global__ __launch_bounds__(T) void plan_binary_decode_kernel(
       } else {
         o[q] = v0;
       }
-      if (!ok0) note_word_exception(tile0 + r, r, seen, res, exc, exc_cap);
-      if (!ok1) note_word_exception(tile0 + r1, r1, seen, res, exc, exc_cap);
+      if (!ok0) atomicOr(&seen[r >> 5], 1u << (r & 31));
+      if (!ok1) atomicOr(&seen[r1 >> 5], 1u << (r1 & 31));
       r += sr;
       j += sj;
       if (j >= Q) {
@@ -188,6 +219,8 @@ __global__ __launch_bounds__(T) void plan_binary_decode_kernel(
       }
     }
   }
+  __syncthreads();
+  if (threadIdx.x < 64) list_tile_exceptions<T>(tile0, seen, res, exc, exc_cap);
 }
 
 
@@ -311,119 +344,6 @@ __global__ __launch_bounds__(T) void plan_binary_encode_kernel(
   }
 }
 
-// Encode, gather form: the record tile goes HBM -> LDS by LDS DMA; each lane
-// then produces whole 16-byte vectors of the tile's wire from it — the
-// template items (header bytes + big-endian value) overlapping the vector,
-// the first found from a per-wire-byte item table — and stores them straight
-// to HBM with non-temporal 16-byte stores: no wire tile, no zero pass, no LDS
-// atomics, one barrier (the decode's structure, run backwards).
-__host__ __device__ __forceinline__ uint32_t rec_region(uint32_t T, uint32_t S) {
-  return (T * S + 32 + 16 * T - 1) / (16 * T) * (16 * T);
-}
-__host__ __device__ __forceinline__ uint32_t gather_lds(uint32_t T, uint32_t S, uint32_t L) {
-  return rec_region(T, S) + kMaxTemplateItems * (uint32_t)sizeof(TemplateItem) + ((L + 15) & ~15u);
-}
-
-template <uint32_t T>
-__global__ __launch_bounds__(T) void plan_binary_encode_gather_kernel(
-    const FixedTemplate* __restrict__ tp, const uint8_t* __restrict__ recs, uint64_t n,
-    uint8_t* __restrict__ out, uint64_t* __restrict__ offsets, DevResult* __restrict__ res) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint32_t L = tp->wire_len, S = tp->record_size, NI = tp->n_items;
-  const uint64_t tile0 = (uint64_t)blockIdx.x * T;
-  const uint32_t nrec = (uint32_t)min((uint64_t)T, n - tile0);
-  TemplateItem* items = (TemplateItem*)(smem + rec_region(T, S));
-  uint8_t* item_at = (uint8_t*)(items + kMaxTemplateItems);
-
-  // 1. record tile HBM -> LDS (16-byte phase of the records preserved)
-  const uint8_t* g = recs + tile0 * S;
-  const uint32_t sh = (uint32_t)((uintptr_t)g & 15);
-  {
-    const uint4* src = (const uint4*)(g - sh);
-    const uint32_t nvec = (nrec * S + sh + 15) >> 4;
-    const uint32_t wave = threadIdx.x >> 6;
-    for (uint32_t k = 0; k * T < nvec; ++k) {
-      const uint32_t i = k * T + threadIdx.x;
-      __builtin_amdgcn_global_load_lds(
-          (const void*)(src + (i < nvec ? i : nvec - 1)),
-          (__attribute__((address_space(3))) void*)(smem + (size_t)(k * T + wave * 64) * 16), 16,
-          0, 0);
-    }
-#ifndef TGPU_NO_DMA_SETTLE
-    prog::lds_dma_settle(smem, threadIdx.x, T, (nvec + T - 1) / T);
-#endif
-  }
-  // 2. the items (wire order) and the item each wire byte belongs to
-  for (uint32_t i = threadIdx.x; i < NI * (uint32_t)sizeof(TemplateItem) / 4; i += T)
-    ((uint32_t*)items)[i] = ((const uint32_t*)tp->items)[i];
-  for (uint32_t w = threadIdx.x; w < L; w += T) {
-    uint32_t k = 0;
-    while (k + 1 < NI && tp->items[k + 1].wire_off <= w) ++k;
-    item_at[w] = (uint8_t)k;
-  }
-  if (offsets) {
-    for (uint32_t i = threadIdx.x; i < nrec; i += T) offsets[tile0 + i] = (tile0 + i) * L;
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) offsets[n] = n * L;
-  }
-  __syncthreads();
-
-  // 3. the tile's wire, one 16-byte vector per lane step
-  const uint32_t M = 0xffffffffu / L + 1;  // p / L == umulhi(p, M) for p < 2^17
-  uint8_t* gout = out + tile0 * L;
-  const uint32_t osh = (uint32_t)((uintptr_t)gout & 15);
-  uint8_t* base = gout - osh;
-  const uint32_t end = osh + nrec * L;
-  const uint32_t nout = (end + 15) >> 4;
-  uint32_t bad = ~0u;
-  for (uint32_t v = threadIdx.x; v < nout; v += T) {
-    const int32_t p0 = (int32_t)(v * 16) - (int32_t)osh;  // tile-relative first byte
-    const uint32_t ps = p0 < 0 ? 0u : (uint32_t)p0;
-    uint32_t r = __umulhi(ps, M);
-    uint32_t k = item_at[ps - r * L];
-    unsigned __int128 win = 0;
-    int32_t pos = (int32_t)(r * L + items[k].wire_off);
-    while (pos < p0 + 16 && r < nrec) {
-      const TemplateItem it = items[k];
-      const uint8_t* m = smem + sh + r * S + it.member_off;
-      unsigned long long vbe = 0;  // big-endian value bytes, first byte lowest
-      switch (it.width) {
-        case 8: {
-          const uint2 x = *(const uint2*)m;
-          vbe = ((unsigned long long)bswap32(x.x) << 32) | bswap32(x.y);
-          break;
-        }
-        case 4: vbe = bswap32(*(const uint32_t*)m); break;
-        case 2: vbe = bswap32(*(const uint16_t*)m) >> 16; break;
-        case 1:
-          vbe = *m;
-          if (it.is_bool && vbe > 1 && r < bad) bad = r;  // validate_bool
-          break;
-        default: break;
-      }
-      const unsigned __int128 F =
-          (unsigned __int128)it.hdr | ((unsigned __int128)vbe << (8 * it.hdr_len));
-      const int32_t d = pos - p0;  // -11 .. 15
-      win |= d >= 0 ? F << (8 * d) : F >> (-8 * d);
-      if (++k == NI) {
-        k = 0;
-        ++r;
-      }
-      pos = (int32_t)(r * L + items[k].wire_off);
-    }
-    const uint32_t lo = v << 4;
-    if (lo >= osh && lo + 16 <= end) {
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      const u32x4 q = {(uint32_t)win, (uint32_t)(win >> 32), (uint32_t)(win >> 64),
-                       (uint32_t)(win >> 96)};
-      __builtin_nontemporal_store(q, (u32x4*)base + v);
-    } else {
-      for (uint32_t b = (lo < osh ? osh : lo); b < (lo + 16 < end ? lo + 16 : end); ++b)
-        base[b] = (uint8_t)(win >> (8 * (b - lo)));
-    }
-  }
-  if (bad != ~0u) atomicMin(&res->first_fail, (unsigned long long)(tile0 + bad));
-}
-
 // ---- variant selection -----------------------------------------------------
 // Defaults are the tuned configuration ("fixed-layout kernels");
 // TGPU_PLAN_DECODE="T,glds,pair,nt" / TGPU_PLAN_ENCODE="T,nt" override them for
@@ -478,8 +398,9 @@ hipError_t launch_plan_binary_decode(const FixedPlan* p, const FixedPlan* d_p, c
   DecVariant use = v;
   if (((uintptr_t)out & 15) != 0) use.pair = 0;  // 16-byte stores need 16-byte records base
   const uint64_t blocks = (n + use.T - 1) / use.T;
-  // + the tile's bitmap of listed exception records (one bit per record)
-  const uint32_t lds = wire_region(use.T, p->wire_len) + (uint32_t)sizeof(FixedPlan) + use.T / 8;
+  // + the tile's bitmap of exception records (one bit per record) + its verdict
+  const uint32_t lds =
+      wire_region(use.T, p->wire_len) + (uint32_t)sizeof(FixedPlan) + use.T / 8 + 16;
   auto* o = (unsigned long long*)out;
   switch (use.T) {
     case 128: return launch_dec_T<128>(use, lds, blocks, stream, d_p, in, n, o, res, exc, exc_cap);
@@ -509,30 +430,6 @@ hipError_t launch_plan_binary_encode(const FixedPlan* p, const FixedPlan* d_p,
   TGPU_ENC(512, 1)
 #undef TGPU_ENC
   return hipErrorInvalidValue;
-}
-
-// TGPU_PLAN_ENCODE_GATHER=<T> (256 | 512; A/B) selects the gather encoder.
-uint32_t plan_encode_gather_tile() {
-  const char* s = getenv("TGPU_PLAN_ENCODE_GATHER");
-  if (!s || !*s || s[0] == '0') return 0;
-  return atoi(s) == 512 ? 512u : 256u;
-}
-
-hipError_t launch_plan_binary_encode_gather(const FixedTemplate* t, const FixedTemplate* d_t,
-                                            const uint8_t* recs, uint64_t n, uint8_t* out,
-                                            uint64_t* offsets, DevResult* res, uint32_t T,
-                                            hipStream_t stream) {
-  if (n == 0) return hipSuccess;
-  if (t->record_size % 8 || t->n_items == 0 || ((uintptr_t)recs & 7)) return hipErrorInvalidValue;
-  const uint64_t blocks = (n + T - 1) / T;
-  const uint32_t lds = gather_lds(T, t->record_size, t->wire_len);
-  if (T == 512)
-    hipLaunchKernelGGL(plan_binary_encode_gather_kernel<512>, dim3((uint32_t)blocks), dim3(512),
-                       lds, stream, d_t, recs, n, out, offsets, res);
-  else
-    hipLaunchKernelGGL(plan_binary_encode_gather_kernel<256>, dim3((uint32_t)blocks), dim3(256),
-                       lds, stream, d_t, recs, n, out, offsets, res);
-  return hipGetLastError();
 }
 
 }  // namespace tgpu

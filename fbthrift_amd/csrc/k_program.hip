@@ -99,24 +99,27 @@ hipError_t launch_program_decode(const DecodeArgs& a, const VProgram* d_prog, ui
   return hipGetLastError();
 }
 
-// The strided tail decode's tile: the largest wire tile the program decode
-// takes (40 KiB) beside its record tile; records up to max_stride bytes.
-uint32_t stream_tail_wire_cap(uint32_t rec_size) {
+// The strided tail decode's tile: records up to L + 32 bytes (a second
+// stride of appended fields), within the program decode's 40 KiB wire tile
+// beside the record tile — sized so 3 workgroups share a CU where the record
+// tile allows (the persistent grid fills the CUs once).
+uint32_t stream_tail_wire_cap(uint32_t rec_size, uint32_t L) {
   const uint32_t rt = (kPT * rec_size + 16 + 15) & ~15u;
   if (rt + 8192 > 163840) return 0;
   const uint32_t room = (163840 - rt) / 4096 * 4096 - 32;
-  return std::min<uint32_t>(room, 40960) & ~15u;
+  const uint32_t want = kPT * (L + 32) + 16;
+  return std::min<uint32_t>(std::min<uint32_t>(room, want), 40960) & ~15u;
 }
 
-uint64_t stream_tail_max_stride(uint32_t rec_size) {
-  const uint32_t cap = stream_tail_wire_cap(rec_size);
+uint64_t stream_tail_max_stride(uint32_t rec_size, uint32_t L) {
+  const uint32_t cap = stream_tail_wire_cap(rec_size, L);
   return cap > 16 ? (cap - 16) / kPT : 0;
 }
 
-hipError_t launch_stream_tail_decode(const DecodeArgs& a, uint32_t rec_size, uint64_t* irr,
-                                     unsigned long long* nirr, hipStream_t stream,
+hipError_t launch_stream_tail_decode(const DecodeArgs& a, uint32_t rec_size, uint32_t L,
+                                     uint64_t* irr, unsigned long long* nirr, hipStream_t stream,
                                      const JitKernels* J, int device) {
-  const uint32_t cap = stream_tail_wire_cap(rec_size);
+  const uint32_t cap = stream_tail_wire_cap(rec_size, L);
   if (!cap || !jit_has(J, 1)) return hipSuccess;
   const uint32_t lds = program_decode_lds(cap, rec_size);
   int cus = 0;

@@ -1067,13 +1067,13 @@ const JitKernels* schema_jit(const tgpu_schema* s, int protocol, int group, uint
 // group, whose strided tail decode re-reads the records from a misfit on
 // (nullptr: a batch under the probe's size, no program, a height the program
 // cannot read at, or the compile policy — the finish kernel's lane walks).
-// TGPU_STREAM_TAIL=1 turns it on (A/B, until measured on the GPU).
+// TGPU_STREAM_TAIL=0 turns it off (A/B).
 const JitKernels* stream_tail_jit(const tgpu_schema* s, int protocol, const DecodeArgs& a) {
   const char* v = getenv("TGPU_STREAM_TAIL");
-  if (!v || v[0] != '1') return nullptr;
+  if (v && v[0] == '0') return nullptr;
   const int32_t height = a.height ? a.height : a.max_depth;
   if (a.n < kFixedProbeMin || !has_prog(s, protocol) || height < 2 || a.max_depth < 2 ||
-      !stream_tail_max_stride(a.rec_size))
+      !stream_tail_max_stride(a.rec_size, s->tmpl.wire_len))
     return nullptr;
   const JitKernels* J =
       jit_kernels(s->prog_tol[prog_protocol(s, protocol)], s->device, JIT_DECODE, a.n, 0, false);
@@ -1841,13 +1841,9 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
       f.fixed_len = fixed;
       f.offs = out_offsets;
       e = launch_program_write_fixed(f, schema->d_prog[prog_protocol(schema, protocol)], s, fj);
-    } else if (e == hipSuccess && schema->has_plan && ((uintptr_t)records & 7) == 0) {
-      const uint32_t gt = plan_encode_gather_tile();
-      e = gt ? launch_plan_binary_encode_gather(&schema->tmpl, schema->d_tmpl, a.recs, n, a.out,
-                                                out_offsets, ctx->d_res, gt, s)
-             : launch_plan_binary_encode(&schema->plan, schema->d_plan, a.recs, n, a.out,
-                                         out_offsets, ctx->d_res, s);
-    }
+    } else if (e == hipSuccess && schema->has_plan && ((uintptr_t)records & 7) == 0)
+      e = launch_plan_binary_encode(&schema->plan, schema->d_plan, a.recs, n, a.out, out_offsets,
+                                    ctx->d_res, s);
     else if (e == hipSuccess)
       e = launch_fixed_binary_encode(&schema->tmpl, schema->d_tmpl, a.recs, n, a.out,
                                      out_offsets, ctx->d_res, s);
@@ -2076,7 +2072,8 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
     if (e == hipSuccess)
       e = blocking ? launch_fixed_exceptions(a, protocol, fixed, s)
                    : launch_fixed_exceptions_stream(
-                         a, protocol, fixed, tj ? stream_tail_max_stride(a.rec_size) : 0, s);
+                         a, protocol, fixed, tj ? stream_tail_max_stride(a.rec_size, fixed) : 0,
+                         s);
     if (blocking) {
       // blocking call: look at the plan kernel's verdict, and index + decode
       // the tail after a non-canonical record in parallel
@@ -2099,8 +2096,8 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
       }
     }
     if (e == hipSuccess && tj)
-      e = launch_stream_tail_decode(a, a.rec_size, a.exc, &ctx->d_res->n_irregular, s, tj,
-                                    schema->device);
+      e = launch_stream_tail_decode(a, a.rec_size, (uint32_t)fixed, a.exc,
+                                    &ctx->d_res->n_irregular, s, tj, schema->device);
     if (e == hipSuccess) e = launch_fixed_stream_finish(a, protocol, fixed, s);
   } else if (n) {
     if (offsets) {

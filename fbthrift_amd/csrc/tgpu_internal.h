@@ -422,10 +422,10 @@ hipError_t launch_fixed_stream_finish(const DecodeArgs& a, int protocol, uint64_
                                       hipStream_t stream);
 // The strided tail decode (J: the tolerant program's JIT_DECODE group),
 // persistent, one launch; max_stride: the longest record its tile takes.
-uint64_t stream_tail_max_stride(uint32_t rec_size);
+uint64_t stream_tail_max_stride(uint32_t rec_size, uint32_t L);
 struct JitKernels;
-hipError_t launch_stream_tail_decode(const DecodeArgs& a, uint32_t rec_size, uint64_t* irr,
-                                     unsigned long long* nirr, hipStream_t stream,
+hipError_t launch_stream_tail_decode(const DecodeArgs& a, uint32_t rec_size, uint32_t L,
+                                     uint64_t* irr, unsigned long long* nirr, hipStream_t stream,
                                      const JitKernels* J, int device);
 // Blocking fixed-layout calls: reads record 0 at offset 0 with the general
 // reader; res->first_misfit = 0 when it is not L bytes long (or fails).
@@ -434,14 +434,6 @@ hipError_t launch_plan_binary_encode(const FixedPlan* p, const FixedPlan* d_p,
                                      const uint8_t* recs, uint64_t n, uint8_t* out,
                                      uint64_t* offsets, DevResult* res,
                                      hipStream_t stream);
-// Gather form of the fixed-layout encode (A/B: TGPU_PLAN_ENCODE_GATHER=<T>;
-// 0 = the plan encode): the record tile by LDS DMA, 16-byte wire vectors
-// built per lane from the template items and stored straight to HBM.
-uint32_t plan_encode_gather_tile();
-hipError_t launch_plan_binary_encode_gather(const FixedTemplate* t, const FixedTemplate* d_t,
-                                            const uint8_t* recs, uint64_t n, uint8_t* out,
-                                            uint64_t* offsets, DevResult* res, uint32_t T,
-                                            hipStream_t stream);
 hipError_t launch_general_decode(const DecodeArgs& a, int protocol,
                                  hipStream_t stream);
 // Compiled-program fast path over an indexed stream (a.offs): canonical records

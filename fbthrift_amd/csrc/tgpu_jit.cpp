@@ -200,9 +200,11 @@ void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t sto
         // a small struct slot is built in registers and leaves with whole
         // 8-byte stores (written member by member into the arena it took a
         // global store per member and per isset byte)
-        const char* defs = getenv("TGPU_JIT_DEFINES");  // (A/B: "TGPU_NESTED_STAGE")
+        // (decode 3.62 -> 2.50 ms on the nested leg with the paired list
+        // elements; A/B: TGPU_JIT_DEFINES naming TGPU_NESTED_NOSTAGE)
+        const char* defs = getenv("TGPU_JIT_DEFINES");
         stage = zero && v.hdr <= 64 && v.hdr % 8 == 0 &&
-                (defs && strstr(defs, "TGPU_NESTED_STAGE"));
+                !(defs && strstr(defs, "TGPU_NESTED_NOSTAGE"));
         if (stage) {
           o << in << "    uint8_t* " << e << "_dst = " << a << " + (uint64_t)" << i << " * " << v.hdr
             << "u;\n"

@@ -263,7 +263,7 @@ __device__ __forceinline__ bool nlist(const VOp op, const bool compact, const Sr
     if (aoff + (uint64_t)n * es > c.arena_cap) return false;
   }
   uint8_t* dst = c.arena + aoff;
-#ifdef TGPU_NLIST_PAIR  // A/B (TGPU_JIT_DEFINES): two elements per window
+#ifndef TGPU_NLIST_SINGLE  // A/B (TGPU_JIT_DEFINES): one element per window
   if (kStore && !compact && op.elem_kind == VEL_FIXED && es == 4 && !c.pos_scale) {
     // Binary 4-byte elements two at a time: one window, one 8-byte store
     // (region arrays are 8-byte aligned)

@@ -87,8 +87,9 @@ def test_every_record_has_an_unknown_field(gpu, sync, tail, monkeypatch):
     (TGPU_STREAM_TAIL=0: the finish kernel's lane walks them all)."""
     monkeypatch.setenv("TGPU_STREAM_TAIL", tail)
     _, wire = canonical(N if tail == "1" else 1 << 16)
-    st, nd = run(gpu, with_extra_field(wire), wire.size // 89, sync)
-    assert st.code == 0 and nd == N
+    n = wire.size // 89
+    st, nd = run(gpu, with_extra_field(wire), n, sync)
+    assert st.code == 0 and nd == n
 
 
 @pytest.mark.parametrize("sync", [True, False])
