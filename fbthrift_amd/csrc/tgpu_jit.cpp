@@ -183,9 +183,22 @@ void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t sto
           << ", kCompact, s" << K << ".length)) return false;\n"
           << in << "  const uint32_t " << n << " = s" << K << ".length;\n"
           << in << "  const uint8_t* " << a << " = lbase + s" << K << ".offset;\n"
-          << in << "  for (uint32_t " << i << " = 0; " << i << " < " << n << "; ++" << i << ") {\n"
-          << in << "    const uint8_t* " << e << " = " << a << " + (uint64_t)" << i << " * " << v.hdr
-          << "u;\n";
+          << in << "  for (uint32_t " << i << " = 0; " << i << " < " << n << "; ++" << i << ") {\n";
+        // a small struct slot is read into registers first (its members
+        // were one dependent global load each); A/B: TGPU_JIT_DEFINES
+        // naming TGPU_NESTED_NOLOADSTAGE
+        const char* defs = getenv("TGPU_JIT_DEFINES");
+        const bool sslot = v.elem_ttype == TGPU_T_STRUCT ||
+                           (v.kind == VOP_MSEQ && v.width == TGPU_T_STRUCT);
+        if (sslot && v.hdr <= 64 && v.hdr % 8 == 0 &&
+            !(defs && strstr(defs, "TGPU_NESTED_NOLOADSTAGE"))) {
+          o << in << "    alignas(8) uint8_t " << e << "[" << v.hdr << "];\n"
+            << in << "    load_slot<" << v.hdr << "u>(" << e << ", " << a << " + (uint64_t)" << i
+            << " * " << v.hdr << "u);\n";
+        } else {
+          o << in << "    const uint8_t* " << e << " = " << a << " + (uint64_t)" << i << " * "
+            << v.hdr << "u;\n";
+        }
       } else {
         o << in << "  uint32_t " << n << ";\n"
           << in << "  uint8_t* " << a << ";\n"

@@ -241,6 +241,20 @@ __device__ __forceinline__ void copy_slot(uint8_t* dst, const uint8_t* src) {
   for (uint32_t b = 0; b < ES; b += 8) *(uint64_t*)(dst + b) = *(const uint64_t*)(src + b);
 }
 
+// A struct slot (ES % 8 == 0) of an encoder's list base into registers: the
+// slot's loads issued together instead of one dependent load per member
+// (8-byte loads when the slot is 8-byte aligned, else 4-byte ones).
+template <uint32_t ES>
+__device__ __forceinline__ void load_slot(uint8_t* dst, const uint8_t* src) {
+  if (((uintptr_t)src & 7) == 0) {
+#pragma unroll
+    for (uint32_t b = 0; b < ES; b += 8) *(uint64_t*)(dst + b) = *(const uint64_t*)(src + b);
+  } else {
+#pragma unroll
+    for (uint32_t b = 0; b < ES; b += 4) *(uint32_t*)(dst + b) = *(const uint32_t*)(src + b);
+  }
+}
+
 // VOP_LIST of a nested program: scalar elements into the region (read_list,
 // tgpu_device.h: allocated only when n > 0), span at base + member.
 template <bool kStore = true, class Src>
@@ -670,6 +684,34 @@ __device__ __forceinline__ bool enc_op(const VOp op, const bool compact, const u
           return true;
         }
       }
+#ifndef TGPU_NLIST_ENC_SINGLE  // A/B (TGPU_JIT_DEFINES): one element per load
+      if constexpr (!O::kCount) {
+        // Binary 4- / 8-byte elements from an 8-byte aligned array: whole
+        // 8-byte words, four loads in flight, one put each
+        if (!compact && op.elem_kind == VEL_FIXED && (es == 4 || es == 8) &&
+            ((uintptr_t)e & 7) == 0) {
+          const uint64_t* q = (const uint64_t*)e;
+          const uint32_t nw = es == 4 ? sp.length / 2 : sp.length;
+          auto be = [es](uint64_t w) -> uint64_t {
+            return es == 8 ? __builtin_bswap64(w)
+                           : (uint64_t)__builtin_bswap32((uint32_t)w) |
+                                 ((uint64_t)__builtin_bswap32((uint32_t)(w >> 32)) << 32);
+          };
+          uint32_t k = 0;
+          for (; k + 4 <= nw; k += 4) {
+            const uint64_t w0 = q[k], w1 = q[k + 1], w2 = q[k + 2], w3 = q[k + 3];
+            o.put(be(w0), 8);
+            o.put(be(w1), 8);
+            o.put(be(w2), 8);
+            o.put(be(w3), 8);
+          }
+          for (; k < nw; ++k) o.put(be(q[k]), 8);
+          if (es == 4 && (sp.length & 1))
+            o.put(__builtin_bswap32(((const uint32_t*)e)[sp.length - 1]), 4);
+          return true;
+        }
+      }
+#endif
       for (uint32_t i = 0; i < sp.length; ++i) {
         const uint8_t* p = e + (uint64_t)i * es;
         if (op.elem_kind == VEL_STRING) {
