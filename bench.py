@@ -1158,10 +1158,12 @@ def transcode(wl, dev, reps=5):
 
 def skim(wl, dev, reps=10):
     """Schemaless skim (tgpu_skim_batch) of the workload's encoded stream with
-    its record index: per record, one 16-byte entry per top-level field.
-    Algorithmic bytes = wire + index (8 B/record) read + entries (16 B/field)
-    + counts (4 B/record) written. HIP events on the launch stream. Checked
-    against the oracle on a sample of records. Secondary line, never `value`."""
+    its record index: per record, one 16-byte entry per top-level field —
+    and, for a schema with a struct-valued field (config 4), the nested skim
+    (tgpu_skim_batch_ex, one level: the struct's fields too). Algorithmic
+    bytes = wire + index (8 B/record) read + entries (16 B/field) + counts
+    (4 B/record) written. HIP events on the launch stream. Checked against
+    the oracle on a sample of records. Secondary line, never `value`."""
     import numpy as np
     import torch
 
@@ -1176,41 +1178,52 @@ def skim(wl, dev, reps=10):
         offs = wl.offs
     else:
         offs = torch.arange(wl.n + 1, dtype=torch.int64, device=dev) * wl.L
-    nf = len(wl.gs.schema.structs[0].fields)
     w = wl.wire[: wl.wire_bytes]
-    fields, counts, done, st = wl.S.skim(w, offs, wl.n, max_fields=nf)
-    assert st.code == 0 and done == wl.n
-    times = []
-    for _ in range(reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        wl.S.skim(w, offs, wl.n, max_fields=nf, check=False, fields=fields, counts=counts)
-        e1.record()
-        torch.cuda.synchronize()
-        times.append(e0.elapsed_time(e1) / 1e3)
-    # oracle check on sampled records (rebased slices)
-    rng = np.random.default_rng(7)
-    oc = offs.cpu().numpy().astype(np.uint64)
-    cnt = counts.cpu().numpy()
-    fv = fields[: nf * wl.n * 16].view(nf, wl.n, 16)
-    for i in rng.integers(0, wl.n, 64):
-        a, b = int(oc[i]), int(oc[i + 1])
-        raw = w[a:b].cpu().numpy()
-        ost, ofl, ocnt, _ = oracle.skim(wl.S.protocol, raw, np.array([0, b - a], np.uint64), 1, nf)
-        g = S.skim_records(fv[:, i].contiguous().view(-1), 1, nf)
-        k = int(ocnt[0])
-        assert ost.code == 0 and cnt[i] == k
-        assert np.array_equal(g[0, :k]["id"], ofl[0, :k]["id"])
-        assert np.array_equal(g[0, :k]["length"], ofl[0, :k]["length"])
-        assert np.array_equal(g[0, :k]["offset"] - a, ofl[0, :k]["offset"])
-    t = float(np.median(times))
-    alg = wl.wire_bytes + 8 * (wl.n + 1) + int(cnt.astype(np.int64).sum()) * 16 + 4 * wl.n
-    return {"kernel": "skim_kernel", "records": wl.n, "fields_per_record": round(
-        float(cnt.mean()), 3), "ms": round(t * 1e3, 4),
-        "gibps_wire": round(wl.wire_bytes / t / 2**30, 2),
-        "achieved_GBps": round(alg / t / 1e9, 1), "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
-        "algorithmic_bytes": alg, "timing": "HIP events around the call, median of %d" % reps,
-        "check": "64 sampled records vs the oracle"}
+    structs = wl.gs.schema.structs
+
+    def run(nest):
+        nf = len(structs[0].fields) + (sum(len(st.fields) for st in structs[1:]) if nest else 0)
+        fields, counts, done, st = wl.S.skim(w, offs, wl.n, max_fields=nf, nest=nest)
+        assert st.code == 0 and done == wl.n
+        times = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            wl.S.skim(w, offs, wl.n, max_fields=nf, check=False, fields=fields, counts=counts,
+                      nest=nest)
+            e1.record()
+            torch.cuda.synchronize()
+            times.append(e0.elapsed_time(e1) / 1e3)
+        # oracle check on sampled records (rebased slices)
+        rng = np.random.default_rng(7)
+        oc = offs.cpu().numpy().astype(np.uint64)
+        cnt = counts.cpu().numpy()
+        fv = fields[: nf * wl.n * 16].view(nf, wl.n, 16)
+        for i in rng.integers(0, wl.n, 64):
+            a, b = int(oc[i]), int(oc[i + 1])
+            raw = w[a:b].cpu().numpy()
+            ost, ofl, ocnt, _ = oracle.skim(wl.S.protocol, raw, np.array([0, b - a], np.uint64),
+                                            1, nf, nest=nest)
+            g = S.skim_records(fv[:, i].contiguous().view(-1), 1, nf)
+            k = int(ocnt[0])
+            assert ost.code == 0 and cnt[i] == k
+            for key in ("id", "flags", "length"):
+                assert np.array_equal(g[0, :k][key], ofl[0, :k][key])
+            assert np.array_equal(g[0, :k]["offset"] - a, ofl[0, :k]["offset"])
+        t = float(np.median(times))
+        alg = wl.wire_bytes + 8 * (wl.n + 1) + int(cnt.astype(np.int64).sum()) * 16 + 4 * wl.n
+        return {"kernel": "skim_kernel", "nest": nest, "records": wl.n,
+                "fields_per_record": round(float(cnt.mean()), 3), "ms": round(t * 1e3, 4),
+                "gibps_wire": round(wl.wire_bytes / t / 2**30, 2),
+                "achieved_GBps": round(alg / t / 1e9, 1),
+                "frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4), "algorithmic_bytes": alg,
+                "timing": "HIP events around the call, median of %d" % reps,
+                "check": "64 sampled records vs the oracle"}
+
+    res = run(0)
+    if len(structs) > 1:
+        res["nested"] = run(1)
+    return res
 
 
 def host_batch(wl, records=1 << 22):

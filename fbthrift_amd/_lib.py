@@ -80,6 +80,7 @@ EXPORTS = [
     "tgpu_schema_compile_check_ex",
     "tgpu_decode_host", "tgpu_encode_host", "tgpu_decode_stream", "tgpu_transcode_batch",
     "tgpu_schema_arena_scale", "tgpu_decode_host_ex", "tgpu_encode_host_ex", "tgpu_skim_batch",
+    "tgpu_skim_batch_ex",
     "tgpu_index_stats", "tgpu_decode_host_chunks", "tgpu_encode_host_chunks",
 ]
 
@@ -90,6 +91,7 @@ CHUNK_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uin
 SKIM_FIELDS = [("id", "<i2"), ("ttype", "u1"), ("flags", "u1"), ("length", "<u4"),
                ("offset", "<u8")]
 SKIM_BOOL, SKIM_TRUE = 1, 2
+SKIM_LEVEL_SHIFT, SKIM_LEVEL_MASK, SKIM_MAX_NEST = 2, 0x3C, 8
 
 _lib = None
 
@@ -148,6 +150,10 @@ def lib():
     L.tgpu_skim_batch.restype = I32
     L.tgpu_skim_batch.argtypes = [P, I32, P, U64, P, U64, P, U32, P, ctypes.POINTER(Limits), P,
                                   ctypes.POINTER(Status), ctypes.POINTER(U64)]
+    L.tgpu_skim_batch_ex.restype = I32
+    L.tgpu_skim_batch_ex.argtypes = [P, I32, P, U64, P, U64, P, U32, P, U32,
+                                     ctypes.POINTER(Limits), P, ctypes.POINTER(Status),
+                                     ctypes.POINTER(U64)]
     L.tgpu_schema_compile.restype = I32
     L.tgpu_schema_compile.argtypes = [P, I32]
     L.tgpu_schema_compile_check_ex.restype = I32

@@ -1,7 +1,8 @@
 // k_skim.hip — schemaless skim of an indexed stream (tgpu_skim_batch).
 //
-// One lane per record walks its top-level fields exactly like the parse loop
-// of protocol::parseObject (thrift/lib/cpp2/protocol/detail/Object.h:416-432):
+// One lane per record walks its top-level fields (and, with max_nest, those of
+// struct-valued fields, pre-order) exactly like the parse loop of
+// protocol::parseObject (thrift/lib/cpp2/protocol/detail/Object.h:416-432):
 // readFieldBegin until STOP; a bool is read (FieldMaskUtil.h:441-450), any
 // other value is passed over by the protocol's skip and kept as (offset,
 // length) of its encoded bytes, the masked parse's setMaskedDataFull
@@ -22,7 +23,9 @@ using namespace dev;
 // The reader walks `src` (the stream, or an LDS copy of bytes
 // [base, base + src_len) of it) in positions relative to `base`; stored
 // offsets and error offsets are absolute.
-template <int P>
+// kNest: the nested form (a.max_nest > 0) — its level stack costs ~35 VGPRs,
+// so the flat skim is its own instantiation.
+template <int P, bool kNest = false>
 __device__ Reader skim_one(const SkimArgs& a, uint64_t i, bool store, const uint8_t* src,
                            uint64_t base, uint64_t src_len, int lane) {
   // slot k of record i at fields[k * n + i] (field-major: a wave's k-th
@@ -40,33 +43,74 @@ __device__ Reader skim_one(const SkimArgs& a, uint64_t i, bool store, const uint
   }
   uint32_t count = 0;
   int32_t prev = 0;
+  // struct-valued fields descended into (a.max_nest levels): the entry slot
+  // reserved for the struct, its value start, its id and the enclosing
+  // level's last field id (Compact's pushed lastFieldId_)
+  uint32_t lvl = 0;
+  constexpr uint32_t kLv = kNest ? TGPU_SKIM_MAX_NEST : 1;
+  uint32_t nslot[kLv];
+  uint64_t nstart[kLv];
+  int32_t nid[kLv];
+  const uint32_t max_nest = kNest ? a.max_nest : 0;
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  auto put = [&](uint32_t k, int32_t id, uint32_t wt, uint32_t flags, uint64_t len, uint64_t off) {
+    // one 16-byte entry {id, ttype, flags | length | offset}
+    const uint64_t o = off + base;
+    const u32x4 e = {(uint32_t)(uint16_t)id | (wt << 16) | (flags << 24), (uint32_t)len,
+                     (uint32_t)o, (uint32_t)(o >> 32)};
+    u32x4* dst = (u32x4*)(out + (uint64_t)k * a.n);
+    if (a.nt_stores) __builtin_nontemporal_store(e, dst);
+    else *dst = e;
+  };
   while (r.ok()) {
     uint32_t wt = 0;
     int32_t id = 0;
-    if (!Pr::field_header(r, prev, wt, id)) break;  // STOP or error
+    if (!Pr::field_header(r, prev, wt, id)) {  // STOP or error
+      if (!r.ok() || !kNest || lvl == 0) break;
+      // a descended struct's STOP: readStructEnd, then its entry
+      r.ascend();
+      --lvl;
+      if (r.pos - nstart[lvl] > 0xffffffffull) {
+        r.fail(TGPU_ERR_UNSUPPORTED, nstart[lvl]);
+        break;
+      }
+      if (store && nslot[lvl] < a.max_fields)
+        put(nslot[lvl], nid[lvl], TGPU_T_STRUCT, lvl << TGPU_SKIM_LEVEL_SHIFT,
+            r.pos - nstart[lvl], nstart[lvl]);
+      prev = nid[lvl];
+      continue;
+    }
     prev = id;
     const uint64_t off = r.pos;
-    uint32_t flags = 0;
-    if (wt == TGPU_T_BOOL) flags = TGPU_SKIM_BOOL | (Pr::read_bool(r) ? TGPU_SKIM_TRUE : 0);
+    if (kNest && wt == TGPU_T_STRUCT && lvl < max_nest) {
+      // parseValue -> parseObjectInplace: the struct's own fields, with the
+      // checks skip(T_STRUCT, lvl) makes (max_depth, readStructBegin)
+      if ((int32_t)lvl >= r.max_depth) {
+        r.fail(TGPU_ERR_DEPTH_LIMIT, r.pos);
+        break;
+      }
+      r.descend(r.pos);
+      if (!r.ok()) break;
+      nslot[lvl] = count;
+      nstart[lvl] = off;
+      nid[lvl] = id;
+      ++count;
+      ++lvl;
+      prev = 0;
+      continue;
+    }
+    uint32_t flags = lvl << TGPU_SKIM_LEVEL_SHIFT;
+    if (wt == TGPU_T_BOOL) flags |= TGPU_SKIM_BOOL | (Pr::read_bool(r) ? TGPU_SKIM_TRUE : 0);
     // leaves inline (skip's explicit stack lives in scratch); structs and
     // containers take the full skip
-    else if (r.max_depth <= 0 || !Pr::skip_leaf(r, wt)) skip<P>(r, wt, 0);
+    else if (r.max_depth <= (int32_t)lvl || !Pr::skip_leaf(r, wt)) skip<P>(r, wt, (int32_t)lvl);
     if (!r.ok()) break;
     // an entry's length is 32 bits: a value of 4 GiB or more is reported
     if (r.pos - off > 0xffffffffull) {
       r.fail(TGPU_ERR_UNSUPPORTED, off);
       break;
     }
-    if (store && count < a.max_fields) {
-      // one 16-byte entry {id, ttype, flags | length | offset}
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      const uint64_t o = off + base;
-      const u32x4 e = {(uint32_t)(uint16_t)id | (wt << 16) | (flags << 24),
-                       (uint32_t)(r.pos - off), (uint32_t)o, (uint32_t)(o >> 32)};
-      u32x4* dst = (u32x4*)(out + (uint64_t)count * a.n);
-      if (a.nt_stores) __builtin_nontemporal_store(e, dst);
-      else *dst = e;
-    }
+    if (store && count < a.max_fields) put(count, id, wt, flags, r.pos - off, off);
     ++count;
   }
   if (store) a.counts[i] = count;
@@ -76,10 +120,10 @@ __device__ Reader skim_one(const SkimArgs& a, uint64_t i, bool store, const uint
   return r;
 }
 
-template <int P>
+template <int P, bool kNest = false>
 __device__ __forceinline__ Reader skim_global(const SkimArgs& a, uint64_t i, bool store,
                                               int lane) {
-  return skim_one<P>(a, i, store, a.in, 0, a.in_len, lane);
+  return skim_one<P, kNest>(a, i, store, a.in, 0, a.in_len, lane);
 }
 
 // One 256-record tile per workgroup: the tile's wire bytes
@@ -88,7 +132,7 @@ __device__ __forceinline__ Reader skim_global(const SkimArgs& a, uint64_t i, boo
 // fails on the copy (damaged input, a length running off the tile) is parsed
 // again from HBM, so every status is the stream's own. Tiles too large for
 // LDS parse from HBM directly. kSkimTile: LDS bytes of the wire copy.
-template <int P, uint32_t kSkimTile>
+template <int P, uint32_t kSkimTile, bool kNest>
 __global__ __launch_bounds__(256) void skim_kernel(SkimArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t tile[kSkimTile + 16];
   const uint64_t r0 = (uint64_t)blockIdx.x * 256;
@@ -111,9 +155,9 @@ __global__ __launch_bounds__(256) void skim_kernel(SkimArgs a) {
   __syncthreads();
   const uint64_t i = r0 + threadIdx.x;
   if (i >= a.n) return;
-  Reader r = staged ? skim_one<P>(a, i, true, tile, a0, b1 - a0, -1)
-                    : skim_global<P>(a, i, true, -1);
-  if (staged && !r.ok() && r.err != kErrDeep) r = skim_global<P>(a, i, true, -1);
+  Reader r = staged ? skim_one<P, kNest>(a, i, true, tile, a0, b1 - a0, -1)
+                    : skim_global<P, kNest>(a, i, true, -1);
+  if (staged && !r.ok() && r.err != kErrDeep) r = skim_global<P, kNest>(a, i, true, -1);
   if (!r.ok()) defer_or_fail(r, a.deep, &a.res->first_fail, i);
 }
 
@@ -125,7 +169,8 @@ __global__ __launch_bounds__(64) void deep_skim_kernel(SkimArgs a) {
   const uint64_t m = *a.deep.count;
   for (uint64_t k = lane; k < m; k += a.deep.lanes) {
     const uint64_t i = a.deep.list[k];
-    const Reader r = skim_global<P>(a, i, true, (int)lane);
+    const Reader r = a.max_nest ? skim_global<P, true>(a, i, true, (int)lane)
+                                : skim_global<P>(a, i, true, (int)lane);
     if (!r.ok()) atomicMin(&a.res->first_fail, (unsigned long long)i);
   }
 }
@@ -136,7 +181,8 @@ __global__ void skim_finish_kernel(SkimArgs a) {
   DevResult* res = a.res;
   const uint64_t f = res->first_fail;
   if (f < a.n) {
-    const Reader r = skim_global<P>(a, f, false, 0);
+    const Reader r = a.max_nest ? skim_global<P, true>(a, f, false, 0)
+                                : skim_global<P>(a, f, false, 0);
     res->code = r.ok() ? TGPU_ERR_INDEX_MISMATCH : r.err;
     res->fail_offset = r.ok() ? r.pos : r.err_off;
     res->n_records = f;
@@ -161,12 +207,14 @@ hipError_t launch_skim(const SkimArgs& a, int protocol, hipStream_t stream) {
     const uint32_t g = (uint32_t)((a.n + 255) / 256);
     uint32_t kb = a.in_len / a.n * 256 <= 24560 ? 24 : 32;
     if (const char* e = getenv("TGPU_SKIM_TILE")) kb = (uint32_t)atoi(e);
-    if (kb == 24)
-      TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL((skim_kernel<P_, 24560>), dim3(g), dim3(256),
-                                                    0, stream, a));
-    else
-      TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL((skim_kernel<P_, 32752>), dim3(g), dim3(256),
-                                                    0, stream, a));
+#define TGPU_SKIM(KB, NEST)                                                                \
+  TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL((skim_kernel<P_, KB, NEST>), dim3(g), dim3(256), \
+                                                0, stream, a))
+    if (kb == 24 && !a.max_nest) TGPU_SKIM(24560, false);
+    else if (kb == 24) TGPU_SKIM(24560, true);
+    else if (!a.max_nest) TGPU_SKIM(32752, false);
+    else TGPU_SKIM(32752, true);
+#undef TGPU_SKIM
   }
   if (a.deep.lanes)
     TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(deep_skim_kernel<P_>,

@@ -2302,7 +2302,16 @@ int tgpu_skim_batch(tgpu_context* ctx, int protocol, const void* in, uint64_t in
                     const uint64_t* offsets, uint64_t n, tgpu_skim_field* fields,
                     uint32_t max_fields, uint32_t* field_counts, const tgpu_limits* limits,
                     void* stream, tgpu_status* st, uint64_t* n_done) {
-  if (!ctx || !valid_protocol(protocol) ||
+  return tgpu_skim_batch_ex(ctx, protocol, in, in_len, offsets, n, fields, max_fields,
+                            field_counts, 0, limits, stream, st, n_done);
+}
+
+int tgpu_skim_batch_ex(tgpu_context* ctx, int protocol, const void* in, uint64_t in_len,
+                       const uint64_t* offsets, uint64_t n, tgpu_skim_field* fields,
+                       uint32_t max_fields, uint32_t* field_counts, uint32_t max_nest,
+                       const tgpu_limits* limits, void* stream, tgpu_status* st,
+                       uint64_t* n_done) {
+  if (!ctx || !valid_protocol(protocol) || max_nest > TGPU_SKIM_MAX_NEST ||
       (n && (!offsets || !field_counts || (max_fields && !fields) || (!in && in_len))) ||
       ((uintptr_t)fields & 15)) {
     fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
@@ -2330,6 +2339,7 @@ int tgpu_skim_batch(tgpu_context* ctx, int protocol, const void* in, uint64_t in
   a.res = ctx->d_res;
   a.deep = deep_args(ctx);
   a.nt_stores = getenv("TGPU_SKIM_NT") ? atoi(getenv("TGPU_SKIM_NT")) : 1;
+  a.max_nest = max_nest;
   (void)hipGetLastError();
   hipError_t e = launch_result_init(ctx->d_res, n, s);
   if (e == hipSuccess) e = launch_skim(a, protocol, s);

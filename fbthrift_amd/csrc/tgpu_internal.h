@@ -291,6 +291,7 @@ struct SkimArgs {
   int32_t string_limit, container_limit, max_depth, height;
   DevResult* res;
   int nt_stores;  // entries stored non-temporally (never re-read here)
+  uint32_t max_nest;  // struct-valued fields descended into (0: top level only)
   DeepArgs deep;
 };
 

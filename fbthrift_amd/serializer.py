@@ -487,9 +487,11 @@ class BatchSerializer:
 
     # -- schemaless skim ----------------------------------------------------
     def skim(self, wire, offsets, n=None, max_fields=16, limits=None, stream=None, check=True,
-             fields=None, counts=None):
+             fields=None, counts=None, nest=0):
         """Top-level fields of records [0, n) of an indexed stream
-        (tgpu_skim_batch): `wire` a uint8 device tensor, `offsets` its n+1
+        (tgpu_skim_batch; nest > 0: also the fields of struct-valued fields
+        that many levels down, pre-order, level in flags bits 2-5 —
+        tgpu_skim_batch_ex): `wire` a uint8 device tensor, `offsets` its n+1
         record starts (device int64). Returns (fields, counts, n_done,
         status): fields a uint8 device tensor of max_fields * n
         tgpu_skim_field entries, field-major (skim_records() views it as a
@@ -510,9 +512,9 @@ class BatchSerializer:
         if limits is not None:
             lim = _lib.Limits(*limits) if not isinstance(limits, _lib.Limits) else limits
         st, done = _lib.Status(), ctypes.c_uint64()
-        _lib.lib().tgpu_skim_batch(
+        _lib.lib().tgpu_skim_batch_ex(
             self.context().handle, self.protocol, _ptr(wire), wire.numel(), _ptr(offsets), n,
-            _ptr(fields), max_fields, _ptr(counts),
+            _ptr(fields), max_fields, _ptr(counts), nest,
             ctypes.byref(lim) if lim is not None else None, _stream(stream), ctypes.byref(st),
             ctypes.byref(done))
         if check:

@@ -659,6 +659,9 @@ typedef struct tgpu_skim_field {
 } tgpu_skim_field;
 
 enum { TGPU_SKIM_BOOL = 1, TGPU_SKIM_TRUE = 2 };
+/* Nested skim (tgpu_skim_batch_ex): flags bits 2-5 hold the entry's struct
+ * nesting level (0 = a top-level field). */
+enum { TGPU_SKIM_LEVEL_SHIFT = 2, TGPU_SKIM_LEVEL_MASK = 0x3c, TGPU_SKIM_MAX_NEST = 8 };
 
 /*
  * Skims records [0, n) of an indexed stream (offsets: device, n + 1 entries,
@@ -676,6 +679,23 @@ int tgpu_skim_batch(tgpu_context* ctx, int protocol, const void* in, uint64_t in
                     const uint64_t* offsets, uint64_t n_records, tgpu_skim_field* fields,
                     uint32_t max_fields, uint32_t* field_counts, const tgpu_limits* limits,
                     void* stream, tgpu_status* st, uint64_t* n_done);
+/*
+ * The same, descending into struct-valued fields up to max_nest levels
+ * (<= TGPU_SKIM_MAX_NEST; 0 = tgpu_skim_batch): parseObject's recursion
+ * (parseValue -> parseObjectInplace, protocol/detail/Object.h:416-432) with
+ * every other value kept as its encoded bytes. Entries are in pre-order (wire
+ * order of the field headers): a descended struct's entry (ttype T_STRUCT,
+ * offset / length of its whole encoded value, as a skip passes over it)
+ * precedes its fields' entries, which carry level + 1 in flags. Depth and
+ * height are checked as apache::thrift::skip would for the same struct
+ * (Protocol.h:187-283: max_depth per nesting level, readStructBegin's
+ * descend). field_counts count every entry, nested ones included.
+ */
+int tgpu_skim_batch_ex(tgpu_context* ctx, int protocol, const void* in, uint64_t in_len,
+                       const uint64_t* offsets, uint64_t n_records, tgpu_skim_field* fields,
+                       uint32_t max_fields, uint32_t* field_counts, uint32_t max_nest,
+                       const tgpu_limits* limits, void* stream, tgpu_status* st,
+                       uint64_t* n_done);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -661,13 +661,16 @@ class GpuBatchSerializer {
    * of protocol::parseObject with every value kept as its encoded bytes
    * (protocol/detail/FieldMaskUtil.h:373-388). fields: max_fields * n
    * entries, field-major (fields[k * n + i] = field k of record i); counts:
-   * n. Device pointers. Throws on the first record the reader rejects. */
+   * n. Device pointers. Throws on the first record the reader rejects.
+   * nest > 0: the fields of struct-valued fields too, that many levels down
+   * (parseObject's recursion; pre-order, the level in flags bits 2-5;
+   * tgpu_skim_batch_ex). */
   void skim(const void* in, uint64_t len, const uint64_t* offsets, uint64_t n,
-            tgpu_skim_field* fields, uint32_t max_fields, uint32_t* counts) {
+            tgpu_skim_field* fields, uint32_t max_fields, uint32_t* counts, uint32_t nest = 0) {
     tgpu_status st{};
     uint64_t done = 0;
-    tgpu_skim_batch(ctx_, Protocol::kId, in, len, offsets, n, fields, max_fields, counts,
-                    &limits_, stream_, &st, &done);
+    tgpu_skim_batch_ex(ctx_, Protocol::kId, in, len, offsets, n, fields, max_fields, counts, nest,
+                       &limits_, stream_, &st, &done);
     if (st.code != TGPU_OK) rethrow(st);
   }
   /* List arena bytes deserialize() needs for `len` input bytes. */

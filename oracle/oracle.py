@@ -189,23 +189,24 @@ SKIM_DTYPE = np.dtype([("id", "<i2"), ("ttype", "u1"), ("flags", "u1"), ("length
                        ("offset", "<u8")])
 
 
-def skim(protocol, wire, offsets, n=None, max_fields=16, limits=None):
-    """Schemaless skim (oracle_skim_batch): returns (status, fields (n,
-    max_fields) SKIM_DTYPE records, counts uint32[n], n_done)."""
+def skim(protocol, wire, offsets, n=None, max_fields=16, limits=None, nest=0):
+    """Schemaless skim (oracle_skim_batch_ex; nest = struct levels descended
+    into): returns (status, fields (n, max_fields) SKIM_DTYPE records, counts
+    uint32[n], n_done)."""
     w = _u8(wire)
     offs = np.ascontiguousarray(offsets, dtype=np.uint64)
     n = offs.size - 1 if n is None else n
     fields = np.zeros((max(max_fields, 1), max(n, 1)), SKIM_DTYPE)  # field-major
     counts = np.zeros(max(n, 1), np.uint32)
     L = lib()
-    L.oracle_skim_batch.restype = ctypes.c_int
-    L.oracle_skim_batch.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
-                                    ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
-                                    ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
-                                    ctypes.c_void_p, ctypes.c_void_p]
+    L.oracle_skim_batch_ex.restype = ctypes.c_int
+    L.oracle_skim_batch_ex.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64,
+                                       ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                       ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lim = Limits(*limits) if limits is not None else None
     st, done = Status(), ctypes.c_uint64()
-    L.oracle_skim_batch(protocol, _p(w), w.size, _p(offs), n, fields.ctypes.data, max_fields,
-                        counts.ctypes.data, ctypes.byref(lim) if lim else None,
-                        ctypes.byref(st), ctypes.byref(done))
+    L.oracle_skim_batch_ex(protocol, _p(w), w.size, _p(offs), n, fields.ctypes.data, max_fields,
+                           counts.ctypes.data, nest, ctypes.byref(lim) if lim else None,
+                           ctypes.byref(st), ctypes.byref(done))
     return st, fields[:max_fields, :n].T, counts[:n], done.value

@@ -1488,9 +1488,49 @@ int64_t oracle_skip_value(int protocol, const void* in, uint64_t in_len, uint64_
 // protocol/detail/FieldMaskUtil.h:373-388); bools are read
 // (FieldMaskUtil.h:441-450). Sequential, record by record; stops at the
 // first record the reader rejects or whose end disagrees with offsets[i+1].
+// One struct level of it: every field's entry in pre-order; a struct-valued
+// field below max_nest recurses as parseValue -> parseObjectInplace does,
+// after the checks skip(T_STRUCT, level) makes (max_depth, readStructBegin's
+// descend, Protocol.h:187-283); any other value is passed over by skip at
+// this level's depth.
+extern "C++" template <class R>
+void skim_level(R& r, uint32_t level, uint32_t max_nest, uint64_t i, uint64_t n,
+                tgpu_skim_field* fields, uint32_t max_fields, uint32_t& count) {
+  int16_t prev = 0;
+  while (true) {
+    uint8_t wt;
+    int16_t id;
+    if (!r.readFieldHeader(prev, wt, id)) return;
+    prev = id;
+    const uint64_t off = r.c.pos;
+    const uint32_t slot = count++;
+    uint8_t flags = (uint8_t)(level << TGPU_SKIM_LEVEL_SHIFT);
+    if (wt == TGPU_T_STRUCT && level < max_nest) {
+      if ((int64_t)level >= r.lim.max_depth) fail(TGPU_ERR_DEPTH_LIMIT, off);
+      r.height.descend(off);  // readStructBegin
+      skim_level(r, level + 1, max_nest, i, n, fields, max_fields, count);
+      r.height.ascend();      // readStructEnd
+    } else if (wt == TGPU_T_BOOL) {
+      flags |= TGPU_SKIM_BOOL | (r.readBool() ? TGPU_SKIM_TRUE : 0);
+    } else {
+      r.skip(wt, (int)level);
+    }
+    // an entry's length is 32 bits: a longer value is not representable
+    if (r.c.pos - off > 0xffffffffull) fail(TGPU_ERR_UNSUPPORTED, off);
+    if (slot < max_fields) {
+      tgpu_skim_field& f = fields[(uint64_t)slot * n + i];
+      f.id = id;
+      f.ttype = wt;
+      f.flags = flags;
+      f.length = (uint32_t)(r.c.pos - off);
+      f.offset = off;
+    }
+  }
+}
+
 extern "C++" template <class R>
 int skim_impl(const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint64_t n,
-              tgpu_skim_field* fields, uint32_t max_fields, uint32_t* counts,
+              tgpu_skim_field* fields, uint32_t max_fields, uint32_t* counts, uint32_t max_nest,
               const Limits& lim, tgpu_status* st, uint64_t* n_done) {
   for (uint64_t i = 0; i < n; ++i) {
     R r;
@@ -1501,28 +1541,7 @@ int skim_impl(const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint6
     try {
       if (offsets[i] > in_len || offsets[i + 1] < offsets[i])
         fail(TGPU_ERR_INDEX_MISMATCH, offsets[i]);
-      int16_t prev = 0;
-      while (true) {
-        uint8_t wt;
-        int16_t id;
-        if (!r.readFieldHeader(prev, wt, id)) break;
-        prev = id;
-        const uint64_t off = r.c.pos;
-        uint8_t flags = 0;
-        if (wt == TGPU_T_BOOL) flags = TGPU_SKIM_BOOL | (r.readBool() ? TGPU_SKIM_TRUE : 0);
-        else r.skip(wt, 0);
-        // an entry's length is 32 bits: a longer value is not representable
-        if (r.c.pos - off > 0xffffffffull) fail(TGPU_ERR_UNSUPPORTED, off);
-        if (count < max_fields) {
-          tgpu_skim_field& f = fields[(uint64_t)count * n + i];
-          f.id = id;
-          f.ttype = wt;
-          f.flags = flags;
-          f.length = (uint32_t)(r.c.pos - off);
-          f.offset = off;
-        }
-        ++count;
-      }
+      skim_level(r, 0, max_nest, i, n, fields, max_fields, count);
       counts[i] = count;
       if (r.c.pos != offsets[i + 1]) fail(TGPU_ERR_INDEX_MISMATCH, r.c.pos);
     } catch (const OErr& e) {
@@ -1536,23 +1555,35 @@ int skim_impl(const uint8_t* in, uint64_t in_len, const uint64_t* offsets, uint6
   return TGPU_OK;
 }
 
+int oracle_skim_batch_ex(int protocol, const void* in, uint64_t in_len, const uint64_t* offsets,
+                         uint64_t n_records, tgpu_skim_field* fields, uint32_t max_fields,
+                         uint32_t* field_counts, uint32_t max_nest, const tgpu_limits* limits,
+                         tgpu_status* st, uint64_t* n_done) {
+  const Limits lim = to_limits(limits);
+  auto p = (const uint8_t*)in;
+  if (max_nest > TGPU_SKIM_MAX_NEST) {
+    set_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+    return TGPU_ERR_INVALID_ARGUMENT;
+  }
+  if (protocol == TGPU_PROTOCOL_BINARY)
+    return skim_impl<BinaryReader>(p, in_len, offsets, n_records, fields, max_fields,
+                                   field_counts, max_nest, lim, st, n_done);
+  if (protocol == TGPU_PROTOCOL_COMPACT)
+    return skim_impl<CompactReader>(p, in_len, offsets, n_records, fields, max_fields,
+                                    field_counts, max_nest, lim, st, n_done);
+  if (protocol == TGPU_PROTOCOL_COMPACT_V1)
+    return skim_impl<CompactV1Reader>(p, in_len, offsets, n_records, fields, max_fields,
+                                      field_counts, max_nest, lim, st, n_done);
+  set_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
+  return TGPU_ERR_INVALID_ARGUMENT;
+}
+
 int oracle_skim_batch(int protocol, const void* in, uint64_t in_len, const uint64_t* offsets,
                       uint64_t n_records, tgpu_skim_field* fields, uint32_t max_fields,
                       uint32_t* field_counts, const tgpu_limits* limits, tgpu_status* st,
                       uint64_t* n_done) {
-  const Limits lim = to_limits(limits);
-  auto p = (const uint8_t*)in;
-  if (protocol == TGPU_PROTOCOL_BINARY)
-    return skim_impl<BinaryReader>(p, in_len, offsets, n_records, fields, max_fields,
-                                   field_counts, lim, st, n_done);
-  if (protocol == TGPU_PROTOCOL_COMPACT)
-    return skim_impl<CompactReader>(p, in_len, offsets, n_records, fields, max_fields,
-                                    field_counts, lim, st, n_done);
-  if (protocol == TGPU_PROTOCOL_COMPACT_V1)
-    return skim_impl<CompactV1Reader>(p, in_len, offsets, n_records, fields, max_fields,
-                                      field_counts, lim, st, n_done);
-  set_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
-  return TGPU_ERR_INVALID_ARGUMENT;
+  return oracle_skim_batch_ex(protocol, in, in_len, offsets, n_records, fields, max_fields,
+                              field_counts, 0, limits, st, n_done);
 }
 
 int oracle_read_varint(const void* in, uint64_t len, int bits, uint64_t* value,

@@ -77,6 +77,12 @@ int oracle_skim_batch(int protocol, const void* in, uint64_t in_len,
                       tgpu_skim_field* fields, uint32_t max_fields,
                       uint32_t* field_counts, const tgpu_limits* limits,
                       tgpu_status* st, uint64_t* n_done);
+/* The same descending into struct-valued fields up to max_nest levels
+ * (tgpu_skim_batch_ex's pre-order entries; the recursion of parseObject). */
+int oracle_skim_batch_ex(int protocol, const void* in, uint64_t in_len, const uint64_t* offsets,
+                         uint64_t n_records, tgpu_skim_field* fields, uint32_t max_fields,
+                         uint32_t* field_counts, uint32_t max_nest, const tgpu_limits* limits,
+                         tgpu_status* st, uint64_t* n_done);
 
 /* Varint / zigzag primitives (VarintUtils-inl.h restated) for unit tests. */
 int oracle_read_varint(const void* in, uint64_t len, int bits,
