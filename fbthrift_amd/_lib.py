@@ -7,7 +7,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libtgpu.so")
+# (TGPU_LIB_PATH: another build of the same library, for diagnosis runs)
+LIB_PATH = os.environ.get("TGPU_LIB_PATH") or os.path.join(_HERE, "lib", "libtgpu.so")
 
 PROTOCOL_BINARY = 0
 PROTOCOL_COMPACT = 2

@@ -1094,6 +1094,14 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, Arena&
           if (aoff + size > A.cap) return r.fail(TGPU_ERR_OUTPUT_OVERFLOW, r.pos);
           obj = A.base + aoff;
         }
+#ifdef TGPU_BOXED_DIRECT  // diagnosis only: the round-3 direct form
+        if (!A.discard()) {
+          zero_bytes(obj, size);
+          *(tgpu_span*)m = tgpu_span{(uint64_t)(obj - A.base), 1, 0};
+        }
+        fr = struct_frame(f.struct_index, obj);
+        continue;
+#endif
         fr.kind = RF_LIST;
         fr.is_set = kBoxedFrame;
         fr.etype = TGPU_T_STRUCT;
