@@ -251,6 +251,7 @@ class VarLen(Workload):
     index (n+1 offsets) the decode then uses; the round trip is checked by
     comparing the fixed members and re-encoding the decoded batch, which must
     reproduce the wire stream byte for byte."""
+    jit_decode = "tgpu_jit_decode"
 
     def __init__(self, n, rank, dev):
         import ctypes
@@ -267,7 +268,7 @@ class VarLen(Workload):
         # the schema compiler's kernels (tgpu_jit.cpp), compiled up front like
         # the reference's generated code; TGPU_JIT=0 keeps the interpreter
         if os.environ.get("TGPU_JIT", "") != "0" and self.gs.compile(self.protocol):
-            self.dec_kernel, self.enc_kernel = "tgpu_jit_decode", "tgpu_jit_write"
+            self.dec_kernel, self.enc_kernel = self.jit_decode, "tgpu_jit_write"
             self.index_kernel = "tgpu_jit_index_spec"
         self.n = n
         self.record_bytes = rs = schema.record_size
@@ -346,6 +347,7 @@ class Mixed(VarLen):
     schema, protocol = "mixed", 2
     default_records = 1 << 26
     dec_kernel, enc_kernel = "program_decode_kernel", "program_write_kernel"
+    jit_decode = "tgpu_jit_decode"
     index_kernel = "index_tile_spec_kernel"
     fixed_ranges = [(0, 16), (48, 54)]
     span_offsets, elem_width = (16, 32), 1
@@ -357,6 +359,9 @@ class Nested(VarLen):
     schema, protocol = "nested", 0
     default_records = 1 << 25
     dec_kernel, enc_kernel = "program_decode_kernel", "program_write_kernel"
+    # records built in registers: the LDS record tile would hold its tiles
+    # to 3 workgroups per CU (k_program.hip launch_program_decode)
+    jit_decode = "tgpu_jit_decode_rr"
     fixed_ranges = [(0, 8), (24, 51), (56, 59)]
     span_offsets, elem_width = (8,), 4
 

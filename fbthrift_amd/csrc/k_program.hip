@@ -62,13 +62,14 @@ __global__ __launch_bounds__(256) void general_decode_list_kernel(DecodeArgs a,
 // 1.64 -> 1.45 ms going from the old fixed 1.3 x mean + 1 KiB to 5
 // workgroups/CU.) TGPU_PROG_DECODE="factor,pad" overrides the upper bound.
 // span_bytes: the wire bytes of the n records (0: a.in_len).
-uint32_t program_decode_wire_cap(const DecodeArgs& a, uint32_t rec_size, uint64_t span_bytes) {
+uint32_t program_decode_wire_cap(const DecodeArgs& a, uint32_t rec_size, uint64_t span_bytes,
+                                 bool regrec) {
   double factor = 1.12, pad = 512.0;
   if (const char* e = getenv("TGPU_PROG_DECODE")) sscanf(e, "%lf,%lf", &factor, &pad);
   const double span = (double)(span_bytes ? span_bytes : a.in_len);
   const double mean = span / (double)(a.n ? a.n : 1) * kPT;
   const double lo = 1.04 * mean + 256.0, hi = std::max(factor * mean + pad, lo);
-  const uint32_t rt = (kPT * rec_size + 16 + 15) & ~15u;
+  const uint32_t rt = regrec ? 0u : (kPT * rec_size + 16 + 15) & ~15u;
   double cap = hi;
   for (uint32_t w = 8; w >= 1; --w) {
     // wire bytes that fit w workgroups (the region is whole 4 KiB staging rounds)
@@ -82,17 +83,31 @@ uint32_t program_decode_wire_cap(const DecodeArgs& a, uint32_t rec_size, uint64_
   return ((uint32_t)cap) & ~15u;
 }
 
-uint32_t program_decode_lds(uint32_t wire_cap, uint32_t rec_size) {
-  return prog::decode_wire_region(wire_cap) + ((kPT * rec_size + 16 + 15) & ~15u);
+uint32_t program_decode_lds(uint32_t wire_cap, uint32_t rec_size, bool regrec = false) {
+  return prog::decode_wire_region(wire_cap) + (regrec ? 0u : ((kPT * rec_size + 16 + 15) & ~15u));
 }
 
 hipError_t launch_program_decode(const DecodeArgs& a, const VProgram* d_prog, uint32_t rec_size,
                                  uint64_t* irregular, unsigned long long* n_irregular,
                                  hipStream_t stream, const JitKernels* jit, uint64_t span_bytes) {
   if (a.n == 0) return hipSuccess;
-  const uint32_t cap = program_decode_wire_cap(a, rec_size, span_bytes);
+  uint32_t cap = program_decode_wire_cap(a, rec_size, span_bytes, false);
   const uint64_t tiles = (a.n + kPT - 1) / kPT;
-  const uint32_t lds = program_decode_lds(cap, rec_size);
+  uint32_t lds = program_decode_lds(cap, rec_size, false);
+  // Records in registers (entry 2) where the LDS record tile holds the tile
+  // down to 3 workgroups per CU or fewer and dropping it fits more: config 4
+  // 1.86 -> 1.69 ms (3 -> 5 workgroups); at 5 (config 3) the per-lane record
+  // stores cost more than the residency gains (1.46 -> 1.78 ms).
+  // TGPU_DECODE_REGREC=0 / 1 forces it off / on (A/B).
+  if (jit && jit_has(jit, 2)) {
+    const char* v = getenv("TGPU_DECODE_REGREC");
+    const uint32_t cap2 = program_decode_wire_cap(a, rec_size, span_bytes, true);
+    const uint32_t lds2 = program_decode_lds(cap2, rec_size, true);
+    const uint32_t w1 = 163840 / lds, w2 = 163840 / lds2;
+    const bool rr = v ? v[0] == '1' : (w1 <= 3 && w2 > w1);
+    if (rr)
+      return jit_launch_decode(jit, a, tiles, cap2, lds2, irregular, n_irregular, stream, 2);
+  }
   if (jit) return jit_launch_decode(jit, a, tiles, cap, lds, irregular, n_irregular, stream);
   hipLaunchKernelGGL(program_decode_kernel, dim3((uint32_t)tiles), dim3(kPT), lds, stream, a,
                      d_prog, rec_size, cap, irregular, n_irregular);

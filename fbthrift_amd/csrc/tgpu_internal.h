@@ -451,6 +451,10 @@ struct JitKernels;
 enum JitGroup { JIT_DECODE = 0, JIT_ENCODE = 1, JIT_INDEX = 2, JIT_NESTED = 3, JIT_NINDEX = 4 };
 const JitKernels* jit_kernels(const VProgram& prog, int device, int group, uint64_t records,
                               uint64_t bytes, bool force);
+// Records of at most 128 bytes, S % 8 == 0, get a second compiled decode
+// that builds records in registers instead of an LDS record tile
+// (decode_tile kRS, JIT_DECODE entry 2).
+bool decode_regrec(uint32_t rec_size);
 // only_group >= 0: that group alone
 int jit_compile_check(const VProgram& P, const char* arch, char* log, uint64_t log_cap,
                       int only_group = -1);

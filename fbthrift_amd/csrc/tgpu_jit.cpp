@@ -73,7 +73,7 @@ std::string cache_key(const VProgram& P, int device, int group) {
 }
 
 const char* const kEntry[5][5] = {
-    {"tgpu_jit_decode", "tgpu_jit_decode_tail", nullptr, nullptr, nullptr},
+    {"tgpu_jit_decode", "tgpu_jit_decode_tail", "tgpu_jit_decode_rr", nullptr, nullptr},
     {"tgpu_jit_size", "tgpu_jit_write", nullptr, nullptr, nullptr},
     {"tgpu_jit_index_spec", "tgpu_jit_index_emit", "tgpu_jit_index_decode",
      "tgpu_jit_index_onepass", "tgpu_jit_index_onepass_decode"},
@@ -475,7 +475,16 @@ std::string gen_source(const VProgram& P, int group) {
          "uint32_t wire_cap, uint64_t* __restrict__ irr, unsigned long long* __restrict__ nirr) "
          "{\n"
          "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
-         "  prog::decode_tile(a, JP{}, kS, wire_cap, irr, nirr, smem);\n"
+      << "  prog::decode_tile(a, JP{}, kS, wire_cap, irr, nirr, smem);\n"
+         "}\n";
+  // the same with records built in registers (no LDS record tile): the host
+  // launches it when the record tile is what limits the workgroups per CU
+  if (group == JIT_DECODE && decode_regrec(P.rec_size))
+    o << "extern \"C\" __global__ __launch_bounds__(256) void tgpu_jit_decode_rr(DecodeArgs a, "
+         "uint32_t wire_cap, uint64_t* __restrict__ irr, unsigned long long* __restrict__ nirr) "
+         "{\n"
+         "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+         "  prog::decode_tile<JP, false, kS>(a, JP{}, kS, wire_cap, irr, nirr, smem);\n"
          "}\n";
   // the tolerant program's persistent strided-tail decode (stream-ordered
   // fixed-layout calls, DevResult tail_*): nothing to do — every workgroup
@@ -611,7 +620,7 @@ bool compile(const VProgram& P, int device, int group, JitKernels& J) {
   for (int k = 0; k < 5 && ok; ++k) {
     if (!kEntry[group][k]) continue;
     ok = hipModuleGetFunction(&J.f[k], J.mod, kEntry[group][k]) == hipSuccess;
-    if (!ok && group == JIT_DECODE && k == 1) {  // tolerant programs only
+    if (!ok && group == JIT_DECODE && (k == 1 || k == 2)) {  // (tolerant programs / small records)
       (void)hipGetLastError();
       J.f[k] = nullptr;
       ok = true;
@@ -646,6 +655,10 @@ const JitKernels* jit_kernels(const VProgram& P, int device, int group, uint64_t
             J->log.c_str());
   cache()[key] = J;  // a failure is remembered too: never retried
   return J->ok ? J : nullptr;
+}
+
+bool decode_regrec(uint32_t rec_size) {
+  return rec_size && rec_size <= 128 && rec_size % 8 == 0;
 }
 
 bool jit_has(const JitKernels* J, int which) { return J && which >= 0 && which < 5 && J->f[which]; }

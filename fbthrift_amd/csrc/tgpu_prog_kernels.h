@@ -78,11 +78,15 @@ __host__ __device__ __forceinline__ uint32_t decode_wire_region(uint32_t wire_ca
 struct TailStride {
   uint64_t first, pos, stride, r0;
 };
-template <class PP, bool kTail = false>
+// kRS > 0 (= S, a multiple of 8, <= 128): each lane builds its record in
+// registers and stores it with 8-byte stores (no LDS record tile: the
+// workgroup's LDS is the wire tile alone, so more workgroups share a CU).
+template <class PP, bool kTail = false, uint32_t kRS = 0>
 __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, uint32_t S,
                                             uint32_t wire_cap, uint64_t* __restrict__ irr,
                                             unsigned long long* __restrict__ nirr,
                                             uint8_t* smem, const TailStride& ts = {}) {
+  static_assert(kRS % 8 == 0 && kRS <= 128, "register record: whole 8-byte words");
   uint8_t* wire = smem;
   uint8_t* rtile = smem + decode_wire_region(wire_cap);
   const uint64_t r0 = kTail ? ts.r0 : (uint64_t)blockIdx.x * kPT;
@@ -117,7 +121,7 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
   }
   uint8_t* gout = a.recs + r0 * S;
   const uint32_t osh = (uint32_t)((uintptr_t)gout & 15);
-  {
+  if constexpr (kRS == 0) {
     const uint4 z = {0u, 0u, 0u, 0u};
     const uint32_t nz = (kPT * S + osh + 15) >> 4;
     for (uint32_t i = threadIdx.x; i < nz; i += kPT) ((uint4*)rtile)[i] = z;
@@ -135,8 +139,13 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
                            (((uintptr_t)a.arena - (uintptr_t)a.in) & 15) == 0;
   const uint32_t r = threadIdx.x;
   bool failed = false;
+  alignas(8) uint8_t rbuf[kRS ? kRS : 8];
   if (r < nrec) {
-    uint8_t* rec = rtile + osh + r * S;
+    uint8_t* rec = kRS ? rbuf : rtile + osh + r * S;
+    if constexpr (kRS != 0) {
+#pragma unroll
+      for (uint32_t b = 0; b < kRS; b += 8) *(uint64_t*)(rbuf + b) = 0;
+    }
     bool ok = tile_ok;
     if (ok) {
       const uint64_t s = L ? t0 + r * L : a.offs[r0 + r], e = L ? s + L : a.offs[r0 + r + 1];
@@ -148,6 +157,16 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
         uint32_t p = (uint32_t)(s - t0) + sh;
         const uint32_t pe = (uint32_t)(e - t0) + sh;
         ok = run_program<true>(P, src, c, p, pe, rec) && p == pe;
+      }
+    }
+    if constexpr (kRS != 0) {  // (the batch's records: 8- or 4-byte aligned)
+      uint8_t* go = gout + (uint64_t)r * kRS;
+      if (((uintptr_t)a.recs & 7) == 0) {
+#pragma unroll
+        for (uint32_t b = 0; b < kRS; b += 8) *(uint64_t*)(go + b) = *(const uint64_t*)(rbuf + b);
+      } else {
+#pragma unroll
+        for (uint32_t b = 0; b < kRS; b += 4) *(uint32_t*)(go + b) = *(const uint32_t*)(rbuf + b);
       }
     }
     if constexpr (kTail) {
@@ -192,6 +211,7 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
       }
     }
   }
+  if constexpr (kRS != 0) return;
   // record tile -> HBM
   const uint32_t end = osh + nrec * S;
   const uint32_t nvec = (end + 15) >> 4;

@@ -70,6 +70,22 @@ def test_decode_golden(gpu, codec, name, indexed):
 
 
 @pytest.mark.parametrize("name", helpers.case_names())
+@pytest.mark.parametrize("rr", ["0", "1"])
+def test_decode_golden_register_records(gpu, name, rr, monkeypatch):
+    """The compiled indexed decode with records built in registers
+    (tgpu_jit_decode_rr, no LDS record tile) and with the record tile, forced
+    either way (TGPU_DECODE_REGREC): the oracle's records and arena."""
+    monkeypatch.setenv("TGPU_JIT", "1")
+    monkeypatch.setenv("TGPU_DECODE_REGREC", rr)
+    c = helpers.Case(name)
+    st, rec, arena, nd, cons = gpu_decode(c.schema, c.protocol, c.wire, c.n, c.offsets, dev=gpu)
+    assert st.code == 0 and nd == c.n, st.as_tuple()
+    ost, orec, oarena, _, _ = oracle.decode(c.schema, c.protocol, c.wire, c.n, offsets=c.offsets)
+    assert np.array_equal(rec[: c.n * c.schema.record_size], orec[: c.n * c.schema.record_size])
+    helpers.assert_arena_equal(c.schema, orec, c.n, c.wire, arena, oarena)
+
+
+@pytest.mark.parametrize("name", helpers.case_names())
 def test_encode_golden(gpu, codec, name):
     c = helpers.Case(name)
     rec, sarena, larena = helpers.pack(c.schema, c.values, c.n)
