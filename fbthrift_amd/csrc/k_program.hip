@@ -95,16 +95,19 @@ hipError_t launch_program_decode(const DecodeArgs& a, const VProgram* d_prog, ui
   const uint64_t tiles = (a.n + kPT - 1) / kPT;
   uint32_t lds = program_decode_lds(cap, rec_size, false);
   // Records in registers (entry 2) where the LDS record tile holds the tile
-  // down to 3 workgroups per CU or fewer and dropping it fits more: config 4
-  // 1.86 -> 1.69 ms (3 -> 5 workgroups); at 5 (config 3) the per-lane record
-  // stores cost more than the residency gains (1.46 -> 1.78 ms).
+  // down to 3 workgroups per CU or fewer, dropping it fits more, and records
+  // are whole 64-byte halves of a cache line: config 4 (S 64) 1.86 -> 1.69 ms
+  // (3 -> 5 workgroups); config 2's S 72 records at the same residency
+  // measured slower (indexed 2.15 -> 2.39 ms: per-lane stores straddling
+  // lines), and at 5 workgroups (config 3) the per-lane record stores cost
+  // more than the residency gains (1.46 -> 1.78 ms).
   // TGPU_DECODE_REGREC=0 / 1 forces it off / on (A/B).
   if (jit && jit_has(jit, 2)) {
     const char* v = getenv("TGPU_DECODE_REGREC");
     const uint32_t cap2 = program_decode_wire_cap(a, rec_size, span_bytes, true);
     const uint32_t lds2 = program_decode_lds(cap2, rec_size, true);
     const uint32_t w1 = 163840 / lds, w2 = 163840 / lds2;
-    const bool rr = v ? v[0] == '1' : (w1 <= 3 && w2 > w1);
+    const bool rr = v ? v[0] == '1' : (rec_size % 64 == 0 && w1 <= 3 && w2 > w1);
     if (rr)
       return jit_launch_decode(jit, a, tiles, cap2, lds2, irregular, n_irregular, stream, 2);
   }
