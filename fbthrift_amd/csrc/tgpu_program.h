@@ -62,12 +62,17 @@ __device__ __forceinline__ void note_exception(bool flag, uint64_t i, DevResult*
 // Each lane reading back one word of every vector it DMA'd, after
 // vmcnt(0), made every such call clean (as did a 128-cycle pause, or
 // staging through registers, which costs 0.2 ms per call); the caller's
-// barrier then waits for these reads (lgkmcnt(0)). `first` = the lane's first
-// vector index, `step` = the vector stride between its DMAs, `n` = its DMAs.
+// barrier then waits for these reads (lgkmcnt(0)). One read of the lane's
+// last DMA'd vector is enough (round 4: the read is a FLAT access to the LDS
+// aperture, returned in order behind the wave's own DMA writes — DESIGN.md
+// §4.2): zero repairs on config 5 and the whole GPU suite green with it, and
+// 1-3 % off every LDS-DMA decode against a read per vector
+// (TGPU_SETTLE_EACH, A/B). `first` = the lane's first vector index, `step` =
+// the vector stride between its DMAs, `n` = its DMAs.
 __device__ __forceinline__ void lds_dma_settle(const uint8_t* lds, uint32_t first, uint32_t step,
                                                uint32_t n) {
   __builtin_amdgcn_s_waitcnt(0);  // (vmcnt(0) expcnt(0) lgkmcnt(0))
-#ifdef TGPU_SETTLE_ONE  // A/B: one read-back per lane (its last DMA'd vector)
+#ifndef TGPU_SETTLE_EACH
   if (n) (void)((const volatile uint32_t*)lds)[(first + (n - 1) * step) * 4];
 #else
   for (uint32_t k = 0; k < n; ++k)
