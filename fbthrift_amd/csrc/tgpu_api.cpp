@@ -51,6 +51,8 @@ struct tgpu_schema {
   VProgram nprog[3]{};
   VProgram* d_nprog[3] = {nullptr, nullptr, nullptr};  // (the index's AOT repair kernels read it)
   uint32_t nprog_depth[3] = {0, 0, 0};
+  // a recursive schema's unrolled program (VOP_DEFER): decode / index only
+  bool nprog_defer[3] = {false, false, false};
   // the wire bytes per record (x16) of the last batch whose size this schema
   // learned (blocking encode / size calls), by protocol id: sizes the
   // compiled write pass's LDS output tile (enc_out_cap)
@@ -542,7 +544,7 @@ uint32_t compact_ctype(uint32_t t) {  // CompactProtocol-inl.h:48-69 TTypeToCTyp
 }
 
 bool push_op(VProgram& P, const VOp& op) {
-  if (P.n_ops >= (uint32_t)kMaxProgramOps) return false;
+  if (P.n_ops >= (uint32_t)kMaxNestedOps) return false;
   P.ops[P.n_ops++] = op;
   return true;
 }
@@ -564,12 +566,18 @@ bool emit_container(const tgpu_schema& sc, uint32_t ttype, uint32_t et, uint32_t
 
 // The structs whose ops are being emitted (nested programs): a struct that
 // contains itself (a recursive schema, through a container or a boxed field)
-// has no finite straight-line program; it stays with the general kernels.
+// has no finite straight-line program. Its first t_unroll levels are
+// unrolled; a value one level deeper is a VOP_DEFER, which hands the record
+// to the general kernels when it is present (t_deferred: one was emitted).
+// t_unroll 0: recursive schemas stay with the general kernels.
 thread_local std::vector<uint32_t> t_open_structs;
+thread_local uint32_t t_unroll = 0;
+thread_local bool t_deferred = false;
 struct OpenStruct {
   bool ok;
   explicit OpenStruct(uint32_t si) {
-    ok = std::find(t_open_structs.begin(), t_open_structs.end(), si) == t_open_structs.end();
+    ok = (uint32_t)std::count(t_open_structs.begin(), t_open_structs.end(), si) <
+         std::max<uint32_t>(t_unroll, 1);
     if (ok) t_open_structs.push_back(si);
   }
   ~OpenStruct() {
@@ -586,7 +594,11 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
   const bool un = (sd.flags & TGPU_STRUCT_UNION) != 0;
   if (un && !nested) return false;
   const OpenStruct open(si);
-  if (nested && !open.ok) return false;  // recursive: the general kernels
+  if (nested && !open.ok) {  // recursive, past the unrolled levels
+    if (!t_unroll) return false;
+    t_deferred = true;
+    return push_op(P, make_op(VOP_DEFER));
+  }
   int32_t prev = 0;
   const uint32_t sbegin = P.n_ops;
   if (nested) {
@@ -878,21 +890,42 @@ bool emit_container(const tgpu_schema& sc, uint32_t ttype, uint32_t et, uint32_t
 
 // The nested program of a schema whose containers hold structs or scalar
 // lists (every field unqualified / required, no maps, no strings inside
-// containers): compiled by JIT_NESTED only.
-bool build_nested_program(const tgpu_schema& sc, int proto, VProgram& P, uint32_t& depth) {
-  P = VProgram{};
-  P.protocol = (uint32_t)proto;
-  P.rec_size = sc.structs[0].size;
-  depth = 0;
-  t_open_structs.clear();
-  return emit_program(sc, 0, 0, proto, P, true, 0, &depth);
+// containers): compiled by JIT_NESTED only. A recursive schema unrolls as
+// many levels as fit the op budget, at most TGPU_NESTED_UNROLL (default 16;
+// 0: none — such schemas keep the general kernels); *deferred: the program
+// holds VOP_DEFERs (decode / measure only: the writer stays general).
+bool build_nested_program(const tgpu_schema& sc, int proto, VProgram& P, uint32_t& depth,
+                          bool* deferred = nullptr) {
+  const char* v = getenv("TGPU_NESTED_UNROLL");
+  const uint32_t max_unroll = v ? (uint32_t)std::min(atoi(v) < 0 ? 0 : atoi(v), 64) : 16u;
+  if (deferred) *deferred = false;
+  for (uint32_t k = max_unroll ? max_unroll : 1; k >= 1; --k) {
+    P = VProgram{};
+    P.protocol = (uint32_t)proto;
+    P.rec_size = sc.structs[0].size;
+    depth = 0;
+    t_open_structs.clear();
+    t_unroll = max_unroll ? k : 0;
+    t_deferred = false;
+    const bool ok = emit_program(sc, 0, 0, proto, P, true, 0, &depth);
+    const bool rec = t_deferred;
+    t_unroll = 0;
+    if (ok) {
+      if (deferred) *deferred = rec;
+      return true;
+    }
+    // (a schema that is not recursive, or whose failure is not the op
+    // budget, fails the same way at every level)
+    if (!max_unroll || (!rec && P.n_ops < (uint32_t)kMaxNestedOps)) break;
+  }
+  return false;
 }
 
 bool build_program(const tgpu_schema& sc, int proto, VProgram& P, bool tolerant = false) {
   P = VProgram{};
   P.protocol = (uint32_t)proto;
   P.rec_size = sc.structs[0].size;
-  if (!emit_program(sc, 0, 0, proto, P)) return false;
+  if (!emit_program(sc, 0, 0, proto, P) || P.n_ops >= (uint32_t)kMaxProgramOps) return false;
   VOp stop = make_op(VOP_CONST);
   stop.hdr_len = 1;
   const tgpu_struct_desc& root = sc.structs[0];
@@ -1114,11 +1147,12 @@ uint64_t measure_scratch(const tgpu_schema* s) {
 // none — no nested program, a height below its nesting (decode),
 // TGPU_NESTED=0, not compiled).
 const JitKernels* nested_jit(const tgpu_schema* schema, int protocol, uint64_t n, int32_t height,
-                             int32_t max_depth) {
+                             int32_t max_depth, bool writer = false) {
   const char* v = getenv("TGPU_NESTED");
   if (v && v[0] == '0') return nullptr;
   const int q = prog_protocol(schema, protocol);
   if (q < 0 || !schema->has_nprog[q] || n == 0) return nullptr;
+  if (writer && schema->nprog_defer[q]) return nullptr;  // (no deferred records on write)
   const int32_t need = (int32_t)schema->nprog_depth[q] + 1;
   if (height < need || max_depth < need) return nullptr;
   return jit_kernels(schema->nprog[q], schema->device, JIT_NESTED, n, 0, false);
@@ -1128,13 +1162,13 @@ const JitKernels* nested_jit(const tgpu_schema* schema, int protocol, uint64_t n
 // then the general decoder over the records it left; false: no such kernel
 // (no nested program, a height below its nesting, TGPU_NESTED=0, not
 // compiled), the caller runs the general decoder.
-// TGPU_NESTED_SRC=hbm: the unstaged variant (A/B).
+// TGPU_NESTED_SRC=hbm / lds: the unstaged / staged variant (A/B).
 bool launch_nested_decode(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
                           const DecodeArgs& a, hipStream_t s, hipError_t& e) {
   const char* v = getenv("TGPU_NESTED_SRC");
-  const bool hbm = v && !strcmp(v, "hbm");
-  v = getenv("TGPU_NESTED_RTILE");  // A/B: 0 = records straight to HBM, no LDS record tile
-  bool rtile = !(v && v[0] == '0');
+  bool hbm = v && !strcmp(v, "hbm");
+  const char* rv = getenv("TGPU_NESTED_RTILE");  // A/B: 0 = records straight to HBM, no LDS record tile
+  bool rtile = !(rv && rv[0] == '0');
   const JitKernels* J =
       nested_jit(schema, protocol, a.n, a.height ? a.height : a.max_depth, a.max_depth);
   if (!J) return false;
@@ -1153,7 +1187,14 @@ bool launch_nested_decode(tgpu_context* ctx, const tgpu_schema* schema, int prot
   // records of ~300 B and more) is dropped: records go straight to HBM
   // (entry 1), the wire tile keeps the LDS
   if (rt && rt + 4096.0 + 4096.0 + 32.0 > lds_max) rtile = false, rt = 0;
-  const double room = lds_max - rt - 4096.0 - 32.0;
+  double room = lds_max - rt - 4096.0 - 32.0;
+  // a mean tile the wire tile cannot hold would fail every tile's staging
+  // (all its records to the general decoder — the golden trees, ~1.5 KB a
+  // record): the record tile gives way first, then the staging (records
+  // read from HBM, entry 1 with wire_cap 0); TGPU_NESTED_SRC=lds keeps it
+  if (cap > room && rt && cap <= lds_max - 4096.0 - 32.0)
+    rtile = false, rt = 0, room = lds_max - 4096.0 - 32.0;
+  if (cap > room && !hbm && !(v && !strcmp(v, "lds"))) hbm = true;
   if (cap > room) cap = room;
   if (cap < 4096.0) cap = 4096.0;
   const uint32_t wire_cap = (uint32_t)cap & ~15u;
@@ -1589,7 +1630,8 @@ int tgpu_schema_create_ex(const tgpu_struct_desc* structs, uint32_t n_structs,
     // the nested program: schemas with containers of structs / containers,
     // and schemas with no canonical record program (optional fields)
     if (s->nested || !flat)
-      s->has_nprog[proto] = build_nested_program(*s, proto, s->nprog[proto], s->nprog_depth[proto]);
+      s->has_nprog[proto] = build_nested_program(*s, proto, s->nprog[proto], s->nprog_depth[proto],
+                                                 &s->nprog_defer[proto]);
     if (s->has_nprog[proto] &&
         (hipMalloc(&s->d_nprog[proto], sizeof(VProgram)) != hipSuccess ||
          hipMemcpy(s->d_nprog[proto], &s->nprog[proto], sizeof(VProgram), hipMemcpyHostToDevice) !=
@@ -1865,7 +1907,7 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
         e = launch_program_encode(a, schema->d_prog[prog_protocol(schema, protocol)], ctx->d_scan_part, false, s,
                                   schema_jit(schema, protocol, JIT_ENCODE, n, 0));
       else {  // (the writer has no depth limit: height / max_depth do not apply)
-        const JitKernels* nj = nested_jit(schema, protocol, n, INT32_MAX, INT32_MAX);
+        const JitKernels* nj = nested_jit(schema, protocol, n, INT32_MAX, INT32_MAX, true);
         if (nj) a.out_cap = nested_out_cap(schema, protocol);
         e = launch_general_encode(a, protocol, nb, s, nj);
       }
@@ -1930,7 +1972,7 @@ int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol
       if (e == hipSuccess) e = launch_size_offsets(a, (n + 255) / 256, s);
     } else {
       e = launch_general_size(a, protocol, (n + 255) / 256, s,
-                              nested_jit(schema, protocol, n, INT32_MAX, INT32_MAX));
+                              nested_jit(schema, protocol, n, INT32_MAX, INT32_MAX, true));
     }
   }
   if (e == hipSuccess && n) e = launch_encode_finish(a, protocol, 0, s);

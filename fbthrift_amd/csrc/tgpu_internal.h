@@ -188,6 +188,10 @@ enum VOpKind : uint8_t {
   // it) up to its VOP_BOX_END (hdr_len: one past it); member: the field's span
   VOP_BOX = 14,
   VOP_BOX_END = 15,
+  // a recursive schema's struct past the levels its nested program unrolls
+  // (build_nested_program): the record is handed to the general kernels
+  // when its value is read; such a program has no writer (nprog_defer)
+  VOP_DEFER = 16,
 };
 enum VElemKind : uint8_t {
   VEL_FIXED = 1,   // big-endian fixed width (Binary ints, doubles/floats, bytes)
@@ -215,13 +219,15 @@ struct VOp {
 // scalars or strings — a newer writer's appended fields
 // (deserialize_struct.whisker: unknown ids go to skip).
 constexpr uint8_t kStopSkipsUnknown = 1;
-constexpr int kMaxProgramOps = 128;
+constexpr int kMaxProgramOps = 128;  // flat record programs
+// nested programs (op indices and value-op counts are bytes: at most 255)
+constexpr int kMaxNestedOps = 255;
 struct VProgram {
   uint32_t n_ops;
   uint32_t rec_size;
   uint32_t protocol;
   uint32_t has_list;
-  VOp ops[kMaxProgramOps];
+  VOp ops[kMaxNestedOps];
 };
 
 // Device-side result slot of a context (one per in-flight call).

@@ -271,6 +271,11 @@ void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t sto
       ++k;
       continue;
     }
+    if (v.kind == VOP_DEFER) {  // a recursive struct past the unrolled levels
+      o << in << "return false;\n";
+      ++k;
+      continue;
+    }
     if (enc) {
       if (v.kind != VOP_ISSET)
         o << in << "if (!enc_op(" << op << ", kCompact, " << b << ", sbase, lbase, o)) return false;\n";
@@ -294,9 +299,11 @@ std::string gen_source(const VProgram& P, int group) {
   // a strict program (no root STOP that skips appended fields) is generated
   // without that path: left in, the dead branch cost config 4's decode 39 %
   // (1.86 -> 2.58 ms; the compiler does not fold it away)
-  bool tails = false;
-  for (uint32_t k = 0; k < P.n_ops; ++k)
+  bool tails = false, defer = false;
+  for (uint32_t k = 0; k < P.n_ops; ++k) {
     tails |= P.ops[k].kind == VOP_CONST && P.ops[k].elem_kind == kStopSkipsUnknown;
+    defer |= P.ops[k].kind == VOP_DEFER;  // a recursive schema's unrolled program
+  }
   if (!tails) o << "#define TGPU_NO_TAILS 1\n";
   o << "#include \"tgpu_prog_kernels.h\"\n"
        "namespace {\n"
@@ -353,7 +360,11 @@ std::string gen_source(const VProgram& P, int group) {
       << (P.protocol == TGPU_PROTOCOL_BINARY ? "false" : "true")
       << ";\n"
          "template <class Src>\n"
-         "__device__ __forceinline__ bool nmeas(const Src& src, const Ctx& c, uint32_t& p, "
+         // a recursive schema's unrolled walk is called, not inlined at each
+         // of its call sites (chain, 10 levels: 36 -> 6.5 s to compile; the
+         // index is not these schemas' hot path)
+      << (defer ? "__device__ __noinline__" : "__device__ __forceinline__")
+      << " bool nmeas(const Src& src, const Ctx& c, uint32_t& p, "
          "const uint32_t end) {\n"
          "  Win W;\n"
          "  uint8_t* rec = nullptr;\n"
@@ -443,8 +454,12 @@ std::string gen_source(const VProgram& P, int group) {
          "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
          "  if (wire_cap) nested_decode_tile<false>(a, NR{}, kS, kCompact, wire_cap, irr, nirr, smem);\n"
          "  else nested_decode_hbm(a, NR{}, kS, kCompact, irr, nirr);\n"
-         "}\n"
-         "namespace {\n"
+         "}\n";
+    // a recursive schema's unrolled program (VOP_DEFER) reads only: its
+    // records are written by the general writer (nested_jit), so no writer
+    // is generated (it roughly doubled the compile)
+    if (defer) return o.str();
+    o << "namespace {\n"
          "template <class O>\n"
          "__device__ __forceinline__ bool nenc(const uint8_t* rec, const uint8_t* sbase, "
          "const uint8_t* lbase, O& o) {\n";
@@ -620,7 +635,9 @@ bool compile(const VProgram& P, int device, int group, JitKernels& J) {
   for (int k = 0; k < 5 && ok; ++k) {
     if (!kEntry[group][k]) continue;
     ok = hipModuleGetFunction(&J.f[k], J.mod, kEntry[group][k]) == hipSuccess;
-    if (!ok && group == JIT_DECODE && (k == 1 || k == 2)) {  // (tolerant programs / small records)
+    // (tolerant programs / small records; a deferring nested program's writer)
+    if (!ok && ((group == JIT_DECODE && (k == 1 || k == 2)) ||
+                (group == JIT_NESTED && (k == 2 || k == 3)))) {
       (void)hipGetLastError();
       J.f[k] = nullptr;
       ok = true;
@@ -674,6 +691,7 @@ hipError_t jit_launch_decode(const JitKernels* J, const DecodeArgs& a, uint64_t 
 
 hipError_t jit_launch_encode(const JitKernels* J, bool write, const EncodeArgs& a, uint64_t grid,
                              uint32_t lds, hipStream_t s, int first) {
+  if (!jit_has(J, first + (write ? 1 : 0))) return hipErrorInvalidDeviceFunction;
   EncodeArgs x = a;
   void* p[] = {&x};
   return launch(J->f[first + (write ? 1 : 0)], grid, lds, s, p);

@@ -7,10 +7,12 @@ every record off the canonical form to the general decoder.
 
 CPU: the nested programs of the bench schema (tests/../bench.py NESTED_TABLE:
 {i64, list<Item>, list<list<i32>>}) and of maps / string elements compile for
-gfx950 in both protocols; recursive schemas have none. GPU: 40 Ki records of that schema against the oracle's decode of
-the same stream, and the nested kernel against the general decoder
+gfx950 in both protocols; recursive schemas an unrolled one. GPU: 40 Ki
+records of that schema against the oracle's decode of the same stream, and the nested kernel against the general decoder
 (TGPU_NESTED=0) bit for bit, incl. records and arena bytes; the golden nested
 cases under TGPU_JIT=1 are in test_nested_containers.py."""
+import os
+
 import numpy as np
 import pytest
 
@@ -40,9 +42,16 @@ def test_nested_program_scope():
     mbool = [[[1, T_LIST, T_MAP, 0, -1, 0, [T_MAP, T_I32, T_BOOL, -1]]]]
     rc, log = compile_check(Schema.from_table(mbool), 2, arch="")
     assert rc == 0, log
-    # struct Tree {1: list<Tree> kids} (recursive): none (general reader)
+    # struct Tree {1: list<Tree> kids} (recursive): unrolled (deeper records:
+    # the general reader); none with TGPU_NESTED_UNROLL=0
     tree = [[[1, T_LIST, T_STRUCT, 0, 0]]]
-    rc, _ = compile_check(Schema.from_table(tree), 0, arch="")
+    rc, log = compile_check(Schema.from_table(tree), 0, arch="")
+    assert rc == 0, log
+    os.environ["TGPU_NESTED_UNROLL"] = "0"
+    try:
+        rc, _ = compile_check(Schema.from_table(tree), 0, arch="")
+    finally:
+        del os.environ["TGPU_NESTED_UNROLL"]
     assert rc == 22
     # map<i32, Item>, map<string, list<string>>, list<map<i32, string>>: one each
     for t in ([[[1, T_MAP, T_I32, 0, 1, T_STRUCT]], [[1, T_I32, 0, 0, -1]]],

@@ -3,7 +3,9 @@ reader: boxed struct fields (cpp.ref / thrift.box, unqualified and optional),
 struct and container map keys, and bools inside maps (Compact writes a
 container bool as a byte 1 / 2, CompactProtocol-inl.h:692-701; Binary as
 0 / 1, a byte >= 2 throws). Recursive schemas (tree / chain) have no finite
-straight-line program and stay with the general kernels.
+straight-line program: theirs unrolls a bounded number of struct levels,
+and a record nesting deeper reaches a VOP_DEFER and goes to the general
+decoder (decode and index only; such programs have no writer).
 
 Reference semantics: deserialize_field.whisker:21-23,49-51 (a boxed field's
 fresh object, pointed to once read), serialize_field.whisker:44-49 (a null
@@ -11,7 +13,8 @@ unqualified boxed field is written as an empty struct),
 TableBasedSerializerImpl.h:300-407 (maps with struct / container keys),
 EncodeHelpers.h:188-205 (pairs inserted once read).
 
-CPU: the programs exist (compile for gfx950); recursive schemas have none.
+CPU: the programs exist (compile for gfx950); recursive schemas have
+unrolled ones (none with TGPU_NESTED_UNROLL=0).
 GPU: the nested program's encode gives the oracle's bytes; its decode the
 oracle's records and arena, indexed and unindexed, with no record left to
 the general decoder (tgpu_index_stats 'general'); the general kernels
@@ -71,15 +74,16 @@ class Case:
 
 
 @pytest.mark.parametrize("protocol", [0, 2])
-def test_programs_exist(protocol):
+def test_programs_exist(protocol, monkeypatch):
     """TABLE compiles (Binary; Compact generated only), keyed has a program,
-    the recursive schemas none."""
+    the recursive schemas an unrolled one (none with TGPU_NESTED_UNROLL=0)."""
     rc, log = compile_check(Schema.from_table(TABLE), protocol, arch="gfx950" if protocol == 0 else "")
     assert rc == 0, log
-    for name in ("keyed",):
+    for name in ("keyed", "tree", "chain"):
         rc, log = compile_check(Schema.from_table(nh.manifest()["nested_schemas"][name]), protocol,
                                 arch="")
         assert rc == 0, log
+    monkeypatch.setenv("TGPU_NESTED_UNROLL", "0")
     for name in ("tree", "chain"):  # recursive: none
         rc, _ = compile_check(Schema.from_table(nh.manifest()["nested_schemas"][name]), protocol,
                               arch="")
@@ -162,6 +166,68 @@ def test_gpu_golden_keyed_through_the_program(gpu, name, monkeypatch):
     assert st.code == 0 and nd == c.n
     assert Ser.context().index_stats()["general"] == 0
     assert nh.materialize_batch(c, rec.cpu().numpy(), arena.cpu().numpy()) == c.values
+
+
+def _levels(name, v):
+    """Struct levels of a golden tree (Tree {v, kids, tag}) / chain (Node {v,
+    next, leaf}) record."""
+    if name.startswith("tree"):
+        return 1 + max([_levels(name, k) for k in v[1]] or [0])
+    n = 0
+    while v is not None:
+        n, v = n + 1, v[1]
+    return n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["tree_binary", "tree_compact", "chain_binary", "chain_compact"])
+@pytest.mark.parametrize("unroll", [None, 6, 12])
+def test_gpu_golden_recursive_through_the_program(gpu, name, unroll, monkeypatch):
+    """The recursive schemas (Tree {list<Tree> kids}, Node {optional boxed
+    Node next}) through their unrolled nested programs: a record whose
+    structs nest deeper than the unrolled levels reaches a VOP_DEFER and is
+    the general decoder's — exactly those, no other. Default unrolling: 16
+    levels (Tree, 9 ops a level) / as many as fit 255 ops (Node, 18 ops a
+    level: 14). Records and arena byte-equal the oracle's; the unindexed
+    stream (nested index walk) the same; the records write back to the
+    golden bytes (through the general writer: such programs have none)."""
+    import torch
+
+    from fbthrift_amd import serializer as SZ
+
+    monkeypatch.setenv("TGPU_JIT", "1")
+    monkeypatch.setenv("TGPU_NESTED", "1")
+    if unroll:
+        monkeypatch.setenv("TGPU_NESTED_UNROLL", str(unroll))
+    else:
+        monkeypatch.delenv("TGPU_NESTED_UNROLL", raising=False)
+    c = nh.NestedCase(name)
+    k = unroll or (16 if name.startswith("tree") else 14)
+    deep = sum(_levels(name, v) > k for v in c.values)
+    gs = SZ.GpuSchema(c.schema)
+    assert gs.compile(c.protocol)
+    Ser = {0: SZ.BinarySerializer, 2: SZ.CompactSerializer}[c.protocol]
+    w = _t(np.frombuffer(c.wire, np.uint8), gpu)
+    offs = _t(c.offsets.astype(np.int64), gpu)
+    rec, arena, st, nd, cons = Ser.deserialize_status(gs, w, c.n, offs)
+    assert st.code == 0 and nd == c.n and cons == len(c.wire), st.as_tuple()
+    assert Ser.context().index_stats()["general"] == deep
+    assert deep < c.n
+    ost, orec, oarena, ond, _ = oracle.decode(c.schema, c.protocol, c.wire, c.n,
+                                              offsets=c.offsets.astype(np.uint64))
+    assert ost.code == 0 and ond == c.n
+    S = c.layout.size[0]
+    grec, garena = rec.cpu().numpy(), arena.cpu().numpy()
+    assert np.array_equal(grec[: c.n * S], orec[: c.n * S])
+    assert np.array_equal(garena[: oarena.size], oarena)
+    assert nh.materialize_batch(c, grec, garena) == c.values
+    urec, uarena, ust, und, ucons = Ser.deserialize_status(gs, w, c.n, None)
+    assert ust.code == 0 and und == c.n and ucons == len(c.wire), ust.as_tuple()
+    assert nh.materialize_batch(c, urec.cpu().numpy(), uarena.cpu().numpy()) == c.values
+    wire, woffs = Ser.serialize(gs, rec, c.n, w, arena)
+    torch.cuda.synchronize()
+    assert wire.cpu().numpy().tobytes() == c.wire
+    assert np.array_equal(woffs.cpu().numpy().astype(np.uint64), c.offsets.astype(np.uint64))
 
 
 @pytest.mark.gpu
