@@ -34,6 +34,7 @@ __global__ void result_init_kernel(DevResult* res, uint64_t n) {
   res->n_irregular = 0;
   res->first_start = kNone;
   res->n_deep = 0;
+  res->n_deep2 = 0;
   res->n_deep_chunks = 0;
   res->first_misfit = kNone;
   res->tail_first = kNone;
@@ -105,16 +106,35 @@ __global__ __launch_bounds__(256) void general_decode_tile_kernel(DecodeArgs a,
 }
 
 // The records the bulk passes deferred (a skip nested past the private
-// frames): each lane keeps max_depth frames in HBM.
+// frames): each lane keeps max_depth frames in HBM. With a wide tier
+// (a.deep.wlanes), `wide` reads the deferred list on its wlanes lanes of
+// kWideFrames frames and passes a record nesting deeper still (kErrDeep from
+// its full slab) to list2, which the max_depth lanes then read.
 template <int P>
-__global__ __launch_bounds__(64) void deep_decode_kernel(DecodeArgs a) {
+__global__ __launch_bounds__(64) void deep_decode_kernel(DecodeArgs a, int wide) {
   const uint32_t lane = blockIdx.x * 64 + threadIdx.x;
-  if (lane >= a.deep.lanes) return;
-  const uint64_t m = *a.deep.count;
-  for (uint64_t k = lane; k < m; k += a.deep.lanes) {
-    const uint64_t i = a.deep.list[k];
-    const Reader r = decode_one<P>(a, i, (int)lane);
-    if (!r.ok()) atomicMin(&a.res->first_fail, (unsigned long long)i);
+  DecodeArgs b = a;
+  const uint64_t* list = a.deep.list;
+  uint64_t m;
+  if (wide) {
+    b.deep.slabs = a.deep.wslabs;
+    b.deep.slab_frames = kWideFrames;
+    b.deep.lanes = a.deep.wlanes;
+    b.deep.more = 1;
+    m = *a.deep.count;
+  } else if (a.deep.wlanes) {
+    list = a.deep.list2;
+    m = *a.deep.count2;
+  } else {
+    m = *a.deep.count;
+  }
+  if (lane >= b.deep.lanes) return;
+  for (uint64_t k = lane; k < m; k += b.deep.lanes) {
+    const uint64_t i = list[k];
+    const Reader r = decode_one<P>(b, i, (int)lane);
+    if (r.ok()) continue;
+    if (wide && r.err == kErrDeep) a.deep.list2[atomicAdd(a.deep.count2, 1ull)] = i;
+    else atomicMin(&a.res->first_fail, (unsigned long long)i);
   }
 }
 
@@ -302,6 +322,29 @@ __device__ __forceinline__ void attach_slab(Writer& w, const DeepArgs& d, int la
   if (lane < 0 || !d.slabs) return;
   w.deep = d.slabs + (uint64_t)lane * slab_lane_bytes(d.slab_frames);
   w.deep_cap = d.slab_frames;
+  w.deep_more = d.more != 0;
+}
+
+// A deep encode pass's tier (deep_decode_kernel's two tiers): the wide one
+// (wide != 0) reads the deferred list with the wide slabs; the max_depth
+// one reads list2 when there is a wide tier, else the deferred list.
+__device__ __forceinline__ EncodeArgs deep_tier(const EncodeArgs& a, int wide,
+                                                const uint64_t*& list, uint64_t& m) {
+  EncodeArgs b = a;
+  list = a.deep.list;
+  if (wide) {
+    b.deep.slabs = a.deep.wslabs;
+    b.deep.slab_frames = kWideFrames;
+    b.deep.lanes = a.deep.wlanes;
+    b.deep.more = 1;
+    m = *a.deep.count;
+  } else if (a.deep.wlanes) {
+    list = a.deep.list2;
+    m = *a.deep.count2;
+  } else {
+    m = *a.deep.count;
+  }
+  return b;
 }
 
 // Size of record i; lane >= 0: a deep-pass lane (HBM frames).
@@ -365,14 +408,22 @@ __global__ __launch_bounds__(256) void encode_size_kernel(EncodeArgs a, uint32_t
   if (threadIdx.x == 0) a.block_sums[blockIdx.x] = t;
 }
 
+// (the wide tier hands a record nesting past its slab to list2, sized by
+// the max_depth tier)
 template <int P>
-__global__ __launch_bounds__(64) void deep_size_kernel(EncodeArgs a) {
+__global__ __launch_bounds__(64) void deep_size_kernel(EncodeArgs a, int wide) {
   const uint32_t lane = blockIdx.x * 64 + threadIdx.x;
-  if (lane >= a.deep.lanes) return;
-  const uint64_t m = *a.deep.count;
-  for (uint64_t k = lane; k < m; k += a.deep.lanes) {
-    const uint64_t i = a.deep.list[k];
-    const Writer w = size_one<P>(a, i, (int)lane);
+  const uint64_t* list;
+  uint64_t m;
+  const EncodeArgs b = deep_tier(a, wide, list, m);
+  if (lane >= b.deep.lanes) return;
+  for (uint64_t k = lane; k < m; k += b.deep.lanes) {
+    const uint64_t i = list[k];
+    const Writer w = size_one<P>(b, i, (int)lane);
+    if (wide && w.err == kErrDeep) {
+      a.deep.list2[atomicAdd(a.deep.count2, 1ull)] = i;
+      continue;
+    }
     if (!w.ok()) {
       atomicMin(&a.res->first_fail, (unsigned long long)i);
       continue;
@@ -402,17 +453,21 @@ __global__ __launch_bounds__(256) void encode_write_kernel(EncodeArgs a, uint32_
   write_record<P>(w, sc, a.recs + i * a.rec_size, a.sbase, a.lbase);
 }
 
+// (the wide tier stops at a record its size pass handed on — same record,
+// same frames, same verdict — and the max_depth tier writes it whole)
 template <int P>
-__global__ __launch_bounds__(64) void deep_write_kernel(EncodeArgs a) {
+__global__ __launch_bounds__(64) void deep_write_kernel(EncodeArgs a, int wide) {
   const uint32_t lane = blockIdx.x * 64 + threadIdx.x;
-  if (lane >= a.deep.lanes) return;
-  const uint64_t m = *a.deep.count;
-  for (uint64_t k = lane; k < m; k += a.deep.lanes) {
-    const uint64_t i = a.deep.list[k];
+  const uint64_t* list;
+  uint64_t m;
+  const EncodeArgs b = deep_tier(a, wide, list, m);
+  if (lane >= b.deep.lanes) return;
+  for (uint64_t k = lane; k < m; k += b.deep.lanes) {
+    const uint64_t i = list[k];
     const uint64_t start = a.offs[i];
     if (a.res->first_fail <= i) continue;
     Writer w{a.out, start, a.cap, 0, 0};
-    attach_slab(w, a.deep, (int)lane);
+    attach_slab(w, b.deep, (int)lane);
     write_record<P, true>(w, a.sc, a.recs + i * a.rec_size, a.sbase, a.lbase);
   }
 }
@@ -527,8 +582,12 @@ hipError_t launch_fixed_probe(const DecodeArgs& a, int protocol, uint64_t L, hip
 
 hipError_t launch_deep_decode(const DecodeArgs& a, int protocol, hipStream_t stream) {
   if (!a.deep.lanes) return hipSuccess;
+  if (a.deep.wlanes)  // the wide tier first (its lanes return at once when none was deferred)
+    TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(deep_decode_kernel<P_>,
+                                                  dim3((a.deep.wlanes + 63) / 64), dim3(64), 0,
+                                                  stream, a, 1));
   TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(deep_decode_kernel<P_>, dim3((a.deep.lanes + 63) / 64),
-                                                dim3(64), 0, stream, a));
+                                                dim3(64), 0, stream, a, 0));
   return hipGetLastError();
 }
 
@@ -562,8 +621,12 @@ hipError_t launch_tail_decode_finish(const DecodeArgs& a, int protocol, uint64_t
 // frames): launched on every call, their lanes exit on an empty list.
 hipError_t launch_deep_size(const EncodeArgs& a, int protocol, hipStream_t stream) {
   if (!a.deep.lanes) return hipSuccess;
+  if (a.deep.wlanes)
+    TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(deep_size_kernel<P_>,
+                                                  dim3((a.deep.wlanes + 63) / 64), dim3(64), 0,
+                                                  stream, a, 1));
   TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(deep_size_kernel<P_>, dim3((a.deep.lanes + 63) / 64),
-                                                dim3(64), 0, stream, a));
+                                                dim3(64), 0, stream, a, 0));
   return hipGetLastError();
 }
 
@@ -591,9 +654,13 @@ hipError_t launch_general_encode(const EncodeArgs& a, int protocol, uint64_t n_b
   if (e != hipSuccess) return e;
   TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_write_kernel<P_>, grid, dim3(256), sb, stream, a,
                                                 sb));
+  if (a.deep.lanes && a.deep.wlanes)
+    TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(deep_write_kernel<P_>,
+                                                  dim3((a.deep.wlanes + 63) / 64), dim3(64), 0,
+                                                  stream, a, 1));
   if (a.deep.lanes)
     TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(deep_write_kernel<P_>, dim3((a.deep.lanes + 63) / 64),
-                                                  dim3(64), 0, stream, a));
+                                                  dim3(64), 0, stream, a, 0));
   return hipGetLastError();
 }
 

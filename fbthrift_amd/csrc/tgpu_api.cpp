@@ -53,6 +53,8 @@ struct tgpu_schema {
   uint32_t nprog_depth[3] = {0, 0, 0};
   // a recursive schema's unrolled program (VOP_DEFER): decode / index only
   bool nprog_defer[3] = {false, false, false};
+  // a struct reachable from itself (the deep passes' wide tier)
+  bool recursive = false;
   // the wire bytes per record (x16) of the last batch whose size this schema
   // learned (blocking encode / size calls), by protocol id: sizes the
   // compiled write pass's LDS output tile (enc_out_cap)
@@ -112,6 +114,9 @@ struct tgpu_context {
   uint64_t reserved = 0;  // records
   // deep-pass skip frames (DeepArgs): slab_lanes x slab_frames, grow-only
   uint8_t* d_slabs = nullptr;
+  uint8_t* d_wslabs = nullptr;  // the deep passes' wide tier (wslab_lanes x kWideFrames)
+  uint32_t wslab_lanes = 0;
+  uint64_t* d_deep2 = nullptr;  // records the wide tier leaves to the max_depth slabs
   uint64_t slab_frames = 0;
   uint32_t slab_lanes = 0;
   // stream indexer workspace (per chunk)
@@ -921,6 +926,23 @@ bool build_nested_program(const tgpu_schema& sc, int proto, VProgram& P, uint32_
   return false;
 }
 
+// Whether a struct is reachable from itself (tgpu_schema::recursive): the
+// nested emitter, one level unrolled, meets a struct already open. (A shape
+// the emitter refuses before that reads as not recursive: one deep tier.)
+bool schema_recursive(const tgpu_schema& sc) {
+  VProgram P{};
+  P.protocol = TGPU_PROTOCOL_BINARY;
+  P.rec_size = sc.structs[0].size;
+  uint32_t depth = 0;
+  t_open_structs.clear();
+  t_unroll = 1;
+  t_deferred = false;
+  (void)emit_program(sc, 0, 0, TGPU_PROTOCOL_BINARY, P, true, 0, &depth);
+  const bool rec = t_deferred;
+  t_unroll = 0;
+  return rec;
+}
+
 bool build_program(const tgpu_schema& sc, int proto, VProgram& P, bool tolerant = false) {
   P = VProgram{};
   P.protocol = (uint32_t)proto;
@@ -1023,11 +1045,13 @@ int ensure_workspace(tgpu_context* ctx, uint64_t n) {
   if (ctx->d_scan_part) (void)hipFree(ctx->d_scan_part);
   if (ctx->d_irr) (void)hipFree(ctx->d_irr);
   if (ctx->d_deep) (void)hipFree(ctx->d_deep);
+  if (ctx->d_deep2) (void)hipFree(ctx->d_deep2);
   ctx->d_offs = nullptr;
   ctx->d_block_sums = nullptr;
   ctx->d_scan_part = nullptr;
   ctx->d_irr = nullptr;
   ctx->d_deep = nullptr;
+  ctx->d_deep2 = nullptr;
   ctx->reserved = 0;
   const uint64_t tiles = (want + 255) / 256;
   if (hipMalloc(&ctx->d_offs, (want + 1) * sizeof(uint64_t)) != hipSuccess) return TGPU_ERR_HIP;
@@ -1038,6 +1062,7 @@ int ensure_workspace(tgpu_context* ctx, uint64_t n) {
     return TGPU_ERR_HIP;
   if (hipMalloc(&ctx->d_irr, want * sizeof(uint64_t)) != hipSuccess) return TGPU_ERR_HIP;
   if (hipMalloc(&ctx->d_deep, want * sizeof(uint64_t)) != hipSuccess) return TGPU_ERR_HIP;
+  if (hipMalloc(&ctx->d_deep2, want * sizeof(uint64_t)) != hipSuccess) return TGPU_ERR_HIP;
   ctx->reserved = want;
   return TGPU_OK;
 }
@@ -1046,12 +1071,25 @@ int ensure_workspace(tgpu_context* ctx, uint64_t n) {
 // frames per lane (the skip's depth check fires first; records nest through
 // containers, each a level of depth, or through boxed fields, past which
 // the slab's record frames are the limit: TGPU_ERR_UNSUPPORTED), up to
-// kMaxDeepFrames; as many lanes (<= 256) as fit 64 MiB. Deferred records are
-// rare (a value nested past the private frames), so the pass's width only
-// bounds its time, never its result.
-int ensure_deep(tgpu_context* ctx, int32_t max_depth) {
+// kMaxDeepFrames; as many lanes (<= 256) as fit 64 MiB. The pass's width
+// only bounds its time, never its result; for a recursive schema (`wide`)
+// whose slabs hold more than kWideFrames, the wide tier (DeepArgs, 256 MiB)
+// reads the deferred records first (such a schema defers most of its
+// records: TGPU_DEEP_WIDE=0 keeps one tier).
+int ensure_deep(tgpu_context* ctx, int32_t max_depth, bool wide = false) {
   const uint64_t want = std::min<uint64_t>(std::max<int64_t>((int64_t)max_depth + 2, 1),
                                            kMaxDeepFrames);
+  const char* wv = getenv("TGPU_DEEP_WIDE");
+  if (wide && want > kWideFrames && !ctx->d_wslabs && !(wv && wv[0] == '0')) {
+    const uint64_t lb = slab_lane_bytes(kWideFrames);
+    const uint32_t lanes =
+        (uint32_t)std::min<uint64_t>(kWideLanes, (256ull << 20) / lb) & ~63u;
+    if (hipMalloc(&ctx->d_wslabs, lanes * lb) != hipSuccess) {
+      ctx->d_wslabs = nullptr;
+      return TGPU_ERR_HIP;
+    }
+    ctx->wslab_lanes = lanes;
+  }
   if (ctx->d_slabs && ctx->slab_frames >= want) return TGPU_OK;
   if (ctx->d_slabs) (void)hipFree(ctx->d_slabs);
   ctx->d_slabs = nullptr;
@@ -1066,8 +1104,14 @@ int ensure_deep(tgpu_context* ctx, int32_t max_depth) {
 }
 
 DeepArgs deep_args(tgpu_context* ctx) {
+  // (the wide tier only when the slabs are deeper than it; TGPU_DEEP_WIDE=0:
+  // one tier, A/B)
+  const char* wv = getenv("TGPU_DEEP_WIDE");
+  const bool wide = ctx->d_wslabs && ctx->d_deep2 && ctx->slab_frames > kWideFrames &&
+                    !(wv && wv[0] == '0');
   return DeepArgs{ctx->d_deep, &ctx->d_res->n_deep, ctx->d_slabs, ctx->slab_frames,
-                  ctx->slab_lanes, 0};
+                  ctx->slab_lanes, 0, wide ? ctx->d_wslabs : nullptr, wide ? ctx->wslab_lanes : 0u,
+                  0, ctx->d_deep2, &ctx->d_res->n_deep2};
 }
 
 int32_t limit_depth(const tgpu_limits* limits) { return limits ? limits->max_depth : 12000; }
@@ -1253,7 +1297,7 @@ uint32_t prog_min_len(const VProgram& P) {
         break;
       case VOP_SEQ: case VOP_MSEQ:
         n += compact ? 1 : (o.kind == VOP_SEQ ? 5 : 6);
-        k = o.hdr_len - 1u;
+        if (o.hdr_len > k + 1) k = o.hdr_len - 1u;  // past the body
         break;
       case VOP_SEND: n += 1; break;
       default: break;
@@ -1346,7 +1390,10 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   const uint64_t lane_words = x.chunk == index_tile_bytes() ? C * index_tile_lanes() : 0;
   // stored starts: a tile holds at most chunk / min_len + 1 record starts
   const bool starts = lane_words && x.prog && index_starts_enabled();
-  const uint32_t min_len = prog_min_len(njit ? schema->nprog[pq] : schema->prog[pq]);
+  // (x.prog set: pq >= 0 — a Compact V1 stream of a schema with doubles has
+  // no program, and prog[-1] was read here)
+  const uint32_t min_len =
+      starts && pq >= 0 ? prog_min_len(njit ? schema->nprog[pq] : schema->prog[pq]) : 1u;
   x.st_cap = starts ? (uint32_t)std::min<uint64_t>(x.chunk / std::max<uint32_t>(min_len, 1) + 2,
                                                    2048)
                     : 0;
@@ -1625,6 +1672,7 @@ int tgpu_schema_create_ex(const tgpu_struct_desc* structs, uint32_t n_structs,
     tgpu_schema_destroy(s);
     return TGPU_ERR_HIP;
   }
+  s->recursive = schema_recursive(*s);
   for (int proto : {TGPU_PROTOCOL_BINARY, TGPU_PROTOCOL_COMPACT}) {
     const bool flat = build_program(*s, proto, s->prog[proto]);
     // the nested program: schemas with containers of structs / containers,
@@ -1793,6 +1841,8 @@ void tgpu_context_destroy(tgpu_context* c) {
   if (c->d_irr) (void)hipFree(c->d_irr);
   if (c->d_deep) (void)hipFree(c->d_deep);
   if (c->d_slabs) (void)hipFree(c->d_slabs);
+  if (c->d_wslabs) (void)hipFree(c->d_wslabs);
+  if (c->d_deep2) (void)hipFree(c->d_deep2);
   if (c->d_index) (void)hipFree(c->d_index);
   if (c->d_xrec) (void)hipFree(c->d_xrec);
   if (c->d_xarena) (void)hipFree(c->d_xarena);
@@ -1892,7 +1942,7 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   } else {
     const uint64_t nb = (n + 255) / 256;
     int rc = ensure_workspace(ctx, n);
-    if (!rc) rc = ensure_deep(ctx, 12000);
+    if (!rc) rc = ensure_deep(ctx, 12000, schema->recursive);
     if (rc) {
       fill_status(st, rc, 0, 0);
       return rc;
@@ -1942,7 +1992,7 @@ int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   }
   const hipStream_t s = (hipStream_t)stream;
   int rc = ensure_workspace(ctx, n);
-  if (!rc) rc = ensure_deep(ctx, 12000);
+  if (!rc) rc = ensure_deep(ctx, 12000, schema->recursive);
   if (rc) {
     fill_status(st, rc, 0, 0);
     return rc;
@@ -2008,7 +2058,7 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
   }
   const hipStream_t s = (hipStream_t)stream;
   int rc = ensure_workspace(ctx, n);
-  if (!rc) rc = ensure_deep(ctx, limit_depth(limits));
+  if (!rc) rc = ensure_deep(ctx, limit_depth(limits), schema->recursive);
   if (rc) {
     fill_status(st, rc, 0, 0);
     return rc;
@@ -2256,7 +2306,7 @@ int tgpu_decode_stream(tgpu_context* ctx, const tgpu_schema* schema, int protoco
   }
   const hipStream_t s = (hipStream_t)stream;
   int rc = ensure_workspace(ctx, max_records + 1);
-  if (!rc) rc = ensure_deep(ctx, limit_depth(limits));
+  if (!rc) rc = ensure_deep(ctx, limit_depth(limits), schema->recursive);
   if (rc) {
     fill_status(st, rc, 0, 0);
     return rc;
@@ -2361,7 +2411,7 @@ int tgpu_skim_batch_ex(tgpu_context* ctx, int protocol, const void* in, uint64_t
   }
   const hipStream_t s = (hipStream_t)stream;
   int rc = ensure_workspace(ctx, n);
-  if (!rc) rc = ensure_deep(ctx, limit_depth(limits));
+  if (!rc) rc = ensure_deep(ctx, limit_depth(limits));  // (schemaless: the skim's deep pass has one tier)
   if (rc) {
     fill_status(st, rc, 0, 0);
     return rc;
@@ -2410,7 +2460,7 @@ int tgpu_index_stream(tgpu_context* ctx, const tgpu_schema* schema, int protocol
     return TGPU_ERR_INVALID_ARGUMENT;
   }
   const hipStream_t s = (hipStream_t)stream;
-  const int drc = ensure_deep(ctx, limit_depth(limits));
+  const int drc = ensure_deep(ctx, limit_depth(limits), schema->recursive);
   if (drc) {
     fill_status(st, drc, 0, 0);
     return drc;

@@ -92,6 +92,7 @@ struct Reader {
   // skip frames past the private kMaxSkipDepth (nullptr: kErrDeep instead)
   uint8_t* deep;
   uint64_t deep_cap;  // frames at `deep`
+  bool deep_more;     // a larger slab follows (the wide tier): full is kErrDeep
 
   __device__ __forceinline__ bool ok() const { return err == 0; }
   __device__ __forceinline__ void fail(int32_t code, uint64_t off) {
@@ -169,6 +170,7 @@ __device__ __forceinline__ Reader make_reader(const uint8_t* in, uint64_t pos, u
   r.bool_val = false;
   r.deep = nullptr;
   r.deep_cap = 0;
+  r.deep_more = false;
   return r;
 }
 
@@ -421,7 +423,7 @@ __device__ void skip(Reader& r, uint32_t type, int32_t depth) {
   SkipFrame priv[kMaxSkipDepth];
   SkipFrame* const st = r.deep ? (SkipFrame*)r.deep : priv;
   const uint64_t cap = r.deep ? r.deep_cap : (uint64_t)kMaxSkipDepth;
-  const int32_t full = r.deep ? TGPU_ERR_UNSUPPORTED : kErrDeep;
+  const int32_t full = r.deep && !r.deep_more ? TGPU_ERR_UNSUPPORTED : kErrDeep;
   int sp = 0;
   uint32_t cur = type;
   int32_t cdepth = depth;
@@ -949,7 +951,7 @@ __device__ void read_record(Reader& r, const DevSchema& sc, uint8_t* rec, Arena&
   ReadFrame priv[kDeep ? 1 : kPrivFrames];
   ReadFrame* const st = kDeep ? slab_read_frames(r) : priv;
   const uint32_t cap = kDeep ? (uint32_t)r.deep_cap : (uint32_t)kPrivFrames;
-  const int32_t full = kDeep ? TGPU_ERR_UNSUPPORTED : kErrDeep;
+  const int32_t full = kDeep && !r.deep_more ? TGPU_ERR_UNSUPPORTED : kErrDeep;
   uint32_t sp = 0;  // frames saved below fr
   ReadFrame fr = struct_frame(0, rec);
   while (r.ok()) {
@@ -1197,6 +1199,7 @@ __device__ __forceinline__ void attach_slab(Reader& r, const DeepArgs& d, uint32
   if (!d.slabs) return;
   r.deep = d.slabs + (uint64_t)lane * slab_lane_bytes(d.slab_frames);
   r.deep_cap = d.slab_frames;
+  r.deep_more = d.more != 0;
 }
 
 // A lane whose reader failed: a value nested past its private skip frames
@@ -1258,6 +1261,7 @@ struct Writer {
   // a deep-pass lane's HBM slab (the reader's layout)
   uint8_t* deep = nullptr;
   uint64_t deep_cap = 0;
+  bool deep_more = false;  // the wide tier's slab: full is kErrDeep
   __device__ __forceinline__ bool ok() const { return err == 0; }
   __device__ __forceinline__ void fail(int32_t code, uint64_t off) {
     if (!err) {
@@ -1551,7 +1555,7 @@ __device__ __forceinline__ void write_record(Writer& w, const DevSchema& sc, con
   WriteFrame priv[kDeep ? 1 : kPrivFrames];
   WriteFrame* const st = kDeep ? (WriteFrame*)(w.deep + slab_skip_bytes(w.deep_cap)) : priv;
   const uint32_t cap = kDeep ? (uint32_t)w.deep_cap : (uint32_t)kPrivFrames;
-  const int32_t full = kDeep ? TGPU_ERR_UNSUPPORTED : kErrDeep;
+  const int32_t full = kDeep && !w.deep_more ? TGPU_ERR_UNSUPPORTED : kErrDeep;
   uint32_t sp = 0;
   st[sp++] = write_frame(sc, 0, rec);
   while (sp > 0 && w.ok()) {

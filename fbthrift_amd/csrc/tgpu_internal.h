@@ -77,13 +77,28 @@ constexpr int32_t kErrDeep = 0x10000;  // internal; never reaches a tgpu_status
 // Frames of one deep-pass lane are capped (the reference's recursion would
 // exhaust a thread stack long before): deeper -> TGPU_ERR_UNSUPPORTED.
 constexpr uint64_t kMaxDeepFrames = 1ull << 22;
+// The general kernels' deep passes (decode, size, write) have two tiers for
+// a recursive schema when max_depth allows more than kWideFrames: the wide
+// tier (up to kWideLanes lanes of kWideFrames frames, 256 MiB — a recursive
+// schema's records mostly nest up to a few hundred frames: a boxed chain
+// node takes 2) reads the deferred records first, and hands the ones
+// nesting deeper still to list2, which the max_depth slabs' lanes (at most
+// 256) read. With one tier a tree stream's deep records queued on ~60
+// lanes (10 s for 1 Mi golden trees, tools/recursive_bench.py).
+constexpr uint64_t kWideFrames = 256;
+constexpr uint32_t kWideLanes = 16384;
 struct DeepArgs {
   uint64_t* list;               // deferred records (or index chunks)
   unsigned long long* count;    // entries in list
   uint8_t* slabs;               // lanes x slab_lane_bytes(slab_frames)
   uint64_t slab_frames;
   uint32_t lanes;
+  uint32_t more;                // these slabs are the wide tier's (deep_decode_kernel)
+  uint8_t* wslabs;              // the wide tier: wlanes x slab_lane_bytes(kWideFrames)
+  uint32_t wlanes;              // (0: one tier)
   uint32_t pad;
+  uint64_t* list2;              // the wide tier's leftovers (count2 entries)
+  unsigned long long* count2;
 };
 // arena == nullptr with this capacity: list elements are read and validated
 // but not stored (the stream indexer measures records without output).
@@ -242,6 +257,7 @@ struct DevResult {
   unsigned long long n_irregular;      // program path: records sent to the general decoder
   unsigned long long first_start;      // stream index: first record start found
   unsigned long long n_deep;           // records deferred to the deep pass
+  unsigned long long n_deep2;          // of those, left by its wide tier
   unsigned long long n_deep_chunks;    // index chunks deferred to the deep emit pass
   unsigned long long first_misfit;     // fixed path: first exception not L bytes long
   // Stream-ordered fixed path, from the first misfit m on (tail_stride 0: none):

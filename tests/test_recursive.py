@@ -198,10 +198,15 @@ def nh_gpu():
 @pytest.mark.gpu
 @pytest.mark.parametrize("protocol", [0, 2])
 @pytest.mark.parametrize("indexed", [False, True])
-def test_gpu_deep_records(gpu, protocol, indexed):
+@pytest.mark.parametrize("wide", ["1", "0"])
+def test_gpu_deep_records(gpu, protocol, indexed, wide, monkeypatch):
     """Records nested far past the private frames: boxed chains (no height)
-    and list trees (height), decoded and encoded by the deep passes; the
-    device matches the oracle byte for byte (records, arena, wire)."""
+    and list trees (height), decoded and encoded by the deep passes — with
+    their wide tier (kWideFrames frames a lane: chain(2000) and tree(400)
+    nest past it and go on to the max_depth lanes) and without it
+    (TGPU_DEEP_WIDE=0); the device matches the oracle byte for byte
+    (records, arena, wire)."""
+    monkeypatch.setenv("TGPU_DEEP_WIDE", wide)
     tn = nh_gpu()
     vals = [chain(i % 7) for i in range(300)] + [chain(2000), chain(40)] + \
            [chain(i % 11) for i in range(300)]

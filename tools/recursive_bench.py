@@ -4,7 +4,9 @@ chain_*: Tree {v, list<Tree> kids, tag}, boxed Node chains), each replicated
 to ~1 Mi records, through the unrolled nested program (TGPU_NESTED=1) and
 through the general decoder alone (TGPU_NESTED=0). Prints one JSON line per
 (case, path): ms per call (device time of the whole decode call, buffers
-preallocated), wire GB/s, and how many records the general decoder took.
+preallocated), wire GB/s, and how many records the general decoder took;
+then the encode of the decoded records (the general writer). TGPU_DEEP_WIDE=0
+in the environment: the general kernels' deep pass without its wide tier.
 
   python tools/recursive_bench.py [--reps 10] [--copies 5000]"""
 import argparse
@@ -63,20 +65,39 @@ def main():
                                   ctypes.byref(st), ctypes.byref(nd), ctypes.byref(cons))
             assert st.code == 0 and nd.value == n, st.as_tuple()
 
-        for nested in ("1", "0"):
-            os.environ["TGPU_NESTED"] = nested
-            call()  # warm-up (and the first-call compile)
+        def timed(fn, reps):
+            fn()  # warm-up (and the first-call compile)
             torch.cuda.synchronize()
             t = time.perf_counter()
-            for _ in range(args.reps):
-                call()
+            for _ in range(reps):
+                fn()
             torch.cuda.synchronize()
-            ms = (time.perf_counter() - t) * 1e3 / args.reps
-            print(json.dumps({"case": name, "path": "nested" if nested == "1" else "general",
+            return (time.perf_counter() - t) * 1e3 / reps
+
+        for nested in ("1", "0"):
+            os.environ["TGPU_NESTED"] = nested
+            ms = timed(call, args.reps)
+            print(json.dumps({"case": name, "op": "decode",
+                              "path": "nested" if nested == "1" else "general",
+                              "deep_tiers": 1 if os.environ.get("TGPU_DEEP_WIDE") == "0" else 2,
                               "records": n, "wire_bytes": wire.numel(), "ms": round(ms, 3),
                               "wire_GBps": round(wire.numel() / ms / 1e6, 1),
                               "general_records": Ser.context().index_stats()["general"]}),
                   flush=True)
+        # encode (the general writer: a recursive schema's program has none)
+        out = torch.empty(wire.numel(), dtype=torch.uint8, device=dev)
+        woffs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+
+        def enc():
+            got, _ = Ser.serialize(gs, recs, n, wire, arena, out=out, offsets=woffs)
+            assert got.numel() == wire.numel()
+
+        ms = timed(enc, args.reps)
+        assert torch.equal(out, wire)
+        print(json.dumps({"case": name, "op": "encode", "path": "general",
+                          "deep_tiers": 1 if os.environ.get("TGPU_DEEP_WIDE") == "0" else 2,
+                          "records": n, "wire_bytes": wire.numel(), "ms": round(ms, 3),
+                          "wire_GBps": round(wire.numel() / ms / 1e6, 1)}), flush=True)
 
 
 if __name__ == "__main__":
