@@ -117,6 +117,16 @@ __device__ bool chain(const IndexArgs& a, uint64_t p, uint64_t hi, bool canonica
   out.err_off = 0;
   out.second = kNo;
   while (p < hi && out.count < max_count) {
+    // speculation without a program: a record starts with a root field's
+    // header or STOP (a false start's chain of garbage records dies early)
+    if (spec && canonical_first && !a.prog && p < a.in_len) {
+      const uint32_t b = a.in[p];
+      if (!((a.hmask[b >> 5] >> (b & 31)) & 1u)) {
+        out.code = TGPU_ERR_INDEX_MISMATCH;  // (internal: the candidate is rejected)
+        out.end = p;
+        return false;
+      }
+    }
     uint64_t q = 0;
     const int got = one_record<P>(a, p, limit, scratch, lane,
                                   !(canonical_first && out.count == 0 && a.prog), q, out);

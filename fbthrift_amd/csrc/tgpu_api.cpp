@@ -926,6 +926,39 @@ bool build_nested_program(const tgpu_schema& sc, int proto, VProgram& P, uint32_
   return false;
 }
 
+// The bytes a record of the root struct can start with (IndexArgs::hmask):
+// the header of a root field that can be the first one written — fields are
+// written in declaration order (serialize_struct.whisker), unqualified,
+// required and boxed ones always, so the candidates run up to the first of
+// those — Binary its type byte, Compact its short-form header (delta from 0,
+// ids 1..15; a bool either value) or the long form's type nibble alone; STOP
+// only when every field may be absent (an empty record; a union root).
+// A record whose first field is unknown to the schema fails the filter: the
+// speculation's fallback pass, which takes any record, covers it.
+void record_first_bytes(const tgpu_schema& sc, int protocol, uint32_t m[8]) {
+  for (int k = 0; k < 8; ++k) m[k] = 0;
+  auto set = [&](uint32_t b) { m[(b & 0xff) >> 5] |= 1u << (b & 31); };
+  const tgpu_struct_desc& root = sc.structs[0];
+  const bool un = (root.flags & TGPU_STRUCT_UNION) != 0;
+  bool always = false;
+  for (uint32_t k = 0; k < root.num_fields && !always; ++k) {
+    const tgpu_field_desc& f = sc.fields[root.first_field + k];
+    always = !un && (f.qualifier == TGPU_UNQUALIFIED || f.qualifier == TGPU_REQUIRED ||
+                     f.qualifier == TGPU_BOXED);
+    if (protocol == TGPU_PROTOCOL_BINARY) {
+      set(f.ttype);
+      continue;
+    }
+    const uint32_t cts[2] = {f.ttype == TGPU_T_BOOL ? 1u : compact_ctype(f.ttype),
+                             f.ttype == TGPU_T_BOOL ? 2u : compact_ctype(f.ttype)};
+    for (uint32_t ct : cts) {
+      if (f.id >= 1 && f.id <= 15) set(((uint32_t)f.id << 4) | ct);
+      else set(ct);
+    }
+  }
+  if (!always) set(0);
+}
+
 // Whether a struct is reachable from itself (tgpu_schema::recursive): the
 // nested emitter, one level unrolled, meets a struct already open. (A shape
 // the emitter refuses before that reads as not recursive: one deep tier.)
@@ -1366,6 +1399,11 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   if (njit) {
     x.prog = schema->d_nprog[pq];
     dec = nullptr;
+  }
+  if (x.prog) {
+    for (uint32_t& w : x.hmask) w = ~0u;
+  } else {
+    record_first_bytes(*schema, protocol, x.hmask);
   }
   x.chunk = index_chunk_bytes(end > begin ? end - begin : 0, x.prog != nullptr);
   x.window = (uint32_t)std::min<uint64_t>(x.chunk, 1024);

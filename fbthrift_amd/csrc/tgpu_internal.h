@@ -399,6 +399,10 @@ struct IndexArgs {
   // (launch_index) rather than in the emit tiles: emit writes starts only,
   // the finish keeps the fused decode's tail rule
   int32_t st_decode;
+  // schemas without a program: the bytes a record of the root struct can
+  // start with (a root field's header, or STOP), one bit each — every
+  // record of a speculated chain must (the fallback pass takes any)
+  uint32_t hmask[8];
 };
 
 // Workgroups of the grid-stride kernels whose lanes run the general reader
