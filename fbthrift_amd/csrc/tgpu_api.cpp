@@ -927,36 +927,49 @@ bool build_nested_program(const tgpu_schema& sc, int proto, VProgram& P, uint32_
 }
 
 // The bytes a record of the root struct can start with (IndexArgs::hmask):
-// the header of a root field that can be the first one written — fields are
-// written in declaration order (serialize_struct.whisker), unqualified,
-// required and boxed ones always, so the candidates run up to the first of
-// those — Binary its type byte, Compact its short-form header (delta from 0,
-// ids 1..15; a bool either value) or the long form's type nibble alone; STOP
-// only when every field may be absent (an empty record; a union root).
-// A record whose first field is unknown to the schema fails the filter: the
+// the header of a root field that can be the first one written. Generated
+// writers emit fields in declaration order (serialize_struct.whisker), or in
+// id order for a struct annotated @SerializeInFieldIdOrder
+// (t_whisker_generator.cc:232-236, fields_in_serialization_order) — the
+// schema descriptor does not say which, so both orders' candidates are taken:
+// in each, the fields up to the first one always written (unqualified,
+// required, boxed). Binary: the field's type byte; Compact: its short-form
+// header (delta from 0, ids 1..15; a bool either value) or the long form's
+// type nibble alone. STOP only when every field may be absent (an empty
+// record; a union root). A record whose first field is unknown to the
+// schema, or written in some third order, fails the filter: the
 // speculation's fallback pass, which takes any record, covers it.
 void record_first_bytes(const tgpu_schema& sc, int protocol, uint32_t m[8]) {
   for (int k = 0; k < 8; ++k) m[k] = 0;
   auto set = [&](uint32_t b) { m[(b & 0xff) >> 5] |= 1u << (b & 31); };
   const tgpu_struct_desc& root = sc.structs[0];
   const bool un = (root.flags & TGPU_STRUCT_UNION) != 0;
-  bool always = false;
-  for (uint32_t k = 0; k < root.num_fields && !always; ++k) {
-    const tgpu_field_desc& f = sc.fields[root.first_field + k];
-    always = !un && (f.qualifier == TGPU_UNQUALIFIED || f.qualifier == TGPU_REQUIRED ||
-                     f.qualifier == TGPU_BOXED);
-    if (protocol == TGPU_PROTOCOL_BINARY) {
-      set(f.ttype);
-      continue;
+  std::vector<uint32_t> decl(root.num_fields), by_id;
+  for (uint32_t k = 0; k < root.num_fields; ++k) decl[k] = root.first_field + k;
+  by_id = decl;
+  std::stable_sort(by_id.begin(), by_id.end(),
+                   [&](uint32_t a, uint32_t b) { return sc.fields[a].id < sc.fields[b].id; });
+  bool may_be_empty = true;
+  for (const std::vector<uint32_t>* order : {&decl, &by_id}) {
+    bool always = false;
+    for (uint32_t k = 0; k < (uint32_t)order->size() && !always; ++k) {
+      const tgpu_field_desc& f = sc.fields[(*order)[k]];
+      always = !un && (f.qualifier == TGPU_UNQUALIFIED || f.qualifier == TGPU_REQUIRED ||
+                       f.qualifier == TGPU_BOXED);
+      if (protocol == TGPU_PROTOCOL_BINARY) {
+        set(f.ttype);
+        continue;
+      }
+      const uint32_t cts[2] = {f.ttype == TGPU_T_BOOL ? 1u : compact_ctype(f.ttype),
+                               f.ttype == TGPU_T_BOOL ? 2u : compact_ctype(f.ttype)};
+      for (uint32_t ct : cts) {
+        if (f.id >= 1 && f.id <= 15) set(((uint32_t)f.id << 4) | ct);
+        else set(ct);
+      }
     }
-    const uint32_t cts[2] = {f.ttype == TGPU_T_BOOL ? 1u : compact_ctype(f.ttype),
-                             f.ttype == TGPU_T_BOOL ? 2u : compact_ctype(f.ttype)};
-    for (uint32_t ct : cts) {
-      if (f.id >= 1 && f.id <= 15) set(((uint32_t)f.id << 4) | ct);
-      else set(ct);
-    }
+    may_be_empty = !always;
   }
-  if (!always) set(0);
+  if (may_be_empty) set(0);
 }
 
 // Whether a struct is reachable from itself (tgpu_schema::recursive): the
@@ -1114,14 +1127,23 @@ int ensure_deep(tgpu_context* ctx, int32_t max_depth, bool wide = false) {
                                            kMaxDeepFrames);
   const char* wv = getenv("TGPU_DEEP_WIDE");
   if (wide && want > kWideFrames && !ctx->d_wslabs && !(wv && wv[0] == '0')) {
+    // The wide tier only makes the pass faster (the max_depth tier alone
+    // gives the same records), so it takes at most 256 MiB and an eighth of
+    // the free device memory, and a device that cannot spare it runs one
+    // tier: a failed allocation is cleared and the call goes on.
     const uint64_t lb = slab_lane_bytes(kWideFrames);
-    const uint32_t lanes =
-        (uint32_t)std::min<uint64_t>(kWideLanes, (256ull << 20) / lb) & ~63u;
-    if (hipMalloc(&ctx->d_wslabs, lanes * lb) != hipSuccess) {
+    size_t free_b = 0, total_b = 0;
+    uint64_t cap = 256ull << 20;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) cap = std::min<uint64_t>(cap, free_b / 8);
+    else (void)hipGetLastError();
+    const uint32_t lanes = (uint32_t)std::min<uint64_t>(kWideLanes, cap / lb) & ~63u;
+    if (lanes && hipMalloc(&ctx->d_wslabs, (uint64_t)lanes * lb) == hipSuccess) {
+      ctx->wslab_lanes = lanes;
+    } else {
+      (void)hipGetLastError();
       ctx->d_wslabs = nullptr;
-      return TGPU_ERR_HIP;
+      ctx->wslab_lanes = 0;
     }
-    ctx->wslab_lanes = lanes;
   }
   if (ctx->d_slabs && ctx->slab_frames >= want) return TGPU_OK;
   if (ctx->d_slabs) (void)hipFree(ctx->d_slabs);

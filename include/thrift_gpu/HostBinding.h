@@ -267,6 +267,14 @@ inline void readValue(const SchemaTables& sc, uint32_t t, int32_t si, uint32_t t
   }
 }
 
+/* Whether a list's element array can move in one copy: scalar elements
+   whose schema width is the bound C++ element's (a list<i16> bound to
+   std::vector<int32_t> takes the per-element path, as before the fast path). */
+inline bool fastElems(const CType& c, const HostType& ht) {
+  return !isContainer(c.elem) && c.elem != TGPU_T_STRING && c.elem != TGPU_T_STRUCT && ht.elem &&
+         scalarBytes(c.elem) == ht.elem->size;
+}
+
 struct ElemCtx {
   const SchemaTables* sc;
   const CType* c;
@@ -279,7 +287,7 @@ struct ElemCtx {
 inline void readContainer(const SchemaTables& sc, const CType& c, const uint8_t* dev,
                           const Sources& src, const HostType& ht, void* host) {
   const tgpu_span s = loadSpan(dev);
-  if (ht.assign && c.ttype == TGPU_T_LIST) {  // the element array, whole
+  if (ht.assign && c.ttype == TGPU_T_LIST && fastElems(c, ht)) {  // the element array, whole
     ht.assign(host, src.arena + s.offset, s.length);
     return;
   }
@@ -382,7 +390,7 @@ void writeContainer(const SchemaTables& sc, const CType& c, const void* host, co
   const uint64_t arr = n ? out.alloc(n * es) : 0;
   if (!Count) storeSpan(dev, arr, n);
   if (!n) return;
-  if (ht.data && c.ttype == TGPU_T_LIST) {  // arithmetic elements: one copy
+  if (ht.data && c.ttype == TGPU_T_LIST && fastElems(c, ht)) {  // arithmetic elements: one copy
     if (!Count) std::memcpy(out.lists + arr, ht.data(host), n * es);
     return;
   }

@@ -85,3 +85,38 @@ def test_gpu_v1_large_nested_roundtrip(gpu):
     assert stats["broken"] * 10 < stats["chunks"], stats
     helpers.assert_values_equal(
         helpers.unpack(schema, grec.cpu().numpy(), n, owire, garena.cpu().numpy()), vals)
+
+
+@pytest.mark.gpu
+def test_gpu_v1_id_ordered_root_keeps_the_speculation(gpu):
+    """A root written in field-id order (@SerializeInFieldIdOrder,
+    t_whisker_generator.cc:232-236) while the schema declares its fields in
+    another order, with a V1 double (no program: the general speculation
+    filtered by the root's first header bytes). The filter takes both orders'
+    first headers, so the chunks stay linked (with declaration order alone
+    every true record start was rejected and the permissive fallback pass
+    read the stream); records equal the oracle's."""
+    import torch
+
+    from fbthrift_amd.serializer import CompactV1Serializer as S, GpuSchema
+
+    T_I32, T_I64, T_DOUBLE = datagen.T_I32, datagen.T_I64, datagen.T_DOUBLE
+    decl = [[[2, T_DOUBLE, 0, 0, -1], [1, T_I64, 0, 0, -1], [3, T_I32, 0, 0, -1]]]
+    by_id = [[[1, T_I64, 0, 0, -1], [2, T_DOUBLE, 0, 0, -1], [3, T_I32, 0, 0, -1]]]
+    n = 200_000
+    sb = Schema.from_table(by_id)
+    vals = datagen.flatten_values(by_id, [(i * 7919 - 5, i * 0.5, (i * 31) % 1000 - 500)
+                                          for i in range(n)])
+    rec, sa, la = helpers.pack(sb, vals, n)
+    ost, wire, _ = oracle.encode(sb, V1, rec, n, sa, la)
+    assert ost.code == 0 and wire[0] == 0x16  # field 1 (i64) first
+    sd = Schema.from_table(decl)
+    dst, drec, _, _, _ = oracle.decode(sd, V1, wire, n)
+    assert dst.code == 0
+    gs = GpuSchema(sd)
+    grec, _, gst, gnd, gcons = S.deserialize_status(
+        gs, torch.from_numpy(np.frombuffer(wire, np.uint8).copy()).to(gpu), n)
+    assert gst.code == 0 and gnd == n and gcons == len(wire)
+    assert np.array_equal(grec.cpu().numpy()[:len(drec)], drec)
+    stats = S.context().index_stats()
+    assert stats["broken"] * 10 < stats["chunks"], stats
