@@ -263,7 +263,13 @@ inline void readValue(const SchemaTables& sc, uint32_t t, int32_t si, uint32_t t
   } else if (isContainer(t)) {
     readContainer(sc, ctypeNode(sc, ti), dev, src, ht, host);
   } else {
-    std::memcpy(host, dev, scalarBytes(t));
+    const uint32_t w = scalarBytes(t);
+    std::memcpy(host, dev, w);
+    // an integer bound to a wider C++ integer: sign-extended (a list<i16>
+    // bound to std::vector<int32_t> reads -3 as -3, not 65533)
+    if (ht.kind == HostType::Scalar && ht.size > w && w < 8 &&
+        (t == TGPU_T_BYTE || t == TGPU_T_I16 || t == TGPU_T_I32) && (dev[w - 1] & 0x80))
+      std::memset(static_cast<uint8_t*>(host) + w, 0xff, ht.size - w);
   }
 }
 

@@ -50,3 +50,16 @@ def test_host_recursive_runs(gpu):
     r = subprocess.run([BIN3], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert "host recursive ok" in r.stdout
+
+
+BIN4 = os.path.join(CPP, "build", "test_binding_width")
+
+
+def test_binding_list_width_guard():
+    """HostBinding.h without a GPU: a list<i16> bound to std::vector<int32_t>
+    takes the per-element path (sign-extended) both ways; a width-matched
+    binding keeps the one-copy path (tests/cpp/test_binding_width.cpp)."""
+    subprocess.run(["make", "-s", "-C", CPP, "build/test_binding_width"], check=True)
+    r = subprocess.run([BIN4], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert "binding width ok" in r.stdout
