@@ -1126,9 +1126,15 @@ def pmc_traffic(kernel, n, config=2, nested=False, root=None):
 
 def transcode(wl, dev, reps=5):
     """Device-resident Binary <-> Compact transcoding of the workload's whole
-    stream (tgpu_transcode_batch: decode into an HBM workspace, re-encode);
-    rate = input wire bytes / time. Checked by transcoding back to the
-    original bytes. Secondary line, never `value`."""
+    stream (tgpu_transcode_batch), in both forms: wire to wire without
+    records in HBM (tgpu_xcode.h: size pass, scan, write pass over the source
+    tile in LDS — schemas with a flat program in both protocols) and the
+    composed decode into an HBM workspace + re-encode (TGPU_XCODE=0); each
+    with the record index given (the workload's offsets) and without (the
+    stream index first). Blocking calls (host status), best of `reps`; rate =
+    input wire bytes / time. Checked: every form's bytes equal, and
+    transcoding back gives the original stream. Secondary line, never
+    `value`."""
     import torch
 
     from fbthrift_amd import serializer as S
@@ -1141,23 +1147,45 @@ def transcode(wl, dev, reps=5):
     w = wl.wire[: wl.wire_bytes]
     out = torch.empty(8 * wl.wire_bytes + 16, dtype=torch.uint8, device=dev)
     res = {"from": src.protocol, "to": to}
-    best = None
-    for _ in range(reps + 1):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        _, offs, st, done, size = src.transcode(wl.gs, w, wl.n, to, out=out)
-        el = time.perf_counter() - t0
-        if st.code or done != wl.n:
-            raise RuntimeError("transcode failed: %s" % (st.as_tuple(),))
-        best = el if best is None else min(best, el)
+    ref = None
+    old = os.environ.get("TGPU_XCODE")
+    try:
+        for form in ("fused", "composed"):
+            os.environ["TGPU_XCODE"] = "1" if form == "fused" else "0"
+            for ix in ("indexed", "unindexed"):
+                offs = wl.offs if ix == "indexed" else None
+                best = None
+                for _ in range(reps + 1):
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    _, _, st, done, size = src.transcode(wl.gs, w, wl.n, to, offsets=offs, out=out,
+                                                         want_offsets=False)
+                    el = time.perf_counter() - t0
+                    if st.code or done != wl.n:
+                        raise RuntimeError("transcode failed: %s" % (st.as_tuple(),))
+                    best = el if best is None else min(best, el)
+                got = out[:size].clone()
+                if ref is None:
+                    ref = got
+                elif not torch.equal(ref, got):
+                    raise RuntimeError("transcode forms disagree (%s %s)" % (form, ix))
+                res["%s_%s_ms" % (form, ix)] = round(best * 1e3, 3)
+                res["%s_%s_gibps_in" % (form, ix)] = round(wl.wire_bytes / best / 2**30, 3)
+    finally:
+        if old is None:
+            os.environ.pop("TGPU_XCODE", None)
+        else:
+            os.environ["TGPU_XCODE"] = old
+    size = ref.numel()
+    out[:size].copy_(ref)
     back = torch.empty(wl.wire_bytes + 16, dtype=torch.uint8, device=dev)
     _, _, st, done, bsize = dst.transcode(wl.gs, out[:size], wl.n, src.protocol, out=back)
     if st.code or bsize != wl.wire_bytes or not torch.equal(back[:bsize], w):
         raise RuntimeError("transcode round trip mismatch")
-    res["gibps_in"] = round(wl.wire_bytes / best / 2**30, 3)
     res["out_bytes"] = size
-    res["ms"] = round(best * 1e3, 3)
-    res["how"] = "blocking call incl. one host sync between the passes; best of %d" % reps
+    res["how"] = ("blocking calls (host status), best of %d; fused = wire to wire, no records "
+                  "in HBM; composed = decode + encode (TGPU_XCODE=0); indexed = the workload's "
+                  "offsets given, unindexed = the stream index first" % reps)
     return res
 
 

@@ -78,7 +78,7 @@ EXPORTS = [
     "tgpu_schema_fixed_wire_size", "tgpu_context_create", "tgpu_context_destroy",
     "tgpu_context_reserve", "tgpu_context_wait", "tgpu_encode_batch", "tgpu_encoded_size",
     "tgpu_decode_batch", "tgpu_index_stream", "tgpu_schema_compile", "tgpu_schema_compile_check",
-    "tgpu_schema_compile_check_ex",
+    "tgpu_schema_compile_check_ex", "tgpu_transcode_compile_check",
     "tgpu_decode_host", "tgpu_encode_host", "tgpu_decode_stream", "tgpu_transcode_batch",
     "tgpu_schema_arena_scale", "tgpu_decode_host_ex", "tgpu_encode_host_ex", "tgpu_skim_batch",
     "tgpu_skim_batch_ex",
@@ -159,6 +159,9 @@ def lib():
     L.tgpu_schema_compile.argtypes = [P, I32]
     L.tgpu_schema_compile_check_ex.restype = I32
     L.tgpu_schema_compile_check_ex.argtypes = [P, U32, P, U32, P, U32, I32, ctypes.c_char_p,
+                                               ctypes.c_char_p, U64]
+    L.tgpu_transcode_compile_check.restype = I32
+    L.tgpu_transcode_compile_check.argtypes = [P, U32, P, U32, I32, I32, ctypes.c_char_p,
                                                ctypes.c_char_p, U64]
     L.tgpu_schema_compile_check.restype = I32
     L.tgpu_schema_compile_check.argtypes = [P, U32, P, U32, I32, ctypes.c_char_p,

@@ -132,6 +132,10 @@ struct tgpu_context {
   uint64_t xrec_bytes = 0;
   uint8_t* d_xarena = nullptr;
   uint64_t xarena_bytes = 0;
+  // transcode without materialized records: output starts when the caller
+  // asked for none (the listed records' holes, the finish's failing record)
+  uint8_t* d_xoffs = nullptr;
+  uint64_t xoffs_bytes = 0;
 };
 
 namespace tgpu {
@@ -1854,6 +1858,30 @@ int tgpu_schema_compile_check_ex(const tgpu_struct_desc* structs, uint32_t n_str
   return jit_compile_check(T, arch, log, log_capacity, JIT_DECODE);
 }
 
+int tgpu_transcode_compile_check(const tgpu_struct_desc* structs, uint32_t n_structs,
+                                 const tgpu_field_desc* fields, uint32_t n_fields,
+                                 int from_protocol, int to_protocol, const char* arch, char* log,
+                                 uint64_t log_capacity) {
+  if (!structs || n_structs == 0 || (!fields && n_fields) || !valid_protocol(from_protocol) ||
+      !valid_protocol(to_protocol))
+    return TGPU_ERR_INVALID_ARGUMENT;
+  SchemaFacts facts;
+  const int rc = validate(structs, n_structs, fields, n_fields, nullptr, 0, facts);
+  if (rc) return rc;
+  tgpu_schema h;
+  h.structs.assign(structs, structs + n_structs);
+  h.fields.assign(fields, fields + n_fields);
+  h.nested = facts.nested;
+  for (uint32_t k = 0; k < n_fields; ++k)
+    h.has_double |= fields[k].ttype == TGPU_T_DOUBLE || fields[k].elem_ttype == TGPU_T_DOUBLE ||
+                    fields[k].val_ttype == TGPU_T_DOUBLE;
+  const int qf = prog_protocol(&h, from_protocol), qt = prog_protocol(&h, to_protocol);
+  VProgram Ps{}, Pd{};
+  if (qf < 0 || qt < 0 || h.nested || !build_program(h, qf, Ps) || !build_program(h, qt, Pd))
+    return TGPU_ERR_UNSUPPORTED;
+  return jit_compile_check_xcode(Ps, Pd, arch, log, log_capacity);
+}
+
 int tgpu_schema_compile_check(const tgpu_struct_desc* structs, uint32_t n_structs,
                               const tgpu_field_desc* fields, uint32_t n_fields, int protocol,
                               const char* arch, char* log, uint64_t log_capacity) {
@@ -1906,6 +1934,7 @@ void tgpu_context_destroy(tgpu_context* c) {
   if (c->d_index) (void)hipFree(c->d_index);
   if (c->d_xrec) (void)hipFree(c->d_xrec);
   if (c->d_xarena) (void)hipFree(c->d_xarena);
+  if (c->d_xoffs) (void)hipFree(c->d_xoffs);
   delete c;
 }
 
@@ -2303,6 +2332,112 @@ int grow(uint8_t*& p, uint64_t& have, uint64_t want) {
 }
 }  // namespace
 
+namespace {
+// The wire-to-wire transcoder (tgpu_xcode.h, k_transcode.hip) applies when
+// both protocols have the schema's flat record program and the stream is not
+// a fixed-layout Binary stream without offsets (that one's fastest read is the
+// plan kernel; it stays on the composed decode + encode). TGPU_XCODE=0: the
+// composed form everywhere (A/B).
+bool xcode_fused(const tgpu_schema* s, int from, int to, const uint64_t* offsets,
+                 uint64_t in_len, uint64_t n) {
+  if (const char* v = getenv("TGPU_XCODE"))
+    if (v[0] == '0') return false;
+  const int qf = prog_protocol(s, from), qt = prog_protocol(s, to);
+  if (qf < 0 || qt < 0 || !s->has_prog[qf] || !s->has_prog[qt]) return false;
+  if (!offsets && from == TGPU_PROTOCOL_BINARY && s->fixed_binary &&
+      in_len >= n * (uint64_t)s->tmpl.wire_len)
+    return false;
+  return true;
+}
+
+int transcode_fused(tgpu_context* ctx, const tgpu_schema* schema, int from, int to,
+                    const void* in, uint64_t in_len, const uint64_t* offsets, uint64_t n, void* out,
+                    uint64_t out_capacity, uint64_t* out_offsets, const tgpu_limits* limits,
+                    void* stream, tgpu_status* st, uint64_t* n_done, uint64_t* out_size) {
+  const hipStream_t s = (hipStream_t)stream;
+  const uint64_t rs = schema->structs[0].size;
+  const uint64_t acap = schema->has_lists ? in_len * tgpu_schema_arena_scale(schema, from) : 0;
+  int rc = ensure_workspace(ctx, n);
+  if (!rc) rc = ensure_deep(ctx, limit_depth(limits), schema->recursive);
+  if (!rc) rc = grow(ctx->d_xrec, ctx->xrec_bytes, std::max<uint64_t>(n * rs, 16));
+  if (!rc && acap) rc = grow(ctx->d_xarena, ctx->xarena_bytes, acap);
+  if (!rc && !out_offsets) rc = grow(ctx->d_xoffs, ctx->xoffs_bytes, (n + 1) * sizeof(uint64_t));
+  if (rc) {
+    fill_status(st, rc, 0, 0);
+    return rc;
+  }
+  const bool blocking = st || n_done || out_size;
+  XcodeArgs x{};
+  DecodeArgs& a = x.d;
+  a.sc = dev_schema(schema, from);
+  a.in = (const uint8_t*)in;
+  a.in_len = in_len;
+  a.n = n;
+  a.recs = ctx->d_xrec;
+  a.arena = acap ? ctx->d_xarena : nullptr;
+  a.arena_cap = acap;
+  a.string_limit = limits ? limits->string_limit : 0;
+  a.container_limit = limits ? limits->container_limit : 0;
+  a.max_depth = limits ? limits->max_depth : 12000;
+  a.height = limits ? limits->height : 0;
+  a.rec_size = (uint32_t)rs;
+  a.check_index = 1;
+  a.res = ctx->d_res;
+  a.deep = deep_args(ctx);
+  EncodeArgs& w = x.e;
+  w.sc = dev_schema(schema, to);
+  w.recs = ctx->d_xrec;
+  w.n = n;
+  w.sbase = a.in;
+  w.lbase = a.arena;
+  w.out = (uint8_t*)out;
+  w.cap = out_capacity;
+  w.offs = out_offsets ? out_offsets : (uint64_t*)ctx->d_xoffs;
+  w.block_sums = ctx->d_block_sums;
+  w.scan_part = ctx->d_scan_part;
+  w.rec_size = (uint32_t)rs;
+  w.res = ctx->d_res;
+  w.deep = a.deep;
+  x.irr = ctx->d_irr;
+  x.nirr = &ctx->d_res->n_irregular;
+  x.want_offs = out_offsets ? 1u : 0u;
+  (void)hipGetLastError();  // drop a stale error left by another library
+  hipError_t e = launch_result_init(ctx->d_res, n, s);
+  if (offsets) {
+    a.offs = offsets;
+  } else {
+    // unindexed: the stream index first (records past the end / the first bad
+    // record re-read that position, so the reader reports them exactly)
+    a.offs = ctx->d_offs;
+    const int irc = launch_index(ctx, schema, from, a.in, in_len, 0, in_len, 0, ctx->d_offs, n, n,
+                                 limits, s, e, nullptr, nullptr, false, blocking);
+    if (irc) {
+      fill_status(st, irc, 0, 0);
+      return irc;
+    }
+    // (the index counted its own general-reader records in n_irregular)
+    if (e == hipSuccess)
+      e = hipMemsetAsync(&ctx->d_res->n_irregular, 0, sizeof(unsigned long long), s);
+  }
+  const int qf = prog_protocol(schema, from), qt = prog_protocol(schema, to);
+  const JitKernels* jit =
+      jit_kernels_xcode(schema->prog[qf], schema->prog[qt], schema->device, n, false);
+  if (e == hipSuccess)
+    e = launch_xcode(x, from, to, schema->d_prog[qf], schema->d_prog[qt], s, jit);
+  ctx->last_op = 2;
+  if (e != hipSuccess) {
+    fill_status(st, TGPU_ERR_HIP, 0, 0);
+    if (st) st->reserved = (int32_t)e;
+    return TGPU_ERR_HIP;
+  }
+  if (blocking) {
+    tgpu_status tmp;
+    return tgpu_context_wait(ctx, stream, st ? st : &tmp, n_done, out_size);
+  }
+  return TGPU_OK;
+}
+}  // namespace
+
 int tgpu_transcode_batch(tgpu_context* ctx, const tgpu_schema* schema, int from_protocol,
                          int to_protocol, const void* in, uint64_t in_len,
                          const uint64_t* offsets, uint64_t n, void* out, uint64_t out_capacity,
@@ -2315,6 +2450,9 @@ int tgpu_transcode_batch(tgpu_context* ctx, const tgpu_schema* schema, int from_
     fill_status(st, TGPU_ERR_INVALID_ARGUMENT, 0, 0);
     return TGPU_ERR_INVALID_ARGUMENT;
   }
+  if (n && xcode_fused(schema, from_protocol, to_protocol, offsets, in_len, n))
+    return transcode_fused(ctx, schema, from_protocol, to_protocol, in, in_len, offsets, n, out,
+                           out_capacity, out_offsets, limits, stream, st, n_done, out_size);
   // records and list elements stay in HBM between the passes (grow-only)
   const uint64_t rs = schema->structs[0].size;
   const uint64_t acap = in_len * tgpu_schema_arena_scale(schema, from_protocol);

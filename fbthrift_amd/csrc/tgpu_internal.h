@@ -338,6 +338,22 @@ struct EncodeArgs {
   DeepArgs deep;
 };
 
+// Wire-to-wire transcoding of an indexed stream (tgpu_xcode.h,
+// k_transcode.hip): d = the source (d.offs n+1 starts; d.arena the list
+// workspace of a Compact source; d.recs the record workspace of the records
+// the source program cannot take, which the general reader decodes), e = the
+// target (e.offs: the listed records' sizes, then every output start the
+// finish or the caller reads; e.recs = d.recs, e.sbase = d.in, e.lbase =
+// d.arena for those records).
+struct XcodeArgs {
+  DecodeArgs d;
+  EncodeArgs e;
+  uint64_t* irr;              // records left to the general reader / writer
+  unsigned long long* nirr;
+  uint32_t want_offs;         // the caller asked for every output start
+  uint32_t pad_;
+};
+
 // ---- stream indexer (k_index.hip) -------------------------------------------
 // Finds the start of every record beginning in [begin, end) of an unindexed
 // stream: lanes speculate record starts per chunk, a serial pass repairs the
@@ -474,7 +490,15 @@ struct JitKernels;
 // straight-line code with one loop per container level.
 // JIT_NINDEX: the stream index's speculation / emit kernels over a nested
 // program's measuring walk.
-enum JitGroup { JIT_DECODE = 0, JIT_ENCODE = 1, JIT_INDEX = 2, JIT_NESTED = 3, JIT_NINDEX = 4 };
+// JIT_XCODE: the transcoder's program pair (tgpu_xcode.h), jit_kernels_xcode.
+enum JitGroup {
+  JIT_DECODE = 0,
+  JIT_ENCODE = 1,
+  JIT_INDEX = 2,
+  JIT_NESTED = 3,
+  JIT_NINDEX = 4,
+  JIT_XCODE = 5
+};
 const JitKernels* jit_kernels(const VProgram& prog, int device, int group, uint64_t records,
                               uint64_t bytes, bool force);
 // Records of at most 128 bytes, S % 8 == 0, get a second compiled decode
@@ -493,6 +517,18 @@ hipError_t jit_launch_decode(const JitKernels* J, const DecodeArgs& a, uint64_t 
 // first: the group's first encode entry (JIT_NESTED: 2, its size / write)
 hipError_t jit_launch_encode(const JitKernels* J, bool write, const EncodeArgs& a, uint64_t grid,
                              uint32_t lds, hipStream_t s, int first = 0);
+// The transcoder's pair (source program's decode, target program's writer);
+// which: 0 size, 1 write, 2 / 3 the same with records in registers.
+const JitKernels* jit_kernels_xcode(const VProgram& ps, const VProgram& pd, int device,
+                                    uint64_t records, bool force);
+hipError_t jit_launch_xcode(const JitKernels* J, int which, const XcodeArgs& x, uint64_t grid,
+                            uint32_t cap, uint32_t ocap, uint32_t lds, hipStream_t s);
+int jit_compile_check_xcode(const VProgram& ps, const VProgram& pd, const char* arch, char* log,
+                            uint64_t log_cap);
+// Wire-to-wire transcoding of x.d's indexed stream (k_transcode.hip): the
+// pair's compiled kernels (jit) or the AOT DynProg pair over d_ps / d_pd.
+hipError_t launch_xcode(const XcodeArgs& x, int from, int to, const VProgram* d_ps,
+                        const VProgram* d_pd, hipStream_t s, const JitKernels* jit);
 // which: 0 speculation, 1 emit, 2 emit + fused decode
 hipError_t jit_launch_index(const JitKernels* J, int which, const IndexArgs& a, uint64_t grid,
                             hipStream_t s);

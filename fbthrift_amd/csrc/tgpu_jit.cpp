@@ -72,13 +72,15 @@ std::string cache_key(const VProgram& P, int device, int group) {
   return k;
 }
 
-const char* const kEntry[5][5] = {
+const char* const kEntry[6][5] = {
     {"tgpu_jit_decode", "tgpu_jit_decode_tail", "tgpu_jit_decode_rr", nullptr, nullptr},
     {"tgpu_jit_size", "tgpu_jit_write", nullptr, nullptr, nullptr},
     {"tgpu_jit_index_spec", "tgpu_jit_index_emit", "tgpu_jit_index_decode",
      "tgpu_jit_index_onepass", "tgpu_jit_index_onepass_decode"},
     {"tgpu_jit_ndecode", "tgpu_jit_ndecode_hbm", "tgpu_jit_nsize", "tgpu_jit_nwrite", nullptr},
-    {"tgpu_jit_nindex_spec", "tgpu_jit_nindex_emit", nullptr, nullptr, nullptr}};
+    {"tgpu_jit_nindex_spec", "tgpu_jit_nindex_emit", nullptr, nullptr, nullptr},
+    {"tgpu_jit_xc_size", "tgpu_jit_xc_write", "tgpu_jit_xc_size_rr", "tgpu_jit_xc_write_rr",
+     nullptr}};
 
 // The record function of a nested program (decode when !enc, the writer
 // when enc): ops [k, stop) of the object at `b` (a variable name). Each
@@ -292,6 +294,82 @@ void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t sto
 
 // The generated translation unit: the program as constants + one entry point
 // per kernel body.
+// A program as compile-time constants: the op array `arr` and the program
+// accessor `name` (tgpu_program.h's DynProg interface, kStatic).
+void gen_prog(std::ostringstream& o, const VProgram& P, const char* arr, const char* name) {
+  o << "__device__ constexpr tgpu::VOp " << arr << "[" << (P.n_ops ? P.n_ops : 1) << "] = {\n";
+  for (uint32_t k = 0; k < P.n_ops; ++k) {
+    const VOp& v = P.ops[k];
+    o << "  {" << (unsigned)v.kind << ", " << (unsigned)v.hdr_len << ", " << (unsigned)v.width
+      << ", " << (unsigned)v.bits << ", " << v.hdr << "u, " << v.member << ", " << v.isset << ", "
+      << (unsigned)v.elem_kind << ", " << (unsigned)v.elem_ttype << ", " << (unsigned)v.elem_ct
+      << ", " << (unsigned)v.is_bool << "},\n";
+  }
+  if (!P.n_ops) o << "  {}\n";
+  o << "};\n"
+       "struct "
+    << name
+    << " {\n"
+       "  static constexpr bool kStatic = true;\n"
+       "  static constexpr uint32_t kN = "
+    << P.n_ops
+    << ";\n"
+       "  __device__ static constexpr uint32_t n_ops() { return kN; }\n"
+       "  __device__ static constexpr uint32_t protocol() { return "
+    << P.protocol
+    << "; }\n"
+       "  __device__ static constexpr bool has_lists() { return "
+    << (P.has_list ? "true" : "false")
+    << "; }\n"
+       "  __device__ constexpr tgpu::VOp op(uint32_t k) const { return "
+    << arr
+    << "[k]; }\n"
+       "};\n";
+}
+
+// The transcoder's pair (JIT_XCODE): the source program's decode and the
+// target program's writer in the two tile passes of tgpu_xcode.h, with
+// records in registers where decode_regrec allows (entries 2, 3).
+std::string gen_source_xcode(const VProgram& Ps, const VProgram& Pd) {
+  std::ostringstream o;
+  o << "// generated by tgpu_jit.cpp for one schema's transcoding pair\n";
+  if (const char* v = getenv("TGPU_JIT_DEFINES")) o << v << "\n";
+  bool tails = false;
+  for (uint32_t k = 0; k < Ps.n_ops; ++k)
+    tails |= Ps.ops[k].kind == VOP_CONST && Ps.ops[k].elem_kind == kStopSkipsUnknown;
+  if (!tails) o << "#define TGPU_NO_TAILS 1\n";
+  o << "#include \"tgpu_xcode.h\"\n"
+       "namespace {\n";
+  gen_prog(o, Ps, "kOps", "JP");
+  gen_prog(o, Pd, "kOps2", "JQ");
+  o << "constexpr uint32_t kS = " << Ps.rec_size
+    << ";\n"
+       "}  // namespace\n"
+       "using namespace tgpu;\n";
+  auto pair = [&](const char* sfx, const char* rs) {
+    o << "extern \"C\" __global__ __launch_bounds__(256) void tgpu_jit_xc_size" << sfx
+      << "(XcodeArgs x, uint32_t cap) {\n"
+         "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+         "  __shared__ unsigned long long part[4];\n"
+         "  prog::xc_size_tile<JP, JQ, "
+      << rs
+      << ">(x, JP{}, JQ{}, kS, cap, smem, part);\n"
+         "}\n"
+         "extern \"C\" __global__ __launch_bounds__(256) void tgpu_jit_xc_write"
+      << sfx
+      << "(XcodeArgs x, uint32_t cap, uint32_t ocap) {\n"
+         "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+         "  __shared__ prog::EncodeShared sm;\n"
+         "  prog::xc_write_tile<JP, JQ, "
+      << rs
+      << ">(x, JP{}, JQ{}, kS, cap, ocap, smem, sm);\n"
+         "}\n";
+  };
+  pair("", "0");
+  if (decode_regrec(Ps.rec_size)) pair("_rr", "kS");
+  return o.str();
+}
+
 std::string gen_source(const VProgram& P, int group) {
   std::ostringstream o;
   o << "// generated by tgpu_jit.cpp for one schema program\n";
@@ -306,33 +384,9 @@ std::string gen_source(const VProgram& P, int group) {
   }
   if (!tails) o << "#define TGPU_NO_TAILS 1\n";
   o << "#include \"tgpu_prog_kernels.h\"\n"
-       "namespace {\n"
-       "__device__ constexpr tgpu::VOp kOps["
-    << (P.n_ops ? P.n_ops : 1) << "] = {\n";
-  for (uint32_t k = 0; k < P.n_ops; ++k) {
-    const VOp& v = P.ops[k];
-    o << "  {" << (unsigned)v.kind << ", " << (unsigned)v.hdr_len << ", " << (unsigned)v.width
-      << ", " << (unsigned)v.bits << ", " << v.hdr << "u, " << v.member << ", " << v.isset << ", "
-      << (unsigned)v.elem_kind << ", " << (unsigned)v.elem_ttype << ", " << (unsigned)v.elem_ct
-      << ", " << (unsigned)v.is_bool << "},\n";
-  }
-  if (!P.n_ops) o << "  {}\n";
-  o << "};\n"
-       "struct JP {\n"
-       "  static constexpr bool kStatic = true;\n"
-       "  static constexpr uint32_t kN = "
-    << P.n_ops
-    << ";\n"
-       "  __device__ static constexpr uint32_t n_ops() { return kN; }\n"
-       "  __device__ static constexpr uint32_t protocol() { return "
-    << P.protocol
-    << "; }\n"
-       "  __device__ static constexpr bool has_lists() { return "
-    << (P.has_list ? "true" : "false")
-    << "; }\n"
-       "  __device__ constexpr tgpu::VOp op(uint32_t k) const { return kOps[k]; }\n"
-       "};\n"
-       "constexpr uint32_t kS = "
+       "namespace {\n";
+  gen_prog(o, P, "kOps", "JP");
+  o << "constexpr uint32_t kS = "
     << P.rec_size
     << ";\n"
        "}  // namespace\n"
@@ -570,9 +624,8 @@ std::string gen_source(const VProgram& P, int group) {
 
 // Generated source -> code object for `arch` (a gcnArchName; with its
 // feature suffix first, then the bare processor name).
-bool compile_code(const VProgram& P, int group, std::string arch, std::vector<char>& code,
-                  std::string& log) {
-  const std::string src = gen_source(P, group);
+bool compile_src(const std::string& src, int group, std::string arch, std::vector<char>& code,
+                 std::string& log) {
   if (const char* d = getenv("TGPU_JIT_DUMP")) {  // debugging: the generated unit
     const std::string path = std::string(d) + "." + std::to_string(group) + ".hip";
     if (FILE* f = fopen(path.c_str(), "w")) {
@@ -620,14 +673,19 @@ bool compile_code(const VProgram& P, int group, std::string arch, std::vector<ch
   return !code.empty();
 }
 
-bool compile(const VProgram& P, int device, int group, JitKernels& J) {
+bool compile_code(const VProgram& P, int group, std::string arch, std::vector<char>& code,
+                  std::string& log) {
+  return compile_src(gen_source(P, group), group, arch, code, log);
+}
+
+bool compile_from(const std::string& src, int device, int group, JitKernels& J) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
     J.log = "hipGetDeviceProperties failed";
     return false;
   }
   std::vector<char> code;
-  if (!compile_code(P, group, prop.gcnArchName, code, J.log)) return false;
+  if (!compile_src(src, group, prop.gcnArchName, code, J.log)) return false;
   int prev = 0;
   (void)hipGetDevice(&prev);
   if (prev != device) (void)hipSetDevice(device);
@@ -637,7 +695,8 @@ bool compile(const VProgram& P, int device, int group, JitKernels& J) {
     ok = hipModuleGetFunction(&J.f[k], J.mod, kEntry[group][k]) == hipSuccess;
     // (tolerant programs / small records; a deferring nested program's writer)
     if (!ok && ((group == JIT_DECODE && (k == 1 || k == 2)) ||
-                (group == JIT_NESTED && (k == 2 || k == 3)))) {
+                (group == JIT_NESTED && (k == 2 || k == 3)) ||
+                (group == JIT_XCODE && (k == 2 || k == 3)))) {
       (void)hipGetLastError();
       J.f[k] = nullptr;
       ok = true;
@@ -646,6 +705,10 @@ bool compile(const VProgram& P, int device, int group, JitKernels& J) {
   if (prev != device) (void)hipSetDevice(prev);
   if (!ok) J.log += "\nmodule load failed";
   return ok;
+}
+
+bool compile(const VProgram& P, int device, int group, JitKernels& J) {
+  return compile_from(gen_source(P, group), device, group, J);
 }
 
 hipError_t launch(hipFunction_t f, uint64_t grid, uint32_t lds, hipStream_t s, void** params) {
@@ -672,6 +735,52 @@ const JitKernels* jit_kernels(const VProgram& P, int device, int group, uint64_t
             J->log.c_str());
   cache()[key] = J;  // a failure is remembered too: never retried
   return J->ok ? J : nullptr;
+}
+
+const JitKernels* jit_kernels_xcode(const VProgram& Ps, const VProgram& Pd, int device,
+                                    uint64_t records, bool force) {
+  const int mode = jit_mode();
+  if (mode == 0) return nullptr;
+  const bool want = force || mode == 1 || records >= kAutoRecords;
+  const std::string key = cache_key(Ps, device, JIT_XCODE) + "|" + cache_key(Pd, device, JIT_XCODE);
+  std::lock_guard<std::mutex> g(g_mu);
+  auto it = cache().find(key);
+  if (it != cache().end()) return it->second->ok ? it->second : nullptr;
+  if (!want) return nullptr;
+  JitKernels* J = new JitKernels();
+  J->ok = compile_from(gen_source_xcode(Ps, Pd), device, JIT_XCODE, *J);
+  if (!J->ok && getenv("TGPU_JIT_VERBOSE"))
+    fprintf(stderr, "tgpu: transcoding kernels not compiled, using the interpreter:\n%s\n",
+            J->log.c_str());
+  cache()[key] = J;
+  return J->ok ? J : nullptr;
+}
+
+hipError_t jit_launch_xcode(const JitKernels* J, int which, const XcodeArgs& x, uint64_t grid,
+                            uint32_t cap, uint32_t ocap, uint32_t lds, hipStream_t s) {
+  if (!jit_has(J, which)) return hipErrorInvalidDeviceFunction;
+  XcodeArgs a = x;
+  void* p2[] = {&a, &cap};
+  void* p3[] = {&a, &cap, &ocap};
+  return launch(J->f[which], grid, lds, s, (which & 1) ? p3 : p2);
+}
+
+int jit_compile_check_xcode(const VProgram& Ps, const VProgram& Pd, const char* arch, char* log,
+                            uint64_t log_cap) {
+  std::string l;
+  bool ok;
+  if (arch && !*arch) {
+    ok = !gen_source_xcode(Ps, Pd).empty();
+  } else {
+    std::vector<char> code;
+    ok = compile_src(gen_source_xcode(Ps, Pd), JIT_XCODE, arch ? arch : "gfx950", code, l);
+  }
+  if (log && log_cap) {
+    const size_t n = l.size() < log_cap - 1 ? l.size() : (size_t)(log_cap - 1);
+    memcpy(log, l.data(), n);
+    log[n] = 0;
+  }
+  return ok ? TGPU_OK : TGPU_ERR_UNSUPPORTED;
 }
 
 bool decode_regrec(uint32_t rec_size) {

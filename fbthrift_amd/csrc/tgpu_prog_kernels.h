@@ -908,7 +908,12 @@ constexpr uint64_t kLanesValid = ~0ull - 3; // pf: the tile's per-lane results a
 constexpr uint64_t kStartsValid = ~0ull - 4; // pf: ... and its record starts are in st16
 constexpr uint32_t kPosCap = 0x7fffff00u;
 constexpr uint32_t kTileLanes = 256;
-constexpr uint32_t kSub = 64;
+// bytes per lane slice: the tile is kTileLanes * kSub bytes (A/B builds:
+// -DTGPU_KSUB with the same TGPU_JIT_DEFINES for the schema kernels)
+#ifndef TGPU_KSUB
+#define TGPU_KSUB 64
+#endif
+constexpr uint32_t kSub = TGPU_KSUB;
 constexpr uint32_t kTile = kTileLanes * kSub;
 #ifndef TGPU_KOVER
 #define TGPU_KOVER 512
@@ -1178,30 +1183,33 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
     // but cheap); the chain runs outside the search so all lanes of the
     // wave run it together
     // (the slice's 64 bits from the 8-byte aligned words around them)
-    const uint32_t g0 = sub_lo >> 3, off = sub_lo & 7;
-    const uint32_t d = g0 >> 3, bo = (g0 & 7) * 8 + off;  // bit offset in word d
+    // (64 positions at a time: a slice of kSub > 64 bytes takes several)
     const uint64_t* cw = (const uint64_t*)cmask;
-    const uint64_t c0 = cw[d], c1 = cw[d + 1];
-    uint64_t cm = bo ? (c0 >> bo) | (c1 << (64 - bo)) : c0;
-    if (sub_hi - sub_lo < 64) cm &= (1ull << (sub_hi - sub_lo)) - 1;
     bool need = true;
-    while (need) {
-      uint32_t cand = kNoPos;
-      while (cm) {
-        const uint32_t c = sub_lo + (uint32_t)__builtin_ctzll(cm);
-        cm &= cm - 1;
+    for (uint32_t b0 = sub_lo; b0 < sub_hi && need; b0 += 64) {
+      const uint32_t g0 = b0 >> 3, off = b0 & 7;
+      const uint32_t d = g0 >> 3, bo = (g0 & 7) * 8 + off;  // bit offset in word d
+      const uint64_t c0 = cw[d], c1 = cw[d + 1];
+      uint64_t cm = bo ? (c0 >> bo) | (c1 << (64 - bo)) : c0;
+      if (sub_hi - b0 < 64) cm &= (1ull << (sub_hi - b0)) - 1;
+      while (need) {
+        uint32_t cand = kNoPos;
+        while (cm) {
+          const uint32_t c = b0 + (uint32_t)__builtin_ctzll(cm);
+          cm &= cm - 1;
 #ifndef TGPU_NO_QUICK_REJECT  // A/B: the measuring walk alone rejects false candidates
-        if (quick_reject(P, src, c)) continue;
+          if (quick_reject(P, src, c)) continue;
 #endif
-        cand = c;
-        break;
-      }
-      if (cand == kNoPos) break;  // no record start in this slice
-      TileLane t;
-      tile_chain(P, src, pc, cand, sub_hi, avail, t);
-      if (t.c) {
-        L = t;
-        need = false;
+          cand = c;
+          break;
+        }
+        if (cand == kNoPos) break;  // no record start in these 64 positions
+        TileLane t;
+        tile_chain(P, src, pc, cand, sub_hi, avail, t);
+        if (t.c) {
+          L = t;
+          need = false;
+        }
       }
     }
   }

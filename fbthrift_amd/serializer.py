@@ -137,6 +137,18 @@ def compile_check(schema, protocol, arch="gfx950"):
     return rc, log.value.decode(errors="replace")
 
 
+def transcode_compile_check(schema, from_protocol, to_protocol, arch="gfx950"):
+    """The wire-to-wire transcoder's kernels (source program's decode + target
+    program's writer, tgpu_xcode.h) generated and compiled for `arch` without
+    a GPU (tgpu_transcode_compile_check). Returns (code, compiler log)."""
+    structs, ns, fields, nf = schema.descriptors()
+    log = ctypes.create_string_buffer(1 << 16)
+    rc = _lib.lib().tgpu_transcode_compile_check(ctypes.addressof(structs), ns,
+                                                 ctypes.addressof(fields), nf, from_protocol,
+                                                 to_protocol, arch.encode(), log, len(log))
+    return rc, log.value.decode(errors="replace")
+
+
 class Context:
     """Workspace + result slot (tgpu_context). One in-flight call at a time."""
 
@@ -302,10 +314,12 @@ class BatchSerializer:
         return records, arena, st, n_dec.value, consumed.value
 
     def transcode(self, gschema, wire, n, to_protocol, offsets=None, out=None, limits=None,
-                  stream=None):
+                  stream=None, want_offsets=True):
         """Re-encodes n records of `wire` (this serializer's protocol) into
         `to_protocol` on the device (tgpu_transcode_batch). Returns (out,
-        out_offsets, status, n_done, out_size); never raises on data errors."""
+        out_offsets, status, n_done, out_size); never raises on data errors.
+        want_offsets=False: no output offsets are asked for (out_offsets is
+        None)."""
         import torch
 
         dev = wire.device
@@ -313,7 +327,7 @@ class BatchSerializer:
             # no wire byte grows by more than 8x in another protocol (a
             # 1-byte Compact varint list element is 8 Binary bytes)
             out = torch.empty(max(8 * wire.numel() + 16, 16), dtype=torch.uint8, device=dev)
-        offs = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        offs = torch.empty(n + 1, dtype=torch.int64, device=dev) if want_offsets else None
         lim = _lib.Limits(*limits) if limits is not None else None
         st = _lib.Status()
         done, size = ctypes.c_uint64(), ctypes.c_uint64()

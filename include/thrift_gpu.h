@@ -368,6 +368,14 @@ int tgpu_schema_compile_check_ex(const tgpu_struct_desc* structs, uint32_t n_str
                                  const tgpu_type_desc* types, uint32_t n_types, int protocol,
                                  const char* arch, char* log, uint64_t log_capacity);
 
+/* The transcoder's kernels for a schema with a flat record program in both
+ * protocols (tgpu_transcode_batch without materialized records): generated
+ * and compiled for `arch` without a GPU, as tgpu_schema_compile_check. */
+int tgpu_transcode_compile_check(const tgpu_struct_desc* structs, uint32_t n_structs,
+                                 const tgpu_field_desc* fields, uint32_t n_fields,
+                                 int from_protocol, int to_protocol, const char* arch, char* log,
+                                 uint64_t log_capacity);
+
 /* ---- context ---------------------------------------------------------- */
 int tgpu_context_create(tgpu_context** out);
 void tgpu_context_destroy(tgpu_context* ctx);

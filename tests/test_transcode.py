@@ -80,9 +80,18 @@ def _gpu_transcode(dev, schema, pf, pt, wire, n, out_cap=None, offsets=None):
     return st, done, bytes(out[:size].cpu().numpy()), offs[: done + 1].cpu().numpy()
 
 
+@pytest.fixture(params=["fused", "composed"])
+def xmode(request, monkeypatch):
+    """Both transcoder forms: wire to wire without records in HBM
+    (tgpu_xcode.h; schemas with a flat program in both protocols) and the
+    composed decode + encode (TGPU_XCODE=0)."""
+    monkeypatch.setenv("TGPU_XCODE", "1" if request.param == "fused" else "0")
+    return request.param
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("src,dst", PAIRS, ids=["%s->%s" % p for p in PAIRS])
-def test_gpu_transcode_golden(gpu, src, dst):
+def test_gpu_transcode_golden(gpu, xmode, src, dst):
     a, b = helpers.Case(src), helpers.Case(dst)
     n = min(a.n, b.n)
     wire = a.wire[: int(a.offsets[n])]
@@ -97,7 +106,7 @@ def test_gpu_transcode_golden(gpu, src, dst):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["maps_compact", "unions_binary", "nested_compact_v1",
                                   "scalars_binary"])
-def test_gpu_transcode_errors_match_oracle(gpu, name):
+def test_gpu_transcode_errors_match_oracle(gpu, xmode, name):
     """Damaged input: the reader's status, the records before it transcoded
     (as the oracle does it); a small output: OUTPUT_OVERFLOW at the record
     that does not fit."""
@@ -117,3 +126,63 @@ def test_gpu_transcode_errors_match_oracle(gpu, name):
                                       out_cap=len(full) // 2)
     assert st.code == 21 and 0 < done < c.n
     assert out == full[: len(out)]
+
+
+def _mixed_stream(n, every, proto):
+    """n config-3 records (Compact / Binary, schema `mixed`) whose record i is
+    written with the fields in another order when i % every == 0 (a record
+    the generated readNoXfer reads through its unexpected-field path, and the
+    record program cannot take): the oracle's bytes, record by record."""
+    import datagen
+    from fbthrift_amd.schema import Schema
+
+    table = datagen.SCHEMAS["mixed"]
+    perm = [5, 0, 3, 1, 4, 2]  # declaration order of the reordered writer
+    t2 = [[table[0][k] for k in perm]]
+    recs = [datagen.gen_mixed(i) for i in range(n)]
+    sa, sb = Schema.from_table(table), Schema.from_table(t2)
+    ra, sta, _ = helpers.pack(sa, datagen.flatten_values(table, recs), n)
+    st, wa, oa = oracle.encode(sa, proto, ra, n, sta)
+    assert st.code == 0
+    rb, stb, _ = helpers.pack(sb, datagen.flatten_values(t2, [[r[k] for k in perm] for r in recs]),
+                              n)
+    st, wb, ob = oracle.encode(sb, proto, rb, n, stb)
+    assert st.code == 0
+    parts, offs = [], [0]
+    for i in range(n):
+        w, o = (wb, ob) if i % every == 0 else (wa, oa)
+        parts.append(w[int(o[i]):int(o[i + 1])])
+        offs.append(offs[-1] + len(parts[-1]))
+    return sa, b"".join(parts), np.array(offs, np.uint64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pf,pt", [(2, 0), (0, 2)])
+def test_gpu_transcode_fused_irregular_records(gpu, codec, pf, pt, monkeypatch):
+    """100 003 records, every 997th off the canonical field order: the fused
+    transcoder lists those for the general reader / writer (index_stats
+    'general' counts them) and its output equals the oracle's serialize<To>(
+    deserialize<From>) byte for byte — indexed and unindexed, with and without
+    output offsets, through the compiled and the interpreting program pair."""
+    import torch
+
+    from fbthrift_amd import serializer as S
+
+    monkeypatch.setenv("TGPU_XCODE", "1")
+    n, every = 100_003, 997
+    schema, wire, offs = _mixed_stream(n, every, pf)
+    st, nd, want, woffs = _oracle_transcode(schema, pf, pt, wire, n)
+    assert st.code == 0 and nd == n
+    ser = {0: S.BinarySerializer, 2: S.CompactSerializer}[pf]
+    gs = S.GpuSchema(schema)
+    w = torch.from_numpy(np.frombuffer(wire, np.uint8).copy()).to(gpu)
+    o = torch.from_numpy(offs.astype(np.int64)).to(gpu)
+    for given in (o, None):
+        for want_offs in (True, False):
+            out, go, gst, done, size = ser.transcode(gs, w, n, pt, offsets=given,
+                                                     want_offsets=want_offs)
+            assert gst.code == 0 and done == n, gst.as_tuple()
+            assert bytes(out[:size].cpu().numpy()) == want
+            if want_offs:
+                assert np.array_equal(go.cpu().numpy().astype(np.uint64), np.asarray(woffs, np.uint64))
+            assert ser.context().index_stats()["general"] == (n + every - 1) // every
