@@ -630,19 +630,34 @@ hipError_t launch_deep_size(const EncodeArgs& a, int protocol, hipStream_t strea
   return hipGetLastError();
 }
 
+// The deep pass's writes (wide tier first, then the max_depth tier).
+hipError_t launch_deep_write(const EncodeArgs& a, int protocol, hipStream_t stream) {
+  if (a.deep.lanes && a.deep.wlanes)
+    TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(deep_write_kernel<P_>,
+                                                  dim3((a.deep.wlanes + 63) / 64), dim3(64), 0,
+                                                  stream, a, 1));
+  if (a.deep.lanes)
+    TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(deep_write_kernel<P_>, dim3((a.deep.lanes + 63) / 64),
+                                                  dim3(64), 0, stream, a, 0));
+  return hipGetLastError();
+}
+
 hipError_t launch_general_encode(const EncodeArgs& a, int protocol, uint64_t n_blocks,
-                                 hipStream_t stream, const JitKernels* nj) {
+                                 hipStream_t stream, const JitKernels* nj, bool defer) {
   if (a.n == 0) return hipSuccess;
   const dim3 grid((uint32_t)n_blocks);
   const uint32_t sb = schema_stage_bytes(a.sc);
-  if (nj) {  // the nested program's passes (no record is deferred: bounded depth)
+  if (nj) {  // the nested program's passes
     hipError_t e = jit_launch_encode(nj, false, a, n_blocks, 0, stream, 2);
+    // (a recursive schema's unrolled writer: the records it deferred)
+    if (e == hipSuccess && defer) e = launch_deep_size(a, protocol, stream);
     if (e == hipSuccess)
       e = launch_scan_tiles(a.block_sums, n_blocks, a.scan_part, &a.res->total_bytes,
                             a.offs + a.n, stream);
     // (a.out_cap: the write pass's LDS output tile, 0 = none)
     if (e == hipSuccess)
       e = jit_launch_encode(nj, true, a, n_blocks, a.out_cap ? a.out_cap + 16 : 0, stream, 2);
+    if (e == hipSuccess && defer) e = launch_deep_write(a, protocol, stream);
     return e;
   }
   TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_size_kernel<P_>, grid, dim3(256), sb, stream, a,
@@ -654,24 +669,18 @@ hipError_t launch_general_encode(const EncodeArgs& a, int protocol, uint64_t n_b
   if (e != hipSuccess) return e;
   TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_write_kernel<P_>, grid, dim3(256), sb, stream, a,
                                                 sb));
-  if (a.deep.lanes && a.deep.wlanes)
-    TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(deep_write_kernel<P_>,
-                                                  dim3((a.deep.wlanes + 63) / 64), dim3(64), 0,
-                                                  stream, a, 1));
-  if (a.deep.lanes)
-    TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(deep_write_kernel<P_>, dim3((a.deep.lanes + 63) / 64),
-                                                  dim3(64), 0, stream, a, 0));
-  return hipGetLastError();
+  return launch_deep_write(a, protocol, stream);
 }
 
 hipError_t launch_general_size(const EncodeArgs& a, int protocol, uint64_t n_blocks,
-                               hipStream_t stream, const JitKernels* nj) {
+                               hipStream_t stream, const JitKernels* nj, bool defer) {
   if (a.n == 0) return hipSuccess;
   const dim3 grid((uint32_t)n_blocks);
   const uint32_t sb = schema_stage_bytes(a.sc);
   hipError_t e;
   if (nj) {
     e = jit_launch_encode(nj, false, a, n_blocks, 0, stream, 2);
+    if (e == hipSuccess && defer) e = launch_deep_size(a, protocol, stream);
   } else {
     TGPU_BY_PROTOCOL(protocol, hipLaunchKernelGGL(encode_size_kernel<P_>, grid, dim3(256), sb, stream,
                                                   a, sb));

@@ -36,17 +36,16 @@ using prog::kPosCap;
 using prog::kTile;
 using prog::kTileLanes;
 
-// A speculated chain reads at most kSpecReach bytes past its chunk's end. A
+// A speculated chain reads at most spec_reach bytes (IndexArgs; 256 KiB
+// unless TGPU_INDEX_SPEC_REACH) past its chunk's end. A
 // false start can parse as a container of many elements that are true
 // records (a list<struct> count read from value bytes), which would otherwise
 // walk the rest of the stream on one lane, for every such candidate; past the
 // reach the candidate is rejected like any other that fails to read, and a
 // chunk whose true straddling record is longer than that is left to the
 // repair lane (unbounded).
-constexpr uint64_t kSpecReach = 256 * 1024;
-
 __device__ __forceinline__ uint64_t spec_limit(const IndexArgs& a, uint64_t hi) {
-  return hi + kSpecReach < a.in_len ? hi + kSpecReach : a.in_len;
+  return hi + a.spec_reach < a.in_len ? hi + a.spec_reach : a.in_len;
 }
 
 // lane >= 0: the deep-pass lane whose HBM skip frames the reader may use.
@@ -106,7 +105,7 @@ __device__ __forceinline__ int one_record(const IndexArgs& a, uint64_t p, uint64
 // A record nested past the private skip frames (lane < 0) ends the chain
 // with out.code = kErrDeep: speculation treats it as a failed chain (the
 // repair lane, which has HBM frames, walks it), emission defers the chunk.
-// spec: a speculated chain (bounded reach, see kSpecReach).
+// spec: a speculated chain (bounded reach, see spec_limit).
 template <int P>
 __device__ bool chain(const IndexArgs& a, uint64_t p, uint64_t hi, bool canonical_first,
                       uint8_t* scratch, Chain& out, uint64_t* emit, uint64_t emit_cap,
@@ -338,60 +337,111 @@ __device__ __forceinline__ void index_spec_fallback_one(const IndexArgs& a, uint
 }
 SCRATCH_KERNEL(index_spec_fallback_kernel, index_spec_fallback_one)
 
-// Parallel link repair, one lane per chunk whose speculated start s[j] is not
-// its predecessor's end T = e[j-1]. A false start inside the record straddling
-// the chunk's start parses as records of its own and soon lands on a true
-// record start, after which it runs in step with the true chain. The lane walks
-// the chain from T and the speculated chain from s[j] together (two pointers,
-// the one behind advances) until they meet: from there the speculated chain is
-// the true one, so s[j] = T and cnt[j] = records from T to the meeting point +
-// the speculated chain's records from it. If the walk from T passes the
-// chunk's end first, that walk is the chunk's chain (e[j] replaced). Chunks
-// without an accepted start are parsed from T. Every result is the chunk's
-// chain given T; index_fix_kernel then verifies the links from the true start
-// in order (a chunk whose T changes there is walked again), so this pass only
-// decides speed. A reader error leaves the chunk to index_fix_kernel.
+// The chain of chunk j from a start T, walked only until it meets the
+// chunk's speculated chain (s[j], cnt[j] records to e[j]): a false start
+// inside the record straddling the chunk's start parses as records of its own
+// and soon lands on a true record start, after which it runs in step with the
+// true chain. Two pointers, the one behind advances; met: from the meeting
+// point the speculated chain is T's, so e[j] stands and the count is the
+// records from T to there + the speculated chain's from there. A walk from T
+// that passes the chunk's end first is the chunk's chain (out.end). limit: the
+// reader's end; lane: deep-pass lane (-1: none). Returns false on a reader
+// error of the walk from T (out.code / err_off / end = the failing start).
 template <int P>
-__device__ __forceinline__ void index_merge_one(const IndexArgs& a, uint64_t j) {
-  if (j == 0) return;
-  const uint64_t T = a.e[j - 1];
-  if (T == kNo || T == kErr || T == kPartial) return;
+__device__ bool walk_meet(const IndexArgs& a, uint64_t j, uint64_t T, uint64_t limit,
+                          uint8_t* scratch, int lane, Chain& out, bool& met) {
+  const uint64_t hi = chunk_hi(a, j);
   const uint64_t s0 = a.s[j], e0 = a.e[j];
-  if (s0 == T || e0 == kErr || e0 == kPartial) return;
-  const bool none = s0 == kNo || e0 == kNo;
-  const uint64_t hi = chunk_hi(a, j), limit = spec_limit(a, hi);
-  uint8_t* scratch = a.scratch + j * a.rec_size;
-  uint64_t pt = T, pf = none ? kNo : s0, ct = 0, cf = 0;
-  Chain c{};
+  const bool spec = s0 != kNo && e0 != kNo && e0 != kErr && e0 != kPartial;
+  uint64_t pt = T, pf = spec ? s0 : kNo, ct = 0, cf = 0;
+  met = false;
+  out.code = 0;
   for (;;) {
-    if (pt == pf) break;  // met: the speculated chain from here is the true one
+    if (pt == pf) {
+      met = true;
+      break;
+    }
     if (pt < pf) {
-      if (pt >= hi) break;  // the walk from T is the chunk's whole chain
+      if (pt >= hi) break;
       uint64_t q;
-      if (one_record<P>(a, pt, limit, scratch, -1, true, q, c) < 0) return;
+      Chain c{};
+      if (one_record<P>(a, pt, limit, scratch, lane, true, q, c) < 0) {
+        out.code = c.code;
+        out.err_off = c.err_off;
+        out.end = pt;
+        out.count = ct;
+        return false;
+      }
       pt = q;
       ++ct;
     } else {
-      if (pf >= hi) {  // passed the speculated chain's end: finish from T alone
+      uint64_t q;
+      Chain c{};
+      // past the speculated chain's end, or a record it cannot read again
+      // (a reach-bounded chain): finish from T alone
+      if (pf >= hi || one_record<P>(a, pf, limit, scratch, lane, true, q, c) < 0) {
         pf = kNo;
         continue;
       }
-      uint64_t q;
-      if (one_record<P>(a, pf, limit, scratch, -1, true, q, c) < 0) return;
       pf = q;
       ++cf;
     }
   }
-  if (pt == pf) {
-    a.cnt[j] = ct + (a.cnt[j] - cf);
-  } else {
-    a.cnt[j] = ct;
-    a.e[j] = pt;
-  }
+  out.count = met ? ct + (a.cnt[j] - cf) : ct;
+  out.end = met ? e0 : pt;
+  return true;
+}
+
+// Parallel link repair, one lane per chunk whose start s[j] is not its
+// predecessor's end T: the chain from T (walk_meet), as of the previous
+// round's ends (ep, a snapshot: every chunk of a round reads the same ends,
+// Jacobi). A chunk whose predecessor was right after round r - 1 is right
+// after round r; chains converge within a few records, so one or two rounds
+// usually leave every link consistent. index_fix_kernel then verifies the
+// links from the true start in order, so these rounds only decide speed. A
+// reader error leaves the chunk to index_fix_kernel. Returns whether the
+// chunk changed.
+template <int P>
+__device__ __forceinline__ bool index_merge_one(const IndexArgs& a, uint64_t j) {
+  if (j == 0) return false;
+  const uint64_t T = a.ep[j - 1];
+  if (T == kNo || T == kErr || T == kPartial) return false;
+  const uint64_t s0 = a.s[j], e0 = a.e[j];
+  if (s0 == T || e0 == kErr || e0 == kPartial) return false;
+  const uint64_t hi = chunk_hi(a, j);
+  Chain c{};
+  bool met;
+  if (!walk_meet<P>(a, j, T, spec_limit(a, hi), a.scratch + j * a.rec_size, -1, c, met))
+    return false;
+  a.cnt[j] = c.count;
+  a.e[j] = c.end;
   a.s[j] = T;
   a.pf[j] = 0;
+  return true;
 }
-SCRATCH_KERNEL(index_merge_kernel, index_merge_one)
+
+// One merge round: snapshot of the ends (ep), then the chunks' walks. The
+// counter of round r is scal[16 + (r & 1)]; a round after one that changed
+// nothing returns at once (stream-ordered, no host read).
+__global__ __launch_bounds__(256) void index_merge_snap_kernel(IndexArgs a, int round) {
+  if (round > 0 && a.scal[16 + ((round - 1) & 1)] == 0) return;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < a.n_chunks; j += stride)
+    a.ep[j] = a.e[j];
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.scal[16 + (round & 1)] = 0;
+}
+
+template <int P>
+__global__ __launch_bounds__(256) void index_merge_round_kernel(IndexArgs a, int round) {
+  if (round > 0 && a.scal[16 + ((round - 1) & 1)] == 0) return;
+  const uint64_t stride = (uint64_t)gridDim.x * 256;
+  unsigned int changed = 0;
+  for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < a.n_chunks; j += stride)
+    changed += index_merge_one<P>(a, j) ? 1u : 0u;
+  const int n = __syncthreads_count(changed != 0);
+  if (threadIdx.x == 0 && n) atomicAdd(&a.scal[16 + (round & 1)], (unsigned long long)n);
+}
+
 
 // ---- LDS tiles (schemas with a program; tgpu_prog_kernels.h) ---------------
 __global__ __launch_bounds__(kTileLanes) void index_tile_spec_kernel(IndexArgs a) {
@@ -496,6 +546,7 @@ __device__ __forceinline__ bool take_over(const IndexArgs& a, uint64_t j, uint64
 template <int P>
 __global__ void index_fix_kernel(IndexArgs a) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (a.scal[18]) return;  // the exhaustive resolution set every chunk
   const uint64_t C = a.n_chunks;
   a.scal[2] = kNo;
   a.scal[1] = C;
@@ -534,8 +585,12 @@ __global__ void index_fix_kernel(IndexArgs a) {
         // the speculated chain started with false records inside the record
         // ending at T; from T on it is the true chain
       } else {
-        Chain c;
-        chain<P>(a, T, hi, false, scratch, c, nullptr, 0, kNo, 0);
+        // the chain from T, until it meets the speculated one (walk_meet:
+        // the lane's work is the records up to the meeting point, not the
+        // chunk)
+        Chain c{};
+        bool met;
+        walk_meet<P>(a, j, T, a.in_len, scratch, 0, c, met);
         a.s[j] = T;
         a.cnt[j] = c.count;
         a.pf[j] = 0;
@@ -560,6 +615,172 @@ __global__ void index_fix_kernel(IndexArgs a) {
     }
     next = j + 1;
   }
+}
+
+// ---- exhaustive resolution (opt-in, TGPU_INDEX_EXHAUSTIVE) ------------------
+// Built for program-less streams whose speculation leaves many links broken,
+// on the premise that false chains of the general reader need not meet the
+// true one inside a chunk (a false record read as a long container lands
+// anywhere), so the merge rounds could not fix them and the verification lane
+// would walk the stream alone (round 4: 3.8 s). Measured: with the
+// speculation's reach bounded by the record length, false chains do meet and
+// the merge rounds repair every link; reading every position is 20-40x
+// slower, so this stays off by default. Every byte position p of chunk j is read as
+// a record start (nxt(p) = its end, or a failure), and pointer jumping over
+// the chunk's positions in LDS (13 rounds: 2^13 > the 4 KiB chunk) gives,
+// for each position, the chain's exit past the chunk's end and its records.
+// The first kXWindow entries go to tables xe / xc; one lane then follows the
+// true path T_0 = begin, T_{j+1} = xe[j][T_j - lo_j] — a lookup per chunk
+// where the verification walks the chunk — and sets s / e / cnt. A true entry
+// past the window (a record straddling more than kXWindow bytes into a
+// chunk) or a record nested past the private frames stops the lookups there
+// and leaves the rest to index_fix_kernel; a record the reader rejects on
+// the path ends the stream as index_fix_kernel would.
+constexpr uint32_t kXChunk = 4096;  // (index_chunk_bytes' lane chunks are at most this)
+constexpr uint32_t kXTerm = 0xffffffffu;
+constexpr uint32_t kXFail = 0x80000000u;  // X: the chain stops at a record the reader rejects
+
+// (each position is read from an LDS copy of the chunk and kXReach bytes past
+// it: a record reaching further reads as a failure here — the path lookup
+// re-reads such a record in HBM and, if it is a record, leaves the chunks
+// from there to the verification walk)
+constexpr uint32_t kXReach = 4096;
+
+template <int P>
+__global__ __launch_bounds__(256) void index_xtab_kernel(IndexArgs a) {
+  __shared__ uint32_t T0[kXChunk], K0[kXChunk], X0[kXChunk];
+  __shared__ uint32_t T1[kXChunk], K1[kXChunk], X1[kXChunk];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kXChunk + kXReach + 32];
+  const uint64_t rs = (a.rec_size + 15) & ~15ull;
+  uint8_t* scratch = a.xscratch + ((uint64_t)blockIdx.x * 256 + threadIdx.x) * rs;
+  const uint32_t root = (a.sc.s[0].size + 15) & ~15u;
+  for (uint64_t j = blockIdx.x; j < a.n_chunks; j += gridDim.x) {
+    const uint64_t lo = chunk_lo(a, j), hi = chunk_hi(a, j);
+    const uint32_t len = (uint32_t)(hi - lo);
+    const uint64_t a0 = lo & ~15ull;
+    const uint64_t b1 = hi + a.x_reach < a.in_len ? hi + a.x_reach : a.in_len;
+    const uint32_t nvec = (uint32_t)((b1 - a0 + 15) >> 4);
+    for (uint32_t v = threadIdx.x; v < nvec; v += 256) {
+      const uint64_t g = a0 + 16ull * v;
+      if (g + 16 <= a.in_len) {
+        *(uint4*)(stage + 16 * v) = *(const uint4*)(a.in + g);
+      } else {
+        for (uint32_t b = 0; b < 16; ++b) stage[16 * v + b] = g + b < a.in_len ? a.in[g + b] : 0;
+      }
+    }
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < len; p += 256) {
+      dev::Reader r = dev::make_reader(stage, lo + p, b1, a.string_limit, a.container_limit,
+                                       a.max_depth, a.height);
+      r.base = a0;
+      dev::Arena A = dev::record_arena<P>(a.sc, nullptr, kDiscardArena, lo + p, scratch + root);
+      dev::read_record_any<P>(r, a.sc, scratch, A);
+      // (a failure, a record reaching past the copy, or one nested past the
+      // private frames: the chain stops here)
+      if (!r.ok()) {
+        T0[p] = kXTerm;
+        K0[p] = 0;
+        X0[p] = kXFail | p;
+      } else if (r.pos >= hi) {
+        T0[p] = kXTerm;
+        K0[p] = 1;
+        X0[p] = (uint32_t)(r.pos - lo);
+      } else {
+        T0[p] = (uint32_t)(r.pos - lo);
+        K0[p] = 1;
+        X0[p] = 0;
+      }
+    }
+    __syncthreads();
+    uint32_t *Ta = T0, *Ka = K0, *Xa = X0, *Tb = T1, *Kb = K1, *Xb = X1;
+    for (int rd = 0; rd < 13; ++rd) {
+      bool open = false;
+      for (uint32_t p = threadIdx.x; p < len; p += 256) {
+        const uint32_t t = Ta[p];
+        if (t == kXTerm) {
+          Tb[p] = t;
+          Kb[p] = Ka[p];
+          Xb[p] = Xa[p];
+        } else {
+          const uint32_t t2 = Ta[t];
+          Tb[p] = t2;
+          Kb[p] = Ka[p] + Ka[t];
+          Xb[p] = Xa[t];
+          open |= t2 != kXTerm;
+        }
+      }
+      uint32_t* sw;
+      sw = Ta; Ta = Tb; Tb = sw;
+      sw = Ka; Ka = Kb; Kb = sw;
+      sw = Xa; Xa = Xb; Xb = sw;
+      if (!__syncthreads_or(open)) break;
+    }
+    for (uint32_t w = threadIdx.x; w < kXWindow; w += 256) {
+      uint64_t x = kNo;
+      uint32_t k = 0;
+      if (w < len) {
+        const uint32_t v = Xa[w];
+        x = (v & kXFail) ? ((1ull << 63) | (lo + (v & ~kXFail))) : lo + v;
+        k = Ka[w];
+      }
+      a.xe[j * kXWindow + w] = x;
+      a.xc[j * kXWindow + w] = k;
+    }
+    __syncthreads();  // (the next chunk reuses the arrays)
+  }
+}
+
+// One lane: the true path through the tables (non-speculative ranges).
+// scal[18] = 1: every chunk set (index_fix_kernel has nothing to do).
+template <int P>
+__global__ void index_xresolve_kernel(IndexArgs a) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint64_t C = a.n_chunks;
+  uint64_t T = a.begin;
+  for (uint64_t j = 0; j < C; ++j) {
+    const uint64_t lo = chunk_lo(a, j), hi = chunk_hi(a, j);
+    if (T >= hi) {  // no record starts in this chunk
+      a.s[j] = T;
+      a.e[j] = T;
+      a.cnt[j] = 0;
+      a.pf[j] = 0;
+      continue;
+    }
+    const uint64_t w = T - lo;
+    if (w >= kXWindow) return;
+    const uint64_t x = a.xe[j * kXWindow + w];
+    const uint32_t k = a.xc[j * kXWindow + w];
+    if (x == kNo) return;
+    if (x >> 63) {
+      // the chain from T stops at a record the reader rejects, k records in;
+      // read it with the deep slab (a record nested past the private frames
+      // is not a failure: the verification walks on from there)
+      const uint64_t f = x & ~(1ull << 63);
+      uint64_t q = 0;
+      Chain c{};
+      if (one_record<P>(a, f, a.in_len, a.scratch, 0, true, q, c) > 0) return;
+      a.s[j] = T;
+      a.cnt[j] = k;
+      a.pf[j] = 0;
+      a.e[j] = f;
+      a.scal[1] = j + 1;
+      a.scal[2] = j;
+      a.scal[3] = k;
+      a.scal[4] = f;
+      a.res->code = c.code;
+      a.res->fail_offset = c.err_off;
+      a.scal[18] = 1;
+      return;
+    }
+    a.s[j] = T;
+    a.e[j] = x;
+    a.cnt[j] = k;
+    a.pf[j] = 0;
+    T = x;
+  }
+  a.scal[1] = C;
+  a.scal[2] = kNo;
+  a.scal[18] = 1;
 }
 
 __global__ __launch_bounds__(256) void index_prep_kernel(IndexArgs a) {
@@ -692,13 +913,15 @@ hipError_t launch_index_empty(DevResult* res, uint64_t* offs, uint64_t pos, uint
 uint64_t index_tile_bytes() { return kTile; }
 uint64_t index_tile_lanes() { return kTileLanes; }
 
-uint64_t index_chunk_bytes(uint64_t span, bool tiles) {
+uint64_t index_chunk_bytes(uint64_t span, bool tiles, uint64_t mean) {
   // schemas with a program: LDS tiles once there are enough of them
   if (tiles && span >= 64ull * kTile) return kTile;
   // lane chunks: ~1k+ chunks keep the chip busy; chunks stay >= 1 KiB so a
   // chunk holds several records and speculation has a long chain to confirm
+  // (about 16 records when the mean record length is known)
   uint64_t c = 4096;
-  while (c > 1024 && span / c < 4096) c >>= 1;
+  while (c > 1024 && (span / c < 4096 || (mean && c > 16 * mean))) c >>= 1;
+  if (const char* v = getenv("TGPU_INDEX_CHUNK")) c = std::max(64, std::min(atoi(v), 4096));
   return c;
 }
 
@@ -757,8 +980,12 @@ __global__ __launch_bounds__(256) void index_summary_kernel(IndexArgs a) {
 }
 
 hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const JitKernels* jit,
-                               bool* fused, uint64_t* h_sync) {
+                               bool* fused, uint64_t* h_sync, const XTabAlloc* xalloc) {
   PhaseTimer pt(stream);
+  {  // (merge-round counters, the exhaustive resolution's flag)
+    const hipError_t e0 = hipMemsetAsync(a.scal + 16, 0, 8 * sizeof(unsigned long long), stream);
+    if (e0 != hipSuccess) return e0;
+  }
   // (st_decode: the caller decodes from the index; the finish keeps the tail rule)
   const bool decode = a.recs && a.prog && a.chunk == kTile && !a.st_decode;
   if (fused) *fused = decode;
@@ -816,8 +1043,17 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
   if (a.prog && !a.speculative && need_fallback)
     TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_spec_fallback_kernel<P_>, sg, b, 0, stream, a));
   pt.mark("fallback");
-  if (need_merge)
-    TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_merge_kernel<P_>, sg, b, 0, stream, a));
+  if (need_merge) {
+    // Jacobi rounds of the parallel repair (TGPU_MERGE_ROUNDS, default 6;
+    // rounds after one that changed nothing return at once)
+    int rounds = 6;
+    if (const char* v = getenv("TGPU_MERGE_ROUNDS")) rounds = atoi(v);
+    for (int r = 0; r < rounds; ++r) {
+      hipLaunchKernelGGL(index_merge_snap_kernel, sg, b, 0, stream, a, r);
+      TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_merge_round_kernel<P_>, sg, b, 0, stream,
+                                                      a, r));
+    }
+  }
   // sst is written by the general speculation and the fallback only (and by
   // the fallback only when it ran: a skipped one leaves an earlier call's
   // starts in the reused workspace)
@@ -827,6 +1063,40 @@ hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const Jit
   e = launch_scan_tiles(a.base, C, a.part, a.scal, nullptr, stream);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(index_list_kernel, g, b, 0, stream, a);
+  // the exhaustive resolution of a program-less stream's links (blocking
+  // calls), opt-in: TGPU_INDEX_EXHAUSTIVE=1 always, =2 when more than 64
+  // links are broken (the count read mid-call). Measured slower than the
+  // merge rounds once the speculation's reach follows the record length
+  // (1.6-3.0 s against 78 ms on the adversarial stream)
+  if (h_sync && xalloc && !a.prog && !a.speculative && a.chunk <= kXChunk) {
+    const char* xv = getenv("TGPU_INDEX_EXHAUSTIVE");
+    const int mode = xv ? atoi(xv) : 0;
+    uint64_t bad = 0;
+    if (mode == 2) {
+      e = hipMemcpyAsync(h_sync, a.scal, sizeof(uint64_t), hipMemcpyDeviceToHost, stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(stream);
+      if (e != hipSuccess) return e;
+      bad = h_sync[0];
+    }
+    if (mode == 1 || (mode == 2 && bad > 64)) {
+      const uint32_t grid = (uint32_t)std::min<uint64_t>(C, 1024);
+      const uint64_t rs = (a.rec_size + 15) & ~15ull;
+      const uint64_t tab = C * kXWindow;
+      const uint64_t bytes = tab * 8 + ((tab * 4 + 15) & ~15ull) + (uint64_t)grid * 256 * rs;
+      uint8_t* w = xalloc->get(xalloc->user, bytes);
+      if (w) {
+        IndexArgs y = a;
+        y.xe = (uint64_t*)w;
+        y.xc = (uint32_t*)(w + tab * 8);
+        y.xscratch = w + tab * 8 + ((tab * 4 + 15) & ~15ull);
+        TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_xtab_kernel<P_>, dim3(grid), b, 0,
+                                                        stream, y));
+        TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_xresolve_kernel<P_>, dim3(1), dim3(64),
+                                                        0, stream, y));
+        pt.mark("exhaustive");
+      }
+    }
+  }
   TGPU_BY_PROTOCOL(a.protocol, hipLaunchKernelGGL(index_fix_kernel<P_>, dim3(1), dim3(64), 0, stream, a));
   pt.mark("fix");
   hipLaunchKernelGGL(index_prep_kernel, g, b, 0, stream, a);

@@ -1,6 +1,8 @@
 // k_transcode.hip — the wire-to-wire transcoder's launch sequence
 // (tgpu_xcode.h) and its general-reader / general-writer kernels for the
 // records the programs cannot take:
+//   xc_one (program pair, single pass: decode, size, look back, emit) — done
+//   unless it listed records; otherwise, or without the single pass:
 //   xc_size (program pair)  -> general decode of the listed records into the
 //   record workspace (+ deep pass) -> xc_irr_size (their target sizes, added
 //   to the tiles' sums) -> tile scan -> xc_write (program pair; holes for the
@@ -35,6 +37,15 @@ __global__ __launch_bounds__(kPT) void xc_write_kernel(XcodeArgs x, const VProgr
   __shared__ prog::EncodeShared sm;
   prog::xc_write_tile<prog::DynProg, prog::DynProg, 0>(x, prog::DynProg{ps}, prog::DynProg{pd}, S,
                                                        wire_cap, ocap, smem, sm);
+}
+
+__global__ __launch_bounds__(kPT) void xc_one_kernel(XcodeArgs x, const VProgram* __restrict__ ps,
+                                                     const VProgram* __restrict__ pd, uint32_t S,
+                                                     uint32_t wire_cap, uint32_t ocap) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  __shared__ prog::EncodeShared sm;
+  prog::xc_one_tile<prog::DynProg, prog::DynProg, 0>(x, prog::DynProg{ps}, prog::DynProg{pd}, S,
+                                                     wire_cap, ocap, smem, sm);
 }
 
 // The listed records' target sizes (decoded by the general reader into
@@ -121,15 +132,50 @@ hipError_t launch_xcode(const XcodeArgs& x, int from, int to, const VProgram* d_
   const uint32_t S = x.d.rec_size;
   const bool rr = jit && jit_has(jit, 2);  // records in registers (S <= 128, S % 8 == 0)
   const uint32_t rt = rr ? 0u : prog::xc_rec_region(S, 0);
-  const uint32_t cap = program_decode_wire_cap(x.d, S, 0, rr);
+  uint32_t cap = program_decode_wire_cap(x.d, S, 0, rr);
+  // output tile: the encoder's 24 KiB (a record past it goes to HBM
+  // directly), or — sized with the wire tile for the most workgroups per CU
+  // that hold 1.04 x the mean tile of each (x.out_mean: the host's estimate)
+  // — what that residency leaves. (Config 3, Compact -> Binary: 16 KiB wire +
+  // 24 KiB output + the static LDS crossed 40 KiB, 3 workgroups per CU.)
+  uint32_t ocap = prog::kOutCap;
+  if (x.out_mean) {
+    const double in_tile = (double)x.d.in_len / (double)n * kPT;
+    const double want_w = 1.04 * in_tile + 256.0, max_w = 1.12 * in_tile + 512.0;
+    const double want_o = std::min(1.04 * (double)x.out_mean * kPT + 256.0, (double)prog::kOutCap);
+    for (uint32_t w = 8; w >= 1; --w) {
+      const uint32_t budget = 163840u / w - 256u - rt;  // (the static LDS and slack)
+      const uint32_t rw = prog::decode_wire_region((uint32_t)want_w);
+      if (rw + want_o + 32 > budget) continue;
+      // the largest wire cap within the staging rounds the tile needs
+      uint32_t c = std::min<uint32_t>((uint32_t)max_w, rw - 32) & ~15u;
+      c = std::max(c, std::min<uint32_t>((uint32_t)want_w, rw - 32) & ~15u);
+      cap = std::max<uint32_t>(c, 4096);
+      ocap = std::min<uint32_t>(prog::kOutCap, budget - prog::decode_wire_region(cap) - 32) & ~15u;
+      break;
+    }
+  }
+  if (const char* v = getenv("TGPU_XC_OCAP"))  // (A/B)
+    if (*v) ocap = (uint32_t)atoi(v) & ~15u;
   const uint32_t lds_a = prog::decode_wire_region(cap) + rt;
-  // output tile: the mean record's target size is unknown before the size
-  // pass; 24 KiB as the encoder's (a record past it goes to HBM directly)
-  const uint32_t ocap = prog::kOutCap;
   const uint32_t lds_c = lds_a + ocap + 32;
   const uint64_t tiles = (n + kPT - 1) / kPT;
   hipError_t e;
-  if (jit) {
+  XcodeArgs y = x;  // (the two-pass kernels: gated behind a single pass)
+  y.gate = x.xstat ? x.xstat + tiles : nullptr;
+  if (x.xstat) {
+    // single pass; the kernels below it find nothing to do unless it listed
+    // records or a wait passed its bound (the gate word)
+    e = hipMemsetAsync(x.xstat, 0, (tiles + 1) * sizeof(unsigned long long), s);
+    if (e != hipSuccess) return e;
+    if (jit && jit_has(jit, rr ? 5 : 4)) {
+      e = jit_launch_xcode(jit, rr ? 5 : 4, x, tiles, cap, ocap, lds_c, s);
+    } else {
+      hipLaunchKernelGGL(xc_one_kernel, dim3((uint32_t)tiles), dim3(kPT), lds_c, s, x, d_ps, d_pd,
+                         S, cap, ocap);
+      e = hipGetLastError();
+    }
+  } else if (jit) {
     e = jit_launch_xcode(jit, rr ? 2 : 0, x, tiles, cap, ocap, lds_a, s);
   } else {
     hipLaunchKernelGGL(xc_size_kernel, dim3((uint32_t)tiles), dim3(kPT), lds_a, s, x, d_ps, d_pd, S,
@@ -153,9 +199,9 @@ hipError_t launch_xcode(const XcodeArgs& x, int from, int to, const VProgram* d_
                           x.want_offs ? x.e.offs + n : nullptr, s);
   if (e != hipSuccess) return e;
   if (jit) {
-    e = jit_launch_xcode(jit, rr ? 3 : 1, x, tiles, cap, ocap, lds_c, s);
+    e = jit_launch_xcode(jit, rr ? 3 : 1, y, tiles, cap, ocap, lds_c, s);
   } else {
-    hipLaunchKernelGGL(xc_write_kernel, dim3((uint32_t)tiles), dim3(kPT), lds_c, s, x, d_ps, d_pd,
+    hipLaunchKernelGGL(xc_write_kernel, dim3((uint32_t)tiles), dim3(kPT), lds_c, s, y, d_ps, d_pd,
                        S, cap, ocap);
     e = hipGetLastError();
   }

@@ -136,6 +136,12 @@ struct tgpu_context {
   // asked for none (the listed records' holes, the finish's failing record)
   uint8_t* d_xoffs = nullptr;
   uint64_t xoffs_bytes = 0;
+  // the stream index's exhaustive resolution (k_index.hip), on demand
+  uint8_t* d_xtab = nullptr;
+  uint64_t xtab_bytes = 0;
+  // the single-pass transcoder's look-back status words (tiles + 1)
+  uint8_t* d_xstat = nullptr;
+  uint64_t xstat_bytes = 0;
 };
 
 namespace tgpu {
@@ -145,11 +151,12 @@ bool valid_protocol(int p) {
   return p == TGPU_PROTOCOL_BINARY || p == TGPU_PROTOCOL_COMPACT || p == TGPU_PROTOCOL_COMPACT_V1;
 }
 // The record program that runs `protocol`: CompactV1 differs from Compact
-// only in the byte order of doubles (CompactV1Protocol-inl.h:36-41,73-79), so
-// a schema without doubles runs Compact's program; with doubles, none (the
-// general kernels, instantiated for CompactV1).
+// only in the byte order of doubles (CompactV1Protocol-inl.h:44-53,84), so
+// a schema without doubles runs Compact's program; with doubles, its own
+// (slot kV1Slot: Compact's ops with the doubles' ops little-endian,
+// kFixedLE).
 int prog_protocol(const tgpu_schema* s, int protocol) {
-  if (protocol == TGPU_PROTOCOL_COMPACT_V1) return s->has_double ? -1 : TGPU_PROTOCOL_COMPACT;
+  if (protocol == TGPU_PROTOCOL_COMPACT_V1) return s->has_double ? kV1Slot : TGPU_PROTOCOL_COMPACT;
   return protocol;
 }
 bool has_prog(const tgpu_schema* s, int protocol) {
@@ -691,13 +698,14 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
     v.isset = (uint16_t)isset;
     if (is_scalar(f.ttype)) {
       const uint32_t w = scalar_size(f.ttype);
-      if (proto == TGPU_PROTOCOL_COMPACT &&
+      if (proto != TGPU_PROTOCOL_BINARY &&
           (f.ttype == TGPU_T_I16 || f.ttype == TGPU_T_I32 || f.ttype == TGPU_T_I64)) {
         v.kind = VOP_VARINT;
         v.bits = f.ttype == TGPU_T_I64 ? 64 : 32;
       }
       v.width = (uint8_t)w;
       v.is_bool = f.ttype == TGPU_T_BOOL;
+      if (proto == TGPU_PROTOCOL_COMPACT_V1 && f.ttype == TGPU_T_DOUBLE) v.bits = kFixedLE;
       if (!push_op(P, v)) return false;
     } else if (f.ttype == TGPU_T_STRING) {
       v.kind = VOP_STRING;
@@ -717,7 +725,8 @@ bool emit_program(const tgpu_schema& sc, uint32_t si, uint32_t base, int proto, 
       v.elem_ct = (uint8_t)compact_ctype(e);
       v.elem_kind = VEL_FIXED;
       if (e == TGPU_T_BOOL) v.elem_kind = VEL_BOOL;
-      if (proto == TGPU_PROTOCOL_COMPACT &&
+      if (proto == TGPU_PROTOCOL_COMPACT_V1 && e == TGPU_T_DOUBLE) v.bits = kFixedLE;
+      if (proto != TGPU_PROTOCOL_BINARY &&
           (e == TGPU_T_I16 || e == TGPU_T_I32 || e == TGPU_T_I64)) {
         v.elem_kind = VEL_VARINT;
         v.bits = e == TGPU_T_I64 ? 64 : 32;
@@ -773,7 +782,8 @@ bool emit_leaf(uint32_t t, uint32_t member, int proto, VProgram& P) {
   } else if (is_scalar(t)) {
     v.width = (uint8_t)scalar_size(t);
     v.is_bool = t == TGPU_T_BOOL;
-    if (proto == TGPU_PROTOCOL_COMPACT && (t == TGPU_T_I16 || t == TGPU_T_I32 || t == TGPU_T_I64)) {
+    if (proto == TGPU_PROTOCOL_COMPACT_V1 && t == TGPU_T_DOUBLE) v.bits = kFixedLE;
+    if (proto != TGPU_PROTOCOL_BINARY && (t == TGPU_T_I16 || t == TGPU_T_I32 || t == TGPU_T_I64)) {
       v.kind = VOP_VARINT;
       v.bits = t == TGPU_T_I64 ? 64 : 32;
     }
@@ -832,7 +842,8 @@ bool emit_container(const tgpu_schema& sc, uint32_t ttype, uint32_t et, uint32_t
       } else {
         v.width = (uint8_t)scalar_size(et);
         v.elem_kind = et == TGPU_T_BOOL ? VEL_BOOL : VEL_FIXED;
-        if (proto == TGPU_PROTOCOL_COMPACT &&
+        if (proto == TGPU_PROTOCOL_COMPACT_V1 && et == TGPU_T_DOUBLE) v.bits = kFixedLE;
+        if (proto != TGPU_PROTOCOL_BINARY &&
             (et == TGPU_T_I16 || et == TGPU_T_I32 || et == TGPU_T_I64)) {
           v.elem_kind = VEL_VARINT;
           v.bits = et == TGPU_T_I64 ? 64 : 32;
@@ -905,12 +916,13 @@ bool emit_container(const tgpu_schema& sc, uint32_t ttype, uint32_t et, uint32_t
 // holds VOP_DEFERs (decode / measure only: the writer stays general).
 bool build_nested_program(const tgpu_schema& sc, int proto, VProgram& P, uint32_t& depth,
                           bool* deferred = nullptr) {
+  if (proto == kV1Slot) proto = TGPU_PROTOCOL_COMPACT_V1;  // (a program slot)
   const char* v = getenv("TGPU_NESTED_UNROLL");
   const uint32_t max_unroll = v ? (uint32_t)std::min(atoi(v) < 0 ? 0 : atoi(v), 64) : 16u;
   if (deferred) *deferred = false;
   for (uint32_t k = max_unroll ? max_unroll : 1; k >= 1; --k) {
     P = VProgram{};
-    P.protocol = (uint32_t)proto;
+    P.protocol = (uint32_t)(proto == TGPU_PROTOCOL_COMPACT_V1 ? TGPU_PROTOCOL_COMPACT : proto);
     P.rec_size = sc.structs[0].size;
     depth = 0;
     t_open_structs.clear();
@@ -993,9 +1005,11 @@ bool schema_recursive(const tgpu_schema& sc) {
   return rec;
 }
 
+// (proto: a protocol id or a program slot: kV1Slot is CompactV1's)
 bool build_program(const tgpu_schema& sc, int proto, VProgram& P, bool tolerant = false) {
+  if (proto == kV1Slot) proto = TGPU_PROTOCOL_COMPACT_V1;
   P = VProgram{};
-  P.protocol = (uint32_t)proto;
+  P.protocol = (uint32_t)(proto == TGPU_PROTOCOL_COMPACT_V1 ? TGPU_PROTOCOL_COMPACT : proto);
   P.rec_size = sc.structs[0].size;
   if (!emit_program(sc, 0, 0, proto, P) || P.n_ops >= (uint32_t)kMaxProgramOps) return false;
   VOp stop = make_op(VOP_CONST);
@@ -1250,15 +1264,22 @@ uint64_t measure_scratch(const tgpu_schema* s) {
 // none — no nested program, a height below its nesting (decode),
 // TGPU_NESTED=0, not compiled).
 const JitKernels* nested_jit(const tgpu_schema* schema, int protocol, uint64_t n, int32_t height,
-                             int32_t max_depth, bool writer = false) {
+                             int32_t max_depth) {
   const char* v = getenv("TGPU_NESTED");
   if (v && v[0] == '0') return nullptr;
   const int q = prog_protocol(schema, protocol);
   if (q < 0 || !schema->has_nprog[q] || n == 0) return nullptr;
-  if (writer && schema->nprog_defer[q]) return nullptr;  // (no deferred records on write)
   const int32_t need = (int32_t)schema->nprog_depth[q] + 1;
   if (height < need || max_depth < need) return nullptr;
   return jit_kernels(schema->nprog[q], schema->device, JIT_NESTED, n, 0, false);
+}
+
+// Whether the schema's nested program is a recursive schema's unrolled one
+// (VOP_DEFER: its writer hands the records nesting past its levels to the
+// general writer's deep pass).
+bool nested_defers(const tgpu_schema* schema, int protocol) {
+  const int q = prog_protocol(schema, protocol);
+  return q >= 0 && schema->nprog_defer[q];
 }
 
 // The nested program's compiled decode (JIT_NESTED) of an indexed batch,
@@ -1426,13 +1447,29 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
     x.prog = schema->d_nprog[pq];
     dec = nullptr;
   }
-  if (x.prog) {
+  const char* hm = getenv("TGPU_INDEX_HMASK");  // "0": no first-byte filter (A/B, tests)
+  if (x.prog || (hm && hm[0] == '0')) {
     for (uint32_t& w : x.hmask) w = ~0u;
   } else {
     record_first_bytes(*schema, protocol, x.hmask);
   }
-  x.chunk = index_chunk_bytes(end > begin ? end - begin : 0, x.prog != nullptr);
+  // program-less speculation runs the general reader from every candidate:
+  // when the call says how many records it expects (a decode of n records),
+  // chunks and the speculated chains' reach follow the mean record length —
+  // a false candidate's chain costs its reach, and more, shorter chunks keep
+  // more lanes busy (1 Mi-record adversarial V1 stream, first-byte filter
+  // off: 5.5 s with 4 KiB chunks and a 256 KiB reach, 78 ms with 1 KiB and
+  // 256 B). Otherwise a 256 KiB reach.
+  const uint64_t span = end > begin ? end - begin : 0;
+  const uint64_t mean = !x.prog && dec && dec->n && dec->n < span ? span / dec->n : 0;
+  x.chunk = index_chunk_bytes(span, x.prog != nullptr, mean);
   x.window = (uint32_t)std::min<uint64_t>(x.chunk, 1024);
+  x.spec_reach = mean ? (uint32_t)std::min<uint64_t>(std::max<uint64_t>(4 * mean, 256), 256u * 1024)
+                      : 256u * 1024;
+  if (const char* v = getenv("TGPU_INDEX_SPEC_REACH")) x.spec_reach = (uint32_t)atoi(v);
+  x.x_reach = 4096;
+  if (const char* v = getenv("TGPU_INDEX_XREACH"))
+    x.x_reach = std::min<uint32_t>((uint32_t)atoi(v), 4096);
   x.n_chunks = end > begin ? (end - begin + x.chunk - 1) / x.chunk : 0;
   x.offs = offs;
   x.max_records = max_records;
@@ -1463,7 +1500,7 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
                     : 0;
   const uint64_t st_bytes = (2 * (uint64_t)x.st_cap * C + 15) & ~15ull;
   const uint64_t need =
-      8 * ((9 + kSpecStarts) * C + parts + 17) + C * rs + 4 * lane_words + 16 + st_bytes;
+      8 * ((9 + kSpecStarts) * C + parts + 25) + C * rs + 4 * lane_words + 16 + st_bytes;
   if (need > ctx->index_bytes) {
     if (ctx->d_index) (void)hipFree(ctx->d_index);
     ctx->d_index = nullptr;
@@ -1482,7 +1519,7 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   x.ec = (unsigned long long*)(w + 7 * C);
   x.part = (unsigned long long*)(w + 8 * C);
   x.scal = (unsigned long long*)(w + 8 * C + parts);
-  x.scratch = (uint8_t*)(w + 8 * C + parts + 16);
+  x.scratch = (uint8_t*)(w + 8 * C + parts + 24);  // (scal: 24 words)
   x.lanes = (uint32_t*)(x.scratch + C * rs);
   x.deep_chunks = (uint64_t*)(x.lanes + lane_words + (lane_words & 1));
   x.sst = x.deep_chunks + C;
@@ -1535,7 +1572,21 @@ int launch_index(tgpu_context* ctx, const tgpu_schema* schema, int protocol, con
   if (h_sync) h_sync[3] = ~0ull;
   ctx->last_scal = x.scal;
   ctx->last_chunks = x.n_chunks;
-  if (e == hipSuccess) e = launch_index_stream(x, s, jit, fused, h_sync);
+  // (grow-only; a failed allocation leaves the verification walk to it)
+  const XTabAlloc xalloc{ctx, [](void* u, uint64_t bytes) -> uint8_t* {
+                           tgpu_context* c = static_cast<tgpu_context*>(u);
+                           if (bytes <= c->xtab_bytes) return c->d_xtab;
+                           if (c->d_xtab) (void)hipFree(c->d_xtab);
+                           c->d_xtab = nullptr;
+                           c->xtab_bytes = 0;
+                           if (hipMalloc(&c->d_xtab, bytes) != hipSuccess) {
+                             (void)hipGetLastError();
+                             return nullptr;
+                           }
+                           c->xtab_bytes = bytes;
+                           return c->d_xtab;
+                         }};
+  if (e == hipSuccess) e = launch_index_stream(x, s, jit, fused, h_sync, &xalloc);
   if (timing) (void)hipEventRecord(tev[1], s);
   struct TimingReport {
     hipEvent_t* ev;
@@ -1737,7 +1788,10 @@ int tgpu_schema_create_ex(const tgpu_struct_desc* structs, uint32_t n_structs,
     return TGPU_ERR_HIP;
   }
   s->recursive = schema_recursive(*s);
-  for (int proto : {TGPU_PROTOCOL_BINARY, TGPU_PROTOCOL_COMPACT}) {
+  // program slots: Binary, Compact, and CompactV1's (kV1Slot) for a schema
+  // with doubles (without, CompactV1 runs Compact's)
+  for (int proto : {(int)TGPU_PROTOCOL_BINARY, (int)TGPU_PROTOCOL_COMPACT, kV1Slot}) {
+    if (proto == kV1Slot && !s->has_double) continue;
     const bool flat = build_program(*s, proto, s->prog[proto]);
     // the nested program: schemas with containers of structs / containers,
     // and schemas with no canonical record program (optional fields)
@@ -1935,6 +1989,8 @@ void tgpu_context_destroy(tgpu_context* c) {
   if (c->d_xrec) (void)hipFree(c->d_xrec);
   if (c->d_xarena) (void)hipFree(c->d_xarena);
   if (c->d_xoffs) (void)hipFree(c->d_xoffs);
+  if (c->d_xtab) (void)hipFree(c->d_xtab);
+  if (c->d_xstat) (void)hipFree(c->d_xstat);
   delete c;
 }
 
@@ -2046,9 +2102,9 @@ int tgpu_encode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
         e = launch_program_encode(a, schema->d_prog[prog_protocol(schema, protocol)], ctx->d_scan_part, false, s,
                                   schema_jit(schema, protocol, JIT_ENCODE, n, 0));
       else {  // (the writer has no depth limit: height / max_depth do not apply)
-        const JitKernels* nj = nested_jit(schema, protocol, n, INT32_MAX, INT32_MAX, true);
+        const JitKernels* nj = nested_jit(schema, protocol, n, INT32_MAX, INT32_MAX);
         if (nj) a.out_cap = nested_out_cap(schema, protocol);
-        e = launch_general_encode(a, protocol, nb, s, nj);
+        e = launch_general_encode(a, protocol, nb, s, nj, nj && nested_defers(schema, protocol));
       }
     }
   }
@@ -2110,8 +2166,9 @@ int tgpu_encoded_size(tgpu_context* ctx, const tgpu_schema* schema, int protocol
                                 schema_jit(schema, protocol, JIT_ENCODE, n, 0));
       if (e == hipSuccess) e = launch_size_offsets(a, (n + 255) / 256, s);
     } else {
-      e = launch_general_size(a, protocol, (n + 255) / 256, s,
-                              nested_jit(schema, protocol, n, INT32_MAX, INT32_MAX, true));
+      const JitKernels* nj = nested_jit(schema, protocol, n, INT32_MAX, INT32_MAX);
+      e = launch_general_size(a, protocol, (n + 255) / 256, s, nj,
+                              nj && nested_defers(schema, protocol));
     }
   }
   if (e == hipSuccess && n) e = launch_encode_finish(a, protocol, 0, s);
@@ -2362,6 +2419,11 @@ int transcode_fused(tgpu_context* ctx, const tgpu_schema* schema, int from, int 
   if (!rc) rc = grow(ctx->d_xrec, ctx->xrec_bytes, std::max<uint64_t>(n * rs, 16));
   if (!rc && acap) rc = grow(ctx->d_xarena, ctx->xarena_bytes, acap);
   if (!rc && !out_offsets) rc = grow(ctx->d_xoffs, ctx->xoffs_bytes, (n + 1) * sizeof(uint64_t));
+  // the single pass (default; TGPU_XCODE_ONEPASS=0: the two tile passes)
+  const char* op = getenv("TGPU_XCODE_ONEPASS");
+  const bool one = !(op && op[0] == '0');
+  const uint64_t tiles = (n + 255) / 256;
+  if (!rc && one) rc = grow(ctx->d_xstat, ctx->xstat_bytes, (tiles + 1) * sizeof(uint64_t));
   if (rc) {
     fill_status(st, rc, 0, 0);
     return rc;
@@ -2401,6 +2463,17 @@ int transcode_fused(tgpu_context* ctx, const tgpu_schema* schema, int from, int 
   x.irr = ctx->d_irr;
   x.nirr = &ctx->d_res->n_irregular;
   x.want_offs = out_offsets ? 1u : 0u;
+  x.xstat = one ? (unsigned long long*)ctx->d_xstat : nullptr;
+  {
+    // the target's bytes per record for the LDS output tile: the source's
+    // mean, or more where the target's smallest record is larger (Compact ->
+    // Binary: fixed-width integers, 3-byte field headers)
+    const int qs = prog_protocol(schema, from), qd = prog_protocol(schema, to);
+    const uint64_t in_mean = n ? in_len / n : 0;
+    const uint64_t ms = prog_min_len(schema->prog[qs]), md = prog_min_len(schema->prog[qd]);
+    const uint64_t est = in_mean + (md > ms ? md - ms : 0);
+    x.out_mean = (uint32_t)std::min<uint64_t>(est, 1u << 20);
+  }
   (void)hipGetLastError();  // drop a stale error left by another library
   hipError_t e = launch_result_init(ctx->d_res, n, s);
   if (offsets) {

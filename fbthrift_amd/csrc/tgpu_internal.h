@@ -234,6 +234,13 @@ struct VOp {
 // scalars or strings — a newer writer's appended fields
 // (deserialize_struct.whisker: unknown ids go to skip).
 constexpr uint8_t kStopSkipsUnknown = 1;
+// FIXED op / LIST op with VEL_FIXED elements (`bits`, otherwise unused
+// there): the value is little-endian on the wire — CompactV1's doubles
+// (CompactV1Protocol-inl.h:44-53,84: writeLE / readLE). A CompactV1
+// program is Compact's (protocol COMPACT) with these ops; it lives in
+// program slot kV1Slot.
+constexpr uint8_t kFixedLE = 1;
+constexpr int kV1Slot = 1;
 constexpr int kMaxProgramOps = 128;  // flat record programs
 // nested programs (op indices and value-op counts are bytes: at most 255)
 constexpr int kMaxNestedOps = 255;
@@ -351,7 +358,14 @@ struct XcodeArgs {
   uint64_t* irr;              // records left to the general reader / writer
   unsigned long long* nirr;
   uint32_t want_offs;         // the caller asked for every output start
-  uint32_t pad_;
+  uint32_t out_mean;          // estimated target bytes per record (LDS sizing; 0: unknown)
+  // single pass (tgpu_xcode.h xc_one_tile): per-tile look-back status words
+  // (tiles + 1, zeroed before the launch; nullptr: the two tile passes)
+  unsigned long long* xstat;
+  // the two-pass kernels behind a single pass run only when *gate != 0 (a
+  // record left to the general reader, or a look-back past its bound);
+  // nullptr: always
+  const unsigned long long* gate;
 };
 
 // ---- stream indexer (k_index.hip) -------------------------------------------
@@ -419,6 +433,26 @@ struct IndexArgs {
   // start with (a root field's header, or STOP), one bit each — every
   // record of a speculated chain must (the fallback pass takes any)
   uint32_t hmask[8];
+  // exhaustive resolution (program-less streams whose speculation left many
+  // links broken, k_index.hip index_xtab_kernel): per chunk and entry offset
+  // w < kXWindow, the chain's exit (bit 63: it ends in a record the reader
+  // rejects, at that position) and its records; per-lane reader scratch
+  uint64_t* xe;
+  uint32_t* xc;
+  uint8_t* xscratch;
+  // bytes a speculated chain may read past its chunk (kSpecReach default;
+  // TGPU_INDEX_SPEC_REACH) and a position's record past the exhaustive
+  // resolution's chunk (<= kXReach; TGPU_INDEX_XREACH)
+  uint32_t spec_reach;
+  uint32_t x_reach;
+};
+constexpr uint32_t kXWindow = 256;  // entry offsets per chunk in the exhaustive tables
+
+// Workspace of the exhaustive resolution, allocated only when a call needs
+// it (tgpu_api.cpp: the context's grow-only buffer); nullptr: unavailable.
+struct XTabAlloc {
+  void* user;
+  uint8_t* (*get)(void* user, uint64_t bytes);
 };
 
 // Workgroups of the grid-stride kernels whose lanes run the general reader
@@ -552,13 +586,15 @@ hipError_t launch_tail_decode_finish(const DecodeArgs& a, int protocol, uint64_t
 hipError_t launch_decode_finish(const DecodeArgs& a, int protocol,
                                 uint64_t fixed_len, hipStream_t stream);
 // nj: a nested program's compiled kernels (JIT_NESTED) for the size / write
-// passes instead of the general writer's (nullptr: the general writer).
+// passes instead of the general writer's (nullptr: the general writer);
+// defer: its program is a recursive schema's unrolled one, whose deferred
+// records the deep pass sizes and writes.
 hipError_t launch_general_encode(const EncodeArgs& a, int protocol,
                                  uint64_t n_blocks, hipStream_t stream,
-                                 const JitKernels* nj = nullptr);
+                                 const JitKernels* nj = nullptr, bool defer = false);
 hipError_t launch_general_size(const EncodeArgs& a, int protocol,
                                uint64_t n_blocks, hipStream_t stream,
-                               const JitKernels* nj = nullptr);
+                               const JitKernels* nj = nullptr, bool defer = false);
 hipError_t launch_encode_finish(const EncodeArgs& a, int protocol,
                                 uint64_t fixed_len, hipStream_t stream);
 hipError_t launch_result_init(DevResult* res, uint64_t n, hipStream_t stream);
@@ -588,7 +624,9 @@ void* context_host_pipe(tgpu_context* ctx);  // created on first use, owned by c
 bool schema_has_lists(const tgpu_schema* schema);
 
 // ---- stream indexer (k_index.hip) launchers
-uint64_t index_chunk_bytes(uint64_t span, bool tiles);
+// mean: the stream's mean record length when known (0: not), program-less
+// streams only
+uint64_t index_chunk_bytes(uint64_t span, bool tiles, uint64_t mean = 0);
 uint64_t index_tile_bytes();
 uint64_t index_tile_lanes();
 // Returns (in *fused) whether the records were decoded during the index
@@ -599,7 +637,8 @@ uint64_t index_tile_lanes();
 // kernels no tile needs; h_sync[3] then holds the record total (else it is
 // left alone).
 hipError_t launch_index_stream(const IndexArgs& a, hipStream_t stream, const JitKernels* jit,
-                               bool* fused, uint64_t* h_sync = nullptr);
+                               bool* fused, uint64_t* h_sync = nullptr,
+                               const XTabAlloc* xalloc = nullptr);
 // After a fused index + decode over a stream range: re-diagnoses a record
 // the index accepted but the decode could not store (list arena overflow).
 hipError_t launch_stream_decode_finish(const DecodeArgs& a, int protocol, hipStream_t stream);

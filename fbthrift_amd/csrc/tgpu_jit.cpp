@@ -42,7 +42,7 @@ namespace tgpu {
 // first need, so a decode-only caller never waits for the encoder.
 struct JitKernels {
   hipModule_t mod = nullptr;
-  hipFunction_t f[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+  hipFunction_t f[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   bool ok = false;
   std::string log;
 };
@@ -72,15 +72,16 @@ std::string cache_key(const VProgram& P, int device, int group) {
   return k;
 }
 
-const char* const kEntry[6][5] = {
-    {"tgpu_jit_decode", "tgpu_jit_decode_tail", "tgpu_jit_decode_rr", nullptr, nullptr},
-    {"tgpu_jit_size", "tgpu_jit_write", nullptr, nullptr, nullptr},
+const char* const kEntry[6][6] = {
+    {"tgpu_jit_decode", "tgpu_jit_decode_tail", "tgpu_jit_decode_rr", nullptr, nullptr, nullptr},
+    {"tgpu_jit_size", "tgpu_jit_write", nullptr, nullptr, nullptr, nullptr},
     {"tgpu_jit_index_spec", "tgpu_jit_index_emit", "tgpu_jit_index_decode",
-     "tgpu_jit_index_onepass", "tgpu_jit_index_onepass_decode"},
-    {"tgpu_jit_ndecode", "tgpu_jit_ndecode_hbm", "tgpu_jit_nsize", "tgpu_jit_nwrite", nullptr},
-    {"tgpu_jit_nindex_spec", "tgpu_jit_nindex_emit", nullptr, nullptr, nullptr},
+     "tgpu_jit_index_onepass", "tgpu_jit_index_onepass_decode", nullptr},
+    {"tgpu_jit_ndecode", "tgpu_jit_ndecode_hbm", "tgpu_jit_nsize", "tgpu_jit_nwrite", nullptr,
+     nullptr},
+    {"tgpu_jit_nindex_spec", "tgpu_jit_nindex_emit", nullptr, nullptr, nullptr, nullptr},
     {"tgpu_jit_xc_size", "tgpu_jit_xc_write", "tgpu_jit_xc_size_rr", "tgpu_jit_xc_write_rr",
-     nullptr}};
+     "tgpu_jit_xc_one", "tgpu_jit_xc_one_rr"}};
 
 // The record function of a nested program (decode when !enc, the writer
 // when enc): ops [k, stop) of the object at `b` (a variable name). Each
@@ -328,8 +329,9 @@ void gen_prog(std::ostringstream& o, const VProgram& P, const char* arr, const c
 }
 
 // The transcoder's pair (JIT_XCODE): the source program's decode and the
-// target program's writer in the two tile passes of tgpu_xcode.h, with
-// records in registers where decode_regrec allows (entries 2, 3).
+// target program's writer in the tile passes of tgpu_xcode.h — size, write
+// and the single pass — with records in registers where decode_regrec
+// allows (entries 2, 3, 5).
 std::string gen_source_xcode(const VProgram& Ps, const VProgram& Pd) {
   std::ostringstream o;
   o << "// generated by tgpu_jit.cpp for one schema's transcoding pair\n";
@@ -361,6 +363,15 @@ std::string gen_source_xcode(const VProgram& Ps, const VProgram& Pd) {
          "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
          "  __shared__ prog::EncodeShared sm;\n"
          "  prog::xc_write_tile<JP, JQ, "
+      << rs
+      << ">(x, JP{}, JQ{}, kS, cap, ocap, smem, sm);\n"
+         "}\n"
+         "extern \"C\" __global__ __launch_bounds__(256) void tgpu_jit_xc_one"
+      << sfx
+      << "(XcodeArgs x, uint32_t cap, uint32_t ocap) {\n"
+         "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+         "  __shared__ prog::EncodeShared sm;\n"
+         "  prog::xc_one_tile<JP, JQ, "
       << rs
       << ">(x, JP{}, JQ{}, kS, cap, ocap, smem, sm);\n"
          "}\n";
@@ -476,6 +487,9 @@ std::string gen_source(const VProgram& P, int group) {
     return o.str();
   }
   if (group == JIT_NESTED) {
+    // a recursive schema's unrolled writer defers the records nesting past
+    // its levels to the general writer's deep pass (nested_size_tile)
+    if (defer) o << "#define TGPU_NESTED_DEFER 1\n";
     o << "#include \"tgpu_nested.h\"\n"
          "namespace {\n"
          "using namespace tgpu;\n"
@@ -509,10 +523,6 @@ std::string gen_source(const VProgram& P, int group) {
          "  if (wire_cap) nested_decode_tile<false>(a, NR{}, kS, kCompact, wire_cap, irr, nirr, smem);\n"
          "  else nested_decode_hbm(a, NR{}, kS, kCompact, irr, nirr);\n"
          "}\n";
-    // a recursive schema's unrolled program (VOP_DEFER) reads only: its
-    // records are written by the general writer (nested_jit), so no writer
-    // is generated (it roughly doubled the compile)
-    if (defer) return o.str();
     o << "namespace {\n"
          "template <class O>\n"
          "__device__ __forceinline__ bool nenc(const uint8_t* rec, const uint8_t* sbase, "
@@ -690,13 +700,13 @@ bool compile_from(const std::string& src, int device, int group, JitKernels& J) 
   (void)hipGetDevice(&prev);
   if (prev != device) (void)hipSetDevice(device);
   bool ok = hipModuleLoadData(&J.mod, code.data()) == hipSuccess;
-  for (int k = 0; k < 5 && ok; ++k) {
+  for (int k = 0; k < 6 && ok; ++k) {
     if (!kEntry[group][k]) continue;
     ok = hipModuleGetFunction(&J.f[k], J.mod, kEntry[group][k]) == hipSuccess;
     // (tolerant programs / small records; a deferring nested program's writer)
     if (!ok && ((group == JIT_DECODE && (k == 1 || k == 2)) ||
                 (group == JIT_NESTED && (k == 2 || k == 3)) ||
-                (group == JIT_XCODE && (k == 2 || k == 3)))) {
+                (group == JIT_XCODE && (k == 2 || k == 3 || k == 5)))) {
       (void)hipGetLastError();
       J.f[k] = nullptr;
       ok = true;
@@ -762,7 +772,7 @@ hipError_t jit_launch_xcode(const JitKernels* J, int which, const XcodeArgs& x, 
   XcodeArgs a = x;
   void* p2[] = {&a, &cap};
   void* p3[] = {&a, &cap, &ocap};
-  return launch(J->f[which], grid, lds, s, (which & 1) ? p3 : p2);
+  return launch(J->f[which], grid, lds, s, (which & 1) || which >= 4 ? p3 : p2);
 }
 
 int jit_compile_check_xcode(const VProgram& Ps, const VProgram& Pd, const char* arch, char* log,
@@ -787,7 +797,7 @@ bool decode_regrec(uint32_t rec_size) {
   return rec_size && rec_size <= 128 && rec_size % 8 == 0;
 }
 
-bool jit_has(const JitKernels* J, int which) { return J && which >= 0 && which < 5 && J->f[which]; }
+bool jit_has(const JitKernels* J, int which) { return J && which >= 0 && which < 6 && J->f[which]; }
 
 hipError_t jit_launch_decode(const JitKernels* J, const DecodeArgs& a, uint64_t grid,
                              uint32_t cap, uint32_t lds, uint64_t* irr, unsigned long long* nirr,

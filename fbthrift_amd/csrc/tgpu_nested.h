@@ -326,7 +326,7 @@ __device__ __forceinline__ bool nlist(const VOp op, const bool compact, const Sr
     } else {
       const uint32_t wb = op.elem_kind == VEL_BOOL ? 1 : es;
       if (p + wb > end) return false;
-      v = bswap_n(src.win8(p), wb);
+      v = fixed_n(src.win8(p), wb, op.elem_kind == VEL_FIXED && op.bits == kFixedLE);
       if (op.elem_kind == VEL_BOOL) {
         if (compact) v = v == 1;
         else if (v > 1) return false;
@@ -633,16 +633,17 @@ __device__ __forceinline__ bool put_map_header(O& o, const VOp op, const bool co
 
 // A fixed-width scalar of w bytes at p as the writer emits it
 // (write_scalar): big-endian, a bool validated (0/1; Compact 1 / 2).
+// (le: little-endian on the wire, kFixedLE — CompactV1 doubles)
 template <class O>
 __device__ __forceinline__ bool put_fixed(O& o, const bool compact, const uint8_t* p, uint32_t w,
-                                          bool is_bool) {
+                                          bool is_bool, bool le = false) {
   const uint64_t raw = load_member(p, w);
   if (is_bool) {
     if (raw > 1) return false;  // validate_bool: INVALID_BOOL_WRITE
     o.put(compact ? (raw ? 1 : 2) : raw, 1);
     return true;
   }
-  o.put(__builtin_bswap64(raw) >> (64 - 8 * w), w);
+  o.put(le ? raw : __builtin_bswap64(raw) >> (64 - 8 * w), w);
   return true;
 }
 
@@ -661,7 +662,7 @@ __device__ __forceinline__ bool enc_op(const VOp op, const bool compact, const u
       return true;
     }
     case VOP_FIXED:
-      return put_fixed(o, compact, base + op.member, op.width, op.is_bool);
+      return put_fixed(o, compact, base + op.member, op.width, op.is_bool, op.bits == kFixedLE);
     case VOP_VARINT:
       nput_varint(o, zz_member(load_member(base + op.member, op.width), op.width, op.bits));
       return true;
@@ -722,7 +723,8 @@ __device__ __forceinline__ bool enc_op(const VOp op, const bool compact, const u
           o.bytes(sbase + st.offset, st.length);
         } else if (op.elem_kind == VEL_VARINT) {
           nput_varint(o, zz_member(load_member(p, es), es, op.bits));
-        } else if (!put_fixed(o, compact, p, es, op.elem_kind == VEL_BOOL)) {
+        } else if (!put_fixed(o, compact, p, es, op.elem_kind == VEL_BOOL,
+                              op.elem_kind == VEL_FIXED && op.bits == kFixedLE)) {
           return false;
         }
       }
@@ -773,8 +775,20 @@ __device__ __forceinline__ void nested_size_tile(const EncodeArgs& a, const E& e
   unsigned long long sz = 0;
   if (i < a.n) {
     Count o;
-    if (enc(a.recs + i * a.rec_size, a.sbase, a.lbase, o)) sz = o.n;
-    else atomicMin(&a.res->first_fail, (unsigned long long)i);
+    if (enc(a.recs + i * a.rec_size, a.sbase, a.lbase, o)) {
+      sz = o.n;
+    } else {
+#ifdef TGPU_NESTED_DEFER
+      // a recursive schema's record nesting past the unrolled levels (or a
+      // value the writer rejects): the general writer's deep pass sizes and
+      // writes it, or reports it (deep_size_kernel / deep_write_kernel); the
+      // write pass leaves its bytes to that pass
+      a.deep.list[atomicAdd(a.deep.count, 1ull)] = i;
+      atomicAdd(&a.res->n_irregular, 1ull);
+#else
+      atomicMin(&a.res->first_fail, (unsigned long long)i);
+#endif
+    }
     a.offs[i] = sz;
   }
   unsigned long long total;

@@ -439,6 +439,47 @@ struct OrSink {
   }
   __device__ __forceinline__ void finish() {}
 };
+//   AccSink  — the zero-filled LDS output tile through an 8-byte accumulator:
+//              every whole aligned 8-byte word of the record is stored plainly
+//              (ds_write_b64), only the record's first and last words — shared
+//              with its neighbours — are OR-ed in (ds_or_b64); one branch per
+//              put (the word boundary). (A/B: TGPU_WRITE_ACC.)
+struct AccSink {
+  uint32_t* w32;  // the tile (LDS: indexed from it, so the accesses stay ds_*)
+  uint32_t d;     // dword index of the current aligned 8-byte word
+  uint64_t acc;   // its pending bytes
+  uint32_t nb;    // bytes in acc (incl. the head of the first word not ours)
+  uint32_t lo;    // first byte of the current word this record owns
+  __device__ __forceinline__ AccSink(uint32_t* tile, uint32_t pos)
+      : w32(tile), d((pos >> 3) << 1), acc(0), nb(pos & 7), lo(pos & 7) {}
+  __device__ __forceinline__ void emit(uint64_t x) {
+    if (lo == 0) {
+      *(uint64_t*)(w32 + d) = x;
+    } else {
+      atomicOr((unsigned long long*)(w32 + d), (unsigned long long)(x & (~0ull << (8 * lo))));
+      lo = 0;
+    }
+    d += 2;
+  }
+  __device__ __forceinline__ void put64(uint64_t v, uint32_t n) {
+    if (n < 8) v &= (1ull << (8 * n)) - 1;
+    acc |= v << (8 * nb);
+    const uint32_t t = nb + n;
+    if (t >= 8) {
+      emit(acc);
+      acc = nb ? v >> (8 * (8 - nb)) : 0;
+      nb = t - 8;
+    } else {
+      nb = t;
+    }
+  }
+  __device__ __forceinline__ void put(uint32_t v, uint32_t n) { put64(v, n); }
+  __device__ __forceinline__ void finish() {
+    if (nb <= lo) return;
+    const uint64_t m = (nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1)) & (~0ull << (8 * lo));
+    atomicOr((unsigned long long*)(w32 + d), (unsigned long long)(acc & m));
+  }
+};
 struct ByteSink {
   uint8_t* base;
   uint32_t q;
@@ -488,9 +529,9 @@ struct StrPrefetch {
 };
 __device__ __forceinline__ void str_prefetch(StrPrefetch& f, const uint8_t* __restrict__ src,
                                              uint32_t len) {
-  const uintptr_t a = (uintptr_t)src;
-  const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
-  const uint32_t need = ((uint32_t)(a & 3) + len + 3) >> 2;
+  const uint32_t sh = (uint32_t)((uintptr_t)src & 3);
+  const uint32_t* w = (const uint32_t*)(src - sh);
+  const uint32_t need = (sh + len + 3) >> 2;
 #pragma unroll
   for (uint32_t i = 0; i < 8; ++i) f.v[i] = i < need ? w[i] : 0u;
 }
@@ -499,9 +540,10 @@ template <class Sink>
 __device__ __forceinline__ void put_bytes(Sink& s, const uint8_t* __restrict__ src, uint32_t len,
                                           const StrPrefetch* pf = nullptr) {
   if (!len) return;
-  const uintptr_t a = (uintptr_t)src;
-  const uint32_t* w = (const uint32_t*)(a & ~(uintptr_t)3);
-  uint32_t sh = (uint32_t)(a & 3);
+  // (the aligned base by pointer arithmetic on src, not an integer cast: the
+  // loads keep src's address space — global_load, not flat_load)
+  uint32_t sh = (uint32_t)((uintptr_t)src & 3);
+  const uint32_t* w = (const uint32_t*)(src - sh);
   uint32_t left = len;
   bool first = true;
   while (left) {
@@ -582,7 +624,8 @@ __device__ __forceinline__ void program_emit(const PP& P, const R& rec,
         put8(s, op.hdr | (rec.u8(op.member) ? 1u : 2u), op.hdr_len);
         break;
       case VOP_FIXED:
-        put_be(s, rec.member(op.member, op.width), op.width);
+        if (op.bits == kFixedLE) put8(s, rec.member(op.member, op.width), op.width);
+        else put_be(s, rec.member(op.member, op.width), op.width);
         break;
       case VOP_VARINT:
         put_varint(s, zz_member(rec.member(op.member, op.width), op.width, op.bits));
@@ -630,7 +673,10 @@ __device__ __forceinline__ void program_emit(const PP& P, const R& rec,
         } else if (op.elem_kind == VEL_BOOL) {
           for_elems(e, len, 1, [&](uint64_t x) { s.put(compact ? (x ? 1u : 2u) : (uint32_t)x, 1); });
         } else {
-          for_elems(e, len, op.width, [&](uint64_t x) { put_be(s, x, op.width); });
+          if (op.bits == kFixedLE)
+            for_elems(e, len, op.width, [&](uint64_t x) { put8(s, x, op.width); });
+          else
+            for_elems(e, len, op.width, [&](uint64_t x) { put_be(s, x, op.width); });
         }
         break;
       }
@@ -711,6 +757,7 @@ struct EncodeShared {
   unsigned long long part[4];
   unsigned int lds_end;
   unsigned long long elo, ehi;  // the tile's list elements in list_base
+  unsigned long long base;      // single-pass transcoder: the tile's output start
 };
 
 // Encode, compiled programs: the tile's list elements are staged in LDS with
@@ -867,9 +914,14 @@ __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uin
       if (!ok) atomicMin(&a.res->first_fail, (unsigned long long)(r0 + r));
     }
     if (fits && rel + sz <= sm.lds_end) {
-      OrSink w((uint32_t*)otile, osh + (uint32_t)rel);
+#ifdef TGPU_WRITE_ACC
+      using Sink = AccSink;
+#else
+      using Sink = OrSink;
+#endif
+      Sink w((uint32_t*)otile, osh + (uint32_t)rel);
       if constexpr (kReg)
-        program_emit<PP, OrSink, RegRec<kReg ? SR : 8>, kAhead>(P, R, a.sbase, lbase, w, &ah);
+        program_emit<PP, Sink, RegRec<kReg ? SR : 8>, kAhead>(P, R, a.sbase, lbase, w, &ah);
       else
         program_emit(P, PtrRec{rec}, a.sbase, lbase, w);
     } else if (tile_base + rel + sz <= a.cap) {

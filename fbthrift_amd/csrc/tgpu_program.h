@@ -152,6 +152,12 @@ __device__ __forceinline__ uint64_t bswap_n(uint64_t x, uint32_t width) {
   const uint64_t b = __builtin_bswap64(x);
   return width == 8 ? b : (b >> (64 - 8 * width));
 }
+// A FIXED value of `width` bytes: big-endian, or little-endian when the op
+// says so (kFixedLE: CompactV1 doubles)
+__device__ __forceinline__ uint64_t fixed_n(uint64_t x, uint32_t width, bool le) {
+  if (!le) return bswap_n(x, width);
+  return width == 8 ? x : (x & ((1ull << (8 * width)) - 1));
+}
 
 // LEB128 at p (VarintUtils-inl.h:94-134): up to 8 bytes from one window,
 // 9-10 byte i64 varints byte-wise. Returns false (irregular) on anything the
@@ -399,7 +405,7 @@ __device__ __forceinline__ bool run_op(const VOp op, const bool compact, const S
     }
     case VOP_FIXED: {
       if (p + op.width > end) return false;
-      uint64_t v = bswap_n(W.at(src, p, op.width), op.width);
+      uint64_t v = fixed_n(W.at(src, p, op.width), op.width, op.bits == kFixedLE);
       // a bool: Binary readBool throws on a byte >= 2 (general path); a
       // Compact container bool is byte == 1 (nested programs' map keys / values)
       if (op.is_bool && !compact && v > 1) return false;
@@ -478,7 +484,7 @@ __device__ __forceinline__ bool run_op(const VOp op, const bool compact, const S
           } else {
             const uint32_t wb = op.elem_kind == VEL_BOOL ? 1 : es;
             if (p + wb > end) return false;
-            v = bswap_n(src.win8(p), wb);
+            v = fixed_n(src.win8(p), wb, op.elem_kind == VEL_FIXED && op.bits == kFixedLE);
             if (op.elem_kind == VEL_BOOL) {
               if (compact) v = v == 1;
               else if (v > 1) return false;

@@ -140,16 +140,65 @@ __device__ __forceinline__ void xc_size_tile(const XcodeArgs& x, const PS& Ps, c
   if (threadIdx.x == 0) x.e.block_sums[blockIdx.x] = total;
 }
 
-// The write pass. Records the size pass listed keep a hole of the size the
-// general writer measured (x.e.offs[r], k_transcode.hip) and their output
-// start in x.e.offs[r]; the general writer fills the hole afterwards.
-template <class PS, class PD, uint32_t kRS>
-__device__ __forceinline__ void xc_write_tile(const XcodeArgs& x, const PS& Ps, const PD& Pd,
-                                              uint32_t S, uint32_t wire_cap, uint32_t ocap,
-                                              uint8_t* smem, EncodeShared& sm) {
+// Single pass (round 5): tile j publishes its output bytes (AGG) as soon as
+// its records are sized, then wave 0 looks back over the predecessors' words
+// — 64 per round trip, summing AGG totals down to the first INCL (a tile
+// whose inclusive prefix is known) — and publishes its own INCL. The status
+// words are single 64-bit relaxed agent-scope atomics (op_ld / op_st: no
+// fences, the single-pass index's lesson, tgpu_prog_kernels.h); workgroups
+// are dispatched in index order, so every predecessor is resident or done
+// and each wait is bounded (kOpSpinCap) all the same: a tile past the bound
+// publishes FAIL, which every later tile inherits.
+//   xstat[j]: 0 not yet | 01 AGG total | 10 INCL prefix | 11 FAIL (bits 63:62)
+constexpr uint64_t kXcAgg = 1ull << 62, kXcIncl = 2ull << 62, kXcFail = 3ull << 62;
+constexpr uint64_t kXcVal = (1ull << 62) - 1;
+
+// Wave 0 (all 64 lanes): tile j's exclusive output prefix; false when a
+// predecessor failed or a wait passed its bound.
+__device__ __forceinline__ bool xc_look_back(unsigned long long* stat, uint64_t j,
+                                             uint64_t& prefix) {
+  const uint32_t l = threadIdx.x;
+  uint64_t sum = 0;
+  for (int64_t top = (int64_t)j - 1; top >= 0; top -= 64) {
+    const int64_t k = top - (int64_t)l;
+    uint64_t w = k >= 0 ? op_ld(stat + k) : kXcIncl;  // (below tile 0: prefix 0)
+    for (uint32_t spin = 0; __any(w == 0); ++spin) {
+      if (spin >= kOpSpinCap) return false;
+      __builtin_amdgcn_s_sleep(1);
+      if (w == 0) w = op_ld(stat + k);
+    }
+    const uint64_t fin = __ballot(w >= kXcIncl);  // INCL or FAIL
+    const uint32_t stop = fin ? (uint32_t)__builtin_ctzll(fin) : 64u;
+    if (stop < 64 && __shfl(w, (int)stop, 64) == kXcFail) return false;
+    uint64_t v = l <= stop ? (w & kXcVal) : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    sum += v;
+    if (fin) break;
+  }
+  prefix = sum;
+  return true;
+}
+
+// The emit pass, two forms.
+// kOne = false, the two-pass write pass: records the size pass listed keep a
+//   hole of the size the general writer measured (x.e.offs[r],
+//   k_transcode.hip) and their output start in x.e.offs[r]; the general
+//   writer fills the hole afterwards. Behind a single pass (x.gate set) it
+//   runs only when that pass left work (a listed record or a failed wait).
+// kOne = true, the single pass: decode, size, look back, emit; a record the
+//   program cannot take is listed and opens the gate (the two-pass kernels
+//   then redo the call from the tile sums left in e.block_sums).
+template <class PS, class PD, uint32_t kRS, bool kOne>
+__device__ __forceinline__ void xc_emit_tile(const XcodeArgs& x, const PS& Ps, const PD& Pd,
+                                             uint32_t S, uint32_t wire_cap, uint32_t ocap,
+                                             uint8_t* smem, EncodeShared& sm) {
   const DecodeArgs& a = x.d;
   const EncodeArgs& e = x.e;
   if ((uint64_t)blockIdx.x * kPT >= a.n) return;
+  if constexpr (!kOne) {
+    if (x.gate && *x.gate == 0) return;
+  }
   uint8_t* wire = smem;
   uint8_t* rtile = smem + decode_wire_region(wire_cap);
   uint8_t* otile = rtile + xc_rec_region(S, kRS);
@@ -168,13 +217,40 @@ __device__ __forceinline__ void xc_write_tile(const XcodeArgs& x, const PS& Ps, 
     if (ok) {
       bool v = true;
       sz = program_size(Pd, PtrRec{rec}, lb, v);
+      if (kOne && !v) atomicMin(&e.res->first_fail, (unsigned long long)(t.r0 + r));
+    } else if constexpr (kOne) {
+      const unsigned long long k = atomicAdd(x.nirr, 1ull);
+      x.irr[k] = t.r0 + r;
+      op_st(x.xstat + ((a.n + kPT - 1) / kPT), 1);  // the gate
     } else {
       sz = e.offs[t.r0 + r];  // the general writer's size (0: not written)
     }
   }
   unsigned long long tile_total;
   const unsigned long long rel = block_exscan256(sz, sm.part, &tile_total);
-  const unsigned long long tile_base = e.block_sums[blockIdx.x];
+  unsigned long long tile_base;
+  if constexpr (kOne) {
+    const uint64_t j = blockIdx.x;
+    if (threadIdx.x == 0) {
+      e.block_sums[j] = tile_total;  // (the two-pass kernels' input if the gate opens)
+      op_st(x.xstat + j, (j == 0 ? kXcIncl : kXcAgg) | tile_total);
+      if (j == 0) sm.base = 0;
+    }
+    if (j > 0 && threadIdx.x < 64) {
+      uint64_t p = 0;
+      const bool got = xc_look_back(x.xstat, j, p);
+      if (threadIdx.x == 0) {
+        op_st(x.xstat + j, got ? kXcIncl | (p + tile_total) : kXcFail);
+        if (!got) op_st(x.xstat + ((a.n + kPT - 1) / kPT), 1);
+        sm.base = got ? p : kNo;
+      }
+    }
+    __syncthreads();
+    tile_base = sm.base;
+    if (tile_base == kNo) return;  // (the gate is open: the two passes redo the call)
+  } else {
+    tile_base = e.block_sums[blockIdx.x];
+  }
   uint8_t* gtile = e.out + tile_base;
   const uint32_t osh = (uint32_t)((uintptr_t)gtile & 15);
   {
@@ -185,7 +261,7 @@ __device__ __forceinline__ void xc_write_tile(const XcodeArgs& x, const PS& Ps, 
   if (r == 0) sm.lds_end = (unsigned int)min(tile_total, (unsigned long long)ocap);
   __syncthreads();
   bool fits = false;
-  if (r < t.nrec) {
+  if (r < t.nrec && (ok || !kOne)) {
     const unsigned long long start = tile_base + rel;
     const bool over = start + sz > e.cap;
     // (every start when the caller asked for offsets; else the listed
@@ -223,6 +299,20 @@ __device__ __forceinline__ void xc_write_tile(const XcodeArgs& x, const PS& Ps, 
       for (uint32_t b = (lo < osh ? osh : lo); b < (hi < end ? hi : end); ++b) gb[b] = otile[b];
     }
   }
+}
+
+template <class PS, class PD, uint32_t kRS>
+__device__ __forceinline__ void xc_write_tile(const XcodeArgs& x, const PS& Ps, const PD& Pd,
+                                              uint32_t S, uint32_t wire_cap, uint32_t ocap,
+                                              uint8_t* smem, EncodeShared& sm) {
+  xc_emit_tile<PS, PD, kRS, false>(x, Ps, Pd, S, wire_cap, ocap, smem, sm);
+}
+
+template <class PS, class PD, uint32_t kRS>
+__device__ __forceinline__ void xc_one_tile(const XcodeArgs& x, const PS& Ps, const PD& Pd,
+                                            uint32_t S, uint32_t wire_cap, uint32_t ocap,
+                                            uint8_t* smem, EncodeShared& sm) {
+  xc_emit_tile<PS, PD, kRS, true>(x, Ps, Pd, S, wire_cap, ocap, smem, sm);
 }
 
 }  // namespace prog

@@ -396,7 +396,10 @@ int tgpu_context_wait(tgpu_context* ctx, void* stream, tgpu_status* st,
  * counter but the first is 0 (a diagnostic: speed, not correctness, depends
  * on it). out[TGPU_ISTAT_GENERAL]: records of the context's last decode call
  * (any kind) that left the compiled / fixed-layout fast path for the general
- * reader (0 on a canonical stream). Returns TGPU_ERR_INVALID_ARGUMENT when
+ * reader (0 on a canonical stream); after an encode, the records a compiled
+ * nested writer left to the general writer (a recursive schema's records
+ * nesting past its unrolled levels); after a transcode, the records left to
+ * the general reader / writer. Returns TGPU_ERR_INVALID_ARGUMENT when
  * the context has run no index (out[TGPU_ISTAT_GENERAL] is still filled).
  */
 enum {

@@ -49,11 +49,22 @@ def test_oracle_rejects_unknown_protocol():
 @pytest.mark.gpu
 def test_v1_program_selection(gpu):
     """A V1 schema without doubles runs Compact's compiled program; with
-    doubles there is none (general kernels) — tgpu_schema_compile says which."""
+    doubles its own (Compact's ops, the doubles little-endian: kFixedLE) —
+    tgpu_schema_compile compiles both."""
     from fbthrift_amd.serializer import GpuSchema
 
     assert GpuSchema(Schema.from_table(datagen.SCHEMAS["mixed"])).compile(V1)
-    assert not GpuSchema(Schema.from_table(datagen.SCHEMAS["nested"])).compile(V1)
+    assert GpuSchema(Schema.from_table(datagen.SCHEMAS["nested"])).compile(V1)
+
+
+def test_v1_program_compiles_on_cpu():
+    """The CompactV1 program of a schema with doubles (flat and nested) is
+    generated and compiled for gfx950 without a GPU."""
+    from fbthrift_amd.serializer import compile_check
+
+    for name in ("nested", "scalars"):
+        rc, log = compile_check(Schema.from_table(datagen.SCHEMAS[name]), V1)
+        assert rc == 0, log[-2000:]
 
 
 @pytest.mark.gpu

@@ -277,3 +277,53 @@ def test_index_variants(gpu, sname, proto, variant, monkeypatch):
     assert st3.as_tuple() == ost.as_tuple() and (nd, cons) == (ond, ocons)
     k = (ond + 1) * schema.size[0]
     assert np.array_equal(rec.cpu().numpy()[:k], orec[:k])
+
+
+@pytest.fixture
+def programless(monkeypatch):
+    """A stream without any record program (TGPU_NESTED=0 and a schema with
+    optional fields: no flat program), the root first-byte filter off, and the
+    exhaustive resolution forced (TGPU_INDEX_EXHAUSTIVE=1: every chunk
+    position read, the true path followed through the tables) — so the
+    general speculation and its repair decide every record start."""
+    monkeypatch.setenv("TGPU_NESTED", "0")
+    monkeypatch.setenv("TGPU_INDEX_HMASK", "0")
+    monkeypatch.setenv("TGPU_INDEX_EXHAUSTIVE", "1")
+
+
+@pytest.mark.parametrize("proto", [2, 0])
+def test_exhaustive_resolution_matches_oracle(gpu, programless, proto):
+    n = 30_000
+    schema, wire, woffs = _stream("sparse", proto, n, seed=6)
+    gs = _gs(schema)
+    w = _t(wire, gpu)
+    offs, got, first, last, st = _ser(proto).index_stream(gs, w)
+    assert (st.code, got, first, last) == (0, n, 0, len(wire)), st.as_tuple()
+    assert np.array_equal(offs.cpu().numpy().astype(np.uint64), woffs)
+    rec, arena, st2, nd, cons = _ser(proto).deserialize_status(gs, w[: len(wire)], n)
+    ost, orec, oarena, ond, ocons = oracle.decode(schema, proto, wire, n)
+    assert st2.as_tuple() == ost.as_tuple() and (nd, cons) == (ond, ocons) == (n, len(wire))
+    assert np.array_equal(rec.cpu().numpy(), orec)
+
+
+@pytest.mark.parametrize("extra", [0, 7])
+def test_exhaustive_resolution_errors(gpu, programless, extra):
+    """A malformed record deep in the stream (and records asked for past its
+    end): status, records before the failure and consumed bytes as the
+    oracle's sequential reader."""
+    proto = 2
+    n = 30_000
+    schema, wire, woffs = _stream("sparse", proto, n, seed=8)
+    w = bytearray(wire)
+    bad = 21_017
+    if not extra:
+        w[int(woffs[bad])] = 0x1E  # ctype 14 header: "don't know what type"
+    wire = bytes(w)
+    gs = _gs(schema)
+    t = _t(wire, gpu)
+    rec, arena, gst, nd, cons = _ser(proto).deserialize_status(gs, t, n + extra)
+    ost, orec, _, ond, ocons = oracle.decode(schema, proto, wire, n + extra)
+    assert ost.code != 0
+    assert gst.as_tuple() == ost.as_tuple() and (nd, cons) == (ond, ocons)
+    k = ond * schema.record_size
+    assert np.array_equal(rec.cpu().numpy()[:k], orec[:k])

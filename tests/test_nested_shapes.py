@@ -190,7 +190,9 @@ def test_gpu_golden_recursive_through_the_program(gpu, name, unroll, monkeypatch
     levels (Tree, 9 ops a level) / as many as fit 255 ops (Node, 18 ops a
     level: 14). Records and arena byte-equal the oracle's; the unindexed
     stream (nested index walk) the same; the records write back to the
-    golden bytes (through the general writer: such programs have none)."""
+    golden bytes through the unrolled writer (round 5), which defers exactly
+    the same records to the general writer's deep pass — the path counter
+    (index_stats 'general' after the encode) counts them."""
     import torch
 
     from fbthrift_amd import serializer as SZ
@@ -228,6 +230,7 @@ def test_gpu_golden_recursive_through_the_program(gpu, name, unroll, monkeypatch
     torch.cuda.synchronize()
     assert wire.cpu().numpy().tobytes() == c.wire
     assert np.array_equal(woffs.cpu().numpy().astype(np.uint64), c.offsets.astype(np.uint64))
+    assert Ser.context().index_stats()["general"] == deep
 
 
 @pytest.mark.gpu

@@ -80,12 +80,14 @@ def _gpu_transcode(dev, schema, pf, pt, wire, n, out_cap=None, offsets=None):
     return st, done, bytes(out[:size].cpu().numpy()), offs[: done + 1].cpu().numpy()
 
 
-@pytest.fixture(params=["fused", "composed"])
+@pytest.fixture(params=["onepass", "twopass", "composed"])
 def xmode(request, monkeypatch):
-    """Both transcoder forms: wire to wire without records in HBM
-    (tgpu_xcode.h; schemas with a flat program in both protocols) and the
-    composed decode + encode (TGPU_XCODE=0)."""
-    monkeypatch.setenv("TGPU_XCODE", "1" if request.param == "fused" else "0")
+    """Every transcoder form: wire to wire without records in HBM
+    (tgpu_xcode.h; schemas with a flat program in both protocols) as the
+    single pass with look-back (default) and as the two tile passes
+    (TGPU_XCODE_ONEPASS=0), and the composed decode + encode (TGPU_XCODE=0)."""
+    monkeypatch.setenv("TGPU_XCODE", "0" if request.param == "composed" else "1")
+    monkeypatch.setenv("TGPU_XCODE_ONEPASS", "1" if request.param == "onepass" else "0")
     return request.param
 
 
@@ -130,7 +132,8 @@ def test_gpu_transcode_errors_match_oracle(gpu, xmode, name):
 
 def _mixed_stream(n, every, proto):
     """n config-3 records (Compact / Binary, schema `mixed`) whose record i is
-    written with the fields in another order when i % every == 0 (a record
+    written with the fields in another order when i % every == 0 (every = 0:
+    none; a record
     the generated readNoXfer reads through its unexpected-field path, and the
     record program cannot take): the oracle's bytes, record by record."""
     import datagen
@@ -150,26 +153,32 @@ def _mixed_stream(n, every, proto):
     assert st.code == 0
     parts, offs = [], [0]
     for i in range(n):
-        w, o = (wb, ob) if i % every == 0 else (wa, oa)
+        w, o = (wb, ob) if every and i % every == 0 else (wa, oa)
         parts.append(w[int(o[i]):int(o[i + 1])])
         offs.append(offs[-1] + len(parts[-1]))
     return sa, b"".join(parts), np.array(offs, np.uint64)
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("every", [997, 0], ids=["irregular", "canonical"])
+@pytest.mark.parametrize("onepass", ["1", "0"], ids=["onepass", "twopass"])
 @pytest.mark.parametrize("pf,pt", [(2, 0), (0, 2)])
-def test_gpu_transcode_fused_irregular_records(gpu, codec, pf, pt, monkeypatch):
-    """100 003 records, every 997th off the canonical field order: the fused
-    transcoder lists those for the general reader / writer (index_stats
-    'general' counts them) and its output equals the oracle's serialize<To>(
+def test_gpu_transcode_fused_irregular_records(gpu, codec, pf, pt, onepass, every, monkeypatch):
+    """100 003 records (391 tiles: the single pass's look-back runs across
+    windows of 64), every 997th off the canonical field order or none: the
+    fused transcoder lists those for the general reader / writer (index_stats
+    'general' counts them; the single pass then opens the gate of the two
+    tile passes) and its output equals the oracle's serialize<To>(
     deserialize<From>) byte for byte — indexed and unindexed, with and without
-    output offsets, through the compiled and the interpreting program pair."""
+    output offsets; an output of half the size stops at the first record that
+    does not fit (OUTPUT_OVERFLOW) with every record before it written."""
     import torch
 
     from fbthrift_amd import serializer as S
 
     monkeypatch.setenv("TGPU_XCODE", "1")
-    n, every = 100_003, 997
+    monkeypatch.setenv("TGPU_XCODE_ONEPASS", onepass)
+    n = 100_003
     schema, wire, offs = _mixed_stream(n, every, pf)
     st, nd, want, woffs = _oracle_transcode(schema, pf, pt, wire, n)
     assert st.code == 0 and nd == n
@@ -185,4 +194,12 @@ def test_gpu_transcode_fused_irregular_records(gpu, codec, pf, pt, monkeypatch):
             assert bytes(out[:size].cpu().numpy()) == want
             if want_offs:
                 assert np.array_equal(go.cpu().numpy().astype(np.uint64), np.asarray(woffs, np.uint64))
-            assert ser.context().index_stats()["general"] == (n + every - 1) // every
+            assert ser.context().index_stats()["general"] == ((n + every - 1) // every
+                                                               if every else 0)
+    cap = len(want) // 2
+    out = torch.empty(cap, dtype=torch.uint8, device=gpu)
+    out, go, gst, done, size = ser.transcode(gs, w, n, pt, offsets=o, out=out)
+    wo = np.asarray(woffs, np.uint64)
+    fit = int(np.searchsorted(wo[1:], cap, side="right"))  # records whose end is <= cap
+    assert gst.code == 21 and done == fit and size == int(wo[fit]), (gst.as_tuple(), done, fit)
+    assert bytes(out[:size].cpu().numpy()) == want[:size]
