@@ -143,15 +143,17 @@ hipError_t launch_xcode(const XcodeArgs& x, int from, int to, const VProgram* d_
     const double in_tile = (double)x.d.in_len / (double)n * kPT;
     const double want_w = 1.04 * in_tile + 256.0, max_w = 1.12 * in_tile + 512.0;
     const double want_o = std::min(1.04 * (double)x.out_mean * kPT + 256.0, (double)prog::kOutCap);
+    // (no w that holds both: the sizes above)
     for (uint32_t w = 8; w >= 1; --w) {
-      const uint32_t budget = 163840u / w - 256u - rt;  // (the static LDS and slack)
+      const int64_t budget = (int64_t)(163840u / w) - 256 - (int64_t)rt;  // (static LDS, slack)
       const uint32_t rw = prog::decode_wire_region((uint32_t)want_w);
-      if (rw + want_o + 32 > budget) continue;
+      if ((double)rw + want_o + 32.0 > (double)budget) continue;
       // the largest wire cap within the staging rounds the tile needs
       uint32_t c = std::min<uint32_t>((uint32_t)max_w, rw - 32) & ~15u;
       c = std::max(c, std::min<uint32_t>((uint32_t)want_w, rw - 32) & ~15u);
       cap = std::max<uint32_t>(c, 4096);
-      ocap = std::min<uint32_t>(prog::kOutCap, budget - prog::decode_wire_region(cap) - 32) & ~15u;
+      ocap = (uint32_t)std::min<int64_t>(prog::kOutCap,
+                                         budget - prog::decode_wire_region(cap) - 32) & ~15u;
       break;
     }
   }

@@ -2419,9 +2419,14 @@ int transcode_fused(tgpu_context* ctx, const tgpu_schema* schema, int from, int 
   if (!rc) rc = grow(ctx->d_xrec, ctx->xrec_bytes, std::max<uint64_t>(n * rs, 16));
   if (!rc && acap) rc = grow(ctx->d_xarena, ctx->xarena_bytes, acap);
   if (!rc && !out_offsets) rc = grow(ctx->d_xoffs, ctx->xoffs_bytes, (n + 1) * sizeof(uint64_t));
-  // the single pass (default; TGPU_XCODE_ONEPASS=0: the two tile passes)
+  // the single pass or the two tile passes (TGPU_XCODE_ONEPASS=1 / 0 force
+  // one): the single pass saves the size pass's read and parse of the
+  // stream, and adds a look-back round trip per tile (3-5 us of a resident
+  // workgroup) — it wins where a tile holds more bytes (config 4, 22.8 KiB
+  // of input per tile: 3.48 vs 4.24 ms) and loses on lighter tiles (config
+  // 3, 13.6 KiB: 3.99 vs 3.51 ms)
   const char* op = getenv("TGPU_XCODE_ONEPASS");
-  const bool one = !(op && op[0] == '0');
+  const bool one = op && *op ? op[0] != '0' : (n && in_len / n * 256 >= 16384);
   const uint64_t tiles = (n + 255) / 256;
   if (!rc && one) rc = grow(ctx->d_xstat, ctx->xstat_bytes, (tiles + 1) * sizeof(uint64_t));
   if (rc) {

@@ -439,47 +439,11 @@ struct OrSink {
   }
   __device__ __forceinline__ void finish() {}
 };
-//   AccSink  — the zero-filled LDS output tile through an 8-byte accumulator:
-//              every whole aligned 8-byte word of the record is stored plainly
-//              (ds_write_b64), only the record's first and last words — shared
-//              with its neighbours — are OR-ed in (ds_or_b64); one branch per
-//              put (the word boundary). (A/B: TGPU_WRITE_ACC.)
-struct AccSink {
-  uint32_t* w32;  // the tile (LDS: indexed from it, so the accesses stay ds_*)
-  uint32_t d;     // dword index of the current aligned 8-byte word
-  uint64_t acc;   // its pending bytes
-  uint32_t nb;    // bytes in acc (incl. the head of the first word not ours)
-  uint32_t lo;    // first byte of the current word this record owns
-  __device__ __forceinline__ AccSink(uint32_t* tile, uint32_t pos)
-      : w32(tile), d((pos >> 3) << 1), acc(0), nb(pos & 7), lo(pos & 7) {}
-  __device__ __forceinline__ void emit(uint64_t x) {
-    if (lo == 0) {
-      *(uint64_t*)(w32 + d) = x;
-    } else {
-      atomicOr((unsigned long long*)(w32 + d), (unsigned long long)(x & (~0ull << (8 * lo))));
-      lo = 0;
-    }
-    d += 2;
-  }
-  __device__ __forceinline__ void put64(uint64_t v, uint32_t n) {
-    if (n < 8) v &= (1ull << (8 * n)) - 1;
-    acc |= v << (8 * nb);
-    const uint32_t t = nb + n;
-    if (t >= 8) {
-      emit(acc);
-      acc = nb ? v >> (8 * (8 - nb)) : 0;
-      nb = t - 8;
-    } else {
-      nb = t;
-    }
-  }
-  __device__ __forceinline__ void put(uint32_t v, uint32_t n) { put64(v, n); }
-  __device__ __forceinline__ void finish() {
-    if (nb <= lo) return;
-    const uint64_t m = (nb >= 8 ? ~0ull : ((1ull << (8 * nb)) - 1)) & (~0ull << (8 * lo));
-    atomicOr((unsigned long long*)(w32 + d), (unsigned long long)(acc & m));
-  }
-};
+// (Round 5, measured on configs 3 / 4 and dropped: an 8-byte accumulating
+// sink — whole aligned words stored with ds_write_b64, only the record's two
+// edge words OR-ed — 2.61 -> 2.70 ms / neutral; skipping the ORs of dwords a
+// value does not reach, and 64-bit ORs on 8-byte words: neutral, 2.59 ->
+// 2.60 / 2.58 ms. The write pass is not bound by its LDS atomics.)
 struct ByteSink {
   uint8_t* base;
   uint32_t q;
@@ -914,11 +878,7 @@ __device__ __forceinline__ void write_tile(const EncodeArgs& a, const PP& P, uin
       if (!ok) atomicMin(&a.res->first_fail, (unsigned long long)(r0 + r));
     }
     if (fits && rel + sz <= sm.lds_end) {
-#ifdef TGPU_WRITE_ACC
-      using Sink = AccSink;
-#else
       using Sink = OrSink;
-#endif
       Sink w((uint32_t*)otile, osh + (uint32_t)rel);
       if constexpr (kReg)
         program_emit<PP, Sink, RegRec<kReg ? SR : 8>, kAhead>(P, R, a.sbase, lbase, w, &ah);

@@ -5,7 +5,9 @@ to ~1 Mi records, through the unrolled nested program (TGPU_NESTED=1) and
 through the general decoder alone (TGPU_NESTED=0). Prints one JSON line per
 (case, path): ms per call (device time of the whole decode call, buffers
 preallocated), wire GB/s, and how many records the general decoder took;
-then the encode of the decoded records (the general writer). TGPU_DEEP_WIDE=0
+then the encode of the decoded records the same two ways (the unrolled
+writer, deferring deeper records to the general writer, and the general
+writer alone). TGPU_DEEP_WIDE=0
 in the environment: the general kernels' deep pass without its wide tier.
 
   python tools/recursive_bench.py [--reps 10] [--copies 5000]"""
@@ -84,7 +86,9 @@ def main():
                               "wire_GBps": round(wire.numel() / ms / 1e6, 1),
                               "general_records": Ser.context().index_stats()["general"]}),
                   flush=True)
-        # encode (the general writer: a recursive schema's program has none)
+        # encode: the unrolled nested writer (round 5; records nesting past
+        # its levels go to the general writer's deep pass) and the general
+        # writer alone
         out = torch.empty(wire.numel(), dtype=torch.uint8, device=dev)
         woffs = torch.empty(n + 1, dtype=torch.int64, device=dev)
 
@@ -92,12 +96,18 @@ def main():
             got, _ = Ser.serialize(gs, recs, n, wire, arena, out=out, offsets=woffs)
             assert got.numel() == wire.numel()
 
-        ms = timed(enc, args.reps)
-        assert torch.equal(out, wire)
-        print(json.dumps({"case": name, "op": "encode", "path": "general",
-                          "deep_tiers": 1 if os.environ.get("TGPU_DEEP_WIDE") == "0" else 2,
-                          "records": n, "wire_bytes": wire.numel(), "ms": round(ms, 3),
-                          "wire_GBps": round(wire.numel() / ms / 1e6, 1)}), flush=True)
+        for nested in ("1", "0"):
+            os.environ["TGPU_NESTED"] = nested
+            out.zero_()
+            ms = timed(enc, args.reps)
+            assert torch.equal(out, wire)
+            print(json.dumps({"case": name, "op": "encode",
+                              "path": "nested" if nested == "1" else "general",
+                              "deep_tiers": 1 if os.environ.get("TGPU_DEEP_WIDE") == "0" else 2,
+                              "records": n, "wire_bytes": wire.numel(), "ms": round(ms, 3),
+                              "wire_GBps": round(wire.numel() / ms / 1e6, 1),
+                              "general_records": Ser.context().index_stats()["general"]}),
+                  flush=True)
 
 
 if __name__ == "__main__":
