@@ -1148,12 +1148,17 @@ def transcode(wl, dev, reps=5):
     out = torch.empty(8 * wl.wire_bytes + 16, dtype=torch.uint8, device=dev)
     res = {"from": src.protocol, "to": to}
     ref = None
+    # (config 2's fixed-layout stream has no offsets array: record i at i * L;
+    # unindexed, its transcoding stays on the plan decode + encode by design)
+    wl_offs = getattr(wl, "offs", None)
+    if wl_offs is None:
+        wl_offs = torch.arange(wl.n + 1, dtype=torch.int64, device=dev) * (wl.wire_bytes // wl.n)
     old = os.environ.get("TGPU_XCODE")
     try:
         for form in ("fused", "composed"):
             os.environ["TGPU_XCODE"] = "1" if form == "fused" else "0"
             for ix in ("indexed", "unindexed"):
-                offs = wl.offs if ix == "indexed" else None
+                offs = wl_offs if ix == "indexed" else None
                 best = None
                 for _ in range(reps + 1):
                     torch.cuda.synchronize()

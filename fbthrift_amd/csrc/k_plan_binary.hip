@@ -643,7 +643,10 @@ DecVariant dec_variant() {
   return v;
 }
 EncVariant enc_variant() {
-  EncVariant v{512, 1, 1, 512};
+  // (256-thread blocks, 512 records per block: 1.953 ms against 1.982 for
+  // 512 threads, tools/kbench.py six interleaved rounds on one box,
+  // profiles/r05/ab/plan_tile_ab.log)
+  EncVariant v{256, 1, 1, 512};
   if (const char* s = getenv("TGPU_PLAN_ENCODE")) {
     unsigned t = 256, tr = 512;
     int nt = 0, ls = 0;

@@ -1288,6 +1288,9 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
 #endif
 constexpr uint32_t kCandCap = TGPU_CAND_CAP;
 constexpr uint32_t kCandWords = kTile / 64 + 2;  // 64-position words of cmask
+// (thread t counts word t; the last thread the words past 256, whose counts
+// are packed 8 bits each into one 64-bit word: at most 8 of them)
+static_assert(kCandWords <= kTileLanes + 8, "TGPU_KSUB > 64 needs a wider word-count packing");
 struct CandLists {
   uint16_t cand[kCandCap + 2];  // candidate positions in order (+ a sentinel)
   uint16_t len[kCandCap];       // record length walked from each (0: not a record)
@@ -1372,12 +1375,13 @@ __device__ __forceinline__ bool spec_tile_cands(const IndexArgs& a, const PP& P,
     for (uint32_t w = kTileLanes; w < nw; ++w) mx |= (uint64_t)__builtin_popcountll(word(w)) << (8 * (w - kTileLanes));
   const uint32_t c0 = (uint32_t)__builtin_popcountll(m0);
   uint32_t cx = 0;
-  for (uint32_t k = 0; k < kCandWords - kTileLanes; ++k) cx += (uint32_t)((mx >> (8 * k)) & 0xff);
+  for (uint32_t k = 0; kCandWords > kTileLanes && k < kCandWords - kTileLanes; ++k)
+    cx += (uint32_t)((mx >> (8 * k)) & 0xff);
   unsigned long long total;
   const uint32_t pre = (uint32_t)block_exscan256(c0 + cx, sm.part, &total);
   const uint32_t N = (uint32_t)total;
   if (N > kCandCap || N > a.st_cap) return false;  // (uniform)
-  sm.cl.wbase[t] = (uint16_t)pre;
+  if (t < kCandWords) sm.cl.wbase[t] = (uint16_t)pre;
   {
     uint32_t k = pre;
     for (uint64_t m = m0; m; m &= m - 1) sm.cl.cand[k++] = (uint16_t)((t << 6) + __builtin_ctzll(m));
@@ -1393,7 +1397,11 @@ __device__ __forceinline__ bool spec_tile_cands(const IndexArgs& a, const PP& P,
   for (uint32_t i = t; i < N; i += kTileLanes) {
     const uint32_t c = sm.cl.cand[i];
     uint32_t q = c;
+#ifdef TGPU_ABL_NOWALK  // timing ablation only (wrong index): no walks
+    const bool ok = false;
+#else
     const bool ok = tile_walk(P, src, pc, q, avail);
+#endif
     const uint32_t len = q - c;
     sm.cl.len[i] = ok ? (uint16_t)(len < 0xffffu ? len : 0xffffu) : 0;
     if (ok) atomicMin(&sm.first_lane, i);
@@ -1433,6 +1441,9 @@ __device__ __forceinline__ bool spec_tile_cands(const IndexArgs& a, const PP& P,
   uint32_t count = 0, e = 0;
   uint16_t* dst = a.st16 + j * a.st_cap;
   uint32_t i = f;
+#ifdef TGPU_ABL_NOCHAIN  // timing ablation only (wrong index): no chain
+  stuck = true;
+#endif
   while (!stuck && f != kNoPos) {
     // candidates [i, i + 64): lane l's record links to candidate i + l + 1
     const uint32_t x = i + lane;

@@ -32,8 +32,8 @@ def main():
     dev = torch.device("cuda:0")
     n = args.records
     gs = GpuSchema(Schema.from_table(datagen.SCHEMAS["flat8"]))
-    BS.context().reserve(n)
     recs = bench.gen_flat8_device(n, 0, dev)
+    BS.context().reserve(n)
     wire = torch.empty(n * 89, dtype=torch.uint8, device=dev)
     back = torch.empty(n * 72, dtype=torch.uint8, device=dev)
     res = {("dec", v): [] for v in args.dec}
