@@ -83,6 +83,7 @@ EXPORTS = [
     "tgpu_schema_arena_scale", "tgpu_decode_host_ex", "tgpu_encode_host_ex", "tgpu_skim_batch",
     "tgpu_skim_batch_ex",
     "tgpu_index_stats", "tgpu_decode_host_chunks", "tgpu_encode_host_chunks",
+    "tgpu_decode_host_chunks_ex",
 ]
 
 # callbacks of the chunk-pipelined host calls
@@ -190,6 +191,11 @@ def lib():
                                           ctypes.POINTER(Limits), U64, CHUNK_FN, P,
                                           ctypes.POINTER(Status), ctypes.POINTER(U64),
                                           ctypes.POINTER(U64)]
+    L.tgpu_decode_host_chunks_ex.restype = I32
+    L.tgpu_decode_host_chunks_ex.argtypes = [P, P, I32, P, U64, U64, P, P, U64,
+                                             ctypes.POINTER(Limits), U64, ctypes.c_uint32,
+                                             CHUNK_FN, P, ctypes.POINTER(Status),
+                                             ctypes.POINTER(U64), ctypes.POINTER(U64)]
     L.tgpu_encoded_size_host.restype = I32
     L.tgpu_encoded_size_host.argtypes = [P, P, I32, P, U64, P, U64, P, ctypes.POINTER(Status),
                                          ctypes.POINTER(U64)]

@@ -167,6 +167,21 @@ void* context_host_pipe(tgpu_context* c) {
   if (!c->host_pipe) c->host_pipe = host_pipe_create();
   return c->host_pipe;
 }
+uint32_t packable_lists(const tgpu_schema* s, int protocol, uint32_t* member, uint32_t* width,
+                        uint32_t max) {
+  const int q = prog_protocol(s, protocol);
+  if (q < 0 || !s->has_prog[q] || s->nested || s->str_elems || !s->has_lists) return 0;
+  const VProgram& P = s->prog[q];
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < P.n_ops; ++i) {
+    if (P.ops[i].kind != VOP_LIST) continue;
+    if (k == max) return 0;
+    member[k] = P.ops[i].member;
+    width[k] = P.ops[i].width;
+    ++k;
+  }
+  return k;
+}
 }  // namespace tgpu
 
 namespace {

@@ -62,8 +62,9 @@ struct HostPipe {
   uint8_t* d_in[kSlots] = {};
   uint8_t* d_out[kSlots] = {};
   uint64_t in_cap = 0, out_cap = 0;
-  // tgpu_decode_host_chunks: the stream, records, arena, offsets
-  GrowBuf din, drec, dar, doffs;
+  // tgpu_decode_host_chunks: the stream, records, arena, offsets; packed
+  // list elements, the packing's tile sums and scan partials, totals
+  GrowBuf din, drec, dar, doffs, dpk, psum, ppart, ptot;
   // tgpu_encode_host_chunks: two slots of records, strings, lists, wire
   GrowBuf erec[2], estr[2], elst[2], eout[2];
 };
@@ -147,7 +148,8 @@ void host_pipe_destroy(void* vp) {
     if (p->s[k]) (void)hipStreamDestroy(p->s[k]);
   }
   pipe_free_buffers(p);
-  for (GrowBuf* b : {&p->din, &p->drec, &p->dar, &p->doffs}) b->release();
+  for (GrowBuf* b : {&p->din, &p->drec, &p->dar, &p->doffs, &p->dpk, &p->psum, &p->ppart, &p->ptot})
+    b->release();
   for (int k = 0; k < 2; ++k)
     for (GrowBuf* b : {&p->erec[k], &p->estr[k], &p->elst[k], &p->eout[k]}) b->release();
   delete p;
@@ -462,6 +464,90 @@ int tgpu_encode_host_ex(tgpu_context* ctx, const tgpu_schema* schema, int protoc
   return code;
 }
 
+// ---- packed list elements (tgpu_decode_host_chunks_ex, TGPU_HOST_PACK_LISTS)
+// The decoded list arena follows the position rule (an element array at
+// scale x its wire position), so a chunk's arena slice is as large as its
+// wire (x scale) whatever share of it the elements are: config 4 sends 373 MB
+// of slices back for 134 MB of elements. Packing moves a finished chunk's
+// element arrays to the front of its slice (record order, no gaps) in a
+// second buffer laid out like the host arena and points the records' spans
+// there, so only the records and the packed bytes cross PCIe back.
+namespace {
+constexpr uint32_t kPackMax = 8;
+struct PackSpec {
+  uint32_t n;
+  uint32_t member[kPackMax];
+  uint32_t width[kPackMax];
+};
+
+__device__ __forceinline__ uint64_t pack_bytes(const uint8_t* rec, const PackSpec& ps) {
+  uint64_t b = 0;
+  for (uint32_t f = 0; f < ps.n; ++f)
+    b += (uint64_t)((const tgpu_span*)(rec + ps.member[f]))->length * ps.width[f];
+  return b;
+}
+
+// inclusive-scan helper of one 256-thread block: returns the exclusive prefix
+// of v, *total the block's sum
+__device__ __forceinline__ unsigned long long block_scan256(unsigned long long v,
+                                                            unsigned long long* wsum,
+                                                            unsigned long long* total) {
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned long long x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  unsigned long long before = 0, all = 0;
+  for (uint32_t k = 0; k < 4; ++k) {
+    before += k < w ? wsum[k] : 0;
+    all += wsum[k];
+  }
+  *total = all;
+  return before + x - v;
+}
+
+__global__ __launch_bounds__(256) void pack_size_kernel(const uint8_t* __restrict__ recs, uint64_t n,
+                                                        uint32_t S, PackSpec ps,
+                                                        unsigned long long* __restrict__ sums) {
+  __shared__ unsigned long long wsum[4];
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const unsigned long long b = i < n ? pack_bytes(recs + i * S, ps) : 0;
+  unsigned long long total;
+  (void)block_scan256(b, wsum, &total);
+  if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+// sums: the scanned tile sums. Element arrays of record i go to
+// dst[base + its prefix ..) (byte copies: the arrays sit at any byte
+// position under the position rule), its spans are rewritten to there.
+__global__ __launch_bounds__(256) void pack_copy_kernel(uint8_t* __restrict__ recs, uint64_t n,
+                                                        uint32_t S, PackSpec ps,
+                                                        const unsigned long long* __restrict__ sums,
+                                                        const uint8_t* __restrict__ arena,
+                                                        uint8_t* __restrict__ dst, uint64_t base) {
+  __shared__ unsigned long long wsum[4];
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  uint8_t* rec = recs + i * S;
+  const unsigned long long b = i < n ? pack_bytes(rec, ps) : 0;
+  unsigned long long total;
+  uint64_t off = base + sums[blockIdx.x] + block_scan256(b, wsum, &total);
+  if (i >= n) return;
+  for (uint32_t f = 0; f < ps.n; ++f) {
+    tgpu_span* sp = (tgpu_span*)(rec + ps.member[f]);
+    const uint64_t bytes = (uint64_t)sp->length * ps.width[f];
+    if (!bytes) continue;
+    const uint8_t* src = arena + sp->offset;
+    for (uint64_t k = 0; k < bytes; ++k) dst[off + k] = src[k];
+    sp->offset = off;
+    off += bytes;
+  }
+}
+}  // namespace
+
 // ---- any schema, chunk-pipelined (tgpu_decode_host_chunks /
 // tgpu_encode_host_chunks) ---------------------------------------------------
 namespace {
@@ -490,6 +576,17 @@ int tgpu_decode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int pr
                             void* h_arena, uint64_t arena_capacity, const tgpu_limits* limits,
                             uint64_t chunk_bytes, tgpu_chunk_fn on_chunk, void* user,
                             tgpu_status* st, uint64_t* n_decoded, uint64_t* consumed) {
+  return tgpu_decode_host_chunks_ex(ctx, schema, protocol, h_in, in_len, n, h_records, h_arena,
+                                    arena_capacity, limits, chunk_bytes, 0u, on_chunk, user, st,
+                                    n_decoded, consumed);
+}
+
+int tgpu_decode_host_chunks_ex(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                               const void* h_in, uint64_t in_len, uint64_t n, void* h_records,
+                               void* h_arena, uint64_t arena_capacity, const tgpu_limits* limits,
+                               uint64_t chunk_bytes, uint32_t flags, tgpu_chunk_fn on_chunk,
+                               void* user, tgpu_status* st, uint64_t* n_decoded,
+                               uint64_t* consumed) {
   if (n_decoded) *n_decoded = 0;
   if (consumed) *consumed = 0;
   if (!ctx || !schema || (n && (!h_in || !h_records)) || (arena_capacity && !h_arena)) {
@@ -529,6 +626,37 @@ int tgpu_decode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int pr
     return TGPU_ERR_HIP;
   }
   const uint64_t P = (in_len + C - 1) / C;
+  // packed list elements (TGPU_HOST_PACK_LISTS; schemas whose arena holds
+  // scalar list elements only): each chunk's element arrays at the front of
+  // its arena slice, the records' spans pointing there; the chunk's packed
+  // size is read back one chunk later (the next chunk's decode is queued
+  // first), then its records and packed bytes go back
+  PackSpec ps{};
+  if ((flags & TGPU_HOST_PACK_LISTS) && scale && arena_capacity)
+    ps.n = packable_lists(schema, protocol, ps.member, ps.width, kPackMax);
+  const bool pack = ps.n > 0;
+  const uint64_t pnb = (n + 255) / 256 + 1;
+  if (pack && (!p->dpk.reserve(arena_capacity) || !p->psum.reserve(pnb * 8) ||
+               !p->ppart.reserve((scan_tiles_parts(pnb) + 1) * 8) || !p->ptot.reserve(P * 8))) {
+    set_status(st, TGPU_ERR_HIP, 0, 0);
+    return TGPU_ERR_HIP;
+  }
+  std::vector<uint64_t> htot_v;
+  uint64_t* htot = nullptr;
+  if (pack) {
+    if (hipHostMalloc((void**)&htot, P * 8, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      htot_v.resize(P);
+      htot = htot_v.data();
+    }
+  }
+  struct HostFree {
+    uint64_t* p;
+    bool pinned;
+    ~HostFree() {
+      if (p && pinned) (void)hipHostFree(p);
+    }
+  } htot_guard{htot, pack && htot_v.empty()};
   Events evin(P), evdec(P), evout(P);
   const hipStream_t sin = p->s[0], sdec = p->s[1], sout = p->s[2];
   for (uint64_t k = 0; k < P; ++k) {
@@ -552,6 +680,35 @@ int tgpu_decode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int pr
       announced = pending[k].r1;
     }
     pending.erase(pending.begin(), pending.begin() + k);
+  };
+  // a decoded chunk's records and arena bytes (from `abuf`, `abytes` at
+  // scale * B) back to the host on sout, announced once they land
+  auto send_back = [&](uint64_t kk, uint64_t rr, uint64_t nk, uint64_t bb, uint64_t abytes,
+                       const uint8_t* abuf) {
+    if (hipStreamWaitEvent(sout, evdec.ev[kk], 0) != hipSuccess ||
+        hipMemcpyAsync((uint8_t*)h_records + rr * S, drec.p + rr * S, nk * S,
+                       hipMemcpyDeviceToHost, sout) != hipSuccess ||
+        (scale && abytes &&
+         hipMemcpyAsync((uint8_t*)h_arena + scale * bb, abuf + scale * bb, abytes,
+                        hipMemcpyDeviceToHost, sout) != hipSuccess) ||
+        hipEventRecord(evout.ev[kk], sout) != hipSuccess)
+      return false;
+    pending.push_back(Range{rr, rr + nk, evout.ev[kk]});
+    return true;
+  };
+  struct Staged {
+    uint64_t k, r0, nk, B;
+  };
+  std::vector<Staged> staged;  // packed chunks whose size is not read yet
+  auto flush_pending = [&]() {
+    while (!staged.empty()) {
+      const Staged c = staged.front();
+      if (hipEventSynchronize(evdec.ev[c.k]) != hipSuccess ||
+          !send_back(c.k, c.r0, c.nk, c.B, htot[c.k], p->dpk.p))
+        return false;
+      staged.erase(staged.begin());
+    }
+    return true;
   };
   uint64_t B = 0, r0 = 0, k = 0;
   bool clean = true;
@@ -578,24 +735,49 @@ int tgpu_decode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int pr
       break;
     }
     if (nk) {
-      if (hipEventRecord(evdec.ev[k], sdec) != hipSuccess ||
-          hipStreamWaitEvent(sout, evdec.ev[k], 0) != hipSuccess ||
-          hipMemcpyAsync((uint8_t*)h_records + r0 * S, drec.p + r0 * S, nk * S,
-                         hipMemcpyDeviceToHost, sout) != hipSuccess ||
-          (scale && hipMemcpyAsync((uint8_t*)h_arena + scale * B, dar.p + scale * B,
-                                   std::min(arena_capacity, scale * last) - scale * B,
-                                   hipMemcpyDeviceToHost, sout) != hipSuccess) ||
-          hipEventRecord(evout.ev[k], sout) != hipSuccess) {
+      if (pack) {
+        // pack the chunk's element arrays (sdec), its packed size to htot[k]
+        const uint64_t nb = (nk + 255) / 256;
+        auto* sums = (unsigned long long*)p->psum.p;
+        hipLaunchKernelGGL(pack_size_kernel, dim3((uint32_t)nb), dim3(256), 0, sdec,
+                           drec.p + r0 * S, nk, S, ps, sums);
+        hipError_t pe = hipGetLastError();
+        if (pe == hipSuccess)
+          pe = launch_scan_tiles(sums, nb, (unsigned long long*)p->ppart.p,
+                                 (unsigned long long*)p->ptot.p + k, nullptr, sdec);
+        if (pe == hipSuccess) {
+          hipLaunchKernelGGL(pack_copy_kernel, dim3((uint32_t)nb), dim3(256), 0, sdec,
+                             drec.p + r0 * S, nk, S, ps, sums, dar.p, p->dpk.p, scale * B);
+          pe = hipGetLastError();
+        }
+        if (pe == hipSuccess)
+          pe = hipMemcpyAsync(htot + k, (uint64_t*)p->ptot.p + k, 8, hipMemcpyDeviceToHost, sdec);
+        if (pe != hipSuccess || hipEventRecord(evdec.ev[k], sdec) != hipSuccess) {
+          clean = false;
+          break;
+        }
+        // the previous chunk's packed size is known once its kernels ran
+        if (!flush_pending()) {
+          clean = false;
+          break;
+        }
+        staged.push_back(Staged{k, r0, nk, B});
+      } else if (hipEventRecord(evdec.ev[k], sdec) != hipSuccess ||
+                 !send_back(k, r0, nk, B, std::min(arena_capacity, scale * last) - scale * B,
+                            dar.p)) {
         clean = false;
         break;
       }
-      pending.push_back(Range{r0, r0 + nk, evout.ev[k]});
     }
     announce(false);
     B = last;
     r0 += nk;
     ++k;
   }
+  if (clean && !flush_pending()) clean = false;
+  // the wire position of the first record not sent back (a chunk still
+  // staged for packing, or the loop's end)
+  const uint64_t Bsent = staged.empty() ? B : staged.front().B;
   (void)hipStreamSynchronize(sin);
   (void)hipStreamSynchronize(sdec);
   announce(true);
@@ -616,9 +798,9 @@ int tgpu_decode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int pr
   if (code != TGPU_ERR_HIP) {
     const uint64_t back = std::min<uint64_t>(n, nd + (code ? 1 : 0));
     // arena bytes of the records from `announced` on: they start at the
-    // wire position of record `announced`, which is B (every announced
+    // wire position of record `announced`, which is Bsent (every announced
     // range ended cleanly at the next one's start)
-    const uint64_t a0 = std::min(arena_capacity, scale * B);
+    const uint64_t a0 = std::min(arena_capacity, scale * Bsent);
     if (code != TGPU_ERR_HIP && back > announced &&
         (hipMemcpy((uint8_t*)h_records + announced * S, drec.p + announced * S,
                    (back - announced) * S, hipMemcpyDeviceToHost) != hipSuccess ||

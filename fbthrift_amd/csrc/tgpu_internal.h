@@ -621,6 +621,13 @@ hipError_t launch_program_write_fixed(const EncodeArgs& a, const VProgram* d_pro
 void* host_pipe_create();
 void host_pipe_destroy(void* pipe);
 void* context_host_pipe(tgpu_context* ctx);  // created on first use, owned by ctx
+// The list spans of a schema whose decoded list arena holds nothing but
+// scalar list / set elements (a flat record program; no nested regions, no
+// strings inside containers): their member offsets and element widths, at
+// most `max` (tgpu_decode_host_chunks_ex's packing). 0: none, or not such a
+// schema.
+uint32_t packable_lists(const tgpu_schema* s, int protocol, uint32_t* member, uint32_t* width,
+                        uint32_t max);
 bool schema_has_lists(const tgpu_schema* schema);
 
 // ---- stream indexer (k_index.hip) launchers

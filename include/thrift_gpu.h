@@ -551,6 +551,26 @@ int tgpu_decode_host_chunks(tgpu_context* ctx, const tgpu_schema* schema, int pr
                             const tgpu_limits* limits, uint64_t chunk_bytes,
                             tgpu_chunk_fn on_chunk, void* user, tgpu_status* st,
                             uint64_t* n_decoded, uint64_t* consumed);
+
+/*
+ * tgpu_decode_host_chunks with flags. TGPU_HOST_PACK_LISTS: for a schema
+ * whose list arena holds only scalar list / set elements (a flat record
+ * program: no containers of structs or of containers, no strings inside
+ * containers), each finished range's element arrays are packed, in record
+ * order, at the front of that range's arena slice and the records' spans
+ * point there; only the records and the packed bytes are copied back (the
+ * slice is as large as its wire bytes x arena scale, config 4's elements
+ * 36 % of it). Span offsets then differ from tgpu_decode_host_ex's; the
+ * values they describe do not. Other schemas ignore the flag. The IOBuf
+ * batch API (GpuBatchSerializer::deserializeBatch) sets it.
+ */
+enum { TGPU_HOST_PACK_LISTS = 1 };
+int tgpu_decode_host_chunks_ex(tgpu_context* ctx, const tgpu_schema* schema, int protocol,
+                               const void* host_in, uint64_t in_len, uint64_t n_records,
+                               void* host_records, void* host_arena, uint64_t arena_capacity,
+                               const tgpu_limits* limits, uint64_t chunk_bytes, uint32_t flags,
+                               tgpu_chunk_fn on_chunk, void* user, tgpu_status* st,
+                               uint64_t* n_decoded, uint64_t* consumed);
 /*
  * Encode: the caller's fill(user, r0, r1, &form) provides the device form of
  * records [r0, r1) (records, and the string / list bases their spans are

@@ -502,9 +502,11 @@ class GpuBatchSerializer {
     };
     tgpu_status st{};
     uint64_t done = 0, consumed = 0;
-    tgpu_decode_host_chunks(ctx_, schema_.get(), Protocol::kId, in, len, n, recs, arena, acap,
-                            &limits_, decodeChunkBytes(len), on_chunk, &feed, &st, &done,
-                            &consumed);
+    // (list elements packed at each range's arena slice: only the records and
+    // the elements cross PCIe back; the binding reads through the spans)
+    tgpu_decode_host_chunks_ex(ctx_, schema_.get(), Protocol::kId, in, len, n, recs, arena, acap,
+                               &limits_, decodeChunkBytes(len), TGPU_HOST_PACK_LISTS, on_chunk,
+                               &feed, &st, &done, &consumed);
     feed.g.wait();  // every announced record materialized (or a hook's exception)
     if (st.code != TGPU_OK) rethrow(st);
     return consumed;

@@ -157,9 +157,9 @@ def test_host_ex_any_schema(gpu, name):
     assert st.as_tuple() == ost.as_tuple() and (nd, cons) == (ond, ocons)
 
 
-def _decode_chunks(gs, protocol, wire, n, chunk_bytes, arena_scale=0):
-    """tgpu_decode_host_chunks over host numpy buffers; returns (records,
-    arena, status, n_decoded, consumed, announced ranges)."""
+def _decode_chunks(gs, protocol, wire, n, chunk_bytes, arena_scale=0, flags=None):
+    """tgpu_decode_host_chunks (or _ex with `flags`) over host numpy buffers;
+    returns (records, arena, status, n_decoded, consumed, announced ranges)."""
     import ctypes
 
     from fbthrift_amd import _lib
@@ -174,10 +174,16 @@ def _decode_chunks(gs, protocol, wire, n, chunk_bytes, arena_scale=0):
     cb = _lib.CHUNK_FN(lambda u, r0, r1: ranges.append((r0, r1)))
     st = _lib.Status()
     nd, cons = ctypes.c_uint64(), ctypes.c_uint64()
-    _lib.lib().tgpu_decode_host_chunks(
-        BinarySerializer.context().handle, gs.handle, protocol, w.ctypes.data, len(w), n,
-        rec.ctypes.data, arena.ctypes.data if acap else None, acap, None, chunk_bytes, cb, None,
-        ctypes.byref(st), ctypes.byref(nd), ctypes.byref(cons))
+    if flags is None:
+        _lib.lib().tgpu_decode_host_chunks(
+            BinarySerializer.context().handle, gs.handle, protocol, w.ctypes.data, len(w), n,
+            rec.ctypes.data, arena.ctypes.data if acap else None, acap, None, chunk_bytes, cb,
+            None, ctypes.byref(st), ctypes.byref(nd), ctypes.byref(cons))
+    else:
+        _lib.lib().tgpu_decode_host_chunks_ex(
+            BinarySerializer.context().handle, gs.handle, protocol, w.ctypes.data, len(w), n,
+            rec.ctypes.data, arena.ctypes.data if acap else None, acap, None, chunk_bytes, flags,
+            cb, None, ctypes.byref(st), ctypes.byref(nd), ctypes.byref(cons))
     return rec, arena, st, nd.value, cons.value, ranges
 
 
@@ -251,3 +257,59 @@ def test_host_decode_chunks_lists(gpu):
         sp = d["f2"][i]
         a, b = int(sp["offset"]), int(sp["length"])
         assert np.array_equal(arena[a:a + 4 * b], oarena[a:a + 4 * b])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("protocol", [0, 2])
+@pytest.mark.parametrize("case", ["clean", "bad_record"])
+def test_host_decode_chunks_packed_lists(gpu, protocol, case):
+    """tgpu_decode_host_chunks_ex with TGPU_HOST_PACK_LISTS (what
+    deserializeBatch sets): config 4's shape through 4 KiB pieces, Binary and
+    Compact. Every record equals the oracle's except its list span's offset;
+    the span describes the same elements, packed at the front of its range's
+    arena slice; a malformed record late in the stream (ranges already packed
+    and announced, others staged) ends in the resident pass with the oracle's
+    status and the records before it intact."""
+    import helpers
+
+    from fbthrift_amd.serializer import GpuSchema
+
+    table = datagen.SCHEMAS["nested"]
+    schema = Schema.from_table(table)
+    n = 3000
+    vals = datagen.flatten_values(table, [datagen.gen_nested(i) for i in range(n)])
+    rec, sarena, larena = helpers.pack(schema, vals, n)
+    st, wire, offs = oracle.encode(schema, protocol, rec, n, sarena, larena)
+    wire = bytearray(wire)
+    if case == "bad_record":
+        # record 2700's first field header: a type no reader takes
+        wire[int(offs[2700])] = 0x05 if protocol == 0 else 0x1E
+    gs = GpuSchema(schema)
+    scale = oracle.arena_scale(schema, protocol)
+    got, arena, st, nd, cons, ranges = _decode_chunks(gs, protocol, wire, n, 4096, scale, 1)
+    ost, orec, oarena, ond, ocons = oracle.decode(schema, protocol, bytes(wire), n)
+    assert st.as_tuple() == ost.as_tuple() and (nd, cons) == (ond, ocons), (st.as_tuple(),
+                                                                           ost.as_tuple())
+    k = nd if st.code == 0 else nd + 1
+    if case == "clean":
+        assert len(ranges) > 10
+    d, o = got.view(schema.dtype()), orec.view(schema.dtype())
+    es = 4
+    packed = 0
+    for i in range(k if st.code == 0 else nd):
+        a, b = int(d["f2"][i]["offset"]), int(d["f2"][i]["length"])
+        oa, ob = int(o["f2"][i]["offset"]), int(o["f2"][i]["length"])
+        assert b == ob, i
+        assert np.array_equal(arena[a:a + es * b], oarena[oa:oa + es * ob]), i
+        packed += a != oa and b > 0
+    assert packed > 0  # the spans did move
+    # the raw record bytes but the span offset (8 bytes at the span's member
+    # offset) equal
+    S = gs.record_size
+    so = schema.dtype().fields["f2"][1]
+    m = nd if st.code else n
+    gr = got[: m * S].reshape(m, S).copy()
+    orr = orec[: m * S].reshape(m, S).copy()
+    gr[:, so:so + 8] = 0
+    orr[:, so:so + 8] = 0
+    assert np.array_equal(gr, orr)
