@@ -629,8 +629,7 @@ int tgpu_decode_host_chunks_ex(tgpu_context* ctx, const tgpu_schema* schema, int
   // packed list elements (TGPU_HOST_PACK_LISTS; schemas whose arena holds
   // scalar list elements only): each chunk's element arrays at the front of
   // its arena slice, the records' spans pointing there; the chunk's packed
-  // size is read back one chunk later (the next chunk's decode is queued
-  // first), then its records and packed bytes go back
+  // size is read back, then its records and packed bytes go back
   PackSpec ps{};
   if ((flags & TGPU_HOST_PACK_LISTS) && scale && arena_capacity)
     ps.n = packable_lists(schema, protocol, ps.member, ps.width, kPackMax);
@@ -756,12 +755,14 @@ int tgpu_decode_host_chunks_ex(tgpu_context* ctx, const tgpu_schema* schema, int
           clean = false;
           break;
         }
-        // the previous chunk's packed size is known once its kernels ran
+        // (tgpu_decode_stream above is a blocking call, so the chunk's
+        // kernels are all but done: its packed size is read at once and its
+        // copy back starts behind the pack)
+        staged.push_back(Staged{k, r0, nk, B});
         if (!flush_pending()) {
           clean = false;
           break;
         }
-        staged.push_back(Staged{k, r0, nk, B});
       } else if (hipEventRecord(evdec.ev[k], sdec) != hipSuccess ||
                  !send_back(k, r0, nk, B, std::min(arena_capacity, scale * last) - scale * B,
                             dar.p)) {

@@ -642,7 +642,7 @@ class GpuBatchSerializer {
   }
 
   /* Records per serializeBatch chunk (0 = 1 Mi) and wire bytes per
-   * deserializeBatch piece (0 = 1/16 of the batch, 4-64 MiB). */
+   * deserializeBatch piece (0 = 1/24 of the batch, 4-64 MiB). */
   void setChunkRecords(uint64_t k) { chunk_records_ = k; }
   void setChunkBytes(uint64_t b) { chunk_bytes_ = b; }
 
@@ -714,7 +714,9 @@ class GpuBatchSerializer {
  private:
   uint64_t decodeChunkBytes(uint64_t len) const {
     if (chunk_bytes_) return chunk_bytes_;
-    return std::min<uint64_t>(64ull << 20, std::max<uint64_t>(4ull << 20, len / 16));
+    // (1/24 of the batch: config 4's 373 MB in 16 MB pieces took 11.0-11.3 ms,
+    // 23 MB pieces 11.9-14.9, 8 MB 13.9-14.8; profiles/r05/ab/host_batch_pieces/)
+    return std::min<uint64_t>(64ull << 20, std::max<uint64_t>(4ull << 20, len / 24));
   }
   /* Pinned host staging kept across calls (grown with 25 % slack). */
   class Pinned {

@@ -262,6 +262,8 @@ static int run(int config, const GpuSchema& schema, const HostStruct& binding, u
   ser.compile();
   // (A/B: records per serializeBatch chunk; default the serializer's)
   if (const char* e = std::getenv("HB_CHUNK_RECORDS")) ser.setChunkRecords(std::strtoull(e, nullptr, 10));
+  // (A/B: wire bytes per deserializeBatch piece; default 1/16 of the batch)
+  if (const char* e = std::getenv("HB_CHUNK_BYTES")) ser.setChunkBytes(std::strtoull(e, nullptr, 10));
   double ser_ms = 1e30, de_ms = 1e30;
   uint64_t wire = 0;
   std::vector<uint8_t> bytes;
