@@ -47,11 +47,13 @@ def test_oracle_rejects_unknown_protocol():
 
 
 @pytest.mark.gpu
-def test_v1_program_selection(gpu):
+def test_v1_program_selection(gpu, monkeypatch):
     """A V1 schema without doubles runs Compact's compiled program; with
     doubles its own (Compact's ops, the doubles little-endian: kFixedLE) —
     tgpu_schema_compile compiles both."""
     from fbthrift_amd.serializer import GpuSchema
+
+    monkeypatch.setenv("TGPU_JIT", "1")  # (the compile policy, whatever the run's)
 
     assert GpuSchema(Schema.from_table(datagen.SCHEMAS["mixed"])).compile(V1)
     assert GpuSchema(Schema.from_table(datagen.SCHEMAS["nested"])).compile(V1)

@@ -113,9 +113,10 @@ def test_corpus_status_parity(gpu, codec, case):
 
 
 @pytest.mark.parametrize("name,protocol", [("mixed", 2), ("nested", 0), ("scalars", 2)])
-def test_schema_compiles_on_device(gpu, name, protocol):
+def test_schema_compiles_on_device(gpu, name, protocol, monkeypatch):
     """The schema compiler loads its kernels on the GPU (so the TGPU_JIT=1
     runs above exercise them, not the interpreter)."""
+    monkeypatch.setenv("TGPU_JIT", "1")  # (the compile policy, whatever the run's)
     assert _gschema(Schema.from_table(datagen.SCHEMAS[name])).compile(protocol)
 
 

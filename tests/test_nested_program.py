@@ -101,6 +101,7 @@ def _decode(Ser, gs, wire, n, offs, monkeypatch, nested):
 @pytest.mark.gpu
 @pytest.mark.parametrize("protocol", [0, 2])
 def test_nested_program_parity(gpu, protocol, monkeypatch):
+    monkeypatch.setenv("TGPU_JIT", "1")  # (the compile policy, whatever the run's)
     n = 40 * 1024
     schema, gs, Ser, wire, offs = _encode(gpu, protocol, n, 0x5eed + protocol)
     assert gs.compile(protocol)  # the nested program exists and compiles here
@@ -279,7 +280,7 @@ def test_nested_program_maps_strings(gpu, name, protocol, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", ["sparse", "strcont", "unions"])
-def test_nested_program_compiles_on_device(gpu, name):
+def test_nested_program_compiles_on_device(gpu, name, monkeypatch):
     """Schemas without a canonical record program — optional fields
     ('sparse'), strings inside containers ('strcont') — get the nested record
     program on the device: the golden parity runs with TGPU_JIT=1
@@ -288,6 +289,7 @@ def test_nested_program_compiles_on_device(gpu, name):
 
     from fbthrift_amd.serializer import GpuSchema
 
+    monkeypatch.setenv("TGPU_JIT", "1")  # (the compile policy, whatever the run's)
     gs = GpuSchema(Schema.from_table(helpers.manifest()["schemas"][name]))
     assert gs.compile(0) and gs.compile(2)
 
