@@ -1052,6 +1052,11 @@ __device__ __forceinline__ bool tile_walk(const PP& P, const TileSrc& src, const
 // random tiles, 200-600 of 217k per config-5 call, none under the profiler;
 // decode_tile's DMA covers whole waves too). The caller's __syncthreads
 // waits for the loads.
+#ifdef TGPU_STAGE_BARRIER
+#define TGPU_STAGE_SYNC() ((void)0)
+#else
+#define TGPU_STAGE_SYNC() __syncthreads()
+#endif
 __device__ __forceinline__ void stage_tile(uint8_t* lds, const uint8_t* gb, uint32_t nvec) {
 #ifdef TGPU_SPEC_REGSTAGE  // A/B: staging through registers
   for (uint32_t i = threadIdx.x; i < nvec; i += kTileLanes)
@@ -1068,7 +1073,10 @@ __device__ __forceinline__ void stage_tile(uint8_t* lds, const uint8_t* gb, uint
   }
   const uint32_t i = whole + threadIdx.x;
   if (i < nvec) ((uint4*)lds)[i] = ((const uint4*)gb)[i];
-#ifndef TGPU_NO_DMA_SETTLE  // A/B: (see lds_dma_settle)
+#if defined(TGPU_STAGE_BARRIER)  // diagnostics: the staging's wait and
+  // barrier exactly as given, in place of the settle and the caller's barrier
+  asm volatile(TGPU_STAGE_BARRIER ::: "memory");
+#elif !defined(TGPU_NO_DMA_SETTLE)  // A/B: (see lds_dma_settle)
   {
     const uint32_t w0 = wave * 64 + (threadIdx.x & 63);  // this lane's first DMA'd vector
     lds_dma_settle(lds, w0, kTileLanes, w0 < whole ? (whole - 1 - w0) / kTileLanes + 1 : 0);
@@ -1163,7 +1171,7 @@ __device__ __forceinline__ bool tile_resolve(const IndexArgs& a, const PP& P, ui
   const uint32_t staged = avail < kTile + kOver + 16 ? avail : kTile + kOver + 16;
   const uint32_t nvec = (staged + 15) >> 4;
   stage_tile(lds, gb, nvec);
-  __syncthreads();
+  TGPU_STAGE_SYNC();
 #ifdef TGPU_SPEC_LATE
   uint32_t late0 = 0;
   for (uint32_t d = threadIdx.x; d < ((staged & ~3u) >> 2); d += kTileLanes)
@@ -1336,7 +1344,7 @@ __device__ __forceinline__ bool spec_tile_cands(const IndexArgs& a, const PP& P,
   const uint32_t avail = (uint32_t)(avail64 < kPosCap ? avail64 : kPosCap);
   const uint32_t staged = avail < kTile + kOver + 16 ? avail : kTile + kOver + 16;
   stage_tile(lds, gb, (staged + 15) >> 4);
-  __syncthreads();
+  TGPU_STAGE_SYNC();
 #ifdef TGPU_SPEC_EARLY  // diagnostics: the staged bytes right after the staging barrier
   {
     uint32_t bad = 0;
@@ -1635,7 +1643,7 @@ __device__ __forceinline__ void index_emit_tile(const IndexArgs& a, const PP& P,
     L.c = v >> 16;
     first = ent;
     ok = true;
-    __syncthreads();
+    TGPU_STAGE_SYNC();
   } else {
     ok = tile_resolve(a, P, j, lds, ent, L, sh, first, sm.E, &sm.flag, &sm.first_lane, &sm.fs,
                       sm.cmask);

@@ -63,16 +63,60 @@ __device__ __forceinline__ void note_exception(bool flag, uint64_t i, DevResult*
 // vmcnt(0), made every such call clean (as did a 128-cycle pause, or
 // staging through registers, which costs 0.2 ms per call); the caller's
 // barrier then waits for these reads (lgkmcnt(0)). One read of the lane's
-// last DMA'd vector is enough (round 4: the read is a FLAT access to the LDS
-// aperture, returned in order behind the wave's own DMA writes — DESIGN.md
-// §4.2): zero repairs on config 5 and the whole GPU suite green with it, and
-// 1-3 % off every LDS-DMA decode against a read per vector
-// (TGPU_SETTLE_EACH, A/B). `first` = the lane's first vector index, `step` =
+// last DMA'd vector is enough: zero repairs on config 5 and the whole GPU
+// suite green with it, and 1-3 % off every LDS-DMA decode against a read per
+// vector (TGPU_SETTLE_EACH, A/B). Round 5: the read is not
+// what orders — the wait alone placed early (TGPU_SETTLE_WAIT_ONLY,
+// TGPU_SETTLE_VMLGKM) is as clean, expcnt plays no part (TGPU_SETTLE_EXPCNT)
+// and idle cycles before the wait do not help (TGPU_SETTLE_NOPS): what every
+// clean form has is work between the wave's vmcnt reaching zero and the
+// readers' first LDS read. `first` = the lane's first vector index, `step` =
 // the vector stride between its DMAs, `n` = its DMAs.
 __device__ __forceinline__ void lds_dma_settle(const uint8_t* lds, uint32_t first, uint32_t step,
                                                uint32_t n) {
+#if defined(TGPU_SETTLE_EXPCNT)  // diagnostics: expcnt(0) alone (inline asm: the
+  // compiler's wait pass would merge a builtin into its own full wait)
+  asm volatile("s_waitcnt expcnt(0)" ::: "memory");
+  (void)lds;
+  (void)first;
+  (void)step;
+  (void)n;
+  return;
+#elif defined(TGPU_SETTLE_VMLGKM)  // diagnostics: vmcnt(0) lgkmcnt(0), expcnt left open
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  (void)lds;
+  (void)first;
+  (void)step;
+  (void)n;
+  return;
+#elif defined(TGPU_SETTLE_NOPS)  // diagnostics: ~40 idle cycles, no wait (the
+  // compiler's own vmcnt(0) lgkmcnt(0) stays right before the barrier)
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");
+  (void)lds;
+  (void)first;
+  (void)step;
+  (void)n;
+  return;
+#endif
   __builtin_amdgcn_s_waitcnt(0);  // (vmcnt(0) expcnt(0) lgkmcnt(0))
-#ifndef TGPU_SETTLE_EACH
+#if defined(TGPU_SETTLE_WAIT_ONLY)  // diagnostics: the full wait alone
+  (void)lds;
+  (void)first;
+  (void)step;
+  (void)n;
+#elif defined(TGPU_SETTLE_SLEEP)  // diagnostics: the wait, then ~4k cycles, no read
+  (void)lds;
+  (void)first;
+  (void)step;
+  (void)n;
+  for (int k = 0; k < 64; ++k) __builtin_amdgcn_s_sleep(1);
+#elif defined(TGPU_SETTLE_DSREAD)  // diagnostics: the read through the LDS address space
+  if (n) {
+    const __attribute__((address_space(3))) volatile uint32_t* l3 =
+        (const __attribute__((address_space(3))) volatile uint32_t*)(lds);
+    (void)l3[(first + (n - 1) * step) * 4];
+  }
+#elif !defined(TGPU_SETTLE_EACH)
   if (n) (void)((const volatile uint32_t*)lds)[(first + (n - 1) * step) * 4];
 #else
   for (uint32_t k = 0; k < n; ++k)
