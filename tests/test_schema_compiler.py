@@ -65,3 +65,17 @@ def test_recursive_program_compiles_with_its_writer(protocol, monkeypatch):
     tree = [[[1, 8, 0, 0, -1], [2, 15, 12, 0, 0]]]
     rc, log = compile_check(Schema.from_table(tree), protocol)
     assert rc == 0, log
+
+
+@pytest.mark.parametrize("define", [
+    "#define TGPU_SETTLE_WAIT_ONLY 1",
+    "#define TGPU_SETTLE_VMLGKM 1",
+    '#define TGPU_STAGE_BARRIER "s_waitcnt vmcnt(0) lgkmcnt(0)\\n\\ts_barrier"',
+])
+def test_settle_diagnostic_variants_compile(define, monkeypatch):
+    """The LDS-DMA settle's diagnostic variants (DESIGN.md §4.2, round 5:
+    the staging's wait and barrier forms A/B'd on config 5 through
+    TGPU_JIT_DEFINES) stay buildable: config 5's schema, all kernel groups."""
+    monkeypatch.setenv("TGPU_JIT_DEFINES", define)
+    rc, log = compile_check(Schema.from_table(M["mixed"]), 2)
+    assert rc == 0, log
