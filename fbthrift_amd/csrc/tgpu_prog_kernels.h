@@ -491,19 +491,93 @@ __device__ __forceinline__ void put_varint(Sink& s, uint64_t v) {
 struct StrPrefetch {
   uint32_t v[8];
 };
+// String payloads as 16-byte vectors of the 16-byte-aligned blocks the string
+// touches (a whole aligned block never reaches a page the string does not),
+// two per batch, shifted into place in registers: 2 loads per 32 bytes where
+// the dword form issues 8. Round 5, config 3 encode 2.61 -> 2.49 ms (the
+// payload loads cost 0.49 ms of it, A/B TGPU_NO_STR_LOAD;
+// profiles/r05/ab/str_x4_ab.log). TGPU_STR_X4=0 keeps the dword form (A/B).
+#ifndef TGPU_STR_X4
+#define TGPU_STR_X4 1
+#endif
+#if TGPU_STR_X4
+typedef uint32_t StrVec __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void str_load32(uint32_t (&v)[8], const uint8_t* __restrict__ blk,
+                                           uint32_t nvec) {
+  StrVec a = {0u, 0u, 0u, 0u}, b = {0u, 0u, 0u, 0u};
+  if (nvec > 0) a = ((const StrVec*)blk)[0];
+  if (nvec > 1) b = ((const StrVec*)blk)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+// v (a block's 8 dwords) -> the dwords of the bytes from `off` (0..15) on
+__device__ __forceinline__ void str_shift(uint32_t (&v)[8], uint32_t off) {
+  const bool d2 = (off & 8) != 0, d1 = (off & 4) != 0;
+  const uint32_t by = off & 3;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i) v[i] = d2 ? (i + 2 < 8 ? v[i + 2] : 0u) : v[i];
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i) v[i] = d1 ? (i + 1 < 8 ? v[i + 1] : 0u) : v[i];
+#pragma unroll
+  for (uint32_t i = 0; i < 7; ++i) v[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], by);
+  v[7] = v[7] >> (8 * by);
+}
+#endif
+
 __device__ __forceinline__ void str_prefetch(StrPrefetch& f, const uint8_t* __restrict__ src,
                                              uint32_t len) {
+#if TGPU_STR_X4
+  {
+    const uint32_t off = (uint32_t)((uintptr_t)src & 15);
+    const uint32_t nv = (off + len + 15) >> 4;
+    str_load32(f.v, src - off, len ? (nv < 2 ? nv : 2) : 0);
+    return;
+  }
+#endif
   const uint32_t sh = (uint32_t)((uintptr_t)src & 3);
   const uint32_t* w = (const uint32_t*)(src - sh);
   const uint32_t need = (sh + len + 3) >> 2;
 #pragma unroll
+#ifndef TGPU_NO_STR_LOAD  // (A/B only, as in put_bytes)
   for (uint32_t i = 0; i < 8; ++i) f.v[i] = i < need ? w[i] : 0u;
+#else
+  for (uint32_t i = 0; i < 8; ++i) f.v[i] = i < need ? i : 0u;
+#endif
 }
 
 template <class Sink>
 __device__ __forceinline__ void put_bytes(Sink& s, const uint8_t* __restrict__ src, uint32_t len,
                                           const StrPrefetch* pf = nullptr) {
   if (!len) return;
+#if TGPU_STR_X4
+  {
+    uint32_t off = (uint32_t)((uintptr_t)src & 15);
+    const uint8_t* blk = src - off;
+    uint32_t left = len;
+    bool first = true;
+    while (left) {
+      const uint32_t nv = (off + left + 15) >> 4;
+      uint32_t v[8];
+      if (pf && first) {
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i) v[i] = pf->v[i];
+      } else {
+        str_load32(v, blk, nv < 2 ? nv : 2);
+      }
+      first = false;
+      str_shift(v, off);
+      const uint32_t room = 32 - off;
+      const uint32_t take = left < room ? left : room;
+#pragma unroll
+      for (uint32_t i = 0; i < 8; ++i)
+        if (4 * i < take) s.put(v[i], take - 4 * i < 4 ? take - 4 * i : 4);
+      left -= take;
+      blk += 32;
+      off = 0;
+    }
+    return;
+  }
+#endif
   // (the aligned base by pointer arithmetic on src, not an integer cast: the
   // loads keep src's address space — global_load, not flat_load)
   uint32_t sh = (uint32_t)((uintptr_t)src & 3);
