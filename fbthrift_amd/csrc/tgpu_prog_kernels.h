@@ -311,10 +311,46 @@ struct RegRec {
 #ifndef TGPU_ELEM_BATCH
 #define TGPU_ELEM_BATCH 8
 #endif
+// 4- and 8-byte elements as 16-byte vectors of the aligned blocks they
+// occupy (str_load32 / str_shift below): each batch takes the whole elements
+// of the 32 bytes from the batch's first element on. TGPU_ELEM_X4=0: one
+// load per element (A/B).
+#ifndef TGPU_ELEM_X4
+#define TGPU_ELEM_X4 1
+#endif
+__device__ __forceinline__ void str_load32(uint32_t (&v)[8], const uint8_t* __restrict__ blk,
+                                           uint32_t nvec);
+__device__ __forceinline__ void str_shift(uint32_t (&v)[8], uint32_t off);
 template <class F>
 __device__ __forceinline__ void for_elems(const uint8_t* __restrict__ e, uint32_t len,
                                           uint32_t width, F&& f) {
   constexpr uint32_t B = TGPU_ELEM_BATCH;
+#if TGPU_ELEM_X4
+  if (width == 4 || width == 8) {
+    uint32_t left = len;
+    while (left) {
+      const uint32_t off = (uint32_t)((uintptr_t)e & 15);
+      const uint32_t fit = (32 - off) / width;  // whole elements in this batch's window
+      const uint32_t m = left < fit ? left : fit;
+      const uint32_t nv = (off + m * width + 15) >> 4;
+      uint32_t v[8];
+      str_load32(v, e - off, nv < 2 ? nv : 2);
+      str_shift(v, off);
+      if (width == 4) {
+#pragma unroll
+        for (uint32_t k = 0; k < 8; ++k)
+          if (k < m) f((uint64_t)v[k]);
+      } else {
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k)
+          if (k < m) f(((uint64_t)v[2 * k + 1] << 32) | v[2 * k]);
+      }
+      e += m * width;
+      left -= m;
+    }
+    return;
+  }
+#endif
   if constexpr (B == 1) {
     for (uint32_t i = 0; i < len; ++i) f(load_member(e + (uint64_t)i * width, width));
   } else {
@@ -497,10 +533,10 @@ struct StrPrefetch {
 // the dword form issues 8. Round 5, config 3 encode 2.61 -> 2.49 ms (the
 // payload loads cost 0.49 ms of it, A/B TGPU_NO_STR_LOAD;
 // profiles/r05/ab/str_x4_ab.log). TGPU_STR_X4=0 keeps the dword form (A/B).
+// for_elems reads 4- and 8-byte list elements the same way (TGPU_ELEM_X4).
 #ifndef TGPU_STR_X4
 #define TGPU_STR_X4 1
 #endif
-#if TGPU_STR_X4
 typedef uint32_t StrVec __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void str_load32(uint32_t (&v)[8], const uint8_t* __restrict__ blk,
                                            uint32_t nvec) {
@@ -522,7 +558,6 @@ __device__ __forceinline__ void str_shift(uint32_t (&v)[8], uint32_t off) {
   for (uint32_t i = 0; i < 7; ++i) v[i] = __builtin_amdgcn_alignbyte(v[i + 1], v[i], by);
   v[7] = v[7] >> (8 * by);
 }
-#endif
 
 __device__ __forceinline__ void str_prefetch(StrPrefetch& f, const uint8_t* __restrict__ src,
                                              uint32_t len) {
