@@ -203,7 +203,8 @@ class Flat8(Workload):
     config_id = 2
     name = "config 2: Binary protocol, flat {1..8: i64} records, encode+decode"
     default_records = 1 << 26
-    dec_kernel, enc_kernel = "plan_binary_decode_kernel", "plan_binary_encode_kernel"
+    # (the lane-stationary plan kernels, k_plan_binary.hip, default since round 5)
+    dec_kernel, enc_kernel = "plan_binary_decode_ls_kernel", "plan_binary_encode_ls_kernel"
 
     def __init__(self, n, rank, dev):
         import torch
