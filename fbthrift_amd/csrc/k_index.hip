@@ -424,7 +424,12 @@ __device__ __forceinline__ bool index_merge_one(const IndexArgs& a, uint64_t j) 
 // counter of round r is scal[16 + (r & 1)]; a round after one that changed
 // nothing returns at once (stream-ordered, no host read).
 __global__ __launch_bounds__(256) void index_merge_snap_kernel(IndexArgs a, int round) {
-  if (round > 0 && a.scal[16 + ((round - 1) & 1)] == 0) return;
+  if (round > 0 && a.scal[16 + ((round - 1) & 1)] == 0) {
+    // skipped: this round's counter still holds round - 2's count, so zero
+    // it, or round + 1 would see it and run a full round again
+    if (blockIdx.x == 0 && threadIdx.x == 0) a.scal[16 + (round & 1)] = 0;
+    return;
+  }
   const uint64_t stride = (uint64_t)gridDim.x * 256;
   for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < a.n_chunks; j += stride)
     a.ep[j] = a.e[j];

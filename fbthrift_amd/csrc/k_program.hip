@@ -62,6 +62,30 @@ __global__ __launch_bounds__(256) void general_decode_list_kernel(DecodeArgs a,
 // 1.64 -> 1.45 ms going from the old fixed 1.3 x mean + 1 KiB to 5
 // workgroups/CU.) TGPU_PROG_DECODE="factor,pad" overrides the upper bound.
 // span_bytes: the wire bytes of the n records (0: a.in_len).
+int64_t device_lds_per_cu() {
+  static const int64_t v = [] {
+    int dev = 0, x = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&x, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) ==
+            hipSuccess &&
+        x > 0)
+      return (int64_t)x;
+    return (int64_t)163840;
+  }();
+  return v;
+}
+uint32_t lds_per_block_limit() {
+  static const uint32_t v = [] {
+    int dev = 0, x = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&x, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) == hipSuccess &&
+        x > 0)
+      return (uint32_t)x;
+    return 0u;
+  }();
+  return v;
+}
+
 uint32_t program_decode_wire_cap(const DecodeArgs& a, uint32_t rec_size, uint64_t span_bytes,
                                  bool regrec) {
   double factor = 1.12, pad = 512.0;

@@ -144,18 +144,29 @@ hipError_t launch_xcode(const XcodeArgs& x, int from, int to, const VProgram* d_
     const double want_w = 1.04 * in_tile + 256.0, max_w = 1.12 * in_tile + 512.0;
     const double want_o = std::min(1.04 * (double)x.out_mean * kPT + 256.0, (double)prog::kOutCap);
     // (no w that holds both: the sizes above)
+    const int64_t cu_lds = device_lds_per_cu();
     for (uint32_t w = 8; w >= 1; --w) {
-      const int64_t budget = (int64_t)(163840u / w) - 256 - (int64_t)rt;  // (static LDS, slack)
+      const int64_t budget = cu_lds / w - 256 - (int64_t)rt;  // (static LDS, slack)
       const uint32_t rw = prog::decode_wire_region((uint32_t)want_w);
-      if ((double)rw + want_o + 32.0 > (double)budget) continue;
-      // the largest wire cap within the staging rounds the tile needs
+      // the largest wire cap within the staging rounds the tile needs (at
+      // least 4 KiB); the fit is checked on the region that cap really takes
       uint32_t c = std::min<uint32_t>((uint32_t)max_w, rw - 32) & ~15u;
       c = std::max(c, std::min<uint32_t>((uint32_t)want_w, rw - 32) & ~15u);
-      cap = std::max<uint32_t>(c, 4096);
-      ocap = (uint32_t)std::min<int64_t>(prog::kOutCap,
-                                         budget - prog::decode_wire_region(cap) - 32) & ~15u;
+      c = std::max<uint32_t>(c, 4096);
+      const int64_t room = budget - (int64_t)prog::decode_wire_region(c) - 32;
+      if ((double)room < want_o || room < (int64_t)kMinXcodeOut) continue;
+      cap = c;
+      ocap = (uint32_t)std::min<int64_t>(prog::kOutCap, room) & ~15u;
       break;
     }
+  }
+  if (lds_per_block_limit() && prog::decode_wire_region(cap) + rt + ocap + 32 >
+                                   lds_per_block_limit()) {
+    // (a device with less LDS than the sizes above: the encoder's own tile
+    // sizes, or whatever the block limit leaves of them)
+    const int64_t room = (int64_t)lds_per_block_limit() -
+                         (int64_t)prog::decode_wire_region(cap) - (int64_t)rt - 32;
+    ocap = (uint32_t)std::max<int64_t>(std::min<int64_t>(room, prog::kOutCap), 0) & ~15u;
   }
   if (const char* v = getenv("TGPU_XC_OCAP"))  // (A/B)
     if (*v) ocap = (uint32_t)atoi(v) & ~15u;

@@ -462,6 +462,14 @@ struct XTabAlloc {
 constexpr uint32_t kScratchGrid = 64;
 
 #ifndef __HIPCC_RTC__
+// LDS of the current device (hipDeviceAttributeMaxSharedMemoryPerMultiprocessor
+// / ...PerBlock, read once per process; 160 KiB / 160 KiB on gfx950, the
+// values the occupancy rules below were tuned on). k_program.hip.
+int64_t device_lds_per_cu();
+uint32_t lds_per_block_limit();
+// the transcoder's smallest useful LDS output tile (a residency that leaves
+// less takes fewer workgroups per CU instead)
+constexpr uint32_t kMinXcodeOut = 1024;
 // Launchers (defined in the .hip files; all asynchronous on `stream`).
 // `t` is the host copy (launch geometry), `d_t` the device copy the kernels read.
 // Fixed-layout decodes: a record they cannot take joins the exception list

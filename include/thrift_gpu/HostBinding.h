@@ -264,12 +264,16 @@ inline void readValue(const SchemaTables& sc, uint32_t t, int32_t si, uint32_t t
     readContainer(sc, ctypeNode(sc, ti), dev, src, ht, host);
   } else {
     const uint32_t w = scalarBytes(t);
-    std::memcpy(host, dev, w);
+    // never more bytes than the bound C++ scalar holds (a list<i64> bound to
+    // std::vector<int32_t> keeps the low 4 bytes; a binding of unknown size
+    // takes the schema width)
+    const uint32_t hw = ht.kind == HostType::Scalar && ht.size ? ht.size : w;
+    std::memcpy(host, dev, w < hw ? w : hw);
     // an integer bound to a wider C++ integer: sign-extended (a list<i16>
     // bound to std::vector<int32_t> reads -3 as -3, not 65533)
-    if (ht.kind == HostType::Scalar && ht.size > w && w < 8 &&
+    if (hw > w && w < 8 &&
         (t == TGPU_T_BYTE || t == TGPU_T_I16 || t == TGPU_T_I32) && (dev[w - 1] & 0x80))
-      std::memset(static_cast<uint8_t*>(host) + w, 0xff, ht.size - w);
+      std::memset(static_cast<uint8_t*>(host) + w, 0xff, hw - w);
   }
 }
 
@@ -437,7 +441,19 @@ void writeValue(const SchemaTables& sc, uint32_t t, int32_t si, uint32_t ti, con
   } else if (isContainer(t)) {
     writeContainer<Count>(sc, ctypeNode(sc, ti), host, ht, out, dev);
   } else if (!Count) {
-    std::memcpy(dev, host, scalarBytes(t));
+    // a C++ scalar narrower than the schema type fills the slot's low bytes
+    // and is sign-extended (std::vector<int32_t> bound to list<i64>); never
+    // read past the host object
+    const uint32_t w = scalarBytes(t);
+    const uint32_t hw = ht.kind == HostType::Scalar && ht.size ? ht.size : w;
+    if (hw >= w) {
+      std::memcpy(dev, host, w);
+    } else {
+      std::memcpy(dev, host, hw);
+      const bool neg = t != TGPU_T_BOOL && t != TGPU_T_DOUBLE && t != TGPU_T_FLOAT &&
+                       (static_cast<const uint8_t*>(host)[hw - 1] & 0x80);
+      std::memset(dev + hw, neg ? 0xff : 0, w - hw);
+    }
   }
 }
 

@@ -4,7 +4,11 @@
 // the one-copy path reads / writes sizeof(E) bytes per element and would
 // misread the 2-byte device elements. A width-matched
 // binding (list<i32> -> std::vector<int32_t>) keeps the one-copy path and
-// gives the same values.
+// gives the same values. A schema type WIDER than the bound element
+// (list<i64> -> std::vector<int32_t>) takes the per-element
+// path too and never copies more than 4 bytes into / out of an element:
+// decode keeps the low bytes, encode sign-extends (built with
+// -fsanitize=address, so an overrun fails the run).
 #include <cstdio>
 #include <cstring>
 #include <vector>
@@ -44,7 +48,10 @@ static int run(uint8_t elem_tt, uint32_t ew) {
   // decode: 5 elements of ew bytes in the arena
   const int32_t want[5] = {-3, 7, 300, -32768, 32767};
   std::vector<uint8_t> arena(64, 0xee);
-  for (int i = 0; i < 5; ++i) std::memcpy(arena.data() + 8 + i * ew, &want[i], ew);
+  for (int i = 0; i < 5; ++i) {
+    const int64_t w64 = want[i];  // (little-endian: the low ew bytes of the value)
+    std::memcpy(arena.data() + 8 + i * ew, &w64, ew);
+  }
   uint8_t dev[24] = {};
   detail::storeSpan(dev, 8, 5);
   dev[16] = 1;
@@ -54,7 +61,7 @@ static int run(uint8_t elem_tt, uint32_t ew) {
   for (int i = 0; i < 5; ++i) CHECK(r.v[i] == want[i]);
 
   // encode: the device form's element array holds ew bytes per element
-  std::vector<uint8_t> lists(64, 0), out(24, 0);
+  std::vector<uint8_t> lists(5 * ew, 0), out(24, 0);
   detail::Sink k;
   detail::writeStruct<true>(sc, 0, (const uint8_t*)&r, hs, k, nullptr);
   CHECK(k.lpos == 5 * ew);
@@ -64,9 +71,10 @@ static int run(uint8_t elem_tt, uint32_t ew) {
   const tgpu_span sp = detail::loadSpan(out.data());
   CHECK(sp.length == 5);
   for (int i = 0; i < 5; ++i) {
-    int32_t x = 0;
+    int64_t x = 0;
     std::memcpy(&x, lists.data() + sp.offset + i * ew, ew);
     if (ew == 2) x = (int16_t)x;
+    if (ew == 4) x = (int32_t)x;
     CHECK(x == want[i]);
   }
   return 0;
@@ -75,6 +83,7 @@ static int run(uint8_t elem_tt, uint32_t ew) {
 int main() {
   if (run(TGPU_T_I16, 2)) return 1;  // width mismatch: per-element path
   if (run(TGPU_T_I32, 4)) return 1;  // matched: the one-copy path
+  if (run(TGPU_T_I64, 8)) return 1;  // schema wider than the element: per element, in bounds
   std::printf("binding width ok\n");
   return 0;
 }

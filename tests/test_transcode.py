@@ -203,3 +203,40 @@ def test_gpu_transcode_fused_irregular_records(gpu, codec, pf, pt, onepass, ever
     fit = int(np.searchsorted(wo[1:], cap, side="right"))  # records whose end is <= cap
     assert gst.code == 21 and done == fit and size == int(wo[fit]), (gst.as_tuple(), done, fit)
     assert bytes(out[:size].cpu().numpy()) == want[:size]
+
+
+def _small_records(n, seed=11):
+    """n records of {1..5: i64} with small values: S = 48 (5 x 8 + 5 isset
+    bytes, 8-aligned), about 11 Compact wire bytes per record."""
+    from fbthrift_amd.schema import Schema
+
+    schema = Schema.from_table([[[k, 10, 0, 0, -1] for k in range(1, 6)]])
+    assert schema.record_size == 48
+    rng = np.random.default_rng(seed)
+    rec = np.zeros(n, dtype=schema.dtype())
+    for f in schema.structs[0].fields:
+        rec[f.name] = rng.integers(-60, 60, n)
+    rec["__isset"][:] = 1
+    return schema, rec.view(np.uint8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pt", [0x102, 0])
+def test_gpu_transcode_small_records_lds_sizing(gpu, xmode, pt):
+    """with the record tile in LDS (the library's own
+    kernels, below the schema compiler's 64 Ki-record threshold) a light
+    record (S 48, ~11 Compact bytes) made the joint LDS sizing take a 4 KiB
+    wire-cap floor it had not fitted, and the output tile size went negative.
+    The transcoded stream must equal the composed decode + encode (the
+    oracle's) byte for byte."""
+    n = 50_000
+    schema, rec = _small_records(n)
+    st, wire, offs = oracle.encode(schema, 2, rec, n, None)
+    assert st.code == 0 and len(wire) < 12 * n
+    ost, ond, want, woffs = _oracle_transcode(schema, 2, pt, wire, n)
+    assert ost.code == 0 and ond == n
+    for given in (None, offs):
+        gst, done, out, o = _gpu_transcode(gpu, schema, 2, pt, wire, n, offsets=given)
+        assert gst.code == 0 and done == n, gst.as_tuple()
+        assert out == want
+        assert np.array_equal(o.astype(np.uint64), np.asarray(woffs, np.uint64))
