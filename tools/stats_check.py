@@ -35,8 +35,14 @@ def trace_rows(d):
 
 
 def base_name(k):
-    """rocprof names carry the argument list for templated kernels."""
-    return k.split("(")[0].strip()
+    """The kernel's own name: rocprof's demangled names carry the return
+    type, namespaces, template and call arguments."""
+    k = k.strip().replace("(anonymous namespace)::", "")
+    if k.startswith("void "):
+        k = k[5:]
+    for c in "<(":
+        k = k.split(c)[0]
+    return k.split("::")[-1].strip()
 
 
 def summarize(rows, kernels, steps):
