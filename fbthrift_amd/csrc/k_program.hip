@@ -21,6 +21,7 @@
 // tgpu_device.h) decodes it, so results and errors are exactly the reference's.
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include "tgpu_device.h"
 #include "tgpu_prog_kernels.h"
@@ -87,17 +88,18 @@ uint32_t lds_per_block_limit() {
 }
 
 uint32_t program_decode_wire_cap(const DecodeArgs& a, uint32_t rec_size, uint64_t span_bytes,
-                                 bool regrec) {
+                                 bool regrec, uint32_t extra) {
   double factor = 1.12, pad = 512.0;
   if (const char* e = getenv("TGPU_PROG_DECODE")) sscanf(e, "%lf,%lf", &factor, &pad);
   const double span = (double)(span_bytes ? span_bytes : a.in_len);
   const double mean = span / (double)(a.n ? a.n : 1) * kPT;
   const double lo = 1.04 * mean + 256.0, hi = std::max(factor * mean + pad, lo);
-  const uint32_t rt = regrec ? 0u : (kPT * rec_size + 16 + 15) & ~15u;
+  const uint32_t rt = (regrec ? 0u : prog::decode_rtile_bytes(rec_size)) + extra;
+  const double cu = (double)device_lds_per_cu();
   double cap = hi;
   for (uint32_t w = 8; w >= 1; --w) {
     // wire bytes that fit w workgroups (the region is whole 4 KiB staging rounds)
-    const double room = std::floor((163840.0 / w - rt) / 4096.0) * 4096.0 - 32.0;
+    const double room = std::floor((cu / w - rt) / 4096.0) * 4096.0 - 32.0;
     if (room >= lo) {
       cap = std::min(room, hi);
       break;
@@ -107,17 +109,25 @@ uint32_t program_decode_wire_cap(const DecodeArgs& a, uint32_t rec_size, uint64_
   return ((uint32_t)cap) & ~15u;
 }
 
-uint32_t program_decode_lds(uint32_t wire_cap, uint32_t rec_size, bool regrec = false) {
-  return prog::decode_wire_region(wire_cap) + (regrec ? 0u : ((kPT * rec_size + 16 + 15) & ~15u));
+uint32_t program_decode_lds(uint32_t wire_cap, uint32_t rec_size, bool regrec = false,
+                            uint32_t extra = 0) {
+  return prog::decode_wire_region(wire_cap) + (regrec ? 0u : prog::decode_rtile_bytes(rec_size)) +
+         extra;
 }
 
 hipError_t launch_program_decode(const DecodeArgs& a, const VProgram* d_prog, uint32_t rec_size,
                                  uint64_t* irregular, unsigned long long* n_irregular,
                                  hipStream_t stream, const JitKernels* jit, uint64_t span_bytes) {
   if (a.n == 0) return hipSuccess;
-  uint32_t cap = program_decode_wire_cap(a, rec_size, span_bytes, false);
+  // the block rule: compiled Binary programs with lists pack their blocks
+  // in the decode tile (pack_wave, no extra LDS); the library's interpreting
+  // kernel leaves the packing to arena_pack_kernel
+  DecodeArgs b = a;
+  if (!jit || !b.pack_flags || !b.pack_k) b.pack_flags = nullptr, b.pack_k = 0;
+  const uint32_t extra = 0;
+  uint32_t cap = program_decode_wire_cap(b, rec_size, span_bytes, false, extra);
   const uint64_t tiles = (a.n + kPT - 1) / kPT;
-  uint32_t lds = program_decode_lds(cap, rec_size, false);
+  uint32_t lds = program_decode_lds(cap, rec_size, false, extra);
   // Records in registers (entry 2) where the LDS record tile holds the tile
   // down to 3 workgroups per CU or fewer, dropping it fits more, and records
   // are whole 64-byte halves of a cache line: config 4 (S 64) 1.86 -> 1.69 ms
@@ -128,15 +138,16 @@ hipError_t launch_program_decode(const DecodeArgs& a, const VProgram* d_prog, ui
   // TGPU_DECODE_REGREC=0 / 1 forces it off / on (A/B).
   if (jit && jit_has(jit, 2)) {
     const char* v = getenv("TGPU_DECODE_REGREC");
-    const uint32_t cap2 = program_decode_wire_cap(a, rec_size, span_bytes, true);
-    const uint32_t lds2 = program_decode_lds(cap2, rec_size, true);
-    const uint32_t w1 = 163840 / lds, w2 = 163840 / lds2;
+    const uint32_t cap2 = program_decode_wire_cap(b, rec_size, span_bytes, true, extra);
+    const uint32_t lds2 = program_decode_lds(cap2, rec_size, true, extra);
+    const uint32_t cu = (uint32_t)device_lds_per_cu();
+    const uint32_t w1 = cu / lds, w2 = cu / lds2;
     const bool rr = v ? v[0] == '1' : (rec_size % 64 == 0 && w1 <= 3 && w2 > w1);
     if (rr)
-      return jit_launch_decode(jit, a, tiles, cap2, lds2, irregular, n_irregular, stream, 2);
+      return jit_launch_decode(jit, b, tiles, cap2, lds2, irregular, n_irregular, stream, 2);
   }
-  if (jit) return jit_launch_decode(jit, a, tiles, cap, lds, irregular, n_irregular, stream);
-  hipLaunchKernelGGL(program_decode_kernel, dim3((uint32_t)tiles), dim3(kPT), lds, stream, a,
+  if (jit) return jit_launch_decode(jit, b, tiles, cap, lds, irregular, n_irregular, stream);
+  hipLaunchKernelGGL(program_decode_kernel, dim3((uint32_t)tiles), dim3(kPT), lds, stream, b,
                      d_prog, rec_size, cap, irregular, n_irregular);
   return hipGetLastError();
 }

@@ -123,7 +123,7 @@ uint32_t list_grid(uint64_t n) {
 // occupancy rule for the decode's tile), the record tile (AOT pair) and, in
 // the write pass, the output tile.
 uint32_t program_decode_wire_cap(const DecodeArgs& a, uint32_t rec_size, uint64_t span_bytes,
-                                 bool regrec);
+                                 bool regrec, uint32_t extra);
 
 hipError_t launch_xcode(const XcodeArgs& x, int from, int to, const VProgram* d_ps,
                         const VProgram* d_pd, hipStream_t s, const JitKernels* jit) {
@@ -132,7 +132,7 @@ hipError_t launch_xcode(const XcodeArgs& x, int from, int to, const VProgram* d_
   const uint32_t S = x.d.rec_size;
   const bool rr = jit && jit_has(jit, 2);  // records in registers (S <= 128, S % 8 == 0)
   const uint32_t rt = rr ? 0u : prog::xc_rec_region(S, 0);
-  uint32_t cap = program_decode_wire_cap(x.d, S, 0, rr);
+  uint32_t cap = program_decode_wire_cap(x.d, S, 0, rr, 0);
   // output tile: the encoder's 24 KiB (a record past it goes to HBM
   // directly), or — sized with the wire tile for the most workgroups per CU
   // that hold 1.04 x the mean tile of each (x.out_mean: the host's estimate)

@@ -59,9 +59,44 @@ struct tgpu_schema {
   // learned (blocking encode / size calls), by protocol id: sizes the
   // compiled write pass's LDS output tile (enc_out_cap)
   std::atomic<uint64_t> mean16[3] = {0, 0, 0};
+  // the block rule's slots (n = 0: the position rule; ArenaPack, k_arena.hip)
+  ArenaPack pack{};
 };
 
 namespace {
+// The block rule's slots of struct si's members (by-value structs flattened):
+// lists / sets of scalars; false when the schema holds anything else in a
+// container (a map, strings or structs as elements), a boxed member, or more
+// than kPackSlots lists (thrift_oracle.cpp block_pack_slots restates it).
+bool block_pack_slots(const tgpu_schema& s, uint32_t si, uint32_t base, ArenaPack& p, int depth) {
+  if (depth > 64) return false;
+  const tgpu_struct_desc& sd = s.structs[si];
+  for (uint32_t k = 0; k < sd.num_fields; ++k) {
+    const tgpu_field_desc& f = s.fields[sd.first_field + k];
+    if (f.qualifier == TGPU_BOXED || f.qualifier == TGPU_OPTIONAL_BOXED) return false;
+    if (f.ttype == TGPU_T_STRUCT) {
+      if (!block_pack_slots(s, (uint32_t)f.struct_index, base + f.member_offset, p, depth + 1))
+        return false;
+    } else if (f.ttype == TGPU_T_MAP) {
+      return false;
+    } else if (f.ttype == TGPU_T_LIST || f.ttype == TGPU_T_SET) {
+      uint32_t es;
+      switch (f.elem_ttype) {
+        case TGPU_T_BOOL: case TGPU_T_BYTE: es = 1; break;
+        case TGPU_T_I16: es = 2; break;
+        case TGPU_T_I32: case TGPU_T_FLOAT: es = 4; break;
+        case TGPU_T_I64: case TGPU_T_DOUBLE: es = 8; break;
+        default: return false;
+      }
+      if (p.n == kPackSlots) return false;
+      p.member[p.n] = base + f.member_offset;
+      p.es[p.n] = es;
+      ++p.n;
+    }
+  }
+  return true;
+}
+
 int proto_slot(int protocol) { return protocol == TGPU_PROTOCOL_BINARY ? 0 : protocol == TGPU_PROTOCOL_COMPACT ? 1 : 2; }
 
 void learn_mean(const tgpu_schema* s, int protocol, uint64_t bytes, uint64_t n) {
@@ -142,10 +177,15 @@ struct tgpu_context {
   // the single-pass transcoder's look-back status words (tiles + 1)
   uint8_t* d_xstat = nullptr;
   uint64_t xstat_bytes = 0;
+  // the block rule: per-block marks of the blocks the decode tiles packed
+  // (reserved / kArenaBlock + 1 words), and the last call's epoch
+  uint32_t* d_pack_flags = nullptr;
+  uint32_t pack_epoch = 0;
 };
 
 namespace tgpu {
 bool schema_has_lists(const tgpu_schema* s) { return s->has_lists; }
+bool schema_block_rule(const tgpu_schema* s) { return s->pack.n > 0; }
 
 bool valid_protocol(int p) {
   return p == TGPU_PROTOCOL_BINARY || p == TGPU_PROTOCOL_COMPACT || p == TGPU_PROTOCOL_COMPACT_V1;
@@ -1142,8 +1182,43 @@ int ensure_workspace(tgpu_context* ctx, uint64_t n) {
   if (hipMalloc(&ctx->d_irr, want * sizeof(uint64_t)) != hipSuccess) return TGPU_ERR_HIP;
   if (hipMalloc(&ctx->d_deep, want * sizeof(uint64_t)) != hipSuccess) return TGPU_ERR_HIP;
   if (hipMalloc(&ctx->d_deep2, want * sizeof(uint64_t)) != hipSuccess) return TGPU_ERR_HIP;
+  // the block rule's per-block marks (compared with the call's epoch: never
+  // cleared, zeroed once here)
+  if (ctx->d_pack_flags) (void)hipFree(ctx->d_pack_flags);
+  ctx->d_pack_flags = nullptr;
+  const uint64_t blocks = (want + kArenaBlock - 1) / kArenaBlock + 1;
+  if (hipMalloc(&ctx->d_pack_flags, blocks * sizeof(uint32_t)) != hipSuccess ||
+      hipMemset(ctx->d_pack_flags, 0, blocks * sizeof(uint32_t)) != hipSuccess)
+    return TGPU_ERR_HIP;
   ctx->reserved = want;
   return TGPU_OK;
+}
+
+// A decode call of a block-rule schema: its epoch and marks (DecodeArgs
+// pack_*), the program's list ops for the compiled decode tile's table.
+void pack_args(tgpu_context* ctx, const tgpu_schema* schema, int protocol, DecodeArgs& a) {
+  a.pack_flags = nullptr;
+  a.pack_k = 0;
+  if (!schema->pack.n || !a.arena) return;
+  // (A/B only: TGPU_ARENA_PACK=0 keeps the position rule — the spans then
+  // differ from the oracle's)
+  if (const char* v = getenv("TGPU_ARENA_PACK"))
+    if (v[0] == '0') return;
+  if (++ctx->pack_epoch == 0) ++ctx->pack_epoch;  // (0: the flags' initial value)
+  a.pack_flags = ctx->d_pack_flags;
+  a.pack_epoch = ctx->pack_epoch;
+  const int q = prog_protocol(schema, protocol);
+  if (protocol == TGPU_PROTOCOL_BINARY && q >= 0 && schema->has_prog[q])
+    a.pack_k = prog_list_ops(schema->prog[q]);
+}
+
+// After a decode call's finish kernel: the blocks the decode did not pack.
+hipError_t finish_pack(const tgpu_schema* schema, int protocol, const DecodeArgs& a,
+                       hipStream_t s) {
+  if (!a.pack_flags) return hipSuccess;
+  ArenaPack p = schema->pack;
+  p.scale = protocol == TGPU_PROTOCOL_BINARY ? 1u : 8u;
+  return launch_arena_pack(a, p, s);
 }
 
 // Frames for the deep pass: max_depth + 2 skip frames and as many record
@@ -1783,6 +1858,9 @@ int tgpu_schema_create_ex(const tgpu_struct_desc* structs, uint32_t n_structs,
   };
   for (uint32_t k = 0; k < n_fields; ++k) note(fields[k].ttype, fields[k].elem_ttype, fields[k].val_ttype);
   for (uint32_t k = 0; k < n_types; ++k) note(types[k].ttype, types[k].elem_ttype, types[k].val_ttype);
+  // the block rule (ArenaPack): flat-list schemas only
+  if (!s->nested && !s->str_elems && s->has_lists && !block_pack_slots(*s, 0, 0, s->pack, 0))
+    s->pack.n = 0;
   if (n_types && (hipMalloc(&s->d_types, sizeof(tgpu_type_desc) * n_types) != hipSuccess ||
                   hipMemcpy(s->d_types, types, sizeof(tgpu_type_desc) * n_types,
                             hipMemcpyHostToDevice) != hipSuccess)) {
@@ -1993,6 +2071,7 @@ void tgpu_context_destroy(tgpu_context* c) {
   if (c->h_res) (void)hipHostFree(c->h_res);
   if (c->h_words) (void)hipHostFree(c->h_words);
   if (c->d_offs) (void)hipFree(c->d_offs);
+  if (c->d_pack_flags) (void)hipFree(c->d_pack_flags);
   if (c->d_block_sums) (void)hipFree(c->d_block_sums);
   if (c->d_scan_part) (void)hipFree(c->d_scan_part);
   if (c->d_irr) (void)hipFree(c->d_irr);
@@ -2353,6 +2432,7 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
                                     &ctx->d_res->n_irregular, s, tj, schema->device);
     if (e == hipSuccess) e = launch_fixed_stream_finish(a, protocol, fixed, s);
   } else if (n) {
+    pack_args(ctx, schema, protocol, a);
     if (offsets) {
       a.offs = offsets;
     } else {
@@ -2379,6 +2459,7 @@ int tgpu_decode_batch(tgpu_context* ctx, const tgpu_schema* schema, int protocol
       e = launch_indexed_decode(ctx, schema, protocol, a, s);
   }
   if (e == hipSuccess && n) e = launch_decode_finish(a, protocol, fixed, s);
+  if (e == hipSuccess && n && !fixed) e = finish_pack(schema, protocol, a, s);
   ctx->last_op = 1;
   if (e != hipSuccess) {
     fill_status(st, TGPU_ERR_HIP, 0, 0);
@@ -2621,6 +2702,7 @@ int tgpu_decode_stream(tgpu_context* ctx, const tgpu_schema* schema, int protoco
   a.check_index = 0;
   a.res = ctx->d_res;
   a.deep = deep_args(ctx);
+  if (max_records) pack_args(ctx, schema, protocol, a);
   (void)hipGetLastError();  // drop a stale error left by another library
   hipError_t e = launch_result_init(ctx->d_res, 0, s);
   bool fused = false;
@@ -2653,6 +2735,7 @@ int tgpu_decode_stream(tgpu_context* ctx, const tgpu_schema* schema, int protoco
         e = hipMemcpyAsync(ctx->d_res, ctx->h_res, sizeof(DevResult), hipMemcpyHostToDevice, s);
     }
   }
+  if (e == hipSuccess && max_records) e = finish_pack(schema, protocol, a, s);
   ctx->last_op = 3;
   if (e != hipSuccess) {
     fill_status(st, TGPU_ERR_HIP, 0, 0);

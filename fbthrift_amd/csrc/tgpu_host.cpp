@@ -626,6 +626,7 @@ int tgpu_decode_host_chunks_ex(tgpu_context* ctx, const tgpu_schema* schema, int
     return TGPU_ERR_HIP;
   }
   const uint64_t P = (in_len + C - 1) / C;
+  const bool blocks = scale && arena_capacity && schema_block_rule(schema);
   // packed list elements (TGPU_HOST_PACK_LISTS; schemas whose arena holds
   // scalar list elements only): each chunk's element arrays at the front of
   // its arena slice, the records' spans pointing there; the chunk's packed
@@ -732,6 +733,22 @@ int tgpu_decode_host_chunks_ex(tgpu_context* ctx, const tgpu_schema* schema, int
     if (rc != TGPU_OK || first != B || last < B || (nk == 0 && end < in_len)) {
       clean = false;  // a record the range cannot end cleanly on: the resident pass
       break;
+    }
+    if (blocks && end < in_len && r0 + nk < n && nk % kArenaBlock) {
+      // the block rule: a piece hands back whole blocks of kArenaBlock
+      // records (its blocks are then the resident pass's, and a fallback's
+      // arena slice starts at a block), the next piece starts at the first
+      // record it did not keep; a range of fewer than one block (records of
+      // over piece / 256 bytes) is decoded again with the next piece added
+      if (nk < kArenaBlock) {
+        ++k;
+        continue;
+      }
+      nk -= nk % kArenaBlock;
+      if (hipMemcpy(&last, (uint64_t*)doffs.p + r0 + nk, 8, hipMemcpyDeviceToHost) != hipSuccess) {
+        clean = false;
+        break;
+      }
     }
     if (nk) {
       if (pack) {

@@ -252,6 +252,24 @@ struct VProgram {
   VOp ops[kMaxNestedOps];
 };
 
+// Block rule (round 6; thrift_gpu.h tgpu_schema_arena_scale): the list / set
+// element arrays of a flat-list schema (containers: lists / sets of scalars
+// only, at most kPackSlots counting by-value struct members, nothing nested
+// or boxed) are packed per block of kArenaBlock records: records in order, a
+// record's arrays in wire order, each 8-byte aligned, from align8(scale x the
+// wire start of the block's first record). Decoders write the position rule
+// (scale x an array's wire position) and arena_pack_kernel (k_arena.hip)
+// moves the blocks a fast path has not packed already (DecodeArgs pack_flags:
+// the compiled Binary decode tile packs each wave's block and marks it).
+constexpr uint32_t kArenaBlock = 64;  // (one wave's records in the decode tile)
+constexpr uint32_t kPackSlots = 8;
+struct ArenaPack {
+  uint32_t n;      // slots (0: the schema keeps the position rule)
+  uint32_t scale;  // arena bytes per wire byte (1 Binary, 8 Compact)
+  uint32_t member[kPackSlots];  // span offset in the record
+  uint32_t es[kPackSlots];      // element bytes
+};
+
 // Device-side result slot of a context (one per in-flight call).
 struct DevResult {
   unsigned long long first_fail;       // first failing record (UINT64_MAX: none)
@@ -306,6 +324,12 @@ struct DecodeArgs {
   // records actually present (device word, e.g. the stream index's total):
   // records [min(n, *n_dev), n) are left alone; nullptr: all n
   const unsigned long long* n_dev;
+  // block rule (ArenaPack): a block packed by the decode tile is marked with
+  // pack_epoch (nullptr: the call does not pack); pack_k = the program's list
+  // ops (the compiled decode tile packs only when they are its own)
+  uint32_t* pack_flags;
+  uint32_t pack_epoch;
+  uint32_t pack_k;
 };
 
 // Schemaless skim of an indexed stream (k_skim.hip, tgpu_skim_batch).
@@ -576,6 +600,16 @@ hipError_t jit_launch_index(const JitKernels* J, int which, const IndexArgs& a, 
                             hipStream_t s);
 
 // jit: the schema's compiled kernels (nullptr: interpret d_prog).
+// VOP_LIST ops of a flat program (the compiled decode tile's block-rule
+// table: prog_list_ops x 8 bytes per record).
+inline uint32_t prog_list_ops(const VProgram& P) {
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < P.n_ops; ++i) k += P.ops[i].kind == VOP_LIST ? 1u : 0u;
+  return k;
+}
+// Block rule: blocks of records [0, m) (m from the finished call's DevResult:
+// n_records, + 1 for a failing record) not marked by the decode (k_arena.hip).
+hipError_t launch_arena_pack(const DecodeArgs& a, const ArenaPack& p, hipStream_t stream);
 hipError_t launch_program_decode(const DecodeArgs& a, const VProgram* d_prog,
                                  uint32_t rec_size, uint64_t* irregular,
                                  unsigned long long* n_irregular, hipStream_t stream,
@@ -637,6 +671,8 @@ void* context_host_pipe(tgpu_context* ctx);  // created on first use, owned by c
 uint32_t packable_lists(const tgpu_schema* s, int protocol, uint32_t* member, uint32_t* width,
                         uint32_t max);
 bool schema_has_lists(const tgpu_schema* schema);
+// the schema's list arrays follow the block rule (ArenaPack n > 0)
+bool schema_block_rule(const tgpu_schema* schema);
 
 // ---- stream indexer (k_index.hip) launchers
 // mean: the stream's mean record length when known (0: not), program-less

@@ -298,6 +298,7 @@ void gen_code(std::ostringstream& o, const VProgram& P, uint32_t k, uint32_t sto
 // A program as compile-time constants: the op array `arr` and the program
 // accessor `name` (tgpu_program.h's DynProg interface, kStatic).
 void gen_prog(std::ostringstream& o, const VProgram& P, const char* arr, const char* name) {
+  // (kLists: the block rule's table in the decode tile, decode_tile pack_tile)
   o << "__device__ constexpr tgpu::VOp " << arr << "[" << (P.n_ops ? P.n_ops : 1) << "] = {\n";
   for (uint32_t k = 0; k < P.n_ops; ++k) {
     const VOp& v = P.ops[k];
@@ -314,6 +315,9 @@ void gen_prog(std::ostringstream& o, const VProgram& P, const char* arr, const c
        "  static constexpr bool kStatic = true;\n"
        "  static constexpr uint32_t kN = "
     << P.n_ops
+    << ";\n"
+       "  static constexpr uint32_t kLists = "
+    << prog_list_ops(P)
     << ";\n"
        "  __device__ static constexpr uint32_t n_ops() { return kN; }\n"
        "  __device__ static constexpr uint32_t protocol() { return "
@@ -446,6 +450,7 @@ std::string gen_source(const VProgram& P, int group) {
          "struct NP {\n"
          "  static constexpr bool kStatic = true;\n"
          "  static constexpr uint32_t kN = 2;\n"
+         "  static constexpr uint32_t kLists = 0;\n"
          "  __device__ static constexpr uint32_t n_ops() { return kN; }\n"
          "  __device__ static constexpr uint32_t protocol() { return "
       << P.protocol

@@ -71,6 +71,133 @@ __device__ __forceinline__ unsigned long long block_exscan256(unsigned long long
 __host__ __device__ __forceinline__ uint32_t decode_wire_region(uint32_t wire_cap) {
   return (wire_cap + 32 + 16 * kPT - 1) / (16 * kPT) * (16 * kPT);  // whole staging rounds
 }
+// Bytes of the LDS record tile (decode_tile without kRS).
+__host__ __device__ __forceinline__ uint32_t decode_rtile_bytes(uint32_t S) {
+  return (kPT * S + 16 + 15) & ~15u;
+}
+template <uint32_t kRS>
+__device__ __forceinline__ void store_reg_record(uint8_t* go, const uint8_t* rbuf,
+                                                 const uint8_t* recs) {
+#ifndef TGPU_RR_STORE8
+  if constexpr (kRS % 16 == 0) {
+    if (((uintptr_t)recs & 15) == 0) {  // whole 16-byte words (S 64: a record = 4 stores)
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+      for (uint32_t b = 0; b < kRS; b += 16) *(u32x4*)(go + b) = *(const u32x4*)(rbuf + b);
+      return;
+    }
+  }
+#endif
+  if (((uintptr_t)recs & 7) == 0) {  // (the batch's records: 8- or 4-byte aligned)
+#pragma unroll
+    for (uint32_t b = 0; b < kRS; b += 8) *(uint64_t*)(go + b) = *(const uint64_t*)(rbuf + b);
+  } else {
+#pragma unroll
+    for (uint32_t b = 0; b < kRS; b += 4) *(uint32_t*)(go + b) = *(const uint32_t*)(rbuf + b);
+  }
+}
+
+// The block rule in a compiled Binary decode tile (kArenaBlock = 64: a
+// block is one wave's records). The wave's records took the program (else it
+// returns false and the wave keeps the position rule): their list elements
+// sit converted in the LDS wire tile, inside the wave's own wire bytes. Each
+// lane takes its arrays' bytes into registers (8-byte words, at most
+// kPackWords per record, else false), the wave's exclusive scan gives each
+// record its packed offset, the lanes write their words back into the
+// wave's wire range at the packed image's position (an array never moves
+// up, and every read of the wave precedes its writes: no other wave reads
+// these bytes), and the wave stores the image with 16-byte vectors, whole
+// lines of the arena — the element bytes only, 32 B / record on config 4
+// against 89 for the position rule's converted wire tile. Spans rewritten.
+// (Measured and dropped, round 6: a block of 256 records with a block scan,
+// the lanes storing their own arrays with 8-byte stores — 1.92 ms against
+// 1.69 for the position rule on config 4, the scattered stores cost 0.39
+// ms; the same with whole vectors gathered through a binary search of an
+// LDS array table — 1.82 ms.)
+constexpr uint32_t kPackWords = 8;  // 64 bytes of arrays per record (config 4: 16 x i32)
+template <class PP, uint32_t kK>
+__device__ __forceinline__ bool pack_wave(const DecodeArgs& a, const PP& P, uint8_t* rec,
+                                          bool lane_ok, uint64_t rstart, uint64_t t0,
+                                          uint32_t sh, uint8_t* wire) {
+  const bool active = rec != nullptr;
+  if (__ballot(active && !lane_ok)) return false;  // (wave-uniform)
+  const uint64_t act = __ballot(active);
+  if (!act) return true;
+  uint32_t o[kK > 0 ? kK : 1], by[kK > 0 ? kK : 1], ps[kK > 0 ? kK : 1];
+  uint32_t size = 0;
+  {
+    uint32_t k = 0;
+    all_ops(P, [&](const VOp op) {
+      if (op.kind == VOP_LIST) {
+        const tgpu_span sp = active ? *(const tgpu_span*)(rec + op.member) : tgpu_span{0, 0, 0};
+        by[k] = sp.length * op.width;
+        ps[k] = by[k] ? (uint32_t)(sp.offset - (t0 - sh)) : 0u;  // LDS position
+        o[k] = size;
+        size += (by[k] + 7) & ~7u;
+        ++k;
+      }
+      return true;
+    });
+  }
+  if (__ballot(size > 8 * kPackWords)) return false;
+  const uint64_t incl = wave_incl_scan(size);
+  const uint32_t pre = (uint32_t)(incl - size);
+  const uint32_t wsize = (uint32_t)__shfl(incl, 63, 64);
+  const uint64_t base = (__shfl(rstart, 0, 64) + 7) & ~7ull;  // align8(scale x start), scale 1
+  if (base + wsize > a.arena_cap) return false;
+  // the lane's packed words: word j is array k's bytes from 8j - o[k]
+  const LdsSrc src{(const uint32_t*)wire};
+  uint64_t w[kPackWords];
+#pragma unroll
+  for (uint32_t j = 0; j < kPackWords; ++j) {
+    uint32_t from = 0;
+    bool have = false;
+#pragma unroll
+    for (uint32_t k = 0; k < kK; ++k)
+      if (8 * j >= o[k] && 8 * j < o[k] + by[k]) from = ps[k] + 8 * j - o[k], have = true;
+    w[j] = have ? src.win8(from) : 0ull;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+  // the image: LDS position q <-> arena offset (t0 - sh) + q (the staging's
+  // congruence: both 16-byte aligned at q = 0), so 8-byte aligned
+  const uint32_t q0 = (uint32_t)(base - (t0 - sh));
+#pragma unroll
+  for (uint32_t j = 0; j < kPackWords; ++j)
+    if (8 * j < size) *(uint64_t*)(wire + q0 + pre + 8 * j) = w[j];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+  // LDS [q0, q0 + wsize) -> arena [base, base + wsize): 16-byte vectors, the
+  // edge halves as 8-byte stores
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t v0 = q0 >> 4, v1 = (q0 + wsize + 15) >> 4;
+  uint8_t* gb = a.arena + (t0 - sh);  // LDS position 0's arena address (16-byte aligned)
+  for (uint32_t v = v0 + lane; v < v1; v += 64) {
+    const uint32_t lo = v << 4, hi = lo + 16;
+    if (lo >= q0 && hi <= q0 + wsize) {
+      __builtin_nontemporal_store(((const u32x4*)wire)[v], (u32x4*)gb + v);
+    } else {
+      if (lo >= q0) ((uint64_t*)gb)[2 * v] = ((const uint64_t*)wire)[2 * v];
+      if (hi <= q0 + wsize) ((uint64_t*)gb)[2 * v + 1] = ((const uint64_t*)wire)[2 * v + 1];
+    }
+  }
+  if (active) {
+    uint32_t k = 0;
+    all_ops(P, [&](const VOp op) {
+      if (op.kind == VOP_LIST) {
+        tgpu_span* sp = (tgpu_span*)(rec + op.member);
+        sp->offset = by[k] ? base + pre + o[k] : 0;
+        ++k;
+      }
+      return true;
+    });
+  }
+  return true;
+}
+
 // kTail: the stream-ordered fixed-layout tail (DevResult tail_*): records
 // r0.. of the tile at pos + (i - first) * stride; their offsets are written,
 // a record not taken is listed (wave-aggregated atomics: a wrong stride
@@ -137,9 +264,18 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
   const bool stage_lists = P.has_lists() && P.protocol() == TGPU_PROTOCOL_BINARY && tile_ok &&
                            a.arena && t1 <= a.arena_cap &&
                            (((uintptr_t)a.arena - (uintptr_t)a.in) & 15) == 0;
+  // Block rule (round 6, ArenaPack): a compiled Binary program packs the
+  // element arrays itself, each wave its block of kArenaBlock records
+  // (pack_wave) when all of them took the program; otherwise the wave keeps
+  // the position rule and arena_pack_kernel packs its block later.
+  constexpr uint32_t kK = (PP::kStatic && !kTail) ? PP::kLists : 0;
+  static_assert(kArenaBlock == 64 && kPT % kArenaBlock == 0, "an arena block is one wave's records");
+  const bool pack_on = kK > 0 && kK <= kPackSlots && stage_lists && !L && a.pack_flags &&
+                       a.pack_k == kK && ((uintptr_t)a.arena & 7) == 0;
   const uint32_t r = threadIdx.x;
   bool failed = false;
-  alignas(8) uint8_t rbuf[kRS ? kRS : 8];
+  bool lane_ok = true;
+  alignas(16) uint8_t rbuf[kRS ? kRS : 8];
   if (r < nrec) {
     uint8_t* rec = kRS ? rbuf : rtile + osh + r * S;
     if constexpr (kRS != 0) {
@@ -159,15 +295,10 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
         ok = run_program<true>(P, src, c, p, pe, rec) && p == pe;
       }
     }
-    if constexpr (kRS != 0) {  // (the batch's records: 8- or 4-byte aligned)
-      uint8_t* go = gout + (uint64_t)r * kRS;
-      if (((uintptr_t)a.recs & 7) == 0) {
-#pragma unroll
-        for (uint32_t b = 0; b < kRS; b += 8) *(uint64_t*)(go + b) = *(const uint64_t*)(rbuf + b);
-      } else {
-#pragma unroll
-        for (uint32_t b = 0; b < kRS; b += 4) *(uint32_t*)(go + b) = *(const uint32_t*)(rbuf + b);
-      }
+    lane_ok = ok;
+    // (pack mode stores the register record once its spans are final)
+    if constexpr (kRS != 0) {
+      if (!pack_on) store_reg_record<kRS>(gout + (uint64_t)r * kRS, rbuf, a.recs);
     }
     if constexpr (kTail) {
       failed = !ok;
@@ -199,7 +330,46 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
     }
   }
   __syncthreads();
-  if (stage_lists) {  // converted wire tile -> arena [t0, t1), coalesced
+  bool packed = false;  // (the tile's arena bytes are written: skip the tile copy)
+  if constexpr (kK > 0) {
+    if (pack_on) {
+      // each wave its own block (kArenaBlock = 64 records): packed, or its
+      // converted wire range as the position rule has it
+      const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+      const uint64_t rs = r < nrec ? a.offs[r0 + r] : 0;
+      uint8_t* rec = r < nrec ? (kRS ? rbuf : rtile + osh + r * S) : nullptr;
+      const bool wpacked = pack_wave<PP, kK>(a, P, rec, lane_ok, rs, t0, sh, wire);
+      if constexpr (kRS != 0) {
+        if (r < nrec) store_reg_record<kRS>(gout + (uint64_t)r * kRS, rbuf, a.recs);
+      }
+      const uint32_t wr0 = wv * 64;
+      if (wr0 < nrec) {
+        if (wpacked) {
+          if (lane == 0) a.pack_flags[(r0 >> 6) + wv] = a.pack_epoch;
+        } else {
+          // the wave's records' bytes [offs[wr0], offs[wr1]) of the converted
+          // tile -> arena, 16-byte vectors (byte stores on the edges shared
+          // with the neighbouring waves)
+          const uint32_t wr1 = min(nrec, wr0 + 64);
+          const uint32_t lo_b = (uint32_t)(a.offs[r0 + wr0] - t0) + sh;
+          const uint32_t hi_b = (uint32_t)(a.offs[r0 + wr1] - t0) + sh;
+          uint8_t* ab = a.arena + t0 - sh;
+          for (uint32_t i = (lo_b >> 4) + lane; i < ((hi_b + 15) >> 4); i += 64) {
+            const uint32_t lo = i << 4, hi = lo + 16;
+            if (lo >= lo_b && hi <= hi_b) {
+              ((uint4*)ab)[i] = ((const uint4*)wire)[i];
+            } else {
+              for (uint32_t b = (lo < lo_b ? lo_b : lo); b < (hi < hi_b ? hi : hi_b); ++b)
+                ab[b] = wire[b];
+            }
+          }
+        }
+      }
+      packed = true;
+      if constexpr (kRS != 0) return;
+    }
+  }
+  if (stage_lists && !packed) {  // converted wire tile -> arena [t0, t1), coalesced
     const uint32_t wend = sh + (uint32_t)(t1 - t0);
     uint8_t* ab = a.arena + t0 - sh;
     for (uint32_t i = threadIdx.x; i < ((wend + 15) >> 4); i += kPT) {

@@ -128,6 +128,7 @@ __device__ __forceinline__ void lds_dma_settle(const uint8_t* lds, uint32_t firs
 struct DynProg {
   static constexpr bool kStatic = false;
   static constexpr uint32_t kN = 0;
+  static constexpr uint32_t kLists = 0;  // (the block rule's packing tile: compiled programs only)
   const VProgram* __restrict__ p;
   __device__ __forceinline__ uint32_t n_ops() const { return p->n_ops; }
   __device__ __forceinline__ uint32_t protocol() const { return p->protocol; }

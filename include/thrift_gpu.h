@@ -328,7 +328,20 @@ uint32_t tgpu_schema_record_size(const tgpu_schema* schema);
  * containers into a region of its own, scale x [record start, record end)
  * of the arena, allocated in wire order (8-byte aligned); its scale bounds
  * element bytes per wire byte (e.g. sizeof(struct) for a list of structs,
- * as an element struct can be a single STOP byte on the wire). */
+ * as an element struct can be a single STOP byte on the wire).
+ * Where arrays go (the records' spans say it; other arena bytes are
+ * unspecified):
+ *  - flat-list schemas (every container a list or set of scalars, at most
+ *    8 of them per record counting by-value struct members; no maps, no
+ *    strings in containers, nothing boxed): the BLOCK RULE. Records are
+ *    grouped by index in blocks of 64; block b's arrays are dense, back to
+ *    back in read order (records in order, a record's arrays in wire
+ *    order), each 8-byte aligned, from align8(scale x the wire start of
+ *    record 64 b) — the elements of a list are one contiguous array, as the
+ *    reference's std::vector is, and the block's arrays fit the wire bytes
+ *    it came from (x scale);
+ *  - other schemas without regions: each array at scale x the wire
+ *    position of its first element (the position rule). */
 uint32_t tgpu_schema_arena_scale(const tgpu_schema* schema, int protocol);
 
 /* Canonical wire length of every record if it is fixed for `protocol`
@@ -537,7 +550,9 @@ int tgpu_encode_host_ex(tgpu_context* ctx, const tgpu_schema* schema, int protoc
  * finished range of records [r0, r1) is announced through on_chunk (may be
  * NULL) while later chunks are still moving, so a caller can materialize
  * them meanwhile (host_records / host_arena as for tgpu_decode_host_ex; the
- * arena slice of a range is arena_scale x its wire bytes). Any chunk that
+ * arena slice of a range is arena_scale x its wire bytes; under the block
+ * rule a range is whole blocks of 64 records, so the arena is exactly
+ * tgpu_decode_host_ex's). Any chunk that
  * does not finish cleanly (a malformed record, more records than
  * n_records, a record longer than a piece) sends the whole batch through
  * the resident pass, so results and status are exactly

@@ -938,6 +938,89 @@ void init_record(const Schema& sc, uint8_t* rec) {
   std::memset(rec, 0, sc.s[0].size);  // default-constructed T (zero defaults)
 }
 
+// ---- block rule (round 6): list / set elements of flat-list schemas --------
+// A schema whose containers are all lists / sets of scalars (no maps, no
+// strings or structs or containers as elements, nothing boxed: not a nested
+// schema), at most kPackSlots of them counting those inside by-value struct
+// members, keeps no per-record arena regions: records are grouped by index
+// in blocks of kArenaBlock, and block b's element arrays are allocated in
+// read order (records in order, a record's arrays in wire order), each
+// 8-byte aligned, from align8(scale x the wire start of the block's first
+// record). Every array then is the dense std::vector the reference's
+// readArithmeticVector fills (protocol_methods.h:390-441), and a block's
+// arrays fit the bytes its wire took (an array's 8 header bytes hold its
+// padding). Restated here as a pass over the position-rule arena (each array
+// moves down: its packed start is never above its wire position x scale).
+constexpr uint32_t kArenaBlock = 64;
+constexpr uint32_t kPackSlots = 8;
+struct PackSlot {
+  uint32_t member, es;
+};
+bool pack_slots_of(const Schema& sc, uint32_t si, uint32_t base, std::vector<PackSlot>& out,
+                   int depth) {
+  if (depth > 64) return false;
+  const tgpu_struct_desc& sd = sc.s[si];
+  for (uint32_t k = 0; k < sd.num_fields; ++k) {
+    const tgpu_field_desc& f = sc.f[sd.first_field + k];
+    if (is_boxed(f)) return false;
+    if (f.ttype == TGPU_T_STRUCT) {
+      if (!pack_slots_of(sc, (uint32_t)f.struct_index, base + f.member_offset, out, depth + 1))
+        return false;
+    } else if (f.ttype == TGPU_T_MAP) {
+      return false;
+    } else if (is_container_t(f.ttype)) {
+      if (!is_scalar(f.elem_ttype)) return false;
+      out.push_back(PackSlot{base + f.member_offset, scalar_size(f.elem_ttype)});
+    }
+  }
+  return true;
+}
+// The slots of a block-packed schema (empty: the position rule applies).
+std::vector<PackSlot> block_pack_slots(const Schema& sc) {
+  std::vector<PackSlot> v;
+  if (nested_schema(sc) || has_string_elems(sc) || !pack_slots_of(sc, 0, 0, v, 0) ||
+      v.size() > kPackSlots)
+    v.clear();
+  return v;
+}
+// Records [0, m) (the failing record included) from the position rule to the
+// block rule: bytes moved in place in increasing order (a byte's destination
+// never lies above its source, nor above a later byte's source); a source
+// byte past the arena's end (a failing record's list resized past it) reads
+// as zero, a destination past it is not written.
+void pack_blocks(const Schema& sc, const std::vector<PackSlot>& slots, const uint64_t* starts,
+                 uint64_t m, uint8_t* recs, uint8_t* arena, uint64_t cap, uint64_t scale) {
+  const uint32_t rs = sc.s[0].size;
+  for (uint64_t b0 = 0; b0 < m; b0 += kArenaBlock) {
+    uint64_t cur = (scale * starts[b0] + 7) & ~7ull;
+    const uint64_t b1 = std::min<uint64_t>(m, b0 + kArenaBlock);
+    for (uint64_t i = b0; i < b1; ++i) {
+      uint8_t* rec = recs + i * rs;
+      std::vector<std::pair<uint64_t, uint32_t>> order;  // (source, slot) of the non-empty arrays
+      for (uint32_t k = 0; k < slots.size(); ++k) {
+        tgpu_span sp;
+        std::memcpy(&sp, rec + slots[k].member, sizeof(sp));
+        if (sp.length) order.emplace_back(sp.offset, k);
+      }
+      std::sort(order.begin(), order.end());
+      for (const auto& o : order) {
+        tgpu_span sp;
+        std::memcpy(&sp, rec + slots[o.second].member, sizeof(sp));
+        const uint64_t bytes = (uint64_t)sp.length * slots[o.second].es;
+        cur = (cur + 7) & ~7ull;
+        if (arena)
+          for (uint64_t t = 0; t < bytes; ++t) {
+            const uint64_t d = cur + t, src = sp.offset + t;
+            if (d < cap) arena[d] = src < cap ? arena[src] : 0;
+          }
+        sp.offset = cur;
+        std::memcpy(rec + slots[o.second].member, &sp, sizeof(sp));
+        cur += bytes;
+      }
+    }
+  }
+}
+
 template <class R>
 int decode_impl(const Schema& sc, const uint8_t* in, uint64_t in_len,
                 const uint64_t* offsets, uint64_t n, uint8_t* recs,
@@ -951,10 +1034,16 @@ int decode_impl(const Schema& sc, const uint8_t* in, uint64_t in_len,
   }
   uint64_t pos = offsets ? offsets[0] : 0;
   const uint32_t rs = sc.s[0].size;
+  const std::vector<PackSlot> slots = dc.regions ? std::vector<PackSlot>() : block_pack_slots(sc);
+  std::vector<uint64_t> starts;
+  auto pack = [&](uint64_t m) {
+    if (!slots.empty() && m) pack_blocks(sc, slots, starts.data(), m, recs, arena, arena_cap, dc.scale);
+  };
   for (uint64_t i = 0; i < n; ++i) {
     uint8_t* rec = recs + i * rs;
     init_record(sc, rec);
     const uint64_t start = offsets ? offsets[i] : pos;
+    if (!slots.empty()) starts.push_back(start);
     R r;
     r.c = Cursor{in, start, in_len};
     r.lim = lim;
@@ -963,12 +1052,14 @@ int decode_impl(const Schema& sc, const uint8_t* in, uint64_t in_len,
     try {
       readStruct(r, 0, rec, dc);
     } catch (const OErr& e) {
+      pack(i + 1);
       set_status(st, e.code, i, e.off);
       if (n_dec) *n_dec = i;
       if (consumed) *consumed = start - (offsets ? offsets[0] : 0);
       return e.code;
     }
     if (offsets && r.c.pos != offsets[i + 1]) {
+      pack(i + 1);
       set_status(st, TGPU_ERR_INDEX_MISMATCH, i, r.c.pos);
       if (n_dec) *n_dec = i;
       if (consumed) *consumed = start - offsets[0];
@@ -976,6 +1067,7 @@ int decode_impl(const Schema& sc, const uint8_t* in, uint64_t in_len,
     }
     pos = r.c.pos;
   }
+  pack(n);
   set_status(st, TGPU_OK, n, 0);
   if (n_dec) *n_dec = n;
   if (consumed) *consumed = pos - (offsets ? offsets[0] : 0);
@@ -1771,8 +1863,11 @@ int oracle_mixed_compact_size(const void* records, uint64_t n, uint64_t* sizes,
 // / readNoXfer fast path (advanceToNextField, BinaryProtocol-inl.h:586-621;
 // readListBegin + readArithmeticVector, BinaryProtocol.cpp:49-72; nested
 // struct via beforeSubobject/afterSubobject) restated for this one schema.
-// List elements decode to an arena at their wire position (the device's
-// layout: scale 1 Binary), natively little-endian.
+// List elements decode natively little-endian into the arena under the
+// device's block rule (scale 1 Binary): blocks of kArenaBlock records, each
+// block's lists back to back (8-byte aligned) from align8(its first wire
+// byte) — each block read by one thread in record order, the arrays written
+// where they belong (no move).
 namespace {
 inline void nested_write(Sink& s, const uint8_t* r, const uint8_t* lb) {
   s.put(TGPU_T_I64); s.putBE(1, 2); s.putBE(ld<uint64_t>(r), 8);
@@ -1827,8 +1922,10 @@ int oracle_nested_binary_decode(const void* in, const uint64_t* offsets, uint64_
   auto hdr = [](const uint8_t* q, uint8_t t, int id) {
     return q[0] == t && q[1] == 0 && q[2] == (uint8_t)id;
   };
-  parallel_for(n, n_threads, [&](uint64_t b, uint64_t e) {
-    for (uint64_t i = b; i < e; ++i) {
+  const uint64_t nb = (n + kArenaBlock - 1) / kArenaBlock;
+  parallel_for(nb, n_threads, [&](uint64_t bb, uint64_t be) {
+    for (uint64_t i = bb * kArenaBlock, cur = 0; i < std::min(n, be * kArenaBlock); ++i) {
+      if (i % kArenaBlock == 0) cur = (offsets[i] + 7) & ~7ull;  // the block's arrays
       uint8_t* o = out + i * 64;
       std::memset(o, 0, 64);
       uint64_t pos = offsets[i];
@@ -1850,10 +1947,11 @@ int oracle_nested_binary_decode(const void* in, const uint64_t* offsets, uint64_
         uint32_t x;
         std::memcpy(&x, p + pos + 4 * k, 4);
         x = __builtin_bswap32(x);
-        std::memcpy(ar + pos + 4 * k, &x, 4);
+        std::memcpy(ar + cur + 4 * k, &x, 4);
       }
-      const tgpu_span sp{cnt ? pos : 0, cnt, 0};
+      const tgpu_span sp{cnt ? cur : 0, cnt, 0};
       std::memcpy(o + 8, &sp, 16);
+      if (cnt) cur = (cur + 4ull * cnt + 7) & ~7ull;
       o[57] = 1;
       pos += 4ull * cnt;
       if (!hdr(p + pos, TGPU_T_STRUCT, 3)) { rc = TGPU_ERR_UNSUPPORTED; continue; }
