@@ -33,7 +33,7 @@ struct PackEnt {
   unsigned long long bytes;  // array bytes (0: an empty list, after the record's arrays)
 };
 
-constexpr uint32_t kChunk = kArenaBlock * 16;  // packed bytes per read / write round
+constexpr uint32_t kChunk = kArenaBlock * 16;  // packed bytes per read / write round (2 words a lane)
 
 // One block (one wave: a lane per record) moved to the block rule.
 __device__ __forceinline__ void pack_block(const DecodeArgs& a, const ArenaPack& p, uint64_t blk,
@@ -98,10 +98,14 @@ __device__ __forceinline__ void pack_block(const DecodeArgs& a, const ArenaPack&
   const uint32_t M = nrec * K;
   const uint64_t T = total, cap = a.arena_cap;
   uint8_t* ar = a.arena;
+  // whole 8-byte words where the arena allows (an array's packed start is
+  // 8-byte aligned, so a word holds one array's bytes and its padding), each
+  // read as the two aligned words its bytes span; bytes otherwise
+  const bool words = ((uintptr_t)ar & 7) == 0;
   for (uint64_t c = 0; c < T; c += kChunk) {
     const uint64_t j0 = c + 16ull * r;
-    uint8_t v[16];
-    uint32_t valid = 0;
+    uint64_t w[2] = {0, 0};
+    uint32_t nb[2] = {0, 0};  // valid leading bytes of each word (8: whole)
     if (j0 < T) {
       uint32_t lo = 0, hi = M;  // the last entry whose packed offset is <= j0
       while (lo < hi) {
@@ -111,23 +115,36 @@ __device__ __forceinline__ void pack_block(const DecodeArgs& a, const ArenaPack&
       }
       uint32_t e = lo ? lo - 1 : 0;
 #pragma unroll
-      for (uint32_t q = 0; q < 16; ++q) {
-        const uint64_t j = j0 + q;
-        v[q] = 0;
+      for (uint32_t q = 0; q < 2; ++q) {
+        const uint64_t j = j0 + 8 * q;
         if (j >= T) continue;
         while (e + 1 < M && tab[e + 1].d <= j) ++e;
         const uint64_t t = j - tab[e].d;
         if (t >= tab[e].bytes) continue;  // alignment padding: unspecified, not written
+        const uint32_t n = (uint32_t)min((uint64_t)8, tab[e].bytes - t);
         const uint64_t s = tab[e].src + t;
-        v[q] = s < cap ? ar[s] : 0;  // (a failing record's list resized past the arena)
-        valid |= 1u << q;
+        const uint64_t al = s & ~7ull;
+        if (words && al + 16 <= cap) {
+          const uint64_t a0 = *(const uint64_t*)(ar + al), a1 = *(const uint64_t*)(ar + al + 8);
+          const uint32_t sh = (uint32_t)(s & 7) * 8;
+          w[q] = sh ? (a0 >> sh) | (a1 << (64 - sh)) : a0;
+        } else {
+          for (uint32_t b = 0; b < n; ++b)  // (a failing record's list resized past the arena: 0)
+            w[q] |= (uint64_t)(s + b < cap ? ar[s + b] : 0) << (8 * b);
+        }
+        nb[q] = n;
       }
     }
     __syncthreads();  // every source byte of the chunk read
 #pragma unroll
-    for (uint32_t q = 0; q < 16; ++q) {
-      const uint64_t dst = base + j0 + q;
-      if (((valid >> q) & 1) && dst < cap) ar[dst] = v[q];
+    for (uint32_t q = 0; q < 2; ++q) {
+      const uint64_t dst = base + j0 + 8 * q;
+      if (nb[q] == 8 && words && dst + 8 <= cap) {
+        *(uint64_t*)(ar + dst) = w[q];
+      } else {
+        for (uint32_t b = 0; b < nb[q]; ++b)
+          if (dst + b < cap) ar[dst + b] = (uint8_t)(w[q] >> (8 * b));
+      }
     }
     __syncthreads();  // before the next chunk's reads (and the next block's table)
   }
