@@ -404,7 +404,10 @@ class FileShards(Mixed):
                    "all_gather of the range boundaries)")
     name = ("config 5: Compact protocol, {4 x i32, 2 x string[0..32]} file split by bytes "
             "across GPUs, encode + boundary discovery + decode")
-    overlap = 1 << 20
+    # bytes of the next rank's range each rank also holds: the longest record
+    # of the file (a record starting before B_{k+1} ends by B_{k+1} + it),
+    # found at setup from every rank's record index, at least min_overlap
+    min_overlap = 4096
 
     def __init__(self, n, rank, dev):
         super().__init__(n, rank, dev)
@@ -428,7 +431,9 @@ class FileShards(Mixed):
         self.world = self.world_size()
         self.enc = self.wire  # this rank's part of the file (in file order)
         self.enc_offs = self.offs
-        sizes = self._gather([self.wire_bytes])
+        longest = self.longest_record()
+        sizes = self._gather([self.wire_bytes, longest])
+        self.overlap = max(self.min_overlap, max(r[1] for r in sizes))
         self.file_off = sum(r[0] for r in sizes[:rank])
         self.file_len = sum(r[0] for r in sizes)
         self.total_wire_bytes = self.file_len
@@ -445,6 +450,11 @@ class FileShards(Mixed):
         self.idx = torch.empty(self.n * 2 + 2, dtype=torch.int64, device=dev)
         self.back = torch.empty(self.n * 2 * self.record_bytes, dtype=torch.uint8, device=dev)
         self.n_local = 0
+
+    def longest_record(self):
+        """Longest record of this rank's encode output (its record index)."""
+        o = self.enc_offs if getattr(self, "enc_offs", None) is not None else self.offs
+        return int((o[1:] - o[:-1]).max().item()) if self.n else 0
 
     def index_range(self, local, begin, end, speculative):
         """Record starts + records of the records that start in
@@ -738,7 +748,8 @@ def main(argv=None):
         "config": {"workload": wl.name, "records_per_gpu": n, "records_total": n * world, "wire_bytes_per_gpu": wl.wire_bytes,
                    "record_bytes": wl.record_bytes,
                    "wire_bytes_per_record": round(wl.wire_bytes / n, 3),
-                   "parallelism": wl.parallelism % world},
+                   "parallelism": wl.parallelism % world,
+                   **({"overlap_bytes": wl.overlap} if hasattr(wl, "overlap") else {})},
         "roofline": {"bound": "hbm", "kernel": wl.dec_kernel,
                      "achieved": round(dec_alg / dec_avg / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(dec_alg / dec_avg / 1e9 / HBM_PEAK_GBS, 4),

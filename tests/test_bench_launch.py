@@ -31,7 +31,7 @@ def _line(out):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_gpus_flag_launches_ranks(world):
     n = 2000
     r = subprocess.run([sys.executable, os.path.join(HERE, "bench_rehearsal.py"),
@@ -47,6 +47,52 @@ def test_gpus_flag_launches_ranks(world):
     assert "all_to_all_single" in line["config"]["parallelism"]
     # whole-job bytes: the file is every rank's encode output
     assert line["value"] > 0
+    # each rank holds the next range's first bytes up to the file's longest
+    # record (config 3 records: at most 4 x 5 + 2 x (5 + 32) + ... < 128 B)
+    assert 4096 <= line["config"]["overlap_bytes"] <= 1 << 20
+
+
+def test_local_rank_maps_to_its_gpu(monkeypatch):
+    """`bench.py --gpus 8` under torch.distributed.run: rank LOCAL_RANK runs
+    on cuda:LOCAL_RANK (CudaRuntime.setup), one process per GPU."""
+    import torch
+
+    seen = []
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 8)
+    monkeypatch.setattr(torch.cuda, "set_device", lambda d: seen.append(d))
+    rt = bench.CudaRuntime()
+    for local in range(8):
+        assert rt.setup(local) == torch.device("cuda", local)
+    assert seen == list(range(8))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("WORLD_SIZE", "8")
+    monkeypatch.setenv("RANK", "6")
+    monkeypatch.setenv("LOCAL_RANK", "6")
+    world, rank, local = bench.resolve_world(8)
+    assert (world, rank, local) == (8, 6, 6) and rt.setup(local) == torch.device("cuda", 6)
+
+
+def test_overlap_is_the_longest_record():
+    """Config 5's overlap: the longest record of the whole file (every rank's
+    index), so the record straddling a range's end is always held."""
+    import torch
+
+    class W(bench.FileShards):
+        def __init__(self, offs):
+            self.n = len(offs) - 1
+            self.offs = torch.tensor(offs, dtype=torch.int64)
+            self.wire = torch.zeros(int(offs[-1]), dtype=torch.uint8)
+            self.wire_bytes = int(offs[-1])
+            self.record_bytes = 56
+
+        def _gather(self, vals):  # a 3-rank file: the other ranks' longest records
+            return [vals, [100, 9000], [100, 20]]
+
+    w = W([0, 10, 60, 5000, 5010])
+    assert w.longest_record() == 4940
+    w.setup_file(0, torch.device("cpu"))
+    assert w.overlap == 9000 and w.file_len == 5010 + 200
 
 
 def test_world_mismatch_exits_nonzero():

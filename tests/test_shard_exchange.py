@@ -11,11 +11,11 @@ import pytest
 from fbthrift_amd import shard
 
 
-def _layout(seed, n=5000, max_len=400):
+def _layout(seed, n=5000, max_len=400, giant=50_000):
     rng = np.random.default_rng(seed)
     lens = rng.integers(1, max_len, n)
     # a few records longer than a whole range
-    lens[n // 3] = 50_000
+    lens[n // 3] = giant
     return np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
 
 
@@ -70,14 +70,14 @@ def test_resolve_pure():
     assert redo == [3] and confirmed[3] == rows[2][2]
 
 
-def _worker(rank, world, port, seed, lie, q):
+def _worker(rank, world, port, seed, lie, q, giant=50_000):
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        starts = _layout(seed)
+        starts = _layout(seed, giant=giant)
         L = int(starts[-1])
         b, e = shard.byte_ranges(L, world)[rank]
         fi = FakeIndex(starts, lie_ranks=lie, rank=rank)
@@ -103,21 +103,27 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,lie", [(2, (1,)), (4, (1, 2)), (4, ())])
-def test_exchange_gloo(world, lie):
+@pytest.mark.parametrize("world,lie,giant", [(2, (1,), 50_000), (4, (1, 2), 50_000),
+                                             (4, (), 50_000),
+                                             # world 8 (north_star's node): one record
+                                             # over 2+ whole ranges (ranges with no
+                                             # record start), three ranks lying
+                                             (8, (1, 3, 6), 600_000), (8, (), 600_000)])
+def test_exchange_gloo(world, lie, giant):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, 7, lie, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 7, lie, q, giant))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=120) for _ in range(world))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    starts = _layout(7)
+    starts = _layout(7, giant=giant)
     ranges = shard.byte_ranges(int(starts[-1]), world)
     counts = _truth(starts, [r[0] for r in ranges], [r[1] for r in ranges])
     assert [r[1] for r in res] == counts
@@ -125,6 +131,11 @@ def test_exchange_gloo(world, lie):
     assert sum(counts) == len(starts) - 1
     if lie:
         assert max(r[5] for r in res) >= 2
+    if world == 8:
+        # the giant record straddles two or more boundaries: its successors
+        # come after one or more ranges that hold no record start
+        assert counts.count(0) >= 1
+        assert all(r[2] == shard.NONE for r in res if r[1] == 0)
 
 
 # ---- the whole config-5 composition on CPU ranks ---------------------------
@@ -212,7 +223,7 @@ def _composition_worker(rank, world, port, n, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_file_split_composition_gloo(world):
     import hashlib
 
@@ -246,5 +257,8 @@ def test_file_split_composition_gloo(world):
             empty_ranges += 1
             assert first == shard.NONE
     assert sum(r[3] for r in res) == n
-    if world == 4:
+    if world >= 4:
         assert empty_ranges >= 1  # a range inside one giant record took the NONE path
+    if world == 8:
+        # the 150 000-byte record covers more than two of the 8 ranges
+        assert empty_ranges >= 2
