@@ -411,9 +411,15 @@ class FileShards(Mixed):
 
     def __init__(self, n, rank, dev):
         super().__init__(n, rank, dev)
-        # the decode call (tgpu_decode_stream): the index speculation, the
-        # copy of its stored record starts, the indexed program decode
-        self.dec_kernel = ("tgpu_jit_index_spec+index_starts_copy_kernel+tgpu_jit_decode"
+        # the decode call (tgpu_decode_stream): round 6, one pass — the
+        # speculation, the look-back and the record decode in one kernel
+        # (tgpu_jit_index_onepass_rr); TGPU_INDEX_ONEPASS=0 keeps the two
+        # passes (the index speculation, the copy of its stored record starts,
+        # the indexed program decode)
+        two = os.environ.get("TGPU_INDEX_ONEPASS", "") in ("0", "1")
+        self.dec_kernel = ("tgpu_jit_index_onepass_rr" if not two and
+                           self.dec_kernel.startswith("tgpu_jit")
+                           else "tgpu_jit_index_spec+index_starts_copy_kernel+tgpu_jit_decode"
                            if self.dec_kernel.startswith("tgpu_jit")
                            else "index_tile_spec_kernel+index_starts_copy_kernel+"
                                 "program_decode_kernel")

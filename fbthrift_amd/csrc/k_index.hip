@@ -511,6 +511,7 @@ __global__ __launch_bounds__(256) void index_onepass_init_kernel(IndexArgs a) {
     a.ep[j] = 0;
   }
   if (j == 0) {
+    a.scal[0] = 0;  // (tgpu_index_stats: no repairs)
     a.scal[1] = a.n_chunks;
     a.scal[2] = kNo;
     for (int k = 6; k < 12; ++k) a.scal[k] = 0;
@@ -1173,12 +1174,14 @@ hipError_t launch_index_finish(const IndexArgs& a, bool decode, hipStream_t stre
   return hipGetLastError();
 }
 
-hipError_t launch_index_onepass(const IndexArgs& a, hipStream_t stream, const JitKernels* jit) {
+hipError_t launch_index_onepass(const IndexArgs& a, hipStream_t stream, const JitKernels* jit,
+                                bool rr) {
   const uint64_t C = a.n_chunks;
   if (!a.prog || a.chunk != kTile || C == 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(index_onepass_init_kernel, dim3((uint32_t)((C + 255) / 256)), dim3(256), 0,
                      stream, a);
   const bool decode = a.recs != nullptr;
+  if (rr) return jit_launch_index(jit, 5, a, C, stream);  // (the caller checked jit_has)
   if (jit) return jit_launch_index(jit, decode ? 4 : 3, a, C, stream);
   if (decode)
     hipLaunchKernelGGL(index_onepass_kernel<true>, dim3((uint32_t)C), dim3(kTileLanes), 0, stream, a);

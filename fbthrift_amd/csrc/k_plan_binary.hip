@@ -25,6 +25,11 @@
 #include "tgpu_internal.h"
 #include "tgpu_program.h"
 
+#ifdef TGPU_PLAN_STALE_CHECK
+// (diagnostics build) plan-decode value words whose staged copy differed from HBM
+__device__ unsigned long long tgpu_plan_stale_words;
+#endif
+
 namespace tgpu {
 namespace {
 
@@ -356,6 +361,18 @@ __global__ __launch_bounds__(T) void plan_binary_decode_ls_kernel(
       if (kNT) __builtin_nontemporal_store(v, o + (size_t)r * Q + j);
       else o[(size_t)r * Q + j] = v;
       if (!ok) atomicOr(&seen[r >> 5], 1u << (r & 31));
+#ifdef TGPU_PLAN_STALE_CHECK
+      if (r + 1 < nrec) {  // diagnostics: the same
+         // word decoded from HBM (its 16-byte window stays inside the tile);
+         // a stale staged word that keeps its header bytes differs here
+        unsigned long long vg = pw.const_bits;
+        bool okg = true;
+#pragma unroll
+        for (uint32_t m = 0; m < KI; ++m)
+          if (m < nit) vg |= ls_decode_item(it[m], (const uint32_t*)(g - sh), base, okg);
+        if (vg != v || okg != ok) atomicAdd(&tgpu_plan_stale_words, 1ull);
+      }
+#endif
     }
   }
   __syncthreads();
@@ -795,3 +812,18 @@ hipError_t launch_plan_binary_encode(const FixedPlan* p, const FixedPlan* d_p,
 }
 
 }  // namespace tgpu
+
+#ifdef TGPU_PLAN_STALE_CHECK
+// (diagnostics build only: not in thrift_gpu.h) the stale-word counter
+extern "C" unsigned long long tgpu_debug_plan_stale(int reset) {
+  unsigned long long v = 0;
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpyFromSymbol(&v, HIP_SYMBOL(tgpu_plan_stale_words), sizeof(v));
+  if (reset) {
+    const unsigned long long z = 0;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(tgpu_plan_stale_words), &z, sizeof(z));
+  }
+  (void)hipGetLastError();
+  return v;
+}
+#endif

@@ -701,7 +701,8 @@ hipError_t launch_index_finish(const IndexArgs& a, bool decode, hipStream_t stre
 // caller then runs launch_index_stream), else the index's arrays as the
 // two-pass index leaves them before its epilogue (launch_index_finish).
 // Program schemas with kTile chunks only.
-hipError_t launch_index_onepass(const IndexArgs& a, hipStream_t stream, const JitKernels* jit);
+hipError_t launch_index_onepass(const IndexArgs& a, hipStream_t stream, const JitKernels* jit,
+                                bool rr = false);
 // Empty range: offs[0..fill_to] = pos, no records.
 hipError_t launch_index_empty(DevResult* res, uint64_t* offs, uint64_t pos, uint64_t fill_to,
                               hipStream_t stream);

@@ -76,7 +76,7 @@ const char* const kEntry[6][6] = {
     {"tgpu_jit_decode", "tgpu_jit_decode_tail", "tgpu_jit_decode_rr", nullptr, nullptr, nullptr},
     {"tgpu_jit_size", "tgpu_jit_write", nullptr, nullptr, nullptr, nullptr},
     {"tgpu_jit_index_spec", "tgpu_jit_index_emit", "tgpu_jit_index_decode",
-     "tgpu_jit_index_onepass", "tgpu_jit_index_onepass_decode", nullptr},
+     "tgpu_jit_index_onepass", "tgpu_jit_index_onepass_decode", "tgpu_jit_index_onepass_rr"},
     {"tgpu_jit_ndecode", "tgpu_jit_ndecode_hbm", "tgpu_jit_nsize", "tgpu_jit_nwrite", nullptr,
      nullptr},
     {"tgpu_jit_nindex_spec", "tgpu_jit_nindex_emit", nullptr, nullptr, nullptr, nullptr},
@@ -634,6 +634,21 @@ std::string gen_source(const VProgram& P, int group) {
          "  __shared__ prog::OnePassShared op;\n"
          "  prog::index_onepass_tile<true>(a, JP{}, lds, sm, rtile, op);\n"
          "}\n";
+  // the one pass over the candidate-list speculation, records decoded into
+  // registers (config 5: each record parsed once; index_onepass_rr_tile)
+  if (group == JIT_INDEX && decode_regrec(P.rec_size))
+    o << "#ifndef TGPU_OP_WAVES\n#define TGPU_OP_WAVES 7\n#endif\n"
+         "extern \"C\" __global__ __launch_bounds__(256) "
+         "__attribute__((amdgpu_waves_per_eu(TGPU_OP_WAVES, 8))) void tgpu_jit_index_onepass_rr("
+         "IndexArgs a) {\n"
+         "  __shared__ __attribute__((aligned(16))) uint8_t lds[prog::kTileLds];\n"
+         "  __shared__ prog::IndexTileShared sm;\n"
+         "  __shared__ prog::OnePassShared op;\n"
+         "  __shared__ prog::CandResult cr;\n"
+         "  // (the chain's starts in the candidates' length array: the chain\n"
+         "  // writes start k after reading every length it still needs)\n"
+         "  prog::index_onepass_rr_tile<JP, kS>(a, JP{}, lds, sm, op, sm.cl.len, cr);\n"
+         "}\n";
   return o.str();
 }
 
@@ -708,8 +723,10 @@ bool compile_from(const std::string& src, int device, int group, JitKernels& J) 
   for (int k = 0; k < 6 && ok; ++k) {
     if (!kEntry[group][k]) continue;
     ok = hipModuleGetFunction(&J.f[k], J.mod, kEntry[group][k]) == hipSuccess;
-    // (tolerant programs / small records; a deferring nested program's writer)
+    // (tolerant programs / small records; a deferring nested program's
+    // writer; the register-record one pass)
     if (!ok && ((group == JIT_DECODE && (k == 1 || k == 2)) ||
+                (group == JIT_INDEX && k == 5) ||
                 (group == JIT_NESTED && (k == 2 || k == 3)) ||
                 (group == JIT_XCODE && (k == 2 || k == 3 || k == 5)))) {
       (void)hipGetLastError();

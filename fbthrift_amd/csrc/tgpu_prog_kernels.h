@@ -1613,10 +1613,17 @@ struct IndexTileShared {
 // the candidate bits. The chain's starts are stored (u16, st16) as it goes.
 // Writes the tile's (s, e, cnt, pf) like index_spec_tile; returns false,
 // with nothing written, when the tile has too many candidates.
-template <class PP>
+// kOnePass (index_onepass_rr_tile): the chain's starts go to `sdst` (LDS)
+// and its result to *res; every wave stays (the caller's barrier follows).
+struct CandResult {
+  uint32_t first, e, count, stuck;  // tile-relative; first kNoPos: none
+  uint32_t sh, staged, avail, thi;
+};
+template <class PP, bool kOnePass = false>
 __device__ __forceinline__ bool spec_tile_cands(const IndexArgs& a, const PP& P, uint64_t j,
                                                 uint8_t* lds, uint32_t ent,
-                                                IndexTileShared& sm) {
+                                                IndexTileShared& sm, uint16_t* sdst = nullptr,
+                                                CandResult* res = nullptr) {
   const uint64_t lo = chunk_lo(a, j);
   const uint64_t hi_abs = chunk_hi(a, j);
   const uint8_t* g = a.in + lo;
@@ -1705,14 +1712,19 @@ __device__ __forceinline__ bool spec_tile_cands(const IndexArgs& a, const PP& P,
     if (late1 != late0) atomicAdd(&a.scal[12], 1ull);  // threads that saw their words change
   }
 #endif
+  if constexpr (!kOnePass) {
 #ifdef TGPU_SPEC_NOEXIT  // A/B: waves 1-3 wait for wave 0 at a final barrier
-  if (t >= 64) {
-    __syncthreads();
-    return true;
-  }
+    if (t >= 64) {
+      __syncthreads();
+      return true;
+    }
 #else
-  if (t >= 64) return true;  // wave 0 follows the chain and writes the tile's result
+    if (t >= 64) return true;  // wave 0 follows the chain and writes the tile's result
 #endif
+  } else {
+    if (threadIdx.x == 0) *res = CandResult{kNoPos, 0, 0, 1, sh, staged, avail, thi};
+    if (t >= 64) return true;
+  }
   const uint32_t lane = t;
   // the chain's first candidate: the range's first byte (tile 0 of a
   // non-speculative call), else the first canonical record
@@ -1729,7 +1741,7 @@ __device__ __forceinline__ bool spec_tile_cands(const IndexArgs& a, const PP& P,
   }
   const uint32_t first = f == kNoPos ? (ent != kNoPos ? ent : kNoPos) : sm.cl.cand[f];
   uint32_t count = 0, e = 0;
-  uint16_t* dst = a.st16 + j * a.st_cap;
+  uint16_t* dst = kOnePass ? sdst : a.st16 + j * a.st_cap;
   uint32_t i = f;
 #ifdef TGPU_ABL_NOCHAIN  // timing ablation only (wrong index): no chain
   stuck = true;
@@ -1802,6 +1814,10 @@ __device__ __forceinline__ bool spec_tile_cands(const IndexArgs& a, const PP& P,
     }
   }
 #endif
+  if constexpr (kOnePass) {
+    if (lane == 0) *res = CandResult{first, e, count, stuck ? 1u : 0u, sh, staged, avail, thi};
+    return true;
+  }
   if (lane == 0) {
     const bool none = first == kNoPos;
     const uint64_t st = lo - sh + first;
@@ -2329,6 +2345,164 @@ __device__ __forceinline__ void index_onepass_tile(const IndexArgs& a, const PP&
 #ifndef TGPU_ONEPASS_NOEMIT  // A/B timing only: no emission
   emit_lanes<kDecode>(a, P, lds, sm, rtile, L, sh, lo, op.prefix);
 #endif
+}
+
+// ---- one pass over the candidate-list speculation, records in registers ------
+// (round 6, verdict item 2: config 5 parses each record once, where the two
+// passes walked every record in the speculation and decoded it again from a
+// second staging of the wire.) Per 16 KiB tile: the candidate-list
+// speculation (spec_tile_cands) with the chain's record starts kept in LDS;
+// the tile's (first, end, count) published as an AGG word and the record
+// base found by the decoupled look-back (op_look_back: a window of 64
+// predecessors per round trip, every link between neighbours checked; no
+// single ticket counter — tiles publish at their own index); then every lane
+// decodes records of the staged tile with the program into registers (kRS)
+// and stores them at their global index, with their starts. Anything
+// unusual — a tile the speculation or the program cannot take, a broken
+// link, a record the program cannot store — publishes FAIL (scal[7]) and the
+// host redoes the range with the two-pass index, which decides everything.
+template <class PP, uint32_t kRS>
+__device__ __forceinline__ void index_onepass_rr_tile(const IndexArgs& a, const PP& P,
+                                                      uint8_t* lds, IndexTileShared& sm,
+                                                      OnePassShared& op, uint16_t* sst,
+                                                      CandResult& cr) {
+  static_assert(kRS % 8 == 0 && kRS <= 128, "register record: whole 8-byte words");
+  const uint64_t j = blockIdx.x;
+  const uint64_t lo = chunk_lo(a, j);
+  const uint32_t sh0 = (uint32_t)((uintptr_t)(a.in + lo) & 15);
+  const uint32_t ent = (j == 0 && !a.speculative) ? sh0 : kNoPos;
+  const bool listed = spec_tile_cands<PP, true>(a, P, j, lds, ent, sm, sst, &cr);
+  __syncthreads();  // wave 0's chain (sst) and result (cr)
+  const uint32_t first = cr.first, count = cr.count, sh = cr.sh;
+  const bool good = listed && !cr.stuck && first != kNoPos && count > 0;
+  const uint64_t sj = lo - sh + first, ej = lo - sh + cr.e;
+  if (threadIdx.x == 0) {
+    op.verdict = kOpFail;
+    const uint64_t aw = good ? op_agg(lo, sj, ej, count) : 0;
+    if (!aw) {
+      atomicExch(&a.scal[7], 1ull);
+      op_st(a.pf + j, kFailTag);
+    } else {
+      op_st(a.pf + j, aw);
+    }
+    op.e = aw;  // (here: the AGG word published, 0 when the tile failed)
+  }
+  __syncthreads();
+  if (!op.e) return;
+  const uint8_t* gb = a.in + lo - sh;
+  const TileSrc src{(const uint32_t*)lds, cr.staged & ~3u, HbmSrc{gb, cr.avail}};
+  const Ctx c{lo - sh, a.arena, a.arena_cap, a.string_limit, a.container_limit, nullptr};
+  // Records of up to 64 bytes in a tile of at most 512: decoded into
+  // registers while wave 0 looks back (waves 1-3 take records [0, 384), wave
+  // 0 the rest after its look-back — the look-back's round trips, 0.67 ms
+  // of the call when nothing overlapped them, hide behind the parse), then
+  // they leave through an LDS image of 256 records in the (by then dead)
+  // wire tile with 16-byte stores (per-lane stores of 56-byte records
+  // measured dearer). Otherwise every lane decodes and stores its records
+  // after the look-back.
+  constexpr bool kStage = kRS <= 64 && kTileLanes * kRS + 16 <= kTileLds;
+#ifdef TGPU_OP_LANE_STORES  // A/B: every record stored by its lane
+  const bool staged = false;
+#else
+  const bool staged = kStage && count <= 2 * kTileLanes;
+#endif
+  const uint32_t t = threadIdx.x;
+  bool bad = false;
+  alignas(16) uint8_t rb[2][kRS];
+  // record of slot q of lane t
+  auto slot = [&](uint32_t q) -> uint32_t { return t < 64 ? 384 + t + 64 * q : (t - 64) + 192 * q; };
+  auto parse = [&](uint32_t q) {
+    const uint32_t i = slot(q);
+#pragma unroll
+    for (uint32_t b = 0; b < kRS; b += 8) *(uint64_t*)(rb[q] + b) = 0;
+    if (i < count) {
+      uint32_t p = sst[i];
+      const uint32_t pe = i + 1 < count ? sst[i + 1] : cr.e;
+      bad |= !(run_program<true>(P, src, c, p, pe, rb[q]) && p == pe);
+    }
+  };
+  // (waves 1-3 skip the look-back block and parse at once; wave 0 after it:
+  // one call site of the unrolled parse)
+  if (t < 64) {
+#ifdef TGPU_OP_ABL_NOLOOK  // timing ablation only (records at wrong positions): no look-back
+    if (t == 0) {
+      op.verdict = kOpIncl;
+      op.prefix = 0;
+    }
+#else
+    op_look_back(a, j, sj, op);
+#endif
+    if (t == 0) {
+      if (op.verdict == kOpIncl) {
+        op_publish_incl(a, j, sj, ej, count, op.prefix, op);  // (FAIL when the fields overflow)
+      } else {  // a broken link (repair) or a failed predecessor: the two passes decide
+        op.verdict = kOpFail;
+        atomicExch(&a.scal[7], 1ull);
+        op_st(a.pf + j, kFailTag);
+      }
+    }
+  }
+  if (staged) {
+    parse(0);
+    parse(1);
+  }
+  __syncthreads();  // look-back done, every staged record parsed (the wire tile is free)
+  if (op.verdict != kOpIncl) return;
+  const uint64_t base = op.prefix;
+  const uint64_t lim = a.max_records < a.n_decode ? a.max_records : a.n_decode;
+  for (uint32_t i = t; i < count; i += kTileLanes)  // record starts
+    if (base + i < a.max_records) a.offs[base + i] = lo - sh + sst[i];
+#ifdef TGPU_OP_ABL_NODECODE  // timing ablation only: the index without the records
+  if (count) return;
+#endif
+  if (staged) {
+#pragma unroll
+    for (uint32_t h = 0; h < 2; ++h) {  // image of records [256 h, 256 h + 256)
+      const uint32_t r0 = h * kTileLanes;
+      if (r0 >= count || base + r0 >= lim) break;  // (uniform)
+      uint32_t nr = count - r0 < kTileLanes ? count - r0 : kTileLanes;
+      if (base + r0 + nr > lim) nr = (uint32_t)(lim - base - r0);
+      uint8_t* g = a.recs + (base + r0) * kRS;
+      const uint32_t osh = (uint32_t)((uintptr_t)g & 15);
+#pragma unroll
+      for (uint32_t q = 0; q < 2; ++q) {
+        const uint32_t i = slot(q);
+        if (i >= r0 && i < r0 + nr) {
+#pragma unroll
+          for (uint32_t b = 0; b < kRS; b += 8)
+            *(uint64_t*)(lds + osh + (i - r0) * kRS + b) = *(const uint64_t*)(rb[q] + b);
+        }
+      }
+      __syncthreads();
+      const uint32_t end = osh + nr * kRS;
+      uint8_t* gbr = g - osh;
+      for (uint32_t v = t; v < ((end + 15) >> 4); v += kTileLanes) {
+        const uint32_t vlo = v << 4, vhi = vlo + 16;
+        if (vlo >= osh && vhi <= end) {
+          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+          __builtin_nontemporal_store(((const u32x4*)lds)[v], (u32x4*)gbr + v);
+        } else {  // (records are 8-byte multiples: the edges are 8-byte halves)
+          if (vlo >= osh && vlo + 8 <= end) ((uint64_t*)gbr)[2 * v] = ((const uint64_t*)lds)[2 * v];
+          if (vlo + 8 >= osh && vhi <= end)
+            ((uint64_t*)gbr)[2 * v + 1] = ((const uint64_t*)lds)[2 * v + 1];
+        }
+      }
+      __syncthreads();
+    }
+  } else {
+    for (uint32_t i = t; i < count; i += kTileLanes) {
+      const uint64_t R = base + i;
+      uint32_t p = sst[i];
+      const uint32_t pe = i + 1 < count ? sst[i + 1] : cr.e;
+      alignas(16) uint8_t rbuf[kRS];
+#pragma unroll
+      for (uint32_t b = 0; b < kRS; b += 8) *(uint64_t*)(rbuf + b) = 0;
+      const bool ok = run_program<true>(P, src, c, p, pe, rbuf) && p == pe;
+      bad |= !ok;
+      if (R < lim) store_reg_record<kRS>(a.recs + R * kRS, rbuf, a.recs);
+    }
+  }
+  if (__syncthreads_or(bad) && t == 0) atomicExch(&a.scal[7], 1ull);
 }
 
 }  // namespace prog

@@ -13,13 +13,19 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
 
 
+SET = set()
+
+
 def apply(v):
     defs = []
-    os.environ.pop("TGPU_ARENA_PACK", None)
+    for k in SET:  # (a variant's env settings end with it)
+        os.environ.pop(k, None)
+    SET.clear()
     for part in v.split(";"):
         if part.startswith("env:"):
             k, _, val = part[4:].partition("=")
             os.environ[k] = val
+            SET.add(k)
         elif part:
             defs.append(part)
     os.environ["TGPU_JIT_DEFINES"] = "\n".join(defs)
