@@ -137,6 +137,14 @@ static uint32_t elem_stage_bytes() {
   return n;
 }
 
+// The single-pass compiled encode (write_tile_one) only under
+// TGPU_ENCODE_ONEPASS=1: measured slower than the size pass + tile scan +
+// write pass on configs 3 and 4
+static bool encode_onepass() {
+  const char* s = getenv("TGPU_ENCODE_ONEPASS");
+  return s && *s == '1';
+}
+
 hipError_t launch_program_encode(const EncodeArgs& a, const VProgram* d_prog,
                                  unsigned long long* part, bool size_only, hipStream_t stream,
                                  const JitKernels* jit) {
@@ -148,6 +156,15 @@ hipError_t launch_program_encode(const EncodeArgs& a, const VProgram* d_prog,
     // the compiled write pass sizes its own records (tile sums suffice)
     EncodeArgs x = a;
     x.recompute = size_only ? 0u : 1u;
+    if (!size_only && encode_onepass() && jit_has(jit, 2) && !x.fixed_len) {
+      // one pass (tgpu_prog_kernels.h write_tile_one): block_sums become the
+      // tiles' look-back status words
+      e = hipMemsetAsync(a.block_sums, 0, tiles * sizeof(unsigned long long), stream);
+      if (e != hipSuccess) return e;
+      return jit_launch_encode(jit, false, x, tiles,
+                               (x.out_cap ? x.out_cap : kOutCap) + 32 + elem_stage_bytes(), stream,
+                               2);
+    }
     e = jit_launch_encode(jit, false, x, tiles, rt, stream);
     if (e == hipSuccess)
       e = launch_scan_tiles(a.block_sums, tiles, part, &a.res->total_bytes, a.offs + a.n, stream);

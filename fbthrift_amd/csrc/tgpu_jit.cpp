@@ -74,7 +74,7 @@ std::string cache_key(const VProgram& P, int device, int group) {
 
 const char* const kEntry[6][6] = {
     {"tgpu_jit_decode", "tgpu_jit_decode_tail", "tgpu_jit_decode_rr", nullptr, nullptr, nullptr},
-    {"tgpu_jit_size", "tgpu_jit_write", nullptr, nullptr, nullptr, nullptr},
+    {"tgpu_jit_size", "tgpu_jit_write", "tgpu_jit_write_one", nullptr, nullptr, nullptr},
     {"tgpu_jit_index_spec", "tgpu_jit_index_emit", "tgpu_jit_index_decode",
      "tgpu_jit_index_onepass", "tgpu_jit_index_onepass_decode", "tgpu_jit_index_onepass_rr"},
     {"tgpu_jit_ndecode", "tgpu_jit_ndecode_hbm", "tgpu_jit_nsize", "tgpu_jit_nwrite", nullptr,
@@ -598,6 +598,12 @@ std::string gen_source(const VProgram& P, int group) {
          "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
          "  __shared__ prog::EncodeShared sm;\n"
          "  prog::write_tile<JP, kS>(a, JP{}, kS, smem, sm);\n"
+         "}\n"
+         "extern \"C\" __global__ __launch_bounds__(256) void tgpu_jit_write_one("
+         "EncodeArgs a) {\n"
+         "  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];\n"
+         "  __shared__ prog::EncodeShared sm;\n"
+         "  prog::write_tile_one<JP, kS>(a, JP{}, smem, sm);\n"
          "}\n";
   if (group == JIT_INDEX)
     o << "extern \"C\" __global__ __launch_bounds__(256) void tgpu_jit_index_spec(IndexArgs a) "

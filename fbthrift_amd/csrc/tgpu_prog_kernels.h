@@ -2505,5 +2505,229 @@ __device__ __forceinline__ void index_onepass_rr_tile(const IndexArgs& a, const 
   if (__syncthreads_or(bad) && t == 0) atomicExch(&a.scal[7], 1ull);
 }
 
+// ================================================ single-pass encode ======
+// Round 6 (verdict item 4): the compiled write pass without the size pass.
+// Tile j sizes its records (register records, as the two-pass write does),
+// publishes its byte total in a.block_sums[j] (AGG; tile 0 its INCL) and
+// emits its records into the zero-filled LDS output tile at phase 0 — no base
+// needed — and wave 0 looks back over the predecessors' words (AGG totals
+// summed down to the first INCL) and publishes INCL. The tile then leaves
+// through 16-byte stores assembled from the phase-0 tile with alignbyte (one
+// more LDS dword per store). The base is only needed for the stores, the
+// start offsets, the output cap check and the records past the LDS tile.
+// Measured (config 3, kbench_env / kbench_jit A/Bs on one box each): the body
+// without a look-back runs 2.07 ms against 2.51 ms for the two passes, but
+// every look-back form found the base too late for 256-record tiles (~12 µs
+// of workgroup life, ~1,500 resident; the predecessors' words cost a memory
+// round trip each poll): look-back before wave 0's emission 3.11-3.18 ms; a
+// two-level form over 64-tile groups (atomic group sums) 3.80 ms; a fifth
+// wave that only looks back 3.27 ms (6.1 ms grouped); the 256 nearest words
+// loaded ahead of wave 0's emission 3.03 ms (config 4: 1.76 vs 1.55 ms). So
+// the two passes stay the default and this one is TGPU_ENCODE_ONEPASS=1.
+// No failure state: every tile publishes AGG without waiting on anyone, and
+// workgroups dispatch in index order, so every wait ends; past a bound
+// (kEncSpinCap) the waiting wave sizes the silent predecessor's records
+// itself from HBM (correct, only slower) rather than hang.
+// a.block_sums: one status word per tile, zeroed before the launch.
+constexpr uint32_t kEncSpinCap = 1u << 16;
+constexpr uint64_t kEncAgg = 1ull << 62, kEncIncl = 2ull << 62, kEncVal = (1ull << 62) - 1;
+
+template <class PP>
+__device__ __forceinline__ unsigned long long enc_tile_total(const EncodeArgs& a, const PP P,
+                                                         uint64_t k, uint32_t S) {
+  // (wave 0: tile k's byte total, sized from HBM — the look-back's fallback)
+  const uint64_t r0 = k * kET;
+  const uint32_t nrec = (uint32_t)min((uint64_t)kET, a.n - r0);
+  unsigned long long t = 0;
+  for (uint32_t q = threadIdx.x; q < nrec; q += 64) {
+    bool ok = true;
+    t += program_size(P, PtrRec{a.recs + (r0 + q) * S}, a.lbase, ok);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+  return t;
+}
+
+template <class PP>
+__device__ __forceinline__ uint64_t enc_look_back(const EncodeArgs& a, const PP& P, uint64_t j,
+                                                  uint32_t S) {
+  const uint32_t l = threadIdx.x;
+  unsigned long long* st = a.block_sums;
+  uint64_t sum = 0;
+  for (int64_t top = (int64_t)j - 1; top >= 0; top -= 64) {
+    const int64_t k = top - (int64_t)l;
+    uint64_t w = k >= 0 ? op_ld(st + k) : kEncIncl;  // (below tile 0: prefix 0)
+    for (uint32_t spin = 0; __any(w == 0); ++spin) {
+      if (spin >= kEncSpinCap) {
+        for (uint64_t m = __ballot(w == 0); m; m &= m - 1) {
+          const uint32_t q = (uint32_t)__builtin_ctzll(m);
+          const unsigned long long t = enc_tile_total(a, P, (uint64_t)(top - q), S);
+          if (l == q) w = kEncAgg | t;
+        }
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      if (w == 0) w = op_ld(st + k);
+    }
+    const uint64_t fin = __ballot(w >= kEncIncl);
+    const uint32_t stop = fin ? (uint32_t)__builtin_ctzll(fin) : 64u;
+    uint64_t v = l <= stop ? (w & kEncVal) : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    sum += v;
+    if (fin) break;
+  }
+  return sum;
+}
+
+// The tile is one workgroup of 256 lanes (one record each). Wave 0
+// publishes the tile's AGG word and issues the loads of the 256 nearest
+// predecessors' words before it emits its own records; it reads them after
+// its emission, when they have arrived and are mostly final, and only
+// re-polls the ones still empty (then continues 64 per round trip past the
+// window if it held no INCL). Measured variants (config 3, kbench_jit):
+// look-back before wave 0's emission +1.1 ms over no look-back; a fifth wave
+// that only looks back: +0.27 ms for the extra wave alone.
+#ifndef TGPU_ENC1_WIN
+#define TGPU_ENC1_WIN 4  // predecessor words per lane of wave 0 loaded ahead
+#endif
+
+template <class PP, uint32_t SR>
+__device__ __forceinline__ void write_tile_one(const EncodeArgs& a, const PP& P, uint8_t* smem,
+                                               EncodeShared& sm) {
+  static_assert(PP::kStatic && SR > 0, "compiled programs with register records");
+  constexpr uint32_t kW = TGPU_ENC1_WIN;
+  const uint64_t j = blockIdx.x;
+  const uint64_t r0 = j * kET;
+  const uint32_t nrec = (uint32_t)min((uint64_t)kET, a.n - r0);
+  const uint32_t ocap = a.out_cap ? a.out_cap : kOutCap;
+  uint8_t* otile = smem;
+  const uint32_t r = threadIdx.x, lane = r & 63;
+  const bool own = r < nrec;
+  constexpr uint32_t kAhead = TGPU_ENC_AHEAD;
+  RegRec<SR> R;
+  StrAhead<kAhead> ah;
+  if (own) R.load(a.recs + (r0 + r) * SR);
+  unsigned long long sz = 0, tile_total;
+  if (own) {
+    bool ok = true;
+    sz = program_size(P, R, a.lbase, ok);
+    if (!ok) atomicMin(&a.res->first_fail, (unsigned long long)(r0 + r));
+    str_ahead(P, R, a.sbase, ah);
+  }
+  const unsigned long long rel = block_exscan256(sz, sm.part, &tile_total);
+  unsigned long long* ts = a.block_sums;
+  uint64_t w[kW];
+  if (r < 64) {
+    if (r == 0) op_st(ts + j, (j == 0 ? kEncIncl : kEncAgg) | tile_total);
+#pragma unroll
+    for (uint32_t q = 0; q < kW; ++q) {  // (distance lane + 64 q + 1)
+      const int64_t k = (int64_t)j - 1 - (int64_t)(lane + 64 * q);
+      w[q] = k >= 0 ? op_ld(ts + k) : kEncIncl;  // (below tile 0: prefix 0)
+    }
+  }
+  {  // zero the part of the (phase-0) output tile the records OR into
+    const uint4 z = {0u, 0u, 0u, 0u};
+    const uint32_t nz = ((uint32_t)min(tile_total, (unsigned long long)ocap) + 8 + 15) >> 4;
+    for (uint32_t i = r; i < nz; i += kET) ((uint4*)otile)[i] = z;
+  }
+  if (r == 0) sm.lds_end = (unsigned int)min(tile_total, (unsigned long long)ocap);
+  lds_barrier();
+  // (rel is monotone: the records past the first one that misses the LDS
+  // tile miss it too)
+  const bool fits = own && rel + sz <= ocap;
+  if (fits) {
+    OrSink o((uint32_t*)otile, (uint32_t)rel);
+    program_emit<PP, OrSink, RegRec<SR>, kAhead>(P, R, a.sbase, a.lbase, o, &ah);
+  }
+  if (own && !fits) atomicMin(&sm.lds_end, (unsigned int)min(rel, (unsigned long long)ocap));
+  if (r < 64 && j > 0) {
+#if defined(TGPU_ENC1_NOLB)  // (timing ablation only: wrong output)
+    const uint64_t p = j * tile_total;
+#else
+    uint64_t p = 0;
+    bool done = false;
+#pragma unroll
+    for (uint32_t q = 0; q < kW; ++q) {
+      if (done) break;
+      const int64_t k = (int64_t)j - 1 - (int64_t)(lane + 64 * q);
+      for (uint32_t spin = 0; __any(w[q] == 0); ++spin) {
+        if (spin >= kEncSpinCap) {  // (a silent predecessor: size it from HBM)
+          for (uint64_t m = __ballot(w[q] == 0); m; m &= m - 1) {
+            const uint32_t u = (uint32_t)__builtin_ctzll(m);
+            const unsigned long long tt =
+                enc_tile_total(a, P, j - 1 - (u + 64 * q), SR);
+            if (lane == u) w[q] = kEncAgg | tt;
+          }
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        if (w[q] == 0) w[q] = op_ld(ts + k);
+      }
+      const uint64_t fin = __ballot(w[q] >= kEncIncl);
+      const uint32_t stop = fin ? (uint32_t)__builtin_ctzll(fin) : 64u;
+      uint64_t v = lane <= stop ? (w[q] & kEncVal) : 0;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      p += v;
+      done = fin != 0;
+    }
+    if (!done)  // past the window (all AGG): the prefix below its farthest tile
+      p += enc_look_back(a, P, j - 64 * kW, SR);
+#endif
+    if (r == 0) {
+      op_st(ts + j, kEncIncl | (p + tile_total));
+      sm.base = p;
+    }
+  }
+  if (r == 0 && j == 0) sm.base = 0;
+  lds_barrier();
+  const unsigned long long tile_base = sm.base;
+  uint8_t* gtile = a.out + tile_base;
+  if (own) {
+    const unsigned long long start = tile_base + rel;
+    if (a.offs) a.offs[r0 + r] = start;
+    if (start + sz > a.cap) {
+      atomicMin(&a.res->first_fail, (unsigned long long)(r0 + r));
+      atomicMin(&sm.lds_end, (unsigned int)min(rel, (unsigned long long)ocap));
+    } else if (!fits) {  // (one unrolled emitter per kernel: this one from HBM)
+      emit_to_hbm(P, a.recs + (r0 + r) * SR, a.sbase, a.lbase, gtile + rel);
+    }
+  }
+  if (r == 0 && r0 + nrec == a.n) {  // (the scan's totals, two-pass form)
+    if (a.offs) a.offs[a.n] = tile_base + tile_total;
+    a.res->total_bytes = tile_base + tile_total;
+  }
+  lds_barrier();
+  // LDS tile [0, lds_end) -> HBM [gtile, gtile + lds_end): 16-byte stores at
+  // the stream's alignment, each from five LDS dwords (the phase is uniform)
+  const uint32_t osh = (uint32_t)((uintptr_t)gtile & 15);
+  const uint32_t end = osh + sm.lds_end;
+  const uint32_t nvec = (end + 15) >> 4;
+  uint8_t* gb = gtile - osh;
+  const uint32_t* o32 = (const uint32_t*)otile;
+  const uint32_t ph = (16 - osh) & 3;  // (16 i - osh) & 3
+  for (uint32_t i = r; i < nvec; i += kET) {
+    const uint32_t lo = i << 4, hi = lo + 16;
+    if (lo >= osh && hi <= end) {
+      const uint32_t d = (lo - osh) >> 2;
+      const uint32_t w0 = o32[d], w1 = o32[d + 1], w2 = o32[d + 2], w3 = o32[d + 3];
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      u32x4 v;
+      if (ph == 0) {
+        v = u32x4{w0, w1, w2, w3};
+      } else {
+        const uint32_t w4 = o32[d + 4];
+        v = u32x4{__builtin_amdgcn_alignbyte(w1, w0, ph), __builtin_amdgcn_alignbyte(w2, w1, ph),
+                  __builtin_amdgcn_alignbyte(w3, w2, ph), __builtin_amdgcn_alignbyte(w4, w3, ph)};
+      }
+      __builtin_nontemporal_store(v, (u32x4*)gb + i);
+    } else {
+      for (uint32_t b = (lo < osh ? osh : lo); b < (hi < end ? hi : end); ++b)
+        gb[b] = otile[b - osh];
+    }
+  }
+}
+
 }  // namespace prog
 }  // namespace tgpu

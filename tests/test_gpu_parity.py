@@ -305,10 +305,11 @@ def _long_string_records(n, seed, max_len):
 
 @pytest.mark.parametrize("proto", [0, 2])
 @pytest.mark.parametrize("max_len", [40, 3000])
-def test_program_encode_matches_oracle(gpu, proto, max_len):
+def test_program_encode_matches_oracle(gpu, proto, max_len, codec):
     """Compiled-program encode (records in the LDS output tile and, for long
     strings, records written straight to HBM) == oracle bytes and offsets;
-    tgpu_encoded_size agrees."""
+    tgpu_encoded_size agrees. Both program paths (interpreter, schema
+    compiler)."""
     n = 5000
     schema, rec, sarena = _long_string_records(n, 11 + max_len, max_len)
     st, want, woffs = oracle.encode(schema, proto, rec, n, sarena, None)
@@ -324,7 +325,30 @@ def test_program_encode_matches_oracle(gpu, proto, max_len):
 
 
 @pytest.mark.parametrize("proto", [0, 2])
-def test_program_encode_output_overflow(gpu, proto):
+@pytest.mark.parametrize("n,max_len", [(300_000, 24), (40_000, 700)])
+def test_program_encode_one_pass_many_tiles(gpu, proto, n, max_len, monkeypatch):
+    """The single-pass compiled encode (TGPU_ENCODE_ONEPASS=1, an A/B form:
+    slower than the default two passes) over many tiles (1172 / 157 tiles,
+    past its 256-tile look-ahead window; long strings: records past the LDS
+    tile) == the two-pass form == the oracle, with every start offset."""
+    monkeypatch.setenv("TGPU_JIT", "1")
+    schema, rec, sarena = _long_string_records(n, 3 + n, max_len)
+    st, want, woffs = oracle.encode(schema, proto, rec, n, sarena, None)
+    assert st.code == 0
+    gs = _gschema(schema)
+    ser = _ser(proto)
+    got = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("TGPU_ENCODE_ONEPASS", mode)
+        wire, offs = ser.serialize(gs, _t(rec, gpu), n, _t(sarena, gpu))
+        got[mode] = (bytes(_np(wire)), _np(offs).astype(np.uint64))
+    for mode in ("1", "0"):
+        assert got[mode][0] == want, mode
+        assert np.array_equal(got[mode][1], woffs), mode
+
+
+@pytest.mark.parametrize("proto", [0, 2])
+def test_program_encode_output_overflow(gpu, proto, codec):
     """Output capacity ends inside record k: status OUTPUT_OVERFLOW at record
     k (offset = its start), records before it written exactly."""
     import torch
