@@ -520,6 +520,99 @@ __global__ __launch_bounds__(T) void plan_binary_encode_ls_kernel(
   }
 }
 
+// Encode, direct (round 6 A/B, TGPU_PLAN_ENCODE ls=2): the lane-stationary
+// layout without the LDS wire tile — each lane stores its items' bytes
+// straight to HBM with unaligned 8/4/2/1-byte stores (items never share a
+// byte, so no lane's store overlaps another's; the 128-byte lines fill in
+// L2 before they leave). No LDS: occupancy is bounded by registers only.
+typedef unsigned long long u64_u __attribute__((aligned(1)));
+typedef uint32_t u32_u __attribute__((aligned(1)));
+typedef uint16_t u16_u __attribute__((aligned(1)));
+
+template <uint32_t T, uint32_t KI, uint32_t PMAX>
+__global__ __launch_bounds__(T) void plan_binary_encode_direct_kernel(
+    const FixedPlan* __restrict__ pp, const unsigned long long* __restrict__ recs, uint64_t n,
+    uint32_t R, uint32_t passes, uint8_t* __restrict__ out, uint64_t* __restrict__ offsets,
+    DevResult* __restrict__ res) {
+  const uint32_t L = pp->wire_len, Q = pp->n_words;
+  const uint32_t TR = R * passes;
+  const uint64_t tile0 = (uint64_t)blockIdx.x * TR;
+  const uint32_t nrec = (uint32_t)min((uint64_t)TR, n - tile0);
+  const uint32_t tid = threadIdx.x;
+  const bool act = tid < R * Q;
+  const uint32_t r0 = tid / Q, j = act ? tid - r0 * Q : 0;
+  const PlanWord pw = pp->words[j];
+  const uint32_t nit = pw.n_items;
+  const bool load = act && pw.has_value;
+  unsigned long long vals[PMAX];
+#pragma unroll
+  for (uint32_t k = 0; k < PMAX; ++k) {
+    const uint32_t r = r0 + k * R;
+    vals[k] = 0;
+    if (k < passes && load && r < nrec)
+      vals[k] = __builtin_nontemporal_load(recs + (tile0 + r) * Q + j);
+  }
+  PlanItem pit[KI];
+#pragma unroll
+  for (uint32_t m = 0; m < KI; ++m) pit[m] = pp->items[pw.first_item + (m < nit ? m : 0)];
+  uint8_t* gout = out + tile0 * L;
+  bool bad_bool = false;
+  uint32_t bad_rec = 0;
+  if (act) {
+#pragma unroll
+    for (uint32_t k = 0; k < PMAX; ++k) {
+      const uint32_t r = r0 + k * R;
+      if (k < passes && r < nrec) {
+        const unsigned long long v = vals[k];
+#pragma unroll
+        for (uint32_t m = 0; m < KI; ++m) {
+          if (m < nit) {
+            const PlanItem it = pit[m];
+            const uint32_t h = it.hdr_len, w = it.width;
+            const unsigned long long raw = v >> (8 * it.dst);
+            const unsigned long long top = w ? raw << (64 - 8 * w) : 0;
+            const unsigned long long vbe =
+                ((unsigned long long)bswap32((uint32_t)(top >> 32))) |
+                ((unsigned long long)bswap32((uint32_t)top) << 32);
+            if (it.is_bool && (raw & 0xff) > 1) {  // validate_bool
+              bad_bool = true;
+              bad_rec = r;
+            }
+            const unsigned long long Flo = (unsigned long long)it.hdr | (vbe << (8 * h));
+            const unsigned long long Fhi = h ? (vbe >> (64 - 8 * h)) : 0;
+            uint8_t* p = gout + (size_t)r * L + it.wire_off;
+            const uint32_t nb = h + w;
+            unsigned long long x = Flo;
+            uint32_t off = 0;
+            if (nb >= 8) {
+              *(u64_u*)p = Flo;
+              x = Fhi;
+              off = 8;
+            }
+            const uint32_t m2 = nb - off;
+            if (m2 & 4) {
+              *(u32_u*)(p + off) = (uint32_t)x;
+              x >>= 32;
+              off += 4;
+            }
+            if (m2 & 2) {
+              *(u16_u*)(p + off) = (uint16_t)x;
+              x >>= 16;
+              off += 2;
+            }
+            if (m2 & 1) p[off] = (uint8_t)x;
+          }
+        }
+      }
+    }
+  }
+  if (bad_bool) atomicMin(&res->first_fail, (unsigned long long)(tile0 + bad_rec));
+  if (offsets) {
+    for (uint32_t i = tid; i < nrec; i += T) offsets[tile0 + i] = (tile0 + i) * L;
+    if (tile0 + nrec == n && tid == 0) offsets[n] = n * L;
+  }
+}
+
 template <uint32_t T, bool kNT>
 __global__ __launch_bounds__(T) void plan_binary_encode_kernel(
     const FixedPlan* __restrict__ pp, const unsigned long long* __restrict__ recs, uint64_t n,
@@ -723,6 +816,23 @@ hipError_t launch_dec_ls_T(uint32_t KI, int chk, uint32_t R, uint32_t passes, ui
 }
 
 template <uint32_t T>
+hipError_t launch_enc_direct_T(uint32_t KI, uint32_t R, uint32_t passes, uint64_t blocks,
+                               hipStream_t stream, const FixedPlan* d_p,
+                               const unsigned long long* recs, uint64_t n, uint8_t* out,
+                               uint64_t* offsets, DevResult* res) {
+#define TGPU_ENCD(K, PM)                                                                       \
+  if (KI == K && passes <= PM) {                                                               \
+    hipLaunchKernelGGL((plan_binary_encode_direct_kernel<T, K, PM>), dim3((uint32_t)blocks),   \
+                       dim3(T), 0, stream, d_p, recs, n, R, passes, out, offsets, res);        \
+    return hipGetLastError();                                                                  \
+  }
+  TGPU_ENCD(1, 2) TGPU_ENCD(1, 4) TGPU_ENCD(1, 8) TGPU_ENCD(2, 2) TGPU_ENCD(2, 4) TGPU_ENCD(2, 8)
+  TGPU_ENCD(4, 2) TGPU_ENCD(4, 4) TGPU_ENCD(4, 8) TGPU_ENCD(8, 2) TGPU_ENCD(8, 4) TGPU_ENCD(8, 8)
+#undef TGPU_ENCD
+  return hipErrorInvalidValue;
+}
+
+template <uint32_t T>
 hipError_t launch_enc_ls_T(uint32_t KI, uint32_t R, uint32_t passes, uint32_t lds,
                            uint64_t blocks, hipStream_t stream, const FixedPlan* d_p,
                            const unsigned long long* recs, uint64_t n, uint8_t* out,
@@ -789,6 +899,12 @@ hipError_t launch_plan_binary_encode(const FixedPlan* p, const FixedPlan* d_p,
     const uint64_t blocks = (n + TR - 1) / TR;
     const uint32_t lds = ls_wire_region(v.T, TR, p->wire_len);
     const auto* r = (const unsigned long long*)recs;
+    if (v.ls == 2 && passes <= 8) {  // (the direct form: no LDS tile)
+      if (v.T == 256)
+        return launch_enc_direct_T<256>(KI, R, passes, blocks, stream, d_p, r, n, out, offsets,
+                                        res);
+      return launch_enc_direct_T<512>(KI, R, passes, blocks, stream, d_p, r, n, out, offsets, res);
+    }
     if (v.T == 256)
       return launch_enc_ls_T<256>(KI, R, passes, lds, blocks, stream, d_p, r, n, out, offsets, res);
     return launch_enc_ls_T<512>(KI, R, passes, lds, blocks, stream, d_p, r, n, out, offsets, res);

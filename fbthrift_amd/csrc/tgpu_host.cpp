@@ -522,8 +522,8 @@ __global__ __launch_bounds__(256) void pack_size_kernel(const uint8_t* __restric
 }
 
 // sums: the scanned tile sums. Element arrays of record i go to
-// dst[base + its prefix ..) (byte copies: the arrays sit at any byte
-// position under the position rule), its spans are rewritten to there.
+// dst[base + its prefix ..), its spans are rewritten to there (one lane per
+// record, word copies where both ends share an alignment).
 __global__ __launch_bounds__(256) void pack_copy_kernel(uint8_t* __restrict__ recs, uint64_t n,
                                                         uint32_t S, PackSpec ps,
                                                         const unsigned long long* __restrict__ sums,
@@ -541,7 +541,22 @@ __global__ __launch_bounds__(256) void pack_copy_kernel(uint8_t* __restrict__ re
     const uint64_t bytes = (uint64_t)sp->length * ps.width[f];
     if (!bytes) continue;
     const uint8_t* src = arena + sp->offset;
-    for (uint64_t k = 0; k < bytes; ++k) dst[off + k] = src[k];
+    uint8_t* d = dst + off;
+    // words of the widest size both ends share the alignment of (8 / 4 /
+    // 2 / 1 bytes: element arrays are 8-aligned in the arena, the packed
+    // offsets step by the element width), bytes up to it and after
+    const uintptr_t mis = ((uintptr_t)src ^ (uintptr_t)d) | 8;
+    const uint32_t wsz = (uint32_t)(mis & (~mis + 1));
+    uint64_t k = 0;
+    for (; k < bytes && (((uintptr_t)src + k) & (wsz - 1)); ++k) d[k] = src[k];
+    if (wsz == 8) {
+      for (; k + 8 <= bytes; k += 8) *(uint64_t*)(d + k) = *(const uint64_t*)(src + k);
+    } else if (wsz == 4) {
+      for (; k + 4 <= bytes; k += 4) *(uint32_t*)(d + k) = *(const uint32_t*)(src + k);
+    } else if (wsz == 2) {
+      for (; k + 2 <= bytes; k += 2) *(uint16_t*)(d + k) = *(const uint16_t*)(src + k);
+    }
+    for (; k < bytes; ++k) d[k] = src[k];
     sp->offset = off;
     off += bytes;
   }
