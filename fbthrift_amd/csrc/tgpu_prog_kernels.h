@@ -78,7 +78,10 @@ __host__ __device__ __forceinline__ uint32_t decode_rtile_bytes(uint32_t S) {
 template <uint32_t kRS>
 __device__ __forceinline__ void store_reg_record(uint8_t* go, const uint8_t* rbuf,
                                                  const uint8_t* recs) {
-#ifndef TGPU_RR_STORE8
+  // (16-byte stores of a lane's record, TGPU_RR_STORE16: the same time but
+  // +27 B fetched and +40 B written per config-4 record in the PMC counters
+  // — 64 lanes' 16-byte pieces at a 64-byte stride; round 6)
+#ifdef TGPU_RR_STORE16
   if constexpr (kRS % 16 == 0) {
     if (((uintptr_t)recs & 15) == 0) {  // whole 16-byte words (S 64: a record = 4 stores)
       typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -178,7 +181,11 @@ __device__ __forceinline__ bool pack_wave(const DecodeArgs& a, const PP& P, uint
   for (uint32_t v = v0 + lane; v < v1; v += 64) {
     const uint32_t lo = v << 4, hi = lo + 16;
     if (lo >= q0 && hi <= q0 + wsize) {
+#ifdef TGPU_PACK_PLAIN_STORE  // (A/B)
+      *((u32x4*)gb + v) = ((const u32x4*)wire)[v];
+#else
       __builtin_nontemporal_store(((const u32x4*)wire)[v], (u32x4*)gb + v);
+#endif
     } else {
       if (lo >= q0) ((uint64_t*)gb)[2 * v] = ((const uint64_t*)wire)[2 * v];
       if (hi <= q0 + wsize) ((uint64_t*)gb)[2 * v + 1] = ((const uint64_t*)wire)[2 * v + 1];
@@ -342,8 +349,18 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
       const uint64_t rs = r < nrec ? a.offs[r0 + r] : 0;
       uint8_t* rec = r < nrec ? (kRS ? rbuf : rtile + osh + r * S) : nullptr;
       const bool wpacked = pack_wave<PP, kK>(a, P, rec, lane_ok, rs, t0, sh, wire);
+      // the register records leave through the dead wire tile when it holds
+      // them (after every wave's packing): whole lines instead of each
+      // lane's 64-byte record in 8-byte pieces (TGPU_RR_LANE_STORES: those)
+#ifdef TGPU_RR_LANE_STORES
+      constexpr bool kStageRecs = false;
+#else
+      constexpr bool kStageRecs = kRS != 0;
+#endif
+      const bool stage_recs = kStageRecs && ((uintptr_t)gout & 7) == 0 &&
+                              osh + kPT * kRS <= decode_wire_region(wire_cap);
       if constexpr (kRS != 0) {
-        if (r < nrec) store_reg_record<kRS>(gout + (uint64_t)r * kRS, rbuf, a.recs);
+        if (r < nrec && !stage_recs) store_reg_record<kRS>(gout + (uint64_t)r * kRS, rbuf, a.recs);
       }
       const uint32_t wr0 = wv * 64;
       if (wr0 < nrec) {
@@ -369,7 +386,29 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
         }
       }
       packed = true;
-      if constexpr (kRS != 0) return;
+      if constexpr (kRS != 0) {
+        if (stage_recs) {
+          __syncthreads();  // every wave's packing / range copy has read its wire bytes
+          if (r < nrec) {
+#pragma unroll
+            for (uint32_t b = 0; b < kRS; b += 8)
+              *(uint64_t*)(wire + osh + r * kRS + b) = *(const uint64_t*)(rbuf + b);
+          }
+          __syncthreads();
+          const uint32_t end = osh + nrec * kRS;
+          uint8_t* base = gout - osh;
+          for (uint32_t i = threadIdx.x; i < ((end + 15) >> 4); i += kPT) {
+            const uint32_t lo = i << 4, hi = lo + 16;
+            if (lo >= osh && hi <= end) {
+              ((uint4*)base)[i] = ((const uint4*)wire)[i];
+            } else {  // (8-byte aligned records: the edge halves)
+              if (lo >= osh) ((uint64_t*)base)[2 * i] = ((const uint64_t*)wire)[2 * i];
+              if (hi <= end) ((uint64_t*)base)[2 * i + 1] = ((const uint64_t*)wire)[2 * i + 1];
+            }
+          }
+        }
+        return;
+      }
     }
   }
   if (stage_lists && !packed) {  // converted wire tile -> arena [t0, t1), coalesced
