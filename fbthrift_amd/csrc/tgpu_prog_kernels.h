@@ -409,6 +409,9 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
         }
         return;
       }
+      // (the record tile leaves below in 16-byte chunks that cross the waves'
+      // records: every wave's span rewrite must be in LDS first)
+      __syncthreads();
     }
   }
   if (stage_lists && !packed) {  // converted wire tile -> arena [t0, t1), coalesced

@@ -219,6 +219,27 @@ def test_gpu_block_rule_matches_oracle(gpu, codec, name, protocol, every, indexe
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("every", [0, 97])
+@pytest.mark.parametrize("indexed", [True, False])
+def test_gpu_block_rule_record_tile(gpu, monkeypatch, every, indexed):
+    """The compiled Binary tile with an LDS record tile (TGPU_DECODE_REGREC=0
+    on config 4's schema, whose default keeps records in registers): every
+    wave's span rewrite lands before the tile's records leave in 16-byte
+    chunks that cross the waves (a missing barrier there, round 6)."""
+    monkeypatch.setenv("TGPU_JIT", "1")
+    monkeypatch.setenv("TGPU_DECODE_REGREC", "0")
+    n = 20_003
+    schema, wire, offs = stream("nested", 0, n, every)
+    o = offs if indexed else None
+    st, rec, arena, nd, cons = _gpu_decode(gpu, schema, 0, wire, n, o)
+    assert st.code == 0 and nd == n and cons == len(wire), st.as_tuple()
+    ost, orec, oarena, _, _ = oracle.decode(schema, 0, wire, n, offsets=o)
+    S = schema.record_size
+    assert np.array_equal(rec[: n * S], orec[: n * S])
+    helpers.assert_arena_equal(schema, orec, n, wire, arena, oarena)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("protocol", [0, 2])
 def test_gpu_block_rule_failing_list(gpu, protocol):
     """A stream cut inside a list of record 5000: the oracle's status, the
