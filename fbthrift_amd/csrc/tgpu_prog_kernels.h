@@ -119,10 +119,12 @@ __device__ __forceinline__ void store_reg_record(uint8_t* go, const uint8_t* rbu
 // LDS array table — 1.82 ms.)
 constexpr uint32_t kPackWords = 8;  // 64 bytes of arrays per record (config 4: 16 x i32)
 template <class PP, uint32_t kK>
+// (`rec` is always a valid record buffer, `active` says whether the lane
+// has a record: a pointer that may be null kept the register record of the
+// `_rr` tile out of registers — 32 bytes of scratch per lane, round 6)
 __device__ __forceinline__ bool pack_wave(const DecodeArgs& a, const PP& P, uint8_t* rec,
-                                          bool lane_ok, uint64_t rstart, uint64_t t0,
-                                          uint32_t sh, uint8_t* wire) {
-  const bool active = rec != nullptr;
+                                          bool active, bool lane_ok, uint64_t rstart,
+                                          uint64_t t0, uint32_t sh, uint8_t* wire) {
   if (__ballot(active && !lane_ok)) return false;  // (wave-uniform)
   const uint64_t act = __ballot(active);
   if (!act) return true;
@@ -347,8 +349,8 @@ __device__ __forceinline__ void decode_tile(const DecodeArgs& a, const PP& P, ui
       // converted wire range as the position rule has it
       const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
       const uint64_t rs = r < nrec ? a.offs[r0 + r] : 0;
-      uint8_t* rec = r < nrec ? (kRS ? rbuf : rtile + osh + r * S) : nullptr;
-      const bool wpacked = pack_wave<PP, kK>(a, P, rec, lane_ok, rs, t0, sh, wire);
+      uint8_t* rec = kRS ? rbuf : rtile + osh + r * S;  // (inside the tile for r >= nrec)
+      const bool wpacked = pack_wave<PP, kK>(a, P, rec, r < nrec, lane_ok, rs, t0, sh, wire);
       // the register records leave through the dead wire tile when it holds
       // them (after every wave's packing): whole lines instead of each
       // lane's 64-byte record in 8-byte pieces (TGPU_RR_LANE_STORES: those)
